@@ -1,0 +1,162 @@
+/*
+ * recsys_hip.h — C-ABI of librecsys_hip.so, the MI355X (gfx950) sparse-embedding and
+ * feature-interaction engine.
+ *
+ * Every entry point replaces one stock TensorFlow / Keras / DGL kernel that the reference
+ * (neoyinyao/Recommender, read-only at /root/reference) reaches through its Keras layers.
+ * The reference has no native code of its own; the citation on each function names the
+ * reference call site whose semantics it reproduces.
+ *
+ * Conventions:
+ *   - return value: int32 status, 0 = RS_OK, < 0 = RS_E_*; rs_last_error() gives a
+ *     thread-local message for the last failing call on the calling thread.
+ *   - every buffer is a caller-owned DEVICE pointer; the library never allocates
+ *     persistent memory. Scratch comes from a caller workspace sized by the matching
+ *     rs_*_workspace_size() query.
+ *   - every call takes a hipStream_t (passed as void*) and is stream-ordered and
+ *     asynchronous: no host synchronisation inside, graph-capturable.
+ *   - stateless and re-entrant. RNG state (Philox key, counter) is passed explicitly.
+ *   - float tensors are fp32 row-major; ids are int32 or int64 (RS_ID_I32 / RS_ID_I64).
+ *   - out-of-range ids (TF-GPU semantics): the row reads as zeros, its gradient is
+ *     dropped and *err_flag (device int32, may be NULL) gets bit RS_ERRBIT_OOB set.
+ */
+#ifndef RECSYS_HIP_H
+#define RECSYS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_OK 0
+#define RS_E_INVALID (-1)     /* bad argument (shape, dtype, null pointer) */
+#define RS_E_OOB (-2)         /* reserved: host-side id range violation */
+#define RS_E_HIP (-3)         /* a HIP runtime call failed */
+#define RS_E_WORKSPACE (-4)   /* workspace smaller than rs_*_workspace_size() */
+#define RS_E_UNSUPPORTED (-5) /* shape outside what the kernels handle */
+
+#define RS_ID_I32 0
+#define RS_ID_I64 1
+
+#define RS_ERRBIT_OOB 1
+
+/* optimizer kinds for rs_embedding_apply */
+#define RS_OPT_SGD 0        /* var[u] -= lr * g_u                         (ctr/train.py:77-79) */
+#define RS_OPT_LAZY_ADAM 1  /* Adam on touched rows only                   (SURVEY §8a-2 b)   */
+#define RS_OPT_KERAS_ADAM 2 /* Keras OptimizerV2 Adam, dense decay of m/v/var (ctr/train.py:80) */
+#define RS_OPT_ADAGRAD 3    /* reserved */
+
+typedef struct rs_adam_params {
+  float lr;        /* SGD: learning rate. Adam: lr_t = lr*sqrt(1-b2^t)/(1-b1^t), host-computed fp32 */
+  float beta1;
+  float beta2;
+  float one_minus_beta1;
+  float one_minus_beta2;
+  float epsilon;
+} rs_adam_params;
+
+const char* rs_last_error(void);
+int32_t rs_version(void);
+/* number of gfx950 devices visible; 0 when no GPU (used by loaders to fail loudly) */
+int32_t rs_device_count(void);
+
+/* ------------------------------------------------------------------------------------
+ * a-1  Embedding forward (multi-slot gather).
+ * Replaces keras.layers.Embedding.call → ResourceGather:
+ *   ctr/model.py:19 (DeepFM), ctr/model.py:49 (DLRM), esmm/esmm.py:16, esmm/mmoe.py:20,
+ *   esmm/base.py:15, dien/model.py:16-17, eges/model.py:32-33, pinsage/train/layers.py:63-79.
+ * ids: [n_ids] flattened [B, n_slots] (slot = position % n_slots).
+ * slot_offsets: NULL (one shared table, ctr/model.py:10) or [n_slots+1] row offsets of
+ *   per-slot tables packed in one slab (row = slot_offsets[s] + id, valid while
+ *   id < slot_offsets[s+1]-slot_offsets[s]).
+ * out: [n_ids, dim]. */
+int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t dim, const void* ids,
+                         int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
+                         int32_t n_slots, float* out, int32_t* err_flag, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * a-2 (part 1) Duplicate-index coalescing: the IndexedSlices gradient's `unique` +
+ * `unsorted_segment_sum` (Keras OptimizerV2 _deduplicate_indexed_slices, reached from
+ * apply_gradients at ctr/train.py:97, dien/train.py:22, esmm/train.py:104).
+ * Stable LSD radix sort of the global row of every id; outputs
+ *   sorted_rows[n_ids] (uint32, ascending; an OOB id gets the sentinel n_rows, sorting last),
+ *   sorted_pos[n_ids]  (int32 original position, ascending inside a run of equal rows),
+ *   n_unique[1]        (device int32: number of distinct valid rows).
+ * Deterministic: identical inputs give identical outputs. */
+size_t rs_sort_ids_workspace_size(int64_t n_ids);
+int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
+                    int32_t n_slots, int64_t n_rows, uint32_t* sorted_rows, int32_t* sorted_pos,
+                    int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                    void* stream);
+
+/* a-2 (part 2) deduplicated gradient: uniq_rows[u], uniq_grad[u, dim] for the n_unique
+ * distinct valid rows (count from rs_sort_ids), uniq_grad[u] = Σ grad_out[p] over the
+ * positions p of row u. Summation order: sequential over sorted positions inside tiles of
+ * RS_DEDUP_TILE sorted entries, tile partials added in tile order
+ * (oracle/embedding.py:segment_sum_tiled restates it). */
+#define RS_DEDUP_TILE 32
+size_t rs_dedup_workspace_size(int64_t n_ids, int32_t dim);
+int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                int64_t n_ids, const float* grad_out, int32_t dim, int64_t n_rows,
+                                uint32_t* uniq_rows, float* uniq_grad, void* workspace,
+                                size_t ws_bytes, void* stream);
+
+/* a-2 (part 3) fused segmented-sum + optimizer apply on the touched rows
+ * (Keras Adam _resource_apply_sparse / SGD _resource_apply_sparse_duplicate_indices,
+ * [3p] reached from ctr/train.py:80,84,97 and the commented SGD path ctr/train.py:77-79).
+ * Same summation order as rs_embedding_dedup_grad. m, v: optimizer slots [n_rows, dim]
+ * (NULL for SGD). For RS_OPT_KERAS_ADAM call rs_keras_adam_dense_sweep afterwards with the
+ * same touched bitmap ([ceil(n_rows/32)] uint32, zero on entry): the pair reproduces Keras'
+ * dense m/v decay and dense var update. */
+size_t rs_apply_workspace_size(int64_t n_ids, int32_t dim);
+int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float* v, int64_t n_rows,
+                           int32_t dim, const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                           int64_t n_ids, const float* grad_out, const rs_adam_params* params,
+                           uint32_t* touched_bitmap, void* workspace, size_t ws_bytes,
+                           void* stream);
+/* dense sweep for RS_OPT_KERAS_ADAM: rows NOT marked in touched_bitmap get
+ * m=b1*m, v=b2*v, var -= lr*m/(sqrt(v)+eps); the bitmap is cleared afterwards. */
+int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_rows, int32_t dim,
+                                  const rs_adam_params* params, uint32_t* touched_bitmap,
+                                  void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * a-4 DotInteraction(self_interaction, skip_gather) — ctr/layers.py:17-43.
+ * x: [B, F, D]. out row stride out_stride (>= output width):
+ *   skip_gather: F*F values, (i,j) kept where included, zero elsewhere (ctr/layers.py:35-38);
+ *   gather & !self: i<j row-major, F(F-1)/2 (ctr/layers.py:32-34,39-42);
+ *   gather & self: i>=j row-major, F(F+1)/2 (ctr/layers.py:27-30,39-42). */
+int32_t rs_dot_interaction_fwd(const float* x, int64_t batch, int32_t F, int32_t D,
+                               int32_t self_interaction, int32_t skip_gather, float* out,
+                               int64_t out_stride, void* stream);
+int32_t rs_dot_interaction_bwd(const float* x, const float* grad_out, int64_t batch, int32_t F,
+                               int32_t D, int32_t self_interaction, int32_t skip_gather,
+                               int64_t grad_stride, float* grad_x, void* stream);
+
+/* DLRM fused gather + interaction + concat (ctr/model.py:45-55 with
+ * DotInteraction(False, True), ctr/model.py:43):
+ *   out[b] = [ Z(b) (F*F, F = n_slots+1, strict upper kept) , dense[b] (D) ],
+ *   X(b) = [ table[row(b,0)], ..., table[row(b,S-1)], dense[b] ].
+ * bwd re-gathers X from the table and writes grad_emb[b*S+s] and grad_dense[b]. */
+int32_t rs_dlrm_interaction_fwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
+                                int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
+                                const float* dense, int64_t batch, float* out, int64_t out_stride,
+                                int32_t* err_flag, void* stream);
+int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
+                                int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
+                                const float* dense, int64_t batch, const float* grad_out,
+                                int64_t grad_stride, float* grad_emb, float* grad_dense,
+                                void* stream);
+
+/* a-5 DeepFM second-order term — ctr/model.py:21-23:
+ *   out[b] = 0.5 * Σ_d ((Σ_f e[b,f,d])^2 - Σ_f e[b,f,d]^2). */
+int32_t rs_fm_fwd(const float* emb, int64_t batch, int32_t F, int32_t D, float* out, void* stream);
+int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t batch, int32_t F, int32_t D,
+                  float* grad_emb, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RECSYS_HIP_H */

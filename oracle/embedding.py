@@ -1,0 +1,153 @@
+"""Oracle: embedding lookup, duplicate-index coalescing and the sparse optimizer applies.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py; parity unpinned).
+
+References (read as text):
+  a-1 keras.layers.Embedding forward [3p] — call sites ctr/model.py:10,19 (DeepFM),
+      ctr/model.py:42,49 (DLRM), esmm/esmm.py:10-11,16, dien/model.py:11-12,16-17.
+  a-2 gradient → IndexedSlices → _deduplicate_indexed_slices (unique + unsorted_segment_sum)
+      → Keras Adam _resource_apply_sparse [3p]; callers ctr/train.py:80,84,97,
+      dien/train.py:21-22, esmm/train.py:103-104; SGD path ctr/train.py:77-79.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+DEDUP_TILE = 32  # RS_DEDUP_TILE in include/recsys_hip.h
+
+
+def global_rows(ids: np.ndarray, n_rows: int, slot_offsets: np.ndarray | None = None):
+    """Row of every flattened id; -1 where the id is outside its table.
+
+    slot_offsets None → one shared table (ctr/model.py:10: one Embedding for all 26 slots);
+    otherwise per-slot tables packed in one slab, slot = position % n_slots
+    (esmm/esmm.py:10-11 builds one table per feature)."""
+    ids = np.asarray(ids).astype(np.int64)
+    flat = ids.reshape(-1)
+    if slot_offsets is None:
+        ok = (flat >= 0) & (flat < n_rows)
+        return np.where(ok, flat, -1)
+    so = np.asarray(slot_offsets, dtype=np.int64)
+    n_slots = so.size - 1
+    s = np.arange(flat.size) % n_slots
+    card = so[1:] - so[:-1]
+    ok = (flat >= 0) & (flat < card[s])
+    return np.where(ok, so[s] + flat, -1)
+
+
+def embedding_lookup(table: np.ndarray, ids: np.ndarray, slot_offsets=None, raise_oob=True):
+    """out[..., :] = table[row(id), :]. TF-CPU raises on an out-of-range id, TF-GPU returns a
+    zero row [3p tf.gather docs]; raise_oob selects the behaviour."""
+    rows = global_rows(ids, table.shape[0], slot_offsets)
+    if raise_oob and (rows < 0).any():
+        raise IndexError("embedding id out of range")
+    out = np.zeros((rows.size, table.shape[1]), dtype=table.dtype)
+    ok = rows >= 0
+    out[ok] = table[rows[ok]]
+    return out.reshape(*np.asarray(ids).shape, table.shape[1])
+
+
+def sort_ids(ids, n_rows, slot_offsets=None):
+    """Stable sort of rows (OOB rows get the sentinel n_rows and sort last); returns
+    (sorted_rows uint32, sorted_pos int32, n_unique)."""
+    rows = global_rows(ids, n_rows, slot_offsets)
+    keys = np.where(rows < 0, n_rows, rows).astype(np.int64)
+    pos = np.argsort(keys, kind="stable")
+    sk = keys[pos]
+    valid = sk < n_rows
+    n_unique = int(np.unique(sk[valid]).size)
+    return sk.astype(np.uint32), pos.astype(np.int32), n_unique
+
+
+def segment_sum_tiled(sorted_rows, sorted_pos, grad, n_rows, tile=DEDUP_TILE):
+    """Deduplicated gradient with the kernel's fixed summation order.
+
+    The sorted entries are cut into tiles of `tile`; inside a tile the rows of one segment are
+    added sequentially starting from +0.0; the pieces of a segment that spans tiles are then
+    added in tile order, starting from the first piece. Returns (uniq_rows, uniq_grad)."""
+    sorted_rows = np.asarray(sorted_rows).astype(np.int64)
+    sorted_pos = np.asarray(sorted_pos).astype(np.int64)
+    grad = np.asarray(grad, dtype=np.float32)
+    n = sorted_rows.size
+    dim = grad.shape[1]
+    valid = sorted_rows < n_rows
+    nv = int(valid.sum())  # OOB sentinels are last
+    if nv == 0:
+        return np.zeros(0, np.uint32), np.zeros((0, dim), np.float32)
+    keys = sorted_rows[:nv]
+    k = np.arange(nv)
+    tile_id = k // tile
+    # piece = maximal run of equal keys inside one tile
+    piece_head = np.ones(nv, bool)
+    piece_head[1:] = (keys[1:] != keys[:-1]) | (tile_id[1:] != tile_id[:-1])
+    piece_start = np.flatnonzero(piece_head)
+    piece_len = np.diff(np.append(piece_start, nv))
+    n_pieces = piece_start.size
+    rows_g = grad[sorted_pos[:nv]]
+    acc = np.zeros((n_pieces, dim), np.float32)
+    for j in range(int(piece_len.max())):
+        sel = piece_len > j
+        acc[sel] += rows_g[piece_start[sel] + j]
+    # segments over pieces
+    piece_key = keys[piece_start]
+    seg_head = np.ones(n_pieces, bool)
+    seg_head[1:] = piece_key[1:] != piece_key[:-1]
+    seg_start = np.flatnonzero(seg_head)
+    seg_len = np.diff(np.append(seg_start, n_pieces))
+    out = acc[seg_start].copy()
+    for j in range(1, int(seg_len.max())):
+        sel = seg_len > j
+        out[sel] += acc[seg_start[sel] + j]
+    return piece_key[seg_start].astype(np.uint32), out
+
+
+def keras_adam_coefficients(step: int, lr=1e-3, beta1=0.9, beta2=0.999, epsilon=1e-7):
+    """Keras OptimizerV2 Adam._prepare_local [3p TF 2.2]: local_step = iterations + 1 (step is
+    1-based here); lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t), all in float32."""
+    f = np.float32
+    t = f(step)
+    b1p = np.power(f(beta1), t, dtype=np.float32)
+    b2p = np.power(f(beta2), t, dtype=np.float32)
+    lr_t = f(f(lr) * (np.sqrt(f(f(1) - b2p), dtype=np.float32) / f(f(1) - b1p)))
+    return dict(lr=lr_t, beta1=f(beta1), beta2=f(beta2), one_minus_beta1=f(f(1) - f(beta1)),
+                one_minus_beta2=f(f(1) - f(beta2)), epsilon=f(epsilon))
+
+
+def apply_sgd(table, uniq_rows, uniq_grad, lr):
+    """var[u] = var[u] - lr * g_u (duplicates pre-summed; ctr/train.py:77-79 SGD path)."""
+    t = table.copy()
+    u = np.asarray(uniq_rows, np.int64)
+    t[u] = t[u] - np.float32(lr) * uniq_grad
+    return t
+
+
+def _adam_rows(w, m, v, g, c):
+    f32 = np.float32
+    mm = m * c["beta1"]
+    mm = mm + g * c["one_minus_beta1"]
+    vv = v * c["beta2"]
+    vv = vv + (g * g) * c["one_minus_beta2"]
+    upd = (c["lr"] * mm) / (np.sqrt(vv, dtype=f32) + c["epsilon"])
+    return w - upd, mm, vv
+
+
+def apply_lazy_adam(table, m, v, uniq_rows, uniq_grad, coeffs):
+    """Adam on the touched rows only (TF-Addons LazyAdam semantics, SURVEY §8a-2 mode b)."""
+    t, m2, v2 = table.copy(), m.copy(), v.copy()
+    u = np.asarray(uniq_rows, np.int64)
+    t[u], m2[u], v2[u] = _adam_rows(t[u], m2[u], v2[u], uniq_grad, coeffs)
+    return t, m2, v2
+
+
+def apply_keras_adam(table, m, v, uniq_rows, uniq_grad, coeffs):
+    """Keras Adam._resource_apply_sparse [3p TF 2.2]: m = b1*m (dense), m[u] += (1-b1)*g,
+    v = b2*v (dense), v[u] += (1-b2)*g*g, var -= lr_t*m/(sqrt(v)+eps) (dense, every row)."""
+    f32 = np.float32
+    c = coeffs
+    m2 = m * c["beta1"]
+    v2 = v * c["beta2"]
+    u = np.asarray(uniq_rows, np.int64)
+    m2[u] = m2[u] + uniq_grad * c["one_minus_beta1"]
+    v2[u] = v2[u] + (uniq_grad * uniq_grad) * c["one_minus_beta2"]
+    t = table - (c["lr"] * m2) / (np.sqrt(v2, dtype=f32) + c["epsilon"])
+    return t.astype(f32), m2.astype(f32), v2.astype(f32)

@@ -1,0 +1,123 @@
+"""ctypes binding of librecsys_hip.so (include/recsys_hip.h).
+
+This is the only place Python touches the C-ABI. There is no CPU fallback: if the library is
+missing, or no gfx950 device is visible when a kernel is called, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+import torch
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "_lib" / "librecsys_hip.so"
+HEADER = _PKG.parent / "include" / "recsys_hip.h"
+
+RS_ID_I32 = 0
+RS_ID_I64 = 1
+RS_OPT_SGD = 0
+RS_OPT_LAZY_ADAM = 1
+RS_OPT_KERAS_ADAM = 2
+RS_DEDUP_TILE = 32
+RS_ERRBIT_OOB = 1
+
+
+class AdamParams(C.Structure):
+    _fields_ = [("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
+                ("one_minus_beta1", C.c_float), ("one_minus_beta2", C.c_float),
+                ("epsilon", C.c_float)]
+
+
+_p, _i32, _i64, _sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
+_SIGS = {
+    "rs_last_error": (C.c_char_p, []),
+    "rs_version": (_i32, []),
+    "rs_device_count": (_i32, []),
+    "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
+    "rs_sort_ids_workspace_size": (_sz, [_i64]),
+    "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_dedup_workspace_size": (_sz, [_i64, _i32]),
+    "rs_embedding_dedup_grad": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _p, _sz, _p]),
+    "rs_apply_workspace_size": (_sz, [_i64, _i32]),
+    "rs_embedding_apply": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p,
+                                  C.POINTER(AdamParams), _p, _p, _sz, _p]),
+    "rs_keras_adam_dense_sweep": (_i32, [_p, _p, _p, _i64, _i32, C.POINTER(AdamParams), _p, _p]),
+    "rs_dot_interaction_fwd": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _p, _i64, _p]),
+    "rs_dot_interaction_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _i32, _i64, _p, _p]),
+    "rs_dlrm_interaction_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _i64,
+                                       _p, _p]),
+    "rs_dlrm_interaction_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _i64,
+                                       _p, _p, _p]),
+    "rs_fm_fwd": (_i32, [_p, _i64, _i32, _i32, _p, _p]),
+    "rs_fm_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
+}
+
+_lib = None
+
+
+class RecsysError(RuntimeError):
+    pass
+
+
+def header_symbols() -> list[str]:
+    """Every rs_* function declared in include/recsys_hip.h."""
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(rs_\w+)\s*\(", text, re.M)))
+
+
+def load(path: str | os.PathLike | None = None):
+    """Load the library (no GPU needed). Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RecsysError(f"{p} not built: run `python -m recommender_amd.build` "
+                          "(or __graft_entry__.build())")
+    lib = C.CDLL(str(p))
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(status: int, fn: str):
+    if status != 0:
+        msg = lib().rs_last_error().decode(errors="replace")
+        raise RecsysError(f"{fn} failed with status {status}: {msg}")
+
+
+def call(fn: str, *args):
+    """Invoke a kernel entry point; raises on a non-zero status."""
+    f = getattr(lib(), fn)
+    check(f(*args), fn)
+
+
+def require_device(t: torch.Tensor, name: str = "tensor"):
+    if not t.is_cuda:
+        raise RecsysError(f"{name} must be a GPU tensor (librecsys_hip has no CPU path)")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def id_dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.int64:
+        return RS_ID_I64
+    if t.dtype == torch.int32:
+        return RS_ID_I32
+    raise RecsysError(f"ids must be int32 or int64, got {t.dtype}")

@@ -1,0 +1,546 @@
+// embedding.hip — multi-slot embedding gather (a-1) and the deterministic sparse-gradient
+// apply (a-2): segmented sum over the radix-sorted ids fused with the optimizer update.
+//
+// Row layout: a row of `dim` fp32 is covered by a lane group of LPR lanes (LPR = power of two
+// <= 64), each lane moving VEC floats (16 B when dim % 4 == 0) per chunk, CPL chunks per lane.
+// At dim = 128 a half-wave moves one 512-B row per instruction, so a wave issues two
+// independent rows per load instruction and every load is a full 512-B contiguous segment.
+//
+// Segmented sum (SURVEY §7 "Bit-exact duplicate reduction"): the sorted entries are cut into
+// tiles of RS_DEDUP_TILE; one lane group walks a tile in order, summing consecutive equal rows.
+// A run that is a whole segment is finalised in place (optimizer applied to the table row);
+// a run cut by a tile edge stores a partial ([tile][0] = continuation, [tile][1] = head part),
+// and a fix-up pass folds the partials of each spanning segment in tile order. The order is
+// therefore fixed by the sorted order alone (oracle/embedding.py:segment_sum_tiled).
+#include "common.hpp"
+
+namespace rs {
+
+int32_t radix_sort_pairs(uint32_t*, int32_t*, uint32_t*, int32_t*, int64_t, int64_t, void*, size_t,
+                         hipStream_t);
+size_t radix_sort_ws_size(int64_t);
+int32_t exclusive_scan_i32(const int32_t*, int32_t*, int64_t, int32_t*, void*, size_t, hipStream_t);
+size_t exclusive_scan_ws_size(int64_t);
+
+// ---- vector row I/O ------------------------------------------------------------------
+template <int VEC>
+struct RowIO;
+template <>
+struct RowIO<4> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <>
+struct RowIO<2> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[2]) {
+    float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[2]) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  }
+};
+template <>
+struct RowIO<1> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[1]) { v[0] = *p; }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[1]) { *p = v[0]; }
+};
+
+struct RowGeom {
+  int vec, lpr_log2, cpl;
+};
+
+static RowGeom row_geom(int dim, const void* const* ptrs, int nptr) {
+  int vec = (dim % 4 == 0) ? 4 : (dim % 2 == 0 ? 2 : 1);
+  // downgrade the vector width if any base pointer is not aligned for it
+  for (int i = 0; i < nptr; ++i) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[i]);
+    while (vec > 1 && (a % (vec * 4)) != 0) vec >>= 1;
+  }
+  int chunks = dim / vec;
+  int lpr = 1, l2 = 0;
+  while (lpr < chunks && lpr < 64) { lpr <<= 1; ++l2; }
+  int cpl = (chunks + lpr - 1) / lpr;
+  int c = 1;
+  while (c < cpl) c <<= 1;
+  return {vec, l2, c};
+}
+
+// ---- a-1: gather ----------------------------------------------------------------------
+template <int VEC, int CPL>
+__global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ table, int64_t n_rows,
+                                                     int dim, const void* __restrict__ ids,
+                                                     int32_t dtype, int64_t n_ids,
+                                                     const int64_t* __restrict__ slot_offsets,
+                                                     int32_t n_slots, float* __restrict__ out,
+                                                     int32_t* err_flag, int lpr_log2) {
+  constexpr int U = 4;
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t gpb = blockDim.x >> lpr_log2;
+  const int64_t groups = (int64_t)gridDim.x * gpb;
+  const int64_t g = (int64_t)blockIdx.x * gpb + (threadIdx.x >> lpr_log2);
+  bool oob = false;
+  for (int64_t base = g; base < n_ids; base += groups * U) {
+    float v[U][CPL][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t p = base + u * groups;
+      int64_t r = -2;
+      if (p < n_ids) {
+        r = global_row(ids, dtype, p, slot_offsets, n_slots, n_rows);
+        oob |= (r == -1);
+      }
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (r >= 0 && col < dim) {
+          RowIO<VEC>::load(table + r * dim + col, v[u][c]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[u][c][e] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t p = base + u * groups;
+      if (p < n_ids) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          int col = (gl + c * lpr) * VEC;
+          if (col < dim) RowIO<VEC>::store(out + p * dim + col, v[u][c]);
+        }
+      }
+    }
+  }
+  if (__any(oob) && (threadIdx.x & 63) == 0) flag_oob(err_flag);
+}
+
+// ---- a-2: segmented sum + apply -------------------------------------------------------
+enum { OPT_SGD = RS_OPT_SGD, OPT_LAZY = RS_OPT_LAZY_ADAM, OPT_KERAS = RS_OPT_KERAS_ADAM, OPT_EMIT = 100 };
+
+struct ApplyArgs {
+  float* table;
+  float* m;
+  float* v;
+  int dim;
+  rs_adam_params p;
+  uint32_t* bitmap;       // keras: touched rows
+  float* partial;         // [n_tiles][2][dim]
+  // OPT_EMIT (dedup output)
+  float* uniq_grad;
+  uint32_t* uniq_rows;
+  const int32_t* seg_excl;  // exclusive scan of head flags
+};
+
+template <int OPT, int VEC>
+__device__ __forceinline__ void finalize_chunk(const ApplyArgs& a, uint32_t row, int col,
+                                               const float (&g)[VEC], int32_t seg_id) {
+  if constexpr (OPT == OPT_EMIT) {
+    RowIO<VEC>::store(a.uniq_grad + (int64_t)seg_id * a.dim + col, g);
+  } else if constexpr (OPT == OPT_SGD) {
+    float* t = a.table + (int64_t)row * a.dim + col;
+    float w[VEC];
+    RowIO<VEC>::load(t, w);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) w[e] = w[e] - a.p.lr * g[e];
+    RowIO<VEC>::store(t, w);
+  } else {  // lazy / keras Adam on a touched row (Keras _resource_apply_sparse op order)
+    int64_t off = (int64_t)row * a.dim + col;
+    float w[VEC], m[VEC], v[VEC];
+    RowIO<VEC>::load(a.table + off, w);
+    RowIO<VEC>::load(a.m + off, m);
+    RowIO<VEC>::load(a.v + off, v);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float mm = m[e] * a.p.beta1;
+      mm = mm + g[e] * a.p.one_minus_beta1;
+      float gg = g[e] * g[e];
+      float vv = v[e] * a.p.beta2;
+      vv = vv + gg * a.p.one_minus_beta2;
+      float upd = (a.p.lr * mm) / (sqrtf(vv) + a.p.epsilon);
+      m[e] = mm;
+      v[e] = vv;
+      w[e] = w[e] - upd;
+    }
+    RowIO<VEC>::store(a.table + off, w);
+    RowIO<VEC>::store(a.m + off, m);
+    RowIO<VEC>::store(a.v + off, v);
+  }
+}
+
+template <int OPT, int VEC, int CPL>
+__device__ __forceinline__ void finalize_row(const ApplyArgs& a, uint32_t row, int gl, int lpr,
+                                             const float (&acc)[CPL][VEC], int32_t seg_id) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    int col = (gl + c * lpr) * VEC;
+    if (col < a.dim) finalize_chunk<OPT, VEC>(a, row, col, acc[c], seg_id);
+  }
+  if constexpr (OPT == OPT_KERAS) {
+    if (gl == 0) atomicOr(a.bitmap + (row >> 5), 1u << (row & 31));
+  }
+  if constexpr (OPT == OPT_EMIT) {
+    if (gl == 0) a.uniq_rows[seg_id] = row;
+  }
+}
+
+__device__ __forceinline__ int32_t seg_id_of(const ApplyArgs& a, const uint32_t* keys, int64_t k) {
+  bool head = (k == 0) || keys[k - 1] != keys[k];
+  return a.seg_excl ? a.seg_excl[k] + (head ? 1 : 0) - 1 : 0;
+}
+
+template <int OPT, int VEC, int CPL>
+__global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restrict__ keys,
+                                                       const int32_t* __restrict__ pos, int64_t n,
+                                                       uint32_t n_rows, const float* __restrict__ grad,
+                                                       ApplyArgs a, int lpr_log2, int64_t n_tiles) {
+  constexpr int T = RS_DEDUP_TILE;
+  constexpr int U = 8;
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
+  if (t >= n_tiles) return;
+  const int64_t k0 = t * T;
+  const int64_t k1 = k0 + T < n ? k0 + T : n;
+  const int dim = a.dim;
+
+  uint32_t run_row = keys[k0];
+  int64_t run_start = k0;
+  bool run_starts = (k0 == 0) || keys[k0 - 1] != run_row;
+  float acc[CPL][VEC];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
+
+  auto emit = [&](uint32_t row, bool starts, bool ends, int64_t head_k) {
+    if (row >= n_rows) return;  // OOB sentinel run: gradient dropped
+    if (starts && ends) {
+      finalize_row<OPT, VEC, CPL>(a, row, gl, lpr, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, head_k) : 0);
+    } else {
+      float* dst = a.partial + ((t * 2) + (starts ? 1 : 0)) * (int64_t)dim;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (col < dim) RowIO<VEC>::store(dst + col, acc[c]);
+      }
+    }
+  };
+
+  for (int64_t kb = k0; kb < k1; kb += U) {
+    float r[U][CPL][VEC];
+    uint32_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t k = kb + u;
+      bool valid = k < k1;
+      kk[u] = valid ? keys[k] : 0xFFFFFFFFu;
+      int64_t p = valid ? pos[k] : 0;
+      bool live = valid && kk[u] < n_rows;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (live && col < dim) {
+          RowIO<VEC>::load(grad + p * dim + col, r[u][c]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t k = kb + u;
+      if (k < k1) {
+        if (kk[u] != run_row) {
+          emit(run_row, run_starts, true, run_start);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
+          run_row = kk[u];
+          run_starts = true;
+          run_start = k;
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[c][e] += r[u][c][e];
+      }
+    }
+  }
+  bool ends = (k1 >= n) || keys[k1] != run_row;
+  emit(run_row, run_starts, ends, run_start);
+}
+
+// fix-up: one lane group per tile; works only on tiles that hold the head part of a
+// segment continuing into the next tile.
+template <int OPT, int VEC, int CPL>
+__global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                        uint32_t n_rows, ApplyArgs a, int lpr_log2,
+                                                        int64_t n_tiles) {
+  constexpr int T = RS_DEDUP_TILE;
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
+  if (t >= n_tiles - 1) return;
+  const int64_t k0 = t * T, klast = k0 + T - 1, knext = k0 + T;
+  if (knext >= n) return;
+  const uint32_t row = keys[klast];
+  if (row >= n_rows || keys[knext] != row) return;  // last run does not continue
+  // the segment must start inside this tile
+  if (keys[k0] == row && k0 > 0 && keys[k0 - 1] == row) return;
+  const int dim = a.dim;
+  float acc[CPL][VEC];
+  const float* p1 = a.partial + (t * 2 + 1) * (int64_t)dim;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    int col = (gl + c * lpr) * VEC;
+    if (col < dim) {
+      RowIO<VEC>::load(p1 + col, acc[c]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
+    }
+  }
+  for (int64_t tt = t + 1; tt < n_tiles; ++tt) {
+    const float* p0 = a.partial + (tt * 2) * (int64_t)dim;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      int col = (gl + c * lpr) * VEC;
+      if (col < dim) {
+        float v[VEC];
+        RowIO<VEC>::load(p0 + col, v);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[c][e] += v[e];
+      }
+    }
+    int64_t kn = (tt + 1) * T;
+    if (kn >= n || keys[kn] != row) break;
+  }
+  finalize_row<OPT, VEC, CPL>(a, row, gl, lpr, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, klast) : 0);
+}
+
+__global__ void head_flags_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t n_rows,
+                                  int32_t* __restrict__ flags) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t k = keys[i];
+    flags[i] = (k < n_rows && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+  }
+}
+
+// Keras dense sweep over untouched rows (touched rows were fully updated by the sparse pass)
+template <int VEC>
+__global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restrict__ w,
+                                                                float* __restrict__ m,
+                                                                float* __restrict__ v, int64_t n_rows,
+                                                                int dim, rs_adam_params p,
+                                                                const uint32_t* __restrict__ bitmap) {
+  const int64_t chunks_per_row = dim / VEC;
+  const int64_t total = n_rows * chunks_per_row;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < total; i += stride) {
+    int64_t row = i / chunks_per_row;
+    if ((bitmap[row >> 5] >> (row & 31)) & 1u) continue;
+    int64_t off = i * VEC;
+    float ww[VEC], mm[VEC], vv[VEC];
+    RowIO<VEC>::load(w + off, ww);
+    RowIO<VEC>::load(m + off, mm);
+    RowIO<VEC>::load(v + off, vv);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float m1 = mm[e] * p.beta1;
+      float v1 = vv[e] * p.beta2;
+      float upd = (p.lr * m1) / (sqrtf(v1) + p.epsilon);
+      mm[e] = m1;
+      vv[e] = v1;
+      ww[e] = ww[e] - upd;
+    }
+    RowIO<VEC>::store(w + off, ww);
+    RowIO<VEC>::store(m + off, mm);
+    RowIO<VEC>::store(v + off, vv);
+  }
+}
+
+// ---- host launchers -------------------------------------------------------------------
+template <template <int, int> class K>
+struct Noop {};
+
+#define RS_DISPATCH_VEC_CPL(geom, CALL)                                   \
+  do {                                                                    \
+    switch ((geom).vec * 100 + (geom).cpl) {                              \
+      case 401: { constexpr int VEC = 4, CPL = 1; CALL; } break;          \
+      case 402: { constexpr int VEC = 4, CPL = 2; CALL; } break;          \
+      case 404: { constexpr int VEC = 4, CPL = 4; CALL; } break;          \
+      case 408: { constexpr int VEC = 4, CPL = 8; CALL; } break;          \
+      case 201: { constexpr int VEC = 2, CPL = 1; CALL; } break;          \
+      case 202: { constexpr int VEC = 2, CPL = 2; CALL; } break;          \
+      case 204: { constexpr int VEC = 2, CPL = 4; CALL; } break;          \
+      case 101: { constexpr int VEC = 1, CPL = 1; CALL; } break;          \
+      case 102: { constexpr int VEC = 1, CPL = 2; CALL; } break;          \
+      case 104: { constexpr int VEC = 1, CPL = 4; CALL; } break;          \
+      default:                                                            \
+        set_error("row geometry vec=%d cpl=%d unsupported (dim too large)", (geom).vec, (geom).cpl); \
+        return RS_E_UNSUPPORTED;                                          \
+    }                                                                     \
+  } while (0)
+
+static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos, int64_t n,
+                               int64_t n_rows, const float* grad, const ApplyArgs& a,
+                               const RowGeom& geom, hipStream_t st) {
+  const int64_t n_tiles = ceil_div(n, RS_DEDUP_TILE);
+  const int gpb = 256 >> geom.lpr_log2;
+  const int64_t blocks = ceil_div(n_tiles, gpb);
+  if (blocks == 0) return RS_OK;
+#define RS_SEG_LAUNCH(OPTV)                                                                     \
+  RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
+    seg_tile_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, pos, n, (uint32_t)n_rows, grad, \
+                                                            a, geom.lpr_log2, n_tiles);         \
+    seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,      \
+                                                             geom.lpr_log2, n_tiles);           \
+  }))
+  switch (opt) {
+    case OPT_SGD: RS_SEG_LAUNCH(OPT_SGD); break;
+    case OPT_LAZY: RS_SEG_LAUNCH(OPT_LAZY); break;
+    case OPT_KERAS: RS_SEG_LAUNCH(OPT_KERAS); break;
+    case OPT_EMIT: RS_SEG_LAUNCH(OPT_EMIT); break;
+    default: set_error("unknown optimizer %d", opt); return RS_E_INVALID;
+  }
+#undef RS_SEG_LAUNCH
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t dim, const void* ids,
+                                    int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
+                                    int32_t n_slots, float* out, int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(dim > 0, "dim must be > 0");
+  RS_CHECK_ARG(n_ids >= 0, "n_ids must be >= 0");
+  RS_CHECK_ARG(n_slots >= 1, "n_slots must be >= 1");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(n_ids == 0 || (table && ids && out), "null pointer");
+  if (n_ids == 0) return RS_OK;
+  const void* ptrs[2] = {table, out};
+  RowGeom geom = row_geom(dim, ptrs, 2);
+  hipStream_t st = as_stream(stream);
+  const int gpb = 256 >> geom.lpr_log2;
+  int64_t blocks = std::min<int64_t>(ceil_div(n_ids, gpb * 4), 256 * 16);
+  RS_DISPATCH_VEC_CPL(geom, ({
+    gather_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(table, n_rows, dim, ids, id_dtype, n_ids,
+                                                    slot_offsets, n_slots, out, err_flag,
+                                                    geom.lpr_log2);
+  }));
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static size_t partial_bytes(int64_t n_ids, int32_t dim) {
+  return (size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float);
+}
+
+extern "C" size_t rs_dedup_workspace_size(int64_t n_ids, int32_t dim) {
+  return align_up(partial_bytes(n_ids, dim), 256) + align_up((size_t)n_ids * 4, 256) +
+         exclusive_scan_ws_size(n_ids) + 256;
+}
+
+extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                           int64_t n_ids, const float* grad_out, int32_t dim,
+                                           int64_t n_rows, uint32_t* uniq_rows, float* uniq_grad,
+                                           void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(sorted_rows && sorted_pos && grad_out && uniq_rows && uniq_grad, "null pointer");
+  if (ws_bytes < rs_dedup_workspace_size(n_ids, dim)) {
+    set_error("dedup workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  Carver c(workspace, ws_bytes);
+  float* partial = c.take<float>(partial_bytes(n_ids, dim) / 4);
+  int32_t* seg = c.take<int32_t>(n_ids);
+  void* scan_ws = c.take<char>(exclusive_scan_ws_size(n_ids));
+  int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
+  head_flags_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, seg);
+  RS_CHECK_LAUNCH();
+  int32_t s = exclusive_scan_i32(seg, seg, n_ids, nullptr, scan_ws, exclusive_scan_ws_size(n_ids), st);
+  if (s) return s;
+  ApplyArgs a{};
+  a.dim = dim;
+  a.partial = partial;
+  a.uniq_grad = uniq_grad;
+  a.uniq_rows = uniq_rows;
+  a.seg_excl = seg;
+  const void* ptrs[2] = {grad_out, uniq_grad};
+  RowGeom geom = row_geom(dim, ptrs, 2);
+  return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);
+}
+
+extern "C" size_t rs_apply_workspace_size(int64_t n_ids, int32_t dim) {
+  return align_up(partial_bytes(n_ids, dim), 256) + 256;
+}
+
+extern "C" int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float* v, int64_t n_rows,
+                                      int32_t dim, const uint32_t* sorted_rows,
+                                      const int32_t* sorted_pos, int64_t n_ids,
+                                      const float* grad_out, const rs_adam_params* params,
+                                      uint32_t* touched_bitmap, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(params, "params is null");
+  RS_CHECK_ARG(opt == RS_OPT_SGD || opt == RS_OPT_LAZY_ADAM || opt == RS_OPT_KERAS_ADAM,
+               "unknown optimizer %d", opt);
+  RS_CHECK_ARG(opt == RS_OPT_SGD || (m && v), "Adam needs m and v slots");
+  RS_CHECK_ARG(opt != RS_OPT_KERAS_ADAM || touched_bitmap, "Keras Adam needs the touched bitmap");
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(table && sorted_rows && sorted_pos && grad_out, "null pointer");
+  if (ws_bytes < rs_apply_workspace_size(n_ids, dim)) {
+    set_error("apply workspace too small: need %zu", rs_apply_workspace_size(n_ids, dim));
+    return RS_E_WORKSPACE;
+  }
+  ApplyArgs a{};
+  a.table = table;
+  a.m = m;
+  a.v = v;
+  a.dim = dim;
+  a.p = *params;
+  a.bitmap = touched_bitmap;
+  a.partial = static_cast<float*>(workspace);
+  const void* ptrs[4] = {table, grad_out, m ? m : table, v ? v : table};
+  RowGeom geom = row_geom(dim, ptrs, 4);
+  return launch_segments(opt, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom,
+                         as_stream(stream));
+}
+
+extern "C" int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_rows,
+                                             int32_t dim, const rs_adam_params* params,
+                                             uint32_t* touched_bitmap, void* stream) {
+  RS_CHECK_ARG(table && m && v && params && touched_bitmap, "null pointer");
+  RS_CHECK_ARG(dim > 0 && n_rows > 0, "bad sizes");
+  hipStream_t st = as_stream(stream);
+  const void* ptrs[3] = {table, m, v};
+  RowGeom geom = row_geom(dim, ptrs, 3);
+  int64_t total = n_rows * (dim / geom.vec);
+  int64_t blocks = std::min<int64_t>(ceil_div(total, 256), 256 * 32);
+  switch (geom.vec) {
+    case 4: keras_dense_sweep_kernel<4><<<blocks, 256, 0, st>>>(table, m, v, n_rows, dim, *params, touched_bitmap); break;
+    case 2: keras_dense_sweep_kernel<2><<<blocks, 256, 0, st>>>(table, m, v, n_rows, dim, *params, touched_bitmap); break;
+    default: keras_dense_sweep_kernel<1><<<blocks, 256, 0, st>>>(table, m, v, n_rows, dim, *params, touched_bitmap); break;
+  }
+  RS_CHECK_LAUNCH();
+  RS_CHECK_HIP(hipMemsetAsync(touched_bitmap, 0, (size_t)ceil_div(n_rows, 32) * 4, st));
+  return RS_OK;
+}

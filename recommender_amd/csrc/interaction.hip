@@ -1,0 +1,496 @@
+// interaction.hip — DLRM DotInteraction (a-4, ctr/layers.py:17-43) and the DeepFM
+// second-order FM term (a-5, ctr/model.py:21-23).
+//
+// Fast path (F <= 32, D % 16 == 0 fwd / D % 32 == 0 bwd): one wave per sample on the exact-fp32
+// MFMA (gfx950 has no xf32; v_mfma_f32_*_f32 is an fma chain at the f32 vector rate).
+//   fwd  Z = X·Xᵀ as three 16x16 blocks (0,0), (0,1), (1,1) of v_mfma_f32_16x16x4_f32 — the
+//        (1,0) block is the mirror and is never computed. The K (= D) axis is permuted so that
+//        lane group g = lane>>4 reads 16 contiguous bytes per row per instruction straight from
+//        the table into VGPRs (no LDS staging of X); the same register is both the A and the B
+//        operand of the diagonal blocks.
+//   bwd  dX = S·X with S = M + Mᵀ (M = dZ on the kept pairs) on v_mfma_f32_32x32x2_f32, D
+//        permuted so that every lane loads / stores NTILE = D/32 contiguous floats: a
+//        half-wave moves one whole row per instruction, so the re-gather of X and the
+//        grad-row stores are fully coalesced.
+// DLRM variant (rs_dlrm_interaction_*): X rows come straight from the embedding table by id
+// (fused gather), row F-1 is the bottom-MLP output, and the output row is the top-MLP input
+// [Z (F*F, skip_gather), dense (D)] (ctr/model.py:51-55), so the [B,S,D] embedding tensor
+// is never materialised in HBM; the backward re-gathers the rows instead of re-reading a
+// saved copy (one 512-B read instead of a write + a read per row).
+#include "common.hpp"
+
+namespace rs {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct InterMode {
+  int self_interaction;
+  int skip_gather;
+};
+
+__device__ __forceinline__ bool keep_pair(int i, int j, int self_i) {
+  return self_i ? (i >= j) : (i < j);
+}
+// compact output index of kept pair (i,j) (row-major boolean_mask order, ctr/layers.py:39-42)
+__device__ __forceinline__ int compact_index(int i, int j, int F, int self_i) {
+  return self_i ? (i * (i + 1) / 2 + j) : (i * F - i * (i + 1) / 2 + (j - i - 1));
+}
+__host__ __device__ inline int out_width(int F, int self_i, int skip_gather) {
+  return skip_gather ? F * F : (self_i ? F * (F + 1) / 2 : F * (F - 1) / 2);
+}
+
+// X row source: embedding rows by id (DLRM) or a dense [B, F, D] tensor
+struct GatherSrc {
+  const float* table;
+  int64_t n_rows;
+  const void* ids;
+  int32_t id_dtype;
+  int32_t n_slots;
+  const int64_t* slot_offsets;
+  const float* dense;  // [B, D], row F-1
+  int32_t* err_flag;
+  // pointer to X[b][i] (nullptr = zero row)
+  __device__ __forceinline__ const float* row(int64_t b, int i, int D, bool& oob) const {
+    if (i < n_slots) {
+      int64_t r = global_row(ids, id_dtype, b * n_slots + i, slot_offsets, n_slots, n_rows);
+      if (r < 0) {
+        oob = true;
+        return nullptr;
+      }
+      return table + r * D;
+    }
+    if (i == n_slots) return dense + b * D;
+    return nullptr;
+  }
+};
+struct DenseSrc {
+  const float* x;
+  int F;
+  __device__ __forceinline__ const float* row(int64_t b, int i, int D, bool&) const {
+    return i < F ? x + (b * F + i) * (int64_t)D : nullptr;
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// forward, MFMA: one wave per sample, 4 waves per block
+// ---------------------------------------------------------------------------------------
+template <int D, class Src, bool DLRM_OUT>
+__global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, int F, InterMode md,
+                                                      float* __restrict__ out, int64_t out_stride) {
+  constexpr int NT = D / 16;  // float4 loads per lane per block-row
+  __shared__ float zt[4][32][33];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= batch) return;
+  const int r = lane & 15, g = lane >> 4;
+  bool oob = false;
+  const float* p0 = src.row(b, r, D, oob);
+  const float* p1 = src.row(b, 16 + r, D, oob);
+  if (16 + r >= F) p1 = nullptr;
+  float4 a0[NT], a1[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int col = g * 4 + 16 * t;
+    a0[t] = p0 ? *reinterpret_cast<const float4*>(p0 + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    a1[t] = p1 ? *reinterpret_cast<const float4*>(p1 + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float x0[4] = {a0[t].x, a0[t].y, a0[t].z, a0[t].w};
+    const float x1[4] = {a1[t].x, a1[t].y, a1[t].z, a1[t].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[c], x0[c], c00, 0, 0, 0);
+      c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[c], x1[c], c01, 0, 0, 0);
+      c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[c], x1[c], c11, 0, 0, 0);
+    }
+  }
+  // C layout: lane holds G[4g + reg][r] of each block; mirror into a full 32x32 tile
+  float(*z)[33] = zt[wave];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    int i = 4 * g + reg;
+    z[i][r] = c00[reg];
+    z[i][16 + r] = c01[reg];
+    z[16 + r][i] = c01[reg];
+    z[16 + i][16 + r] = c11[reg];
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  float* orow = out + b * out_stride;
+  if (md.skip_gather) {
+    const int FF = F * F;
+    for (int o = lane; o < FF; o += 64) {
+      int i = o / F, j = o - i * F;
+      orow[o] = keep_pair(i, j, md.self_interaction) ? z[i][j] : 0.f;
+    }
+  } else {
+    for (int o = lane; o < F * F; o += 64) {
+      int i = o / F, j = o - i * F;
+      if (keep_pair(i, j, md.self_interaction)) orow[compact_index(i, j, F, md.self_interaction)] = z[i][j];
+    }
+  }
+  if constexpr (DLRM_OUT) {
+    // concat the bottom-MLP output behind Z (ctr/model.py:54)
+    const float* dn = src.dense + b * D;
+    float* od = orow + out_width(F, md.self_interaction, md.skip_gather);
+    for (int d = lane; d < D; d += 64) od[d] = dn[d];
+    if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backward, MFMA: dX = S · X, one wave per sample
+// ---------------------------------------------------------------------------------------
+template <int D, class Src, bool DLRM_OUT>
+__global__ __launch_bounds__(256) void inter_bwd_mfma(Src src, int64_t batch, int F, InterMode md,
+                                                      const float* __restrict__ gout, int64_t gstride,
+                                                      float* __restrict__ gx,      // dense: [B,F,D]
+                                                      float* __restrict__ gemb,    // DLRM: [B*S, D]
+                                                      float* __restrict__ gdense)  // DLRM: [B, D]
+{
+  constexpr int NTILE = D / 32;
+  constexpr int KS = 16;  // up to 32 k-rows in steps of 2
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= batch) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int ks = (F + 1) >> 1;
+  const float* grow = gout + b * gstride;
+  bool oob = false;
+
+  floatx16 acc[NTILE];
+#pragma unroll
+  for (int c = 0; c < NTILE; ++c)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[c][e] = 0.f;
+
+  // S[r][k] for k = 2s + h
+  auto s_val = [&](int i, int k) -> float {
+    if (i >= F || k >= F) return 0.f;
+    float v = 0.f;
+    if (keep_pair(i, k, md.self_interaction))
+      v += md.skip_gather ? grow[i * F + k] : grow[compact_index(i, k, F, md.self_interaction)];
+    if (keep_pair(k, i, md.self_interaction))
+      v += md.skip_gather ? grow[k * F + i] : grow[compact_index(k, i, F, md.self_interaction)];
+    return v;
+  };
+
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s < ks) {
+      const int k = 2 * s + h;
+      const float* xr = k < F ? src.row(b, k, D, oob) : nullptr;
+      float xv[NTILE];
+      if (xr) {
+        if constexpr (NTILE == 4) {
+          float4 t = *reinterpret_cast<const float4*>(xr + NTILE * r);
+          xv[0] = t.x; xv[1] = t.y; xv[2] = t.z; xv[3] = t.w;
+        } else if constexpr (NTILE == 2) {
+          float2 t = *reinterpret_cast<const float2*>(xr + NTILE * r);
+          xv[0] = t.x; xv[1] = t.y;
+        } else {
+#pragma unroll
+          for (int c = 0; c < NTILE; ++c) xv[c] = xr[NTILE * r + c];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NTILE; ++c) xv[c] = 0.f;
+      }
+      const float av = s_val(r, k);
+#pragma unroll
+      for (int c = 0; c < NTILE; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xv[c], acc[c], 0, 0, 0);
+    }
+  }
+  // D layout: acc[c][reg] = dX[i = (reg&3) + 8*(reg>>2) + 4*h][d = NTILE*r + c]
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (i >= F) continue;
+    float v[NTILE];
+#pragma unroll
+    for (int c = 0; c < NTILE; ++c) v[c] = acc[c][reg];
+    float* dst;
+    if constexpr (DLRM_OUT) {
+      if (i < src.n_slots) {
+        dst = gemb + (b * src.n_slots + i) * (int64_t)D;
+      } else {
+        // bottom-MLP row: interaction grad + the concat pass-through (ctr/model.py:54)
+        const float* gd = grow + out_width(F, md.self_interaction, md.skip_gather);
+#pragma unroll
+        for (int c = 0; c < NTILE; ++c) v[c] += gd[NTILE * r + c];
+        dst = gdense + b * D;
+      }
+    } else {
+      dst = gx + (b * F + i) * (int64_t)D;
+    }
+    if constexpr (NTILE == 4) {
+      *reinterpret_cast<float4*>(dst + NTILE * r) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (NTILE == 2) {
+      *reinterpret_cast<float2*>(dst + NTILE * r) = make_float2(v[0], v[1]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < NTILE; ++c) dst[NTILE * r + c] = v[c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// generic (any F, D): one wave per sample, X staged in LDS
+// ---------------------------------------------------------------------------------------
+template <class Src, bool DLRM_OUT>
+__global__ __launch_bounds__(64) void inter_fwd_generic(Src src, int64_t batch, int F, int D,
+                                                        InterMode md, float* __restrict__ out,
+                                                        int64_t out_stride) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [F][D+1]
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int ld = D + 1;
+  bool oob = false;
+  for (int i = 0; i < F; ++i) {
+    const float* xr = src.row(b, i, D, oob);
+    for (int d = lane; d < D; d += 64) xs[i * ld + d] = xr ? xr[d] : 0.f;
+  }
+  __syncthreads();
+  float* orow = out + b * out_stride;
+  for (int o = lane; o < F * F; o += 64) {
+    int i = o / F, j = o - i * F;
+    bool keep = keep_pair(i, j, md.self_interaction);
+    if (!keep && !md.skip_gather) continue;
+    float s = 0.f;
+    if (keep)
+      for (int d = 0; d < D; ++d) s = fmaf(xs[i * ld + d], xs[j * ld + d], s);
+    if (md.skip_gather)
+      orow[o] = s;
+    else
+      orow[compact_index(i, j, F, md.self_interaction)] = s;
+  }
+  if constexpr (DLRM_OUT) {
+    float* od = orow + out_width(F, md.self_interaction, md.skip_gather);
+    for (int d = lane; d < D; d += 64) od[d] = src.dense[b * D + d];
+    if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+  }
+}
+
+template <class Src, bool DLRM_OUT>
+__global__ __launch_bounds__(64) void inter_bwd_generic(Src src, int64_t batch, int F, int D,
+                                                        InterMode md, const float* __restrict__ gout,
+                                                        int64_t gstride, float* __restrict__ gx,
+                                                        float* __restrict__ gemb,
+                                                        float* __restrict__ gdense) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;                 // [F][D+1]
+  float* ss = sm + F * (D + 1);   // [F][F+1]
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int ld = D + 1, ls = F + 1;
+  bool oob = false;
+  const float* grow = gout + b * gstride;
+  for (int i = 0; i < F; ++i) {
+    const float* xr = src.row(b, i, D, oob);
+    for (int d = lane; d < D; d += 64) xs[i * ld + d] = xr ? xr[d] : 0.f;
+  }
+  for (int o = lane; o < F * F; o += 64) {
+    int i = o / F, k = o - i * F;
+    float v = 0.f;
+    if (keep_pair(i, k, md.self_interaction))
+      v += md.skip_gather ? grow[i * F + k] : grow[compact_index(i, k, F, md.self_interaction)];
+    if (keep_pair(k, i, md.self_interaction))
+      v += md.skip_gather ? grow[k * F + i] : grow[compact_index(k, i, F, md.self_interaction)];
+    ss[i * ls + k] = v;
+  }
+  __syncthreads();
+  for (int o = lane; o < F * D; o += 64) {
+    int i = o / D, d = o - i * D;
+    float s = 0.f;
+    for (int k = 0; k < F; ++k) s = fmaf(ss[i * ls + k], xs[k * ld + d], s);
+    if constexpr (DLRM_OUT) {
+      if (i < src.n_slots) {
+        gemb[(b * src.n_slots + i) * (int64_t)D + d] = s;
+      } else {
+        gdense[b * D + d] = s + grow[out_width(F, md.self_interaction, md.skip_gather) + d];
+      }
+    } else {
+      gx[(b * F + i) * (int64_t)D + d] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// FM (DeepFM second order): out[b] = 0.5 * Σ_d (sum_f e)^2 - Σ_f e^2
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fm_fwd_kernel(const float* __restrict__ emb, int64_t batch,
+                                                     int F, int D, float* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= batch) return;
+  const float* e = emb + b * F * (int64_t)D;
+  float part = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    float s = 0.f, q = 0.f;
+    for (int f = 0; f < F; ++f) {
+      float x = e[f * D + d];
+      s += x;
+      q += x * x;
+    }
+    part += s * s - q;
+  }
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off);
+  if (lane == 0) out[b] = 0.5f * part;
+}
+
+__global__ __launch_bounds__(256) void fm_bwd_kernel(const float* __restrict__ emb,
+                                                     const float* __restrict__ gout, int64_t batch,
+                                                     int F, int D, float* __restrict__ gemb) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= batch) return;
+  const float* e = emb + b * F * (int64_t)D;
+  float* ge = gemb + b * F * (int64_t)D;
+  const float g = gout[b];
+  for (int d = lane; d < D; d += 64) {
+    float s = 0.f;
+    for (int f = 0; f < F; ++f) s += e[f * D + d];
+    // d/de_fd of 0.5*((Σe)^2 - Σe^2) = Σe - e_fd
+    for (int f = 0; f < F; ++f) ge[f * D + d] = g * (s - e[f * D + d]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host dispatch
+// ---------------------------------------------------------------------------------------
+template <class Src, bool DLRM_OUT>
+static int32_t launch_fwd(const Src& src, int64_t batch, int F, int D, InterMode md, float* out,
+                          int64_t out_stride, bool aligned16, hipStream_t st) {
+  if (batch == 0) return RS_OK;
+  if (F <= 32 && aligned16) {
+    int64_t blocks = ceil_div(batch, 4);
+    switch (D) {
+      case 16: inter_fwd_mfma<16, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, out, out_stride); RS_CHECK_LAUNCH(); return RS_OK;
+      case 32: inter_fwd_mfma<32, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, out, out_stride); RS_CHECK_LAUNCH(); return RS_OK;
+      case 64: inter_fwd_mfma<64, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, out, out_stride); RS_CHECK_LAUNCH(); return RS_OK;
+      case 128: inter_fwd_mfma<128, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, out, out_stride); RS_CHECK_LAUNCH(); return RS_OK;
+      case 256: inter_fwd_mfma<256, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, out, out_stride); RS_CHECK_LAUNCH(); return RS_OK;
+      default: break;
+    }
+  }
+  size_t lds = (size_t)F * (D + 1) * 4;
+  if (lds > 64 * 1024) {
+    set_error("interaction F=%d D=%d too large for the generic kernel", F, D);
+    return RS_E_UNSUPPORTED;
+  }
+  inter_fwd_generic<Src, DLRM_OUT><<<batch, 64, lds, st>>>(src, batch, F, D, md, out, out_stride);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+template <class Src, bool DLRM_OUT>
+static int32_t launch_bwd(const Src& src, int64_t batch, int F, int D, InterMode md,
+                          const float* gout, int64_t gstride, float* gx, float* gemb, float* gdense,
+                          bool aligned16, hipStream_t st) {
+  if (batch == 0) return RS_OK;
+  if (F <= 32 && aligned16) {
+    int64_t blocks = ceil_div(batch, 4);
+    switch (D) {
+      case 32: inter_bwd_mfma<32, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, gout, gstride, gx, gemb, gdense); RS_CHECK_LAUNCH(); return RS_OK;
+      case 64: inter_bwd_mfma<64, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, gout, gstride, gx, gemb, gdense); RS_CHECK_LAUNCH(); return RS_OK;
+      case 128: inter_bwd_mfma<128, Src, DLRM_OUT><<<blocks, 256, 0, st>>>(src, batch, F, md, gout, gstride, gx, gemb, gdense); RS_CHECK_LAUNCH(); return RS_OK;
+      default: break;
+    }
+  }
+  size_t lds = ((size_t)F * (D + 1) + (size_t)F * (F + 1)) * 4;
+  if (lds > 64 * 1024) {
+    set_error("interaction F=%d D=%d too large for the generic kernel", F, D);
+    return RS_E_UNSUPPORTED;
+  }
+  inter_bwd_generic<Src, DLRM_OUT><<<batch, 64, lds, st>>>(src, batch, F, D, md, gout, gstride, gx,
+                                                           gemb, gdense);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int32_t rs_dot_interaction_fwd(const float* x, int64_t batch, int32_t F, int32_t D,
+                                          int32_t self_interaction, int32_t skip_gather, float* out,
+                                          int64_t out_stride, void* stream) {
+  RS_CHECK_ARG(F >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  RS_CHECK_ARG(out_stride >= out_width(F, self_interaction, skip_gather), "out_stride too small");
+  RS_CHECK_ARG(batch == 0 || (x && out), "null pointer");
+  DenseSrc src{x, F};
+  return launch_fwd<DenseSrc, false>(src, batch, F, D, {self_interaction, skip_gather}, out,
+                                     out_stride, al16(x), as_stream(stream));
+}
+
+extern "C" int32_t rs_dot_interaction_bwd(const float* x, const float* grad_out, int64_t batch,
+                                          int32_t F, int32_t D, int32_t self_interaction,
+                                          int32_t skip_gather, int64_t grad_stride, float* grad_x,
+                                          void* stream) {
+  RS_CHECK_ARG(F >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  RS_CHECK_ARG(grad_stride >= out_width(F, self_interaction, skip_gather), "grad_stride too small");
+  RS_CHECK_ARG(batch == 0 || (x && grad_out && grad_x), "null pointer");
+  DenseSrc src{x, F};
+  return launch_bwd<DenseSrc, false>(src, batch, F, D, {self_interaction, skip_gather}, grad_out,
+                                     grad_stride, grad_x, nullptr, nullptr, al16(x) && al16(grad_x),
+                                     as_stream(stream));
+}
+
+extern "C" int32_t rs_dlrm_interaction_fwd(const float* table, int64_t n_rows, int32_t D,
+                                           const void* ids, int32_t id_dtype, int32_t n_slots,
+                                           const int64_t* slot_offsets, const float* dense,
+                                           int64_t batch, float* out, int64_t out_stride,
+                                           int32_t* err_flag, void* stream) {
+  const int F = n_slots + 1;
+  RS_CHECK_ARG(n_slots >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(out_stride >= F * F + D, "out_stride too small");
+  RS_CHECK_ARG(batch == 0 || (table && ids && dense && out), "null pointer");
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
+  return launch_fwd<GatherSrc, true>(src, batch, F, D, {0, 1}, out, out_stride,
+                                     al16(table) && al16(dense), as_stream(stream));
+}
+
+extern "C" int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D,
+                                           const void* ids, int32_t id_dtype, int32_t n_slots,
+                                           const int64_t* slot_offsets, const float* dense,
+                                           int64_t batch, const float* grad_out, int64_t grad_stride,
+                                           float* grad_emb, float* grad_dense, void* stream) {
+  const int F = n_slots + 1;
+  RS_CHECK_ARG(n_slots >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  RS_CHECK_ARG(grad_stride >= F * F + D, "grad_stride too small");
+  RS_CHECK_ARG(batch == 0 || (table && ids && dense && grad_out && grad_emb && grad_dense),
+               "null pointer");
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, nullptr};
+  return launch_bwd<GatherSrc, true>(src, batch, F, D, {0, 1}, grad_out, grad_stride, nullptr,
+                                     grad_emb, grad_dense,
+                                     al16(table) && al16(dense) && al16(grad_emb) && al16(grad_dense),
+                                     as_stream(stream));
+}
+
+extern "C" int32_t rs_fm_fwd(const float* emb, int64_t batch, int32_t F, int32_t D, float* out,
+                             void* stream) {
+  RS_CHECK_ARG(F >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  if (batch == 0) return RS_OK;
+  RS_CHECK_ARG(emb && out, "null pointer");
+  fm_fwd_kernel<<<ceil_div(batch, 4), 256, 0, as_stream(stream)>>>(emb, batch, F, D, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t batch, int32_t F,
+                             int32_t D, float* grad_emb, void* stream) {
+  RS_CHECK_ARG(F >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  if (batch == 0) return RS_OK;
+  RS_CHECK_ARG(emb && grad_out && grad_emb, "null pointer");
+  fm_bwd_kernel<<<ceil_div(batch, 4), 256, 0, as_stream(stream)>>>(emb, grad_out, batch, F, D,
+                                                                   grad_emb);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}

@@ -1,0 +1,408 @@
+// sort.hip — stable LSD radix sort of embedding rows (the `unique` half of Keras'
+// _deduplicate_indexed_slices, SURVEY §2.3 row "Gather-gradient + Unique + UnsortedSegmentSum"),
+// plus the device-wide scans the dedup and sharding passes use.
+//
+// Design (MI355X): keys are global table rows (uint32, < 2^31), values are the original
+// flattened positions p = b*S + s. Only ceil(log2(n_rows+1)) key bits are sorted, split evenly
+// into passes of <= 8 bits. Each pass = per-tile digit histogram → one-block exclusive scan
+// over [digit][tile] → stable scatter. Inside a tile each wave owns a contiguous 64*K-key
+// stretch; a key's rank among equal digits in its wave comes from a 64-lane ballot match
+// (RADIX_BITS ballots, popcount below the lane), so order is exactly the input order.
+#include "common.hpp"
+
+namespace rs {
+
+constexpr int kSortThreads = 256;         // 4 waves
+constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile
+constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
+constexpr int kMaxBins = 256;
+
+// ---- keys from ids ------------------------------------------------------------------
+__global__ void make_keys_kernel(const void* __restrict__ ids, int32_t dtype, int64_t n,
+                                 const int64_t* __restrict__ slot_offsets, int32_t n_slots,
+                                 int64_t n_rows, uint32_t* __restrict__ keys,
+                                 int32_t* __restrict__ vals, int32_t* err_flag) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  bool oob = false;
+  for (; i < n; i += stride) {
+    int64_t r = global_row(ids, dtype, i, slot_offsets, n_slots, n_rows);
+    if (r < 0) {
+      oob = true;
+      r = n_rows;  // sentinel: sorts after every valid row
+    }
+    keys[i] = static_cast<uint32_t>(r);
+    vals[i] = static_cast<int32_t>(i);
+  }
+  if (__any(oob) && (threadIdx.x & 63) == 0) flag_oob(err_flag);
+}
+
+// match mask: lanes of this wave whose digit equals mine
+template <int BITS>
+__device__ __forceinline__ uint64_t match_digit(uint32_t digit, bool valid) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    uint64_t bb = __ballot((digit >> b) & 1u);
+    m &= ((digit >> b) & 1u) ? bb : ~bb;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt64() {
+  int lane = threadIdx.x & 63;
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// histogram: hist[digit * n_tiles + tile]
+template <int BITS>
+__global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
+    const uint32_t* __restrict__ keys, int64_t n, int shift, int32_t* __restrict__ hist,
+    int n_tiles) {
+  constexpr int BINS = 1 << BITS;
+  __shared__ int32_t cnt[BINS];
+  for (int d = threadIdx.x; d < BINS; d += blockDim.x) cnt[d] = 0;
+  __syncthreads();
+  int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll 4
+  for (int k = 0; k < kSortKeysPerLane; ++k) {
+    int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+    if (i < n) {
+      uint32_t d = (keys[i] >> shift) & (BINS - 1);
+      atomicAdd(&cnt[d], 1);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < BINS; d += blockDim.x) hist[(int64_t)d * n_tiles + blockIdx.x] = cnt[d];
+}
+
+// single-block exclusive scan, in place (n up to a few 100k)
+__global__ __launch_bounds__(1024) void scan_single_block_kernel(int32_t* __restrict__ a, int64_t n,
+                                                                 int32_t* __restrict__ total) {
+  __shared__ int32_t part[1024];
+  int t = threadIdx.x;
+  int64_t per = (n + 1023) / 1024;
+  int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
+  int32_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += a[i];
+  part[t] = s;
+  __syncthreads();
+  // Hillis-Steele over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    int32_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int32_t run = t == 0 ? 0 : part[t - 1];
+  for (int64_t i = lo; i < hi; ++i) {
+    int32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  if (t == 1023 && total) *total = part[1023];
+}
+
+// stable scatter
+template <int BITS>
+__global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
+    const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, int64_t n, int shift,
+    const int32_t* __restrict__ hist_scanned, int n_tiles, uint32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out) {
+  constexpr int BINS = 1 << BITS;
+  constexpr int WAVES = kSortThreads / 64;
+  __shared__ int32_t wcnt[WAVES][BINS];  // per-wave running counts, then per-wave base offsets
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int d = threadIdx.x; d < WAVES * BINS; d += blockDim.x) (&wcnt[0][0])[d] = 0;
+  __syncthreads();
+
+  const int64_t base = (int64_t)blockIdx.x * kSortTile + (int64_t)wave * 64 * kSortKeysPerLane;
+  uint32_t key[kSortKeysPerLane];
+  int32_t val[kSortKeysPerLane];
+  int32_t rank[kSortKeysPerLane];
+#pragma unroll
+  for (int k = 0; k < kSortKeysPerLane; ++k) {
+    int64_t i = base + k * 64 + lane;
+    bool valid = i < n;
+    key[k] = valid ? keys_in[i] : 0u;
+    val[k] = valid ? vals_in[i] : 0;
+  }
+  const uint64_t lt = lanemask_lt64();
+#pragma unroll
+  for (int k = 0; k < kSortKeysPerLane; ++k) {
+    int64_t i = base + k * 64 + lane;
+    bool valid = i < n;
+    uint32_t d = (key[k] >> shift) & (BINS - 1);
+    uint64_t m = match_digit<BITS>(d, valid);
+    int32_t before = __popcll(m & lt);
+    int32_t prev = valid ? wcnt[wave][d] : 0;
+    rank[k] = prev + before;
+    // the highest lane of each match group publishes the new count (after all lanes read)
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (m >> lane) == 1ull) wcnt[wave][d] = prev + before + 1;
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // convert per-wave counts to absolute bases: global tile offset + earlier waves' counts
+  for (int d = threadIdx.x; d < BINS; d += blockDim.x) {
+    int32_t run = hist_scanned[(int64_t)d * n_tiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+      int32_t c = wcnt[w][d];
+      wcnt[w][d] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSortKeysPerLane; ++k) {
+    int64_t i = base + k * 64 + lane;
+    if (i < n) {
+      uint32_t d = (key[k] >> shift) & (BINS - 1);
+      int32_t dst = wcnt[wave][d] + rank[k];
+      keys_out[dst] = key[k];
+      vals_out[dst] = val[k];
+    }
+  }
+}
+
+// count distinct valid rows in a sorted key array
+__global__ void count_unique_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t n_rows,
+                                    int32_t* __restrict__ n_unique) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int32_t c = 0;
+  for (; i < n; i += stride) {
+    uint32_t k = keys[i];
+    c += (k < n_rows && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+  }
+  // wave reduce
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(n_unique, c);
+}
+
+static int key_bits_for(int64_t n_rows) {
+  // keys are in [0, n_rows] (n_rows = OOB sentinel)
+  int b = 1;
+  while (b < 32 && ((int64_t)1 << b) <= n_rows) ++b;
+  return b;
+}
+
+struct SortPlan {
+  int passes;
+  int bits;   // per pass
+  int n_tiles;
+};
+
+static SortPlan plan_sort(int64_t n_ids, int64_t n_rows) {
+  SortPlan p;
+  int kb = key_bits_for(n_rows);
+  p.passes = (kb + 7) / 8;
+  p.bits = (kb + p.passes - 1) / p.passes;
+  p.n_tiles = (int)ceil_div(n_ids, kSortTile);
+  return p;
+}
+
+// workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles]
+static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int32_t** vals_alt,
+                             int32_t** hist) {
+  int n_tiles = (int)ceil_div(n_ids, kSortTile);
+  *keys_alt = c.take<uint32_t>(n_ids);
+  *vals_alt = c.take<int32_t>(n_ids);
+  *hist = c.take<int32_t>((size_t)kMaxBins * n_tiles + 1);
+  return c.off;
+}
+
+template <int BITS>
+static int32_t launch_pass(const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                           int64_t n, int shift, int32_t* hist, int n_tiles, hipStream_t st) {
+  radix_hist_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, n, shift, hist, n_tiles);
+  RS_CHECK_LAUNCH();
+  scan_single_block_kernel<<<1, 1024, 0, st>>>(hist, (int64_t)(1 << BITS) * n_tiles, nullptr);
+  RS_CHECK_LAUNCH();
+  radix_scatter_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, vin, n, shift, hist, n_tiles,
+                                                               kout, vout);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static int32_t dispatch_pass(int bits, const uint32_t* kin, const int32_t* vin, uint32_t* kout,
+                             int32_t* vout, int64_t n, int shift, int32_t* hist, int n_tiles,
+                             hipStream_t st) {
+  switch (bits) {
+    case 1: return launch_pass<1>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 2: return launch_pass<2>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 3: return launch_pass<3>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 4: return launch_pass<4>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 5: return launch_pass<5>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 6: return launch_pass<6>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 7: return launch_pass<7>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 8: return launch_pass<8>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+  }
+  set_error("radix pass bits %d unsupported", bits);
+  return RS_E_UNSUPPORTED;
+}
+
+// Sort (keys, vals) ascending by key (stable); result ends in keys_out/vals_out.
+// keys_in/vals_in are clobbered.
+int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out,
+                         int32_t* vals_out, int64_t n, int64_t n_rows, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  SortPlan p = plan_sort(n, n_rows);
+  Carver c(ws, ws_bytes);
+  uint32_t* kalt;
+  int32_t* valt;
+  int32_t* hist;
+  sort_ws_layout(n, c, &kalt, &valt, &hist);
+  if (!c.ok()) {
+    set_error("sort workspace too small: need %zu have %zu", c.off, ws_bytes);
+    return RS_E_WORKSPACE;
+  }
+  // A = (keys_in, vals_in), B = (kalt, valt): A→B→A… and the last pass writes the output
+  uint32_t* ka = keys_in;
+  int32_t* va = vals_in;
+  for (int pass = 0; pass < p.passes; ++pass) {
+    bool last = pass == p.passes - 1;
+    uint32_t* kb = last ? keys_out : (ka == keys_in ? kalt : keys_in);
+    int32_t* vb = last ? vals_out : (va == vals_in ? valt : vals_in);
+    int32_t s = dispatch_pass(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, p.n_tiles, st);
+    if (s) return s;
+    ka = kb;
+    va = vb;
+  }
+  return RS_OK;
+}
+
+size_t radix_sort_ws_size(int64_t n) {
+  Carver c(nullptr, 0);
+  uint32_t* a;
+  int32_t* b;
+  int32_t* h;
+  return sort_ws_layout(n, c, &a, &b, &h) + 256;
+}
+
+// ---- device-wide exclusive scan of int32 (3-phase) -----------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 16;
+constexpr int kScanTile = kScanThreads * kScanPerThread;
+
+__global__ __launch_bounds__(kScanThreads) void scan_tile_sums_kernel(const int32_t* __restrict__ in,
+                                                                      int64_t n,
+                                                                      int32_t* __restrict__ sums) {
+  __shared__ int32_t red[kScanThreads / 64];
+  int64_t base = (int64_t)blockIdx.x * kScanTile;
+  int32_t s = 0;
+  for (int k = 0; k < kScanPerThread; ++k) {
+    int64_t i = base + (int64_t)k * kScanThreads + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) t += red[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_tile_apply_kernel(const int32_t* __restrict__ in,
+                                                                       int64_t n,
+                                                                       const int32_t* __restrict__ sums,
+                                                                       int32_t* __restrict__ out) {
+  // each thread scans a contiguous run of kScanPerThread elements
+  __shared__ int32_t part[kScanThreads];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPerThread;
+  int32_t v[kScanPerThread];
+  int32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; ++k) {
+    int64_t i = base + k;
+    v[k] = i < n ? in[i] : 0;
+    s += v[k];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < kScanThreads; off <<= 1) {
+    int32_t t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int32_t run = sums[blockIdx.x] + (threadIdx.x ? part[threadIdx.x - 1] : 0);
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; ++k) {
+    int64_t i = base + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+}
+
+size_t exclusive_scan_ws_size(int64_t n) { return align_up((ceil_div(n, kScanTile) + 1) * 4, 256); }
+
+// out may alias in. total (device, may be null) receives the sum.
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* total, void* ws,
+                           size_t ws_bytes, hipStream_t st) {
+  int64_t tiles = ceil_div(n, kScanTile);
+  if (ws_bytes < exclusive_scan_ws_size(n)) {
+    set_error("scan workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  int32_t* sums = static_cast<int32_t*>(ws);
+  if (n == 0) {
+    if (total) RS_CHECK_HIP(hipMemsetAsync(total, 0, 4, st));
+    return RS_OK;
+  }
+  scan_tile_sums_kernel<<<tiles, kScanThreads, 0, st>>>(in, n, sums);
+  RS_CHECK_LAUNCH();
+  scan_single_block_kernel<<<1, 1024, 0, st>>>(sums, tiles, total);
+  RS_CHECK_LAUNCH();
+  scan_tile_apply_kernel<<<tiles, kScanThreads, 0, st>>>(in, n, sums, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" size_t rs_sort_ids_workspace_size(int64_t n_ids) {
+  Carver c(nullptr, 0);
+  c.take<uint32_t>(n_ids);
+  c.take<int32_t>(n_ids);
+  return c.off + radix_sort_ws_size(n_ids) + 512;
+}
+
+extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
+                               const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                               uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
+                               int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(n_ids >= 0 && n_ids < (int64_t(1) << 31), "n_ids out of range");
+  RS_CHECK_ARG(n_rows > 0 && n_rows < (int64_t(1) << 31) - 1, "n_rows out of range");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(n_slots >= 1, "n_slots must be >= 1");
+  RS_CHECK_ARG(ids || n_ids == 0, "ids is null");
+  hipStream_t st = as_stream(stream);
+  if (n_unique) RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, sizeof(int32_t), st));
+  if (n_ids == 0) return RS_OK;
+  Carver c(workspace, ws_bytes);
+  uint32_t* keys = c.take<uint32_t>(n_ids);
+  int32_t* vals = c.take<int32_t>(n_ids);
+  size_t rest_off = align_up(c.off, 256);
+  if (rest_off > ws_bytes) {
+    set_error("sort workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
+  make_keys_kernel<<<blocks, 256, 0, st>>>(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, keys,
+                                           vals, err_flag);
+  RS_CHECK_LAUNCH();
+  int32_t s = radix_sort_pairs(keys, vals, sorted_rows, sorted_pos, n_ids, n_rows,
+                               static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, st);
+  if (s) return s;
+  if (n_unique) {
+    count_unique_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, n_unique);
+    RS_CHECK_LAUNCH();
+  }
+  return RS_OK;
+}

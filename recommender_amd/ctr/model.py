@@ -1,0 +1,81 @@
+"""ctr/model.py surface (reference ctr/model.py:6-58): DeepFM and DLRM over ONE shared
+Embedding(vocab_size, embedding_size) for all categorical slots (ctr/model.py:10,42).
+
+DLRM's lookup → concat(bottom MLP) → DotInteraction(False, True) → concat chain
+(ctr/model.py:49-55) runs as ONE fused kernel pair (rs_dlrm_interaction_fwd/bwd): the rows are
+gathered by id straight into the MFMA interaction and the top-MLP input [Z, bottom] is written
+directly; `self.interaction` is kept for the reference attribute surface.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..embedding import Embedding, SlabEmbedding
+from ..functional import dlrm_interaction, fm_interaction
+from .layers import MLP, DotInteraction
+
+
+class DeepFM(nn.Module):
+    def __init__(self, embedding_size, vocab_size, num_int_fea, num_cat_fea, mlp_units,
+                 device=None, slot_cardinalities=None, generator=None):
+        super().__init__()
+        self.embedding_size = embedding_size
+        self.num_int_fea = num_int_fea
+        self.num_cat_fea = num_cat_fea
+        if slot_cardinalities is None:
+            self.embedding_layer = Embedding(vocab_size, embedding_size, device=device, generator=generator)
+        else:
+            self.embedding_layer = SlabEmbedding(slot_cardinalities, embedding_size, device=device, generator=generator)
+        self.mlp = MLP(mlp_units, final_activation=None,
+                       in_features=num_cat_fea * embedding_size + num_int_fea, device=device,
+                       generator=generator)
+
+    def forward(self, inputs, training=None, mask=None):
+        cat_features, int_features = inputs["cat_features"], inputs["int_features"]
+        int_features = int_features.reshape(-1, self.num_int_fea).float()
+        cat_features = cat_features.reshape(-1, self.num_cat_fea)
+        cat_embedding = self.embedding_layer(cat_features)              # [B, S, D]
+        interaction = fm_interaction(cat_embedding)                     # ctr/model.py:21-23
+        deep_cat_input = cat_embedding.reshape(-1, self.num_cat_fea * self.embedding_size)
+        deep_input = torch.cat([deep_cat_input, int_features], dim=1)  # ctr/model.py:25-26
+        dense_output = self.mlp(deep_input).squeeze(1)
+        return torch.sigmoid(interaction + dense_output)                # ctr/model.py:28-30
+
+    call = forward
+
+
+class DLRM(nn.Module):
+    def __init__(self, bottom_mlp_units, top_mlp_units, embedding_size, vocab_size, num_cat_fea,
+                 num_int_fea, device=None, slot_cardinalities=None, generator=None):
+        super().__init__()
+        if bottom_mlp_units[-1] != embedding_size:
+            raise ValueError("the last bottom-MLP width must equal embedding_size (ctr/model.py:55)")
+        self.num_cat_fea = num_cat_fea
+        self.num_int_fea = num_int_fea
+        self.embedding_size = embedding_size
+        self.bottom_mlp = MLP(bottom_mlp_units, final_activation="relu", in_features=num_int_fea,
+                              device=device, generator=generator)
+        F = num_cat_fea + 1
+        self.top_mlp = MLP(top_mlp_units, final_activation="sigmoid",
+                           in_features=F * F + embedding_size, device=device, generator=generator)
+        if slot_cardinalities is None:
+            self.embedding_layer = Embedding(vocab_size, embedding_size, device=device, generator=generator)
+        else:
+            self.embedding_layer = SlabEmbedding(slot_cardinalities, embedding_size, device=device, generator=generator)
+        self.interaction = DotInteraction(False, True)
+
+    def interact(self, cat_features, bmlp_activation):
+        """[Z (F*F), bottom] — ctr/model.py:49-55 fused into one kernel."""
+        return dlrm_interaction(self.embedding_layer, cat_features, bmlp_activation)
+
+    def forward(self, x, training=None, mask=None):
+        cat_features, int_features = x["cat_features"], x["int_features"]
+        int_features = int_features.reshape(-1, self.num_int_fea).float()
+        cat_features = cat_features.reshape(-1, self.num_cat_fea)
+        bmlp_activation = self.bottom_mlp(int_features)
+        tmlp_input = self.interact(cat_features, bmlp_activation)
+        tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)
+        return self.top_mlp(tmlp_input).squeeze(1)
+
+    call = forward

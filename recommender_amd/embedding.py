@@ -1,0 +1,97 @@
+"""Embedding tables — the keras.layers.Embedding surface backed by librecsys_hip.
+
+`Embedding(input_dim, output_dim, mask_zero)` mirrors keras.layers.Embedding [3p] as used at
+ctr/model.py:10, dien/model.py:11-12, esmm/esmm.py:10-11: weight [input_dim, output_dim] fp32,
+initialised U(-0.05, 0.05) (Keras 'uniform'), `compute_mask(ids) = ids != 0` (mask_zero).
+
+`SlabEmbedding(cardinalities, dim)` packs one table per slot into a single HBM slab with row
+offsets ("one slab with slot offsets"); a lookup takes ids [B, n_slots].
+
+Gradients: the table is not an autograd leaf. A lookup's backward hands (ids, grad rows) to
+`accumulate_grad`; a sparse optimizer (recommender_amd.optim) drains them with `take_grad`.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from .functional import embedding_lookup
+
+
+class Embedding(nn.Module):
+    def __init__(self, input_dim: int, output_dim: int, mask_zero: bool = False, device=None,
+                 slot_offsets: torch.Tensor | None = None, init_range: float = 0.05,
+                 generator: torch.Generator | None = None, weight: torch.Tensor | None = None):
+        super().__init__()
+        device = torch.device(device) if device is not None else torch.device("cuda")
+        self.input_dim = int(input_dim)
+        self.output_dim = int(output_dim)
+        self.mask_zero = bool(mask_zero)
+        if weight is not None:
+            if tuple(weight.shape) != (self.input_dim, self.output_dim):
+                raise ValueError("weight shape mismatch")
+            w = weight.to(device=device, dtype=torch.float32).contiguous()
+        else:
+            w = torch.empty(self.input_dim, self.output_dim, device=device, dtype=torch.float32)
+            w.uniform_(-init_range, init_range, generator=generator)
+        self.register_buffer("weight", w)
+        self.register_buffer("slot_offsets",
+                             None if slot_offsets is None else slot_offsets.to(device, torch.int64))
+        self.register_buffer("err_flag", torch.zeros(1, dtype=torch.int32, device=device))
+        # zero-size leaf that keeps the lookup inside the autograd graph
+        self.grad_handle = nn.Parameter(torch.zeros(0, device=device), requires_grad=True)
+        self._pending: list[tuple[torch.Tensor, torch.Tensor]] = []
+
+    @property
+    def n_slots(self) -> int:
+        return 1 if self.slot_offsets is None else self.slot_offsets.numel() - 1
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        return embedding_lookup(self, ids)
+
+    def compute_mask(self, ids: torch.Tensor):
+        return ids != 0 if self.mask_zero else None
+
+    # ---- sparse gradient plumbing ----
+    def accumulate_grad(self, ids: torch.Tensor, grad_rows: torch.Tensor):
+        self._pending.append((ids.reshape(-1), grad_rows.reshape(-1, self.output_dim)))
+
+    def has_grad(self) -> bool:
+        return bool(self._pending)
+
+    def take_grad(self):
+        """(ids [N] flattened in position order, grad rows [N, dim]) of every lookup since the
+        last call, concatenated in call order; clears the pending list."""
+        p, self._pending = self._pending, []
+        if not p:
+            return None
+        if len(p) == 1:
+            return p[0]
+        # every lookup holds a multiple of n_slots ids, so position % n_slots stays the slot
+        ids = torch.cat([i.to(torch.int64) for i, _ in p])
+        return ids, torch.cat([g for _, g in p])
+
+    def zero_grad_pending(self):
+        self._pending = []
+
+    def oob_detected(self) -> bool:
+        """True if any lookup since the last reset saw an out-of-range id (synchronises)."""
+        return bool(self.err_flag.item() & L.RS_ERRBIT_OOB)
+
+    def reset_oob(self):
+        self.err_flag.zero_()
+
+    def extra_repr(self):
+        return f"{self.input_dim}, {self.output_dim}, mask_zero={self.mask_zero}, slots={self.n_slots}"
+
+
+class SlabEmbedding(Embedding):
+    """Per-slot tables of `cardinalities[s]` rows packed in one slab; ids [..., n_slots]."""
+
+    def __init__(self, cardinalities, dim: int, device=None, **kw):
+        card = torch.as_tensor(list(cardinalities), dtype=torch.int64)
+        offs = torch.zeros(card.numel() + 1, dtype=torch.int64)
+        offs[1:] = torch.cumsum(card, 0)
+        super().__init__(int(offs[-1]), dim, device=device, slot_offsets=offs, **kw)
+        self.cardinalities = card.tolist()

@@ -1,0 +1,149 @@
+"""torch.autograd wrappers around the C-ABI kernels (the only callers of recommender_amd._lib).
+
+Embedding gradients never become dense [V, D] tensors: the backward of a lookup hands its
+upstream rows (position order) and ids to the owning EmbeddingTable, and the sparse optimizer
+(recommender_amd.optim) sorts, segment-sums and applies them in one fused pass.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+
+def _ids_flat(ids: torch.Tensor) -> torch.Tensor:
+    ids = ids.contiguous()
+    L.require_device(ids, "ids")
+    L.id_dtype_code(ids)
+    return ids
+
+
+class _EmbeddingLookup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, handle, table_module, ids):
+        w = table_module.weight
+        L.require_device(w, "embedding table")
+        ids = _ids_flat(ids)
+        dim = w.shape[1]
+        out = torch.empty(*ids.shape, dim, device=w.device, dtype=torch.float32)
+        so = table_module.slot_offsets
+        n_slots = 1 if so is None else so.numel() - 1
+        L.call("rs_embedding_fwd", L.ptr(w), w.shape[0], dim, L.ptr(ids), L.id_dtype_code(ids),
+               ids.numel(), L.ptr(so), n_slots, L.ptr(out), L.ptr(table_module.err_flag),
+               L.stream_ptr(w.device))
+        ctx.table_module = table_module
+        ctx.ids = ids
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        ctx.table_module.accumulate_grad(ctx.ids, grad_out.reshape(-1, grad_out.shape[-1]))
+        return None, None, None
+
+
+def embedding_lookup(table_module, ids: torch.Tensor) -> torch.Tensor:
+    return _EmbeddingLookup.apply(table_module.grad_handle, table_module, ids)
+
+
+class _DotInteraction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, self_interaction, skip_gather):
+        L.require_device(x, "x")
+        x = x.contiguous().float()
+        B, F, D = x.shape
+        if skip_gather:
+            w = F * F
+        else:
+            w = F * (F + 1) // 2 if self_interaction else F * (F - 1) // 2
+        out = torch.empty(B, w, device=x.device, dtype=torch.float32)
+        L.call("rs_dot_interaction_fwd", L.ptr(x), B, F, D, int(self_interaction),
+               int(skip_gather), L.ptr(out), w, L.stream_ptr(x.device))
+        ctx.save_for_backward(x)
+        ctx.flags = (int(self_interaction), int(skip_gather), w)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (x,) = ctx.saved_tensors
+        si, sg, w = ctx.flags
+        B, F, D = x.shape
+        g = grad_out.contiguous()
+        gx = torch.empty_like(x)
+        L.call("rs_dot_interaction_bwd", L.ptr(x), L.ptr(g), B, F, D, si, sg, w, L.ptr(gx),
+               L.stream_ptr(x.device))
+        return gx, None, None
+
+
+def dot_interaction(x, self_interaction: bool, skip_gather: bool):
+    return _DotInteraction.apply(x, self_interaction, skip_gather)
+
+
+class _DLRMInteraction(torch.autograd.Function):
+    """Fused gather + DotInteraction(False, True) + concat (ctr/model.py:49-55)."""
+
+    @staticmethod
+    def forward(ctx, handle, dense, table_module, ids):
+        w = table_module.weight
+        L.require_device(w, "embedding table")
+        ids = _ids_flat(ids)
+        dense = dense.contiguous()
+        B, S = ids.shape
+        D = w.shape[1]
+        F = S + 1
+        if dense.shape != (B, D):
+            raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
+        out = torch.empty(B, F * F + D, device=w.device, dtype=torch.float32)
+        L.call("rs_dlrm_interaction_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
+               L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
+               L.ptr(out), F * F + D, L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+        ctx.table_module = table_module
+        ctx.ids = ids
+        ctx.save_for_backward(dense)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (dense,) = ctx.saved_tensors
+        tm = ctx.table_module
+        w = tm.weight
+        ids = ctx.ids
+        B, S = ids.shape
+        D = w.shape[1]
+        g = grad_out.contiguous()
+        grad_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
+        grad_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
+        L.call("rs_dlrm_interaction_bwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
+               L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, L.ptr(g),
+               g.shape[1], L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
+        tm.accumulate_grad(ids, grad_emb)
+        return None, grad_dense, None, None
+
+
+def dlrm_interaction(table_module, ids, dense):
+    return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids)
+
+
+class _FM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, emb):
+        L.require_device(emb, "emb")
+        emb = emb.contiguous().float()
+        B, F, D = emb.shape
+        out = torch.empty(B, device=emb.device, dtype=torch.float32)
+        L.call("rs_fm_fwd", L.ptr(emb), B, F, D, L.ptr(out), L.stream_ptr(emb.device))
+        ctx.save_for_backward(emb)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (emb,) = ctx.saved_tensors
+        B, F, D = emb.shape
+        g = grad_out.contiguous()
+        ge = torch.empty_like(emb)
+        L.call("rs_fm_bwd", L.ptr(emb), L.ptr(g), B, F, D, L.ptr(ge), L.stream_ptr(emb.device))
+        return ge
+
+
+def fm_interaction(emb):
+    """DeepFM second-order term 0.5*Σ_d((Σ_f e)^2 - Σ_f e^2) (ctr/model.py:21-23)."""
+    return _FM.apply(emb)

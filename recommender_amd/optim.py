@@ -1,0 +1,238 @@
+"""Optimizers: sparse appliers for embedding tables (fused HIP segmented-sum + update) and
+Keras-semantics dense optimizers for the MLP parameters.
+
+Embedding (a-2):
+  SparseSGD        var[u] -= lr * Σ g           (the DLRM SGD path, ctr/train.py:77-79)
+  SparseAdam(lazy) Adam on touched rows only     (roofline mode)
+  SparseAdam(keras) Keras OptimizerV2 Adam exactly: dense decay of m/v and dense var update of
+                   every row (ctr/train.py:80,84 `tf.keras.optimizers.Adam()` defaults)
+Dense:
+  KerasAdam        Keras Adam update rule on torch tensors (lr_t folding, eps outside sqrt)
+  DLRMScheduler    warmup-linear then cosine decay (ctr/util.py:7-37)
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .embedding import Embedding
+
+
+def keras_adam_coefficients(step: int, lr=1e-3, beta1=0.9, beta2=0.999, epsilon=1e-7):
+    """Keras Adam._prepare_local [3p TF 2.2] in float32; `step` = iterations + 1."""
+    f = np.float32
+    t = f(step)
+    b1p = np.power(f(beta1), t, dtype=np.float32)
+    b2p = np.power(f(beta2), t, dtype=np.float32)
+    lr_t = f(f(lr) * (np.sqrt(f(f(1) - b2p), dtype=np.float32) / f(f(1) - b1p)))
+    return L.AdamParams(float(lr_t), float(f(beta1)), float(f(beta2)), float(f(f(1) - f(beta1))),
+                        float(f(f(1) - f(beta2))), float(f(epsilon)))
+
+
+class _Workspace:
+    """Grow-only device scratch buffers keyed by name."""
+
+    def __init__(self):
+        self.bufs: dict[str, torch.Tensor] = {}
+
+    def get(self, name, nbytes, device):
+        b = self.bufs.get(name)
+        if b is None or b.numel() < nbytes or b.device != device:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self.bufs[name] = b
+        return b
+
+
+class SortedIds:
+    """Radix-sorted ids of one step (rs_sort_ids): sorted rows (uint32 bits in int32),
+    original positions, device count of distinct valid rows."""
+
+    def __init__(self, ids: torch.Tensor, n_rows: int, slot_offsets: torch.Tensor | None = None,
+                 err_flag: torch.Tensor | None = None, ws: _Workspace | None = None):
+        ws = ws or _Workspace()
+        ids = ids.contiguous()
+        L.require_device(ids, "ids")
+        n = ids.numel()
+        dev = ids.device
+        self.n = n
+        self.rows = torch.empty(n, dtype=torch.int32, device=dev)
+        self.pos = torch.empty(n, dtype=torch.int32, device=dev)
+        self.n_unique = torch.zeros(1, dtype=torch.int32, device=dev)
+        n_slots = 1 if slot_offsets is None else slot_offsets.numel() - 1
+        nbytes = L.lib().rs_sort_ids_workspace_size(n)
+        w = ws.get("sort", nbytes, dev)
+        L.call("rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets), n_slots,
+               int(n_rows), L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique),
+               L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
+
+    @classmethod
+    def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None):
+        return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws)
+
+
+def dedup_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
+               ws: _Workspace | None = None, sorted_ids: SortedIds | None = None):
+    """(uniq_rows int64 [U], uniq_grad [U, dim]) — the deduplicated IndexedSlices gradient.
+    Synchronises once to read U."""
+    ws = ws or _Workspace()
+    dev = table.weight.device
+    s = sorted_ids or SortedIds.for_table(table, ids, ws)
+    n, dim = s.n, table.output_dim
+    g = grad_rows.contiguous()
+    uniq_rows = torch.empty(n, dtype=torch.int32, device=dev)
+    uniq_grad = torch.empty(n, dim, dtype=torch.float32, device=dev)
+    nbytes = L.lib().rs_dedup_workspace_size(n, dim)
+    w = ws.get("dedup", nbytes, dev)
+    L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(g), dim,
+           table.input_dim, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(),
+           L.stream_ptr(dev))
+    u = int(s.n_unique.item())
+    return uniq_rows[:u].to(torch.int64) & 0xFFFFFFFF, uniq_grad[:u]
+
+
+class SparseOptimizer:
+    kind = L.RS_OPT_SGD
+
+    def __init__(self, tables, lr=0.01):
+        if isinstance(tables, Embedding):
+            tables = [tables]
+        self.tables = list(tables)
+        self.lr = lr
+        self.iterations = 0
+        self.ws = _Workspace()
+
+    def _params(self) -> L.AdamParams:
+        lr = self.lr(self.iterations) if callable(self.lr) else self.lr
+        return L.AdamParams(float(np.float32(lr)), 0.0, 0.0, 0.0, 0.0, 0.0)
+
+    def _slots(self, t: Embedding):
+        return None, None, None
+
+    def apply(self, table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor, params,
+              sorted_ids: SortedIds | None = None):
+        dev = table.weight.device
+        s = sorted_ids or SortedIds.for_table(table, ids, self.ws)
+        g = grad_rows.contiguous()
+        m, v, bitmap = self._slots(table)
+        nbytes = L.lib().rs_apply_workspace_size(s.n, table.output_dim)
+        w = self.ws.get("apply", nbytes, dev)
+        L.call("rs_embedding_apply", self.kind, L.ptr(table.weight), L.ptr(m), L.ptr(v),
+               table.input_dim, table.output_dim, L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g),
+               params, L.ptr(bitmap), L.ptr(w), w.numel(), L.stream_ptr(dev))
+        if self.kind == L.RS_OPT_KERAS_ADAM:
+            L.call("rs_keras_adam_dense_sweep", L.ptr(table.weight), L.ptr(m), L.ptr(v),
+                   table.input_dim, table.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
+
+    def step(self):
+        params = self._params()
+        for t in self.tables:
+            got = t.take_grad()
+            if got is None:
+                if self.kind == L.RS_OPT_KERAS_ADAM:
+                    # Keras still decays m/v and moves var densely when the slice is empty
+                    m, v, bitmap = self._slots(t)
+                    L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
+                           t.input_dim, t.output_dim, params, L.ptr(bitmap),
+                           L.stream_ptr(t.weight.device))
+                continue
+            ids, g = got
+            self.apply(t, ids, g, params)
+        self.iterations += 1
+
+    def zero_grad(self):
+        for t in self.tables:
+            t.zero_grad_pending()
+
+
+class SparseSGD(SparseOptimizer):
+    """var[u] -= lr * Σ_{p: id_p = u} g_p. lr may be a float or a schedule step → lr."""
+    kind = L.RS_OPT_SGD
+
+
+class SparseAdam(SparseOptimizer):
+    """mode='keras': exact Keras Adam (dense m/v decay + dense var update, 24·V·D bytes/step);
+    mode='lazy': the same update restricted to touched rows."""
+
+    def __init__(self, tables, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, mode="keras"):
+        super().__init__(tables, lr)
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+        if mode not in ("keras", "lazy"):
+            raise ValueError("mode must be 'keras' or 'lazy'")
+        self.kind = L.RS_OPT_KERAS_ADAM if mode == "keras" else L.RS_OPT_LAZY_ADAM
+        self.state = {}
+        for t in self.tables:
+            w = t.weight
+            m = torch.zeros_like(w)
+            v = torch.zeros_like(w)
+            bitmap = (torch.zeros((t.input_dim + 31) // 32, dtype=torch.int32, device=w.device)
+                      if self.kind == L.RS_OPT_KERAS_ADAM else None)
+            self.state[id(t)] = (m, v, bitmap)
+
+    def _slots(self, t):
+        return self.state[id(t)]
+
+    def _params(self):
+        lr = self.lr(self.iterations) if callable(self.lr) else self.lr
+        return keras_adam_coefficients(self.iterations + 1, lr, self.beta_1, self.beta_2,
+                                       self.epsilon)
+
+
+class KerasAdam(torch.optim.Optimizer):
+    """Keras OptimizerV2 Adam update for dense tensors [3p TF 2.2 _resource_apply_dense]:
+    m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g; var -= lr_t*m/(sqrt(v)+eps)."""
+
+    def __init__(self, params, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        super().__init__(params, dict(lr=lr, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon))
+        self.iterations = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        self.iterations += 1
+        for group in self.param_groups:
+            c = keras_adam_coefficients(self.iterations, group["lr"], group["beta_1"],
+                                        group["beta_2"], group["epsilon"])
+            ps = [p for p in group["params"] if p.grad is not None and p.numel() > 0]
+            if not ps:
+                continue
+            ms, vs, gs = [], [], []
+            for p in ps:
+                st = self.state[p]
+                if not st:
+                    st["m"] = torch.zeros_like(p)
+                    st["v"] = torch.zeros_like(p)
+                ms.append(st["m"])
+                vs.append(st["v"])
+                gs.append(p.grad)
+            torch._foreach_mul_(ms, c.beta1)
+            torch._foreach_add_(ms, torch._foreach_mul(gs, c.one_minus_beta1))
+            torch._foreach_mul_(vs, c.beta2)
+            torch._foreach_add_(vs, torch._foreach_mul(torch._foreach_mul(gs, gs), c.one_minus_beta2))
+            den = torch._foreach_add(torch._foreach_sqrt(vs), c.epsilon)
+            upd = torch._foreach_div(torch._foreach_mul(ms, c.lr), den)
+            torch._foreach_sub_(ps, upd)
+
+
+class DLRMScheduler:
+    """ctr/util.py:7-37: lr = initial*step/warmup for step <= warmup, else cosine decay to
+    alpha over decay_steps."""
+
+    def __init__(self, initial_learning_rate, warmup_steps, decay_steps, alpha):
+        self.initial_learning_rate = initial_learning_rate
+        self.warmup_steps = warmup_steps
+        self.decay_steps = decay_steps
+        self.alpha = alpha
+
+    def __call__(self, step):
+        f = np.float32
+        step = f(step)
+        warm = f(self.warmup_steps)
+        if step <= warm:
+            return float(f(step / warm) * f(self.initial_learning_rate))
+        g = min(step, f(warm + f(self.decay_steps)))
+        frac = f((g - warm) / f(self.decay_steps))
+        cos = f(0.5) * (f(1.0) + f(math.cos(f(math.pi) * frac)))
+        decayed = f((f(1) - f(self.alpha)) * cos + f(self.alpha))
+        return float(f(self.initial_learning_rate) * decayed)

@@ -1,0 +1,135 @@
+"""GPU parity: embedding gather, radix sort / dedup and the sparse optimizer applies vs the
+CPU oracle (bit-exact: gather is a copy, sort is integer work, the segmented sums follow the
+oracle's fixed order and -ffp-contract=off keeps the update roundings identical)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import embedding as O
+from recommender_amd import _lib as L
+from recommender_amd.embedding import Embedding, SlabEmbedding
+from recommender_amd.optim import SortedIds, SparseAdam, SparseSGD, dedup_grad, keras_adam_coefficients
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def zipf_ids(rng, n, card, a=1.05):
+    x = rng.zipf(a, size=n) - 1
+    return np.minimum(x, card - 1)
+
+
+@pytest.mark.parametrize("dim", [16, 18, 64, 128, 160, 7])
+@pytest.mark.parametrize("id_dtype", [np.int64, np.int32])
+def test_gather_shared_table(dim, id_dtype, rng):
+    V, B, S = 5000, 257, 26
+    w = rng.standard_normal((V, dim)).astype(np.float32)
+    ids = rng.integers(0, V, (B, S)).astype(id_dtype)
+    t = Embedding(V, dim, device=DEV, weight=torch.from_numpy(w))
+    out = t(torch.from_numpy(ids).to(DEV))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), O.embedding_lookup(w, ids))
+    assert not t.oob_detected()
+
+
+def test_gather_slab_and_oob(rng):
+    card = [7, 1, 300, 50]
+    dim = 64
+    t = SlabEmbedding(card, dim, device=DEV)
+    w = t.weight.cpu().numpy()
+    so = np.concatenate([[0], np.cumsum(card)])
+    ids = np.stack([rng.integers(0, c, 1000) for c in card], 1).astype(np.int64)
+    ids[3, 1] = 1      # out of range for a 1-row slot
+    ids[10, 2] = -5    # negative
+    out = t(torch.from_numpy(ids).to(DEV)).detach().cpu().numpy()
+    ref = O.embedding_lookup(w, ids, so, raise_oob=False)
+    np.testing.assert_array_equal(out, ref)
+    assert (out[3, 1] == 0).all() and (out[10, 2] == 0).all()
+    assert t.oob_detected()
+    with pytest.raises(IndexError):
+        O.embedding_lookup(w, ids, so, raise_oob=True)
+
+
+@pytest.mark.parametrize("n,V", [(1, 10), (1000, 7), (4096 * 3 + 17, 1000), (200_000, 40_000_000), (65536, 3)])
+def test_sort_ids(n, V, rng):
+    ids = zipf_ids(rng, n, V).astype(np.int64)
+    ids[::97] = V + 3  # OOB
+    s = SortedIds(torch.from_numpy(ids).to(DEV), V)
+    rows_ref, pos_ref, nu_ref = O.sort_ids(ids, V)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
+def test_sort_ids_empty():
+    s = SortedIds(torch.zeros(0, dtype=torch.int64, device=DEV), 10)
+    assert s.n == 0 and int(s.n_unique.item()) == 0
+
+
+@pytest.mark.parametrize("dim", [128, 64, 18, 16, 160, 3])
+@pytest.mark.parametrize("dist", ["zipf", "one_hot_row", "uniform"])
+def test_dedup_grad_order(dim, dist, rng):
+    V, n = 20_000, 33 * 32 + 5
+    if dist == "zipf":
+        ids = zipf_ids(rng, n, V)
+    elif dist == "one_hot_row":
+        ids = np.full(n, 17)
+        ids[::5] = 3
+    else:
+        ids = rng.integers(0, V, n)
+    ids = ids.astype(np.int64)
+    g = rng.standard_normal((n, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV)
+    ur, ug = dedup_grad(t, torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+    sr, sp, nu = O.sort_ids(ids, V)
+    rr, rg = O.segment_sum_tiled(sr, sp, g, V)
+    np.testing.assert_array_equal(ur.cpu().numpy(), rr.astype(np.int64))
+    np.testing.assert_array_equal(ug.cpu().numpy(), rg)
+
+
+@pytest.mark.parametrize("dim", [128, 18])
+def test_sgd_apply_bitexact(dim, rng):
+    V, B, S = 30_000, 512, 26
+    w0 = rng.standard_normal((V, dim)).astype(np.float32)
+    ids = zipf_ids(rng, B * S, V).reshape(B, S).astype(np.int64)
+    g = rng.standard_normal((B * S, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV, weight=torch.from_numpy(w0))
+    opt = SparseSGD(t, lr=0.05)
+    t.accumulate_grad(torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+    opt.step()
+    sr, sp, _ = O.sort_ids(ids, V)
+    ur, ug = O.segment_sum_tiled(sr, sp, g, V)
+    ref = O.apply_sgd(w0, ur, ug, np.float32(0.05))
+    np.testing.assert_array_equal(t.weight.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("mode", ["lazy", "keras"])
+def test_adam_apply_bitexact(mode, rng):
+    V, dim, n = 5000, 64, 4000
+    w0 = rng.standard_normal((V, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV, weight=torch.from_numpy(w0))
+    opt = SparseAdam(t, lr=1e-3, mode=mode)
+    w, m, v = w0.copy(), np.zeros_like(w0), np.zeros_like(w0)
+    for step in range(1, 4):
+        ids = zipf_ids(rng, n, V).astype(np.int64)
+        g = rng.standard_normal((n, dim)).astype(np.float32)
+        t.accumulate_grad(torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+        opt.step()
+        sr, sp, _ = O.sort_ids(ids, V)
+        ur, ug = O.segment_sum_tiled(sr, sp, g, V)
+        c = O.keras_adam_coefficients(step)
+        if mode == "lazy":
+            w, m, v = O.apply_lazy_adam(w, m, v, ur, ug, c)
+        else:
+            w, m, v = O.apply_keras_adam(w, m, v, ur, ug, c)
+    mg, vg, _ = opt.state[id(t)]
+    np.testing.assert_array_equal(mg.cpu().numpy(), m)
+    np.testing.assert_array_equal(vg.cpu().numpy(), v)
+    np.testing.assert_array_equal(t.weight.cpu().numpy(), w)
+
+
+def test_keras_adam_coefficients_match_oracle():
+    for step in (1, 2, 10, 1000):
+        c = keras_adam_coefficients(step)
+        r = O.keras_adam_coefficients(step)
+        assert np.float32(c.lr) == r["lr"]

@@ -1,0 +1,96 @@
+"""GPU parity: DotInteraction (all four self/skip_gather modes), the fused DLRM gather +
+interaction, and the FM term vs the float64 oracle, within the north-star 1e-5 relative
+tolerance (scaled by the Cauchy-Schwarz bound of each dot product)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import embedding as OE
+from oracle import interaction as O
+from recommender_amd.embedding import Embedding, SlabEmbedding
+from recommender_amd.functional import dlrm_interaction, dot_interaction, fm_interaction
+from tests.conftest import assert_close_rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-5
+
+
+def _pair_scale(x, self_i, skip):
+    n = np.sqrt((np.asarray(x, np.float64) ** 2).sum(-1))  # [B, F]
+    s = n[:, :, None] * n[:, None, :]
+    keep = O.kept_mask(x.shape[1], self_i)
+    return s.reshape(x.shape[0], -1) if skip else s[:, keep]
+
+
+@pytest.mark.parametrize("F,D", [(27, 128), (27, 64), (27, 16), (5, 32), (32, 128), (2, 16), (27, 18), (33, 16), (17, 100)])
+@pytest.mark.parametrize("self_i,skip", [(False, True), (False, False), (True, False), (True, True)])
+def test_dot_interaction(F, D, self_i, skip, rng):
+    B = 67
+    x = rng.standard_normal((B, F, D)).astype(np.float32)
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    out = dot_interaction(xt, self_i, skip)
+    ref = O.dot_interaction(x, self_i, skip)
+    assert out.shape == ref.shape
+    assert_close_rel(out.detach().cpu().numpy(), ref, RTOL, _pair_scale(x, self_i, skip), "fwd")
+    g = rng.standard_normal(ref.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(DEV))
+    gref = O.dot_interaction_bwd(x, g, self_i, skip)
+    gscale = np.abs(g).max() * np.sqrt((x.astype(np.float64) ** 2).sum(-1)).max() * 2
+    assert_close_rel(xt.grad.cpu().numpy(), gref, RTOL, gscale, "bwd")
+
+
+def test_dot_interaction_known_answer():
+    # X = [[1,2],[3,4],[5,6]]: Z = [[5,11,17],[11,25,39],[17,39,61]]
+    x = torch.tensor([[[1., 2.], [3., 4.], [5., 6.]]], device=DEV)
+    np.testing.assert_array_equal(dot_interaction(x, False, False).cpu().numpy(), [[11, 17, 39]])
+    np.testing.assert_array_equal(dot_interaction(x, True, False).cpu().numpy(), [[5, 11, 25, 17, 39, 61]])
+    np.testing.assert_array_equal(dot_interaction(x, False, True).cpu().numpy(),
+                                  [[0, 11, 17, 0, 0, 39, 0, 0, 0]])
+
+
+@pytest.mark.parametrize("D", [128, 64, 16, 24])
+@pytest.mark.parametrize("slab", [False, True])
+def test_dlrm_fused(D, slab, rng):
+    B, S, V = 300, 26, 10_000
+    if slab:
+        card = rng.integers(1, 800, S)
+        t = SlabEmbedding(card, D, device=DEV)
+        so = np.concatenate([[0], np.cumsum(card)])
+        ids = np.stack([rng.integers(0, c, B) for c in card], 1).astype(np.int64)
+    else:
+        t = Embedding(V, D, device=DEV)
+        so = None
+        ids = rng.integers(0, V, (B, S)).astype(np.int32)
+    w = t.weight.cpu().numpy()
+    dense = rng.standard_normal((B, D)).astype(np.float32)
+    dt = torch.from_numpy(dense).to(DEV).requires_grad_(True)
+    out = dlrm_interaction(t, torch.from_numpy(ids).to(DEV), dt)
+    ref = O.dlrm_interaction(w, ids, dense, so)
+    F = S + 1
+    emb = OE.embedding_lookup(w, ids, so)
+    x = np.concatenate([emb, dense[:, None]], 1)
+    scale = np.concatenate([_pair_scale(x, False, True), np.abs(dense)], 1)
+    assert_close_rel(out.detach().cpu().numpy(), ref, RTOL, scale, "fwd")
+    g = rng.standard_normal(ref.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(DEV))
+    ge_ref, gd_ref = O.dlrm_interaction_bwd(w, ids, dense, g, so)
+    got_ids, got_rows = t.take_grad()
+    np.testing.assert_array_equal(got_ids.cpu().numpy(), ids.reshape(-1))
+    gscale = np.abs(g).max() * np.sqrt((x.astype(np.float64) ** 2).sum(-1)).max() * 2
+    assert_close_rel(got_rows.cpu().numpy(), ge_ref, RTOL, gscale, "grad_emb")
+    assert_close_rel(dt.grad.cpu().numpy(), gd_ref, RTOL, gscale, "grad_dense")
+
+
+@pytest.mark.parametrize("F,D", [(26, 16), (3, 7), (26, 128)])
+def test_fm(F, D, rng):
+    B = 129
+    e = rng.standard_normal((B, F, D)).astype(np.float32)
+    et = torch.from_numpy(e).to(DEV).requires_grad_(True)
+    out = fm_interaction(et)
+    scale = (np.abs(e).sum(1) ** 2).sum(-1)
+    assert_close_rel(out.detach().cpu().numpy(), O.fm(e), RTOL, scale, "fm fwd")
+    g = rng.standard_normal(B).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(DEV))
+    gscale = np.abs(g)[:, None, None] * np.abs(e).sum(1, keepdims=True)
+    assert_close_rel(et.grad.cpu().numpy(), O.fm_bwd(e, g), RTOL, gscale, "fm bwd")
