@@ -1,0 +1,232 @@
+"""North-star benchmark: Criteo-shaped DLRM train step (fwd + bwd + optimizer) on MI355X.
+
+metric: examples/sec fwd+bwd, Criteo-DLRM 26×40M×128 batch 65536 (BASELINE.json), per GPU
+batch 65 536 (weak scaling over ranks). One step = DLRM forward (bottom MLP, fused gather +
+MFMA DotInteraction, top MLP), mean BCE, backward (fused re-gather interaction bwd, MLPs),
+dense SGD and the fused sparse SGD apply on the embedding slab (the reference's DLRM SGD path,
+ctr/train.py:77-79). Inputs are pre-generated on device (no host I/O in the timed region).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from recommender_amd import _lib as L  # noqa: E402
+from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
+from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_sort_ids", "rs_embedding_apply"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch")
+    ap.add_argument("--rows", type=int, default=40_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--slots", type=int, default=26)
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lazy_adam", "keras_adam"])
+    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=2)
+    ap.add_argument("--cpu-baseline-batch", type=int, default=8192)
+    return ap.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def make_pool(args, cards, rank, dev):
+    rng = np.random.default_rng([args.seed, rank])
+    pool = []
+    for _ in range(args.pool):
+        cat, dn, lb = criteo_batch(rng, args.batch, cards)
+        pool.append((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
+                     torch.from_numpy(lb).to(dev)))
+    return pool
+
+
+def measured_unique(pool, model):
+    from recommender_amd.optim import SortedIds
+
+    t = model.embedding_layer
+    us = [int(SortedIds.for_table(t, b[0]).n_unique.item()) for b in pool]
+    return float(np.mean(us))
+
+
+def kernel_bytes(name, B, S, D, id_bytes, U):
+    """Algorithmic HBM bytes of one launch."""
+    F = S + 1
+    N = B * S
+    if name == "rs_dlrm_interaction_fwd":
+        return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * (F * F + D))
+    if name == "rs_dlrm_interaction_bwd":
+        return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * (F * F + D) + S * 4 * D + 4 * D)
+    if name == "rs_embedding_apply":
+        return N * 8 + N * 4 * D + U * 2 * 4 * D
+    if name == "rs_sort_ids":
+        return N * id_bytes + N * 8
+    return 0
+
+
+def cpu_baseline(args, cards):
+    """The oracle's NumPy DLRM SGD step (oracle/ctr.py) on the host cores, bounded sample."""
+    from threadpoolctl import threadpool_info
+
+    from oracle.ctr import DLRMState, dlrm_sgd_step
+
+    D, S = args.dim, args.slots
+    rng = np.random.default_rng(args.seed)
+    V = sum(cards)
+    table = np.empty((V, D), np.float32)
+    table[:] = np.float32(0.01)
+    so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+
+    def mk(units, fin):
+        out = []
+        for u in units:
+            lim = np.sqrt(6.0 / (fin + u))
+            out.append((rng.uniform(-lim, lim, (fin, u)).astype(np.float32), np.zeros(u, np.float32)))
+            fin = u
+        return out
+
+    F = S + 1
+    st = DLRMState(table, so, mk([512, 256, D], 13), mk([512, 256, 1], F * F + D))
+    B = args.cpu_baseline_batch
+    batches = [criteo_batch(rng, B, cards) for _ in range(args.cpu_baseline_steps + 1)]
+    dlrm_sgd_step(st, *batches[0], 0.01)  # warm-up
+    t0 = time.perf_counter()
+    for b in batches[1:]:
+        dlrm_sgd_step(st, *b, 0.01)
+    dt = time.perf_counter() - t0
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    return {"value": B * args.cpu_baseline_steps / dt, "unit": "examples/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/ctr.py dlrm_sgd_step (NumPy fp32), {args.cpu_baseline_steps} steps of "
+                      f"batch {B} on the same 26x{V}x{D} slab / Zipf ids, after 1 warm-up step; "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    L.load()
+    if L.lib().rs_device_count() < 1:
+        raise SystemExit("no GPU visible to librecsys_hip")
+    D, S = args.dim, args.slots
+    cards = criteo_cardinalities(args.rows, S)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed)
+    model = build_model("DLRM", D, args.rows, S, 13, dev, slot_cardinalities=cards,
+                        bottom=[512, 256, D], top=[512, 256, 1], generator=g)
+    step = TrainStep(model, args.optimizer, lr=0.01 if args.optimizer == "sgd" else 1e-3)
+    pool = make_pool(args, cards, rank, dev)
+    U = measured_unique(pool, model)
+
+    for i in range(args.warmup):
+        step(pool[i % len(pool)])
+    timer = L.KernelTimer(WATCH)
+    L.set_timer(timer)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    timer.enabled = True
+    t0 = time.perf_counter()
+    ev0.record()
+    for i in range(args.steps):
+        loss = step(pool[i % len(pool)])
+    ev1.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    timer.enabled = False
+    L.set_timer(None)
+    wall = t1 - t0
+    if world > 1:
+        tt = torch.tensor([wall], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+    ms_step = wall / args.steps * 1e3
+    value = args.batch * world * args.steps / wall
+
+    tot = timer.totals_ms()
+    kern = {}
+    for name, (ms, cnt) in tot.items():
+        if cnt:
+            avg = ms / cnt
+            by = kernel_bytes(name, args.batch, S, D, 8, U)
+            kern[name] = {"avg_us": round(avg * 1e3, 2), "calls": cnt,
+                          "algorithmic_bytes": int(by),
+                          "achieved_GBs": round(by / (avg * 1e-3) / 1e9, 1)}
+    dom = max(kern, key=lambda k: kern[k]["avg_us"]) if kern else None
+    roof = None
+    if dom:
+        a = kern[dom]["achieved_GBs"]
+        roof = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None}
+    # whole embedding path per SURVEY §8(d): fwd S(id+8D) + bwd S(id+4D) + (U/B)*8D per example
+    emb_names = [n for n in WATCH if n in kern]
+    emb_us = sum(kern[n]["avg_us"] for n in emb_names)
+    per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / args.batch) * 8 * D
+    emb_path = {"kernels": emb_names, "us_per_step": round(emb_us, 1),
+                "bytes_per_example": round(per_ex, 1),
+                "achieved_GBs": round(per_ex * args.batch / (emb_us * 1e-6) / 1e9, 1) if emb_us else None,
+                "frac_of_peak": round(per_ex * args.batch / (emb_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if emb_us else None,
+                "unique_rows_per_step": U}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline_steps > 0:
+        cpu = cpu_baseline(args, cards)
+
+    if rank == 0:
+        out = {
+            "metric": "examples/sec fwd+bwd, Criteo-DLRM 26×40M×128 batch 65536, 1/2/4/8 GPU",
+            "value": round(value, 1), "unit": "examples/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (Criteo-Kaggle-skewed 26-slot slab, bounded Zipf(1.05) ids, seed 4)",
+            "config": {"workload": f"dlrm_criteo_{S}x{args.rows}x{D}", "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch, "rows": args.rows, "dim": D, "slots": S,
+                       "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
+                       "optimizer": args.optimizer, "parallelism": f"dp{world}" if world > 1 else "single"},
+            "roofline": roof, "embedding_path": emb_path, "kernels": kern,
+            "cpu_baseline": cpu, "loss": float(loss.item()),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,9 +96,40 @@ def check(status: int, fn: str):
         raise RecsysError(f"{fn} failed with status {status}: {msg}")
 
 
+class KernelTimer:
+    """Records HIP events around the C-ABI calls named in `names` (on the current stream, the
+    stream every kernel is launched on) while enabled; bench.py uses it for per-kernel time."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events: dict[str, list] = {n: [] for n in self.names}
+        self.enabled = False
+
+    def totals_ms(self):
+        torch.cuda.synchronize()
+        return {n: (sum(s.elapsed_time(e) for s, e in ev), len(ev)) for n, ev in self.events.items()}
+
+
+_timer: KernelTimer | None = None
+
+
+def set_timer(t: KernelTimer | None):
+    global _timer
+    _timer = t
+
+
 def call(fn: str, *args):
     """Invoke a kernel entry point; raises on a non-zero status."""
     f = getattr(lib(), fn)
+    t = _timer
+    if t is not None and t.enabled and fn in t.names:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        st = f(*args)
+        e.record()
+        t.events[fn].append((s, e))
+        check(st, fn)
+        return
     check(f(*args), fn)
 
 

@@ -1,0 +1,118 @@
+"""ctr/train.py counterpart (reference ctr/train.py:11-97): DLRM / DeepFM training on
+synthetic Criteo-shaped data through the MI355X engine.
+
+Same flags and defaults as the reference (--gpus, --gpu_memory_limit, --model_type,
+--train_batch_size, --test_batch_size, --seed; 26 cat / 13 int features, vocab 1 000 000,
+dim 16, 3 epochs, DLRM units [512,256,64,16] / [512,256,1], Adam) plus:
+  --optimizer  keras_adam (reference default, ctr/train.py:80,84) | lazy_adam | sgd
+               (the commented DLRM SGD + DLRMScheduler path, ctr/train.py:77-79)
+  --steps_per_epoch, --rows/--slab (per-slot tables), --embedding_size.
+The reference's `model.fit` differentiates the per-example BCE vector (reduction NONE,
+ctr/train.py:85), i.e. the gradient of the SUM over the batch [3p Keras 2.2]; --loss_reduction
+selects sum (reference) or mean.
+"""
+from __future__ import annotations
+
+import argparse
+import time
+
+import numpy as np
+import torch
+
+from ..nn import binary_crossentropy
+from ..optim import DLRMScheduler, KerasAdam, SparseAdam, SparseSGD
+from ..synthetic import criteo_batch, criteo_cardinalities
+from .model import DLRM, DeepFM
+
+
+class TrainStep:
+    """One optimizer step of a ctr model: forward, BCE, backward, dense + sparse apply."""
+
+    def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None):
+        self.model = model
+        dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
+        tables = [model.embedding_layer]
+        self.loss_reduction = loss_reduction
+        if optimizer == "sgd":
+            lr = sched or (lr if lr is not None else 0.01)
+            self.opt_dense = torch.optim.SGD(dense, lr=lr if not callable(lr) else lr(0))
+            self.opt_sparse = SparseSGD(tables, lr=lr)
+            self._sched = lr if callable(lr) else None
+        elif optimizer in ("keras_adam", "lazy_adam"):
+            lr = lr if lr is not None else 1e-3
+            self.opt_dense = KerasAdam(dense, lr=lr)
+            self.opt_sparse = SparseAdam(tables, lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy")
+            self._sched = None
+        else:
+            raise ValueError(f"unknown optimizer {optimizer}")
+
+    def __call__(self, batch):
+        cat, dense_x, label = batch
+        if self._sched is not None:
+            for g in self.opt_dense.param_groups:
+                g["lr"] = self._sched(self.opt_sparse.iterations)
+        self.opt_dense.zero_grad(set_to_none=True)
+        p = self.model({"cat_features": cat, "int_features": dense_x})
+        per_ex = binary_crossentropy(label, p)
+        loss = per_ex.sum() if self.loss_reduction == "sum" else per_ex.mean()
+        loss.backward()
+        self.opt_dense.step()
+        self.opt_sparse.step()
+        return loss
+
+
+def build_model(model_type, embedding_size, vocab_size, num_cat_fea, num_int_fea, device,
+                slot_cardinalities=None, bottom=None, top=None, mlp_units=None, generator=None):
+    if model_type == "DLRM":
+        bottom = bottom or [512, 256, 64, embedding_size]
+        top = top or [512, 256, 1]
+        return DLRM(bottom, top, embedding_size, vocab_size, num_cat_fea, num_int_fea, device=device,
+                    slot_cardinalities=slot_cardinalities, generator=generator)
+    if model_type == "DeepFM":
+        return DeepFM(embedding_size, vocab_size, num_int_fea, num_cat_fea, mlp_units or [512, 256, 1],
+                      device=device, slot_cardinalities=slot_cardinalities, generator=generator)
+    raise ValueError(model_type)
+
+
+def train(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=str, default="0")
+    ap.add_argument("--gpu_memory_limit", type=int, default=20480)  # parsed, unused (as reference)
+    ap.add_argument("--model_type", type=str, default="DLRM")
+    ap.add_argument("--train_batch_size", type=int, default=1024)
+    ap.add_argument("--test_batch_size", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--optimizer", default="keras_adam", choices=["keras_adam", "lazy_adam", "sgd"])
+    ap.add_argument("--loss_reduction", default="sum", choices=["sum", "mean"])
+    ap.add_argument("--embedding_size", type=int, default=16)
+    ap.add_argument("--vocab_size", type=int, default=1_000_000)
+    ap.add_argument("--slab", action="store_true", help="per-slot tables (Criteo skew) in one slab")
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--steps_per_epoch", type=int, default=50)
+    args = ap.parse_args(argv)
+    torch.manual_seed(args.seed)
+    dev = torch.device("cuda")
+    num_int_fea, num_cat_fea = 13, 26
+    cards = criteo_cardinalities(args.vocab_size, num_cat_fea) if args.slab else [args.vocab_size] * num_cat_fea
+    model = build_model(args.model_type, args.embedding_size, args.vocab_size, num_cat_fea,
+                        num_int_fea, dev, slot_cardinalities=cards if args.slab else None)
+    sched = DLRMScheduler(0.01, 100, 10000, 0.0001) if args.optimizer == "sgd" else None
+    step = TrainStep(model, args.optimizer, loss_reduction=args.loss_reduction, sched=sched)
+    rng = np.random.default_rng(args.seed)
+    for epoch in range(1, args.epochs + 1):
+        t0 = time.time()
+        tot = 0.0
+        for _ in range(args.steps_per_epoch):
+            cat, dn, lb = criteo_batch(rng, args.train_batch_size, cards)
+            if not args.slab:
+                cat = cat % args.vocab_size
+            batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev), torch.from_numpy(lb).to(dev))
+            tot += float(step(batch))
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} "
+              f"{args.steps_per_epoch * args.train_batch_size / dt:.0f} ex/s")
+
+
+if __name__ == "__main__":
+    train()

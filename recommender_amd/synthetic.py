@@ -1,0 +1,63 @@
+"""Synthetic Criteo-shaped inputs (no datasets are reachable offline).
+
+- 26 categorical slots with Criteo-Kaggle-like cardinality skew, scaled so the slab holds
+  exactly `total_rows` rows (40M for the north star);
+- ids: per-slot bounded Zipf(alpha=1.05) ranks (inverse-CDF of the bounded power law), mapped
+  to rows by a fixed multiplicative permutation so hot ids are spread over the slot;
+- 13 dense features log1p(x), x ~ Geometric(p=0.01) (the log(x+1) of ctr/tfrecord_io.py:53);
+- labels ~ Bernoulli(0.256).
+Seeded with numpy PCG64(seed); seed 4 = the reference default (ctr/train.py:18).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# Criteo Kaggle (display advertising challenge) per-column cardinalities
+CRITEO_KAGGLE_CARDINALITIES = [
+    1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194, 27,
+    14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572,
+]
+
+
+def criteo_cardinalities(total_rows: int = 40_000_000, n_slots: int = 26) -> list[int]:
+    base = np.array(CRITEO_KAGGLE_CARDINALITIES[:n_slots], dtype=np.float64)
+    small = base < 100_000
+    budget = total_rows - base[small].sum()
+    if budget <= 0:
+        out = np.maximum(1, np.floor(base * total_rows / base.sum())).astype(np.int64)
+    else:
+        big = base[~small]
+        out = base.copy()
+        out[~small] = np.floor(big * budget / big.sum())
+        out = out.astype(np.int64)
+    out[np.argmax(out)] += total_rows - out.sum()
+    assert out.sum() == total_rows and (out >= 1).all()
+    return out.tolist()
+
+
+def bounded_zipf(rng: np.random.Generator, n: int, card: int, alpha: float = 1.05) -> np.ndarray:
+    """Ranks in [0, card) with P(k) ~ (k+1)^-alpha (continuous inverse-CDF approximation)."""
+    if card <= 1:
+        return np.zeros(n, np.int64)
+    u = rng.random(n)
+    a1 = 1.0 - alpha
+    x = ((card ** a1 - 1.0) * u + 1.0) ** (1.0 / a1)
+    return np.minimum(np.floor(x).astype(np.int64) - 1, card - 1).clip(0)
+
+
+def _spread(ranks: np.ndarray, card: int) -> np.ndarray:
+    """Bijective rank → id map inside a slot (multiplier coprime with card)."""
+    mult = 2654435761 % card if card > 2 else 1
+    while np.gcd(mult, card) != 1:
+        mult += 1
+    return (ranks * mult) % card
+
+
+def criteo_batch(rng: np.random.Generator, batch: int, cards, alpha: float = 1.05,
+                 num_int_fea: int = 13, id_dtype=np.int64):
+    cat = np.empty((batch, len(cards)), dtype=id_dtype)
+    for s, c in enumerate(cards):
+        cat[:, s] = _spread(bounded_zipf(rng, batch, c, alpha), c)
+    dense = np.log1p(rng.geometric(0.01, size=(batch, num_int_fea)).astype(np.float32))
+    label = (rng.random(batch) < 0.256).astype(np.float32)
+    return cat, dense.astype(np.float32), label
