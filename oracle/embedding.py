@@ -14,6 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 DEDUP_TILE = 32  # RS_DEDUP_TILE in include/recsys_hip.h
+FIX_CHUNK = 32   # kFixChunk in recommender_amd/csrc/embedding.hip (level-1 fix-up fold)
 
 
 def global_rows(ids: np.ndarray, n_rows: int, slot_offsets: np.ndarray | None = None):
@@ -63,8 +64,9 @@ def segment_sum_tiled(sorted_rows, sorted_pos, grad, n_rows, tile=DEDUP_TILE):
     """Deduplicated gradient with the kernel's fixed summation order.
 
     The sorted entries are cut into tiles of `tile`; inside a tile the rows of one segment are
-    added sequentially starting from +0.0; the pieces of a segment that spans tiles are then
-    added in tile order, starting from the first piece. Returns (uniq_rows, uniq_grad)."""
+    added sequentially starting from +0.0 (a "piece"); the pieces of a segment that spans tiles
+    are folded in tile order in chunks of FIX_CHUNK pieces (each chunk sequentially from its
+    first piece), and the chunk sums are folded in order. Returns (uniq_rows, uniq_grad)."""
     sorted_rows = np.asarray(sorted_rows).astype(np.int64)
     sorted_pos = np.asarray(sorted_pos).astype(np.int64)
     grad = np.asarray(grad, dtype=np.float32)
@@ -88,16 +90,33 @@ def segment_sum_tiled(sorted_rows, sorted_pos, grad, n_rows, tile=DEDUP_TILE):
     for j in range(int(piece_len.max())):
         sel = piece_len > j
         acc[sel] += rows_g[piece_start[sel] + j]
-    # segments over pieces
+    # segments over pieces: a segment's pieces are one per tile it touches, in tile order.
+    # Fold pieces in chunks of FIX_CHUNK (each chunk sequentially from its first piece), then
+    # fold the chunk sums sequentially (rs fix-up levels 1 and 2).
     piece_key = keys[piece_start]
     seg_head = np.ones(n_pieces, bool)
     seg_head[1:] = piece_key[1:] != piece_key[:-1]
     seg_start = np.flatnonzero(seg_head)
     seg_len = np.diff(np.append(seg_start, n_pieces))
-    out = acc[seg_start].copy()
-    for j in range(1, int(seg_len.max())):
-        sel = seg_len > j
-        out[sel] += acc[seg_start[sel] + j]
+    seg_of_piece = np.repeat(np.arange(seg_start.size), seg_len)
+    idx_in_seg = np.arange(n_pieces) - seg_start[seg_of_piece]
+    chunk_head = (idx_in_seg % FIX_CHUNK) == 0
+    chunk_start = np.flatnonzero(chunk_head)
+    chunk_len = np.diff(np.append(chunk_start, n_pieces))
+    # a chunk never crosses a segment: cut lengths at segment ends
+    seg_end = (seg_start + seg_len)[seg_of_piece[chunk_start]]
+    chunk_len = np.minimum(chunk_len, seg_end - chunk_start)
+    csum = acc[chunk_start].copy()
+    for j in range(1, int(chunk_len.max())):
+        sel = chunk_len > j
+        csum[sel] += acc[chunk_start[sel] + j]
+    seg_of_chunk = seg_of_piece[chunk_start]
+    cseg_start = np.flatnonzero(np.r_[True, seg_of_chunk[1:] != seg_of_chunk[:-1]])
+    cseg_len = np.diff(np.append(cseg_start, chunk_start.size))
+    out = csum[cseg_start].copy()
+    for j in range(1, int(cseg_len.max())):
+        sel = cseg_len > j
+        out[sel] += csum[cseg_start[sel] + j]
     return piece_key[seg_start].astype(np.uint32), out
 
 

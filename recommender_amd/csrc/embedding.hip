@@ -133,6 +133,7 @@ struct ApplyArgs {
   rs_adam_params p;
   uint32_t* bitmap;       // keras: touched rows
   float* partial;         // [n_tiles][2][dim]
+  float* chunk;           // [n_tiles][2][dim] level-1 chunk sums of spanning segments
   // OPT_EMIT (dedup output)
   float* uniq_grad;
   uint32_t* uniq_rows;
@@ -280,12 +281,128 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restric
   emit(run_row, run_starts, ends, run_start);
 }
 
-// fix-up: one lane group per tile; works only on tiles that hold the head part of a
-// segment continuing into the next tile.
+// ---- fix-up of segments that span tiles ----------------------------------------------
+// A spanning segment with head tile h and last tile e has the ordered partial list
+//   P[0] = partial[h][1], P[i] = partial[h+i][0] (i = 1..e-h).
+// Level 1: chunk c = P[32c .. 32c+31] is folded sequentially by one lane group (leader tile
+// h+32c) into chunk[h+32c][role] (role 1 = head chunk, 0 = continuation chunk).
+// Level 2: one lane group per head tile folds the chunks in order and finalises the row.
+// For spans of <= 32 tiles this is the plain sequential fold of the partials.
+constexpr int kFixChunk = 32;
+
+__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* keys, int64_t n, uint32_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// head tile / last tile of the segment of sorted entry k
+__device__ __forceinline__ void seg_tiles(const uint32_t* keys, int64_t n, int64_t k, int64_t& h,
+                                          int64_t& e) {
+  const uint32_t key = keys[k];
+  h = lower_bound_u32(keys, n, key) / RS_DEDUP_TILE;
+  e = (lower_bound_u32(keys, n, key + 1) - 1) / RS_DEDUP_TILE;
+}
+
+template <int VEC, int CPL>
+__device__ __forceinline__ void fold_partials(const float* base_first, const float* part, int64_t t0,
+                                              int64_t cnt, int dim, int gl, int lpr,
+                                              float (&acc)[CPL][VEC]) {
+  // acc = base_first; acc += part[(t0 + i) * 2 + 0] for i in [0, cnt)
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    int col = (gl + c * lpr) * VEC;
+    if (col < dim) {
+      RowIO<VEC>::load(base_first + col, acc[c]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
+    }
+  }
+  constexpr int U = 8;
+  for (int64_t i = 0; i < cnt; i += U) {
+    float r[U][CPL][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* p = part + ((t0 + i + u) * 2) * (int64_t)dim;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (i + u < cnt && col < dim) {
+          RowIO<VEC>::load(p + col, r[u][c]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u < cnt)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[c][e] += r[u][c][e];
+  }
+}
+
+// level 1: one lane group per tile, in up to two roles
+template <int VEC, int CPL>
+__global__ __launch_bounds__(256) void seg_chunk_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                        uint32_t n_rows, ApplyArgs a, int lpr_log2,
+                                                        int64_t n_tiles, float* __restrict__ chunk) {
+  constexpr int T = RS_DEDUP_TILE;
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
+  if (t >= n_tiles) return;
+  const int dim = a.dim;
+  const int64_t k0 = t * T;
+  const int64_t klast = (k0 + T < n ? k0 + T : n) - 1;
+  float acc[CPL][VEC];
+  // role 1: head of a segment that continues into tile t+1
+  if (klast + 1 < n && keys[klast] < n_rows && keys[klast + 1] == keys[klast] &&
+      !(k0 > 0 && keys[k0] == keys[klast] && keys[k0 - 1] == keys[klast])) {
+    int64_t h, e;
+    seg_tiles(keys, n, klast, h, e);
+    // chunk 0 = P[0..31] = partial[t][1] + partial[t+1..min(t+31, e)][0]
+    int64_t cnt = e - t < kFixChunk - 1 ? e - t : kFixChunk - 1;
+    fold_partials<VEC, CPL>(a.partial + (t * 2 + 1) * (int64_t)dim, a.partial, t + 1, cnt, dim, gl,
+                            lpr, acc);
+    float* dst = chunk + (t * 2 + 1) * (int64_t)dim;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      int col = (gl + c * lpr) * VEC;
+      if (col < dim) RowIO<VEC>::store(dst + col, acc[c]);
+    }
+  }
+  // role 0: continuation tile that leads a chunk (P index t-h is a multiple of 32)
+  if (k0 > 0 && keys[k0] < n_rows && keys[k0 - 1] == keys[k0]) {
+    int64_t h, e;
+    seg_tiles(keys, n, k0, h, e);
+    if ((t - h) % kFixChunk == 0) {
+      int64_t cnt = e - t < kFixChunk - 1 ? e - t : kFixChunk - 1;
+      fold_partials<VEC, CPL>(a.partial + (t * 2) * (int64_t)dim, a.partial, t + 1, cnt, dim, gl,
+                              lpr, acc);
+      float* dst = chunk + (t * 2) * (int64_t)dim;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (col < dim) RowIO<VEC>::store(dst + col, acc[c]);
+      }
+    }
+  }
+}
+
+// level 2: one lane group per head tile of a spanning segment
 template <int OPT, int VEC, int CPL>
 __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                         uint32_t n_rows, ApplyArgs a, int lpr_log2,
-                                                        int64_t n_tiles) {
+                                                        int64_t n_tiles,
+                                                        const float* __restrict__ chunk) {
   constexpr int T = RS_DEDUP_TILE;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
@@ -295,35 +412,47 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
   if (knext >= n) return;
   const uint32_t row = keys[klast];
   if (row >= n_rows || keys[knext] != row) return;  // last run does not continue
-  // the segment must start inside this tile
-  if (keys[k0] == row && k0 > 0 && keys[k0 - 1] == row) return;
+  if (keys[k0] == row && k0 > 0 && keys[k0 - 1] == row) return;  // segment started earlier
+  int64_t h, e;
+  seg_tiles(keys, n, klast, h, e);
   const int dim = a.dim;
   float acc[CPL][VEC];
-  const float* p1 = a.partial + (t * 2 + 1) * (int64_t)dim;
+  // acc = chunk[t][1]; acc += chunk[t + 32c][0] for c = 1 .. (e - t) / 32
+  const int64_t n_more = (e - t) / kFixChunk;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     int col = (gl + c * lpr) * VEC;
     if (col < dim) {
-      RowIO<VEC>::load(p1 + col, acc[c]);
+      RowIO<VEC>::load(chunk + (t * 2 + 1) * (int64_t)dim + col, acc[c]);
     } else {
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
+      for (int e2 = 0; e2 < VEC; ++e2) acc[c][e2] = 0.f;
     }
   }
-  for (int64_t tt = t + 1; tt < n_tiles; ++tt) {
-    const float* p0 = a.partial + (tt * 2) * (int64_t)dim;
+  constexpr int U = 8;
+  for (int64_t i = 1; i <= n_more; i += U) {
+    float r[U][CPL][VEC];
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      int col = (gl + c * lpr) * VEC;
-      if (col < dim) {
-        float v[VEC];
-        RowIO<VEC>::load(p0 + col, v);
+    for (int u = 0; u < U; ++u) {
+      const float* p = chunk + ((t + (i + u) * kFixChunk) * 2) * (int64_t)dim;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[c][e] += v[e];
+      for (int c = 0; c < CPL; ++c) {
+        int col = (gl + c * lpr) * VEC;
+        if (i + u <= n_more && col < dim) {
+          RowIO<VEC>::load(p + col, r[u][c]);
+        } else {
+#pragma unroll
+          for (int e2 = 0; e2 < VEC; ++e2) r[u][c][e2] = 0.f;
+        }
       }
     }
-    int64_t kn = (tt + 1) * T;
-    if (kn >= n || keys[kn] != row) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u <= n_more)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int e2 = 0; e2 < VEC; ++e2) acc[c][e2] += r[u][c][e2];
   }
   finalize_row<OPT, VEC, CPL>(a, row, gl, lpr, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, klast) : 0);
 }
@@ -406,8 +535,10 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     seg_tile_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, pos, n, (uint32_t)n_rows, grad, \
                                                             a, geom.lpr_log2, n_tiles);         \
+    seg_chunk_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,            \
+                                                       geom.lpr_log2, n_tiles, a.chunk);        \
     seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,      \
-                                                             geom.lpr_log2, n_tiles);           \
+                                                             geom.lpr_log2, n_tiles, a.chunk);  \
   }))
   switch (opt) {
     case OPT_SGD: RS_SEG_LAUNCH(OPT_SGD); break;
@@ -449,7 +580,11 @@ extern "C" int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t 
 }
 
 static size_t partial_bytes(int64_t n_ids, int32_t dim) {
-  return (size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float);
+  // tile partials + level-1 chunk sums, each [n_tiles][2][dim]
+  return 2 * align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256);
+}
+static float* chunk_of(float* partial, int64_t n_ids, int32_t dim) {
+  return partial + align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256) / 4;
 }
 
 extern "C" size_t rs_dedup_workspace_size(int64_t n_ids, int32_t dim) {
@@ -481,6 +616,7 @@ extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const in
   ApplyArgs a{};
   a.dim = dim;
   a.partial = partial;
+  a.chunk = chunk_of(partial, n_ids, dim);
   a.uniq_grad = uniq_grad;
   a.uniq_rows = uniq_rows;
   a.seg_excl = seg;
@@ -519,6 +655,7 @@ extern "C" int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float
   a.p = *params;
   a.bitmap = touched_bitmap;
   a.partial = static_cast<float*>(workspace);
+  a.chunk = chunk_of(a.partial, n_ids, dim);
   const void* ptrs[4] = {table, grad_out, m ? m : table, v ? v : table};
   RowGeom geom = row_geom(dim, ptrs, 4);
   return launch_segments(opt, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom,

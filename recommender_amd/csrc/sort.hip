@@ -54,7 +54,8 @@ __device__ __forceinline__ uint64_t lanemask_lt64() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-// histogram: hist[digit * n_tiles + tile]
+// histogram: hist[digit * n_tiles + tile]. Equal digits inside a wave are aggregated by a
+// ballot match so skewed (Zipf) keys do not serialise on one LDS counter.
 template <int BITS>
 __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     const uint32_t* __restrict__ keys, int64_t n, int shift, int32_t* __restrict__ hist,
@@ -63,14 +64,17 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
   __shared__ int32_t cnt[BINS];
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) cnt[d] = 0;
   __syncthreads();
+  const int lane = threadIdx.x & 63;
   int64_t base = (int64_t)blockIdx.x * kSortTile;
 #pragma unroll 4
   for (int k = 0; k < kSortKeysPerLane; ++k) {
     int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
-    if (i < n) {
-      uint32_t d = (keys[i] >> shift) & (BINS - 1);
-      atomicAdd(&cnt[d], 1);
-    }
+    bool valid = i < n;
+    uint32_t d = valid ? (keys[i] >> shift) & (BINS - 1) : 0;
+    uint64_t m = match_digit<BITS>(d, valid);
+    // lowest lane of each match group adds the group size
+    if (valid && (m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))) == 0)
+      atomicAdd(&cnt[d], __popcll(m));
   }
   __syncthreads();
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) hist[(int64_t)d * n_tiles + blockIdx.x] = cnt[d];
@@ -166,9 +170,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   }
 }
 
-// count distinct valid rows in a sorted key array
-__global__ void count_unique_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t n_rows,
-                                    int32_t* __restrict__ n_unique) {
+// count distinct valid rows in a sorted key array (one atomic per block)
+__global__ __launch_bounds__(256) void count_unique_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                           uint32_t n_rows, int32_t* __restrict__ n_unique) {
+  __shared__ int32_t red[4];
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int32_t c = 0;
@@ -176,9 +181,13 @@ __global__ void count_unique_kernel(const uint32_t* __restrict__ keys, int64_t n
     uint32_t k = keys[i];
     c += (k < n_rows && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
   }
-  // wave reduce
   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(n_unique, c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = red[0] + red[1] + red[2] + red[3];
+    if (t) atomicAdd(n_unique, t);
+  }
 }
 
 static int key_bits_for(int64_t n_rows) {
@@ -203,23 +212,30 @@ static SortPlan plan_sort(int64_t n_ids, int64_t n_rows) {
   return p;
 }
 
-// workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles]
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* total, void* ws,
+                           size_t ws_bytes, hipStream_t st);
+size_t exclusive_scan_ws_size(int64_t n);
+
+// workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles], scan scratch
 static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int32_t** vals_alt,
-                             int32_t** hist) {
+                             int32_t** hist, void** scan_ws) {
   int n_tiles = (int)ceil_div(n_ids, kSortTile);
   *keys_alt = c.take<uint32_t>(n_ids);
   *vals_alt = c.take<int32_t>(n_ids);
   *hist = c.take<int32_t>((size_t)kMaxBins * n_tiles + 1);
+  *scan_ws = c.take<char>(exclusive_scan_ws_size((int64_t)kMaxBins * n_tiles + 1));
   return c.off;
 }
 
 template <int BITS>
 static int32_t launch_pass(const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
-                           int64_t n, int shift, int32_t* hist, int n_tiles, hipStream_t st) {
+                           int64_t n, int shift, int32_t* hist, void* scan_ws, int n_tiles,
+                           hipStream_t st) {
   radix_hist_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, n, shift, hist, n_tiles);
   RS_CHECK_LAUNCH();
-  scan_single_block_kernel<<<1, 1024, 0, st>>>(hist, (int64_t)(1 << BITS) * n_tiles, nullptr);
-  RS_CHECK_LAUNCH();
+  const int64_t hn = (int64_t)(1 << BITS) * n_tiles;
+  int32_t s = exclusive_scan_i32(hist, hist, hn, nullptr, scan_ws, exclusive_scan_ws_size(hn), st);
+  if (s) return s;
   radix_scatter_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, vin, n, shift, hist, n_tiles,
                                                                kout, vout);
   RS_CHECK_LAUNCH();
@@ -227,17 +243,17 @@ static int32_t launch_pass(const uint32_t* kin, const int32_t* vin, uint32_t* ko
 }
 
 static int32_t dispatch_pass(int bits, const uint32_t* kin, const int32_t* vin, uint32_t* kout,
-                             int32_t* vout, int64_t n, int shift, int32_t* hist, int n_tiles,
-                             hipStream_t st) {
+                             int32_t* vout, int64_t n, int shift, int32_t* hist, void* scan_ws,
+                             int n_tiles, hipStream_t st) {
   switch (bits) {
-    case 1: return launch_pass<1>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 2: return launch_pass<2>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 3: return launch_pass<3>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 4: return launch_pass<4>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 5: return launch_pass<5>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 6: return launch_pass<6>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 7: return launch_pass<7>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
-    case 8: return launch_pass<8>(kin, vin, kout, vout, n, shift, hist, n_tiles, st);
+    case 1: return launch_pass<1>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 2: return launch_pass<2>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 3: return launch_pass<3>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 4: return launch_pass<4>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 5: return launch_pass<5>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 6: return launch_pass<6>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 7: return launch_pass<7>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 8: return launch_pass<8>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
   }
   set_error("radix pass bits %d unsupported", bits);
   return RS_E_UNSUPPORTED;
@@ -253,7 +269,8 @@ int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out
   uint32_t* kalt;
   int32_t* valt;
   int32_t* hist;
-  sort_ws_layout(n, c, &kalt, &valt, &hist);
+  void* scan_ws;
+  sort_ws_layout(n, c, &kalt, &valt, &hist, &scan_ws);
   if (!c.ok()) {
     set_error("sort workspace too small: need %zu have %zu", c.off, ws_bytes);
     return RS_E_WORKSPACE;
@@ -265,7 +282,7 @@ int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out
     bool last = pass == p.passes - 1;
     uint32_t* kb = last ? keys_out : (ka == keys_in ? kalt : keys_in);
     int32_t* vb = last ? vals_out : (va == vals_in ? valt : vals_in);
-    int32_t s = dispatch_pass(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, p.n_tiles, st);
+    int32_t s = dispatch_pass(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, scan_ws, p.n_tiles, st);
     if (s) return s;
     ka = kb;
     va = vb;
@@ -278,7 +295,8 @@ size_t radix_sort_ws_size(int64_t n) {
   uint32_t* a;
   int32_t* b;
   int32_t* h;
-  return sort_ws_layout(n, c, &a, &b, &h) + 256;
+  void* w;
+  return sort_ws_layout(n, c, &a, &b, &h, &w) + 256;
 }
 
 // ---- device-wide exclusive scan of int32 (3-phase) -----------------------------------
@@ -401,7 +419,7 @@ extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
                                static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, st);
   if (s) return s;
   if (n_unique) {
-    count_unique_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, n_unique);
+    count_unique_kernel<<<std::min(blocks, 512), 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, n_unique);
     RS_CHECK_LAUNCH();
   }
   return RS_OK;

@@ -30,6 +30,48 @@ def get_activation(act):
     return _ACTS[act]
 
 
+def _splitk_chunks(batch: int, fan_in: int, fan_out: int) -> int:
+    """Batch split for the K = batch weight-gradient GEMM: hipBLASLt's single-pass fp32 kernels
+    for [in, B]·[B, out] with B = 65 536 run at 7-64 TF/s; a batched GEMM over 16-64 batch
+    chunks followed by a sum runs at 90-120 TF/s (tools/probe_gemm.py, MI355X)."""
+    if batch < 8192 or fan_in * fan_out > 4_000_000:
+        return 1
+    for c in (64, 32, 16, 8):
+        if batch % c == 0:
+            return c
+    return 1
+
+
+class _DenseFn(torch.autograd.Function):
+    """y = x @ kernel + bias with a split-K weight gradient (deterministic: fixed chunking,
+    torch's fixed-order sum over chunks)."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, bias):
+        y = torch.addmm(bias, x, kernel) if bias is not None else x @ kernel
+        ctx.save_for_backward(x, kernel)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, kernel = ctx.saved_tensors
+        dx = dk = db = None
+        if ctx.needs_input_grad[0]:
+            dx = dy @ kernel.t()
+        if ctx.needs_input_grad[1]:
+            B, fi = x.shape
+            fo = dy.shape[1]
+            c = _splitk_chunks(B, fi, fo)
+            if c > 1:
+                dk = torch.bmm(x.view(c, B // c, fi).transpose(1, 2), dy.view(c, B // c, fo)).sum(0)
+            else:
+                dk = x.t() @ dy
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+        return dx, dk, db
+
+
 class Dense(nn.Module):
     def __init__(self, units: int, activation=None, use_bias: bool = True, in_features=None,
                  device=None, generator: torch.Generator | None = None):
@@ -55,11 +97,10 @@ class Dense(nn.Module):
     def forward(self, x):
         if self.kernel is None:
             self.build(x.shape[-1], x.device)
-        if self.bias is not None:
-            if x.dim() == 2:
-                y = torch.addmm(self.bias, x, self.kernel)
-            else:
-                y = torch.matmul(x, self.kernel) + self.bias
+        if x.dim() == 2 and x.is_cuda:
+            y = _DenseFn.apply(x, self.kernel, self.bias)
+        elif self.bias is not None:
+            y = torch.matmul(x, self.kernel) + self.bias
         else:
             y = torch.matmul(x, self.kernel)
         return self.activation(y) if self.activation is not None else y
