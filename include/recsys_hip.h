@@ -137,18 +137,22 @@ int32_t rs_dot_interaction_bwd(const float* x, const float* grad_out, int64_t ba
 
 /* DLRM fused gather + interaction + concat (ctr/model.py:45-55 with
  * DotInteraction(False, True), ctr/model.py:43):
- *   out[b] = [ Z(b) (F*F, F = n_slots+1, strict upper kept) , dense[b] (D) ],
- *   X(b) = [ table[row(b,0)], ..., table[row(b,S-1)], dense[b] ].
+ *   X(b) = [ table[row(b,0)], ..., table[row(b,S-1)], dense[b] ]  (F = n_slots + 1 rows),
+ *   compact = 0: out[b] = [ Z(b) (F*F, strict upper kept, zeros elsewhere), dense[b] ]
+ *                (the reference's skip_gather layout, ctr/model.py:55),
+ *   compact = 1: out[b] = [ Z(b) strict upper in row-major order (F(F-1)/2), dense[b] ]
+ *                (the same values without the structural zeros; the caller drops the
+ *                matching zero-input rows of the top-MLP kernel).
  * bwd re-gathers X from the table and writes grad_emb[b*S+s] and grad_dense[b]. */
 int32_t rs_dlrm_interaction_fwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
                                 int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
-                                const float* dense, int64_t batch, float* out, int64_t out_stride,
-                                int32_t* err_flag, void* stream);
+                                const float* dense, int64_t batch, int32_t compact, float* out,
+                                int64_t out_stride, int32_t* err_flag, void* stream);
 int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
                                 int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
-                                const float* dense, int64_t batch, const float* grad_out,
-                                int64_t grad_stride, float* grad_emb, float* grad_dense,
-                                void* stream);
+                                const float* dense, int64_t batch, int32_t compact,
+                                const float* grad_out, int64_t grad_stride, float* grad_emb,
+                                float* grad_dense, void* stream);
 
 /* a-5 DeepFM second-order term — ctr/model.py:21-23:
  *   out[b] = 0.5 * Σ_d ((Σ_f e[b,f,d])^2 - Σ_f e[b,f,d]^2). */

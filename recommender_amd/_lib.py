@@ -47,10 +47,10 @@ _SIGS = {
     "rs_keras_adam_dense_sweep": (_i32, [_p, _p, _p, _i64, _i32, C.POINTER(AdamParams), _p, _p]),
     "rs_dot_interaction_fwd": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _p, _i64, _p]),
     "rs_dot_interaction_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _i32, _i64, _p, _p]),
-    "rs_dlrm_interaction_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _i64,
-                                       _p, _p]),
-    "rs_dlrm_interaction_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _i64,
-                                       _p, _p, _p]),
+    "rs_dlrm_interaction_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _i32, _p,
+                                       _i64, _p, _p]),
+    "rs_dlrm_interaction_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _i32, _p,
+                                       _i64, _p, _p, _p]),
     "rs_fm_fwd": (_i32, [_p, _i64, _i32, _i32, _p, _p]),
     "rs_fm_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
 }

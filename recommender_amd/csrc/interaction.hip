@@ -72,6 +72,29 @@ struct DenseSrc {
   }
 };
 
+// invert compact_index for the non-self (i < j) layout: row i starts at i*F - i(i+1)/2
+__device__ __forceinline__ void compact_pair(int o, int F, int self_i, int& i, int& j) {
+  if (self_i) {  // o = i(i+1)/2 + j, j <= i
+    int ii = (int)((sqrtf(8.f * o + 1.f) - 1.f) * 0.5f);
+    while (ii * (ii + 1) / 2 > o) --ii;
+    while ((ii + 1) * (ii + 2) / 2 <= o) ++ii;
+    i = ii;
+    j = o - ii * (ii + 1) / 2;
+  } else {
+    const float b = 2.f * F - 1.f;
+    int ii = (int)((b - sqrtf(b * b - 8.f * o)) * 0.5f);
+    if (ii < 0) ii = 0;
+    while (ii > 0 && ii * F - ii * (ii + 1) / 2 > o) --ii;
+    while ((ii + 1) * F - (ii + 1) * (ii + 2) / 2 <= o) ++ii;
+    i = ii;
+    j = o - (ii * F - ii * (ii + 1) / 2) + ii + 1;
+  }
+}
+
+__device__ __forceinline__ const float* shfl_ptr(const float* p, int src) {
+  return reinterpret_cast<const float*>(__shfl(reinterpret_cast<long long>(p), src));
+}
+
 // ---------------------------------------------------------------------------------------
 // forward, MFMA: one wave per sample, 4 waves per block
 // ---------------------------------------------------------------------------------------
@@ -85,8 +108,11 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   if (b >= batch) return;
   const int r = lane & 15, g = lane >> 4;
   bool oob = false;
-  const float* p0 = src.row(b, r, D, oob);
-  const float* p1 = src.row(b, 16 + r, D, oob);
+  // lane k < F resolves row k once; the MFMA lanes fetch the pointers by shuffle
+  const float* mine = lane < F ? src.row(b, lane, D, oob) : nullptr;
+  const float* p0 = shfl_ptr(mine, r);
+  const float* p1 = shfl_ptr(mine, 16 + r);
+  if (r >= F) p0 = nullptr;
   if (16 + r >= F) p1 = nullptr;
   float4 a0[NT], a1[NT];
 #pragma unroll
@@ -120,22 +146,23 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
   __builtin_amdgcn_wave_barrier();
   float* orow = out + b * out_stride;
+  const int nz = out_width(F, md.self_interaction, md.skip_gather);
   if (md.skip_gather) {
-    const int FF = F * F;
-    for (int o = lane; o < FF; o += 64) {
+    for (int o = lane; o < nz; o += 64) {
       int i = o / F, j = o - i * F;
       orow[o] = keep_pair(i, j, md.self_interaction) ? z[i][j] : 0.f;
     }
   } else {
-    for (int o = lane; o < F * F; o += 64) {
-      int i = o / F, j = o - i * F;
-      if (keep_pair(i, j, md.self_interaction)) orow[compact_index(i, j, F, md.self_interaction)] = z[i][j];
+    for (int o = lane; o < nz; o += 64) {
+      int i, j;
+      compact_pair(o, F, md.self_interaction, i, j);
+      orow[o] = z[i][j];
     }
   }
   if constexpr (DLRM_OUT) {
     // concat the bottom-MLP output behind Z (ctr/model.py:54)
     const float* dn = src.dense + b * D;
-    float* od = orow + out_width(F, md.self_interaction, md.skip_gather);
+    float* od = orow + nz;
     for (int d = lane; d < D; d += 64) od[d] = dn[d];
     if (__any(oob) && lane == 0) flag_oob(src.err_flag);
   }
@@ -144,6 +171,8 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
 // ---------------------------------------------------------------------------------------
 // backward, MFMA: dX = S · X, one wave per sample
 // ---------------------------------------------------------------------------------------
+constexpr int kMaxGradRow = 32 * 32 + 256;
+
 template <int D, class Src, bool DLRM_OUT>
 __global__ __launch_bounds__(256) void inter_bwd_mfma(Src src, int64_t batch, int F, InterMode md,
                                                       const float* __restrict__ gout, int64_t gstride,
@@ -153,56 +182,69 @@ __global__ __launch_bounds__(256) void inter_bwd_mfma(Src src, int64_t batch, in
 {
   constexpr int NTILE = D / 32;
   constexpr int KS = 16;  // up to 32 k-rows in steps of 2
+  __shared__ float gsm[4][kMaxGradRow];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   if (b >= batch) return;
   const int r = lane & 31, h = lane >> 5;
   const int ks = (F + 1) >> 1;
-  const float* grow = gout + b * gstride;
+  const int nz = out_width(F, md.self_interaction, md.skip_gather);
   bool oob = false;
 
+  // (1) row pointers: lane k < F resolves row k
+  const float* mine = lane < F ? src.row(b, lane, D, oob) : nullptr;
+  // (2) stage the incoming gradient row (coalesced)
+  float* gs = gsm[wave];
+  const float* grow = gout + b * gstride;
+  const int gw = nz + (DLRM_OUT ? D : 0);
+  for (int o = lane; o < gw; o += 64) gs[o] = grow[o];
+  // (3) every X row this lane feeds to the MFMA: rows k = 2s + h, NTILE floats at NTILE*r
+  float xv[KS][NTILE];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    const float* xr = shfl_ptr(mine, k < 64 ? k : 0);
+    if (k >= F) xr = nullptr;
+    if (xr) {
+      if constexpr (NTILE == 4) {
+        float4 t = *reinterpret_cast<const float4*>(xr + NTILE * r);
+        xv[s][0] = t.x; xv[s][1] = t.y; xv[s][2] = t.z; xv[s][3] = t.w;
+      } else if constexpr (NTILE == 2) {
+        float2 t = *reinterpret_cast<const float2*>(xr + NTILE * r);
+        xv[s][0] = t.x; xv[s][1] = t.y;
+      } else {
+#pragma unroll
+        for (int c = 0; c < NTILE; ++c) xv[s][c] = xr[NTILE * r + c];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NTILE; ++c) xv[s][c] = 0.f;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  // (4) S[r][k] = M[r][k] + M[k][r] from the staged gradient
+  auto m_at = [&](int i, int k) -> float {
+    if (!keep_pair(i, k, md.self_interaction)) return 0.f;
+    return md.skip_gather ? gs[i * F + k] : gs[compact_index(i, k, F, md.self_interaction)];
+  };
+  float sa[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    sa[s] = (r < F && k < F) ? m_at(r, k) + m_at(k, r) : 0.f;
+  }
   floatx16 acc[NTILE];
 #pragma unroll
   for (int c = 0; c < NTILE; ++c)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[c][e] = 0.f;
-
-  // S[r][k] for k = 2s + h
-  auto s_val = [&](int i, int k) -> float {
-    if (i >= F || k >= F) return 0.f;
-    float v = 0.f;
-    if (keep_pair(i, k, md.self_interaction))
-      v += md.skip_gather ? grow[i * F + k] : grow[compact_index(i, k, F, md.self_interaction)];
-    if (keep_pair(k, i, md.self_interaction))
-      v += md.skip_gather ? grow[k * F + i] : grow[compact_index(k, i, F, md.self_interaction)];
-    return v;
-  };
-
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (s < ks) {
-      const int k = 2 * s + h;
-      const float* xr = k < F ? src.row(b, k, D, oob) : nullptr;
-      float xv[NTILE];
-      if (xr) {
-        if constexpr (NTILE == 4) {
-          float4 t = *reinterpret_cast<const float4*>(xr + NTILE * r);
-          xv[0] = t.x; xv[1] = t.y; xv[2] = t.z; xv[3] = t.w;
-        } else if constexpr (NTILE == 2) {
-          float2 t = *reinterpret_cast<const float2*>(xr + NTILE * r);
-          xv[0] = t.x; xv[1] = t.y;
-        } else {
-#pragma unroll
-          for (int c = 0; c < NTILE; ++c) xv[c] = xr[NTILE * r + c];
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < NTILE; ++c) xv[c] = 0.f;
-      }
-      const float av = s_val(r, k);
 #pragma unroll
       for (int c = 0; c < NTILE; ++c)
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xv[c], acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[s], xv[s][c], acc[c], 0, 0, 0);
     }
   }
   // D layout: acc[c][reg] = dX[i = (reg&3) + 8*(reg>>2) + 4*h][d = NTILE*r + c]
@@ -219,9 +261,8 @@ __global__ __launch_bounds__(256) void inter_bwd_mfma(Src src, int64_t batch, in
         dst = gemb + (b * src.n_slots + i) * (int64_t)D;
       } else {
         // bottom-MLP row: interaction grad + the concat pass-through (ctr/model.py:54)
-        const float* gd = grow + out_width(F, md.self_interaction, md.skip_gather);
 #pragma unroll
-        for (int c = 0; c < NTILE; ++c) v[c] += gd[NTILE * r + c];
+        for (int c = 0; c < NTILE; ++c) v[c] += gs[nz + NTILE * r + c];
         dst = gdense + b * D;
       }
     } else {
@@ -445,30 +486,33 @@ extern "C" int32_t rs_dot_interaction_bwd(const float* x, const float* grad_out,
 extern "C" int32_t rs_dlrm_interaction_fwd(const float* table, int64_t n_rows, int32_t D,
                                            const void* ids, int32_t id_dtype, int32_t n_slots,
                                            const int64_t* slot_offsets, const float* dense,
-                                           int64_t batch, float* out, int64_t out_stride,
-                                           int32_t* err_flag, void* stream) {
+                                           int64_t batch, int32_t compact, float* out,
+                                           int64_t out_stride, int32_t* err_flag, void* stream) {
   const int F = n_slots + 1;
+  const InterMode md{0, compact ? 0 : 1};
   RS_CHECK_ARG(n_slots >= 1 && D >= 1 && batch >= 0, "bad sizes");
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
-  RS_CHECK_ARG(out_stride >= F * F + D, "out_stride too small");
+  RS_CHECK_ARG(out_stride >= out_width(F, 0, md.skip_gather) + D, "out_stride too small");
   RS_CHECK_ARG(batch == 0 || (table && ids && dense && out), "null pointer");
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
-  return launch_fwd<GatherSrc, true>(src, batch, F, D, {0, 1}, out, out_stride,
+  return launch_fwd<GatherSrc, true>(src, batch, F, D, md, out, out_stride,
                                      al16(table) && al16(dense), as_stream(stream));
 }
 
 extern "C" int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D,
                                            const void* ids, int32_t id_dtype, int32_t n_slots,
                                            const int64_t* slot_offsets, const float* dense,
-                                           int64_t batch, const float* grad_out, int64_t grad_stride,
-                                           float* grad_emb, float* grad_dense, void* stream) {
+                                           int64_t batch, int32_t compact, const float* grad_out,
+                                           int64_t grad_stride, float* grad_emb, float* grad_dense,
+                                           void* stream) {
   const int F = n_slots + 1;
+  const InterMode md{0, compact ? 0 : 1};
   RS_CHECK_ARG(n_slots >= 1 && D >= 1 && batch >= 0, "bad sizes");
-  RS_CHECK_ARG(grad_stride >= F * F + D, "grad_stride too small");
+  RS_CHECK_ARG(grad_stride >= out_width(F, 0, md.skip_gather) + D, "grad_stride too small");
   RS_CHECK_ARG(batch == 0 || (table && ids && dense && grad_out && grad_emb && grad_dense),
                "null pointer");
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, nullptr};
-  return launch_bwd<GatherSrc, true>(src, batch, F, D, {0, 1}, grad_out, grad_stride, nullptr,
+  return launch_bwd<GatherSrc, true>(src, batch, F, D, md, grad_out, grad_stride, nullptr,
                                      grad_emb, grad_dense,
                                      al16(table) && al16(dense) && al16(grad_emb) && al16(grad_dense),
                                      as_stream(stream));

@@ -46,8 +46,14 @@ class DeepFM(nn.Module):
 
 
 class DLRM(nn.Module):
+    """compact=True (default) feeds the top MLP only the F(F-1)/2 + D non-structural-zero
+    inputs: the interaction writes the strict upper triangle without its zeros and the first
+    top-MLP layer multiplies by the matching rows of its [F*F + D, units] kernel. The zero
+    inputs contribute exactly 0 to every sum, so logits and gradients are the reference's;
+    the kernel rows of the zero inputs receive an exactly-zero gradient as in the reference."""
+
     def __init__(self, bottom_mlp_units, top_mlp_units, embedding_size, vocab_size, num_cat_fea,
-                 num_int_fea, device=None, slot_cardinalities=None, generator=None):
+                 num_int_fea, device=None, slot_cardinalities=None, generator=None, compact=True):
         super().__init__()
         if bottom_mlp_units[-1] != embedding_size:
             raise ValueError("the last bottom-MLP width must equal embedding_size (ctr/model.py:55)")
@@ -64,18 +70,29 @@ class DLRM(nn.Module):
         else:
             self.embedding_layer = SlabEmbedding(slot_cardinalities, embedding_size, device=device, generator=generator)
         self.interaction = DotInteraction(False, True)
+        self.compact = compact
+        iu = torch.triu_indices(F, F, 1)
+        rows = torch.cat([iu[0] * F + iu[1], F * F + torch.arange(embedding_size)])
+        self.register_buffer("compact_rows", rows.to(device=self.embedding_layer.weight.device))
 
-    def interact(self, cat_features, bmlp_activation):
-        """[Z (F*F), bottom] — ctr/model.py:49-55 fused into one kernel."""
-        return dlrm_interaction(self.embedding_layer, cat_features, bmlp_activation)
+    def interact(self, cat_features, bmlp_activation, compact=False):
+        """[Z, bottom] — ctr/model.py:49-55 fused into one kernel."""
+        return dlrm_interaction(self.embedding_layer, cat_features, bmlp_activation, compact)
 
     def forward(self, x, training=None, mask=None):
         cat_features, int_features = x["cat_features"], x["int_features"]
         int_features = int_features.reshape(-1, self.num_int_fea).float()
         cat_features = cat_features.reshape(-1, self.num_cat_fea)
         bmlp_activation = self.bottom_mlp(int_features)
-        tmlp_input = self.interact(cat_features, bmlp_activation)
-        tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)
-        return self.top_mlp(tmlp_input).squeeze(1)
+        if not self.compact:
+            tmlp_input = self.interact(cat_features, bmlp_activation)
+            tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)
+            return self.top_mlp(tmlp_input).squeeze(1)
+        tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
+        first = self.top_mlp.mlp[0]
+        h = first(tmlp_input, kernel=first.kernel.index_select(0, self.compact_rows))
+        for layer in self.top_mlp.mlp[1:]:
+            h = layer(h)
+        return h.squeeze(1)
 
     call = forward

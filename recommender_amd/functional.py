@@ -82,7 +82,7 @@ class _DLRMInteraction(torch.autograd.Function):
     """Fused gather + DotInteraction(False, True) + concat (ctr/model.py:49-55)."""
 
     @staticmethod
-    def forward(ctx, handle, dense, table_module, ids):
+    def forward(ctx, handle, dense, table_module, ids, compact):
         w = table_module.weight
         L.require_device(w, "embedding table")
         ids = _ids_flat(ids)
@@ -92,12 +92,14 @@ class _DLRMInteraction(torch.autograd.Function):
         F = S + 1
         if dense.shape != (B, D):
             raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
-        out = torch.empty(B, F * F + D, device=w.device, dtype=torch.float32)
+        width = (F * (F - 1) // 2 if compact else F * F) + D
+        out = torch.empty(B, width, device=w.device, dtype=torch.float32)
         L.call("rs_dlrm_interaction_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
                L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
-               L.ptr(out), F * F + D, L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+               int(compact), L.ptr(out), width, L.ptr(table_module.err_flag), L.stream_ptr(w.device))
         ctx.table_module = table_module
         ctx.ids = ids
+        ctx.compact = int(compact)
         ctx.save_for_backward(dense)
         return out
 
@@ -113,14 +115,16 @@ class _DLRMInteraction(torch.autograd.Function):
         grad_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
         grad_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
         L.call("rs_dlrm_interaction_bwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
-               L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, L.ptr(g),
-               g.shape[1], L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
+               L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, ctx.compact,
+               L.ptr(g), g.shape[1], L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
         tm.accumulate_grad(ids, grad_emb)
-        return None, grad_dense, None, None
+        return None, grad_dense, None, None, None
 
 
-def dlrm_interaction(table_module, ids, dense):
-    return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids)
+def dlrm_interaction(table_module, ids, dense, compact: bool = False):
+    """[Z, dense] with Z the strict-upper X·Xᵀ of X = [emb(ids), dense]: F*F wide with zeros
+    (reference layout) or, compact=True, the F(F-1)/2 kept values only."""
+    return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids, compact)
 
 
 class _FM(torch.autograd.Function):

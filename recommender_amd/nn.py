@@ -94,15 +94,16 @@ class Dense(nn.Module):
         self.kernel = nn.Parameter(k)
         self.bias = nn.Parameter(torch.zeros(self.units, device=device)) if self.use_bias else None
 
-    def forward(self, x):
+    def forward(self, x, kernel=None):
         if self.kernel is None:
             self.build(x.shape[-1], x.device)
+        k = self.kernel if kernel is None else kernel
         if x.dim() == 2 and x.is_cuda:
-            y = _DenseFn.apply(x, self.kernel, self.bias)
+            y = _DenseFn.apply(x, k, self.bias)
         elif self.bias is not None:
-            y = torch.matmul(x, self.kernel) + self.bias
+            y = torch.matmul(x, k) + self.bias
         else:
-            y = torch.matmul(x, self.kernel)
+            y = torch.matmul(x, k)
         return self.activation(y) if self.activation is not None else y
 
 

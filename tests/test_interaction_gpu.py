@@ -51,7 +51,8 @@ def test_dot_interaction_known_answer():
 
 @pytest.mark.parametrize("D", [128, 64, 16, 24])
 @pytest.mark.parametrize("slab", [False, True])
-def test_dlrm_fused(D, slab, rng):
+@pytest.mark.parametrize("compact", [False, True])
+def test_dlrm_fused(D, slab, compact, rng):
     B, S, V = 300, 26, 10_000
     if slab:
         card = rng.integers(1, 800, S)
@@ -65,15 +66,24 @@ def test_dlrm_fused(D, slab, rng):
     w = t.weight.cpu().numpy()
     dense = rng.standard_normal((B, D)).astype(np.float32)
     dt = torch.from_numpy(dense).to(DEV).requires_grad_(True)
-    out = dlrm_interaction(t, torch.from_numpy(ids).to(DEV), dt)
+    out = dlrm_interaction(t, torch.from_numpy(ids).to(DEV), dt, compact)
     ref = O.dlrm_interaction(w, ids, dense, so)
     F = S + 1
+    keep_cols = np.r_[np.flatnonzero(np.triu(np.ones((F, F), bool), 1).reshape(-1)), F * F + np.arange(D)]
+    if compact:
+        ref = ref[:, keep_cols]
     emb = OE.embedding_lookup(w, ids, so)
     x = np.concatenate([emb, dense[:, None]], 1)
     scale = np.concatenate([_pair_scale(x, False, True), np.abs(dense)], 1)
+    if compact:
+        scale = scale[:, keep_cols]
     assert_close_rel(out.detach().cpu().numpy(), ref, RTOL, scale, "fwd")
     g = rng.standard_normal(ref.shape).astype(np.float32)
     out.backward(torch.from_numpy(g).to(DEV))
+    if compact:
+        gfull = np.zeros((B, F * F + D), np.float32)
+        gfull[:, keep_cols] = g
+        g = gfull
     ge_ref, gd_ref = O.dlrm_interaction_bwd(w, ids, dense, g, so)
     got_ids, got_rows = t.take_grad()
     np.testing.assert_array_equal(got_ids.cpu().numpy(), ids.reshape(-1))
@@ -94,3 +104,29 @@ def test_fm(F, D, rng):
     out.backward(torch.from_numpy(g).to(DEV))
     gscale = np.abs(g)[:, None, None] * np.abs(e).sum(1, keepdims=True)
     assert_close_rel(et.grad.cpu().numpy(), O.fm_bwd(e, g), RTOL, gscale, "fm bwd")
+
+
+def test_dlrm_model_compact_equals_reference_layout(rng):
+    from recommender_amd.ctr.model import DLRM
+
+    S, D, B, V = 26, 32, 256, 5000
+    g = torch.Generator(device=DEV)
+    g.manual_seed(0)
+    m1 = DLRM([64, D], [64, 1], D, V, S, 13, device=DEV, generator=g, compact=False)
+    m2 = DLRM([64, D], [64, 1], D, V, S, 13, device=DEV, compact=True)
+    m2.load_state_dict(m1.state_dict())
+    m2.embedding_layer.weight.copy_(m1.embedding_layer.weight)
+    x = {"cat_features": torch.from_numpy(rng.integers(0, V, (B, S))).to(DEV),
+         "int_features": torch.from_numpy(rng.standard_normal((B, 13)).astype(np.float32)).to(DEV)}
+    p1, p2 = m1(x), m2(x)
+    assert_close_rel(p2.detach().cpu().numpy(), p1.detach().cpu().numpy(), 1e-5, 1e-3, "logits")
+    p1.sum().backward()
+    p2.sum().backward()
+    k1 = m1.top_mlp.mlp[0].kernel.grad.cpu().numpy()
+    k2 = m2.top_mlp.mlp[0].kernel.grad.cpu().numpy()
+    assert_close_rel(k2, k1, 1e-5, np.abs(k1).max() * 1e-2, "top kernel grad")
+    F = S + 1
+    zero_rows = np.setdiff1d(np.arange(F * F + D), m2.compact_rows.cpu().numpy())
+    assert (k2[zero_rows] == 0).all() and (k1[zero_rows] == 0).all()
+    (i1, r1), (i2, r2) = m1.embedding_layer.take_grad(), m2.embedding_layer.take_grad()
+    assert_close_rel(r2.cpu().numpy(), r1.cpu().numpy(), 1e-5, np.abs(r1.cpu().numpy()).max() * 1e-2, "emb grad")
