@@ -143,6 +143,7 @@ int32_t rs_dot_interaction_bwd(const float* x, const float* grad_out, int64_t ba
  *   compact = 1: out[b] = [ Z(b) strict upper in row-major order (F(F-1)/2), dense[b] ]
  *                (the same values without the structural zeros; the caller drops the
  *                matching zero-input rows of the top-MLP kernel).
+ * Columns [width, out_stride) of each output row are zero-filled (GEMM alignment padding).
  * bwd re-gathers X from the table and writes grad_emb[b*S+s] and grad_dense[b]. */
 int32_t rs_dlrm_interaction_fwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
                                 int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
@@ -159,6 +160,26 @@ int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D, c
 int32_t rs_fm_fwd(const float* emb, int64_t batch, int32_t F, int32_t D, float* out, void* stream);
 int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t batch, int32_t F, int32_t D,
                   float* grad_emb, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Keras binary_crossentropy on probabilities (ctr/train.py:85, dien/train.py:18,
+ * esmm/train.py:101-102; [3p] TF 2.2 backend: clip to [eps, 1-eps], -(y log(p+eps) +
+ * (1-y) log(1-p+eps))), fused. reduction 0 = none (out[n]), 1 = sum, 2 = mean (out[1]);
+ * sums fold per-block partials in block order (deterministic). grad_out: [n] for
+ * reduction 0, else [1]. */
+size_t rs_bce_workspace_size(int64_t n);
+int32_t rs_bce_fwd(const float* p, const float* y, int64_t n, float eps, int32_t reduction,
+                   float* out, void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_bce_bwd(const float* p, const float* y, int64_t n, float eps, int32_t reduction,
+                   const float* grad_out, float* grad_p, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Dense-layer backward epilogue (Keras Dense with activation, ctr/layers.py:5-14,
+ * esmm/layers.py:4-13): dz = act'(y) ⊙ dy (act 0 = linear: dz not written, 1 = relu,
+ * 2 = sigmoid; y is the layer output) and db[n] = Σ_b dz[b, n] (deterministic fold). */
+size_t rs_act_bwd_colsum_workspace_size(int64_t B, int32_t N);
+int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N, int32_t act,
+                          float* dz, float* db, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

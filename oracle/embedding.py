@@ -65,8 +65,8 @@ def segment_sum_tiled(sorted_rows, sorted_pos, grad, n_rows, tile=DEDUP_TILE):
 
     The sorted entries are cut into tiles of `tile`; inside a tile the rows of one segment are
     added sequentially starting from +0.0 (a "piece"); the pieces of a segment that spans tiles
-    are folded in tile order in chunks of FIX_CHUNK pieces (each chunk sequentially from its
-    first piece), and the chunk sums are folded in order. Returns (uniq_rows, uniq_grad)."""
+    are folded per aligned group of FIX_CHUNK tiles (sequentially from the group's first
+    piece), and the group sums are folded in order. Returns (uniq_rows, uniq_grad)."""
     sorted_rows = np.asarray(sorted_rows).astype(np.int64)
     sorted_pos = np.asarray(sorted_pos).astype(np.int64)
     grad = np.asarray(grad, dtype=np.float32)
@@ -90,22 +90,20 @@ def segment_sum_tiled(sorted_rows, sorted_pos, grad, n_rows, tile=DEDUP_TILE):
     for j in range(int(piece_len.max())):
         sel = piece_len > j
         acc[sel] += rows_g[piece_start[sel] + j]
-    # segments over pieces: a segment's pieces are one per tile it touches, in tile order.
-    # Fold pieces in chunks of FIX_CHUNK (each chunk sequentially from its first piece), then
-    # fold the chunk sums sequentially (rs fix-up levels 1 and 2).
+    # segments over pieces: a segment has one piece per tile it touches, in tile order.
+    # Level 1 folds the pieces of each ALIGNED group of FIX_CHUNK tiles (sequentially from the
+    # group's first piece); level 2 folds the group sums in order (rs fix-up levels 1 and 2).
     piece_key = keys[piece_start]
+    piece_tile = tile_id[piece_start]
     seg_head = np.ones(n_pieces, bool)
     seg_head[1:] = piece_key[1:] != piece_key[:-1]
     seg_start = np.flatnonzero(seg_head)
-    seg_len = np.diff(np.append(seg_start, n_pieces))
-    seg_of_piece = np.repeat(np.arange(seg_start.size), seg_len)
-    idx_in_seg = np.arange(n_pieces) - seg_start[seg_of_piece]
-    chunk_head = (idx_in_seg % FIX_CHUNK) == 0
+    seg_of_piece = np.cumsum(seg_head) - 1
+    grp = piece_tile // FIX_CHUNK
+    chunk_head = seg_head.copy()
+    chunk_head[1:] |= grp[1:] != grp[:-1]
     chunk_start = np.flatnonzero(chunk_head)
     chunk_len = np.diff(np.append(chunk_start, n_pieces))
-    # a chunk never crosses a segment: cut lengths at segment ends
-    seg_end = (seg_start + seg_len)[seg_of_piece[chunk_start]]
-    chunk_len = np.minimum(chunk_len, seg_end - chunk_start)
     csum = acc[chunk_start].copy()
     for j in range(1, int(chunk_len.max())):
         sel = chunk_len > j

@@ -134,6 +134,7 @@ struct ApplyArgs {
   uint32_t* bitmap;       // keras: touched rows
   float* partial;         // [n_tiles][2][dim]
   float* chunk;           // [n_tiles][2][dim] level-1 chunk sums of spanning segments
+  uint8_t* tile_flags;    // [n_tiles] bit0: head of a spanning segment, bit1: aligned-group lead
   // OPT_EMIT (dedup output)
   float* uniq_grad;
   uint32_t* uniq_rows;
@@ -279,73 +280,86 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restric
   }
   bool ends = (k1 >= n) || keys[k1] != run_row;
   emit(run_row, run_starts, ends, run_start);
+  // fix-up roles of this tile (consumed by seg_chunk_kernel / seg_fixup_kernel)
+  if (gl == 0) {
+    uint8_t f = 0;
+    if (!ends && run_starts && run_row < n_rows) f |= 1;  // last run opens a spanning segment
+    const uint32_t fk = keys[k0];
+    if ((t % 32) == 0 && k0 > 0 && fk < n_rows && keys[k0 - 1] == fk) f |= 2;
+    a.tile_flags[t] = f;
+  }
 }
 
 // ---- fix-up of segments that span tiles ----------------------------------------------
-// A spanning segment with head tile h and last tile e has the ordered partial list
-//   P[0] = partial[h][1], P[i] = partial[h+i][0] (i = 1..e-h).
-// Level 1: chunk c = P[32c .. 32c+31] is folded sequentially by one lane group (leader tile
-// h+32c) into chunk[h+32c][role] (role 1 = head chunk, 0 = continuation chunk).
-// Level 2: one lane group per head tile folds the chunks in order and finalises the row.
-// For spans of <= 32 tiles this is the plain sequential fold of the partials.
+// A spanning segment with head tile h and last tile e has one partial per tile:
+//   P(h) = partial[h][1] (head part), P(t) = partial[t][0] for t = h+1..e.
+// Level 1: inside each ALIGNED group of kFixChunk tiles, the segment's partials are folded in
+// tile order by one lane group (the head tile for the head's group, else the group's first
+// tile) into chunk[leader][role] (role 1 = head group, 0 = continuation group).
+// Level 2: one lane group per head tile folds the group sums in order and finalises the row.
+// No search is needed: every boundary test is a load of the first key of a tile.
 constexpr int kFixChunk = 32;
 
-__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* keys, int64_t n, uint32_t v) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (keys[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// head tile / last tile of the segment of sorted entry k
-__device__ __forceinline__ void seg_tiles(const uint32_t* keys, int64_t n, int64_t k, int64_t& h,
-                                          int64_t& e) {
-  const uint32_t key = keys[k];
-  h = lower_bound_u32(keys, n, key) / RS_DEDUP_TILE;
-  e = (lower_bound_u32(keys, n, key + 1) - 1) / RS_DEDUP_TILE;
-}
-
 template <int VEC, int CPL>
-__device__ __forceinline__ void fold_partials(const float* base_first, const float* part, int64_t t0,
-                                              int64_t cnt, int dim, int gl, int lpr,
-                                              float (&acc)[CPL][VEC]) {
-  // acc = base_first; acc += part[(t0 + i) * 2 + 0] for i in [0, cnt)
+__device__ __forceinline__ void load_or_zero(const float* p, int dim, int gl, int lpr,
+                                             float (&acc)[CPL][VEC]) {
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     int col = (gl + c * lpr) * VEC;
     if (col < dim) {
-      RowIO<VEC>::load(base_first + col, acc[c]);
+      RowIO<VEC>::load(p + col, acc[c]);
     } else {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) acc[c][e] = 0.f;
     }
   }
+}
+
+template <int VEC, int CPL>
+__device__ __forceinline__ void store_row(float* p, int dim, int gl, int lpr,
+                                          const float (&acc)[CPL][VEC]) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    int col = (gl + c * lpr) * VEC;
+    if (col < dim) RowIO<VEC>::store(p + col, acc[c]);
+  }
+}
+
+// acc += partial[t][0] for t = t1, t1+1, ... while tile t's first key == key, t < t_end
+template <int VEC, int CPL>
+__device__ __forceinline__ void fold_group(const uint32_t* keys, int64_t n, uint32_t key,
+                                           const float* part, int64_t t1, int64_t t_end, int dim,
+                                           int gl, int lpr, float (&acc)[CPL][VEC]) {
+  constexpr int T = RS_DEDUP_TILE;
   constexpr int U = 8;
-  for (int64_t i = 0; i < cnt; i += U) {
+  for (int64_t t = t1; t < t_end; t += U) {
+    bool in[U];
     float r[U][CPL][VEC];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* p = part + ((t0 + i + u) * 2) * (int64_t)dim;
+      const int64_t tt = t + u;
+      in[u] = tt < t_end && tt * T < n && keys[tt * T] == key;
+    }
+    bool more = true;
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        int col = (gl + c * lpr) * VEC;
-        if (i + u < cnt && col < dim) {
-          RowIO<VEC>::load(p + col, r[u][c]);
-        } else {
+    for (int u = 0; u < U; ++u) {
+      more = more && in[u];
+      in[u] = more;  // the segment is contiguous: stop at the first tile it does not reach
+    }
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
-        }
+    for (int u = 0; u < U; ++u) {
+      if (in[u]) {
+        load_or_zero<VEC, CPL>(part + ((t + u) * 2) * (int64_t)dim, dim, gl, lpr, r[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i + u < cnt)
+      if (in[u])
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
 #pragma unroll
           for (int e = 0; e < VEC; ++e) acc[c][e] += r[u][c][e];
+    if (!more) return;
   }
 }
 
@@ -359,41 +373,26 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(const uint32_t* __restri
   const int gl = threadIdx.x & (lpr - 1);
   const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
   if (t >= n_tiles) return;
+  const uint8_t flags = a.tile_flags[t];
+  if (flags == 0) return;
   const int dim = a.dim;
   const int64_t k0 = t * T;
   const int64_t klast = (k0 + T < n ? k0 + T : n) - 1;
+  const int64_t group_end = (t / kFixChunk + 1) * kFixChunk;  // first tile of the next group
   float acc[CPL][VEC];
-  // role 1: head of a segment that continues into tile t+1
-  if (klast + 1 < n && keys[klast] < n_rows && keys[klast + 1] == keys[klast] &&
-      !(k0 > 0 && keys[k0] == keys[klast] && keys[k0 - 1] == keys[klast])) {
-    int64_t h, e;
-    seg_tiles(keys, n, klast, h, e);
-    // chunk 0 = P[0..31] = partial[t][1] + partial[t+1..min(t+31, e)][0]
-    int64_t cnt = e - t < kFixChunk - 1 ? e - t : kFixChunk - 1;
-    fold_partials<VEC, CPL>(a.partial + (t * 2 + 1) * (int64_t)dim, a.partial, t + 1, cnt, dim, gl,
-                            lpr, acc);
-    float* dst = chunk + (t * 2 + 1) * (int64_t)dim;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      int col = (gl + c * lpr) * VEC;
-      if (col < dim) RowIO<VEC>::store(dst + col, acc[c]);
-    }
+  // role 1: head tile of a segment that continues into tile t+1
+  if (flags & 1) {
+    const uint32_t lk = keys[klast];
+    load_or_zero<VEC, CPL>(a.partial + (t * 2 + 1) * (int64_t)dim, dim, gl, lpr, acc);
+    fold_group<VEC, CPL>(keys, n, lk, a.partial, t + 1, group_end, dim, gl, lpr, acc);
+    store_row<VEC, CPL>(chunk + (t * 2 + 1) * (int64_t)dim, dim, gl, lpr, acc);
   }
-  // role 0: continuation tile that leads a chunk (P index t-h is a multiple of 32)
-  if (k0 > 0 && keys[k0] < n_rows && keys[k0 - 1] == keys[k0]) {
-    int64_t h, e;
-    seg_tiles(keys, n, k0, h, e);
-    if ((t - h) % kFixChunk == 0) {
-      int64_t cnt = e - t < kFixChunk - 1 ? e - t : kFixChunk - 1;
-      fold_partials<VEC, CPL>(a.partial + (t * 2) * (int64_t)dim, a.partial, t + 1, cnt, dim, gl,
-                              lpr, acc);
-      float* dst = chunk + (t * 2) * (int64_t)dim;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        int col = (gl + c * lpr) * VEC;
-        if (col < dim) RowIO<VEC>::store(dst + col, acc[c]);
-      }
-    }
+  // role 0: first tile of an aligned group, continuing a segment from the previous group
+  if (flags & 2) {
+    const uint32_t fk = keys[k0];
+    load_or_zero<VEC, CPL>(a.partial + (t * 2) * (int64_t)dim, dim, gl, lpr, acc);
+    fold_group<VEC, CPL>(keys, n, fk, a.partial, t + 1, group_end, dim, gl, lpr, acc);
+    store_row<VEC, CPL>(chunk + (t * 2) * (int64_t)dim, dim, gl, lpr, acc);
   }
 }
 
@@ -404,55 +403,39 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
                                                         int64_t n_tiles,
                                                         const float* __restrict__ chunk) {
   constexpr int T = RS_DEDUP_TILE;
+  constexpr int U = 4;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
   const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
   if (t >= n_tiles - 1) return;
-  const int64_t k0 = t * T, klast = k0 + T - 1, knext = k0 + T;
-  if (knext >= n) return;
+  if (!(a.tile_flags[t] & 1)) return;  // not the head tile of a spanning segment
+  const int64_t klast = t * T + T - 1;
   const uint32_t row = keys[klast];
-  if (row >= n_rows || keys[knext] != row) return;  // last run does not continue
-  if (keys[k0] == row && k0 > 0 && keys[k0 - 1] == row) return;  // segment started earlier
-  int64_t h, e;
-  seg_tiles(keys, n, klast, h, e);
   const int dim = a.dim;
   float acc[CPL][VEC];
-  // acc = chunk[t][1]; acc += chunk[t + 32c][0] for c = 1 .. (e - t) / 32
-  const int64_t n_more = (e - t) / kFixChunk;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    int col = (gl + c * lpr) * VEC;
-    if (col < dim) {
-      RowIO<VEC>::load(chunk + (t * 2 + 1) * (int64_t)dim + col, acc[c]);
-    } else {
-#pragma unroll
-      for (int e2 = 0; e2 < VEC; ++e2) acc[c][e2] = 0.f;
-    }
-  }
-  constexpr int U = 8;
-  for (int64_t i = 1; i <= n_more; i += U) {
+  load_or_zero<VEC, CPL>(chunk + (t * 2 + 1) * (int64_t)dim, dim, gl, lpr, acc);
+  // following groups: leader tile g*32 continues the segment iff its first key == row
+  for (int64_t g = t / kFixChunk + 1;; g += U) {
+    bool in[U];
     float r[U][CPL][VEC];
+    bool more = true;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* p = chunk + ((t + (i + u) * kFixChunk) * 2) * (int64_t)dim;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        int col = (gl + c * lpr) * VEC;
-        if (i + u <= n_more && col < dim) {
-          RowIO<VEC>::load(p + col, r[u][c]);
-        } else {
-#pragma unroll
-          for (int e2 = 0; e2 < VEC; ++e2) r[u][c][e2] = 0.f;
-        }
-      }
+      const int64_t tt = (g + u) * kFixChunk;
+      in[u] = more && tt < n_tiles && keys[tt * T] == row;
+      more = in[u];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i + u <= n_more)
+      if (in[u]) load_or_zero<VEC, CPL>(chunk + ((g + u) * kFixChunk * 2) * (int64_t)dim, dim, gl, lpr, r[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (in[u])
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
 #pragma unroll
-          for (int e2 = 0; e2 < VEC; ++e2) acc[c][e2] += r[u][c][e2];
+          for (int e = 0; e < VEC; ++e) acc[c][e] += r[u][c][e];
+    if (!more) break;
   }
   finalize_row<OPT, VEC, CPL>(a, row, gl, lpr, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, klast) : 0);
 }
@@ -580,8 +563,13 @@ extern "C" int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t 
 }
 
 static size_t partial_bytes(int64_t n_ids, int32_t dim) {
-  // tile partials + level-1 chunk sums, each [n_tiles][2][dim]
-  return 2 * align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256);
+  // tile partials + level-1 chunk sums, each [n_tiles][2][dim], + one flag byte per tile
+  return 2 * align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256) +
+         align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE), 256);
+}
+static uint8_t* flags_of(float* partial, int64_t n_ids, int32_t dim) {
+  return reinterpret_cast<uint8_t*>(partial) +
+         2 * align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256);
 }
 static float* chunk_of(float* partial, int64_t n_ids, int32_t dim) {
   return partial + align_up((size_t)ceil_div(n_ids, RS_DEDUP_TILE) * 2 * dim * sizeof(float), 256) / 4;
@@ -617,6 +605,7 @@ extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const in
   a.dim = dim;
   a.partial = partial;
   a.chunk = chunk_of(partial, n_ids, dim);
+  a.tile_flags = flags_of(partial, n_ids, dim);
   a.uniq_grad = uniq_grad;
   a.uniq_rows = uniq_rows;
   a.seg_excl = seg;
@@ -656,6 +645,7 @@ extern "C" int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float
   a.bitmap = touched_bitmap;
   a.partial = static_cast<float*>(workspace);
   a.chunk = chunk_of(a.partial, n_ids, dim);
+  a.tile_flags = flags_of(a.partial, n_ids, dim);
   const void* ptrs[4] = {table, grad_out, m ? m : table, v ? v : table};
   RowGeom geom = row_geom(dim, ptrs, 4);
   return launch_segments(opt, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom,

@@ -164,6 +164,8 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
     const float* dn = src.dense + b * D;
     float* od = orow + nz;
     for (int d = lane; d < D; d += 64) od[d] = dn[d];
+    // zero the alignment padding of the row (compact layout padded for the GEMM tiles)
+    for (int64_t o = nz + D + lane; o < out_stride; o += 64) orow[o] = 0.f;
     if (__any(oob) && lane == 0) flag_oob(src.err_flag);
   }
 }
@@ -310,8 +312,10 @@ __global__ __launch_bounds__(64) void inter_fwd_generic(Src src, int64_t batch, 
       orow[compact_index(i, j, F, md.self_interaction)] = s;
   }
   if constexpr (DLRM_OUT) {
-    float* od = orow + out_width(F, md.self_interaction, md.skip_gather);
+    const int nz = out_width(F, md.self_interaction, md.skip_gather);
+    float* od = orow + nz;
     for (int d = lane; d < D; d += 64) od[d] = src.dense[b * D + d];
+    for (int64_t o = nz + D + lane; o < out_stride; o += 64) orow[o] = 0.f;
     if (__any(oob) && lane == 0) flag_oob(src.err_flag);
   }
 }

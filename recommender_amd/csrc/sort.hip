@@ -15,7 +15,7 @@ namespace rs {
 constexpr int kSortThreads = 256;         // 4 waves
 constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile
 constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
-constexpr int kMaxBins = 256;
+constexpr int kMaxBins = 512;
 
 // ---- keys from ids ------------------------------------------------------------------
 __global__ void make_keys_kernel(const void* __restrict__ ids, int32_t dtype, int64_t n,
@@ -80,31 +80,53 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) hist[(int64_t)d * n_tiles + blockIdx.x] = cnt[d];
 }
 
-// single-block exclusive scan, in place (n up to a few 100k)
+// single-block exclusive scan, in place (n up to a few 100k): the 1024 threads sweep the
+// array in coalesced 4096-element stripes; a stripe is scanned in LDS and carried forward.
 __global__ __launch_bounds__(1024) void scan_single_block_kernel(int32_t* __restrict__ a, int64_t n,
                                                                  int32_t* __restrict__ total) {
-  __shared__ int32_t part[1024];
-  int t = threadIdx.x;
-  int64_t per = (n + 1023) / 1024;
-  int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
-  int32_t s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += a[i];
-  part[t] = s;
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry_s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) carry_s = 0;
   __syncthreads();
-  // Hillis-Steele over 1024 partials
-  for (int off = 1; off < 1024; off <<= 1) {
-    int32_t v = t >= off ? part[t - off] : 0;
+  for (int64_t base = 0; base < n; base += 4096) {
+    // each thread owns 4 consecutive elements of the stripe
+    int32_t v[4];
+    int64_t i0 = base + (int64_t)t * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (i0 + k < n) ? a[i0 + k] : 0;
+    int32_t s = v[0] + v[1] + v[2] + v[3];
+    // inclusive wave scan
+    int32_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
     __syncthreads();
-    part[t] += v;
+    if (t < 16) {
+      int32_t ws = wsum[t];
+      int32_t xs = ws;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        int32_t y = __shfl_up(xs, off, 16);
+        if ((t & 15) >= off) xs += y;
+      }
+      wsum[t] = xs - ws;  // exclusive over waves
+    }
+    __syncthreads();
+    int32_t run = carry_s + wsum[w] + x - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < n) a[i0 + k] = run;
+      run += v[k];
+    }
+    __syncthreads();
+    if (t == 1023) carry_s = run;
     __syncthreads();
   }
-  int32_t run = t == 0 ? 0 : part[t - 1];
-  for (int64_t i = lo; i < hi; ++i) {
-    int32_t v = a[i];
-    a[i] = run;
-    run += v;
-  }
-  if (t == 1023 && total) *total = part[1023];
+  if (t == 0 && total) *total = carry_s;
 }
 
 // stable scatter
@@ -206,7 +228,7 @@ struct SortPlan {
 static SortPlan plan_sort(int64_t n_ids, int64_t n_rows) {
   SortPlan p;
   int kb = key_bits_for(n_rows);
-  p.passes = (kb + 7) / 8;
+  p.passes = (kb + 8) / 9;  // digits of <= 9 bits (512 bins): 3 passes for 40M rows
   p.bits = (kb + p.passes - 1) / p.passes;
   p.n_tiles = (int)ceil_div(n_ids, kSortTile);
   return p;
@@ -254,6 +276,7 @@ static int32_t dispatch_pass(int bits, const uint32_t* kin, const int32_t* vin, 
     case 6: return launch_pass<6>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
     case 7: return launch_pass<7>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
     case 8: return launch_pass<8>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    case 9: return launch_pass<9>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
   }
   set_error("radix pass bits %d unsupported", bits);
   return RS_E_UNSUPPORTED;

@@ -73,6 +73,11 @@ class DLRM(nn.Module):
         self.compact = compact
         iu = torch.triu_indices(F, F, 1)
         rows = torch.cat([iu[0] * F + iu[1], F * F + torch.arange(embedding_size)])
+        # the kernel pads the compact row to 64 columns with zeros; map the padding onto
+        # structural-zero rows (lower triangle incl. diagonal) so their gradient stays 0
+        pad = (rows.numel() + 63) // 64 * 64 - rows.numel()
+        il = torch.tril_indices(F, F, 0)
+        rows = torch.cat([rows, (il[0] * F + il[1])[:pad]])
         self.register_buffer("compact_rows", rows.to(device=self.embedding_layer.weight.device))
 
     def interact(self, cat_features, bmlp_activation, compact=False):
@@ -87,12 +92,16 @@ class DLRM(nn.Module):
         if not self.compact:
             tmlp_input = self.interact(cat_features, bmlp_activation)
             tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)
-            return self.top_mlp(tmlp_input).squeeze(1)
-        tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
-        first = self.top_mlp.mlp[0]
-        h = first(tmlp_input, kernel=first.kernel.index_select(0, self.compact_rows))
-        for layer in self.top_mlp.mlp[1:]:
-            h = layer(h)
-        return h.squeeze(1)
+            out = self.top_mlp(tmlp_input).squeeze(1)
+        else:
+            tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
+            first = self.top_mlp.mlp[0]
+            h = first(tmlp_input, rows=self.compact_rows)
+            for layer in self.top_mlp.mlp[1:]:
+                h = layer(h)
+            out = h.squeeze(1)
+        # forward kernels are queued: the side-stream sort now runs beside them
+        self.embedding_layer.presort(cat_features)
+        return out
 
     call = forward

@@ -7,9 +7,10 @@ dim 16, 3 epochs, DLRM units [512,256,64,16] / [512,256,1], Adam) plus:
   --optimizer  keras_adam (reference default, ctr/train.py:80,84) | lazy_adam | sgd
                (the commented DLRM SGD + DLRMScheduler path, ctr/train.py:77-79)
   --steps_per_epoch, --rows/--slab (per-slot tables), --embedding_size.
-The reference's `model.fit` differentiates the per-example BCE vector (reduction NONE,
-ctr/train.py:85), i.e. the gradient of the SUM over the batch [3p Keras 2.2]; --loss_reduction
-selects sum (reference) or mean.
+Loss: BinaryCrossentropy(reduction=NONE) (ctr/train.py:85) still calls
+keras.losses.binary_crossentropy, which averages over the LAST axis [3p TF 2.2]; the models
+output [B] (ctr/model.py:27,57), so the loss the reference differentiates is the batch mean.
+--loss_reduction keeps `sum` available.
 """
 from __future__ import annotations
 
@@ -19,7 +20,8 @@ import time
 import numpy as np
 import torch
 
-from ..nn import binary_crossentropy
+from ..functional import binary_crossentropy
+from ..nn import overlapped_weight_grads
 from ..optim import DLRMScheduler, KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import criteo_batch, criteo_cardinalities
 from .model import DLRM, DeepFM
@@ -28,23 +30,52 @@ from .model import DLRM, DeepFM
 class TrainStep:
     """One optimizer step of a ctr model: forward, BCE, backward, dense + sparse apply."""
 
-    def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None):
+    def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
+                 fused=True, overlap_wgrad=False):
         self.model = model
         dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
         tables = [model.embedding_layer]
         self.loss_reduction = loss_reduction
+        # measured on MI355X: a weight-grad GEMM beside the interaction backward only
+        # time-slices the CUs (no net gain), so the overlap is opt-in
+        self.wgrad = overlapped_weight_grads(model.embedding_layer.weight.device) if overlap_wgrad else None
         if optimizer == "sgd":
             lr = sched or (lr if lr is not None else 0.01)
             self.opt_dense = torch.optim.SGD(dense, lr=lr if not callable(lr) else lr(0))
-            self.opt_sparse = SparseSGD(tables, lr=lr)
+            self.opt_sparse = SparseSGD(tables, lr=lr, fused=fused)
             self._sched = lr if callable(lr) else None
         elif optimizer in ("keras_adam", "lazy_adam"):
             lr = lr if lr is not None else 1e-3
             self.opt_dense = KerasAdam(dense, lr=lr)
-            self.opt_sparse = SparseAdam(tables, lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy")
+            self.opt_sparse = SparseAdam(tables, lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy",
+                                         fused=fused)
             self._sched = None
         else:
             raise ValueError(f"unknown optimizer {optimizer}")
+
+    def capture(self, batch, warmup: int = 3):
+        """Capture one whole step (forward, loss, backward, dense + sparse apply) on `batch`'s
+        tensors into a HIP graph; returns a replay callable. Scalars (learning rates) are
+        frozen into the graph, so capture only with constant-lr SGD."""
+        if self._sched is not None or not isinstance(self.opt_sparse, SparseSGD):
+            raise RuntimeError("graph capture needs constant-lr SGD (scalars are frozen)")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self(batch)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self(batch)
+        self._graph_loss = loss
+
+        def replay():
+            g.replay()
+            return loss
+
+        return replay
 
     def __call__(self, batch):
         cat, dense_x, label = batch
@@ -53,9 +84,12 @@ class TrainStep:
                 g["lr"] = self._sched(self.opt_sparse.iterations)
         self.opt_dense.zero_grad(set_to_none=True)
         p = self.model({"cat_features": cat, "int_features": dense_x})
-        per_ex = binary_crossentropy(label, p)
-        loss = per_ex.sum() if self.loss_reduction == "sum" else per_ex.mean()
-        loss.backward()
+        loss = binary_crossentropy(label, p, reduction=self.loss_reduction)
+        if self.wgrad is not None:
+            with self.wgrad:
+                loss.backward()
+        else:
+            loss.backward()
         self.opt_dense.step()
         self.opt_sparse.step()
         return loss
@@ -83,7 +117,7 @@ def train(argv=None):
     ap.add_argument("--test_batch_size", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--optimizer", default="keras_adam", choices=["keras_adam", "lazy_adam", "sgd"])
-    ap.add_argument("--loss_reduction", default="sum", choices=["sum", "mean"])
+    ap.add_argument("--loss_reduction", default="mean", choices=["sum", "mean"])
     ap.add_argument("--embedding_size", type=int, default=16)
     ap.add_argument("--vocab_size", type=int, default=1_000_000)
     ap.add_argument("--slab", action="store_true", help="per-slot tables (Criteo skew) in one slab")

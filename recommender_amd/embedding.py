@@ -42,6 +42,10 @@ class Embedding(nn.Module):
         # zero-size leaf that keeps the lookup inside the autograd graph
         self.grad_handle = nn.Parameter(torch.zeros(0, device=device), requires_grad=True)
         self._pending: list[tuple[torch.Tensor, torch.Tensor]] = []
+        # fused sparse optimizer (set by SparseOptimizer(..., fused=True)): the sort runs on
+        # its side stream ahead of the dense forward, the apply inside the backward
+        self.fused_optimizer = None
+        self._presorted = None
 
     @property
     def n_slots(self) -> int:
@@ -52,6 +56,21 @@ class Embedding(nn.Module):
 
     def compute_mask(self, ids: torch.Tensor):
         return ids != 0 if self.mask_zero else None
+
+    # ---- fused-optimizer plumbing ----
+    def presort(self, ids: torch.Tensor):
+        """Queue the radix sort of this step's ids on the fused optimizer's side stream. Call it
+        after the step's forward kernels are queued: the host then issues the sort while the
+        GPU is busy with the forward, and the sort runs beside it. The lookup's backward reuses
+        it (or sorts on the spot when no presort was issued)."""
+        if self.fused_optimizer is not None and torch.is_grad_enabled():
+            self._presorted = (ids, self.fused_optimizer.sort_async(self, ids))
+
+    def take_presorted(self, ids: torch.Tensor):
+        p, self._presorted = self._presorted, None
+        if p is not None and p[0] is ids:
+            return p[1]
+        return self.fused_optimizer.sort_async(self, ids)
 
     # ---- sparse gradient plumbing ----
     def accumulate_grad(self, ids: torch.Tensor, grad_rows: torch.Tensor):

@@ -37,7 +37,12 @@ class _EmbeddingLookup(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        ctx.table_module.accumulate_grad(ctx.ids, grad_out.reshape(-1, grad_out.shape[-1]))
+        tm = ctx.table_module
+        g = grad_out.reshape(-1, grad_out.shape[-1])
+        if tm.fused_optimizer is not None:
+            tm.fused_optimizer.apply_async(tm, ctx.ids, g.contiguous(), tm.take_presorted(ctx.ids))
+        else:
+            tm.accumulate_grad(ctx.ids, g)
         return None, None, None
 
 
@@ -93,6 +98,8 @@ class _DLRMInteraction(torch.autograd.Function):
         if dense.shape != (B, D):
             raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
         width = (F * (F - 1) // 2 if compact else F * F) + D
+        if compact:  # pad to a multiple of 64 columns: well-tiled top-MLP GEMMs
+            width = (width + 63) // 64 * 64
         out = torch.empty(B, width, device=w.device, dtype=torch.float32)
         L.call("rs_dlrm_interaction_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
                L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
@@ -117,13 +124,17 @@ class _DLRMInteraction(torch.autograd.Function):
         L.call("rs_dlrm_interaction_bwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
                L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, ctx.compact,
                L.ptr(g), g.shape[1], L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
-        tm.accumulate_grad(ids, grad_emb)
+        if tm.fused_optimizer is not None:
+            tm.fused_optimizer.apply_async(tm, ids, grad_emb, tm.take_presorted(ids))
+        else:
+            tm.accumulate_grad(ids, grad_emb)
         return None, grad_dense, None, None, None
 
 
 def dlrm_interaction(table_module, ids, dense, compact: bool = False):
     """[Z, dense] with Z the strict-upper X·Xᵀ of X = [emb(ids), dense]: F*F wide with zeros
-    (reference layout) or, compact=True, the F(F-1)/2 kept values only."""
+    (reference layout) or, compact=True, the F(F-1)/2 kept values only (row zero-padded to a
+    multiple of 64 columns)."""
     return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids, compact)
 
 
@@ -151,3 +162,37 @@ class _FM(torch.autograd.Function):
 def fm_interaction(emb):
     """DeepFM second-order term 0.5*Σ_d((Σ_f e)^2 - Σ_f e^2) (ctr/model.py:21-23)."""
     return _FM.apply(emb)
+
+
+_RED = {"none": 0, "sum": 1, "mean": 2}
+
+
+class _BCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p, y, reduction, eps):
+        L.require_device(p, "y_pred")
+        p = p.contiguous().float()
+        y = y.contiguous().float().reshape(p.shape)
+        n = p.numel()
+        red = _RED[reduction]
+        out = torch.empty(p.shape if red == 0 else (), device=p.device, dtype=torch.float32)
+        ws = torch.empty(max(1, L.lib().rs_bce_workspace_size(n) // 4), device=p.device)
+        L.call("rs_bce_fwd", L.ptr(p), L.ptr(y), n, eps, red, L.ptr(out), L.ptr(ws),
+               ws.numel() * 4, L.stream_ptr(p.device))
+        ctx.save_for_backward(p, y)
+        ctx.red, ctx.eps = red, eps
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p, y = ctx.saved_tensors
+        g = g.contiguous().float()
+        dp = torch.empty_like(p)
+        L.call("rs_bce_bwd", L.ptr(p), L.ptr(y), p.numel(), ctx.eps, ctx.red, L.ptr(g), L.ptr(dp),
+               L.stream_ptr(p.device))
+        return dp, None, None, None
+
+
+def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float = 1e-7):
+    """Fused keras binary_crossentropy on probabilities (one kernel forward, one backward)."""
+    return _BCE.apply(y_pred, y_true, reduction, epsilon)

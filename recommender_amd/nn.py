@@ -36,40 +36,113 @@ def _splitk_chunks(batch: int, fan_in: int, fan_out: int) -> int:
     chunks followed by a sum runs at 90-120 TF/s (tools/probe_gemm.py, MI355X)."""
     if batch < 8192 or fan_in * fan_out > 4_000_000:
         return 1
+    # enough chunks to fill the chip, few enough that the [c, in, out] partials stay ~16 MB
+    target = max(8, min(64, (16 << 20) // max(1, fan_in * fan_out * 4)))
     for c in (64, 32, 16, 8):
-        if batch % c == 0:
+        if c <= target and batch % c == 0:
             return c
     return 1
 
 
+_ACT_CODE = {"relu": 1, "sigmoid": 2}
+_wgrad_stream: torch.cuda.Stream | None = None
+
+
+class overlapped_weight_grads:
+    """Context for a backward pass: Dense weight/bias gradients are computed on a second HIP
+    stream and written straight into .grad, so the dX chain (and the memory-bound kernels on
+    it, e.g. the interaction backward) runs beside the compute-bound weight-gradient GEMMs.
+    On exit the current stream waits for that stream."""
+
+    def __init__(self, device=None):
+        self.stream = torch.cuda.Stream(device=device)
+
+    def __enter__(self):
+        global _wgrad_stream
+        self._prev = _wgrad_stream
+        _wgrad_stream = self.stream
+        return self
+
+    def __exit__(self, *exc):
+        global _wgrad_stream
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+        _wgrad_stream = self._prev
+        return False
+
+
+def _accum_grad(param: torch.Tensor, g: torch.Tensor):
+    if param.grad is None:
+        param.grad = g
+    else:
+        param.grad.add_(g)
+
+
 class _DenseFn(torch.autograd.Function):
-    """y = x @ kernel + bias with a split-K weight gradient (deterministic: fixed chunking,
-    torch's fixed-order sum over chunks)."""
+    """y = act(x @ kernel[rows] + bias) for a Keras Dense layer (kernel [in, out]).
+
+    backward: dz = act'(y)*dy and the bias gradient in one kernel (rs_act_bwd_colsum);
+    dx = dz @ kernelᵀ; the weight gradient is a split-K batched GEMM (fixed chunking, fixed
+    fold order: deterministic). Weight and bias gradients are written into .grad directly
+    (on the overlapped weight-grad stream when one is active)."""
 
     @staticmethod
-    def forward(ctx, x, kernel, bias):
-        y = torch.addmm(bias, x, kernel) if bias is not None else x @ kernel
-        ctx.save_for_backward(x, kernel)
-        ctx.has_bias = bias is not None
+    def forward(ctx, x, handle, layer, rows):
+        k = layer.kernel if rows is None else layer.kernel.index_select(0, rows)
+        b = layer.bias
+        z = torch.addmm(b, x, k) if b is not None else x @ k
+        act = layer.act_code
+        if act == 1:
+            y = torch.relu_(z)
+        elif act == 2:
+            y = torch.sigmoid_(z)
+        else:
+            y = z
+        ctx.layer, ctx.rows, ctx.act = layer, rows, act
+        ctx.save_for_backward(x, k, y if act else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, kernel = ctx.saved_tensors
-        dx = dk = db = None
-        if ctx.needs_input_grad[0]:
-            dx = dy @ kernel.t()
-        if ctx.needs_input_grad[1]:
-            B, fi = x.shape
-            fo = dy.shape[1]
+        from . import _lib as L
+
+        x, k, y = ctx.saved_tensors
+        layer, act = ctx.layer, ctx.act
+        dy = dy.contiguous()
+        B, fi = x.shape
+        fo = dy.shape[1]
+        main = torch.cuda.current_stream(dy.device)
+        db = None
+        if act or layer.bias is not None:
+            dz = torch.empty_like(dy) if act else dy
+            db = torch.empty(fo, device=dy.device, dtype=torch.float32)
+            ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, fo) // 4),
+                             device=dy.device)
+            L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, fo, act, L.ptr(dz), L.ptr(db),
+                   L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
+        else:
+            dz = dy
+        dx = dz @ k.t() if ctx.needs_input_grad[0] else None
+        side = _wgrad_stream
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side if side is not None else main):
             c = _splitk_chunks(B, fi, fo)
             if c > 1:
-                dk = torch.bmm(x.view(c, B // c, fi).transpose(1, 2), dy.view(c, B // c, fo)).sum(0)
+                dk = torch.bmm(x.view(c, B // c, fi).transpose(1, 2), dz.view(c, B // c, fo)).sum(0)
             else:
-                dk = x.t() @ dy
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.sum(0)
-        return dx, dk, db
+                dk = x.t() @ dz
+            if ctx.rows is not None:
+                full = torch.zeros_like(layer.kernel)
+                full.index_copy_(0, ctx.rows, dk)
+                dk = full
+            _accum_grad(layer.kernel, dk)
+            if db is not None and layer.bias is not None:
+                _accum_grad(layer.bias, db)
+        if side is not None:
+            for t in (x, dz, db):
+                if t is not None:
+                    t.record_stream(side)
+        return dx, None, None, None
 
 
 class Dense(nn.Module):
@@ -78,6 +151,8 @@ class Dense(nn.Module):
         super().__init__()
         self.units = int(units)
         self.activation = get_activation(activation)
+        self.act_code = _ACT_CODE.get(activation, 0) if isinstance(activation, (str, type(None))) else (
+            1 if activation is torch.relu else 2 if activation is torch.sigmoid else -1)
         self.use_bias = use_bias
         self._device = device
         self._generator = generator
@@ -94,17 +169,24 @@ class Dense(nn.Module):
         self.kernel = nn.Parameter(k)
         self.bias = nn.Parameter(torch.zeros(self.units, device=device)) if self.use_bias else None
 
-    def forward(self, x, kernel=None):
+    def forward(self, x, rows: torch.Tensor | None = None):
+        """rows: optional index of kernel rows to use (the input holds only those features;
+        the other rows get an exactly-zero gradient)."""
         if self.kernel is None:
             self.build(x.shape[-1], x.device)
-        k = self.kernel if kernel is None else kernel
-        if x.dim() == 2 and x.is_cuda:
-            y = _DenseFn.apply(x, k, self.bias)
-        elif self.bias is not None:
-            y = torch.matmul(x, k) + self.bias
-        else:
-            y = torch.matmul(x, k)
+        if x.dim() == 2 and x.is_cuda and self.act_code >= 0 and torch.is_grad_enabled():
+            return _DenseFn.apply(x, self._handle(), self, rows)
+        k = self.kernel if rows is None else self.kernel.index_select(0, rows)
+        y = torch.matmul(x, k)
+        if self.bias is not None:
+            y = y + self.bias
         return self.activation(y) if self.activation is not None else y
+
+    def _handle(self):
+        # a differentiable input so the Function is recorded whenever the params need grad
+        if not hasattr(self, "_gh") or self._gh.device != self.kernel.device:
+            self._gh = torch.zeros(0, device=self.kernel.device, requires_grad=True)
+        return self._gh
 
 
 def binary_crossentropy(y_true, y_pred, from_logits: bool = False, epsilon: float = 1e-7):

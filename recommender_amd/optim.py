@@ -51,7 +51,8 @@ class SortedIds:
     original positions, device count of distinct valid rows."""
 
     def __init__(self, ids: torch.Tensor, n_rows: int, slot_offsets: torch.Tensor | None = None,
-                 err_flag: torch.Tensor | None = None, ws: _Workspace | None = None):
+                 err_flag: torch.Tensor | None = None, ws: _Workspace | None = None,
+                 count_unique: bool = True):
         ws = ws or _Workspace()
         ids = ids.contiguous()
         L.require_device(ids, "ids")
@@ -60,7 +61,7 @@ class SortedIds:
         self.n = n
         self.rows = torch.empty(n, dtype=torch.int32, device=dev)
         self.pos = torch.empty(n, dtype=torch.int32, device=dev)
-        self.n_unique = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.n_unique = torch.zeros(1, dtype=torch.int32, device=dev) if count_unique else None
         n_slots = 1 if slot_offsets is None else slot_offsets.numel() - 1
         nbytes = L.lib().rs_sort_ids_workspace_size(n)
         w = ws.get("sort", nbytes, dev)
@@ -69,8 +70,9 @@ class SortedIds:
                L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
 
     @classmethod
-    def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None):
-        return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws)
+    def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None,
+                  count_unique: bool = True):
+        return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws, count_unique)
 
 
 def dedup_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
@@ -94,15 +96,49 @@ def dedup_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
 
 
 class SparseOptimizer:
+    """Sparse appliers for Embedding tables.
+
+    fused=False: lookups hand (ids, grad rows) to the table; step() sorts and applies.
+    fused=True (one lookup per table per step): the ids are radix-sorted on a side HIP stream
+    as soon as the lookup (or Embedding.presort) sees them, and the segmented-sum + update runs
+    on that stream right after the lookup's backward kernel — overlapping the rest of the
+    dense backward. step() joins the side stream into the current one."""
     kind = L.RS_OPT_SGD
 
-    def __init__(self, tables, lr=0.01):
+    def __init__(self, tables, lr=0.01, fused=False):
         if isinstance(tables, Embedding):
             tables = [tables]
         self.tables = list(tables)
         self.lr = lr
         self.iterations = 0
         self.ws = _Workspace()
+        self.fused = fused
+        self.side = None
+        self._applied = set()
+        if fused:
+            dev = self.tables[0].weight.device
+            self.side = torch.cuda.Stream(device=dev)
+            for t in self.tables:
+                t.fused_optimizer = self
+
+    # ---- fused path ----
+    def sort_async(self, table: Embedding, ids: torch.Tensor) -> SortedIds:
+        main = torch.cuda.current_stream(ids.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            s = SortedIds.for_table(table, ids, self.ws, count_unique=False)
+        ids.record_stream(self.side)
+        return s
+
+    def apply_async(self, table: Embedding, ids, grad_rows, sorted_ids: SortedIds):
+        if id(table) in self._applied:
+            raise RuntimeError("fused sparse optimizer: a table was looked up twice in one step")
+        main = torch.cuda.current_stream(grad_rows.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.apply(table, ids, grad_rows, self._params(), sorted_ids=sorted_ids)
+        grad_rows.record_stream(self.side)
+        self._applied.add(id(table))
 
     def _params(self) -> L.AdamParams:
         lr = self.lr(self.iterations) if callable(self.lr) else self.lr
@@ -114,7 +150,7 @@ class SparseOptimizer:
     def apply(self, table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor, params,
               sorted_ids: SortedIds | None = None):
         dev = table.weight.device
-        s = sorted_ids or SortedIds.for_table(table, ids, self.ws)
+        s = sorted_ids or SortedIds.for_table(table, ids, self.ws, count_unique=False)
         g = grad_rows.contiguous()
         m, v, bitmap = self._slots(table)
         nbytes = L.lib().rs_apply_workspace_size(s.n, table.output_dim)
@@ -127,11 +163,15 @@ class SparseOptimizer:
                    table.input_dim, table.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
 
     def step(self):
+        applied = set()
+        if self.fused:
+            torch.cuda.current_stream(self.tables[0].weight.device).wait_stream(self.side)
+            applied, self._applied = self._applied, set()
         params = self._params()
         for t in self.tables:
             got = t.take_grad()
             if got is None:
-                if self.kind == L.RS_OPT_KERAS_ADAM:
+                if self.kind == L.RS_OPT_KERAS_ADAM and id(t) not in applied:
                     # Keras still decays m/v and moves var densely when the slice is empty
                     m, v, bitmap = self._slots(t)
                     L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
@@ -156,8 +196,9 @@ class SparseAdam(SparseOptimizer):
     """mode='keras': exact Keras Adam (dense m/v decay + dense var update, 24·V·D bytes/step);
     mode='lazy': the same update restricted to touched rows."""
 
-    def __init__(self, tables, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, mode="keras"):
-        super().__init__(tables, lr)
+    def __init__(self, tables, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, mode="keras",
+                 fused=False):
+        super().__init__(tables, lr, fused=fused)
         self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
         if mode not in ("keras", "lazy"):
             raise ValueError("mode must be 'keras' or 'lazy'")

@@ -72,6 +72,10 @@ def test_dlrm_fused(D, slab, compact, rng):
     keep_cols = np.r_[np.flatnonzero(np.triu(np.ones((F, F), bool), 1).reshape(-1)), F * F + np.arange(D)]
     if compact:
         ref = ref[:, keep_cols]
+        pad = (ref.shape[1] + 63) // 64 * 64 - ref.shape[1]
+        got_pad = out.detach()[:, ref.shape[1]:].cpu().numpy()
+        assert got_pad.shape[1] == pad and (got_pad == 0).all()
+        out = out[:, : ref.shape[1]]
     emb = OE.embedding_lookup(w, ids, so)
     x = np.concatenate([emb, dense[:, None]], 1)
     scale = np.concatenate([_pair_scale(x, False, True), np.abs(dense)], 1)
@@ -130,3 +134,56 @@ def test_dlrm_model_compact_equals_reference_layout(rng):
     assert (k2[zero_rows] == 0).all() and (k1[zero_rows] == 0).all()
     (i1, r1), (i2, r2) = m1.embedding_layer.take_grad(), m2.embedding_layer.take_grad()
     assert_close_rel(r2.cpu().numpy(), r1.cpu().numpy(), 1e-5, np.abs(r1.cpu().numpy()).max() * 1e-2, "emb grad")
+
+
+@pytest.mark.parametrize("reduction", ["none", "sum", "mean"])
+def test_bce_fused(reduction, rng):
+    from oracle.ctr import bce, bce_grad
+    from recommender_amd.functional import binary_crossentropy
+
+    n = 10_007
+    p = rng.random(n).astype(np.float32)
+    p[:5] = [0.0, 1.0, 1e-9, 1 - 1e-9, 0.5]
+    y = (rng.random(n) < 0.3).astype(np.float32)
+    pt = torch.from_numpy(p).to(DEV).requires_grad_(True)
+    out = binary_crossentropy(torch.from_numpy(y).to(DEV), pt, reduction=reduction)
+    ref = bce(y, p).astype(np.float64)
+    ref = {"none": ref, "sum": ref.sum(), "mean": ref.mean()}[reduction]
+    assert_close_rel(out.detach().cpu().numpy(), ref, 1e-5, 0.0, "bce")
+    g = torch.ones_like(out)
+    out.backward(g)
+    gref = bce_grad(y, p).astype(np.float64) * y.size  # oracle is for the mean
+    if reduction == "mean":
+        gref = gref / n
+    assert_close_rel(pt.grad.cpu().numpy(), gref, 1e-5, 0.0, "bce grad")
+
+
+@pytest.mark.parametrize("act", [None, "relu", "sigmoid"])
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dense_layer_grads(act, overlap, rng):
+    """Dense (Keras layout) forward/backward with the fused activation+bias epilogue and the
+    split-K weight gradient vs torch fp32 autograd."""
+    from recommender_amd.nn import Dense, overlapped_weight_grads
+
+    B, fi, fo = 16384, 96, 40
+    layer = Dense(fo, act, in_features=fi, device=DEV)
+    x = torch.from_numpy(rng.standard_normal((B, fi)).astype(np.float32)).to(DEV).requires_grad_(True)
+    k_ref = layer.kernel.detach().clone().requires_grad_(True)
+    b_ref = layer.bias.detach().clone().requires_grad_(True)
+    x_ref = x.detach().clone().requires_grad_(True)
+    z = x_ref @ k_ref + b_ref
+    y_ref = {None: z, "relu": torch.relu(z), "sigmoid": torch.sigmoid(z)}[act]
+    g = torch.from_numpy(rng.standard_normal((B, fo)).astype(np.float32)).to(DEV)
+    y_ref.backward(g)
+    if overlap:
+        with overlapped_weight_grads():
+            y = layer(x)
+            y.backward(g)
+    else:
+        y = layer(x)
+        y.backward(g)
+    torch.cuda.synchronize()
+    for got, ref, name in ((y, y_ref, "y"), (x.grad, x_ref.grad, "dx"), (layer.kernel.grad, k_ref.grad, "dk"),
+                           (layer.bias.grad, b_ref.grad, "db")):
+        r = ref.detach().cpu().numpy()
+        assert_close_rel(got.detach().cpu().numpy(), r, 1e-4, np.abs(r).max(), name)
