@@ -29,13 +29,14 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_sort_ids", "rs_embedding_apply"]
+WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_sort_ids", "rs_embedding_apply",
+         "rs_sort_ids_sharded", "rs_embedding_dedup_grad"]
 # the roofline kernel: the embedding-path kernel with the most algorithmic HBM traffic per step
 # (re-gather of every row + grad-row write). It runs on the main stream, so its HIP-event time
 # is its own; the sort/apply run on the fused optimizer's side stream beside dense GEMMs, so
 # their event spans include co-run time and are reported as such.
 ROOF_KERNEL = "rs_dlrm_interaction_bwd"
-SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply"}
+SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_sort_ids_sharded", "rs_embedding_dedup_grad"}
 
 
 def parse():
@@ -62,8 +63,14 @@ def init_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local % max(ndev, 1))
+        # RS_DIST_BACKEND=gloo: rehearse several ranks on one GPU (exchange staged through host)
+        backend = os.environ.get("RS_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -86,7 +93,7 @@ def measured_unique(pool, model):
     from recommender_amd.optim import SortedIds
 
     t = model.embedding_layer
-    us = [int(SortedIds.for_table(t, b[0]).n_unique.item()) for b in pool]
+    us = [int(SortedIds(b[0], t.input_dim, t.slot_offsets).n_unique.item()) for b in pool]
     return float(np.mean(us))
 
 
@@ -148,7 +155,7 @@ def cpu_baseline(args, cards):
 def main():
     args = parse()
     world, rank, local = init_dist(args)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     L.load()
     if L.lib().rs_device_count() < 1:
@@ -157,10 +164,23 @@ def main():
     cards = criteo_cardinalities(args.rows, S)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed)
-    model = build_model("DLRM", D, args.rows, S, 13, dev, slot_cardinalities=cards,
-                        bottom=[512, 256, D], top=[512, 256, 1], generator=g)
+    comm = None
+    if world > 1:
+        # row-sharded slab over the ranks (RCCL all-to-all), data-parallel dense MLPs
+        from recommender_amd.ctr.model import DLRM
+        from recommender_amd.sharded import Comm, ShardedSlabEmbedding
+
+        comm = Comm()
+        g.manual_seed(args.seed + 1000 * rank)
+        emb = ShardedSlabEmbedding(cards, D, comm, device=dev, generator=g)
+        g.manual_seed(args.seed)
+        model = DLRM([512, 256, D], [512, 256, 1], D, args.rows, S, 13, device=dev,
+                     generator=g, embedding_layer=emb)
+    else:
+        model = build_model("DLRM", D, args.rows, S, 13, dev, slot_cardinalities=cards,
+                            bottom=[512, 256, D], top=[512, 256, 1], generator=g)
     step = TrainStep(model, args.optimizer, lr=0.01 if args.optimizer == "sgd" else 1e-3,
-                     fused=bool(args.fused))
+                     fused=bool(args.fused), comm=comm)
     pool = make_pool(args, cards, rank, dev)
     U = measured_unique(pool, model)
 
@@ -203,7 +223,7 @@ def main():
             kern[name] = {"avg_us": round(avg * 1e3, 2), "calls": cnt,
                           "algorithmic_bytes": int(by),
                           "achieved_GBs": round(by / (avg * 1e-3) / 1e9, 1),
-                          "stream": "side (co-running)" if (name in SIDE_STREAM and args.fused) else "main"}
+                          "stream": "side (co-running)" if (name in SIDE_STREAM and (args.fused or world > 1)) else "main"}
     dom = ROOF_KERNEL if ROOF_KERNEL in kern else None
     roof = None
     if dom:
@@ -237,7 +257,8 @@ def main():
             "config": {"workload": f"dlrm_criteo_{S}x{args.rows}x{D}", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "rows": args.rows, "dim": D, "slots": S,
                        "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
-                       "optimizer": args.optimizer, "parallelism": f"dp{world}" if world > 1 else "single"},
+                       "optimizer": args.optimizer,
+                       "parallelism": f"row-sharded slab x{world} (RCCL all-to-all) + dp{world} MLPs" if world > 1 else "single"},
             "roofline": roof, "embedding_path": emb_path, "kernels": kern,
             "cpu_baseline": cpu, "loss": float(loss.item()),
         }

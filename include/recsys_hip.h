@@ -91,6 +91,24 @@ int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids, const int6
                     int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
                     void* stream);
 
+/* Row-sharded variant: rows dealt cyclically over `world` ranks
+ * (owner = row % world, local row = row / world). Keys are owner-major:
+ * key = owner * ceil(n_rows/world) + local row, so the sorted unique keys are grouped by owner
+ * rank with the owner's local rows ascending; the OOB sentinel is world * ceil(n_rows/world).
+ * world = 1 is rs_sort_ids. */
+int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_t n_ids,
+                            const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                            int32_t world, uint32_t* sorted_keys, int32_t* sorted_pos,
+                            int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                            void* stream);
+/* From sorted keys: uniq_keys[u] (ascending), inverse[p] = u of position p (-1 for an OOB id),
+ * n_unique[1], and owner_counts[world] (unique keys per owner rank; may be NULL).
+ * Workspace: rs_sort_ids_workspace_size(n_ids) suffices. */
+int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos, int64_t n_ids,
+                          int64_t n_rows, int32_t world, uint32_t* uniq_keys, int32_t* inverse,
+                          int32_t* n_unique, int32_t* owner_counts, void* workspace,
+                          size_t ws_bytes, void* stream);
+
 /* a-2 (part 2) deduplicated gradient: uniq_rows[u], uniq_grad[u, dim] for the n_unique
  * distinct valid rows (count from rs_sort_ids), uniq_grad[u] = Σ grad_out[p] over the
  * positions p of row u. Summation order: sequential over sorted positions inside tiles of

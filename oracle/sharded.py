@@ -1,0 +1,51 @@
+"""Oracle: the row-sharded embedding step over W ranks — TEST INFRASTRUCTURE ONLY
+(see oracle/__init__.py; parity unpinned).
+
+Restates recommender_amd/sharded.py's semantics: rows dealt cyclically (owner = row % W, local
+row = row // W); each rank deduplicates its gradient with the tiled fold over owner-major keys;
+owners receive (local row, grad) lists rank-major, fold them with the same tiled order and
+apply SGD with lr/W. The reference itself only has replicated MirroredStrategy tables
+(ctr/train.py:71); the all-to-all layout is required by BASELINE.json's north star.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .embedding import global_rows, segment_sum_tiled, sort_ids
+
+
+def owner_keys(rows: np.ndarray, n_rows: int, world: int):
+    stride = -(-n_rows // world)
+    key_space = n_rows if world == 1 else stride * world
+    keys = np.where(rows < 0, key_space, (rows % world) * stride + rows // world)
+    return keys, stride, key_space
+
+
+def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_offsets=None):
+    """Returns the updated full table after one sharded SGD step."""
+    V, D = full_table.shape
+    stride = -(-V // world)
+    recv = [[] for _ in range(world)]  # recv[o] = list of (local rows, grads) from rank 0..W-1
+    for r in range(world):
+        rows = global_rows(per_rank_ids[r], V, slot_offsets)
+        keys, _, key_space = owner_keys(rows, V, world)
+        order = np.argsort(keys, kind="stable")
+        sk = keys[order].astype(np.uint32)
+        uk, ug = segment_sum_tiled(sk, order.astype(np.int32), per_rank_grads[r], key_space)
+        uk = uk.astype(np.int64)
+        for o in range(world):
+            sel = (uk // stride) == o
+            recv[o].append((uk[sel] - o * stride, ug[sel]))
+    out = full_table.copy()
+    lr_w = np.float32(float(np.float32(lr)) / world) if world > 1 else np.float32(lr)
+    for o in range(world):
+        local = np.concatenate([x[0] for x in recv[o]])
+        grads = np.concatenate([x[1] for x in recv[o]]) if local.size else np.zeros((0, D), np.float32)
+        if local.size == 0:
+            continue
+        shard_rows = (V - o + world - 1) // world
+        sr, sp, _ = sort_ids(local, shard_rows)
+        ur, ug = segment_sum_tiled(sr, sp, grads, shard_rows)
+        g_rows = ur.astype(np.int64) * world + o
+        out[g_rows] = out[g_rows] - lr_w * ug
+    return out

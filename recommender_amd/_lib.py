@@ -39,6 +39,9 @@ _SIGS = {
     "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_sort_ids_sharded": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _sz,
+                                   _p]),
+    "rs_unique_inverse": (_i32, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_dedup_workspace_size": (_sz, [_i64, _i32]),
     "rs_embedding_dedup_grad": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _p, _sz, _p]),
     "rs_apply_workspace_size": (_sz, [_i64, _i32]),

@@ -18,20 +18,27 @@ constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per til
 constexpr int kMaxBins = 512;
 
 // ---- keys from ids ------------------------------------------------------------------
+// world == 1: key = global row. world > 1 (rows dealt cyclically over ranks): owner-major key
+// = (row % world) * shard_stride + row / world, so sorted unique keys come grouped by owner rank
+// with the owner's local row (key % shard_stride) ascending inside each group.
 __global__ void make_keys_kernel(const void* __restrict__ ids, int32_t dtype, int64_t n,
                                  const int64_t* __restrict__ slot_offsets, int32_t n_slots,
-                                 int64_t n_rows, uint32_t* __restrict__ keys,
+                                 int64_t n_rows, int32_t world, int64_t shard_stride,
+                                 int64_t key_space, uint32_t* __restrict__ keys,
                                  int32_t* __restrict__ vals, int32_t* err_flag) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   bool oob = false;
   for (; i < n; i += stride) {
     int64_t r = global_row(ids, dtype, i, slot_offsets, n_slots, n_rows);
+    int64_t k;
     if (r < 0) {
       oob = true;
-      r = n_rows;  // sentinel: sorts after every valid row
+      k = key_space;  // sentinel: sorts after every valid row
+    } else {
+      k = world == 1 ? r : (r % world) * shard_stride + r / world;
     }
-    keys[i] = static_cast<uint32_t>(r);
+    keys[i] = static_cast<uint32_t>(k);
     vals[i] = static_cast<int32_t>(i);
   }
   if (__any(oob) && (threadIdx.x & 63) == 0) flag_oob(err_flag);
@@ -210,6 +217,50 @@ __global__ __launch_bounds__(256) void count_unique_kernel(const uint32_t* __res
     int32_t t = red[0] + red[1] + red[2] + red[3];
     if (t) atomicAdd(n_unique, t);
   }
+}
+
+__global__ void head_flags_u32_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t key_space,
+                                      int32_t* __restrict__ flags) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t k = keys[i];
+    flags[i] = (k < key_space && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+  }
+}
+
+// unique keys, inverse map and per-owner counts from the sorted keys (excl = exclusive scan of
+// the head flags): uniq[seg] = key, inverse[pos[k]] = seg for valid keys, -1 for OOB ones.
+__global__ void unique_inverse_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ pos,
+                                      const int32_t* __restrict__ excl, int64_t n, uint32_t key_space,
+                                      uint32_t* __restrict__ uniq, int32_t* __restrict__ inverse) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    const uint32_t k = keys[i];
+    const bool valid = k < key_space;
+    const bool head = valid && (i == 0 || keys[i - 1] != k);
+    const int32_t seg = excl[i] + (head ? 1 : 0) - 1;
+    if (head) uniq[seg] = k;
+    inverse[pos[i]] = valid ? seg : -1;
+  }
+}
+
+// owner_counts[o] = #unique keys in [o*stride, (o+1)*stride) (uniq sorted ascending)
+__global__ void owner_counts_kernel(const uint32_t* __restrict__ uniq, const int32_t* __restrict__ n_unique,
+                                    int64_t shard_stride, int32_t world, int32_t* __restrict__ counts) {
+  const int o = threadIdx.x;
+  if (o >= world) return;
+  const int32_t nu = *n_unique;
+  auto lb = [&](int64_t v) {
+    int32_t lo = 0, hi = nu;
+    while (lo < hi) {
+      int32_t mid = (lo + hi) >> 1;
+      if ((int64_t)uniq[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  counts[o] = lb((int64_t)(o + 1) * shard_stride) - lb((int64_t)o * shard_stride);
 }
 
 static int key_bits_for(int64_t n_rows) {
@@ -407,23 +458,89 @@ int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
 
 using namespace rs;
 
+static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
+                             const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                             int32_t world, uint32_t* sorted_keys, int32_t* sorted_pos,
+                             int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                             hipStream_t st, int64_t* key_space_out);
+
 extern "C" size_t rs_sort_ids_workspace_size(int64_t n_ids) {
   Carver c(nullptr, 0);
   c.take<uint32_t>(n_ids);
   c.take<int32_t>(n_ids);
-  return c.off + radix_sort_ws_size(n_ids) + 512;
+  return c.off + radix_sort_ws_size(n_ids) + exclusive_scan_ws_size(n_ids) + 1024;
 }
 
 extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
                                const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                                uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
                                int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream) {
+  return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr);
+}
+
+extern "C" int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_t n_ids,
+                                       const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                                       int32_t world, uint32_t* sorted_keys, int32_t* sorted_pos,
+                                       int32_t* n_unique, int32_t* err_flag, void* workspace,
+                                       size_t ws_bytes, void* stream) {
+  return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, world, sorted_keys,
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr);
+}
+
+extern "C" int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos,
+                                     int64_t n_ids, int64_t n_rows, int32_t world,
+                                     uint32_t* uniq_keys, int32_t* inverse, int32_t* n_unique,
+                                     int32_t* owner_counts, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  RS_CHECK_ARG(world >= 1 && n_rows > 0 && n_ids >= 0, "bad sizes");
+  RS_CHECK_ARG(n_ids == 0 || (sorted_keys && sorted_pos && uniq_keys && inverse && n_unique),
+               "null pointer");
+  hipStream_t st = as_stream(stream);
+  const int64_t stride = ceil_div(n_rows, world);
+  const int64_t key_space = world == 1 ? n_rows : stride * world;
+  RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, 4, st));
+  if (n_ids == 0) {
+    if (owner_counts) RS_CHECK_HIP(hipMemsetAsync(owner_counts, 0, 4 * (size_t)world, st));
+    return RS_OK;
+  }
+  Carver c(workspace, ws_bytes);
+  int32_t* excl = c.take<int32_t>(n_ids);
+  void* scan_ws = c.take<char>(exclusive_scan_ws_size(n_ids));
+  if (!c.ok()) {
+    set_error("unique workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
+  head_flags_u32_kernel<<<blocks, 256, 0, st>>>(sorted_keys, n_ids, (uint32_t)key_space, excl);
+  RS_CHECK_LAUNCH();
+  int32_t s = exclusive_scan_i32(excl, excl, n_ids, n_unique, scan_ws, exclusive_scan_ws_size(n_ids), st);
+  if (s) return s;
+  unique_inverse_kernel<<<blocks, 256, 0, st>>>(sorted_keys, sorted_pos, excl, n_ids,
+                                                (uint32_t)key_space, uniq_keys, inverse);
+  RS_CHECK_LAUNCH();
+  if (owner_counts) {
+    owner_counts_kernel<<<1, 64 * ((world + 63) / 64), 0, st>>>(uniq_keys, n_unique, stride, world,
+                                                                owner_counts);
+    RS_CHECK_LAUNCH();
+  }
+  return RS_OK;
+}
+
+static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
+                             const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                             int32_t world, uint32_t* sorted_rows, int32_t* sorted_pos,
+                             int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                             hipStream_t st, int64_t*) {
   RS_CHECK_ARG(n_ids >= 0 && n_ids < (int64_t(1) << 31), "n_ids out of range");
   RS_CHECK_ARG(n_rows > 0 && n_rows < (int64_t(1) << 31) - 1, "n_rows out of range");
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
   RS_CHECK_ARG(n_slots >= 1, "n_slots must be >= 1");
+  RS_CHECK_ARG(world >= 1 && world <= 1024, "world out of range");
   RS_CHECK_ARG(ids || n_ids == 0, "ids is null");
-  hipStream_t st = as_stream(stream);
+  const int64_t shard_stride = ceil_div(n_rows, world);
+  const int64_t key_space = world == 1 ? n_rows : shard_stride * world;
+  RS_CHECK_ARG(key_space < (int64_t(1) << 31) - 1, "key space out of range");
   if (n_unique) RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, sizeof(int32_t), st));
   if (n_ids == 0) return RS_OK;
   Carver c(workspace, ws_bytes);
@@ -435,14 +552,14 @@ extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
     return RS_E_WORKSPACE;
   }
   int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
-  make_keys_kernel<<<blocks, 256, 0, st>>>(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, keys,
-                                           vals, err_flag);
+  make_keys_kernel<<<blocks, 256, 0, st>>>(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, world,
+                                           shard_stride, key_space, keys, vals, err_flag);
   RS_CHECK_LAUNCH();
-  int32_t s = radix_sort_pairs(keys, vals, sorted_rows, sorted_pos, n_ids, n_rows,
+  int32_t s = radix_sort_pairs(keys, vals, sorted_rows, sorted_pos, n_ids, key_space,
                                static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, st);
   if (s) return s;
   if (n_unique) {
-    count_unique_kernel<<<std::min(blocks, 512), 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, n_unique);
+    count_unique_kernel<<<std::min(blocks, 512), 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);
     RS_CHECK_LAUNCH();
   }
   return RS_OK;

@@ -53,7 +53,8 @@ class DLRM(nn.Module):
     the kernel rows of the zero inputs receive an exactly-zero gradient as in the reference."""
 
     def __init__(self, bottom_mlp_units, top_mlp_units, embedding_size, vocab_size, num_cat_fea,
-                 num_int_fea, device=None, slot_cardinalities=None, generator=None, compact=True):
+                 num_int_fea, device=None, slot_cardinalities=None, generator=None, compact=True,
+                 embedding_layer=None):
         super().__init__()
         if bottom_mlp_units[-1] != embedding_size:
             raise ValueError("the last bottom-MLP width must equal embedding_size (ctr/model.py:55)")
@@ -65,12 +66,15 @@ class DLRM(nn.Module):
         F = num_cat_fea + 1
         self.top_mlp = MLP(top_mlp_units, final_activation="sigmoid",
                            in_features=F * F + embedding_size, device=device, generator=generator)
-        if slot_cardinalities is None:
+        if embedding_layer is not None:
+            self.embedding_layer = embedding_layer  # e.g. a ShardedSlabEmbedding
+        elif slot_cardinalities is None:
             self.embedding_layer = Embedding(vocab_size, embedding_size, device=device, generator=generator)
         else:
             self.embedding_layer = SlabEmbedding(slot_cardinalities, embedding_size, device=device, generator=generator)
         self.interaction = DotInteraction(False, True)
         self.compact = compact
+        self._exchanged = None
         iu = torch.triu_indices(F, F, 1)
         rows = torch.cat([iu[0] * F + iu[1], F * F + torch.arange(embedding_size)])
         # the kernel pads the compact row to 64 columns with zeros; map the padding onto
@@ -78,10 +82,15 @@ class DLRM(nn.Module):
         pad = (rows.numel() + 63) // 64 * 64 - rows.numel()
         il = torch.tril_indices(F, F, 0)
         rows = torch.cat([rows, (il[0] * F + il[1])[:pad]])
-        self.register_buffer("compact_rows", rows.to(device=self.embedding_layer.weight.device))
+        self.register_buffer("compact_rows", rows.to(device=self.top_mlp.mlp[0].kernel.device))
 
     def interact(self, cat_features, bmlp_activation, compact=False):
-        """[Z, bottom] — ctr/model.py:49-55 fused into one kernel."""
+        """[Z, bottom] — ctr/model.py:49-55 fused into one kernel. With a row-sharded slab the
+        kernel reads this step's exchanged unique rows through the inverse index."""
+        if self._exchanged is not None:
+            view, inv = self._exchanged
+            self._exchanged = None
+            return dlrm_interaction(view, inv, bmlp_activation, compact)
         return dlrm_interaction(self.embedding_layer, cat_features, bmlp_activation, compact)
 
     def forward(self, x, training=None, mask=None):
@@ -89,6 +98,9 @@ class DLRM(nn.Module):
         int_features = int_features.reshape(-1, self.num_int_fea).float()
         cat_features = cat_features.reshape(-1, self.num_cat_fea)
         bmlp_activation = self.bottom_mlp(int_features)
+        if hasattr(self.embedding_layer, "exchange"):
+            # row-sharded slab: the all-to-all exchange (side stream) overlaps the bottom MLP
+            self._exchanged = self.embedding_layer.exchange(cat_features)
         if not self.compact:
             tmlp_input = self.interact(cat_features, bmlp_activation)
             tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)

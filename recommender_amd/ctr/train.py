@@ -31,14 +31,25 @@ class TrainStep:
     """One optimizer step of a ctr model: forward, BCE, backward, dense + sparse apply."""
 
     def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
-                 fused=True, overlap_wgrad=False):
+                 fused=True, overlap_wgrad=False, comm=None):
+        """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
+        all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
+        by its owners inside the backward."""
+        from ..sharded import ShardedSlabEmbedding
+
         self.model = model
+        self.comm = comm
         dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
-        tables = [model.embedding_layer]
+        self.dense = dense
+        emb = model.embedding_layer
+        self.sharded = isinstance(emb, ShardedSlabEmbedding)
+        tables = [emb.shard if self.sharded else emb]
+        if self.sharded:
+            fused = False
         self.loss_reduction = loss_reduction
         # measured on MI355X: a weight-grad GEMM beside the interaction backward only
         # time-slices the CUs (no net gain), so the overlap is opt-in
-        self.wgrad = overlapped_weight_grads(model.embedding_layer.weight.device) if overlap_wgrad else None
+        self.wgrad = overlapped_weight_grads(dense[0].device) if overlap_wgrad else None
         if optimizer == "sgd":
             lr = sched or (lr if lr is not None else 0.01)
             self.opt_dense = torch.optim.SGD(dense, lr=lr if not callable(lr) else lr(0))
@@ -52,6 +63,8 @@ class TrainStep:
             self._sched = None
         else:
             raise ValueError(f"unknown optimizer {optimizer}")
+        if self.sharded:
+            emb.set_optimizer(self.opt_sparse)
 
     def capture(self, batch, warmup: int = 3):
         """Capture one whole step (forward, loss, backward, dense + sparse apply) on `batch`'s
@@ -90,9 +103,25 @@ class TrainStep:
                 loss.backward()
         else:
             loss.backward()
+        if self.comm is not None and self.comm.world > 1:
+            self._allreduce_dense()
         self.opt_dense.step()
-        self.opt_sparse.step()
+        if self.sharded:
+            self.model.embedding_layer.join()
+            self.opt_sparse.iterations += 1
+        else:
+            self.opt_sparse.step()
         return loss
+
+    def _allreduce_dense(self):
+        """One bucketed RCCL all-reduce of every dense gradient (≈3 MB for the DLRM MLPs),
+        averaged over ranks — the MirroredStrategy dense-gradient sync."""
+        grads = [p.grad for p in self.dense if p.grad is not None]
+        flat = torch._utils._flatten_dense_tensors(grads)
+        self.comm.all_reduce_(flat)
+        flat.mul_(1.0 / self.comm.world)
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
 
 
 def build_model(model_type, embedding_size, vocab_size, num_cat_fea, num_int_fea, device,

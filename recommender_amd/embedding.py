@@ -31,7 +31,8 @@ class Embedding(nn.Module):
         if weight is not None:
             if tuple(weight.shape) != (self.input_dim, self.output_dim):
                 raise ValueError("weight shape mismatch")
-            w = weight.to(device=device, dtype=torch.float32).contiguous()
+            # always a private copy: the table is updated in place by the sparse optimizers
+            w = weight.detach().to(device=device, dtype=torch.float32).clone().contiguous()
         else:
             w = torch.empty(self.input_dim, self.output_dim, device=device, dtype=torch.float32)
             w.uniform_(-init_range, init_range, generator=generator)

@@ -52,7 +52,7 @@ class SortedIds:
 
     def __init__(self, ids: torch.Tensor, n_rows: int, slot_offsets: torch.Tensor | None = None,
                  err_flag: torch.Tensor | None = None, ws: _Workspace | None = None,
-                 count_unique: bool = True):
+                 count_unique: bool = True, world: int = 1):
         ws = ws or _Workspace()
         ids = ids.contiguous()
         L.require_device(ids, "ids")
@@ -65,9 +65,14 @@ class SortedIds:
         n_slots = 1 if slot_offsets is None else slot_offsets.numel() - 1
         nbytes = L.lib().rs_sort_ids_workspace_size(n)
         w = ws.get("sort", nbytes, dev)
-        L.call("rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets), n_slots,
-               int(n_rows), L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique),
-               L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
+        if world == 1:
+            L.call("rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets), n_slots,
+                   int(n_rows), L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique),
+                   L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
+        else:
+            L.call("rs_sort_ids_sharded", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets),
+                   n_slots, int(n_rows), int(world), L.ptr(self.rows), L.ptr(self.pos),
+                   L.ptr(self.n_unique), L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
 
     @classmethod
     def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None,
