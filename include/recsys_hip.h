@@ -180,6 +180,39 @@ int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t batch, int32_
                   float* grad_emb, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * DIEN recurrences; one wave per example, H <= 64, uint8 mask [B, L]
+ * (ids != 0, dien/model.py:68); masked steps carry the state. The input projections of all
+ * steps (x·W + b) and all weight gradients are caller GEMMs.
+ * a-9  keras GRU, reset_after (InterestExtract dien/layers.py:79,131):
+ *      xw [B,L,3H] = [x_z,x_r,x_h]; U [H,3H] recurrent kernel; rb [3H] recurrent bias;
+ *      out [B,L,H] state after every step; saved [B,L,4H] = [z, r, hh, inner_h] (may be NULL).
+ *      bwd: dout [B,L,H] → dxw [B,L,3H] (grad of x·W+b), dinner [B,L,3H] (grad of h·U+rb). */
+int32_t rs_gru_fwd(const float* xw, const float* U, const float* rb, const uint8_t* mask,
+                   int64_t B, int32_t L, int32_t H, float* out, float* saved, void* stream);
+int32_t rs_gru_bwd(const float* dout, const float* out, const float* saved, const float* U,
+                   const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
+                   float* dinner, void* stream);
+/* a-11 AUGRUCell under keras RNN (dien/layers.py:161-204): xw = [x·Ku_x+bu, x·Kr_x+br,
+ *      x·Kh_x+bh]; Kuh, Krh [H,H] = h rows of the update/reset kernels ([h, x] concat order),
+ *      Khr [H,H] = r·h rows of the candidate kernel ([x, r·h] order); att [B,L].
+ *      final_h [B,H]; states [B,L,H]; saved [B,L,4H] = [u, r, hh, r·h_prev].
+ *      bwd: dfinal [B,H] → dxw [B,L,3H], datt [B,L]. */
+int32_t rs_augru_fwd(const float* xw, const float* att, const float* Kuh, const float* Krh,
+                     const float* Khr, const uint8_t* mask, int64_t B, int32_t L, int32_t H,
+                     float* final_h, float* states, float* saved, void* stream);
+int32_t rs_augru_bwd(const float* dfinal, const float* att, const float* states,
+                     const float* saved, const float* Kuh, const float* Krh, const float* Khr,
+                     const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
+                     float* datt, void* stream);
+/* a-10 DIENAttention (dien/layers.py:145-158): a = softmax_t(h_t·q + (1-m_t)(-1e9)),
+ *      q = K·target [B,H] (caller); bwd: da → dhs [B,L,H] (= ds_t q, written), dq [B,H]. */
+int32_t rs_dien_attention_fwd(const float* hs, const float* q, const uint8_t* mask, int64_t B,
+                              int32_t L, int32_t H, float* a, void* stream);
+int32_t rs_dien_attention_bwd(const float* hs, const float* q, const float* a, const float* da,
+                              int64_t B, int32_t L, int32_t H, float* dhs, float* dq,
+                              void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Keras binary_crossentropy on probabilities (ctr/train.py:85, dien/train.py:18,
  * esmm/train.py:101-102; [3p] TF 2.2 backend: clip to [eps, 1-eps], -(y log(p+eps) +
  * (1-y) log(1-p+eps))), fused. reduction 0 = none (out[n]), 1 = sum, 2 = mean (out[1]);

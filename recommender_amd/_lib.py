@@ -59,6 +59,12 @@ _SIGS = {
     "rs_bce_workspace_size": (_sz, [_i64]),
     "rs_bce_fwd": (_i32, [_p, _p, _i64, C.c_float, _i32, _p, _p, _sz, _p]),
     "rs_bce_bwd": (_i32, [_p, _p, _i64, C.c_float, _i32, _p, _p, _p]),
+    "rs_gru_fwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_augru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _p]),
+    "rs_augru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_dien_attention_fwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p]),
+    "rs_dien_attention_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_act_bwd_colsum_workspace_size": (_sz, [_i64, _i32]),
     "rs_act_bwd_colsum": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
 }

@@ -1,0 +1,489 @@
+// dien.hip — DIEN interest extraction / evolution recurrences (a-9..a-11):
+//   GRU      keras.layers.GRU(units, return_sequences=True) [3p TF 2.2, reset_after=True]
+//            (InterestExtract, dien/layers.py:79,131), masked steps carry the state;
+//   AUGRU    AUGRUCell under keras.layers.RNN (dien/layers.py:161-204): u = a·σ(·), opposite
+//            update convention to the GRU, masked steps carry the state, output = last state;
+//   ATTN     DIENAttention (dien/layers.py:145-158): softmax_L(h_t·(K t) + (1-m_t)(-1e9)).
+// Design (MI355X): the recurrence is latency-bound (100 dependent steps, [B,H]x[H,3H] per step),
+// so one wave owns one example for the whole sequence: lane j < H keeps unit j's state and the
+// j-th column (fwd) or row (bwd) of every recurrent weight in VGPRs, and the state vector is
+// broadcast by v_readlane (scalar operand of the FMA) — no LDS, no barriers, no per-step launch.
+// The input projections x·W (+bias) of all steps and all weight gradients are plain GEMMs done
+// by the caller (hipBLASLt); the kernels only do what is inherently sequential.
+#include "common.hpp"
+
+namespace rs {
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float bcast(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+// ---------------------------------------------------------------------------------------
+// GRU (Keras reset_after): xw[b,t] = [x_z, x_r, x_h] = x·W + b_in (caller),
+// inner = h·U + rb; z = σ(x_z+inner_z); r = σ(x_r+inner_r); hh = tanh(x_h + r·inner_h);
+// h = z·h_prev + (1-z)·hh.  saved[b,t] = [z, r, hh, inner_h].
+// ---------------------------------------------------------------------------------------
+template <int HM>
+__global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ xw,
+                                                      const float* __restrict__ U,
+                                                      const float* __restrict__ rb,
+                                                      const uint8_t* __restrict__ mask, int64_t B,
+                                                      int L, int H, float* __restrict__ out,
+                                                      float* __restrict__ saved) {
+  const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const bool act = j < H;
+  const int H3 = 3 * H;
+  float uz[HM], ur[HM], uh[HM];
+#pragma unroll
+  for (int k = 0; k < HM; ++k) {
+    const bool ok = act && k < H;
+    uz[k] = ok ? U[k * H3 + j] : 0.f;
+    ur[k] = ok ? U[k * H3 + H + j] : 0.f;
+    uh[k] = ok ? U[k * H3 + 2 * H + j] : 0.f;
+  }
+  const float rbz = act ? rb[j] : 0.f, rbr = act ? rb[H + j] : 0.f, rbh = act ? rb[2 * H + j] : 0.f;
+  const float* xb = xw + b * (int64_t)L * H3;
+  const uint8_t* mb = mask + b * L;
+  float h = 0.f;
+  float nz = act ? xb[j] : 0.f, nr = act ? xb[H + j] : 0.f, nh = act ? xb[2 * H + j] : 0.f;
+  for (int t = 0; t < L; ++t) {
+    const float xz = nz, xr = nr, xh = nh;
+    if (t + 1 < L && act) {  // prefetch the next step's input projection
+      const float* xn = xb + (int64_t)(t + 1) * H3;
+      nz = xn[j];
+      nr = xn[H + j];
+      nh = xn[2 * H + j];
+    }
+    float iz = 0.f, ir = 0.f, ih = 0.f;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) {
+      const float hk = bcast(h, k);
+      iz = fmaf(hk, uz[k], iz);
+      ir = fmaf(hk, ur[k], ir);
+      ih = fmaf(hk, uh[k], ih);
+    }
+    iz += rbz;
+    ir += rbr;
+    ih += rbh;
+    const float z = sigm(xz + iz), r = sigm(xr + ir);
+    const float hh = tanhf(xh + r * ih);
+    const float hn = z * h + (1.f - z) * hh;
+    if (mb[t]) h = act ? hn : 0.f;
+    if (act) {
+      const int64_t o = b * L + t;
+      out[o * H + j] = h;
+      if (saved) {
+        float* s = saved + o * 4 * H;
+        s[j] = z;
+        s[H + j] = r;
+        s[2 * H + j] = hh;
+        s[3 * H + j] = ih;
+      }
+    }
+  }
+}
+
+// dout[b,t] = dL/dh_t (every step); writes dxw = [dpre_z, dpre_r, dpre_h] (grad of x·W + b_in)
+// and dinner = [dpre_z, dpre_r, r·dpre_h] (grad of h·U + rb); dU / dW / biases are GEMMs.
+template <int HM>
+__global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ dout,
+                                                      const float* __restrict__ out,
+                                                      const float* __restrict__ saved,
+                                                      const float* __restrict__ U,
+                                                      const uint8_t* __restrict__ mask, int64_t B,
+                                                      int L, int H, float* __restrict__ dxw,
+                                                      float* __restrict__ dinner) {
+  const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const bool act = j < H;
+  const int H3 = 3 * H;
+  float wz[HM], wr[HM], wh[HM];  // row j of U: U[j][g*H + k]
+#pragma unroll
+  for (int k = 0; k < HM; ++k) {
+    const bool ok = act && k < H;
+    wz[k] = ok ? U[j * H3 + k] : 0.f;
+    wr[k] = ok ? U[j * H3 + H + k] : 0.f;
+    wh[k] = ok ? U[j * H3 + 2 * H + k] : 0.f;
+  }
+  const uint8_t* mb = mask + b * L;
+  float dh = 0.f;
+  for (int t = L - 1; t >= 0; --t) {
+    const int64_t o = b * L + t;
+    if (act) dh += dout[o * H + j];
+    float* dx = dxw + o * H3;
+    float* di = dinner + o * H3;
+    if (!mb[t]) {  // state carried: the gradient passes through unchanged
+      if (act) {
+        dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
+        di[j] = di[H + j] = di[2 * H + j] = 0.f;
+      }
+      continue;
+    }
+    float z = 0.f, r = 0.f, hh = 0.f, ih = 0.f, hp = 0.f;
+    if (act) {
+      const float* s = saved + o * 4 * H;
+      z = s[j];
+      r = s[H + j];
+      hh = s[2 * H + j];
+      ih = s[3 * H + j];
+      hp = t > 0 ? out[(o - 1) * H + j] : 0.f;
+    }
+    const float dz = dh * (hp - hh);
+    const float dph = dh * (1.f - z) * (1.f - hh * hh);
+    const float dih = dph * r;
+    const float dr = dph * ih;
+    const float dpz = act ? dz * z * (1.f - z) : 0.f;
+    const float dpr = act ? dr * r * (1.f - r) : 0.f;
+    const float dihm = act ? dih : 0.f;
+    if (act) {
+      dx[j] = dpz;
+      dx[H + j] = dpr;
+      dx[2 * H + j] = dph;
+      di[j] = dpz;
+      di[H + j] = dpr;
+      di[2 * H + j] = dih;
+    }
+    float acc = dh * z;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) {
+      acc = fmaf(bcast(dpz, k), wz[k], acc);
+      acc = fmaf(bcast(dpr, k), wr[k], acc);
+      acc = fmaf(bcast(dihm, k), wh[k], acc);
+    }
+    dh = act ? acc : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// AUGRU: xw[b,t] = [x·Ku_x + bu, x·Kr_x + br, x·Kh_x + bh]; Kuh/Krh = the h rows of the update
+// and reset kernels ([prev, x] concat order), Khr = the r·h rows of the candidate kernel
+// ([x, r·h] order). u = σ(xu + h·Kuh), r = σ(xr + h·Krh), hh = tanh(xh + (r⊙h)·Khr),
+// u' = a_t·u, h = u'·hh + (1-u')·h_prev. saved[b,t] = [u, r, hh, r⊙h_prev].
+// ---------------------------------------------------------------------------------------
+template <int HM>
+__global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict__ xw,
+                                                        const float* __restrict__ att,
+                                                        const float* __restrict__ Kuh,
+                                                        const float* __restrict__ Krh,
+                                                        const float* __restrict__ Khr,
+                                                        const uint8_t* __restrict__ mask, int64_t B,
+                                                        int L, int H, float* __restrict__ final_h,
+                                                        float* __restrict__ states,
+                                                        float* __restrict__ saved) {
+  const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const bool act = j < H;
+  const int H3 = 3 * H;
+  float ku[HM], kr[HM], kh[HM];
+#pragma unroll
+  for (int k = 0; k < HM; ++k) {
+    const bool ok = act && k < H;
+    ku[k] = ok ? Kuh[k * H + j] : 0.f;
+    kr[k] = ok ? Krh[k * H + j] : 0.f;
+    kh[k] = ok ? Khr[k * H + j] : 0.f;
+  }
+  const float* xb = xw + b * (int64_t)L * H3;
+  const uint8_t* mb = mask + b * L;
+  const float* ab = att + b * L;
+  float h = 0.f;
+  for (int t = 0; t < L; ++t) {
+    const float* x = xb + (int64_t)t * H3;
+    const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
+    const float a = ab[t];
+    float iu = 0.f, ir = 0.f;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) {
+      const float hk = bcast(h, k);
+      iu = fmaf(hk, ku[k], iu);
+      ir = fmaf(hk, kr[k], ir);
+    }
+    const float u = sigm(xu + iu), r = sigm(xr + ir);
+    const float rh = act ? r * h : 0.f;
+    float ihh = 0.f;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) ihh = fmaf(bcast(rh, k), kh[k], ihh);
+    const float hh = tanhf(xh + ihh);
+    const float ua = u * a;
+    const float hn = ua * hh + (1.f - ua) * h;
+    if (mb[t]) h = act ? hn : 0.f;
+    if (act) {
+      const int64_t o = b * L + t;
+      if (states) states[o * H + j] = h;
+      if (saved) {
+        float* s = saved + o * 4 * H;
+        s[j] = u;
+        s[H + j] = r;
+        s[2 * H + j] = hh;
+        s[3 * H + j] = rh;
+      }
+    }
+  }
+  if (act) final_h[b * H + j] = h;
+}
+
+// dfinal[b] = dL/d(last state); writes dxw = [dpre_u, dpre_r, dpre_hh] and datt[b,t].
+template <int HM>
+__global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict__ dfinal,
+                                                        const float* __restrict__ att,
+                                                        const float* __restrict__ states,
+                                                        const float* __restrict__ saved,
+                                                        const float* __restrict__ Kuh,
+                                                        const float* __restrict__ Krh,
+                                                        const float* __restrict__ Khr,
+                                                        const uint8_t* __restrict__ mask, int64_t B,
+                                                        int L, int H, float* __restrict__ dxw,
+                                                        float* __restrict__ datt) {
+  const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const bool act = j < H;
+  const int H3 = 3 * H;
+  float ku[HM], kr[HM], kh[HM];  // rows j
+#pragma unroll
+  for (int k = 0; k < HM; ++k) {
+    const bool ok = act && k < H;
+    ku[k] = ok ? Kuh[j * H + k] : 0.f;
+    kr[k] = ok ? Krh[j * H + k] : 0.f;
+    kh[k] = ok ? Khr[j * H + k] : 0.f;
+  }
+  const uint8_t* mb = mask + b * L;
+  const float* ab = att + b * L;
+  float dh = act ? dfinal[b * H + j] : 0.f;
+  for (int t = L - 1; t >= 0; --t) {
+    const int64_t o = b * L + t;
+    float* dx = dxw + o * H3;
+    if (!mb[t]) {
+      if (act) dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
+      if (j == 0) datt[o] = 0.f;
+      continue;
+    }
+    float u = 0.f, r = 0.f, hh = 0.f, hp = 0.f;
+    if (act) {
+      const float* s = saved + o * 4 * H;
+      u = s[j];
+      r = s[H + j];
+      hh = s[2 * H + j];
+      hp = t > 0 ? states[(o - 1) * H + j] : 0.f;
+    }
+    const float a = ab[t];
+    const float ua = u * a;
+    const float dua = dh * (hh - hp);
+    float dhp = dh * (1.f - ua);
+    // attention-score gradient: Σ_j dua_j · u_j
+    float ds = act ? dua * u : 0.f;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ds += __shfl_xor(ds, off);
+    if (j == 0) datt[o] = ds;
+    const float dpu = act ? dua * a * u * (1.f - u) : 0.f;
+    const float dph = act ? dh * ua * (1.f - hh * hh) : 0.f;
+    float drh = 0.f;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) drh = fmaf(bcast(dph, k), kh[k], drh);
+    const float dr = drh * hp;
+    dhp = fmaf(drh, r, dhp);
+    const float dpr = act ? dr * r * (1.f - r) : 0.f;
+#pragma unroll
+    for (int k = 0; k < HM; ++k) {
+      dhp = fmaf(bcast(dpu, k), ku[k], dhp);
+      dhp = fmaf(bcast(dpr, k), kr[k], dhp);
+    }
+    if (act) {
+      dx[j] = dpu;
+      dx[H + j] = dpr;
+      dx[2 * H + j] = dph;
+    }
+    dh = act ? dhp : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// DIENAttention: s_t = h_t·q + (1-m_t)(-1e9), q = K·target (caller); a = softmax over t.
+// One wave per example, lanes over time steps.
+// ---------------------------------------------------------------------------------------
+constexpr int kAttMaxT = 4;  // L <= 256
+
+__global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ hs,
+                                                      const float* __restrict__ q,
+                                                      const uint8_t* __restrict__ mask, int64_t B,
+                                                      int L, int H, float* __restrict__ a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const float* qb = q + b * H;  // uniform loads: every lane reads the same q_i
+  float s[kAttMaxT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < kAttMaxT; ++c) {
+    const int t = lane + 64 * c;
+    s[c] = -INFINITY;
+    if (t < L) {
+      const float* hr = hs + (b * L + t) * (int64_t)H;
+      float acc = 0.f;
+      for (int i = 0; i < H; ++i) acc = fmaf(hr[i], qb[i], acc);
+      const float m = mask[b * L + t] ? 1.f : 0.f;
+      acc = acc + (1.f - m) * -1e9f;
+      s[c] = acc;
+      mx = fmaxf(mx, acc);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < kAttMaxT; ++c) {
+    const int t = lane + 64 * c;
+    s[c] = t < L ? expf(s[c] - mx) : 0.f;
+    sum += s[c];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+#pragma unroll
+  for (int c = 0; c < kAttMaxT; ++c) {
+    const int t = lane + 64 * c;
+    if (t < L) a[b * L + t] = s[c] / sum;
+  }
+}
+
+// ds_t = a_t (da_t - Σ a·da); dhs[b,t,:] = ds_t·q (written, not accumulated); dq = Σ_t ds_t h_t
+__global__ __launch_bounds__(256) void att_bwd_kernel(const float* __restrict__ hs,
+                                                      const float* __restrict__ q,
+                                                      const float* __restrict__ a,
+                                                      const float* __restrict__ da, int64_t B, int L,
+                                                      int H, float* __restrict__ dhs,
+                                                      float* __restrict__ dq) {
+  __shared__ float dsm[4][64 * kAttMaxT];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < kAttMaxT; ++c) {
+    const int t = lane + 64 * c;
+    if (t < L) dot += a[b * L + t] * da[b * L + t];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+#pragma unroll
+  for (int c = 0; c < kAttMaxT; ++c) {
+    const int t = lane + 64 * c;
+    if (t < L) dsm[wave][t] = a[b * L + t] * (da[b * L + t] - dot);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  // lane i < H: dq_i = Σ_t ds_t h_{t,i}; dhs rows: lane i writes column i of every step
+  const float qi = lane < H ? q[b * H + lane] : 0.f;
+  float acc = 0.f;
+  for (int t = 0; t < L; ++t) {
+    const float ds = dsm[wave][t];
+    if (lane < H) {
+      const int64_t o = (b * L + t) * (int64_t)H + lane;
+      acc = fmaf(ds, hs[o], acc);
+      dhs[o] = ds * qi;
+    }
+  }
+  if (lane < H) dq[b * H + lane] = acc;
+}
+
+static int hm_for(int H) {
+  if (H <= 8) return 8;
+  if (H <= 16) return 16;
+  if (H <= 24) return 24;
+  if (H <= 32) return 32;
+  if (H <= 40) return 40;
+  if (H <= 48) return 48;
+  if (H <= 64) return 64;
+  return 0;
+}
+
+#define RS_HM_DISPATCH(H, CALL)                                       \
+  switch (hm_for(H)) {                                                \
+    case 8: { constexpr int HM = 8; CALL; } break;                   \
+    case 16: { constexpr int HM = 16; CALL; } break;                 \
+    case 24: { constexpr int HM = 24; CALL; } break;                 \
+    case 32: { constexpr int HM = 32; CALL; } break;                 \
+    case 40: { constexpr int HM = 40; CALL; } break;                 \
+    case 48: { constexpr int HM = 48; CALL; } break;                 \
+    case 64: { constexpr int HM = 64; CALL; } break;                 \
+    default: set_error("recurrent units %d > 64 unsupported", H); return RS_E_UNSUPPORTED; \
+  }
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int32_t rs_gru_fwd(const float* xw, const float* U, const float* rb, const uint8_t* mask,
+                              int64_t B, int32_t L, int32_t H, float* out, float* saved,
+                              void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(xw && U && rb && mask && out, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_HM_DISPATCH(H, ({ gru_fwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(xw, U, rb, mask, B, L, H, out, saved); }));
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_gru_bwd(const float* dout, const float* out, const float* saved, const float* U,
+                              const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
+                              float* dinner, void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(dout && out && saved && U && mask && dxw && dinner, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_HM_DISPATCH(H, ({ gru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dout, out, saved, U, mask, B, L, H, dxw, dinner); }));
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_augru_fwd(const float* xw, const float* att, const float* Kuh, const float* Krh,
+                                const float* Khr, const uint8_t* mask, int64_t B, int32_t L,
+                                int32_t H, float* final_h, float* states, float* saved,
+                                void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(xw && att && Kuh && Krh && Khr && mask && final_h, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_HM_DISPATCH(H, ({ augru_fwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(xw, att, Kuh, Krh, Khr, mask, B, L, H, final_h, states, saved); }));
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_augru_bwd(const float* dfinal, const float* att, const float* states,
+                                const float* saved, const float* Kuh, const float* Krh,
+                                const float* Khr, const uint8_t* mask, int64_t B, int32_t L,
+                                int32_t H, float* dxw, float* datt, void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(dfinal && att && states && saved && Kuh && Krh && Khr && mask && dxw && datt,
+               "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_HM_DISPATCH(H, ({ augru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dfinal, att, states, saved, Kuh, Krh, Khr, mask, B, L, H, dxw, datt); }));
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_dien_attention_fwd(const float* hs, const float* q, const uint8_t* mask,
+                                         int64_t B, int32_t L, int32_t H, float* a, void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && L <= 64 * kAttMaxT && H >= 1 && H <= 64, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(hs && q && mask && a, "null pointer");
+  att_fwd_kernel<<<ceil_div(B, 4), 256, 0, as_stream(stream)>>>(hs, q, mask, B, L, H, a);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_dien_attention_bwd(const float* hs, const float* q, const float* a,
+                                         const float* da, int64_t B, int32_t L, int32_t H,
+                                         float* dhs, float* dq, void* stream) {
+  RS_CHECK_ARG(B >= 0 && L >= 1 && L <= 64 * kAttMaxT && H >= 1 && H <= 64, "bad sizes");
+  if (B == 0) return RS_OK;
+  RS_CHECK_ARG(hs && q && a && da && dhs && dq, "null pointer");
+  att_bwd_kernel<<<ceil_div(B, 4), 256, 0, as_stream(stream)>>>(hs, q, a, da, B, L, H, dhs, dq);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}

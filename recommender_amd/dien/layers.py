@@ -1,0 +1,351 @@
+"""dien/layers.py surface (reference dien/layers.py:1-204) on the MI355X engine.
+
+The three recurrent pieces run in the HIP kernels of csrc/dien.hip (rs_gru_*, rs_augru_*,
+rs_dien_attention_*): the kernels do the sequential part, the input projections of all steps
+and every weight gradient are single GEMMs here. Parameters keep Keras layouts and
+initialisers: GRU kernel [X,3H] glorot, recurrent_kernel [H,3H] orthogonal, bias [2,3H]
+(input row, recurrent row; reset_after=True); AUGRUCell's three Dense layers on [h, x] /
+[x, r·h]; DIENAttention kernel [H, X_target] glorot.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from .. import _lib as L
+from ..nn import Dense
+
+
+def _glorot(shape, device, gen=None):
+    lim = math.sqrt(6.0 / (shape[0] + shape[1]))
+    on = gen.device if gen is not None else device
+    return torch.empty(*shape, device=on).uniform_(-lim, lim, generator=gen).to(device)
+
+
+def _mask_u8(mask, shape, device):
+    if mask is None:
+        return torch.ones(shape, dtype=torch.uint8, device=device)
+    return mask.to(torch.uint8).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------
+class _GRUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, recurrent_kernel, bias, mask_u8):
+        B, T, X = x.shape
+        H = recurrent_kernel.shape[0]
+        xw = torch.addmm(bias[0], x.reshape(-1, X), kernel).view(B, T, 3 * H)
+        out = torch.empty(B, T, H, device=x.device)
+        saved = torch.empty(B, T, 4 * H, device=x.device)
+        rk = recurrent_kernel.contiguous()
+        L.call("rs_gru_fwd", L.ptr(xw), L.ptr(rk), L.ptr(bias[1].contiguous()), L.ptr(mask_u8), B, T,
+               H, L.ptr(out), L.ptr(saved), L.stream_ptr(x.device))
+        ctx.save_for_backward(x, kernel, rk, out, saved, mask_u8)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, kernel, rk, out, saved, mask_u8 = ctx.saved_tensors
+        B, T, X = x.shape
+        H = rk.shape[0]
+        dout = dout.contiguous()
+        dxw = torch.empty(B, T, 3 * H, device=x.device)
+        dinner = torch.empty(B, T, 3 * H, device=x.device)
+        L.call("rs_gru_bwd", L.ptr(dout), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
+               H, L.ptr(dxw), L.ptr(dinner), L.stream_ptr(x.device))
+        dxw2, din2 = dxw.view(-1, 3 * H), dinner.view(-1, 3 * H)
+        hp = torch.cat([torch.zeros(B, 1, H, device=x.device), out[:, :-1]], 1).reshape(-1, H)
+        dx = (dxw2 @ kernel.t()).view(B, T, X) if ctx.needs_input_grad[0] else None
+        dk = x.reshape(-1, X).t() @ dxw2
+        drk = hp.t() @ din2
+        db = torch.stack([dxw2.sum(0), din2.sum(0)])
+        return dx, dk, drk, db, None
+
+
+class GRU(nn.Module):
+    """keras.layers.GRU(units, return_sequences=True) [3p TF 2.2: reset_after=True, sigmoid
+    recurrent activation, tanh activation]; masked steps carry the state."""
+
+    def __init__(self, units, input_dim=None, device=None, generator=None):
+        super().__init__()
+        self.units = units
+        self._device, self._gen = device, generator
+        self.kernel = None
+        if input_dim is not None:
+            self.build(input_dim)
+
+    def build(self, input_dim, device=None):
+        dev = device or self._device or "cuda"
+        H = self.units
+        self.kernel = nn.Parameter(_glorot((input_dim, 3 * H), dev, self._gen))
+        rk = torch.empty(3 * H, H)
+        g = self._gen if (self._gen is not None and self._gen.device.type == "cpu") else None
+        nn.init.orthogonal_(rk, generator=g)
+        self.recurrent_kernel = nn.Parameter(rk.t().contiguous().to(dev))
+        self.bias = nn.Parameter(torch.zeros(2, 3 * H, device=dev))
+
+    def forward(self, x, mask=None):
+        if self.kernel is None:
+            self.build(x.shape[-1], x.device)
+        L.require_device(x, "GRU input")
+        m = _mask_u8(mask, x.shape[:2], x.device)
+        return _GRUFn.apply(x.contiguous(), self.kernel, self.recurrent_kernel, self.bias, m)
+
+
+# ---------------------------------------------------------------------------------------------
+class _AUGRUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, att, ku, bu, kr, br, kh, bh, mask_u8):
+        B, T, X = x.shape
+        H = ku.shape[1]
+        # x parts: update/reset kernels take [h, x] (rows H: are x), candidate takes [x, r·h]
+        wx = torch.cat([ku[H:], kr[H:], kh[:X]], dim=1)                 # [X, 3H]
+        bx = torch.cat([bu, br, bh])
+        xw = torch.addmm(bx, x.reshape(-1, X), wx).view(B, T, 3 * H)
+        kuh, krh, khr = ku[:H].contiguous(), kr[:H].contiguous(), kh[X:].contiguous()
+        final = torch.empty(B, H, device=x.device)
+        states = torch.empty(B, T, H, device=x.device)
+        saved = torch.empty(B, T, 4 * H, device=x.device)
+        a = att.reshape(B, T).contiguous()
+        L.call("rs_augru_fwd", L.ptr(xw), L.ptr(a), L.ptr(kuh), L.ptr(krh), L.ptr(khr),
+               L.ptr(mask_u8), B, T, H, L.ptr(final), L.ptr(states), L.ptr(saved),
+               L.stream_ptr(x.device))
+        ctx.save_for_backward(x, a, wx, kuh, krh, khr, states, saved, mask_u8)
+        ctx.att_shape = att.shape
+        return final
+
+    @staticmethod
+    def backward(ctx, dfinal):
+        x, a, wx, kuh, krh, khr, states, saved, mask_u8 = ctx.saved_tensors
+        B, T, X = x.shape
+        H = kuh.shape[0]
+        dxw = torch.empty(B, T, 3 * H, device=x.device)
+        datt = torch.empty(B, T, device=x.device)
+        L.call("rs_augru_bwd", L.ptr(dfinal.contiguous()), L.ptr(a), L.ptr(states), L.ptr(saved),
+               L.ptr(kuh), L.ptr(krh), L.ptr(khr), L.ptr(mask_u8), B, T, H, L.ptr(dxw),
+               L.ptr(datt), L.stream_ptr(x.device))
+        d2 = dxw.view(-1, 3 * H)
+        dpu, dpr, dph = d2[:, :H], d2[:, H:2 * H], d2[:, 2 * H:]
+        x2 = x.reshape(-1, X)
+        hp = torch.cat([torch.zeros(B, 1, H, device=x.device), states[:, :-1]], 1).reshape(-1, H)
+        rh = saved[:, :, 3 * H:].reshape(-1, H)
+        dwx = x2.t() @ d2                                                 # [X, 3H]
+        dku = torch.cat([hp.t() @ dpu, dwx[:, :H]], 0)
+        dkr = torch.cat([hp.t() @ dpr, dwx[:, H:2 * H]], 0)
+        dkh = torch.cat([dwx[:, 2 * H:], rh.t() @ dph], 0)
+        dx = (d2 @ wx.t()).view(B, T, X) if ctx.needs_input_grad[0] else None
+        return (dx, datt.view(ctx.att_shape), dku, dpu.sum(0), dkr, dpr.sum(0), dkh, dph.sum(0),
+                None)
+
+
+class AUGRUCell(nn.Module):
+    """dien/layers.py:161-188: update/reset gates Dense(H, sigmoid) on [h_prev, x], candidate
+    Dense(H, tanh) on [x, r·h_prev]; u ← a·u; h = u·hh + (1-u)·h_prev."""
+
+    def __init__(self, units, input_dim, device=None, generator=None):
+        super().__init__()
+        self.units = units
+        H, X = units, input_dim
+        self.update_gate = Dense(H, "sigmoid", in_features=H + X, device=device, generator=generator)
+        self.reset_gate = Dense(H, "sigmoid", in_features=H + X, device=device, generator=generator)
+        self.hidden_layer = Dense(H, "tanh", in_features=X + H, device=device, generator=generator)
+
+    @property
+    def state_size(self):
+        return self.units
+
+
+class InterestEvolve(nn.Module):
+    """dien/layers.py:191-204: keras.layers.RNN(AUGRUCell) over [history_state, score], masked
+    steps carry the state, returns the last state [B, H]."""
+
+    def __init__(self, gru_units, input_dim=None, device=None, generator=None):
+        super().__init__()
+        self.gru_units = gru_units
+        self.augru = AUGRUCell(gru_units, input_dim if input_dim is not None else gru_units, device,
+                               generator)
+
+    def forward(self, inputs, training=False, mask=None):
+        history_state, attention_score = inputs
+        c = self.augru
+        m = _mask_u8(mask, history_state.shape[:2], history_state.device)
+        return _AUGRUFn.apply(history_state.contiguous(), attention_score, c.update_gate.kernel,
+                              c.update_gate.bias, c.reset_gate.kernel, c.reset_gate.bias,
+                              c.hidden_layer.kernel, c.hidden_layer.bias, m)
+
+
+# ---------------------------------------------------------------------------------------------
+class _AttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, target, hidden, kernel, mask_u8):
+        B, T, H = hidden.shape
+        t2 = target.reshape(B, -1)
+        q = (t2 @ kernel.t()).contiguous()                          # q = K·t  [B, H]
+        a = torch.empty(B, T, device=hidden.device)
+        hs = hidden.contiguous()
+        L.call("rs_dien_attention_fwd", L.ptr(hs), L.ptr(q), L.ptr(mask_u8), B, T, H, L.ptr(a),
+               L.stream_ptr(hidden.device))
+        ctx.save_for_backward(t2, hs, kernel, q, a)
+        ctx.tshape = target.shape
+        return a.unsqueeze(-1)
+
+    @staticmethod
+    def backward(ctx, da):
+        t2, hs, kernel, q, a = ctx.saved_tensors
+        B, T, H = hs.shape
+        dhs = torch.empty_like(hs)
+        dq = torch.empty(B, H, device=hs.device)
+        L.call("rs_dien_attention_bwd", L.ptr(hs), L.ptr(q), L.ptr(a),
+               L.ptr(da.reshape(B, T).contiguous()), B, T, H, L.ptr(dhs), L.ptr(dq),
+               L.stream_ptr(hs.device))
+        dk = dq.t() @ t2                                              # [H, Xt]
+        dt = (dq @ kernel).view(ctx.tshape)
+        return dt, dhs, dk, None
+
+
+class DIENAttention(nn.Module):
+    """dien/layers.py:136-158: score = softmax_L((H·K)·tᵀ + (1-mask)·(-1e9)) → [B, L, 1]."""
+
+    def __init__(self, hidden_dim=None, target_dim=None, device=None, generator=None):
+        super().__init__()
+        self._device, self._gen = device, generator
+        self.kernel = None
+        if hidden_dim is not None and target_dim is not None:
+            self.build(hidden_dim, target_dim)
+
+    def build(self, hidden_dim, target_dim, device=None):
+        self.kernel = nn.Parameter(_glorot((hidden_dim, target_dim), device or self._device or "cuda", self._gen))
+
+    def forward(self, inputs, training=False, mask=None):
+        target, hidden_state = inputs
+        if self.kernel is None:
+            self.build(hidden_state.shape[-1], target.shape[-1], hidden_state.device)
+        m = _mask_u8(mask, hidden_state.shape[:2], hidden_state.device)
+        return _AttentionFn.apply(target, hidden_state, self.kernel, m)
+
+
+# ---------------------------------------------------------------------------------------------
+class BatchNormalization(nn.Module):
+    """keras.layers.BatchNormalization [3p]: momentum 0.99, epsilon 1e-3; training → batch
+    statistics + moving-average update; inference → moving statistics."""
+
+    def __init__(self, dim, momentum=0.99, epsilon=1e-3, device=None):
+        super().__init__()
+        self.momentum, self.epsilon = momentum, epsilon
+        self.gamma = nn.Parameter(torch.ones(dim, device=device))
+        self.beta = nn.Parameter(torch.zeros(dim, device=device))
+        self.register_buffer("moving_mean", torch.zeros(dim, device=device))
+        self.register_buffer("moving_variance", torch.ones(dim, device=device))
+
+    def forward(self, x, training=False):
+        if training:
+            mean = x.mean(0)
+            var = x.var(0, unbiased=False)
+            with torch.no_grad():
+                self.moving_mean.mul_(self.momentum).add_(mean.detach() * (1 - self.momentum))
+                self.moving_variance.mul_(self.momentum).add_(var.detach() * (1 - self.momentum))
+        else:
+            mean, var = self.moving_mean, self.moving_variance
+        return (x - mean) * torch.rsqrt(var + self.epsilon) * self.gamma + self.beta
+
+
+def compute_his_average(his_embedding, mask):
+    """dien/layers.py:5-17: masked mean over the history (0/0 → NaN for an empty history)."""
+    m = mask.unsqueeze(-1).to(his_embedding.dtype)
+    return (his_embedding * m).sum(1) / m.sum(1)
+
+
+class MLP(nn.Module):
+    """dien/layers.py:20-31: BatchNormalization on the input, relu hidden layers."""
+
+    def __init__(self, units, last_activation, in_features, device=None, generator=None):
+        super().__init__()
+        self.bn = BatchNormalization(in_features, device=device)
+        layers, fin = [], in_features
+        for u in units[:-1]:
+            layers.append(Dense(u, "relu", in_features=fin, device=device, generator=generator))
+            fin = u
+        layers.append(Dense(units[-1], last_activation, in_features=fin, device=device, generator=generator))
+        self.mlp = nn.ModuleList(layers)
+
+    def forward(self, inputs, training=False):
+        x = self.bn(inputs, training=training)
+        for layer in self.mlp:
+            x = layer(x)
+        return x
+
+
+class LocalActivationUnit(nn.Module):
+    """dien/layers.py:34-59 (DIN): unnormalised weights Dense(80σ)→Dense(40σ)→Dense(1) on
+    [t, h, t-h, t·h], masked, then weightsᵀ·H."""
+
+    def __init__(self, dim, device=None, generator=None):
+        super().__init__()
+        self.layer_1 = Dense(80, "sigmoid", in_features=4 * dim, device=device, generator=generator)
+        self.layer_2 = Dense(40, "sigmoid", in_features=80, device=device, generator=generator)
+        self.layer_3 = Dense(1, None, in_features=40, device=device, generator=generator)
+
+    def forward(self, inputs, mask=None):
+        target, history = inputs
+        B, T, D = history.shape
+        t = target.expand(B, T, D)
+        c = torch.cat([t, history, t - history, t * history], -1).reshape(B * T, 4 * D)
+        w = self.layer_3(self.layer_2(self.layer_1(c))).view(B, T, 1)
+        w = w * mask.unsqueeze(-1).to(w.dtype)
+        return (w.transpose(1, 2) @ history).squeeze(1)
+
+
+class AuxiliaryNet(nn.Module):
+    """dien/layers.py:62-73: Dense(80σ) → Dense(40σ) → Dense(1)."""
+
+    def __init__(self, mlp_units, in_features, device=None, generator=None):
+        super().__init__()
+        layers, fin = [], in_features
+        for u in mlp_units[:-1]:
+            layers.append(Dense(u, "sigmoid", in_features=fin, device=device, generator=generator))
+            fin = u
+        layers.append(Dense(mlp_units[-1], None, in_features=fin, device=device, generator=generator))
+        self.layers = nn.ModuleList(layers)
+
+    def forward(self, inputs, training=False, **kwargs):
+        shp = inputs.shape
+        x = inputs.reshape(-1, shp[-1])
+        for layer in self.layers:
+            x = layer(x)
+        return x.view(*shp[:-1], -1)
+
+
+def _sigmoid_ce(labels, logits):
+    # tf.nn.sigmoid_cross_entropy_with_logits: max(x,0) - x*z + log(1 + exp(-|x|))
+    return torch.clamp(logits, min=0) - logits * labels + torch.log1p(torch.exp(-logits.abs()))
+
+
+class InterestExtract(nn.Module):
+    """dien/layers.py:76-133: GRU over the positive history + auxiliary loss on
+    (h_t, e_{t+1}) for positive / negative next items, masked mean over 2·Σmask[:,1:]."""
+
+    def __init__(self, gru_units, input_dim, device=None, generator=None):
+        super().__init__()
+        self.gru = GRU(gru_units, input_dim, device, generator)
+        self.auxiliary_net = AuxiliaryNet([80, 40, 1], gru_units + input_dim, device, generator)
+
+    def compute_auxiliary_loss(self, inputs, training=False, mask=None):
+        hidden_state, pos_his, neg_his = inputs
+        h = hidden_state[:, :-1, :]
+        m = mask[:, 1:].to(h.dtype)
+        both = torch.cat([torch.cat([h, pos_his[:, 1:, :]], -1),
+                          torch.cat([h, neg_his[:, 1:, :]], -1)], 0)     # one pass for pos + neg
+        logits = self.auxiliary_net(both).squeeze(-1)
+        B = h.shape[0]
+        pos_loss = _sigmoid_ce(torch.ones_like(logits[:B]), logits[:B]) * m
+        neg_loss = _sigmoid_ce(torch.zeros_like(logits[B:]), logits[B:]) * m
+        s = torch.cat([pos_loss, neg_loss], -1).sum(-1)
+        return s / (m.sum(-1) * 2.0)
+
+    def forward(self, inputs, training=False, mask=None):
+        pos_history, neg_history = inputs
+        hidden_state = self.gru(pos_history, mask=mask)
+        aux = self.compute_auxiliary_loss((hidden_state, pos_history, neg_history), training, mask)
+        return hidden_state, aux

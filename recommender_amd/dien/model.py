@@ -1,0 +1,88 @@
+"""dien/model.py surface (reference dien/model.py:7-80): item / category tables with
+mask_zero=True (dien/model.py:11-12), flat embeddings item‖cat (:14-19), BASE (masked history
+mean), DIN (local activation), DIEN (GRU + aux loss, attention, AUGRU; returns
+(prob [B,1], aux [B]); its MLP runs BatchNormalization in inference mode because the
+reference calls self.mlp(embedding) without `training` (dien/model.py:79))."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..embedding import Embedding
+from .layers import (MLP, DIENAttention, InterestEvolve, InterestExtract, LocalActivationUnit,
+                     compute_his_average)
+
+
+class BaseModel(nn.Module):
+    def __init__(self, item_vocab_size, item_embedding_size, cat_vocab_size, cat_embedding_size,
+                 mlp_units, device=None, generator=None):
+        super().__init__()
+        D = item_embedding_size + cat_embedding_size
+        self.embedding_dim = D
+        self.mlp = MLP(mlp_units, "sigmoid", 2 * D, device, generator)
+        self.item_embedding = Embedding(item_vocab_size, item_embedding_size, mask_zero=True,
+                                        device=device, generator=generator)
+        self.cat_embedding = Embedding(cat_vocab_size, cat_embedding_size, mask_zero=True,
+                                       device=device, generator=generator)
+
+    def compute_flat_embedding(self, inputs):
+        item, cat = inputs
+        return torch.cat([self.item_embedding(item), self.cat_embedding(cat)], dim=-1)
+
+    def compute_prob(self, inputs):
+        return self.forward(inputs)
+
+    def forward(self, inputs, training=False, mask=None):
+        mask = self.item_embedding.compute_mask(inputs["pos_his_item"])
+        target = self.compute_flat_embedding((inputs["target_item"], inputs["target_cat"])).squeeze(1)
+        his = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]))
+        rep = compute_his_average(his, mask)
+        return self.mlp(torch.cat([target, rep], -1), training=training)
+
+    call = forward
+
+
+class DIN(BaseModel):
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.local_activation_unit = LocalActivationUnit(self.embedding_dim, kwargs.get("device"),
+                                                         kwargs.get("generator"))
+
+    def forward(self, inputs, training=False, mask=None):
+        mask = self.item_embedding.compute_mask(inputs["pos_his_item"])
+        target = self.compute_flat_embedding((inputs["target_item"], inputs["target_cat"]))
+        his = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]))
+        rep = self.local_activation_unit((target, his), mask=mask)
+        return self.mlp(torch.cat([target.squeeze(1), rep], -1), training=training)
+
+    call = forward
+
+
+class DIEN(BaseModel):
+    def __init__(self, interest_extract_gru_units, interest_evolve_gru_units, **kwargs):
+        super().__init__(**kwargs)
+        dev, gen = kwargs.get("device"), kwargs.get("generator")
+        D = self.embedding_dim
+        self.interest_extract_layer = InterestExtract(interest_extract_gru_units, D, dev, gen)
+        self.attention = DIENAttention(interest_extract_gru_units, D, dev, gen)
+        self.interest_evolve = InterestEvolve(interest_evolve_gru_units, interest_extract_gru_units, dev, gen)
+        if interest_evolve_gru_units != D:
+            raise ValueError("the MLP input is [target (D), evolved interest]; the reference uses "
+                             "36 units with 18+18 embeddings")
+
+    def compute_prob(self, inputs):
+        prob, _ = self.forward(inputs)
+        return prob
+
+    def forward(self, inputs, training=False, mask=None):
+        mask = self.item_embedding.compute_mask(inputs["pos_his_item"])
+        target = self.compute_flat_embedding((inputs["target_item"], inputs["target_cat"]))
+        pos = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]))
+        neg = self.compute_flat_embedding((inputs["neg_his_item"], inputs["neg_his_cat"]))
+        hidden, aux = self.interest_extract_layer((pos, neg), training, mask)
+        score = self.attention((target, hidden), training, mask)
+        rep = self.interest_evolve((hidden, score), training, mask)
+        prob = self.mlp(torch.cat([target.squeeze(1), rep], -1))  # inference BN (dien/model.py:79)
+        return prob, aux
+
+    call = forward

@@ -1,0 +1,105 @@
+"""dien/train.py counterpart (reference dien/train.py:12-143): BASE / DIN / DIEN on synthetic
+Amazon-shaped sequences. Flags and defaults as the reference (--gpus --gpu_memory_limit
+--model_type --history_max_length --epochs --train_batch_size --test_batch_size --seed) plus
+--item_vocab/--cat_vocab (default 63 001 / 801, Amazon-Electronics-shaped) and
+--steps_per_epoch. train_step_dien (dien/train.py:13-24): loss = mean BCE + mean aux; Keras
+Adam on every parameter (embedding tables: exact Keras Adam with the dense decay)."""
+from __future__ import annotations
+
+import argparse
+import time
+
+import numpy as np
+import torch
+
+from ..functional import binary_crossentropy
+from ..optim import KerasAdam, SparseAdam
+from . import DIEN, DIN, BaseModel
+
+
+def synthetic_batch(rng, batch, hist_len, item_vocab, cat_vocab, negatives=True):
+    """Post-padded / pre-truncated histories (dien/data_loader.py:44,48) of length
+    2 + Geometric(0.1) clipped to hist_len; items U[1, V) with a fixed item→cat map; uniform
+    negative history (dien/data_loader.py:58); labels Bernoulli(0.5)."""
+    item2cat = 1 + (np.arange(item_vocab) * 2654435761 % max(cat_vocab - 1, 1))
+    lens = np.clip(2 + rng.geometric(0.1, batch), 2, hist_len)
+    valid = np.arange(hist_len)[None, :] < lens[:, None]
+    pos = np.where(valid, rng.integers(1, item_vocab, (batch, hist_len)), 0).astype(np.int32)
+    feats = {
+        "target_item": rng.integers(1, item_vocab, (batch, 1)).astype(np.int32),
+        "pos_his_item": pos,
+        "pos_his_cat": np.where(valid, item2cat[pos], 0).astype(np.int32),
+    }
+    feats["target_cat"] = item2cat[feats["target_item"]].astype(np.int32)
+    if negatives:
+        neg = rng.integers(1, item_vocab, (batch, hist_len)).astype(np.int32)
+        feats["neg_his_item"] = neg
+        feats["neg_his_cat"] = item2cat[neg].astype(np.int32)
+    label = (rng.random((batch, 1)) < 0.5).astype(np.float32)
+    return feats, label
+
+
+class DIENStep:
+    def __init__(self, model, lr=1e-3):
+        self.model = model
+        tables = [model.item_embedding, model.cat_embedding]
+        dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
+        self.opt_dense = KerasAdam(dense, lr=lr)
+        self.opt_sparse = SparseAdam(tables, lr=lr, mode="keras")
+        self.is_dien = isinstance(model, DIEN)
+
+    def __call__(self, feats, label):
+        self.opt_dense.zero_grad(set_to_none=True)
+        if self.is_dien:
+            pred, aux = self.model(feats, training=True)
+            bce = binary_crossentropy(label, pred, reduction="mean")
+            aux = aux.mean()
+            total = bce + aux
+        else:
+            pred = self.model(feats, training=True)
+            total = aux = binary_crossentropy(label, pred, reduction="mean")
+        total.backward()
+        self.opt_dense.step()
+        self.opt_sparse.step()
+        return total, aux
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=str, default="0")
+    ap.add_argument("--gpu_memory_limit", type=int, default=4096)
+    ap.add_argument("--model_type", type=str, default="BASE")
+    ap.add_argument("--history_max_length", type=int, default=100)
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--train_batch_size", type=int, default=128)
+    ap.add_argument("--test_batch_size", type=int, default=2048)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--item_vocab", type=int, default=63001)
+    ap.add_argument("--cat_vocab", type=int, default=801)
+    ap.add_argument("--steps_per_epoch", type=int, default=50)
+    args = ap.parse_args(argv)
+    torch.manual_seed(args.seed)
+    kw = dict(item_vocab_size=args.item_vocab, item_embedding_size=18, cat_vocab_size=args.cat_vocab,
+              cat_embedding_size=18, mlp_units=[200, 80, 1], device="cuda")
+    if args.model_type == "DIEN":
+        model = DIEN(36, 36, **kw)
+    elif args.model_type == "DIN":
+        model = DIN(**kw)
+    else:
+        model = BaseModel(**kw)
+    step = DIENStep(model)
+    rng = np.random.default_rng(args.seed)
+    for epoch in range(1, args.epochs + 1):
+        t0, tot = time.time(), 0.0
+        for _ in range(args.steps_per_epoch):
+            f, lab = synthetic_batch(rng, args.train_batch_size, args.history_max_length,
+                                     args.item_vocab, args.cat_vocab, args.model_type == "DIEN")
+            feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
+            tot += float(step(feats, torch.from_numpy(lab).cuda())[0])
+        torch.cuda.synchronize()
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} "
+              f"{args.steps_per_epoch * args.train_batch_size / (time.time() - t0):.0f} ex/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""esmm/train.py counterpart (reference esmm/train.py:153-255): BASE / ESMM / MMOE on
+synthetic Ali-CCP-shaped data through the MI355X engine. Same flags and defaults as the
+reference (--gpus --gpu_memory_limit --epochs --train_batch_size --test_batch_size
+--auc_num_thresholds --train_ctr_tfrecord --model_type --test_steps --seed) plus
+--rows (scale the 18 tables to this many rows, e.g. 40000000 for SURVEY cfg4) and
+--steps_per_epoch. Multi-task loss: mean BCE over [ctr, ctcvr] (esmm/train.py:100-102);
+Keras Adam (esmm/train.py:104,125) — dense KerasAdam + sparse Keras-exact Adam on the slab."""
+from __future__ import annotations
+
+import argparse
+import time
+
+import numpy as np
+import torch
+
+from ..functional import binary_crossentropy
+from ..optim import KerasAdam, SparseAdam, SparseSGD
+from ..synthetic import aliccp_batch, scaled_vocab
+from . import ESMM, FEAT_VOCAB, MMOE, BaseModel
+
+
+def build(model_type, feat_vocab, embedding_size=18, device="cuda", generator=None, sharded_comm=None):
+    mlp_units = [360, 200, 80, 1]  # esmm/train.py:217
+    if model_type == "ESMM":
+        return ESMM(mlp_units, feat_vocab, embedding_size, device, generator, sharded_comm)
+    if model_type == "MMOE":  # esmm/train.py:245-253
+        return MMOE(2, 8, [200, 80], [40, 1], feat_vocab, embedding_size, device, generator, sharded_comm)
+    if model_type == "BASE":
+        return BaseModel(mlp_units, "sigmoid", feat_vocab, embedding_size, device, generator, sharded_comm)
+    raise ValueError(model_type)
+
+
+class MultiTaskStep:
+    """train_step of esmm/train.py:97-106: y_pred [B,2], mean BCE, Adam."""
+
+    def __init__(self, model, optimizer="keras_adam", lr=1e-3):
+        self.model = model
+        dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
+        slab = model.embedding_layer.slab
+        table = getattr(slab, "shard", slab)
+        if optimizer == "sgd":
+            self.opt_dense = torch.optim.SGD(dense, lr=lr)
+            self.opt_sparse = SparseSGD([table], lr=lr)
+        else:
+            self.opt_dense = KerasAdam(dense, lr=lr)
+            self.opt_sparse = SparseAdam([table], lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy")
+        self.sharded = slab is not table
+        if self.sharded:
+            slab.set_optimizer(self.opt_sparse)
+
+    def __call__(self, feats, label):
+        self.opt_dense.zero_grad(set_to_none=True)
+        y = self.model(feats)
+        loss = binary_crossentropy(label, y, reduction="mean")
+        loss.backward()
+        self.opt_dense.step()
+        if self.sharded:
+            self.model.embedding_layer.slab.join()
+            self.opt_sparse.iterations += 1
+        else:
+            self.opt_sparse.step()
+        return loss
+
+
+def train(argv=None):
+    ap = argparse.ArgumentParser(description="ESMM model train config")
+    ap.add_argument("--gpus", type=str, default="0")
+    ap.add_argument("--gpu_memory_limit", type=int, default=4096)
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--train_batch_size", type=int, default=512)
+    ap.add_argument("--test_batch_size", type=int, default=2048)
+    ap.add_argument("--auc_num_thresholds", type=int, default=10000)
+    ap.add_argument("--train_ctr_tfrecord", type=str, default="(synthetic)")
+    ap.add_argument("--model_type", type=str, default="MMOE")
+    ap.add_argument("--test_steps", type=int, default=3000)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--steps_per_epoch", type=int, default=50)
+    ap.add_argument("--optimizer", default="keras_adam", choices=["keras_adam", "lazy_adam", "sgd"])
+    args = ap.parse_args(argv)
+    torch.manual_seed(args.seed)
+    vocab = scaled_vocab(FEAT_VOCAB, args.rows) if args.rows else dict(FEAT_VOCAB)
+    model = build(args.model_type, vocab)
+    step = MultiTaskStep(model, args.optimizer)
+    rng = np.random.default_rng(args.seed)
+    for epoch in range(1, args.epochs + 1):
+        t0, tot = time.time(), 0.0
+        for _ in range(args.steps_per_epoch):
+            f, lab = aliccp_batch(rng, args.train_batch_size, vocab)
+            feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
+            tot += float(step(feats, torch.from_numpy(lab).cuda()))
+        torch.cuda.synchronize()
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.5f} "
+              f"{args.steps_per_epoch * args.train_batch_size / (time.time() - t0):.0f} ex/s")
+
+
+if __name__ == "__main__":
+    train()

@@ -151,8 +151,13 @@ class Dense(nn.Module):
         super().__init__()
         self.units = int(units)
         self.activation = get_activation(activation)
-        self.act_code = _ACT_CODE.get(activation, 0) if isinstance(activation, (str, type(None))) else (
-            1 if activation is torch.relu else 2 if activation is torch.sigmoid else -1)
+        # fused-kernel activation code: 0 linear, 1 relu, 2 sigmoid, -1 other (plain torch path)
+        if activation is None or activation == "linear":
+            self.act_code = 0
+        elif isinstance(activation, str):
+            self.act_code = _ACT_CODE.get(activation, -1)
+        else:
+            self.act_code = 1 if activation is torch.relu else 2 if activation is torch.sigmoid else -1
         self.use_bias = use_bias
         self._device = device
         self._generator = generator

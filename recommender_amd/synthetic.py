@@ -61,3 +61,26 @@ def criteo_batch(rng: np.random.Generator, batch: int, cards, alpha: float = 1.0
     dense = np.log1p(rng.geometric(0.01, size=(batch, num_int_fea)).astype(np.float32))
     label = (rng.random(batch) < 0.256).astype(np.float32)
     return cat, dense.astype(np.float32), label
+
+
+def scaled_vocab(vocab: dict, total_rows: int) -> dict:
+    """Scale a per-feature vocabulary to `total_rows` rows keeping the ratios (SURVEY §8d cfg4:
+    the esmm/train.py:197-215 ratios scaled to 40M rows); every feature keeps >= its original
+    size when that is smaller than the scale would give."""
+    base = np.array(list(vocab.values()), dtype=np.float64)
+    out = np.maximum(1, np.floor(base * total_rows / base.sum())).astype(np.int64)
+    out[np.argmax(out)] += total_rows - out.sum()
+    return dict(zip(vocab.keys(), out.tolist()))
+
+
+def aliccp_batch(rng: np.random.Generator, batch: int, vocab: dict, alpha: float = 1.05):
+    """Ali-CCP-shaped features {feat: [B, 1] int32 ids in 1..n} (0 = OOV, esmm/
+    process_public_dataset.py:100,110) and labels [B, 2] = [click, purchase] with the dataset's
+    rates (click 3.9%, purchase given click 0.54%; esmm/tfrecord_io.py:27-29)."""
+    feats = {}
+    for f, n in vocab.items():
+        ids = 1 + _spread(bounded_zipf(rng, batch, max(int(n) - 1, 1), alpha), max(int(n) - 1, 1))
+        feats[f] = ids.astype(np.int32).reshape(batch, 1)
+    click = rng.random(batch) < 0.0389
+    buy = click & (rng.random(batch) < 0.0054)
+    return feats, np.stack([click, buy], 1).astype(np.float32)
