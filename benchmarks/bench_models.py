@@ -40,7 +40,7 @@ def run(step_fn, batches, steps, warmup, watch):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien", "mmoe", "esmm", "deepfm"])
+    ap.add_argument("--model", default="dien", choices=["dien", "mmoe", "esmm", "deepfm", "pinsage"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
@@ -79,6 +79,30 @@ def main():
             batches.append(({k: torch.from_numpy(v).to(dev) for k, v in f.items()}, torch.from_numpy(lab).to(dev)))
         watch = ["rs_embedding_fwd", "rs_sort_ids", "rs_embedding_apply"]
         cfg = {"workload": f"{args.model}_aliccp_18x{args.rows}x18", "batch": B, "optimizer": "lazy_adam"}
+    elif args.model == "pinsage":
+        from recommender_amd.pinsage import PinSageModel, PinSageSampler
+        from recommender_amd.pinsage.sampler import item_pairs
+        from recommender_amd.pinsage.train import ML20M, PinSageStep, build_graph
+
+        B = args.batch or 4096
+        g = build_graph(ML20M, 4)
+        m = PinSageModel(g, g.itype, 2, 8, 32, 16)
+        train = PinSageStep(m)
+        smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+        ctr = {"step": 0}
+
+        def step(_):
+            h, p, n = item_pairs(g, B, 4, ctr["step"])
+            ctr["step"] += 1
+            return train(*smp.sample_from_item_pairs(h, p, n))
+
+        batches = [(None,)]
+        watch = ["rs_item_pairs", "rs_pinsage_neighbors", "rs_unique_first", "rs_pinsage_block",
+                 "rs_weighted_mean_agg_fwd", "rs_weighted_mean_agg_bwd",
+                 "rs_frobenius_normalize_fwd", "rs_frobenius_normalize_bwd", "rs_embedding_fwd",
+                 "rs_embedding_apply", "rs_keras_adam_dense_sweep"]
+        cfg = {"workload": "pinsage_ml20m_b4096", "batch": B, "walk": [2, 4, 0, 3],
+               "graph_edges": g.n_edges}
     else:
         from recommender_amd.ctr.train import TrainStep, build_model
         from recommender_amd.synthetic import criteo_batch

@@ -232,6 +232,103 @@ size_t rs_act_bwd_colsum_workspace_size(int64_t B, int32_t N);
 int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N, int32_t act,
                           float* dz, float* db, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * PinSage sampling + aggregation. The graph is the bipartite
+ * item/user CSR in both directions: i2u_indptr [n_items+1] int64, i2u_idx int32 user ids,
+ * u2i_indptr [n_users+1], u2i_idx item ids. Randomness is Philox4x32-10 keyed by `seed`
+ * (64-bit) and a purpose word; counters (subject, walk | layer << 16, step, draw / 4), so
+ * a draw depends only on (seed, step, subject): launch- and shard-invariant. Bounded ints
+ * are (r * n) >> 32. oracle/pinsage.py restates every function bit for bit. */
+
+/* Raw Philox4x32-10 (known-answer tests): out[4i..4i+3] = philox(ctr[4i..4i+3], (k0, k1)). */
+int32_t rs_philox4x32_10(const uint32_t* ctr, int64_t n, uint32_t k0, uint32_t k1,
+                         uint32_t* out, void* stream);
+
+/* dgl.sampling.random_walk(g, seeds, metapath=[item→user, user→item] * n_traversals,
+ * restart_prob) [3p DGL 0.6.1] as used by PinSAGESampler (pinsage/train/data_loader.py:26-27):
+ * num_walks walks per seed; traces [n_seeds*num_walks, 2*n_traversals+1] int32 (row
+ * s*num_walks + j = walk j of seed s), -1 after a dead end; with restart_prob > 0 a trace ends
+ * after a transition whose stop draw falls below restart_prob. Uniform neighbour choice. */
+int32_t rs_metapath_walk(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                         const int64_t* u2i_indptr, const int32_t* u2i_idx, const int32_t* seeds,
+                         int64_t n_seeds, int32_t num_walks, int32_t n_traversals,
+                         float restart_prob, uint64_t seed, uint32_t step, uint32_t layer,
+                         int32_t* traces, void* stream);
+
+/* a-14 item2item_batch_sampler (pinsage/train/data_loader.py:6-18): for pairs
+ * i = pair_base .. pair_base+batch-1: head, neg ~ U[0, n_items), pos = item after one
+ * item→user→item walk from head; pairs whose walk dead-ends are dropped (mask pos != -1,
+ * :15-18), order kept. heads/pos_tails/neg_tails [batch] (first *n_valid written). */
+size_t rs_item_pairs_workspace_size(int32_t batch);
+int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                      const int64_t* u2i_indptr, const int32_t* u2i_idx, int32_t n_items,
+                      int64_t pair_base, int32_t batch, uint64_t seed, uint32_t step,
+                      int32_t* heads, int32_t* pos_tails, int32_t* neg_tails, int32_t* n_valid,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+/* Set of (dst, src) item pairs for the leak-edge removal of generate_blocks
+ * (pinsage/train/data_loader.py:34-39): table [capacity] uint64, capacity a power of two > n,
+ * filled with 0xFF bytes by the caller before the first build. */
+int32_t rs_pair_set_build(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* table,
+                          int64_t capacity, void* stream);
+
+/* a-15 dgl.sampling.PinSAGESampler(g, item, user, n_traversals, restart_prob, num_walks,
+ * num_neighbors) [3p] (pinsage/train/data_loader.py:26-27) + remove_edges (:34-39): per seed,
+ * num_walks walks of n_traversals item→user→item traversals; every item reached after a
+ * traversal is one visit (self-visits count); the num_neighbors most visited (count desc,
+ * item id asc — DGL's tie order is unspecified) become in-edges with weight = count; then
+ * edges (src, dst=seed) in the exclusion set (excl_capacity 0 = none) are dropped without
+ * back-filling. nbr/cnt [n_seeds, num_neighbors], -1/0 in empty slots.
+ * Limits: num_walks <= 64, n_traversals <= 8. */
+int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                             const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                             const int32_t* seeds, int64_t n_seeds, int32_t num_walks,
+                             int32_t n_traversals, float restart_prob, uint64_t seed,
+                             uint32_t step, uint32_t layer, int32_t num_neighbors,
+                             const uint64_t* excl_table, int64_t excl_capacity, int32_t* nbr,
+                             int32_t* cnt, void* stream);
+
+/* First-appearance unique (dgl.compact_graphs / dgl.to_block node order,
+ * pinsage/train/data_loader.py:40,48): uniq = distinct ids >= 0 in order of first position,
+ * local[i] = index of ids[i] in uniq (-1 for ids < 0; may be NULL). ids >= n_nodes set
+ * RS_ERRBIT_OOB in err_flag (may be NULL) and count as -1. */
+size_t rs_unique_first_workspace_size(int64_t n_nodes, int64_t n);
+int32_t rs_unique_first(const int32_t* ids, int64_t n, int64_t n_nodes, int32_t* uniq,
+                        int32_t* local, int32_t* n_unique, int32_t* err_flag, void* workspace,
+                        size_t ws_bytes, void* stream);
+
+/* dgl.to_block(frontier, dst_nodes) (pinsage/train/data_loader.py:40): from nbr_local
+ * [n_dst, k] (src local ids, -1 = no edge) and cnt: CSR by dst (indptr [n_dst+1], edges in
+ * slot order: edge_src, edge_dst, edge_w = (float)count), *n_edges, and the transpose
+ * t_indptr [n_src+1] / t_edge [n_dst*k capacity] listing each src's edges in edge order. */
+size_t rs_pinsage_block_workspace_size(int64_t n_dst, int32_t k);
+int32_t rs_pinsage_block(const int32_t* nbr_local, const int32_t* cnt, int64_t n_dst, int32_t k,
+                         int64_t n_src, int32_t* indptr, int32_t* edge_src, int32_t* edge_dst,
+                         float* edge_w, int32_t* n_edges, int32_t* t_indptr, int32_t* t_edge,
+                         void* workspace, size_t ws_bytes, void* stream);
+
+/* a-18 Convolve weighted mean-pool (pinsage/train/layers.py:17-24: update_all(u_mul_e, sum),
+ * update_all(copy_e, sum), clip ws >= 1, divide): nv[d] = Σ_e w_e u[src_e] / max(Σ_e w_e, 1)
+ * over d's edges in CSR order; wsum[d] = Σ_e w_e (may be NULL). bwd: grad_u[s] =
+ * Σ_{e of s} w_e / max(wsum[dst_e], 1) · grad_nv[dst_e] (transpose order; every src row
+ * written). */
+int32_t rs_weighted_mean_agg_fwd(const float* u, int64_t n_src, int32_t H, const int32_t* indptr,
+                                 const int32_t* edge_src, const float* edge_w, int64_t n_dst,
+                                 float* nv, float* wsum, void* stream);
+int32_t rs_weighted_mean_agg_bwd(const float* grad_nv, int32_t H, const int32_t* t_indptr,
+                                 const int32_t* t_edge, const int32_t* edge_dst,
+                                 const float* edge_w, const float* wsum, int64_t n_src,
+                                 float* grad_u, void* stream);
+
+/* Global Frobenius normalisation y = x / ||x||_F (one scalar over the whole block,
+ * pinsage/train/layers.py:28-29); norm [1] device. bwd: dx = (dy - y <dy, y>) / norm.
+ * Fixed-partition reductions (deterministic). */
+size_t rs_frobenius_workspace_size(int64_t n);
+int32_t rs_frobenius_normalize_fwd(const float* x, int64_t n, float* y, float* norm,
+                                   void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_frobenius_normalize_bwd(const float* dy, const float* y, const float* norm, int64_t n,
+                                   float* dx, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

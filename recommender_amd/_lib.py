@@ -32,6 +32,7 @@ class AdamParams(C.Structure):
 
 
 _p, _i32, _i64, _sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
+_u32, _u64 = C.c_uint32, C.c_uint64
 _SIGS = {
     "rs_last_error": (C.c_char_p, []),
     "rs_version": (_i32, []),
@@ -67,6 +68,25 @@ _SIGS = {
     "rs_dien_attention_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_act_bwd_colsum_workspace_size": (_sz, [_i64, _i32]),
     "rs_act_bwd_colsum": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
+    "rs_philox4x32_10": (_i32, [_p, _i64, _u32, _u32, _p, _p]),
+    "rs_metapath_walk": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, C.c_float, _u64, _u32,
+                                _u32, _p, _p]),
+    "rs_item_pairs_workspace_size": (_sz, [_i32]),
+    "rs_item_pairs": (_i32, [_p, _p, _p, _p, _i32, _i64, _i32, _u64, _u32, _p, _p, _p, _p, _p,
+                             _sz, _p]),
+    "rs_pair_set_build": (_i32, [_p, _p, _i64, _p, _i64, _p]),
+    "rs_pinsage_neighbors": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, C.c_float, _u64, _u32,
+                                    _u32, _i32, _p, _i64, _p, _p, _p]),
+    "rs_unique_first_workspace_size": (_sz, [_i64, _i64]),
+    "rs_unique_first": (_i32, [_p, _i64, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_pinsage_block_workspace_size": (_sz, [_i64, _i32]),
+    "rs_pinsage_block": (_i32, [_p, _p, _i64, _i32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
+                                _p]),
+    "rs_weighted_mean_agg_fwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _i64, _p, _p, _p]),
+    "rs_weighted_mean_agg_bwd": (_i32, [_p, _i32, _p, _p, _p, _p, _p, _i64, _p, _p]),
+    "rs_frobenius_workspace_size": (_sz, [_i64]),
+    "rs_frobenius_normalize_fwd": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
+    "rs_frobenius_normalize_bwd": (_i32, [_p, _p, _p, _i64, _p, _p, _sz, _p]),
 }
 
 _lib = None

@@ -1,0 +1,151 @@
+"""PinSage layers (pinsage/train/layers.py) on the engine's kernels.
+
+Convolve          :7-30   fc_1 (Dense relu) → rs_weighted_mean_agg (u_mul_e/sum, copy_e/sum,
+                          clip ws >= 1, divide) → concat h_dst → fc_2 (Dense relu) →
+                          rs_frobenius_normalize (one norm over the whole block, :28-29)
+SageNet           :33-46
+FeatureProjector  :49-81  year / genre-as-{0,1}-ids mean / id embeddings (rs_embedding_fwd)
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .. import _lib as L
+from ..embedding import Embedding
+from ..nn import Dense
+from .graph import Block, HeteroGraph
+
+
+class _WeightedMeanAgg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u: torch.Tensor, block: Block):
+        L.require_device(u, "u")
+        u = u.contiguous()
+        n_src, H = u.shape
+        dev = u.device
+        nv = torch.empty(block.n_dst, H, device=dev)
+        wsum = torch.empty(max(block.n_dst, 1), device=dev)
+        L.call("rs_weighted_mean_agg_fwd", L.ptr(u), n_src, H, L.ptr(block.indptr),
+               L.ptr(block.edge_src), L.ptr(block.edge_w), block.n_dst, L.ptr(nv), L.ptr(wsum),
+               L.stream_ptr(dev))
+        ctx.block = block
+        ctx.n_src = n_src
+        ctx.save_for_backward(wsum)
+        return nv
+
+    @staticmethod
+    def backward(ctx, g):
+        (wsum,) = ctx.saved_tensors
+        b = ctx.block
+        g = g.contiguous()
+        H = g.shape[1]
+        gu = torch.empty(ctx.n_src, H, device=g.device)
+        L.call("rs_weighted_mean_agg_bwd", L.ptr(g), H, L.ptr(b.t_indptr), L.ptr(b.t_edge),
+               L.ptr(b.edge_dst), L.ptr(b.edge_w), L.ptr(wsum), ctx.n_src, L.ptr(gu),
+               L.stream_ptr(g.device))
+        return gu, None
+
+
+def weighted_mean_agg(u: torch.Tensor, block: Block) -> torch.Tensor:
+    return _WeightedMeanAgg.apply(u, block)
+
+
+class _FrobeniusNormalize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor):
+        L.require_device(x, "x")
+        x = x.contiguous()
+        n = x.numel()
+        y = torch.empty_like(x)
+        norm = torch.empty(1, device=x.device)
+        ws = torch.empty(L.lib().rs_frobenius_workspace_size(n), dtype=torch.uint8, device=x.device)
+        L.call("rs_frobenius_normalize_fwd", L.ptr(x), n, L.ptr(y), L.ptr(norm), L.ptr(ws),
+               ws.numel(), L.stream_ptr(x.device))
+        ctx.save_for_backward(y, norm)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        y, norm = ctx.saved_tensors
+        g = g.contiguous()
+        n = g.numel()
+        dx = torch.empty_like(g)
+        ws = torch.empty(L.lib().rs_frobenius_workspace_size(n), dtype=torch.uint8, device=g.device)
+        L.call("rs_frobenius_normalize_bwd", L.ptr(g), L.ptr(y), L.ptr(norm), n, L.ptr(dx),
+               L.ptr(ws), ws.numel(), L.stream_ptr(g.device))
+        return dx
+
+
+def frobenius_normalize(x: torch.Tensor) -> torch.Tensor:
+    return _FrobeniusNormalize.apply(x)
+
+
+class Convolve(nn.Module):
+    def __init__(self, conv_hidden_size: int, conv_output_size: int, in_size: int | None = None,
+                 device=None, generator: torch.Generator | None = None):
+        super().__init__()
+        self.fc_1 = Dense(conv_hidden_size, "relu", in_features=in_size, device=device,
+                          generator=generator)
+        self.fc_2 = Dense(conv_output_size, "relu",
+                          in_features=None if in_size is None else conv_hidden_size + in_size,
+                          device=device, generator=generator)
+
+    def forward(self, block: Block, h):
+        h_src, h_dst = h
+        u = self.fc_1(h_src)                              # neighbour transformation
+        nv = weighted_mean_agg(u, block)                  # importance pooling
+        new = self.fc_2(torch.cat([nv, h_dst], dim=-1))   # concat transformation
+        return frobenius_normalize(new)                   # l2 normalisation (global)
+
+
+class SageNet(nn.Module):
+    def __init__(self, num_layers: int, conv_hidden_size: int, conv_output_size: int,
+                 in_size: int | None = None, device=None, generator=None):
+        super().__init__()
+        sizes = [in_size] + [conv_output_size] * num_layers
+        self.convolves = nn.ModuleList(
+            Convolve(conv_hidden_size, conv_output_size, sizes[i], device, generator)
+            for i in range(num_layers))
+        self.fc_1 = Dense(conv_hidden_size, "relu", in_features=conv_output_size, device=device,
+                          generator=generator)
+        self.fc_2 = Dense(conv_output_size, None, in_features=conv_hidden_size, device=device,
+                          generator=generator)
+
+    def forward(self, blocks, h_src):
+        for convolve, block in zip(self.convolves, blocks):
+            h_dst = h_src[: block.num_dst_nodes()]
+            h_src = convolve(block, (h_src, h_dst))
+        return self.fc_2(self.fc_1(h_src))
+
+
+class FeatureProjector(nn.Module):
+    def __init__(self, full_graph: HeteroGraph, itype: str, embedding_size: int, device=None,
+                 generator: torch.Generator | None = None):
+        super().__init__()
+        self.itype = itype
+        self.full_graph = full_graph
+        data = full_graph.nodes[itype].data
+        dev = device or full_graph.device
+        self.year = data["year"].to(dev, torch.int32).contiguous()
+        self.genre = data["genre"].to(dev, torch.int32).contiguous()  # multi-hot → {0,1} ids
+        self.item_id = data["id"].to(dev, torch.int32).contiguous()
+        year_vocab_size = int(self.year.max().item()) + 1
+        genre_vocab_size = self.genre.shape[1]
+        id_vocab_size = full_graph.number_of_nodes(itype)
+        self.year_embedding = Embedding(year_vocab_size, embedding_size, device=dev,
+                                        generator=generator)
+        self.genre_embedding = Embedding(genre_vocab_size, embedding_size, device=dev,
+                                         generator=generator)
+        self.id_embedding = Embedding(id_vocab_size, embedding_size, device=dev,
+                                      generator=generator)
+
+    def tables(self):
+        return [self.year_embedding, self.genre_embedding, self.id_embedding]
+
+    def forward(self, induces_ids: torch.Tensor) -> torch.Tensor:
+        ids = induces_ids.to(torch.int64)
+        year_embedding = self.year_embedding(self.year.index_select(0, ids))
+        genre_embedding = self.genre_embedding(self.genre.index_select(0, ids)).mean(dim=1)
+        id_embedding = self.id_embedding(self.item_id.index_select(0, ids))
+        return torch.cat([year_embedding, genre_embedding, id_embedding], dim=-1)

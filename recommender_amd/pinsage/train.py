@@ -1,0 +1,119 @@
+"""PinSage training loop counterpart of pinsage/train/train.py.
+
+Per step (train.py:79-90): item2item pairs → sample_from_item_pairs (compact + 2 blocks) →
+PinSageModel → margin_loss(delta=1) → backward → Keras Adam on every variable (dense params:
+KerasAdam; the three embedding tables: SparseAdam(mode='keras'), the IndexedSlices path of
+train.py:45-46). Hyper-parameters default to train.py:63-70.
+
+Multi-GPU: pairs are sharded by global pair index (rank r draws pairs
+[r*B, (r+1)*B) of each step), the graph and tables are replicated, and one bucketed
+all-reduce averages the dense grads together with the densified table grads. Graph
+synthetic: MovieLens-shaped (recommender_amd.synthetic.movielens_graph); no dataset is
+reachable offline, and the hit-rate evaluation (train.py:86-90) is out of this path.
+"""
+from __future__ import annotations
+
+import argparse
+import time
+
+import numpy as np
+import torch
+
+from ..optim import KerasAdam, SparseAdam, dedup_grad
+from ..synthetic import ML20M, movielens_graph
+from .graph import HeteroGraph
+from .model import PinSageModel, margin_loss
+from .sampler import PinSageSampler, item_pairs
+
+ML1M = dict(n_users=6_040, n_items=3_706, n_edges=1_000_209)
+
+
+def build_graph(shape: dict, seed: int = 4, device="cuda") -> HeteroGraph:
+    rng = np.random.default_rng(seed)
+    users, items, year, genre = movielens_graph(rng, **shape)
+    return HeteroGraph(users, items, shape["n_users"], shape["n_items"], device=device,
+                       item_data={"year": year, "genre": genre})
+
+
+class PinSageStep:
+    def __init__(self, model: PinSageModel, lr: float = 1e-3, comm=None):
+        self.model = model
+        self.dense = model.dense_parameters()
+        self.opt_dense = KerasAdam(self.dense, lr=lr)
+        self.opt_sparse = SparseAdam(model.tables(), lr=lr, mode="keras")
+        self.comm = comm
+        self.world = comm.world if comm is not None else 1
+
+    def __call__(self, pos_graph, neg_graph, blocks):
+        self.opt_dense.zero_grad(set_to_none=True)
+        pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
+        loss = margin_loss(pos_score, neg_score, delta=1.0)
+        loss.backward()
+        if self.world > 1:
+            self._allreduce_and_apply_tables()
+            self.opt_dense.step()
+        else:
+            self.opt_dense.step()
+            self.opt_sparse.step()
+        return loss.detach()
+
+    def _allreduce_and_apply_tables(self):
+        """Densify each table's IndexedSlices grad (deterministic segmented sum), bucket it
+        with the dense grads into one all-reduce, average over ranks, then apply the tables
+        as fully-touched slices (identical to Keras' dense m/v decay for untouched rows)."""
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.dense]
+        tables = self.model.tables()
+        dense_tab = []
+        for t in tables:
+            got = t.take_grad()
+            g = torch.zeros(t.input_dim, t.output_dim, device=t.weight.device)
+            if got is not None:
+                rows, ug = dedup_grad(t, got[0], got[1])
+                g.index_copy_(0, rows, ug)
+            dense_tab.append(g)
+        bucket = grads + dense_tab
+        flat = torch._utils._flatten_dense_tensors(bucket)
+        self.comm.all_reduce_(flat)
+        flat.mul_(1.0 / self.world)
+        out = torch._utils._unflatten_dense_tensors(flat, bucket)
+        for p, g in zip(self.dense, out[: len(self.dense)]):
+            p.grad = g
+        params = self.opt_sparse._params()
+        for t, g in zip(tables, out[len(self.dense):]):
+            ids = torch.arange(t.input_dim, device=g.device, dtype=torch.int32)
+            self.opt_sparse.apply(t, ids, g, params)
+        self.opt_sparse.iterations += 1
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--graph", choices=["ml1m", "ml20m"], default="ml1m")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--train_batch_size", type=int, default=32)
+    ap.add_argument("--seed", type=int, default=4)
+    args = ap.parse_args(argv)
+    num_layers = 2
+    embedding_size = 8
+    conv_hidden_size, conv_output_size = 32, 16
+    random_walk_length, num_random_walks, termination_prob, num_neighbors = 2, 4, 0, 3
+    torch.manual_seed(args.seed)
+    g = build_graph(ML1M if args.graph == "ml1m" else ML20M, args.seed)
+    model = PinSageModel(g, g.itype, num_layers, embedding_size, conv_hidden_size,
+                         conv_output_size)
+    step_fn = PinSageStep(model)
+    sampler = PinSageSampler(g, g.itype, g.utype, num_layers, random_walk_length,
+                             num_random_walks, termination_prob, num_neighbors, seed=args.seed)
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        heads, pos, neg = item_pairs(g, args.train_batch_size, args.seed, step)
+        batch = sampler.sample_from_item_pairs(heads, pos, neg, g.itype)
+        loss = step_fn(*batch)
+        if step % 50 == 0:
+            print(f"step {step} step_loss {float(loss):.4f}")
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{args.steps / dt:.1f} it/s, {args.steps * args.train_batch_size / dt:.0f} pairs/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -84,3 +84,43 @@ def aliccp_batch(rng: np.random.Generator, batch: int, vocab: dict, alpha: float
     click = rng.random(batch) < 0.0389
     buy = click & (rng.random(batch) < 0.0054)
     return feats, np.stack([click, buy], 1).astype(np.float32)
+
+
+# ---- MovieLens-shaped bipartite graph ---------------------------------
+ML20M = dict(n_users=138_493, n_items=26_744, n_edges=20_000_263)
+
+
+def movielens_graph(rng: np.random.Generator, n_users: int, n_items: int, n_edges: int,
+                    min_user_deg: int = 20, n_genres: int = 20, n_years: int = 120):
+    """ML-20M-shaped user–item rating graph: user degrees min_user_deg + Pareto(1.2) tail
+    (ML-20M keeps users with >= 20 ratings), item popularity power law P(rank r) ~ (r+1)^-0.5
+    (top item ≈ 0.3% of ratings, as in ML-20M), each (user, item) pair at most once; item
+    features year id < n_years and a 1–3-hot genre vector [n_items, n_genres] (int8).
+    Returns (users, items) edge arrays sorted user-major, plus year, genre."""
+    budget = n_edges - min_user_deg * n_users
+    raw = rng.pareto(1.2, n_users) + 1.0
+    cap = max(min_user_deg, n_items // 3)
+    pop = (np.arange(n_items, dtype=np.float64) + 1.0) ** -0.5
+    cdf = np.cumsum(rng.permutation(pop))
+    cdf /= cdf[-1]
+    deg = np.minimum(min_user_deg + np.floor(budget * raw / raw.sum()).astype(np.int64), cap)
+    users = np.repeat(np.arange(n_users, dtype=np.int64), deg)
+    items = np.minimum(np.searchsorted(cdf, rng.random(users.size)), n_items - 1)
+    keys = np.unique(users * n_items + items)
+    for _ in range(4):  # top up the edges lost to duplicate (user, item) draws
+        missing = n_edges - keys.size
+        if missing <= 0:
+            break
+        users = rng.choice(n_users, size=int(missing * 1.2) + 16, p=deg / deg.sum())
+        items = np.minimum(np.searchsorted(cdf, rng.random(users.size)), n_items - 1)
+        keys = np.unique(np.concatenate([keys, users * n_items + items]))
+    if keys.size > n_edges:
+        keys = np.sort(rng.choice(keys, n_edges, replace=False))
+    users, items = keys // n_items, keys % n_items
+    year = rng.integers(0, n_years, n_items).astype(np.int64)
+    genre = np.zeros((n_items, n_genres), np.int8)
+    ng = rng.integers(1, 4, n_items)
+    for k in range(3):
+        m = ng > k
+        genre[np.nonzero(m)[0], rng.integers(0, n_genres, int(m.sum()))] = 1
+    return users, items, year, genre

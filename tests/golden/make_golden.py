@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle import embedding as OE  # noqa: E402
 from oracle import interaction as OI  # noqa: E402
+from oracle import pinsage as OP  # noqa: E402
 
 
 def zipf_ids(rng, n, card):
@@ -57,7 +58,28 @@ def main():
     ge = rng.standard_normal(9).astype(np.float32)
     out.update(fm_e=e, fm_out=OI.fm(e), fm_g=ge, fm_ge=OI.fm_bwd(e, ge))
     np.savez_compressed(os.path.join(HERE, "interaction.npz"), **out)
+    pinsage_fixture()
     print("wrote", os.listdir(HERE))
+
+
+def pinsage_fixture():
+    """a-14..a-16: a 40-user / 70-item graph with dead ends; one step of pairs + 2-layer
+    blocks (walk params (2, 4, 0, 3) of pinsage/train/train.py:69) with leak-edge removal."""
+    rng = np.random.default_rng(4)
+    u = rng.integers(0, 36, 300)
+    i = rng.integers(0, 64, 300)
+    key = np.unique(u * 70 + i)
+    users, items = key // 70, key % 70
+    g = OP.BipartiteGraph.from_edges(users, items, 40, 70)
+    seed, step = 4, 2
+    h, p, n = OP.item_pairs(g, 0, 48, seed, step)
+    seeds, pe, ne, blocks = OP.sample_from_item_pairs(g, h, p, n, 2, 4, 2, 0.0, 3, seed, step)
+    out = dict(users=users, items=items, heads=h, pos=p, neg=n, seeds=seeds, pos_src=pe[0],
+               pos_dst=pe[1], neg_dst=ne[1])
+    for li, b in enumerate(blocks):
+        for f in ("src_nodes", "indptr", "edge_src", "edge_dst", "edge_w", "t_indptr", "t_edge"):
+            out[f"b{li}_{f}"] = getattr(b, f)
+    np.savez_compressed(os.path.join(HERE, "pinsage.npz"), **out)
 
 
 if __name__ == "__main__":
