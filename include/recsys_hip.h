@@ -329,6 +329,32 @@ int32_t rs_frobenius_normalize_fwd(const float* x, int64_t n, float* y, float* n
 int32_t rs_frobenius_normalize_bwd(const float* dy, const float* y, const float* norm, int64_t n,
                                    float* dx, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * EGES / GES / DeepWalk (eges/model.py).
+ * Skip-gram logits, fused gather + dot (DeepWalk.call :26-36, GES.call :58-64):
+ * logits[b, j] = out_table[match_ids[b, j]] · hidden[b] ([batch, n_match] ids, id_dtype as
+ * rs_embedding_fwd; OOB ids read zero rows and set RS_ERRBIT_OOB). bwd: grad_rows
+ * [batch*n_match, dim] = g[b, j] * hidden[b] (the output table's IndexedSlices values, position
+ * order) and grad_hidden[b] = Σ_j g[b, j] * out_table[match_ids[b, j]]. */
+int32_t rs_match_logits_fwd(const float* table, int64_t n_rows, int32_t dim,
+                            const void* match_ids, int32_t id_dtype, int32_t n_match,
+                            const float* hidden, int64_t batch, float* logits, int32_t* err_flag,
+                            void* stream);
+int32_t rs_match_logits_bwd(const float* table, int64_t n_rows, int32_t dim,
+                            const void* match_ids, int32_t id_dtype, int32_t n_match,
+                            const float* hidden, const float* grad_logits, int64_t batch,
+                            float* grad_rows, float* grad_hidden, void* stream);
+/* Side-information pooling over side [batch, n_side, dim]: weight_logits [batch, n_side] →
+ * hidden = softmax(weight_logits) · side (EGES.get_hidden :92-102; attn [batch, n_side] saved,
+ * may be NULL) or, with weight_logits NULL, hidden = (Σ_s side_s) / n_side (GES.get_hidden
+ * :74-80). bwd: attn NULL selects the mean mode; grad_weight_logits is the softmax backward.
+ * n_side <= 16. */
+int32_t rs_side_pool_fwd(const float* side, const float* weight_logits, int64_t batch,
+                         int32_t n_side, int32_t dim, float* hidden, float* attn, void* stream);
+int32_t rs_side_pool_bwd(const float* side, const float* attn, const float* grad_hidden,
+                         int64_t batch, int32_t n_side, int32_t dim, float* grad_side,
+                         float* grad_weight_logits, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

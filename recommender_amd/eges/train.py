@@ -1,0 +1,90 @@
+"""Training counterpart of eges/train.py (loop :14-24: sigmoid CE on the 1+num_ns skip-gram
+logits, reduce_mean, Keras Adam on every table — IndexedSlices → SparseAdam(mode='keras')).
+
+Data: synthetic skip-gram batches of the reference's shapes (target [B,1], cat/brand [B,1],
+context [B, 1+num_ns], label [1, 0, .., 0]); the weighted walk + skipgrams + log-uniform
+negative pipeline (eges/data_loader.py:28-62) is SURVEY §8f "next" and not on this path.
+Hyper-parameters from eges/train.py:45-54,75-92 (emb 160, num_ns 5, batch 1024, seed 4)."""
+from __future__ import annotations
+
+import argparse
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..optim import SparseAdam
+from .model import EGES, GES, DeepWalk
+
+
+def log_uniform(rng, n, range_max):
+    """tf.random.log_uniform_candidate_sampler's distribution P(k) = log((k+2)/(k+1)) /
+    log(range_max+1), by inverse CDF (without its uniqueness rejection)."""
+    u = rng.random(n)
+    return np.minimum((np.exp(u * np.log(range_max + 1.0)) - 1.0).astype(np.int64), range_max - 1)
+
+
+def synthetic_batch(rng, batch, n_items, n_cat, n_brand, num_ns=5):
+    target = rng.integers(1, n_items, (batch, 1))
+    pos = rng.integers(1, n_items, (batch, 1))
+    neg = log_uniform(rng, batch * num_ns, n_items).reshape(batch, num_ns)
+    context = np.concatenate([pos, neg], 1)
+    item2cat = (np.arange(n_items) * 2654435761) % n_cat
+    item2brand = (np.arange(n_items) * 40503) % n_brand
+    label = np.zeros((batch, 1 + num_ns), np.float32)
+    label[:, 0] = 1
+    return (target.astype(np.int32), item2cat[target].astype(np.int32),
+            item2brand[target].astype(np.int32), context.astype(np.int32), label)
+
+
+class EGESStep:
+    def __init__(self, model, lr=1e-3):
+        self.model = model
+        self.opt = SparseAdam(model.tables(), lr=lr, mode="keras")
+
+    def __call__(self, inputs, labels):
+        logits = self.model(inputs)
+        loss = F.binary_cross_entropy_with_logits(logits, labels)  # sigmoid CE, reduce_mean
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+
+def build(model_type, n_items, n_cat, n_brand, embedding_size=160, device="cuda", generator=None):
+    if model_type == "BGE":
+        return DeepWalk(n_items, embedding_size, device=device, generator=generator)
+    if model_type == "GES":
+        return GES(n_items, n_cat, n_brand, embedding_size, device=device, generator=generator)
+    if model_type == "EGES":
+        return EGES(n_items, n_cat, n_brand, embedding_size, 3, device=device, generator=generator)
+    raise ValueError(model_type)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model_type", default="BGE", choices=["BGE", "GES", "EGES"])
+    ap.add_argument("--train_batch_size", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--n_items", type=int, default=63001)
+    args = ap.parse_args(argv)
+    rng = np.random.default_rng(args.seed)
+    n_cat, n_brand = 801, 3000
+    model = build(args.model_type, args.n_items, n_cat, n_brand)
+    step = EGESStep(model)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        *inp, lab = synthetic_batch(rng, args.train_batch_size, args.n_items, n_cat, n_brand)
+        inp = [torch.from_numpy(a).cuda() for a in inp]
+        if args.model_type == "BGE":
+            inp = [inp[0], inp[3]]
+        loss = step(tuple(inp), torch.from_numpy(lab).cuda())
+        if s % 50 == 0:
+            print(f"step {s} loss {float(loss):.4f}")
+    torch.cuda.synchronize()
+    print(f"{args.steps * args.train_batch_size / (time.perf_counter() - t0):.0f} examples/s")
+
+
+if __name__ == "__main__":
+    main()
