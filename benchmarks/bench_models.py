@@ -40,7 +40,7 @@ def run(step_fn, batches, steps, warmup, watch):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien", "mmoe", "esmm", "deepfm", "pinsage"])
+    ap.add_argument("--model", default="dien", choices=["dien", "mmoe", "esmm", "deepfm", "pinsage", "eges"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
@@ -103,6 +103,23 @@ def main():
                  "rs_embedding_apply", "rs_keras_adam_dense_sweep"]
         cfg = {"workload": "pinsage_ml20m_b4096", "batch": B, "walk": [2, 4, 0, 3],
                "graph_edges": g.n_edges}
+    elif args.model == "eges":
+        from recommender_amd.eges.train import EGESStep, build, synthetic_batch
+
+        B = args.batch or 1024
+        n_items, n_cat, n_brand = 63001, 801, 3000
+        m = build("EGES", n_items, n_cat, n_brand, 160)
+        train = EGESStep(m)
+        batches = []
+        for _ in range(4):
+            *inp, lab = synthetic_batch(rng, B, n_items, n_cat, n_brand)
+            batches.append((tuple(torch.from_numpy(a).to(dev) for a in inp),
+                            torch.from_numpy(lab).to(dev)))
+        step = train
+        watch = ["rs_embedding_fwd", "rs_side_pool_fwd", "rs_side_pool_bwd", "rs_match_logits_fwd",
+                 "rs_match_logits_bwd", "rs_sort_ids", "rs_embedding_apply",
+                 "rs_keras_adam_dense_sweep"]
+        cfg = {"workload": "eges_b1024_d160_ns5", "batch": B, "items": n_items}
     else:
         from recommender_amd.ctr.train import TrainStep, build_model
         from recommender_amd.synthetic import criteo_batch

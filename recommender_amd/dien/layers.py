@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from .. import _lib as L
-from ..nn import Dense
+from ..nn import Dense, wgrad
 
 
 def _glorot(shape, device, gen=None):
@@ -58,8 +58,8 @@ class _GRUFn(torch.autograd.Function):
         dxw2, din2 = dxw.view(-1, 3 * H), dinner.view(-1, 3 * H)
         hp = torch.cat([torch.zeros(B, 1, H, device=x.device), out[:, :-1]], 1).reshape(-1, H)
         dx = (dxw2 @ kernel.t()).view(B, T, X) if ctx.needs_input_grad[0] else None
-        dk = x.reshape(-1, X).t() @ dxw2
-        drk = hp.t() @ din2
+        dk = wgrad(x.reshape(-1, X), dxw2)
+        drk = wgrad(hp, din2)
         db = torch.stack([dxw2.sum(0), din2.sum(0)])
         return dx, dk, drk, db, None
 
@@ -131,10 +131,11 @@ class _AUGRUFn(torch.autograd.Function):
         x2 = x.reshape(-1, X)
         hp = torch.cat([torch.zeros(B, 1, H, device=x.device), states[:, :-1]], 1).reshape(-1, H)
         rh = saved[:, :, 3 * H:].reshape(-1, H)
-        dwx = x2.t() @ d2                                                 # [X, 3H]
-        dku = torch.cat([hp.t() @ dpu, dwx[:, :H]], 0)
-        dkr = torch.cat([hp.t() @ dpr, dwx[:, H:2 * H]], 0)
-        dkh = torch.cat([dwx[:, 2 * H:], rh.t() @ dph], 0)
+        dwx = wgrad(x2, d2)                                               # [X, 3H]
+        dhur = wgrad(hp, d2[:, :2 * H])                                   # [H, 2H]
+        dku = torch.cat([dhur[:, :H], dwx[:, :H]], 0)
+        dkr = torch.cat([dhur[:, H:], dwx[:, H:2 * H]], 0)
+        dkh = torch.cat([dwx[:, 2 * H:], wgrad(rh, dph)], 0)
         dx = (d2 @ wx.t()).view(B, T, X) if ctx.needs_input_grad[0] else None
         return (dx, datt.view(ctx.att_shape), dku, dpu.sum(0), dkr, dpr.sum(0), dkh, dph.sum(0),
                 None)

@@ -4,13 +4,15 @@ outputs[1] = outputs[0] * outputs[1], output [B, num_tasks].
 
 The experts keep their own parameters (`self.experts[i]`, the reference attribute surface) but
 run as ONE wide GEMM for the first layer (concatenated kernels) and ONE batched GEMM per
-deeper layer instead of num_experts small GEMMs."""
+deeper layer instead of num_experts small GEMMs; their weight gradients are split-K GEMMs
+(recommender_amd.nn.wgrad / bwgrad) — hipBLASLt's K = batch kernels are 10x slower."""
 from __future__ import annotations
 
 import torch
 from torch import nn
 
-from ..nn import Dense
+from ..eges.model import side_pool
+from ..nn import Dense, batched_linear, linear
 from .layers import MLP
 from .tables import FeatureTables
 
@@ -42,19 +44,23 @@ class MMOE(nn.Module):
         l0 = [m[0] for m in layers]
         k0 = torch.cat([l.kernel for l in l0], dim=1)             # [in, E*H0]
         b0 = torch.cat([l.bias for l in l0])
-        h = torch.relu(torch.addmm(b0, x, k0)).view(x.shape[0], E, -1).transpose(0, 1)  # [E,B,H0]
+        h = torch.relu(linear(x, k0, b0)).view(x.shape[0], E, -1).transpose(0, 1)  # [E,B,H0]
+        h = h.contiguous()
         for j in range(1, len(layers[0])):
             k = torch.stack([m[j].kernel for m in layers])           # [E, Hin, Hout]
             b = torch.stack([m[j].bias for m in layers])[:, None, :]
-            h = torch.relu(torch.baddbmm(b, h, k))
+            h = torch.relu(batched_linear(h, k, b))
         return h.transpose(0, 1)                                     # [B, E, H]
 
     def _towers(self, x):
-        ex = self.experts_outputs(x)
+        ex = self.experts_outputs(x).contiguous()                     # [B, E, H]
         outs = []
         for i in range(self.num_tasks):
-            gw = self.gates[i](x).unsqueeze(1)                        # [B, 1, E]
-            w = torch.bmm(gw, ex).squeeze(1)                          # [B, H]
+            # softmax gate (Dense(E, softmax)) · experts, fused: rs_side_pool applies the
+            # softmax to the gate logits and pools the expert rows in one pass (a [1,E]·[E,H]
+            # matmul per example as 65 536 batched GEMMs costs ~1 ms per call)
+            logits = self.gates[i].preactivation(x).unsqueeze(1)      # [B, 1, E]
+            w = side_pool(ex, logits).squeeze(1)                      # [B, H]
             outs.append(self.task_towers[i](w))
         return outs
 

@@ -30,18 +30,93 @@ def get_activation(act):
     return _ACTS[act]
 
 
+def _splitk_plan(K: int, fan_in: int, fan_out: int, batches: int = 1):
+    """(chunks, rows per chunk) for a K-deep weight-gradient GEMM [in, K]·[K, out]: hipBLASLt's
+    single-pass fp32 kernels for K >= 8k run at 7-64 TF/s (tiny-N tiles over a huge K); a
+    batched GEMM over 8-64 K-chunks + a fixed-order sum runs at 90-120 TF/s
+    (tools/probe_gemm.py, MI355X). Partials stay within ~16 MB."""
+    if K < 8192 or fan_in * fan_out > 4_000_000:
+        return 1, K
+    target = max(8, min(64, (16 << 20) // max(1, batches * fan_in * fan_out * 4)))
+    c = 64
+    while c > target or K // c < 1024:
+        c //= 2
+    return (c, K // c) if c >= 2 else (1, K)
+
+
 def _splitk_chunks(batch: int, fan_in: int, fan_out: int) -> int:
-    """Batch split for the K = batch weight-gradient GEMM: hipBLASLt's single-pass fp32 kernels
-    for [in, B]·[B, out] with B = 65 536 run at 7-64 TF/s; a batched GEMM over 16-64 batch
-    chunks followed by a sum runs at 90-120 TF/s (tools/probe_gemm.py, MI355X)."""
-    if batch < 8192 or fan_in * fan_out > 4_000_000:
-        return 1
-    # enough chunks to fill the chip, few enough that the [c, in, out] partials stay ~16 MB
-    target = max(8, min(64, (16 << 20) // max(1, fan_in * fan_out * 4)))
-    for c in (64, 32, 16, 8):
-        if c <= target and batch % c == 0:
-            return c
-    return 1
+    return _splitk_plan(batch, fan_in, fan_out)[0]
+
+
+def wgrad(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """xᵀ·g for x [K, in], g [K, out] with K the batch (split-K, deterministic: fixed chunking,
+    fixed fold order; a K not divisible by the chunk count adds its tail rows last)."""
+    K, fi = x.shape
+    fo = g.shape[1]
+    c, chunk = _splitk_plan(K, fi, fo)
+    if c == 1:
+        return x.t() @ g
+    m = c * chunk
+    out = torch.bmm(x[:m].reshape(c, chunk, fi).transpose(1, 2), g[:m].reshape(c, chunk, fo)).sum(0)
+    if m < K:
+        out += x[m:].t() @ g[m:]
+    return out
+
+
+def bwgrad(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """Batched xᵀ·g: x [E, K, in], g [E, K, out] → [E, in, out], split-K per batch entry."""
+    E, K, fi = x.shape
+    fo = g.shape[2]
+    c, chunk = _splitk_plan(K, fi, fo, E)
+    if c == 1:
+        return torch.bmm(x.transpose(1, 2), g)
+    m = c * chunk
+    out = torch.bmm(x[:, :m].reshape(E * c, chunk, fi).transpose(1, 2),
+                    g[:, :m].reshape(E * c, chunk, fo)).view(E, c, fi, fo).sum(1)
+    if m < K:
+        out += torch.bmm(x[:, m:].transpose(1, 2), g[:, m:])
+    return out
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x·k (+ b); backward with the split-K weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, k, b):
+        ctx.save_for_backward(x, k)
+        ctx.has_b = b is not None
+        return torch.addmm(b, x, k) if b is not None else x @ k
+
+    @staticmethod
+    def backward(ctx, g):
+        x, k = ctx.saved_tensors
+        g = g.contiguous()
+        dx = g @ k.t() if ctx.needs_input_grad[0] else None
+        return dx, wgrad(x, g), (g.sum(0) if ctx.has_b else None)
+
+
+def linear(x: torch.Tensor, k: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    return _LinearFn.apply(x, k, b)
+
+
+class _BatchedLinearFn(torch.autograd.Function):
+    """y[e] = x[e]·k[e] + b[e] for x [E, B, in], k [E, in, out], b [E, 1, out]."""
+
+    @staticmethod
+    def forward(ctx, x, k, b):
+        ctx.save_for_backward(x, k)
+        return torch.baddbmm(b, x, k)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, k = ctx.saved_tensors
+        g = g.contiguous()
+        dx = torch.bmm(g, k.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        return dx, bwgrad(x, g), g.sum(1, keepdim=True)
+
+
+def batched_linear(x, k, b):
+    return _BatchedLinearFn.apply(x, k, b)
 
 
 _ACT_CODE = {"relu": 1, "sigmoid": 2}
@@ -86,11 +161,11 @@ class _DenseFn(torch.autograd.Function):
     (on the overlapped weight-grad stream when one is active)."""
 
     @staticmethod
-    def forward(ctx, x, handle, layer, rows):
+    def forward(ctx, x, handle, layer, rows, act=None):
         k = layer.kernel if rows is None else layer.kernel.index_select(0, rows)
         b = layer.bias
         z = torch.addmm(b, x, k) if b is not None else x @ k
-        act = layer.act_code
+        act = layer.act_code if act is None else act
         if act == 1:
             y = torch.relu_(z)
         elif act == 2:
@@ -126,11 +201,7 @@ class _DenseFn(torch.autograd.Function):
         if side is not None:
             side.wait_stream(main)
         with torch.cuda.stream(side if side is not None else main):
-            c = _splitk_chunks(B, fi, fo)
-            if c > 1:
-                dk = torch.bmm(x.view(c, B // c, fi).transpose(1, 2), dz.view(c, B // c, fo)).sum(0)
-            else:
-                dk = x.t() @ dz
+            dk = wgrad(x, dz)
             if ctx.rows is not None:
                 full = torch.zeros_like(layer.kernel)
                 full.index_copy_(0, ctx.rows, dk)
@@ -142,7 +213,7 @@ class _DenseFn(torch.autograd.Function):
             for t in (x, dz, db):
                 if t is not None:
                     t.record_stream(side)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 class Dense(nn.Module):
@@ -179,13 +250,27 @@ class Dense(nn.Module):
         the other rows get an exactly-zero gradient)."""
         if self.kernel is None:
             self.build(x.shape[-1], x.device)
-        if x.dim() == 2 and x.is_cuda and self.act_code >= 0 and torch.is_grad_enabled():
-            return _DenseFn.apply(x, self._handle(), self, rows)
+        if x.dim() == 2 and x.is_cuda and torch.is_grad_enabled():
+            if self.act_code >= 0:
+                return _DenseFn.apply(x, self._handle(), self, rows)
+            # other activations (softmax, tanh, ...): fused linear + bias grad, then torch
+            z = _DenseFn.apply(x, self._handle(), self, rows, 0)
+            return self.activation(z) if self.activation is not None else z
         k = self.kernel if rows is None else self.kernel.index_select(0, rows)
         y = torch.matmul(x, k)
         if self.bias is not None:
             y = y + self.bias
         return self.activation(y) if self.activation is not None else y
+
+    def preactivation(self, x):
+        """x·kernel + bias without the activation (for callers that fuse it, e.g. MMOE's gate
+        softmax inside rs_side_pool)."""
+        if self.kernel is None:
+            self.build(x.shape[-1], x.device)
+        if x.dim() == 2 and x.is_cuda and torch.is_grad_enabled():
+            return _DenseFn.apply(x, self._handle(), self, None, 0)
+        y = torch.matmul(x, self.kernel)
+        return y + self.bias if self.bias is not None else y
 
     def _handle(self):
         # a differentiable input so the Function is recorded whenever the params need grad

@@ -236,8 +236,9 @@ def test_frobenius_normalize(shape):
     y2 = x2 / torch.norm(x2)
     y2.backward(g)
     assert_close_rel(y.detach().cpu(), y2.detach().cpu(), RTOL, msg="frob fwd")
-    assert_close_rel(x.grad.cpu(), x2.grad.cpu(), RTOL, scale=float(x2.grad.abs().max()) * 1e-3,
-                     msg="frob bwd")
+    # a 1x1 block has an exactly-zero gradient: judge against the input scale there
+    assert_close_rel(x.grad.cpu(), x2.grad.cpu(), RTOL,
+                     scale=max(float(x2.grad.abs().max()) * 1e-3, 1e-6), msg="frob bwd")
 
 
 def torch_reference_repr(model, blocks):
