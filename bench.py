@@ -61,7 +61,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = "inter_bwd_mfma"  # device symbol of rs_dlrm_interaction_bwd
+PMC_KERNEL_REGEX = "dlrm_bwd_pipe|inter_bwd_mfma"  # device symbols of rs_dlrm_interaction_bwd
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 

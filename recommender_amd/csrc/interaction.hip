@@ -17,6 +17,8 @@
 // [Z (F*F, skip_gather), dense (D)] (ctr/model.py:51-55), so the [B,S,D] embedding tensor
 // is never materialised in HBM; the backward re-gathers the rows instead of re-reading a
 // saved copy (one 512-B read instead of a write + a read per row).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace rs {
@@ -282,6 +284,207 @@ __global__ __launch_bounds__(256) void inter_bwd_mfma(Src src, int64_t batch, in
 }
 
 // ---------------------------------------------------------------------------------------
+// DLRM backward, software-pipelined (the production path for D = 128): each wave walks
+// kPipeEPW consecutive examples. The ids of b+2 are loaded while b is processed, the row
+// pointers of b+1 are resolved before b's MFMAs, and b+1's rows are gathered into the operand
+// registers as soon as b's MFMA chain has read them — overlapping b's MFMA drain, its grad-row
+// stores and the staging of the next grad row. Every wait is a counted in-order vmcnt (plain
+// global loads, no LDS-DMA), so b's stores never hold up b+1's loads. Per-example arithmetic
+// is that of inter_bwd_mfma (same MFMA order): bit-identical results.
+// Measured (1x MI355X, north-star batch): 393 us → 298-320 us at 2 waves/SIMD (186 VGPR + 64
+// AGPR); forcing 3 waves spills and is slower (385 us); 64 examples per wave loses to the tail.
+// The same pipelining of the forward (3 waves/SIMD) measured 277-280 us against 244 us for
+// the 5-wave inter_fwd_mfma, so the forward keeps the one-example-per-wave kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int kPipeEPW = 16;  // upper bound; the launch sizes it to the occupancy (pipe_epw)
+
+// Examples per wave so that the grid is exactly kPipeRounds full rounds of resident waves
+// (a partial last round idles most SIMDs: 16 examples/wave at 3 waves/SIMD is 1.33 rounds).
+constexpr int kPipeRounds = 2;
+static int pipe_epw(const void* kernel, int64_t batch) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t slots = (int64_t)cus * per_cu * 4 * kPipeRounds;  // waves over all rounds
+  const int64_t e = ceil_div(batch, slots);
+  return (int)(e < 1 ? 1 : (e > 64 ? 64 : e));
+}
+
+typedef __attribute__((address_space(1))) const floatx4 gfloatx4;
+typedef __attribute__((address_space(1))) const float gfloat;
+
+// a zero row in global memory: absent / out-of-table rows are gathered from here, so the
+// pipelined gathers need no per-row select (a select would keep a lane mask live per row)
+__device__ const float kZeroRow[256] = {};
+
+template <int D, int GREG, int KS, bool SELF, bool SKIP, bool ID64>
+__global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batch, int F,
+                                                     const float* __restrict__ gout,
+                                                     int64_t gstride, float* __restrict__ gemb,
+                                                     float* __restrict__ gdense, int epw) {
+  static_assert(D == 128, "pipelined backward is laid out for D = 128 (4 floats per lane)");
+  constexpr int NTILE = 4;
+  // per wave: the staged grad row + one zero slot (index ZS) that dropped pairs read
+  constexpr int ZS = GREG * 64;
+  __shared__ float gsm[4][ZS + 4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
+  if (first >= batch) return;
+  const int64_t last = first + epw < batch ? first + epw : batch;
+  const int r = lane & 31, h = lane >> 5;
+  const int nz = out_width(F, SELF, SKIP);
+  const int S = src.n_slots;
+  // lane i < S owns slot i: its table range is loaded once
+  int64_t lo = 0, n_ok = src.n_rows;
+  if (lane < S && src.slot_offsets) {
+    lo = src.slot_offsets[lane];
+    n_ok = src.slot_offsets[lane + 1] - lo;
+  }
+  bool oob = false;
+  auto raw_id = [&](int64_t b) -> int64_t {
+    const int64_t bb = b < last ? b : first;  // past the end: a valid, unused load
+    if (lane >= S) return 0;
+    return ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + lane]
+                : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + lane]);
+  };
+  // lane k's row of example b (kZeroRow for absent / OOB rows and for k >= F)
+  auto row_of = [&](int64_t b, int64_t id) -> const float* {
+    const bool live = b < last;
+    const bool id_ok = id >= 0 && id < n_ok;
+    if (lane < S && !id_ok && live) oob = true;
+    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
+    return (lane == S && live) ? src.dense + b * D : kZeroRow;
+  };
+  float xv[KS][NTILE];
+  auto load_rows = [&](const float* mine, int s) {
+    const float* xr = shfl_ptr(mine, 2 * s + h);
+    const floatx4 t = *(gfloatx4*)(xr + NTILE * r);  // global_load_dwordx4 (not flat)
+    xv[s][0] = t[0];
+    xv[s][1] = t[1];
+    xv[s][2] = t[2];
+    xv[s][3] = t[3];
+  };
+  float gnx[GREG];
+  auto load_g = [&](int64_t b) {  // GREG*64 <= gstride: the whole padded row is readable
+    const int64_t bb = b < last ? b : first;
+    gfloat* grow = (gfloat*)(gout + bb * gstride);
+#pragma unroll
+    for (int j = 0; j < GREG; ++j) gnx[j] = grow[lane + 64 * j];
+  };
+  // prologue: example `first` in flight, ids of first+1 in flight
+  const float* cur = row_of(first, raw_id(first));
+  int64_t id_next = raw_id(first + 1);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) load_rows(cur, s);
+  load_g(first);
+  float* gs = gsm[wave];
+  if (lane == 0) gs[ZS] = 0.f;
+  for (int64_t b = first; b < last; ++b) {
+    // lane-derived values recomputed per example from an opaque lane id: hoisted out of the
+    // loop they would pin ~70 VGPRs (LDS indices, store offsets) for the whole loop
+    int lanev;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
+    const int r = lanev & 31, h = lanev >> 5;
+    // (1) stage this example's grad row; resolve b+1's rows; put b+2's ids in flight
+#pragma unroll
+    for (int j = 0; j < GREG; ++j) gs[lane + 64 * j] = gnx[j];
+    const float* nxt = row_of(b + 1, id_next);
+    id_next = raw_id(b + 2);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the staged row is visible to the wave
+    __builtin_amdgcn_wave_barrier();
+    float sa[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 2 * s + h;
+      const bool in = r < F && k < F;
+      const bool p1 = in && keep_pair(r, k, SELF);
+      const bool p2 = in && keep_pair(k, r, SELF);
+      const int j1 = p1 ? (SKIP ? r * F + k : compact_index(r, k, F, SELF)) : ZS;
+      const int j2 = p2 ? (SKIP ? k * F + r : compact_index(k, r, F, SELF)) : ZS;
+      sa[s] = gs[j1] + gs[j2];
+    }
+    // (2) dX = S·X; each k-step's registers are refilled with b+1's rows right behind it
+    floatx16 acc[NTILE];
+#pragma unroll
+    for (int c = 0; c < NTILE; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[c][e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int c = 0; c < NTILE; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[s], xv[s][c], acc[c], 0, 0, 0);
+    }
+    // every operand register has been read by its MFMA: refill them with b+1's rows while the
+    // MFMA chain drains and this example's grad rows are stored
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) load_rows(nxt, s);
+    __builtin_amdgcn_sched_barrier(0);
+    // bottom-MLP pass-through of this example (read before the LDS row is restaged)
+    float dpass[NTILE];
+#pragma unroll
+    for (int c = 0; c < NTILE; ++c) dpass[c] = gs[nz + NTILE * r + c];
+    load_g(b + 1);
+    // (3) grad rows (position order) + bottom grad
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (i < F) {
+        float v[NTILE];
+#pragma unroll
+        for (int c = 0; c < NTILE; ++c) v[c] = acc[c][reg] + (i == S ? dpass[c] : 0.f);
+        float* dst = (i < S ? gemb + (b * S + i) * (int64_t)D : gdense + b * D) + NTILE * r;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+}
+
+template <int GREG, int KS, bool ID64>
+static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode md,
+                          const float* gout, int64_t gstride, float* gemb, float* gdense, int,
+                          hipStream_t st) {
+  auto go = [&](auto kern) {
+    static int epw_cached = 0;
+    static int64_t batch_cached = -1;
+    if (batch != batch_cached) {
+      epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch);
+      batch_cached = batch;
+    }
+    const int epw = epw_cached;
+    kern<<<ceil_div(batch, 4 * (int64_t)epw), 256, 0, st>>>(src, batch, F, gout, gstride, gemb,
+                                                           gdense, epw);
+  };
+  if (md.self_interaction) {
+    if (md.skip_gather) go(dlrm_bwd_pipe<128, GREG, KS, true, true, ID64>);
+    else go(dlrm_bwd_pipe<128, GREG, KS, true, false, ID64>);
+  } else {
+    if (md.skip_gather) go(dlrm_bwd_pipe<128, GREG, KS, false, true, ID64>);
+    else go(dlrm_bwd_pipe<128, GREG, KS, false, false, ID64>);
+  }
+}
+
+template <int GREG, int KS>
+static void launch_pipe(const GatherSrc& src, int64_t batch, int F, InterMode md,
+                        const float* gout, int64_t gstride, float* gemb, float* gdense, int epw,
+                        hipStream_t st) {
+  if (src.id_dtype == RS_ID_I64)
+    launch_pipe_t<GREG, KS, true>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+  else
+    launch_pipe_t<GREG, KS, false>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+}
+
+// ---------------------------------------------------------------------------------------
 // generic (any F, D): one wave per sample, X staged in LDS
 // ---------------------------------------------------------------------------------------
 template <class Src, bool DLRM_OUT>
@@ -437,6 +640,25 @@ static int32_t launch_bwd(const Src& src, int64_t batch, int F, int D, InterMode
                           const float* gout, int64_t gstride, float* gx, float* gemb, float* gdense,
                           bool aligned16, hipStream_t st) {
   if (batch == 0) return RS_OK;
+  if constexpr (DLRM_OUT && std::is_same<Src, GatherSrc>::value) {
+    const int epw = kPipeEPW;
+    const int gw = out_width(F, md.self_interaction, md.skip_gather) + D;
+    if (F <= 32 && aligned16 && D == 128 && gw <= 20 * 64) {
+      const bool k14 = F <= 28;
+      if (gw <= 8 * 64 && gstride >= 8 * 64) {
+        if (k14) launch_pipe<8, 14>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+        else launch_pipe<8, 16>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+        RS_CHECK_LAUNCH();
+        return RS_OK;
+      }
+      if (gstride >= 20 * 64) {
+        if (k14) launch_pipe<20, 14>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+        else launch_pipe<20, 16>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+        RS_CHECK_LAUNCH();
+        return RS_OK;
+      }
+    }
+  }
   if (F <= 32 && aligned16) {
     int64_t blocks = ceil_div(batch, 4);
     switch (D) {

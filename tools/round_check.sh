@@ -1,0 +1,8 @@
+# full GPU validation + bench + rocprof summary (run under gpurun)
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-baseline-steps 0 --pmc 0 > gpurun_out/prof_bench.log 2>&1 || { echo "rocprof failed"; exit 1; }
+echo prof ok
