@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-baseline-batch", type=int, default=16384)
     ap.add_argument("--graph", type=int, default=0, help="1: time HIP-graph replays of the step")
     ap.add_argument("--fused", type=int, default=1, help="fused side-stream sparse optimizer")
+    ap.add_argument("--prio", type=int, default=0,
+                    help="1: run the step on a high-priority HIP stream (side-stream work fills in)")
     ap.add_argument("--pmc", type=int, default=1,
                     help="1: measure the roofline kernel's HBM traffic with two rocprofv3 --pmc "
                          "child runs (FETCH_SIZE, WRITE_SIZE) before this process touches the GPU")
@@ -244,6 +246,10 @@ def main():
     pool = make_pool(args, cards, rank, dev)
     U = measured_unique(pool, model)
 
+    if args.prio:
+        hp = torch.cuda.Stream(device=dev, priority=-1)
+        hp.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(hp)
     for i in range(args.warmup):
         step(pool[i % len(pool)])
     runners = [lambda b=b: step(b) for b in pool]
