@@ -373,18 +373,20 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
     xv[s][3] = t[3];
   };
   float gnx[GREG];
-  auto load_g = [&](int64_t b) {  // GREG*64 <= gstride: the whole padded row is readable
+  const int glast = (int)gstride - 1;  // reads past the row end are clamped (the values there
+                                       // are never used: every index read is < gw)
+  auto load_g = [&](int64_t b, int ln) {  // ln: a lane id (the loop passes the opaque one)
     const int64_t bb = b < last ? b : first;
     gfloat* grow = (gfloat*)(gout + bb * gstride);
 #pragma unroll
-    for (int j = 0; j < GREG; ++j) gnx[j] = grow[lane + 64 * j];
+    for (int j = 0; j < GREG; ++j) gnx[j] = grow[min(ln + 64 * j, glast)];
   };
   // prologue: example `first` in flight, ids of first+1 in flight
   const float* cur = row_of(first, raw_id(first));
   int64_t id_next = raw_id(first + 1);
 #pragma unroll
   for (int s = 0; s < KS; ++s) load_rows(cur, s);
-  load_g(first);
+  load_g(first, lane);
   float* gs = gsm[wave];
   if (lane == 0) gs[ZS] = 0.f;
   for (int64_t b = first; b < last; ++b) {
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
     float dpass[NTILE];
 #pragma unroll
     for (int c = 0; c < NTILE; ++c) dpass[c] = gs[nz + NTILE * r + c];
-    load_g(b + 1);
+    load_g(b + 1, lanev);
     // (3) grad rows (position order) + bottom grad
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -645,13 +647,13 @@ static int32_t launch_bwd(const Src& src, int64_t batch, int F, int D, InterMode
     const int gw = out_width(F, md.self_interaction, md.skip_gather) + D;
     if (F <= 32 && aligned16 && D == 128 && gw <= 20 * 64) {
       const bool k14 = F <= 28;
-      if (gw <= 8 * 64 && gstride >= 8 * 64) {
+      if (gw <= 8 * 64) {
         if (k14) launch_pipe<8, 14>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
         else launch_pipe<8, 16>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
         RS_CHECK_LAUNCH();
         return RS_OK;
       }
-      if (gstride >= 20 * 64) {
+      {
         if (k14) launch_pipe<20, 14>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
         else launch_pipe<20, 16>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
         RS_CHECK_LAUNCH();

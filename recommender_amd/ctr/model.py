@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from ..embedding import Embedding, SlabEmbedding
-from ..functional import dlrm_interaction, fm_interaction
+from ..functional import COMPACT_ALIGN, dlrm_interaction, fm_interaction
 from .layers import MLP, DotInteraction
 
 
@@ -77,9 +77,9 @@ class DLRM(nn.Module):
         self._exchanged = None
         iu = torch.triu_indices(F, F, 1)
         rows = torch.cat([iu[0] * F + iu[1], F * F + torch.arange(embedding_size)])
-        # the kernel pads the compact row to 64 columns with zeros; map the padding onto
+        # the kernel pads the compact row to COMPACT_ALIGN columns with zeros; map the padding onto
         # structural-zero rows (lower triangle incl. diagonal) so their gradient stays 0
-        pad = (rows.numel() + 63) // 64 * 64 - rows.numel()
+        pad = (rows.numel() + COMPACT_ALIGN - 1) // COMPACT_ALIGN * COMPACT_ALIGN - rows.numel()
         il = torch.tril_indices(F, F, 0)
         rows = torch.cat([rows, (il[0] * F + il[1])[:pad]])
         self.register_buffer("compact_rows", rows.to(device=self.top_mlp.mlp[0].kernel.device))

@@ -10,6 +10,11 @@ import torch
 
 from . import _lib as L
 
+# compact DLRM row alignment: 479 = 351 + 128 columns → 480 (float4-aligned rows for the
+# interaction kernels). The top-MLP first layer's three GEMMs (fwd, dgrad, split-K wgrad)
+# measured 866 µs at K = 512 vs 768-804 µs at K = 480-496 (tools/probe_k480.py, 1x MI355X).
+COMPACT_ALIGN = 16
+
 
 def _ids_flat(ids: torch.Tensor) -> torch.Tensor:
     ids = ids.contiguous()
@@ -98,8 +103,8 @@ class _DLRMInteraction(torch.autograd.Function):
         if dense.shape != (B, D):
             raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
         width = (F * (F - 1) // 2 if compact else F * F) + D
-        if compact:  # pad to a multiple of 64 columns: well-tiled top-MLP GEMMs
-            width = (width + 63) // 64 * 64
+        if compact:  # pad to a multiple of COMPACT_ALIGN columns (top-MLP GEMM tiling)
+            width = (width + COMPACT_ALIGN - 1) // COMPACT_ALIGN * COMPACT_ALIGN
         out = torch.empty(B, width, device=w.device, dtype=torch.float32)
         L.call("rs_dlrm_interaction_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
                L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
@@ -134,7 +139,7 @@ class _DLRMInteraction(torch.autograd.Function):
 def dlrm_interaction(table_module, ids, dense, compact: bool = False):
     """[Z, dense] with Z the strict-upper X·Xᵀ of X = [emb(ids), dense]: F*F wide with zeros
     (reference layout) or, compact=True, the F(F-1)/2 kept values only (row zero-padded to a
-    multiple of 64 columns)."""
+    multiple of COMPACT_ALIGN columns)."""
     return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids, compact)
 
 

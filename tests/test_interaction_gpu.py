@@ -8,7 +8,7 @@ import torch
 from oracle import embedding as OE
 from oracle import interaction as O
 from recommender_amd.embedding import Embedding, SlabEmbedding
-from recommender_amd.functional import dlrm_interaction, dot_interaction, fm_interaction
+from recommender_amd.functional import COMPACT_ALIGN, dlrm_interaction, dot_interaction, fm_interaction
 from tests.conftest import assert_close_rel
 
 pytestmark = pytest.mark.gpu
@@ -72,7 +72,7 @@ def test_dlrm_fused(D, slab, compact, rng):
     keep_cols = np.r_[np.flatnonzero(np.triu(np.ones((F, F), bool), 1).reshape(-1)), F * F + np.arange(D)]
     if compact:
         ref = ref[:, keep_cols]
-        pad = (ref.shape[1] + 63) // 64 * 64 - ref.shape[1]
+        pad = (ref.shape[1] + COMPACT_ALIGN - 1) // COMPACT_ALIGN * COMPACT_ALIGN - ref.shape[1]
         got_pad = out.detach()[:, ref.shape[1]:].cpu().numpy()
         assert got_pad.shape[1] == pad and (got_pad == 0).all()
         out = out[:, : ref.shape[1]]

@@ -236,9 +236,10 @@ def test_frobenius_normalize(shape):
     y2 = x2 / torch.norm(x2)
     y2.backward(g)
     assert_close_rel(y.detach().cpu(), y2.detach().cpu(), RTOL, msg="frob fwd")
-    # a 1x1 block has an exactly-zero gradient: judge against the input scale there
-    assert_close_rel(x.grad.cpu(), x2.grad.cpu(), RTOL,
-                     scale=max(float(x2.grad.abs().max()) * 1e-3, 1e-6), msg="frob bwd")
+    # the gradient's natural size is |dy| / ||x||; a 1x1 block's exact gradient is 0 (torch
+    # returns rounding noise there), so the floor is taken from that size
+    nat = float(g.abs().max()) / float(x2.detach().norm())
+    assert_close_rel(x.grad.cpu(), x2.grad.cpu(), RTOL, scale=nat * 1e-2, msg="frob bwd")
 
 
 def torch_reference_repr(model, blocks):
