@@ -1,0 +1,198 @@
+"""Per-kernel roofline table for the secondary paths (DIEN attention + GRU/AUGRU,
+PinSage sampling + mean-pool, EGES, ESMM-shaped embedding) at their BASELINE config shapes.
+
+Every kernel is called through the C ABI on device-resident inputs, timed with HIP events
+over `--iters` launches on the stream it runs on, and reported with its ALGORITHMIC bytes per
+launch (each input byte read once, each output byte written once; the formulas are next to
+each case and in DESIGN.md §4), achieved GB/s and the fraction of the 8 TB/s HBM peak.
+The recurrent DIEN kernels carry L dependent steps per example, so they are latency-bound by
+construction ("DIEN is really latency-bound"); their fraction says how far.
+
+Usage: python benchmarks/bench_kernels.py [--iters 20] > profiles/rNN_kernel_roofline.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from recommender_amd import _lib as L  # noqa: E402
+
+PEAK = 8000.0  # GB/s, MI355X HBM3E spec
+DEV = "cuda"
+
+
+def timed(fn, iters):
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def report(name, cfg, us, nbytes, out):
+    gbs = nbytes / (us * 1e-6) / 1e9
+    line = {"kernel": name, "config": cfg, "avg_us": round(us, 2), "algorithmic_bytes": int(nbytes),
+            "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / PEAK, 4)}
+    out.append(line)
+    print(json.dumps(line), flush=True)
+
+
+def dien(iters, out):
+    B, T, H = 4096, 100, 36
+    g = torch.Generator(device=DEV).manual_seed(0)
+    xw = torch.randn(B, T, 3 * H, device=DEV, generator=g)
+    U = torch.randn(H, 3 * H, device=DEV, generator=g) * 0.1
+    rb = torch.zeros(3 * H, device=DEV)
+    lens = torch.randint(2, T + 1, (B,), device=DEV, generator=g)
+    mask = (torch.arange(T, device=DEV)[None] < lens[:, None]).to(torch.uint8).contiguous()
+    outp = torch.empty(B, T, H, device=DEV)
+    saved = torch.empty(B, T, 4 * H, device=DEV)
+    st = L.stream_ptr(DEV)
+    cfg = {"B": B, "L": T, "H": H}
+    us = timed(lambda: L.call("rs_gru_fwd", L.ptr(xw), L.ptr(U), L.ptr(rb), L.ptr(mask), B, T, H,
+                              L.ptr(outp), L.ptr(saved), st), iters)
+    report("rs_gru_fwd", cfg, us, B * T * (12 * H + 1 + 4 * H + 16 * H), out)
+    dout = torch.randn(B, T, H, device=DEV, generator=g)
+    dxw = torch.empty(B, T, 3 * H, device=DEV)
+    din = torch.empty(B, T, 3 * H, device=DEV)
+    us = timed(lambda: L.call("rs_gru_bwd", L.ptr(dout), L.ptr(outp), L.ptr(saved), L.ptr(U),
+                              L.ptr(mask), B, T, H, L.ptr(dxw), L.ptr(din), st), iters)
+    report("rs_gru_bwd", cfg, us, B * T * (4 * H + 4 * H + 16 * H + 1 + 12 * H + 12 * H), out)
+    att = torch.rand(B, T, device=DEV, generator=g)
+    kuh = torch.randn(H, H, device=DEV, generator=g) * 0.1
+    final = torch.empty(B, H, device=DEV)
+    states = torch.empty(B, T, H, device=DEV)
+    us = timed(lambda: L.call("rs_augru_fwd", L.ptr(xw), L.ptr(att), L.ptr(kuh), L.ptr(kuh),
+                              L.ptr(kuh), L.ptr(mask), B, T, H, L.ptr(final), L.ptr(states),
+                              L.ptr(saved), st), iters)
+    report("rs_augru_fwd", cfg, us, B * T * (12 * H + 4 + 1 + 4 * H + 16 * H) + 4 * B * H, out)
+    dfinal = torch.randn(B, H, device=DEV, generator=g)
+    datt = torch.empty(B, T, device=DEV)
+    us = timed(lambda: L.call("rs_augru_bwd", L.ptr(dfinal), L.ptr(att), L.ptr(states),
+                              L.ptr(saved), L.ptr(kuh), L.ptr(kuh), L.ptr(kuh), L.ptr(mask), B, T,
+                              H, L.ptr(dxw), L.ptr(datt), st), iters)
+    report("rs_augru_bwd", cfg, us, B * T * (4 + 4 * H + 16 * H + 1 + 12 * H + 4) + 4 * B * H, out)
+    hs = torch.randn(B, T, H, device=DEV, generator=g)
+    q = torch.randn(B, H, device=DEV, generator=g)
+    a = torch.empty(B, T, device=DEV)
+    us = timed(lambda: L.call("rs_dien_attention_fwd", L.ptr(hs), L.ptr(q), L.ptr(mask), B, T, H,
+                              L.ptr(a), st), iters)
+    report("rs_dien_attention_fwd", cfg, us, B * T * (4 * H + 1 + 4) + 4 * B * H, out)
+    da = torch.randn(B, T, device=DEV, generator=g)
+    dhs = torch.empty_like(hs)
+    dq = torch.empty_like(q)
+    us = timed(lambda: L.call("rs_dien_attention_bwd", L.ptr(hs), L.ptr(q), L.ptr(a), L.ptr(da), B,
+                              T, H, L.ptr(dhs), L.ptr(dq), st), iters)
+    report("rs_dien_attention_bwd", cfg, us, B * T * (4 * H + 4 + 4 + 4 * H) + 8 * B * H, out)
+
+
+def pinsage(iters, out):
+    from recommender_amd.pinsage import PinSageSampler
+    from recommender_amd.pinsage.layers import weighted_mean_agg  # noqa: F401
+    from recommender_amd.pinsage.sampler import item_pairs
+    from recommender_amd.pinsage.train import ML20M, build_graph
+
+    g = build_graph(ML20M, 4)
+    smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    h, p, n = item_pairs(g, 4096, 4, 0)
+    seeds, _, ns = smp.unique_first(torch.cat([h, p, n]), g.n_items)
+    seeds = seeds[: int(ns.item())].contiguous()
+    S = seeds.numel()
+    cfg = {"graph": "ml20m_shaped", "edges": g.n_edges, "seeds": S, "walks": 4, "traversals": 2,
+           "k": 3}
+    # 4 walks x 4 hops, each hop: indptr pair (16 B) + one neighbour id (4 B); out 3 x (4 + 4) B
+    us = timed(lambda: smp.neighbors(seeds, 0, None, 0), iters)
+    report("rs_pinsage_neighbors", cfg, us, S * (4 + 4 * 4 * 20 + 3 * 8), out)
+    nbr, cnt = smp.neighbors(seeds, 0, None, 0)
+    ids = torch.cat([seeds, nbr.reshape(-1)])
+    us = timed(lambda: smp.unique_first(ids, g.n_items), iters)
+    report("rs_unique_first", {"n": ids.numel(), "n_nodes": g.n_items}, us,
+           ids.numel() * (4 + 4 + 4 + 4) + g.n_items * 4, out)
+    blk = smp.to_block(seeds, nbr, cnt)
+    E = int(blk.n_edges.item())
+    Hh = 32
+    u = torch.randn(blk.n_src, Hh, device=DEV)
+    nv = torch.empty(blk.n_dst, Hh, device=DEV)
+    wsum = torch.empty(blk.n_dst, device=DEV)
+    st = L.stream_ptr(DEV)
+    acfg = {"n_dst": blk.n_dst, "n_src": blk.n_src, "edges": E, "H": Hh}
+    us = timed(lambda: L.call("rs_weighted_mean_agg_fwd", L.ptr(u), blk.n_src, Hh, L.ptr(blk.indptr),
+                              L.ptr(blk.edge_src), L.ptr(blk.edge_w), blk.n_dst, L.ptr(nv),
+                              L.ptr(wsum), st), iters)
+    report("rs_weighted_mean_agg_fwd", acfg, us, E * (4 + 4 + 4 * Hh) + blk.n_dst * (8 + 4 * Hh), out)
+    gu = torch.empty_like(u)
+    us = timed(lambda: L.call("rs_weighted_mean_agg_bwd", L.ptr(nv), Hh, L.ptr(blk.t_indptr),
+                              L.ptr(blk.t_edge), L.ptr(blk.edge_dst), L.ptr(blk.edge_w), L.ptr(wsum),
+                              blk.n_src, L.ptr(gu), st), iters)
+    report("rs_weighted_mean_agg_bwd", acfg, us,
+           E * (4 + 4 + 4 + 4 + 4 * Hh) + blk.n_src * (4 + 4 * Hh), out)
+
+
+def eges(iters, out):
+    from recommender_amd.embedding import Embedding
+
+    B, M, D, V = 1024, 6, 160, 63001
+    t = Embedding(V, D, device=DEV)
+    ids = torch.randint(0, V, (B, M), device=DEV, dtype=torch.int32)
+    h = torch.randn(B, D, device=DEV)
+    logits = torch.empty(B, M, device=DEV)
+    st = L.stream_ptr(DEV)
+    cfg = {"B": B, "M": M, "D": D}
+    us = timed(lambda: L.call("rs_match_logits_fwd", L.ptr(t.weight), V, D, L.ptr(ids), 0, M, L.ptr(h),
+                              B, L.ptr(logits), L.ptr(t.err_flag), st), iters)
+    report("rs_match_logits_fwd", cfg, us, B * M * (4 + 4 * D) + B * 4 * D + B * M * 4, out)
+    rows = torch.empty(B * M, D, device=DEV)
+    gh = torch.empty(B, D, device=DEV)
+    us = timed(lambda: L.call("rs_match_logits_bwd", L.ptr(t.weight), V, D, L.ptr(ids), 0, M, L.ptr(h),
+                              L.ptr(logits), B, L.ptr(rows), L.ptr(gh), st), iters)
+    report("rs_match_logits_bwd", cfg, us,
+           B * M * (4 + 4 * D + 4) + B * 4 * D + B * M * 4 * D + B * 4 * D, out)
+
+
+def embedding(iters, out):
+    from recommender_amd.esmm import FEAT_VOCAB
+    from recommender_amd.synthetic import aliccp_batch, scaled_vocab
+
+    vocab = scaled_vocab(FEAT_VOCAB, 40_000_000)
+    card = torch.tensor(list(vocab.values()), dtype=torch.int64)
+    so = torch.zeros(card.numel() + 1, dtype=torch.int64)
+    so[1:] = torch.cumsum(card, 0)
+    V, D, B, S = int(so[-1]), 18, 65536, card.numel()
+    table = torch.empty(V, D, device=DEV).uniform_(-0.05, 0.05)
+    feats, _ = aliccp_batch(np.random.default_rng(4), B, vocab)
+    ids = torch.from_numpy(np.concatenate(list(feats.values()), 1)).to(DEV).contiguous()
+    so = so.to(DEV)
+    outp = torch.empty(B, S, D, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    st = L.stream_ptr(DEV)
+    cfg = {"tables": S, "rows": V, "D": D, "B": B}
+    us = timed(lambda: L.call("rs_embedding_fwd", L.ptr(table), V, D, L.ptr(ids), 0, ids.numel(),
+                              L.ptr(so), S, L.ptr(outp), L.ptr(err), st), iters)
+    report("rs_embedding_fwd", cfg, us, ids.numel() * (4 + 2 * 4 * D), out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="dien,pinsage,eges,embedding")
+    args = ap.parse_args()
+    L.load()
+    out = []
+    for name in args.only.split(","):
+        globals()[name](args.iters, out)
+
+
+if __name__ == "__main__":
+    main()

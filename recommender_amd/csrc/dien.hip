@@ -307,13 +307,25 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------------------
 constexpr int kAttMaxT = 4;  // L <= 256
 
-__global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ hs,
-                                                      const float* __restrict__ q,
-                                                      const uint8_t* __restrict__ mask, int64_t B,
-                                                      int L, int H, float* __restrict__ a) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-  if (b >= B) return;
+// One wave (one block) per example: the example's [L, H] block of hidden states is contiguous,
+// so it is staged into LDS with coalesced loads (row stride H+1: conflict-free row reads), then
+// lane t computes s_t from LDS. (Lanes walking their own 4H-byte row straight from HBM made
+// every load instruction touch 64 rows: 85% of wave cycles waiting on memory.)
+__global__ __launch_bounds__(64) void att_fwd_kernel(const float* __restrict__ hs,
+                                                     const float* __restrict__ q,
+                                                     const uint8_t* __restrict__ mask, int64_t B,
+                                                     int L, int H, float* __restrict__ a) {
+  extern __shared__ float hsm[];  // [L][H + 1]
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int ld = H + 1;
+  const float* hb = hs + b * (int64_t)L * H;
+  const int n = L * H;
+  for (int o = lane; o < n; o += 64) {
+    const int t = o / H, i = o - t * H;
+    hsm[t * ld + i] = hb[o];
+  }
+  __syncthreads();
   const float* qb = q + b * H;  // uniform loads: every lane reads the same q_i
   float s[kAttMaxT];
   float mx = -INFINITY;
@@ -322,7 +334,7 @@ __global__ __launch_bounds__(256) void att_fwd_kernel(const float* __restrict__ 
     const int t = lane + 64 * c;
     s[c] = -INFINITY;
     if (t < L) {
-      const float* hr = hs + (b * L + t) * (int64_t)H;
+      const float* hr = hsm + t * ld;
       float acc = 0.f;
       for (int i = 0; i < H; ++i) acc = fmaf(hr[i], qb[i], acc);
       const float m = mask[b * L + t] ? 1.f : 0.f;
@@ -394,6 +406,7 @@ static int hm_for(int H) {
   if (H <= 16) return 16;
   if (H <= 24) return 24;
   if (H <= 32) return 32;
+  if (H <= 36) return 36;
   if (H <= 40) return 40;
   if (H <= 48) return 48;
   if (H <= 64) return 64;
@@ -406,6 +419,7 @@ static int hm_for(int H) {
     case 16: { constexpr int HM = 16; CALL; } break;                 \
     case 24: { constexpr int HM = 24; CALL; } break;                 \
     case 32: { constexpr int HM = 32; CALL; } break;                 \
+    case 36: { constexpr int HM = 36; CALL; } break;                 \
     case 40: { constexpr int HM = 40; CALL; } break;                 \
     case 48: { constexpr int HM = 48; CALL; } break;                 \
     case 64: { constexpr int HM = 64; CALL; } break;                 \
@@ -472,7 +486,11 @@ extern "C" int32_t rs_dien_attention_fwd(const float* hs, const float* q, const 
   RS_CHECK_ARG(B >= 0 && L >= 1 && L <= 64 * kAttMaxT && H >= 1 && H <= 64, "bad sizes");
   if (B == 0) return RS_OK;
   RS_CHECK_ARG(hs && q && mask && a, "null pointer");
-  att_fwd_kernel<<<ceil_div(B, 4), 256, 0, as_stream(stream)>>>(hs, q, mask, B, L, H, a);
+  const size_t lds = (size_t)L * (H + 1) * sizeof(float);
+  if (lds > 64 * 1024)
+    RS_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(att_fwd_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  att_fwd_kernel<<<(unsigned)B, 64, lds, as_stream(stream)>>>(hs, q, mask, B, L, H, a);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
