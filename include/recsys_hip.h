@@ -355,6 +355,16 @@ int32_t rs_side_pool_bwd(const float* side, const float* attn, const float* grad
                          int64_t batch, int32_t n_side, int32_t dim, float* grad_side,
                          float* grad_weight_logits, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Keras thresholded AUC (keras.metrics.AUC in ctr/train.py:86,
+ * dien/train.py:43-44, esmm/train.py:164). thresholds [n_thresholds] ascending float32 (the
+ * Keras grid: -eps, i/(T-1) for i = 1..T-2, 1+eps); counts [2, n_thresholds+1] int64,
+ * accumulated: counts[label != 0][#thresholds < pred] += 1 (a prediction outside [0, 1]
+ * sets RS_ERRBIT_OOB, as Keras asserts). TP_i = Σ_{b > i} counts[1][b], FP_i likewise. */
+int32_t rs_auc_update(const float* pred, const float* label, int64_t n, const float* thresholds,
+                      int32_t n_thresholds, unsigned long long* counts, int32_t* err_flag,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,7 @@ _SIGS = {
     "rs_match_logits_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p, _p]),
     "rs_side_pool_fwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_auc_update": (_i32, [_p, _p, _i64, _p, _i32, _p, _p, _p]),
 }
 
 _lib = None

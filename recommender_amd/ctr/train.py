@@ -22,6 +22,7 @@ import torch
 
 from ..functional import binary_crossentropy
 from ..nn import overlapped_weight_grads
+from ..metrics import AUC
 from ..optim import DLRMScheduler, KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import criteo_batch, criteo_cardinalities
 from .model import DLRM, DeepFM
@@ -97,6 +98,7 @@ class TrainStep:
                 g["lr"] = self._sched(self.opt_sparse.iterations)
         self.opt_dense.zero_grad(set_to_none=True)
         p = self.model({"cat_features": cat, "int_features": dense_x})
+        self.last_pred = p.detach()
         loss = binary_crossentropy(label, p, reduction=self.loss_reduction)
         if self.wgrad is not None:
             with self.wgrad:
@@ -162,18 +164,21 @@ def train(argv=None):
     sched = DLRMScheduler(0.01, 100, 10000, 0.0001) if args.optimizer == "sgd" else None
     step = TrainStep(model, args.optimizer, loss_reduction=args.loss_reduction, sched=sched)
     rng = np.random.default_rng(args.seed)
+    auc = AUC(num_thresholds=200)  # keras.metrics.AUC() default, ctr/train.py:86
     for epoch in range(1, args.epochs + 1):
         t0 = time.time()
         tot = 0.0
+        auc.reset_states()
         for _ in range(args.steps_per_epoch):
             cat, dn, lb = criteo_batch(rng, args.train_batch_size, cards)
             if not args.slab:
                 cat = cat % args.vocab_size
             batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev), torch.from_numpy(lb).to(dev))
             tot += float(step(batch))
+            auc.update_state(batch[2], step.last_pred)
         torch.cuda.synchronize()
         dt = time.time() - t0
-        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} "
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} auc {auc.result():.4f} "
               f"{args.steps_per_epoch * args.train_batch_size / dt:.0f} ex/s")
 
 

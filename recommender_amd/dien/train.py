@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from ..functional import binary_crossentropy
+from ..metrics import AUC
 from ..optim import KerasAdam, SparseAdam
 from . import DIEN, DIN, BaseModel
 
@@ -52,11 +53,13 @@ class DIENStep:
         self.opt_dense.zero_grad(set_to_none=True)
         if self.is_dien:
             pred, aux = self.model(feats, training=True)
+            self.last_pred = pred.detach()
             bce = binary_crossentropy(label, pred, reduction="mean")
             aux = aux.mean()
             total = bce + aux
         else:
             pred = self.model(feats, training=True)
+            self.last_pred = pred.detach()
             total = aux = binary_crossentropy(label, pred, reduction="mean")
         total.backward()
         self.opt_dense.step()
@@ -89,15 +92,19 @@ def main(argv=None):
         model = BaseModel(**kw)
     step = DIENStep(model)
     rng = np.random.default_rng(args.seed)
+    auc = AUC(num_thresholds=20000)  # dien/train.py:43-44
     for epoch in range(1, args.epochs + 1):
         t0, tot = time.time(), 0.0
+        auc.reset_states()
         for _ in range(args.steps_per_epoch):
             f, lab = synthetic_batch(rng, args.train_batch_size, args.history_max_length,
                                      args.item_vocab, args.cat_vocab, args.model_type == "DIEN")
             feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
-            tot += float(step(feats, torch.from_numpy(lab).cuda())[0])
+            label = torch.from_numpy(lab).cuda()
+            tot += float(step(feats, label)[0])
+            auc.update_state(label, step.last_pred)
         torch.cuda.synchronize()
-        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} "
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} auc {auc.result():.4f} "
               f"{args.steps_per_epoch * args.train_batch_size / (time.time() - t0):.0f} ex/s")
 
 

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from ..functional import binary_crossentropy
+from ..metrics import AUC
 from ..optim import KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import aliccp_batch, scaled_vocab
 from . import ESMM, FEAT_VOCAB, MMOE, BaseModel
@@ -51,6 +52,7 @@ class MultiTaskStep:
     def __call__(self, feats, label):
         self.opt_dense.zero_grad(set_to_none=True)
         y = self.model(feats)
+        self.last_pred = y.detach()
         loss = binary_crossentropy(label, y, reduction="mean")
         loss.backward()
         self.opt_dense.step()
@@ -83,14 +85,23 @@ def train(argv=None):
     model = build(args.model_type, vocab)
     step = MultiTaskStep(model, args.optimizer)
     rng = np.random.default_rng(args.seed)
+    # ctr and ctcvr AUCs over outputs [ctr, ctcvr] (esmm/train.py:58-61, 10000 thresholds)
+    ctr_auc = AUC(num_thresholds=args.auc_num_thresholds)
+    ctcvr_auc = AUC(num_thresholds=args.auc_num_thresholds)
     for epoch in range(1, args.epochs + 1):
         t0, tot = time.time(), 0.0
+        ctr_auc.reset_states()
+        ctcvr_auc.reset_states()
         for _ in range(args.steps_per_epoch):
             f, lab = aliccp_batch(rng, args.train_batch_size, vocab)
             feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
-            tot += float(step(feats, torch.from_numpy(lab).cuda()))
+            label = torch.from_numpy(lab).cuda()
+            tot += float(step(feats, label))
+            ctr_auc.update_state(label[:, 0], step.last_pred[:, 0])
+            ctcvr_auc.update_state(label[:, 1], step.last_pred[:, 1])
         torch.cuda.synchronize()
-        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.5f} "
+        print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.5f} ctr_auc {ctr_auc.result():.4f} "
+              f"ctcvr_auc {ctcvr_auc.result():.4f} "
               f"{args.steps_per_epoch * args.train_batch_size / (time.time() - t0):.0f} ex/s")
 
 
