@@ -183,10 +183,34 @@ def embedding(iters, out):
     report("rs_embedding_fwd", cfg, us, ids.numel() * (4 + 2 * 4 * D), out)
 
 
+def criteo(iters, out):
+    """Criteo TSV ingestion: line index + parse + vocab lookup over a ~45 MB synthetic text
+    (algorithmic bytes: text read once, outputs written once)."""
+    from recommender_amd.data import CriteoVocab, read_criteo_tsv
+    from tests.criteo_text import make_tsv
+
+    text = make_tsv(np.random.default_rng(4), 200_000, vocab=5000).encode()
+    vocab = CriteoVocab.build(text)
+    n = text.count(b"\n") + 1
+    out_bytes = n * (26 * 8 + 13 * 4 + 4)
+    us = timed(lambda: vocab.encode(text), max(3, iters // 4))
+    cfg = {"lines": n, "text_MB": round(len(text) / 1e6, 1), "vocab": vocab.size,
+           "includes": "pinned host->device copy of the text + 3 host syncs"}
+    report("criteo_encode(host tsv->device ids)", cfg, us, len(text) + out_bytes, out)
+    dtext = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(DEV)
+    us = timed(lambda: vocab.encode(dtext), iters)
+    cfg = dict(cfg, includes="text already in HBM; line index + parse + lookup + 3 host syncs")
+    report("criteo_encode(device tsv->ids)", cfg, us, len(text) + out_bytes, out)
+    _, _, hashes, _ = read_criteo_tsv(dtext)
+    us = timed(lambda: vocab.lookup(hashes), iters)
+    report("rs_vocab_lookup", {"tokens": hashes.numel(), "capacity": vocab.capacity}, us,
+           hashes.numel() * 16, out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", default="dien,pinsage,eges,embedding")
+    ap.add_argument("--only", default="dien,pinsage,eges,embedding,criteo")
     args = ap.parse_args()
     L.load()
     out = []

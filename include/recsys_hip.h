@@ -365,6 +365,40 @@ int32_t rs_auc_update(const float* pred, const float* label, int64_t n, const fl
                       int32_t n_thresholds, unsigned long long* counts, int32_t* err_flag,
                       void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Criteo TSV ingestion (ctr/tfrecord_io.py:15-96), text resident in HBM.
+ * rs_line_index: line_starts [n_newlines + 1] int64 (line 0 at byte 0, line k after the k-th
+ *   '\n'); *n_newlines device int32; line_starts NULL = count only.
+ * rs_criteo_parse: per line "label \t n_int ints \t n_cat tokens": label [n_lines] f32,
+ *   dense [n_lines, n_int] = logf(max(int, 0) + 1) (''/negative → 0, tfrecord_io.py:47-53),
+ *   hashes [n_lines, n_cat] = FNV-1a 64 of each token (empty → the column's imputation token,
+ *   :24-25; the last token keeps the line's '\n' as Python's split does); a line with the
+ *   wrong field count sets RS_ERRBIT_OOB and yields zeros / imputation tokens.
+ * rs_vocab_count: open-addressing table (capacity a power of two; keys filled with 0xFF,
+ *   counts / first_pos with 0 / 0xFF by the caller): count += 1, first_pos = min(pos_base + i)
+ *   (the reference dict's insertion order, :15-30).
+ * rs_vocab_collect: slots with count > min_count (10, :33) → first_out / slot_out (slot
+ *   order), *n_kept; the caller sorts them by first position and rs_vocab_assign gives slot
+ *   sorted_slots[r] the id r (ids pre-filled with -1).
+ * rs_vocab_lookup: id of every token, 0 when absent (OOV → 0, :64-67). */
+size_t rs_line_index_workspace_size(int64_t n_bytes);
+int32_t rs_line_index(const uint8_t* text, int64_t n_bytes, int64_t* line_starts,
+                      int32_t* n_newlines, void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_criteo_parse(const uint8_t* text, int64_t n_bytes, const int64_t* line_starts,
+                        int64_t n_lines, int32_t n_int, int32_t n_cat, float* label, float* dense,
+                        uint64_t* hashes, int32_t* err_flag, void* stream);
+int32_t rs_vocab_count(const uint64_t* hashes, int64_t n, int64_t pos_base, uint64_t* keys,
+                       uint32_t* counts, uint64_t* first_pos, int64_t capacity, int32_t* err_flag,
+                       void* stream);
+size_t rs_vocab_collect_workspace_size(int64_t capacity);
+int32_t rs_vocab_collect(const uint64_t* keys, const uint32_t* counts, const uint64_t* first_pos,
+                         int64_t capacity, uint32_t min_count, uint64_t* first_out,
+                         int32_t* slot_out, int32_t* n_kept, void* workspace, size_t ws_bytes,
+                         void* stream);
+int32_t rs_vocab_assign(const int32_t* sorted_slots, int64_t n_kept, int32_t* ids, void* stream);
+int32_t rs_vocab_lookup(const uint64_t* hashes, int64_t n, const uint64_t* keys,
+                        const int32_t* ids, int64_t capacity, int64_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,6 +92,14 @@ _SIGS = {
     "rs_side_pool_fwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_auc_update": (_i32, [_p, _p, _i64, _p, _i32, _p, _p, _p]),
+    "rs_line_index_workspace_size": (_sz, [_i64]),
+    "rs_line_index": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
+    "rs_criteo_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
+    "rs_vocab_count": (_i32, [_p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
+    "rs_vocab_collect_workspace_size": (_sz, [_i64]),
+    "rs_vocab_collect": (_i32, [_p, _p, _p, _i64, _u32, _p, _p, _p, _p, _sz, _p]),
+    "rs_vocab_assign": (_i32, [_p, _i64, _p, _p]),
+    "rs_vocab_lookup": (_i32, [_p, _i64, _p, _p, _i64, _p, _p]),
 }
 
 _lib = None
