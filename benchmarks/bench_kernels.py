@@ -161,6 +161,43 @@ def eges(iters, out):
            B * M * (4 + 4 * D + 4) + B * 4 * D + B * M * 4 * D + B * 4 * D, out)
 
 
+def eges_sampler(iters, out):
+    """EGES pair pipeline on a 63001-item weighted graph, 65536 walks of
+    length 10 per refill. Bytes: traces written + per hop indptr pair / log2(deg) prefix probes
+    / one index (random reads, latency-bound); skipgrams: traces read, flag + offset per slot,
+    pairs written; negatives: ids written (the CDF table is L2-resident; the kernel is ALU-bound)."""
+    from recommender_amd.eges.sampler import EGESPairSampler, skipgram_slots
+    from tests.eges_graph import make_graph
+
+    V, W, Lw = 63001, 65536, 10
+    indptr, indices, w = make_graph(np.random.default_rng(4), V, 1_000_000, 50)
+    s = EGESPairSampler(indptr, indices, w, V, device=DEV, walks_per_refill=W)
+    deg = max(1.0, indices.size / V)
+    probes = int(np.ceil(np.log2(deg + 1)))
+    cfg = {"items": V, "edges": int(indices.size), "walks": W, "length": Lw}
+    us = timed(lambda: s.walks(W, 1), iters)
+    report("rs_eges_walks", cfg, us, W * (Lw + 1) * 4 + W * Lw * (16 + 4 + 8 * probes), out)
+    tr = s.walks(W, 1)
+    slots = skipgram_slots(Lw + 1, 5)
+    us = timed(lambda: s.skipgrams(tr), iters)
+    tgt, _ = s.skipgrams(tr)
+    P = tgt.numel()
+    report("rs_skipgram_pairs(+1 sync)", dict(cfg, pairs=P), us,
+           W * (Lw + 1) * 4 * 2 + W * slots * 16 + P * 8, out)
+    us = timed(lambda: s.negatives(P, 1), iters)
+    report("rs_log_uniform_sample(ALU-bound: Philox + CDF walk)", {"pairs": P, "num_ns": 5,
+                                                                 "range": V}, us, P * 5 * 4, out)
+    def refill():
+        s._target, s._context = s._target[:0], s._context[:0]
+        s.refill()
+
+    us = timed(refill, max(3, iters // 4))
+    line = {"kernel": "eges_refill(walks+skipgrams+negatives)", "config": dict(cfg, pairs=P),
+            "avg_us": round(us, 2), "pairs_per_s": round(P / (us * 1e-6))}
+    out.append(line)
+    print(json.dumps(line), flush=True)
+
+
 def embedding(iters, out):
     from recommender_amd.esmm import FEAT_VOCAB
     from recommender_amd.synthetic import aliccp_batch, scaled_vocab
@@ -210,7 +247,7 @@ def criteo(iters, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", default="dien,pinsage,eges,embedding,criteo")
+    ap.add_argument("--only", default="dien,pinsage,eges,eges_sampler,embedding,criteo")
     args = ap.parse_args()
     L.load()
     out = []

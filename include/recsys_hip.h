@@ -399,6 +399,31 @@ int32_t rs_vocab_assign(const int32_t* sorted_slots, int64_t n_kept, int32_t* id
 int32_t rs_vocab_lookup(const uint64_t* hashes, int64_t n, const uint64_t* keys,
                         const int32_t* ids, int64_t capacity, int64_t* out, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * EGES training pairs (eges/data_loader.py:28-62), Philox-keyed draws.
+ * rs_eges_walks: walk i (global walk_base + i) starts at 1 + U[0, n_items-1) and takes `length`
+ *   weighted steps (dgl random_walk prob='weight': edge e of v with probability w_e / W_v;
+ *   cumw = per-node inclusive float64 prefix of the CSR edge weights); traces
+ *   [n_walks, length+1], -1 after a dead end.
+ * rs_skipgram_pairs: keras skipgrams(window, negative_samples=0) over every trace (pairs of
+ *   items > 0 in enumeration order, no shuffle): target / context [≤ n_traces*slots],
+ *   *n_pairs.
+ * rs_log_uniform_sample: log_uniform_candidate_sampler(num_sampled, unique=True, range_max):
+ *   cdf [range_max] uint32 = floor(log(k+2)/log(range_max+1)·2^32); out [n_pairs, num_sampled].
+ * rs_csr_weight_prefix: cumw[e] = Σ_{lo(v) ≤ f ≤ e} w[f] per node v (sequential float64). */
+int32_t rs_csr_weight_prefix(const int64_t* indptr, const float* weights, int64_t n_nodes,
+                             double* cumw, void* stream);
+int32_t rs_eges_walks(const int64_t* indptr, const int32_t* indices, const double* cumw,
+                      int32_t n_items, int64_t walk_base, int32_t n_walks, int32_t length,
+                      uint64_t seed, uint32_t step, int32_t* traces, void* stream);
+size_t rs_skipgram_workspace_size(int32_t n_traces, int32_t len, int32_t window);
+int32_t rs_skipgram_pairs(const int32_t* traces, int32_t n_traces, int32_t len, int32_t window,
+                          int32_t* target, int32_t* context, int32_t* n_pairs, void* workspace,
+                          size_t ws_bytes, void* stream);
+int32_t rs_log_uniform_sample(const uint32_t* cdf, int32_t range_max, int64_t pair_base,
+                              int32_t n_pairs, int32_t num_sampled, uint64_t seed, uint32_t step,
+                              int32_t* out, int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,8 +7,13 @@
 //                 a = 1/S as (Σ_s side) / S (GES :74-80).
 // One wave per example, lanes over D (coalesced rows), xor-shuffle reductions (fixed order).
 #include "common.hpp"
+#include "rng.hpp"
 
 namespace rs {
+
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* total, void* ws,
+                           size_t ws_bytes, hipStream_t st);
+size_t exclusive_scan_ws_size(int64_t n);
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -137,6 +142,153 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_bwd_kernel(
     for (int s = 0; s < S; ++s) grad_w[b * S + s] = a[s] * (ga[s] - dot);
 }
 
+// ---- training-pair sampler (eges/data_loader.py:28-62) -------------
+// walk i (global index walk_base + i) starts at 1 + U[0, n_items - 1) (:30, item 0 is OOV) and
+// takes `length` weighted steps (dgl.sampling.random_walk(prob='weight') [3p]: out-edge e of
+// node v with probability w_e / Σ w): draw r, target = (r + 0.5) / 2^32 · W_v, first edge whose
+// inclusive prefix weight (float64, per node) exceeds it. -1 after a dead end.
+constexpr uint32_t kPurposeEgesSeed = 0x400;
+constexpr uint32_t kPurposeEgesWalk = 0x500;
+constexpr uint32_t kPurposeEgesNeg = 0x600;
+
+__global__ __launch_bounds__(256) void eges_walk_kernel(const int64_t* __restrict__ indptr,
+                                                        const int32_t* __restrict__ indices,
+                                                        const double* __restrict__ cumw,
+                                                        int32_t n_items, int64_t walk_base,
+                                                        int32_t n_walks, int32_t length,
+                                                        uint64_t seed, uint32_t step,
+                                                        int32_t* __restrict__ traces) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_walks) return;
+  const uint32_t gi = (uint32_t)(walk_base + i);
+  int32_t node = 1 + (int32_t)bounded(draw(seed, kPurposeEgesSeed, gi, 0u, step, 0u),
+                                      (uint32_t)(n_items - 1));
+  int32_t* out = traces + (int64_t)i * (length + 1);
+  out[0] = node;
+  DrawStream ds(seed, kPurposeEgesWalk, gi, 0u, step);
+  for (int32_t h = 0; h < length; ++h) {
+    if (node >= 0) {
+      const int64_t lo = indptr[node], hi = indptr[node + 1];
+      if (hi <= lo || !(cumw[hi - 1] > 0.0)) {
+        node = -1;
+      } else {
+        const uint32_t r = ds.at((uint32_t)h);
+        const double target = ((double)r + 0.5) * 2.3283064365386963e-10 * cumw[hi - 1];
+        int64_t a = lo, b = hi - 1;  // first e in [lo, hi) with cumw[e] > target
+        while (a < b) {
+          const int64_t m = (a + b) >> 1;
+          if (cumw[m] > target) b = m;
+          else a = m + 1;
+        }
+        node = indices[a];
+      }
+    }
+    out[h + 1] = node;
+  }
+}
+
+// per-node inclusive prefix of the CSR edge weights, sequential float64 sum (one thread per
+// node; built once per graph)
+__global__ __launch_bounds__(256) void weight_prefix_kernel(const int64_t* __restrict__ indptr,
+                                                            const float* __restrict__ w,
+                                                            int64_t n_nodes,
+                                                            double* __restrict__ cumw) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  double acc = 0.0;
+  for (int64_t e = indptr[v]; e < indptr[v + 1]; ++e) {
+    acc += (double)w[e];
+    cumw[e] = acc;
+  }
+}
+
+// keras.preprocessing.sequence.skipgrams(seq, window_size, negative_samples=0) [3p]: for every
+// position i with w_i != 0, every j != i within the window with w_j != 0 gives (w_i, w_j); the
+// reference's shuffle only reorders. A slot per (trace, i, j) in enumeration order; items
+// <= 0 (OOV 0, dead end -1) are skipped.
+// slot k of a trace → (i, j): slots enumerate i ascending, then j ascending over the window
+__device__ __forceinline__ void skipgram_slot(int32_t k, int32_t len, int32_t window, int32_t& i,
+                                              int32_t& j) {
+  for (i = 0; i < len; ++i) {
+    const int32_t j0 = i - window < 0 ? 0 : i - window;
+    const int32_t j1 = i + window + 1 > len ? len : i + window + 1;
+    const int32_t c = j1 - j0 - 1;
+    if (k < c) {
+      j = j0 + k;
+      if (j >= i) ++j;
+      return;
+    }
+    k -= c;
+  }
+}
+
+// one thread per (trace, slot): coalesced flag / offset traffic
+__global__ __launch_bounds__(256) void skipgram_flag_kernel(const int32_t* __restrict__ traces,
+                                                            int64_t n_slots, int32_t len,
+                                                            int32_t window, int32_t slots,
+                                                            int32_t* __restrict__ flag) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  const int64_t t = s / slots;
+  int32_t i, j;
+  skipgram_slot((int32_t)(s - t * slots), len, window, i, j);
+  const int32_t* tr = traces + t * len;
+  flag[s] = tr[i] > 0 && tr[j] > 0;
+}
+
+__global__ __launch_bounds__(256) void skipgram_emit_kernel(const int32_t* __restrict__ traces,
+                                                            int64_t n_slots, int32_t len,
+                                                            int32_t window, int32_t slots,
+                                                            const int32_t* __restrict__ flag,
+                                                            const int32_t* __restrict__ offs,
+                                                            int32_t* __restrict__ target,
+                                                            int32_t* __restrict__ context) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots || !flag[s]) return;
+  const int64_t t = s / slots;
+  int32_t i, j;
+  skipgram_slot((int32_t)(s - t * slots), len, window, i, j);
+  const int32_t* tr = traces + t * len;
+  target[offs[s]] = tr[i];
+  context[offs[s]] = tr[j];
+}
+
+// tf.random.log_uniform_candidate_sampler(num_sampled, unique=True, range_max) [3p]:
+// P(k) = log((k+2)/(k+1)) / log(range_max+1), sampled without repeats. Draw r → the first k with
+// cdf[k] > r (cdf[k] = floor(log(k+2)/log(range_max+1) · 2^32), built on the host), rejecting
+// classes already taken for this pair.
+__global__ __launch_bounds__(256) void log_uniform_kernel(const uint32_t* __restrict__ cdf,
+                                                          int32_t range_max, int64_t pair_base,
+                                                          int32_t n_pairs, int32_t num_sampled,
+                                                          uint64_t seed, uint32_t step,
+                                                          int32_t* __restrict__ out,
+                                                          int32_t* __restrict__ err_flag) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const uint32_t gp = (uint32_t)(pair_base + p);
+  int32_t* o = out + (int64_t)p * num_sampled;
+  int32_t got = 0;
+  DrawStream ds(seed, kPurposeEgesNeg, gp, 0u, step);
+  const float l2r = log2f((float)range_max + 1.0f) * 2.3283064365386963e-10f;
+  for (uint32_t d = 0; got < num_sampled; ++d) {
+    if (d >= 4096u * (uint32_t)num_sampled) {  // degenerate range: stop, flag
+      for (; got < num_sampled; ++got) o[got] = 0;
+      flag_oob(err_flag);
+      break;
+    }
+    const uint32_t r = ds.at(d);
+    // first k with cdf[k] > r (range_max - 1 if none): start at the float inverse-CDF guess
+    // (off by at most a step or two) and walk to the exact answer on the table
+    int32_t a = (int32_t)exp2f((float)r * l2r) - 1;
+    a = a < 0 ? 0 : a > range_max - 1 ? range_max - 1 : a;
+    while (a < range_max - 1 && cdf[a] <= r) ++a;
+    while (a > 0 && cdf[a - 1] > r) --a;
+    bool dup = false;
+    for (int32_t q = 0; q < got; ++q) dup |= o[q] == a;
+    if (!dup) o[got++] = a;
+  }
+}
+
 inline unsigned waves_grid(int64_t B) { return (unsigned)ceil_div(B < 1 ? 1 : B, kWavesPerBlock); }
 
 }  // namespace rs
@@ -191,6 +343,91 @@ extern "C" int32_t rs_side_pool_bwd(const float* side, const float* attn, const 
   if (batch == 0) return RS_OK;
   pool_bwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
       side, attn, grad_hidden, batch, n_side, dim, grad_side, grad_weight_logits);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_eges_walks(const int64_t* indptr, const int32_t* indices, const double* cumw,
+                                 int32_t n_items, int64_t walk_base, int32_t n_walks,
+                                 int32_t length, uint64_t seed, uint32_t step, int32_t* traces,
+                                 void* stream) {
+  RS_CHECK_ARG(n_items >= 2 && n_walks >= 0 && length >= 0, "rs_eges_walks: bad sizes");
+  if (n_walks == 0) return RS_OK;
+  eges_walk_kernel<<<(unsigned)ceil_div(n_walks, 256), 256, 0, as_stream(stream)>>>(
+      indptr, indices, cumw, n_items, walk_base, n_walks, length, seed, step, traces);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static int32_t skipgram_slots(int32_t len, int32_t window) {
+  int32_t k = 0;
+  for (int32_t i = 0; i < len; ++i) {
+    const int32_t j0 = i - window < 0 ? 0 : i - window;
+    const int32_t j1 = i + window + 1 > len ? len : i + window + 1;
+    k += j1 - j0 - 1;
+  }
+  return k;
+}
+
+extern "C" size_t rs_skipgram_workspace_size(int32_t n_traces, int32_t len, int32_t window) {
+  const int64_t n = (int64_t)n_traces * skipgram_slots(len, window);
+  Carver c(nullptr, 0);
+  c.take<int32_t>(n);
+  c.take<int32_t>(n);
+  c.take<char>(exclusive_scan_ws_size(n < 1 ? 1 : n));
+  return c.off + 256;
+}
+
+extern "C" int32_t rs_skipgram_pairs(const int32_t* traces, int32_t n_traces, int32_t len,
+                                     int32_t window, int32_t* target, int32_t* context,
+                                     int32_t* n_pairs, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  RS_CHECK_ARG(n_traces >= 0 && len >= 1 && window >= 1, "rs_skipgram_pairs: bad sizes");
+  hipStream_t st = as_stream(stream);
+  const int32_t slots = skipgram_slots(len, window);
+  const int64_t n = (int64_t)n_traces * slots;
+  if (n == 0) {
+    RS_CHECK_HIP(hipMemsetAsync(n_pairs, 0, 4, st));
+    return RS_OK;
+  }
+  Carver c(workspace, ws_bytes);
+  int32_t* flag = c.take<int32_t>(n);
+  int32_t* offs = c.take<int32_t>(n);
+  void* sws = c.take<char>(exclusive_scan_ws_size(n));
+  if (!c.ok()) {
+    set_error("rs_skipgram_pairs: workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  const unsigned g = (unsigned)ceil_div(n, 256);
+  skipgram_flag_kernel<<<g, 256, 0, st>>>(traces, n, len, window, slots, flag);
+  RS_CHECK_LAUNCH();
+  int32_t s = exclusive_scan_i32(flag, offs, n, n_pairs, sws, exclusive_scan_ws_size(n), st);
+  if (s) return s;
+  skipgram_emit_kernel<<<g, 256, 0, st>>>(traces, n, len, window, slots, flag, offs, target,
+                                          context);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_log_uniform_sample(const uint32_t* cdf, int32_t range_max, int64_t pair_base,
+                                         int32_t n_pairs, int32_t num_sampled, uint64_t seed,
+                                         uint32_t step, int32_t* out, int32_t* err_flag,
+                                         void* stream) {
+  RS_CHECK_ARG(range_max >= 1 && num_sampled >= 1 && num_sampled <= range_max && n_pairs >= 0,
+               "rs_log_uniform_sample: bad sizes");
+  if (n_pairs == 0) return RS_OK;
+  log_uniform_kernel<<<(unsigned)ceil_div(n_pairs, 256), 256, 0, as_stream(stream)>>>(
+      cdf, range_max, pair_base, n_pairs, num_sampled, seed, step, out, err_flag);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_csr_weight_prefix(const int64_t* indptr, const float* weights,
+                                        int64_t n_nodes, double* cumw, void* stream) {
+  RS_CHECK_ARG(n_nodes >= 0, "rs_csr_weight_prefix: bad sizes");
+  if (n_nodes == 0) return RS_OK;
+  weight_prefix_kernel<<<(unsigned)ceil_div(n_nodes, 256), 256, 0, as_stream(stream)>>>(
+      indptr, weights, n_nodes, cumw);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

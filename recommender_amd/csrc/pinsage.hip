@@ -21,6 +21,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "rng.hpp"
 
 namespace rs {
 
@@ -31,39 +32,6 @@ size_t radix_sort_ws_size(int64_t n);
 int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* total, void* ws,
                            size_t ws_bytes, hipStream_t st);
 size_t exclusive_scan_ws_size(int64_t n);
-
-// ---- Philox4x32-10 -----------------------------------------------------------------------
-struct U4 {
-  uint32_t x, y, z, w;
-};
-
-__host__ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
-           (uint32_t)p0};
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
-
-__device__ __forceinline__ uint32_t draw(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b,
-                                         uint32_t c, uint32_t idx) {
-  U4 r = philox4x32_10(U4{a, b, c, idx >> 2}, (uint32_t)seed, (uint32_t)(seed >> 32) ^ purpose);
-  switch (idx & 3) {
-    case 0: return r.x;
-    case 1: return r.y;
-    case 2: return r.z;
-    default: return r.w;
-  }
-}
-
-__device__ __forceinline__ uint32_t bounded(uint32_t r, uint32_t n) {
-  return (uint32_t)(((uint64_t)r * n) >> 32);
-}
 
 struct Graph {
   const int64_t* i2u_ptr;

@@ -1,9 +1,10 @@
 """Training counterpart of eges/train.py (loop :14-24: sigmoid CE on the 1+num_ns skip-gram
 logits, reduce_mean, Keras Adam on every table — IndexedSlices → SparseAdam(mode='keras')).
 
-Data: synthetic skip-gram batches of the reference's shapes (target [B,1], cat/brand [B,1],
-context [B, 1+num_ns], label [1, 0, .., 0]); the weighted walk + skipgrams + log-uniform
-negative pipeline (eges/data_loader.py:28-62) is SURVEY §8f "next" and not on this path.
+Data: the reference's pair pipeline (eges/data_loader.py:28-62: weighted walk → skipgrams →
+log-uniform negatives) runs on the device (eges/sampler.py, EGESPairSampler) over a synthetic
+weighted item graph (the JD session data is not available offline); `synthetic_batch` keeps
+the i.i.d. batches of the same shapes for the model benchmarks.
 Hyper-parameters from eges/train.py:45-54,75-92 (emb 160, num_ns 5, batch 1024, seed 4)."""
 from __future__ import annotations
 
@@ -16,6 +17,7 @@ import torch.nn.functional as F
 
 from ..optim import SparseAdam
 from .model import EGES, GES, DeepWalk
+from .sampler import EGESPairSampler
 
 
 def log_uniform(rng, n, range_max):
@@ -23,6 +25,22 @@ def log_uniform(rng, n, range_max):
     log(range_max+1), by inverse CDF (without its uniqueness rejection)."""
     u = rng.random(n)
     return np.minimum((np.exp(u * np.log(range_max + 1.0)) - 1.0).astype(np.int64), range_max - 1)
+
+
+def synthetic_item_graph(rng, n_items, n_edges):
+    """Symmetric weighted co-occurrence CSR over items 1..n_items-1 (0 = OOV, no edges):
+    popularity-skewed endpoints, integer session-count weights."""
+    pop = rng.zipf(1.3, 2 * n_edges) % (n_items - 1) + 1
+    src, dst = pop[:n_edges], pop[n_edges:]
+    keep = src != dst
+    s = np.concatenate([src[keep], dst[keep]])
+    d = np.concatenate([dst[keep], src[keep]])
+    w = rng.integers(1, 10, s.size).astype(np.float32)
+    order = np.argsort(s, kind="stable")
+    s, d, w = s[order], d[order], w[order]
+    indptr = np.zeros(n_items + 1, np.int64)
+    np.add.at(indptr, s + 1, 1)
+    return np.cumsum(indptr), d.astype(np.int32), w
 
 
 def synthetic_batch(rng, batch, n_items, n_cat, n_brand, num_ns=5):
@@ -71,15 +89,17 @@ def main(argv=None):
     args = ap.parse_args(argv)
     rng = np.random.default_rng(args.seed)
     n_cat, n_brand = 801, 3000
+    indptr, indices, weights = synthetic_item_graph(rng, args.n_items, 16 * args.n_items)
+    items = np.arange(args.n_items)
+    sampler = EGESPairSampler(indptr, indices, weights, args.n_items,
+                              item2cat=(items * 2654435761) % n_cat,
+                              item2brand=(items * 40503) % n_brand, seed=args.seed)
     model = build(args.model_type, args.n_items, n_cat, n_brand)
     step = EGESStep(model)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        *inp, lab = synthetic_batch(rng, args.train_batch_size, args.n_items, n_cat, n_brand)
-        inp = [torch.from_numpy(a).cuda() for a in inp]
-        if args.model_type == "BGE":
-            inp = [inp[0], inp[3]]
-        loss = step(tuple(inp), torch.from_numpy(lab).cuda())
+        *inp, lab = sampler.next_batch(args.train_batch_size, args.model_type)
+        loss = step(tuple(inp), lab)
         if s % 50 == 0:
             print(f"step {s} loss {float(loss):.4f}")
     torch.cuda.synchronize()
