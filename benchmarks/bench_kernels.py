@@ -198,6 +198,49 @@ def eges_sampler(iters, out):
     print(json.dumps(line), flush=True)
 
 
+def pinsage_eval(iters, out):
+    """PinSage evaluation at ML-1M / ML-20M shapes: rs_masked_topk bytes =
+    the score rows read once + the exclusion CSR + the top-k written; plus the whole
+    get_item_reprs → recommend → hit_rate pass on ML-1M, wall clock."""
+    import time
+
+    from recommender_amd.pinsage import PinSageModel, PinSageSampler
+    from recommender_amd.pinsage.evaluation import (get_item_reprs, hit_rate_eval, masked_topk,
+                                                    recommend)
+    from recommender_amd.pinsage.train import ML1M, build_dataset
+    from recommender_amd.synthetic import ML20M
+
+    for name, shape in (("ml1m", ML1M), ("ml20m", ML20M)):
+        g, val, _ = build_dataset(shape, 4, DEV)
+        R = min(g.n_users, 8192)
+        scores = torch.randn(R, g.n_items, device=DEV)
+        nb = R * g.n_items * 4 + int(g.u2i_indptr[R]) * 4 + R * 8 + R * 10 * 4
+        us = timed(lambda: masked_topk(scores, 10, 0, g), iters)
+        report("rs_masked_topk", {"graph": name, "rows": R, "items": g.n_items, "k": 10}, us, nb,
+               out)
+        if name != "ml1m":
+            continue
+        torch.manual_seed(0)
+        model = PinSageModel(g, g.itype, 2, 8, 32, 16)
+        smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reprs = get_item_reprs(model, smp, g, g.itype, 32)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            recs = recommend(g, 10, reprs, None, g.utype, "timestamp", 32)
+            hr = hit_rate_eval(recs, val.tocsr())
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+        line = {"kernel": "pinsage_eval(get_item_reprs bs32 + recommend + hit_rate)",
+                "config": {"graph": name, "users": g.n_users, "items": g.n_items, "k": 10},
+                "item_reprs_ms": round((t1 - t0) * 1e3, 2),
+                "recommend_hit_rate_ms": round((t2 - t1) * 1e3, 3), "hit_rate": hr}
+        out.append(line)
+        print(json.dumps(line), flush=True)
+
+
 def embedding(iters, out):
     from recommender_amd.esmm import FEAT_VOCAB
     from recommender_amd.synthetic import aliccp_batch, scaled_vocab
@@ -247,7 +290,7 @@ def criteo(iters, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", default="dien,pinsage,eges,eges_sampler,embedding,criteo")
+    ap.add_argument("--only", default="dien,pinsage,pinsage_eval,eges,eges_sampler,embedding,criteo")
     args = ap.parse_args()
     L.load()
     out = []

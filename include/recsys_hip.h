@@ -424,6 +424,24 @@ int32_t rs_log_uniform_sample(const uint32_t* cdf, int32_t range_max, int64_t pa
                               int32_t n_pairs, int32_t num_sampled, uint64_t seed, uint32_t step,
                               int32_t* out, int32_t* err_flag, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * PinSage evaluation (pinsage/train/evaluation.py:27-65).
+ * rs_latest_item: per user the item of its latest u2i edge by timestamp (select_topk(k=1),
+ *   evaluation.py:33-34; ties → smaller item id); -1 and ++*n_missing for users without edges.
+ * rs_masked_topk: rows r of scores [n_rows, ld] (user user_base + r) → the k best items
+ *   (score desc, item asc) after setting the user's excl CSR items to -inf (:41-46); k ≤ 64,
+ *   n_items ≤ 2^20. out_scores may be NULL.
+ * rs_hit_flags: hit[r] = any(recs[r, :] ∈ truth CSR row of user user_base + r) (:54-65). */
+int32_t rs_latest_item(const int64_t* u2i_indptr, const int32_t* u2i_items,
+                       const int64_t* timestamps, int64_t n_users, int32_t* latest,
+                       int32_t* n_missing, void* stream);
+int32_t rs_masked_topk(const float* scores, int64_t ld, int32_t n_rows, int32_t n_items,
+                       int64_t user_base, const int64_t* excl_indptr, const int32_t* excl_items,
+                       int32_t k, int32_t* out_items, float* out_scores, void* stream);
+int32_t rs_hit_flags(const int32_t* recs, int64_t n_rows, int32_t k, int64_t user_base,
+                     const int64_t* truth_indptr, const int32_t* truth_items, int32_t* hit,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

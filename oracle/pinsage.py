@@ -303,3 +303,59 @@ def get_repr(blocks, year, genre, tables, conv_params, head_params):
 def margin_loss(pos_score, neg_score, delta=1.0):
     """train.py:17-20: mean(clip(neg + delta - pos, 0, inf))."""
     return float(np.mean(np.clip(neg_score + delta - pos_score, 0, np.inf)))
+
+
+# ---- evaluation (pinsage/train/evaluation.py:27-65, util.py:5-24) --------------------------
+def latest_item(u2i_indptr, u2i, ts):
+    """select_topk(k=1, timestamp) per user (:33-34); ties → smaller item; -1 without edges."""
+    out = np.full(len(u2i_indptr) - 1, -1, np.int32)
+    for u in range(len(out)):
+        lo, hi = int(u2i_indptr[u]), int(u2i_indptr[u + 1])
+        if hi > lo:
+            t, it = ts[lo:hi], u2i[lo:hi]
+            m = t == t.max()
+            out[u] = it[m].min()
+    return out
+
+
+def masked_topk_scores(scores, excl_indptr=None, excl=None, user_base=0):
+    """similarity[i, interacted] = -inf (:41-44)."""
+    s = np.array(scores, np.float32, copy=True)
+    if excl_indptr is not None:
+        for r in range(s.shape[0]):
+            u = user_base + r
+            s[r, excl[excl_indptr[u]:excl_indptr[u + 1]]] = -np.inf
+    return s
+
+
+def masked_topk(scores, k, excl_indptr=None, excl=None, user_base=0):
+    """top-k of the masked similarity rows by (score desc, item asc) (:45-46)."""
+    s = masked_topk_scores(scores, excl_indptr, excl, user_base)
+    out = np.empty((s.shape[0], k), np.int32)
+    items = np.arange(s.shape[1])
+    for r in range(s.shape[0]):
+        out[r] = np.lexsort((items, -s[r].astype(np.float64)))[:k]
+    return out
+
+
+def hit_rate(recs, truth_indptr, truth):
+    """relevance.any(axis=1).mean() (:54-65)."""
+    hits = [np.isin(recs[u], truth[truth_indptr[u]:truth_indptr[u + 1]]).any()
+            for u in range(len(recs))]
+    return float(np.mean(hits)), np.asarray(hits, np.int32)
+
+
+def split_by_time(users, ts):
+    """util.py:5-24: per user sorted by time, last → test (> 1 rating), second-to-last → val
+    (> 2 ratings); ties keep edge order. Returns the three sorted edge-index arrays."""
+    tr, va, te = [], [], []
+    for u in np.unique(users):
+        e = np.nonzero(users == u)[0]
+        e = e[np.argsort(ts[e], kind="stable")]
+        if e.size > 1:
+            te.append(e[-1])
+        if e.size > 2:
+            va.append(e[-2])
+        tr.extend(e[: e.size - min(e.size - 1, 2)] if e.size > 1 else e)
+    return np.sort(np.asarray(tr, np.int64)), np.sort(np.asarray(va, np.int64)), \
+        np.sort(np.asarray(te, np.int64))

@@ -100,6 +100,9 @@ _SIGS = {
     "rs_vocab_collect": (_i32, [_p, _p, _p, _i64, _u32, _p, _p, _p, _p, _sz, _p]),
     "rs_vocab_assign": (_i32, [_p, _i64, _p, _p]),
     "rs_vocab_lookup": (_i32, [_p, _i64, _p, _p, _i64, _p, _p]),
+    "rs_latest_item": (_i32, [_p, _p, _p, _i64, _p, _p, _p]),
+    "rs_masked_topk": (_i32, [_p, _i64, _i32, _i32, _i64, _p, _p, _i32, _p, _p, _p]),
+    "rs_hit_flags": (_i32, [_p, _i64, _i32, _i64, _p, _p, _p, _p]),
     "rs_csr_weight_prefix": (_i32, [_p, _p, _i64, _p, _p]),
     "rs_eges_walks": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _u64, _u32, _p, _p]),
     "rs_skipgram_workspace_size": (_sz, [_i32, _i32, _i32]),

@@ -24,8 +24,11 @@ class _NodeView:
 
 class HeteroGraph:
     def __init__(self, users, items, n_users: int, n_items: int, device="cuda",
-                 item_data: dict | None = None, utype: str = "user", itype: str = "movie"):
-        """users/items: the rating edges (numpy or torch int). Builds both CSRs on device."""
+                 item_data: dict | None = None, utype: str = "user", itype: str = "movie",
+                 edge_data: dict | None = None):
+        """users/items: the rating edges (numpy or torch int). Builds both CSRs on device.
+        edge_data: per-edge columns (e.g. {'timestamp': ...}), kept in u2i CSR order as
+        `g.u2i_edata[name]` (the 'watched' etype's edata, graph_builder.py)."""
         dev = torch.device(device)
         u = torch.as_tensor(np.asarray(users), dtype=torch.int64, device=dev)
         i = torch.as_tensor(np.asarray(items), dtype=torch.int64, device=dev)
@@ -36,6 +39,8 @@ class HeteroGraph:
         key_u = u * self.n_items + i
         _, o = torch.sort(key_u, stable=True)
         self.u2i = i[o].to(torch.int32).contiguous()
+        self.u2i_edata = {k: torch.as_tensor(np.asarray(v), device=dev)[o].contiguous()
+                          for k, v in (edge_data or {}).items()}
         self.u2i_indptr = self._indptr(u, self.n_users)
         key_i = i * self.n_users + u
         _, o = torch.sort(key_i, stable=True)

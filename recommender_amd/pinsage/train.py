@@ -8,8 +8,10 @@ train.py:45-46). Hyper-parameters default to train.py:63-70.
 Multi-GPU: pairs are sharded by global pair index (rank r draws pairs
 [r*B, (r+1)*B) of each step), the graph and tables are replicated, and one bucketed
 all-reduce averages the dense grads together with the densified table grads. Graph
-synthetic: MovieLens-shaped (recommender_amd.synthetic.movielens_graph); no dataset is
-reachable offline, and the hit-rate evaluation (train.py:86-90) is out of this path.
+synthetic: MovieLens-shaped (recommender_amd.synthetic.movielens_graph) with synthetic rating
+times; no dataset is reachable offline. Every `--eval_every` steps (test_steps = 1000,
+train.py:69,84-88) the device evaluation of pinsage/evaluation.py runs: item reprs →
+recommend(top_k 10) → hit-rate against the time-split validation matrix.
 """
 from __future__ import annotations
 
@@ -21,6 +23,8 @@ import torch
 
 from ..optim import KerasAdam, SparseAdam, dedup_grad
 from ..synthetic import ML20M, movielens_graph
+from .evaluation import (build_val_test_matrix, get_item_reprs, hit_rate_eval, recommend,
+                         train_test_split_by_time)
 from .graph import HeteroGraph
 from .model import PinSageModel, margin_loss
 from .sampler import PinSageSampler, item_pairs
@@ -33,6 +37,20 @@ def build_graph(shape: dict, seed: int = 4, device="cuda") -> HeteroGraph:
     users, items, year, genre = movielens_graph(rng, **shape)
     return HeteroGraph(users, items, shape["n_users"], shape["n_items"], device=device,
                        item_data={"year": year, "genre": genre})
+
+
+def build_dataset(shape: dict, seed: int = 4, device="cuda"):
+    """(train_g, val_matrix, test_matrix): the synthetic graph with rating times, split per user
+    by time (util.py:5-39; the reference's process_movielens.py does this offline)."""
+    rng = np.random.default_rng(seed)
+    users, items, year, genre = movielens_graph(rng, **shape)
+    ts = rng.integers(0, 1_000_000_000, users.size)
+    tr, va, te = train_test_split_by_time(users, ts)
+    g = HeteroGraph(users[tr], items[tr], shape["n_users"], shape["n_items"], device=device,
+                    item_data={"year": year, "genre": genre},
+                    edge_data={"timestamp": ts[tr]})
+    val, test = build_val_test_matrix(users, items, va, te, shape["n_users"], shape["n_items"])
+    return g, val, test
 
 
 class PinSageStep:
@@ -91,13 +109,15 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--train_batch_size", type=int, default=32)
     ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--eval_every", type=int, default=1000)
+    ap.add_argument("--top_k", type=int, default=10)
     args = ap.parse_args(argv)
     num_layers = 2
     embedding_size = 8
     conv_hidden_size, conv_output_size = 32, 16
     random_walk_length, num_random_walks, termination_prob, num_neighbors = 2, 4, 0, 3
     torch.manual_seed(args.seed)
-    g = build_graph(ML1M if args.graph == "ml1m" else ML20M, args.seed)
+    g, val_matrix, _ = build_dataset(ML1M if args.graph == "ml1m" else ML20M, args.seed)
     model = PinSageModel(g, g.itype, num_layers, embedding_size, conv_hidden_size,
                          conv_output_size)
     step_fn = PinSageStep(model)
@@ -110,6 +130,10 @@ def main(argv=None):
         loss = step_fn(*batch)
         if step % 50 == 0:
             print(f"step {step} step_loss {float(loss):.4f}")
+        if args.eval_every and step % args.eval_every == 0:
+            reprs = get_item_reprs(model, sampler, g, g.itype, 32)
+            recs = recommend(g, args.top_k, reprs, None, g.utype, "timestamp", 32)
+            print(f"step {step} hit_rate {hit_rate_eval(recs, val_matrix.tocsr()):.4f}")
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print(f"{args.steps / dt:.1f} it/s, {args.steps * args.train_batch_size / dt:.0f} pairs/s")
