@@ -287,10 +287,71 @@ def criteo(iters, out):
            hashes.numel() * 16, out)
 
 
+def textpipe(iters, out):
+    """Ali-CCP join + vocab + encode and Amazon (DIEN) vocab + encode on
+    synthetic text already in HBM, beside the oracle's CPU time for the same text. Algorithmic
+    bytes: every text byte read once + the id / label outputs written once."""
+    import time
+
+    from oracle import textpipe as O
+    from recommender_amd.data import AliCCPVocab, DienVocab, aliccp_join
+    from recommender_amd.data.aliccp import parse_kv_csv
+    from tests.textpipe_text import make_aliccp, make_amazon
+
+    rng = np.random.default_rng(4)
+    sk, cm = make_aliccp(rng, 100_000, 5_000, n_vals=3000)
+    dsk = torch.frombuffer(bytearray(sk.encode()), dtype=torch.uint8).to(DEV)
+    dcm = torch.frombuffer(bytearray(cm.encode()), dtype=torch.uint8).to(DEV)
+    rows = aliccp_join(dsk, dcm)
+    vocab = AliCCPVocab.build(rows)
+
+    def full():
+        r = aliccp_join(dsk, dcm)
+        v = AliCCPVocab.build(r)
+        return v.encode(r)
+
+    us = timed(full, max(3, iters // 4))
+    t0 = time.perf_counter()
+    orows = O.aliccp_join(sk, cm)
+    O.aliccp_encode(orows, O.aliccp_vocab(orows))
+    cpu_s = time.perf_counter() - t0
+    nbytes = dsk.numel() + dcm.numel() + rows.n * (18 * 4 + 8)
+    cfg = {"skeleton_lines": sk.count("\n"), "common_lines": cm.count("\n"), "kept": rows.n,
+           "text_MB": round((dsk.numel() + dcm.numel()) / 1e6, 1), "vocab": sum(vocab.sizes),
+           "oracle_cpu_s": round(cpu_s, 3),
+           "includes": "parse both files, map, join, count, collect, sort, assign, encode; 6 host syncs"}
+    report("aliccp_pipeline(device csv->ids)", cfg, us, nbytes, out)
+    us = timed(lambda: parse_kv_csv(dsk, 3, 5, True), iters)
+    report("rs_kv_parse(skeleton, incl. line index)", {"lines": cfg["skeleton_lines"]}, us,
+           dsk.numel() + rows.n * 18 * 9, out)
+
+    text = make_amazon(rng, 100_000, n_items=60_000, n_cats=800, max_hist=100)
+    dt = torch.frombuffer(bytearray(text.encode()), dtype=torch.uint8).to(DEV)
+    v = DienVocab.build(dt)
+
+    def dien_full():
+        vv = DienVocab.build(dt)
+        return vv.encode(dt, 100, sample_negative=True, seed=4)
+
+    us = timed(dien_full, max(3, iters // 4))
+    t0 = time.perf_counter()
+    items, cats, i2c = O.dien_vocab(text)
+    O.dien_encode(text, items, cats, 100)
+    cpu_s = time.perf_counter() - t0
+    n = text.count("\n")
+    nbytes = dt.numel() + n * (4 * 100 * 4 + 12)
+    cfg = {"lines": n, "maxlen": 100, "text_MB": round(dt.numel() / 1e6, 1),
+           "items": v.items.size, "cats": v.cats.size, "oracle_cpu_s_without_negatives": round(cpu_s, 3),
+           "includes": "parse (2 passes), 2 vocab builds, item->cat map, encode + negatives; 5 host syncs"}
+    report("dien_pipeline(device text->ids)", cfg, us, nbytes, out)
+    us = timed(lambda: v.encode(dt, 100, sample_negative=True, seed=4), iters)
+    report("dien_encode(device text->ids, vocab built)", {"lines": n}, us, nbytes, out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", default="dien,pinsage,pinsage_eval,eges,eges_sampler,embedding,criteo")
+    ap.add_argument("--only", default="dien,pinsage,pinsage_eval,eges,eges_sampler,embedding,criteo,textpipe")
     args = ap.parse_args()
     L.load()
     out = []

@@ -442,6 +442,81 @@ int32_t rs_hit_flags(const int32_t* recs, int64_t n_rows, int32_t k, int64_t use
                      const int64_t* truth_indptr, const int32_t* truth_items, int32_t* hit,
                      void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Ali-CCP and Amazon (DIEN) text → ids (esmm/process_public_dataset.py:40-153,
+ * dien/util.py:4-37, dien/data_loader.py:27-63). Lines come from rs_line_index; each line is
+ * str.strip()ped as the reference does.
+ * rs_vocab_count_masked: rs_vocab_count over the entries with present[i] != 0.
+ * rs_kv_parse: CSV line, field kv_field holds re.split('\x01|\x02|\x03') (field, value, weight)
+ *   triples; vals [n_lines, n_cols] = FNV-1a 64 of the LAST value of field col_hashes[c]
+ *   (dict(zip) semantics), present [n_lines, n_cols]; key_hash [n_lines] = hash of field
+ *   key_field (may be NULL); with_labels: labels [n_lines, 2] = int fields 1, 2 and keep = not
+ *   (field 1 == "0" and field 2 == "1") (:56). A line with too few fields sets RS_ERRBIT_OOB.
+ * rs_map_insert: key_hash[i] → i in a (keys ~0, vals -1 filled) table; a later i wins.
+ * rs_aliccp_join: kept skeleton lines compacted in order (*n_kept): out_keys [n_kept, n_cols] =
+ *   (column, value) hash with the common line's value overriding (:60), '0' when absent;
+ *   out_present; out_labels [n_kept, 2]. An unknown common id sets RS_ERRBIT_OOB (KeyError).
+ * rs_vocab_regroup: sort_key = (first % n_groups) * per_group + first / n_groups, group.
+ * rs_vocab_assign_grouped: ids[slots[order[r]]] = id_base + r - (first rank of r's group); order
+ *   and group may be NULL (identity order, one group).
+ * rs_vocab_lookup_i32: ids as int32, oov_id when absent (RS_ERRBIT_OOB too if err_on_oov).
+ * rs_dien_parse: line "label\tuser\titem\tcat\this_items\this_cats", histories '\x02'-separated.
+ *   Count pass (item_off NULL): n_hi, n_hc [n_lines] token counts, label. Fill pass: item_hash at
+ *   item_off[l] (target) and item_off[l] + 1 + k (history k), cat_hash likewise at cat_off.
+ * rs_dien_item_cat: cat_of_item[id] = cat id of the item's LAST (item, cat) pair in the stream
+ *   (target pair, then zip(history)), -1 for an item without one.
+ * rs_dien_encode: target_item / his_item ids (unknown → unk_item), target_cat / his_cat (unknown →
+ *   0 + RS_ERRBIT_OOB, the reference's KeyError); histories keep the LAST maxlen tokens, zero-padded
+ *   after (pad_sequences padding='post', truncating='pre'); neg_item (may be NULL) = 1 +
+ *   U[0, n_item_ids - 1) by Philox (seed, line_base + l, position), neg_cat = cat_of_item. */
+int32_t rs_vocab_count_masked(const uint64_t* hashes, const uint8_t* present, int64_t n,
+                              int64_t pos_base, uint64_t* keys, uint32_t* counts,
+                              uint64_t* first_pos, int64_t capacity, int32_t* err_flag,
+                              void* stream);
+int32_t rs_kv_parse(const uint8_t* text, int64_t n_bytes, const int64_t* line_starts,
+                    int64_t n_lines, int32_t key_field, int32_t kv_field, int32_t with_labels,
+                    const uint64_t* col_hashes, int32_t n_cols, uint64_t* key_hash, int32_t* keep,
+                    int32_t* labels, uint64_t* vals, uint8_t* present, int32_t* err_flag,
+                    void* stream);
+int32_t rs_map_insert(const uint64_t* key_hash, int64_t n, uint64_t* keys, int32_t* vals,
+                      int64_t capacity, int32_t* err_flag, void* stream);
+size_t rs_aliccp_join_workspace_size(int64_t n_lines);
+int32_t rs_aliccp_join(const int32_t* keep, int64_t n_lines, int32_t n_cols,
+                       const uint64_t* common_id, const uint64_t* skel_vals,
+                       const uint8_t* skel_present, const int32_t* skel_labels,
+                       const uint64_t* map_keys, const int32_t* map_vals, int64_t map_capacity,
+                       const uint64_t* common_vals, const uint8_t* common_present,
+                       uint64_t* out_keys, uint8_t* out_present, int32_t* out_labels,
+                       int32_t* n_kept, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                       void* stream);
+int32_t rs_vocab_regroup(const uint64_t* first_pos, int64_t n, int32_t n_groups, int64_t per_group,
+                         int64_t* sort_key, int32_t* group, void* stream);
+int32_t rs_vocab_assign_grouped(const int32_t* order, const int32_t* slots, const int32_t* group,
+                                int64_t n_kept, int32_t id_base, int32_t* ids, void* stream);
+int32_t rs_vocab_lookup_i32(const uint64_t* hashes, int64_t n, const uint64_t* keys,
+                            const int32_t* ids, int64_t capacity, int32_t oov_id,
+                            int32_t err_on_oov, int32_t* out, int32_t* err_flag, void* stream);
+int32_t rs_dien_parse(const uint8_t* text, int64_t n_bytes, const int64_t* line_starts,
+                      int64_t n_lines, const int64_t* item_off, const int64_t* cat_off,
+                      int32_t* n_hi, int32_t* n_hc, float* label, uint64_t* item_hash,
+                      uint64_t* cat_hash, int32_t* err_flag, void* stream);
+size_t rs_dien_item_cat_workspace_size(int64_t item_capacity);
+int32_t rs_dien_item_cat(const uint64_t* item_hash, const uint64_t* cat_hash,
+                         const int64_t* item_off, const int64_t* cat_off, const int32_t* n_hi,
+                         const int32_t* n_hc, int64_t n_lines, const uint64_t* item_keys,
+                         const int32_t* item_ids, int64_t item_capacity, const uint64_t* cat_keys,
+                         const int32_t* cat_ids, int64_t cat_capacity, int32_t* cat_of_item,
+                         void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_dien_encode(const uint64_t* item_hash, const uint64_t* cat_hash,
+                       const int64_t* item_off, const int64_t* cat_off, const int32_t* n_hi,
+                       const int32_t* n_hc, int64_t n_lines, const uint64_t* item_keys,
+                       const int32_t* item_ids, int64_t item_capacity, int32_t unk_item,
+                       const uint64_t* cat_keys, const int32_t* cat_ids, int64_t cat_capacity,
+                       int32_t maxlen, const int32_t* cat_of_item, int32_t n_item_ids,
+                       uint64_t seed, int64_t line_base, int32_t* target_item, int32_t* target_cat,
+                       int32_t* his_item, int32_t* his_cat, int32_t* neg_item, int32_t* neg_cat,
+                       int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

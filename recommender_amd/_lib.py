@@ -108,6 +108,22 @@ _SIGS = {
     "rs_skipgram_workspace_size": (_sz, [_i32, _i32, _i32]),
     "rs_skipgram_pairs": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_log_uniform_sample": (_i32, [_p, _i32, _i64, _i32, _i32, _u64, _u32, _p, _p, _p]),
+    "rs_vocab_count_masked": (_i32, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
+    "rs_kv_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p,
+                           _p, _p]),
+    "rs_map_insert": (_i32, [_p, _i64, _p, _p, _i64, _p, _p]),
+    "rs_aliccp_join_workspace_size": (_sz, [_i64]),
+    "rs_aliccp_join": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p,
+                              _p, _p, _p, _sz, _p]),
+    "rs_vocab_regroup": (_i32, [_p, _i64, _i32, _i64, _p, _p, _p]),
+    "rs_vocab_assign_grouped": (_i32, [_p, _p, _p, _i64, _i32, _p, _p]),
+    "rs_vocab_lookup_i32": (_i32, [_p, _i64, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_dien_parse": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "rs_dien_item_cat_workspace_size": (_sz, [_i64]),
+    "rs_dien_item_cat": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _p,
+                                _sz, _p]),
+    "rs_dien_encode": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _i64, _i32, _p, _p, _i64,
+                              _i32, _p, _i32, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
 }
 
 _lib = None

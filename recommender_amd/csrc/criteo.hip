@@ -14,6 +14,7 @@
 //   lookup          id of every token, 0 when absent (OOV → 0, tfrecord_io.py:64-67)
 // Token identity is a 64-bit hash (collision odds ~N²/2^65, ~3e-5 for 33M distinct tokens).
 #include "common.hpp"
+#include "hashtab.hpp"
 
 namespace rs {
 
@@ -22,15 +23,6 @@ int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
 size_t exclusive_scan_ws_size(int64_t n);
 
 constexpr int kLineBlock = 4096;  // bytes per newline-count block
-constexpr uint64_t kFnvBasis = 1469598103934665603ull;
-constexpr uint64_t kFnvPrime = 1099511628211ull;
-constexpr uint64_t kEmptySlot = ~0ull;
-
-__device__ __forceinline__ uint64_t fnv1a(const uint8_t* p, int n) {
-  uint64_t h = kFnvBasis;
-  for (int i = 0; i < n; ++i) h = (h ^ p[i]) * kFnvPrime;
-  return h;
-}
 
 // the imputation token of an empty categorical field in column c (deterministic stand-in for
 // the reference's random 10-character string per column)
@@ -154,30 +146,27 @@ __global__ __launch_bounds__(256) void criteo_parse_kernel(
   }
 }
 
-__device__ __forceinline__ uint32_t vslot(uint64_t key, uint32_t mask) {
-  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & mask;
-}
 
+// one table insert + one atomicAdd / atomicMin per distinct key of the wave (wave_key_group);
+// the group's lowest lane holds its first position (positions ascend with the lane)
 __global__ __launch_bounds__(256) void vocab_count_kernel(const uint64_t* __restrict__ hashes,
+                                                          const uint8_t* __restrict__ present,
                                                           int64_t n, int64_t pos_base,
                                                           uint64_t* keys, uint32_t* counts,
                                                           unsigned long long* first,
                                                           uint32_t mask, int32_t* err_flag) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t key = hashes[i] == kEmptySlot ? kEmptySlot - 1 : hashes[i];
-  uint32_t h = vslot(key, mask);
-  for (uint32_t probe = 0; probe <= mask; ++probe) {
-    const unsigned long long prev =
-        atomicCAS(reinterpret_cast<unsigned long long*>(keys + h), kEmptySlot, key);
-    if (prev == kEmptySlot || prev == key) {
-      atomicAdd(counts + h, 1u);
-      atomicMin(first + h, (unsigned long long)(pos_base + i));
-      return;
-    }
-    h = (h + 1) & mask;
+  const bool act = i < n && (!present || present[i]);
+  const uint64_t key = act ? table_key(hashes[i]) : 0;
+  const uint64_t grp = wave_key_group(key, act);
+  if (!act || __builtin_ctzll(grp) != (int)__lane_id()) return;
+  const int64_t h = table_insert(keys, mask, key);
+  if (h < 0) {
+    flag_oob(err_flag);  // table full
+    return;
   }
-  flag_oob(err_flag);  // table full
+  atomicAdd(counts + h, (uint32_t)__popcll(grp));
+  atomicMin(first + h, (unsigned long long)(pos_base + i));
 }
 
 // slots whose count > min_count: (first position, slot) pairs, compacted in slot order
@@ -214,19 +203,8 @@ __global__ __launch_bounds__(256) void vocab_lookup_kernel(const uint64_t* __res
                                                            uint32_t mask, int64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t key = hashes[i] == kEmptySlot ? kEmptySlot - 1 : hashes[i];
-  uint32_t h = vslot(key, mask);
-  int64_t id = 0;  // OOV → 0
-  for (uint32_t probe = 0; probe <= mask; ++probe) {
-    const uint64_t k = keys[h];
-    if (k == key) {
-      id = ids[h] >= 0 ? ids[h] : 0;
-      break;
-    }
-    if (k == kEmptySlot) break;
-    h = (h + 1) & mask;
-  }
-  out[i] = id;
+  const int64_t h = table_find(keys, mask, hashes[i]);
+  out[i] = (h >= 0 && ids[h] >= 0) ? ids[h] : 0;  // OOV → 0
 }
 
 inline unsigned grid256(int64_t n) { return (unsigned)ceil_div(n < 1 ? 1 : n, 256); }
@@ -289,7 +267,21 @@ extern "C" int32_t rs_vocab_count(const uint64_t* hashes, int64_t n, int64_t pos
                "rs_vocab_count: capacity must be a power of two");
   if (n == 0) return RS_OK;
   vocab_count_kernel<<<grid256(n), 256, 0, as_stream(stream)>>>(
-      hashes, n, pos_base, keys, counts, reinterpret_cast<unsigned long long*>(first_pos),
+      hashes, nullptr, n, pos_base, keys, counts, reinterpret_cast<unsigned long long*>(first_pos),
+      (uint32_t)(capacity - 1), err_flag);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_vocab_count_masked(const uint64_t* hashes, const uint8_t* present, int64_t n,
+                                         int64_t pos_base, uint64_t* keys, uint32_t* counts,
+                                         uint64_t* first_pos, int64_t capacity, int32_t* err_flag,
+                                         void* stream) {
+  RS_CHECK_ARG(capacity >= 2 && (capacity & (capacity - 1)) == 0 && capacity <= ((int64_t)1 << 32),
+               "rs_vocab_count_masked: capacity must be a power of two");
+  if (n == 0) return RS_OK;
+  vocab_count_kernel<<<grid256(n), 256, 0, as_stream(stream)>>>(
+      hashes, present, n, pos_base, keys, counts, reinterpret_cast<unsigned long long*>(first_pos),
       (uint32_t)(capacity - 1), err_flag);
   RS_CHECK_LAUNCH();
   return RS_OK;

@@ -13,28 +13,14 @@ the reference's read_tfrecord yields (tfrecord_io.py:78-96), already on the devi
 """
 from __future__ import annotations
 
-import os
-
-import numpy as np
 import torch
 
 from .. import _lib as L
 from ..optim import SortedIds
+from .text import line_index, pow2_at_least, text_to_device
 
 NUM_INT, NUM_CAT = 13, 26
 MIN_COUNT = 10  # count > 10 (tfrecord_io.py:33)
-
-
-def _text_to_device(src, device) -> torch.Tensor:
-    if isinstance(src, torch.Tensor):
-        return src.to(device=device, dtype=torch.uint8).contiguous()
-    if isinstance(src, (str, os.PathLike)):
-        data = np.fromfile(src, dtype=np.uint8)
-    elif isinstance(src, (bytes, bytearray)):
-        data = np.frombuffer(bytes(src), dtype=np.uint8)
-    else:
-        data = np.asarray(src, dtype=np.uint8)
-    return torch.from_numpy(data).pin_memory().to(device, non_blocking=True)
 
 
 def read_criteo_tsv(src, device="cuda"):
@@ -42,20 +28,13 @@ def read_criteo_tsv(src, device="cuda"):
     (label [n] f32, dense [n, 13] f32, token hashes [n, 26] uint64 as int64, n_lines).
     One host sync sizes the line index (the newline count)."""
     dev = torch.device(device)
-    text = _text_to_device(src, dev)
+    text = text_to_device(src, dev)
     n_bytes = text.numel()
     if n_bytes == 0:
         z = torch.zeros(0, device=dev)
         return z, z.view(0, NUM_INT), torch.zeros(0, NUM_CAT, dtype=torch.int64, device=dev), 0
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = torch.empty(L.lib().rs_line_index_workspace_size(n_bytes), dtype=torch.uint8, device=dev)
+    starts, n_lines = line_index(text)
     st = L.stream_ptr(dev)
-    L.call("rs_line_index", L.ptr(text), n_bytes, None, L.ptr(cnt), L.ptr(ws), ws.numel(), st)
-    info = torch.stack([cnt[0], text[-1].to(torch.int32)]).cpu()
-    n_nl, last_byte = int(info[0]), int(info[1])
-    n_lines = n_nl if last_byte == 10 else n_nl + 1
-    starts = torch.empty(n_nl + 1, dtype=torch.int64, device=dev)
-    L.call("rs_line_index", L.ptr(text), n_bytes, L.ptr(starts), L.ptr(cnt), L.ptr(ws), ws.numel(), st)
     label = torch.empty(n_lines, device=dev)
     dense = torch.empty(n_lines, NUM_INT, device=dev)
     hashes = torch.empty(n_lines, NUM_CAT, dtype=torch.int64, device=dev)
@@ -65,13 +44,6 @@ def read_criteo_tsv(src, device="cuda"):
     if int(err.item()):
         raise ValueError("malformed Criteo line (field count != 40)")
     return label, dense, hashes, n_lines
-
-
-def _pow2_at_least(n: int) -> int:
-    c = 2
-    while c < n:
-        c <<= 1
-    return c
 
 
 class CriteoVocab:
@@ -87,7 +59,7 @@ class CriteoVocab:
         n_tok = n_lines * NUM_CAT
         if n_tok >= (1 << 31):
             raise ValueError("train file too large for one pass (positions are int32 keys)")
-        cap = _pow2_at_least(max(2 * n_tok, 1024))
+        cap = pow2_at_least(max(2 * n_tok, 1024))
         keys = torch.full((cap,), -1, dtype=torch.int64, device=dev)  # 0xFF.. = empty slot
         counts = torch.zeros(cap, dtype=torch.int32, device=dev)
         first = torch.full((cap,), -1, dtype=torch.int64, device=dev)
