@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from recommender_amd import _lib as L  # noqa: E402
+from recommender_amd.ctr.layers import MLP  # noqa: E402
 from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
@@ -57,6 +58,10 @@ def parse():
     ap.add_argument("--fused", type=int, default=1, help="fused side-stream sparse optimizer")
     ap.add_argument("--prio", type=int, default=0,
                     help="1: run the step on a high-priority HIP stream (side-stream work fills in)")
+    ap.add_argument("--mlp-bwd", default="factored", choices=["factored", "layerwise"],
+                    help="ctr MLP backward: factored linear chain (default) or layer by layer")
+    ap.add_argument("--compare-layerwise", type=int, default=1,
+                    help="1: after the timed steps, also time the layer-by-layer MLP backward")
     ap.add_argument("--pmc", type=int, default=1,
                     help="1: measure the roofline kernel's HBM traffic with two rocprofv3 --pmc "
                          "child runs (FETCH_SIZE, WRITE_SIZE) before this process touches the GPU")
@@ -85,7 +90,7 @@ def measure_traffic(args):
              "--cpu-baseline-steps", "0", "--pmc", "0", "--batch", str(args.batch), "--rows",
              str(args.rows), "--dim", str(args.dim), "--slots", str(args.slots), "--optimizer",
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
-             str(args.fused)]
+             str(args.fused), "--mlp-bwd", args.mlp_bwd, "--compare-layerwise", "0"]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -213,6 +218,7 @@ def cpu_baseline(args, cards):
 
 def main():
     args = parse()
+    MLP.factored_backward = args.mlp_bwd == "factored"
     traffic, traffic_detail = None, None
     if args.pmc and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         traffic, traffic_detail = measure_traffic(args)  # before any GPU initialisation
@@ -280,6 +286,28 @@ def main():
     ms_step = wall / args.steps * 1e3
     value = args.batch * world * args.steps / wall
 
+    # the same steps with the layer-by-layer MLP backward (reference evaluation order), for the
+    # record: same model, same batches, timed the same way
+    layerwise_ms = None
+    if args.compare_layerwise and args.mlp_bwd == "factored" and not args.graph:
+        MLP.factored_backward = False
+        for i in range(2):
+            step(pool[i % len(pool)])
+        torch.cuda.synchronize()
+        barrier(world)
+        ta = time.perf_counter()
+        for i in range(args.steps):
+            step(pool[i % len(pool)])
+        torch.cuda.synchronize()
+        barrier(world)
+        lw = time.perf_counter() - ta
+        if world > 1:
+            tt = torch.tensor([lw], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            lw = float(tt.item())
+        layerwise_ms = round(lw / args.steps * 1e3, 3)
+        MLP.factored_backward = True
+
     tot = timer.totals_ms()
     kern = {}
     for name, (ms, cnt) in tot.items():
@@ -328,6 +356,12 @@ def main():
                        "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
                        "optimizer": args.optimizer,
                        "parallelism": f"row-sharded slab x{world} (RCCL all-to-all) + dp{world} MLPs" if world > 1 else "single"},
+            "mlp_backward": {"mode": args.mlp_bwd,
+                             "note": "ctr MLP hidden layers are linear (ctr/layers.py:8); the factored "
+                                     "backward takes every layer's gradient from the last layer's "
+                                     "(same gradients in exact arithmetic, fp32 summation order differs; "
+                                     "tests/test_mlp_chain_gpu.py); forward is layer by layer",
+                             "ms_per_step_layerwise_bwd": layerwise_ms},
             "roofline": roof, "embedding_path": emb_path, "kernels": kern,
             "cpu_baseline": cpu, "loss": float(loss.item()),
         }

@@ -348,6 +348,64 @@ def textpipe(iters, out):
     report("dien_encode(device text->ids, vocab built)", {"lines": n}, us, nbytes, out)
 
 
+def dlrm_path(iters, out):
+    """The north-star embedding path's four launches run alone and back to back on one stream
+    (no co-running GEMMs), at the bench config: 26 slots over a 40M x 128 fp32 slab, batch
+    65 536, Zipf ids. SGD with lr 0 so repeated applies move the same bytes without drifting.
+    Bytes: SURVEY §8(d) per-kernel formulas (bench.py kernel_bytes); path = §8(d) whole-path."""
+    from bench import kernel_bytes
+    from recommender_amd.optim import SortedIds
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    S, D, B, V = 26, 128, 65536, 40_000_000
+    cards = criteo_cardinalities(V, S)
+    so = torch.tensor(np.concatenate([[0], np.cumsum(cards)]), dtype=torch.int64, device=DEV)
+    table = torch.empty(V, D, device=DEV)
+    table.uniform_(-0.05, 0.05)
+    cat, _, _ = criteo_batch(np.random.default_rng(4), B, cards)
+    ids = torch.from_numpy(cat).to(DEV)
+    dense = torch.randn(B, D, device=DEV)
+    Z = 27 * 26 // 2 + D
+    inter = torch.empty(B, 512, device=DEV)
+    gout = torch.randn(B, 512, device=DEV) * 1e-3
+    gemb = torch.empty(B * S, D, device=DEV)
+    gden = torch.empty(B, D, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    st = L.stream_ptr(torch.device(DEV))
+    s0 = SortedIds(ids, V, so, err, count_unique=True)
+    U = int(s0.n_unique.item())
+    ws = torch.empty(L.lib().rs_apply_workspace_size(B * S, D), dtype=torch.uint8, device=DEV)
+    prm = L.AdamParams(0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+
+    def fwd():
+        L.call("rs_dlrm_interaction_fwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
+               L.ptr(dense), B, 1, L.ptr(inter), 512, L.ptr(err), st)
+
+    def srt():
+        return SortedIds(ids, V, so, err, count_unique=False)
+
+    def bwd():
+        L.call("rs_dlrm_interaction_bwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
+               L.ptr(dense), B, 1, L.ptr(gout), 512, L.ptr(gemb), L.ptr(gden), st)
+
+    def apply():
+        L.call("rs_embedding_apply", L.RS_OPT_SGD, L.ptr(table), None, None, V, D, L.ptr(s0.rows),
+               L.ptr(s0.pos), B * S, L.ptr(gemb), prm, None, L.ptr(ws), ws.numel(), st)
+
+    bwd()
+    tot = 0.0
+    for name, fn in (("rs_dlrm_interaction_fwd", fwd), ("rs_sort_ids", srt),
+                     ("rs_dlrm_interaction_bwd", bwd), ("rs_embedding_apply", apply)):
+        us = timed(fn, iters)
+        tot += us
+        report(name + " (alone)", {"B": B, "S": S, "D": D, "rows": V, "unique": U}, us,
+               kernel_bytes(name, B, S, D, 8, U), out)
+    per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
+    report("embedding_path (4 launches back to back, alone)",
+           {"B": B, "S": S, "D": D, "unique": U, "bytes_per_example": round(per_ex, 1)},
+           tot, per_ex * B, out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)

@@ -7,13 +7,21 @@ ctr/layers.py:23-43, computed by the gfx950 MFMA kernel rs_dot_interaction_fwd/b
 """
 from __future__ import annotations
 
+import torch
 from torch import nn
 
 from ..functional import dot_interaction
-from ..nn import Dense
+from ..nn import Dense, linear_chain
 
 
 class MLP(nn.Module):
+    """factored_backward=True (default): the hidden layers are linear, so the backward runs as
+    one linear chain (nn._LinearChainFn: every layer's gradient from the last layer's, no
+    full-width dgrad GEMMs). False: layer-by-layer autograd. The forward is layerwise either
+    way and bit-identical between the two."""
+
+    factored_backward = True
+
     def __init__(self, units, final_activation, in_features=None, device=None, generator=None):
         super().__init__()
         layers = []
@@ -25,8 +33,15 @@ class MLP(nn.Module):
                             generator=generator))
         self.mlp = nn.ModuleList(layers)
 
-    def forward(self, x):
-        for layer in self.mlp:
+    def forward(self, x, rows=None):
+        """rows: optional index of first-layer kernel rows the input holds (DLRM compact row)."""
+        layers = list(self.mlp)
+        if (self.factored_backward and x.dim() == 2 and x.is_cuda and torch.is_grad_enabled()
+                and all(l.kernel is not None and l.act_code >= 0 for l in layers)
+                and all(l.act_code == 0 for l in layers[:-1])):
+            return linear_chain(x, layers, rows)
+        x = layers[0](x, rows=rows)
+        for layer in layers[1:]:
             x = layer(x)
         return x
 

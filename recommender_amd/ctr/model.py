@@ -107,11 +107,7 @@ class DLRM(nn.Module):
             out = self.top_mlp(tmlp_input).squeeze(1)
         else:
             tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
-            first = self.top_mlp.mlp[0]
-            h = first(tmlp_input, rows=self.compact_rows)
-            for layer in self.top_mlp.mlp[1:]:
-                h = layer(h)
-            out = h.squeeze(1)
+            out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)
         # forward kernels are queued: the side-stream sort now runs beside them
         self.embedding_layer.presort(cat_features)
         return out

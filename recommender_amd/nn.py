@@ -216,6 +216,84 @@ class _DenseFn(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+class _LinearChainFn(torch.autograd.Function):
+    """A chain of Dense layers whose hidden layers are linear (ctr/layers.py:8: the reference's
+    ctr MLP puts no activation on hidden layers), y = act(h_{L-1}·K_L + b_L),
+    h_l = h_{l-1}·K_l + b_l. The forward is evaluated layer by layer, exactly as the layerwise
+    path (bit-identical outputs). The backward uses that every upstream gradient of a linear
+    chain is the last layer's gradient G = act'(y)⊙dy pushed through a fixed matrix:
+        g_l = G·Q_lᵀ with Q_l = K_{l+1}···K_L  ([n_l, n_L]),
+        dK_l = h_{l-1}ᵀ·g_l = (h_{l-1}ᵀ·G)·Q_lᵀ,   db_l = (Σ_b G)·Q_lᵀ,   dx = G·Q_0ᵀ.
+    The same gradients in exact arithmetic, with one K = batch reduction of width n_L per layer
+    instead of a full-width dgrad + wgrad GEMM pair: for DLRM's top MLP (n_L = 1) every batch-
+    sized product becomes a GEMV. Only the fp32 summation order differs (like any GEMM tiling)."""
+
+    @staticmethod
+    def forward(ctx, x, handle, layers, rows):
+        hs = [x]
+        h = x
+        last = len(layers) - 1
+        ks = []
+        for i, layer in enumerate(layers):
+            k = layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
+            ks.append(k)
+            h = torch.addmm(layer.bias, h, k) if layer.bias is not None else h @ k
+            if i == last:
+                if layer.act_code == 1:
+                    h = torch.relu_(h)
+                elif layer.act_code == 2:
+                    h = torch.sigmoid_(h)
+            else:
+                hs.append(h)
+        ctx.layers, ctx.rows = layers, rows
+        ctx.save_for_backward(h if layers[-1].act_code else None, *hs, *ks)
+        return h
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib as L
+
+        layers, rows = ctx.layers, ctx.rows
+        n = len(layers)
+        saved = ctx.saved_tensors
+        y, hs, ks = saved[0], saved[1:1 + n], saved[1 + n:]
+        last = layers[-1]
+        dy = dy.contiguous()
+        B, fo = dy.shape
+        act = last.act_code
+        db = None
+        if act or last.bias is not None:
+            G = torch.empty_like(dy) if act else dy
+            db = torch.empty(fo, device=dy.device, dtype=torch.float32)
+            ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, fo) // 4),
+                             device=dy.device)
+            L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, fo, act, L.ptr(G), L.ptr(db),
+                   L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
+        else:
+            G = dy
+        Q = None  # K_{l+1}···K_L
+        for i in range(n - 1, -1, -1):
+            layer = layers[i]
+            M = wgrad(hs[i], G)                       # h_{l-1}ᵀ·G   [n_{l-1}, n_L]
+            dk = M if Q is None else M @ Q.t()
+            if i == 0 and rows is not None:
+                full = torch.zeros_like(layer.kernel)
+                full.index_copy_(0, rows, dk)
+                dk = full
+            _accum_grad(layer.kernel, dk)
+            if layer.bias is not None and db is not None:
+                _accum_grad(layer.bias, db if Q is None else db @ Q.t())
+            Q = ks[i] if Q is None else ks[i] @ Q
+        dx = G @ Q.t() if ctx.needs_input_grad[0] else None
+        return dx, None, None, None
+
+
+def linear_chain(x, layers, rows=None, handle=None):
+    """y of a Dense chain with linear hidden layers (see _LinearChainFn)."""
+    return _LinearChainFn.apply(x, handle if handle is not None else layers[-1]._handle(),
+                                layers, rows)
+
+
 class Dense(nn.Module):
     def __init__(self, units: int, activation=None, use_bias: bool = True, in_features=None,
                  device=None, generator: torch.Generator | None = None):
