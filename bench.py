@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--fused", type=int, default=1, help="fused side-stream sparse optimizer")
     ap.add_argument("--prio", type=int, default=0,
                     help="1: run the step on a high-priority HIP stream (side-stream work fills in)")
+    ap.add_argument("--defer-join", type=int, default=1,
+                    help="1: the sparse update joins at the next step's first table read "
+                         "(overlaps the next bottom MLP) instead of at the end of the step")
     ap.add_argument("--mlp-bwd", default="factored", choices=["factored", "layerwise"],
                     help="ctr MLP backward: factored linear chain (default) or layer by layer")
     ap.add_argument("--compare-layerwise", type=int, default=1,
@@ -90,7 +93,7 @@ def measure_traffic(args):
              "--cpu-baseline-steps", "0", "--pmc", "0", "--batch", str(args.batch), "--rows",
              str(args.rows), "--dim", str(args.dim), "--slots", str(args.slots), "--optimizer",
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
-             str(args.fused), "--mlp-bwd", args.mlp_bwd, "--compare-layerwise", "0"]
+             str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd, "--compare-layerwise", "0"]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -248,7 +251,7 @@ def main():
         model = build_model("DLRM", D, args.rows, S, 13, dev, slot_cardinalities=cards,
                             bottom=[512, 256, D], top=[512, 256, 1], generator=g)
     step = TrainStep(model, args.optimizer, lr=0.01 if args.optimizer == "sgd" else 1e-3,
-                     fused=bool(args.fused), comm=comm)
+                     fused=bool(args.fused), comm=comm, defer_sparse_join=bool(args.defer_join))
     pool = make_pool(args, cards, rank, dev)
     U = measured_unique(pool, model)
 

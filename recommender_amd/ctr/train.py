@@ -32,7 +32,7 @@ class TrainStep:
     """One optimizer step of a ctr model: forward, BCE, backward, dense + sparse apply."""
 
     def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
-                 fused=True, overlap_wgrad=False, comm=None):
+                 fused=True, overlap_wgrad=False, comm=None, defer_sparse_join=False):
         """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
         all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
         by its owners inside the backward."""
@@ -54,13 +54,13 @@ class TrainStep:
         if optimizer == "sgd":
             lr = sched or (lr if lr is not None else 0.01)
             self.opt_dense = torch.optim.SGD(dense, lr=lr if not callable(lr) else lr(0))
-            self.opt_sparse = SparseSGD(tables, lr=lr, fused=fused)
+            self.opt_sparse = SparseSGD(tables, lr=lr, fused=fused, defer_join=defer_sparse_join)
             self._sched = lr if callable(lr) else None
         elif optimizer in ("keras_adam", "lazy_adam"):
             lr = lr if lr is not None else 1e-3
             self.opt_dense = KerasAdam(dense, lr=lr)
             self.opt_sparse = SparseAdam(tables, lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy",
-                                         fused=fused)
+                                         fused=fused, defer_join=defer_sparse_join)
             self._sched = None
         else:
             raise ValueError(f"unknown optimizer {optimizer}")

@@ -47,6 +47,15 @@ class Embedding(nn.Module):
         # its side stream ahead of the dense forward, the apply inside the backward
         self.fused_optimizer = None
         self._presorted = None
+        # deferred join (SparseOptimizer(defer_join=True)): the event the next table read waits on
+        self._pending_update = None
+
+    def wait_update(self):
+        """Order the current stream after a deferred sparse update of this table (no-op when
+        none is pending). Every kernel that reads the table calls this first."""
+        ev, self._pending_update = self._pending_update, None
+        if ev is not None:
+            torch.cuda.current_stream(self.weight.device).wait_event(ev)
 
     @property
     def n_slots(self) -> int:

@@ -26,6 +26,7 @@ def _ids_flat(ids: torch.Tensor) -> torch.Tensor:
 class _EmbeddingLookup(torch.autograd.Function):
     @staticmethod
     def forward(ctx, handle, table_module, ids):
+        table_module.wait_update()
         w = table_module.weight
         L.require_device(w, "embedding table")
         ids = _ids_flat(ids)
@@ -93,6 +94,7 @@ class _DLRMInteraction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, handle, dense, table_module, ids, compact):
+        table_module.wait_update()
         w = table_module.weight
         L.require_device(w, "embedding table")
         ids = _ids_flat(ids)

@@ -218,19 +218,23 @@ class _DenseFn(torch.autograd.Function):
 
 class _LinearChainFn(torch.autograd.Function):
     """A chain of Dense layers whose hidden layers are linear (ctr/layers.py:8: the reference's
-    ctr MLP puts no activation on hidden layers), y = act(h_{L-1}·K_L + b_L),
-    h_l = h_{l-1}·K_l + b_l. The forward is evaluated layer by layer, exactly as the layerwise
-    path (bit-identical outputs). The backward uses that every upstream gradient of a linear
-    chain is the last layer's gradient G = act'(y)⊙dy pushed through a fixed matrix:
-        g_l = G·Q_lᵀ with Q_l = K_{l+1}···K_L  ([n_l, n_L]),
-        dK_l = h_{l-1}ᵀ·g_l = (h_{l-1}ᵀ·G)·Q_lᵀ,   db_l = (Σ_b G)·Q_lᵀ,   dx = G·Q_0ᵀ.
-    The same gradients in exact arithmetic, with one K = batch reduction of width n_L per layer
-    instead of a full-width dgrad + wgrad GEMM pair: for DLRM's top MLP (n_L = 1) every batch-
-    sized product becomes a GEMV. Only the fp32 summation order differs (like any GEMM tiling)."""
+    ctr MLP puts no activation on hidden layers): h_l = h_{l-1}·K_l + b_l, y = act(h_{L-1}·K_L
+    + b_L). The forward is evaluated layer by layer exactly as the layerwise path (bit-identical
+    outputs). The backward uses the chain's linearity twice:
+      * every upstream gradient is the last layer's, G = act'(y)⊙dy, through a fixed matrix:
+        g_l = G·Q_lᵀ with Q_l = K_{l+1}···K_L ([n_l, n_L]), so dK_l = (h_{l-1}ᵀ·G)·Q_lᵀ,
+        db_l = s·Q_lᵀ (s = Σ_b G) and dx = G·Q_0ᵀ;
+      * every hidden input is an affine map of the chain input, h_{l-1} = x·R_{l-1} + c_{l-1}
+        (R_{l-1} = K_1···K_{l-1}, c_l = c_{l-1}·K_l + b_l), so h_{l-1}ᵀ·G = R_{l-1}ᵀ·(xᵀ·G) +
+        c_{l-1}⊗s.
+    The only batch-deep work left is A = xᵀ·G ([n_0, n_L], one split-K reduction), s, and dx;
+    everything else is a product of weight-sized matrices. The same gradients in exact
+    arithmetic as the layer-by-layer backward; only the fp32 summation order differs (as it does
+    between any two GEMM tilings). tests/test_mlp_chain_gpu.py checks it against the float64
+    layerwise oracle."""
 
     @staticmethod
     def forward(ctx, x, handle, layers, rows):
-        hs = [x]
         h = x
         last = len(layers) - 1
         ks = []
@@ -243,10 +247,8 @@ class _LinearChainFn(torch.autograd.Function):
                     h = torch.relu_(h)
                 elif layer.act_code == 2:
                     h = torch.sigmoid_(h)
-            else:
-                hs.append(h)
         ctx.layers, ctx.rows = layers, rows
-        ctx.save_for_backward(h if layers[-1].act_code else None, *hs, *ks)
+        ctx.save_for_backward(h if layers[-1].act_code else None, x, *ks)
         return h
 
     @staticmethod
@@ -255,34 +257,44 @@ class _LinearChainFn(torch.autograd.Function):
 
         layers, rows = ctx.layers, ctx.rows
         n = len(layers)
-        saved = ctx.saved_tensors
-        y, hs, ks = saved[0], saved[1:1 + n], saved[1 + n:]
+        y, x, *ks = ctx.saved_tensors
         last = layers[-1]
         dy = dy.contiguous()
         B, fo = dy.shape
         act = last.act_code
-        db = None
+        G, s = dy, None
         if act or last.bias is not None:
             G = torch.empty_like(dy) if act else dy
-            db = torch.empty(fo, device=dy.device, dtype=torch.float32)
+            s = torch.empty(fo, device=dy.device, dtype=torch.float32)
             ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, fo) // 4),
                              device=dy.device)
-            L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, fo, act, L.ptr(G), L.ptr(db),
+            L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, fo, act, L.ptr(G), L.ptr(s),
                    L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
-        else:
-            G = dy
+        A = wgrad(x, G)  # xᵀ·G  [n_0, n_L]
+        if n > 1 and s is None:
+            s = G.sum(0)
+        # M_l = h_{l-1}ᵀ·G from A via the affine maps R, c (forward order)
+        Ms, R, c = [], None, None
+        for i in range(n):
+            Ms.append(A if i == 0 else torch.addmm(torch.outer(c, s), R.t(), A))
+            if i < n - 1:
+                b = layers[i].bias
+                R = ks[i] if R is None else R @ ks[i]
+                if c is None:
+                    c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device)
+                else:
+                    c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
         Q = None  # K_{l+1}···K_L
         for i in range(n - 1, -1, -1):
             layer = layers[i]
-            M = wgrad(hs[i], G)                       # h_{l-1}ᵀ·G   [n_{l-1}, n_L]
-            dk = M if Q is None else M @ Q.t()
+            dk = Ms[i] if Q is None else Ms[i] @ Q.t()
             if i == 0 and rows is not None:
                 full = torch.zeros_like(layer.kernel)
                 full.index_copy_(0, rows, dk)
                 dk = full
             _accum_grad(layer.kernel, dk)
-            if layer.bias is not None and db is not None:
-                _accum_grad(layer.bias, db if Q is None else db @ Q.t())
+            if layer.bias is not None and s is not None:
+                _accum_grad(layer.bias, s if Q is None else s @ Q.t())
             Q = ks[i] if Q is None else ks[i] @ Q
         dx = G @ Q.t() if ctx.needs_input_grad[0] else None
         return dx, None, None, None

@@ -110,7 +110,11 @@ class SparseOptimizer:
     dense backward. step() joins the side stream into the current one."""
     kind = L.RS_OPT_SGD
 
-    def __init__(self, tables, lr=0.01, fused=False):
+    def __init__(self, tables, lr=0.01, fused=False, defer_join=False):
+        """defer_join (fused only): step() does not make the current stream wait for the side
+        stream; the tables' next readers do (Embedding.wait_update), so the update overlaps
+        whatever the next step runs before its first table read (e.g. the bottom MLP). Readers
+        outside the engine's kernels must call torch.cuda.synchronize() (or wait_update())."""
         if isinstance(tables, Embedding):
             tables = [tables]
         self.tables = list(tables)
@@ -118,6 +122,7 @@ class SparseOptimizer:
         self.iterations = 0
         self.ws = _Workspace()
         self.fused = fused
+        self.defer_join = bool(defer_join) and fused
         self.side = None
         self._applied = set()
         if fused:
@@ -170,7 +175,13 @@ class SparseOptimizer:
     def step(self):
         applied = set()
         if self.fused:
-            torch.cuda.current_stream(self.tables[0].weight.device).wait_stream(self.side)
+            if self.defer_join:
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                for t in self.tables:
+                    t._pending_update = ev
+            else:
+                torch.cuda.current_stream(self.tables[0].weight.device).wait_stream(self.side)
             applied, self._applied = self._applied, set()
         params = self._params()
         for t in self.tables:
@@ -202,8 +213,8 @@ class SparseAdam(SparseOptimizer):
     mode='lazy': the same update restricted to touched rows."""
 
     def __init__(self, tables, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, mode="keras",
-                 fused=False):
-        super().__init__(tables, lr, fused=fused)
+                 fused=False, defer_join=False):
+        super().__init__(tables, lr, fused=fused, defer_join=defer_join)
         self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
         if mode not in ("keras", "lazy"):
             raise ValueError("mode must be 'keras' or 'lazy'")

@@ -138,19 +138,21 @@ def test_keras_adam_coefficients_match_oracle():
 @pytest.mark.parametrize("optimizer", ["sgd", "lazy_adam", "keras_adam"])
 def test_fused_side_stream_apply_matches_unfused(optimizer, rng):
     """The side-stream fused optimizer (sort before the dense forward, apply inside the
-    backward) must give the same table bit for bit as the step()-time apply."""
+    backward; optionally joined only at the next step's first table read) must give the same
+    table bit for bit as the step()-time apply."""
     from recommender_amd.ctr.train import TrainStep, build_model
     from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
 
     cards = criteo_cardinalities(300_000, 26)
     models, steps = [], []
-    for fused in (False, True):
+    for fused, defer in ((False, False), (True, False), (True, True)):
         g = torch.Generator(device=DEV)
         g.manual_seed(7)
         m = build_model("DLRM", 32, sum(cards), 26, 13, DEV, slot_cardinalities=cards,
                         bottom=[64, 32], top=[64, 1], generator=g)
         models.append(m)
-        steps.append(TrainStep(m, optimizer, lr=0.05 if optimizer == "sgd" else 1e-3, fused=fused))
+        steps.append(TrainStep(m, optimizer, lr=0.05 if optimizer == "sgd" else 1e-3, fused=fused,
+                               defer_sparse_join=defer))
     r = np.random.default_rng(3)
     for _ in range(3):
         cat, dn, lb = criteo_batch(r, 2048, cards)
@@ -158,8 +160,9 @@ def test_fused_side_stream_apply_matches_unfused(optimizer, rng):
         for st in steps:
             st(b)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(models[0].embedding_layer.weight.cpu().numpy(),
-                                  models[1].embedding_layer.weight.cpu().numpy())
+    ref = models[0].embedding_layer.weight.cpu().numpy()
+    for m in models[1:]:  # fused, and fused with the join deferred to the next table read
+        np.testing.assert_array_equal(ref, m.embedding_layer.weight.cpu().numpy())
 
 
 def test_golden_fixture_on_gpu():

@@ -1,8 +1,8 @@
 """The ctr MLP's factored backward (nn._LinearChainFn; the reference's hidden Dense layers are
 linear, ctr/layers.py:8) against the layer-by-layer float64 oracle (oracle/ctr.py mlp_backward):
 forward bit-identical to the layerwise path; kernel / bias / input gradients within 1e-5 of the
-oracle relative to the magnitude bound of the factored products, (|h|ᵀ|G|)·|Q|ᵀ, which bounds
-both evaluation orders."""
+oracle relative to the magnitude bound of the factored products, (|R|ᵀ|x|ᵀ|G| + |c|⊗Σ|G|)·|Q|ᵀ,
+which bounds both evaluation orders."""
 import numpy as np
 import pytest
 import torch
@@ -64,12 +64,19 @@ def test_factored_backward_matches_oracle(units, act, fin, B, rows, rng):
         G = G * out * (1 - out)
     elif act == "relu":
         G = G * (out > 0)
+    # magnitude bounds of the factored products: h_{l-1} = x·R + c, so
+    # |h_{l-1}ᵀ·G| <= |R|ᵀ·(|x|ᵀ·|G|) + |c|⊗Σ|G|  (>= |h_{l-1}|ᵀ·|G|, the layerwise bound)
+    aG = np.abs(G)
+    base = np.abs(x.astype(np.float64)).T @ aG
+    Mb, absR, absc = [], None, None
+    for i, (k, b) in enumerate(layers):
+        Mb.append(base if i == 0 else absR.T @ base + np.outer(absc, aG.sum(0)))
+        absR = np.abs(k) if absR is None else absR @ np.abs(k)
+        absc = np.abs(b) if absc is None else np.abs(k).T @ absc + np.abs(b)
     absQ = None
     bounds = {}
     for i in range(len(layers) - 1, -1, -1):
-        h = np.abs(cache[i])
-        bound = np.abs(h).T @ np.abs(G)
-        bscale = np.abs(G).sum(0)
+        bound, bscale = Mb[i], aG.sum(0)
         if absQ is not None:
             bound, bscale = bound @ absQ.T, bscale @ absQ.T
         bounds[i] = bound
