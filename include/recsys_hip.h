@@ -173,6 +173,17 @@ int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D, c
                                 const float* grad_out, int64_t grad_stride, float* grad_emb,
                                 float* grad_dense, void* stream);
 
+/* Rank-one upstream gradient (the factored top-MLP backward, recommender_amd/nn.py
+ * _LinearChainFn): grad row b = gscale[b] * grad_row[0..width), bit-identical to
+ * rs_dlrm_interaction_bwd on the materialised rows; compact layout, D = 128, F <= 32 only
+ * (RS_E_UNSUPPORTED otherwise). */
+int32_t rs_dlrm_interaction_bwd_rank1(const float* table, int64_t n_rows, int32_t D,
+                                      const void* ids, int32_t id_dtype, int32_t n_slots,
+                                      const int64_t* slot_offsets, const float* dense,
+                                      int64_t batch, const float* gscale, const float* grad_row,
+                                      int64_t width, float* grad_emb, float* grad_dense,
+                                      void* stream);
+
 /* a-5 DeepFM second-order term — ctr/model.py:21-23:
  *   out[b] = 0.5 * Σ_d ((Σ_f e[b,f,d])^2 - Σ_f e[b,f,d]^2). */
 int32_t rs_fm_fwd(const float* emb, int64_t batch, int32_t F, int32_t D, float* out, void* stream);
@@ -354,6 +365,18 @@ int32_t rs_side_pool_fwd(const float* side, const float* weight_logits, int64_t 
 int32_t rs_side_pool_bwd(const float* side, const float* attn, const float* grad_hidden,
                          int64_t batch, int32_t n_side, int32_t dim, float* grad_side,
                          float* grad_weight_logits, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Factored linear-chain backward of a ctr MLP (hidden Dense layers linear, ctr/layers.py:8):
+ * with G = act'(y) ⊙ dy (act 0 linear, 1 relu, 2 sigmoid on the output y [B, nl]),
+ * out[0 .. n0*nl) = xᵀ·G (row-major [n0, nl]), out[n0*nl ..] = Σ_b G; x [B, n0] with row
+ * stride ldx; g_out (may be NULL) receives G. Shapes: nl == 1 and n0 <= 1024, or nl <= 256
+ * and n0 <= 32 (nl == 1 also needs n0, ldx multiples of 4 and a 16-B aligned x). Deterministic
+ * (fixed row chunks folded in order). */
+size_t rs_chain_reduce_workspace_size(int64_t B, int32_t n0, int32_t nl);
+int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, const float* dy, const float* y,
+                        int32_t nl, int32_t act, int64_t B, float* out, float* g_out,
+                        void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Keras thresholded AUC (keras.metrics.AUC in ctr/train.py:86,

@@ -108,6 +108,10 @@ _SIGS = {
     "rs_skipgram_workspace_size": (_sz, [_i32, _i32, _i32]),
     "rs_skipgram_pairs": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_log_uniform_sample": (_i32, [_p, _i32, _i64, _i32, _i32, _u64, _u32, _p, _p, _p]),
+    "rs_dlrm_interaction_bwd_rank1": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p,
+                                             _i64, _p, _p, _p]),
+    "rs_chain_reduce_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "rs_chain_reduce": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _sz, _p]),
     "rs_vocab_count_masked": (_i32, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
     "rs_kv_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p,
                            _p, _p]),

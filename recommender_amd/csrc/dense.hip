@@ -83,6 +83,129 @@ __global__ __launch_bounds__(256) void fold_chunks_kernel(const float* __restric
   if (w == 0 && col < N) out[col] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+
+// ---- factored linear-chain backward: A = xᵀ·G and s = Σ_b G in one pass ----------------
+// G = act'(y) ⊙ dy is formed on the fly (the formula of act_bwd_colsum_kernel) and optionally
+// written out. Rows are cut into fixed chunks of kChainRows; each block folds its chunk in row
+// order, the chunk partials [n0*nl + nl] are folded in chunk order by fold_chunks_kernel:
+// deterministic.
+constexpr int kChainRows = 128;
+
+template <int ACT>
+__device__ __forceinline__ float act_grad(float g, float y) {
+  if constexpr (ACT == 1) return y > 0.f ? g : 0.f;
+  if constexpr (ACT == 2) return g * (y * (1.f - y));
+  return g;
+}
+
+// nl == 1: thread (phase, column group) moves 4 consecutive columns per row (float4); the
+// 256/cgp row phases of a block are folded in phase order through LDS. Every thread forms g_b
+// itself (broadcast loads); the phase's group-0 thread accumulates Σ g and writes g_out.
+constexpr int kVecRows = 64;
+
+template <int ACT>
+__global__ __launch_bounds__(256) void chain_reduce_vec_kernel(
+    const float* __restrict__ x, int64_t ldx, int n0, int cgp, const float* __restrict__ dy,
+    const float* __restrict__ y, int64_t B, float* __restrict__ gout, float* __restrict__ part) {
+  __shared__ float4 red[256];
+  __shared__ float sred[256];
+  const int t = threadIdx.x;
+  const int P = 256 / cgp;
+  const int cg = t % cgp, ph = t / cgp;
+  const int c0 = 4 * cg;
+  const bool live = c0 < n0;
+  const int64_t r0 = (int64_t)blockIdx.x * kVecRows;
+  const int64_t r1 = r0 + kVecRows < B ? r0 + kVecRows : B;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float sacc = 0.f;
+#pragma unroll 4
+  for (int64_t b = r0 + ph; b < r1; b += P) {
+    const float g = act_grad<ACT>(dy[b], ACT ? y[b] : 0.f);
+    if (live) {
+      const float4 v = *reinterpret_cast<const float4*>(x + b * ldx + c0);
+      acc.x += v.x * g;
+      acc.y += v.y * g;
+      acc.z += v.z * g;
+      acc.w += v.w * g;
+    }
+    if (cg == 0) {
+      sacc += g;
+      if (gout) gout[b] = g;
+    }
+  }
+  red[t] = acc;
+  sred[t] = sacc;
+  __syncthreads();
+  float* pp = part + (int64_t)blockIdx.x * (n0 + 1);
+  if (t < cgp && live) {
+    float4 v = red[t];
+    for (int q = 1; q < P; ++q) {
+      const float4 w = red[q * cgp + t];
+      v.x += w.x;
+      v.y += w.y;
+      v.z += w.z;
+      v.w += w.w;
+    }
+    pp[c0] = v.x;
+    if (c0 + 1 < n0) pp[c0 + 1] = v.y;
+    if (c0 + 2 < n0) pp[c0 + 2] = v.z;
+    if (c0 + 3 < n0) pp[c0 + 3] = v.w;
+  }
+  if (t == 0) {
+    float v = sred[0];
+    for (int q = 1; q < P; ++q) v += sred[q * cgp];
+    pp[n0] = v;
+  }
+}
+
+// n0 <= N0MAX, nl <= 256: thread (phase, j) walks rows r0 + phase, r0 + phase + P, ...; the
+// chunk's x rows are staged in LDS; the P phase sums are folded in phase order
+template <int ACT, int N0MAX>
+__global__ __launch_bounds__(256) void chain_reduce_outer_kernel(
+    const float* __restrict__ x, int64_t ldx, int n0, const float* __restrict__ dy,
+    const float* __restrict__ y, int nl, int nlp, int64_t B, float* __restrict__ gout,
+    float* __restrict__ part) {
+  __shared__ float xs[kChainRows * N0MAX];
+  __shared__ float red[256 * (N0MAX + 1)];
+  const int t = threadIdx.x;
+  const int P = 256 / nlp;
+  const int j = t % nlp, ph = t / nlp;
+  const int64_t r0 = (int64_t)blockIdx.x * kChainRows;
+  const int64_t r1 = r0 + kChainRows < B ? r0 + kChainRows : B;
+  const int nr = (int)(r1 - r0);
+  for (int e = t; e < nr * n0; e += 256) xs[e] = x[(r0 + e / n0) * ldx + e % n0];
+  __syncthreads();
+  float acc[N0MAX];
+#pragma unroll
+  for (int i = 0; i < N0MAX; ++i) acc[i] = 0.f;
+  float sacc = 0.f;
+  if (j < nl) {
+#pragma unroll 2
+    for (int r = ph; r < nr; r += P) {
+      const int64_t o = (r0 + r) * nl + j;
+      const float g = act_grad<ACT>(dy[o], ACT ? y[o] : 0.f);
+#pragma unroll
+      for (int i = 0; i < N0MAX; ++i)
+        if (i < n0) acc[i] += xs[r * n0 + i] * g;
+      sacc += g;
+      if (gout) gout[o] = g;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N0MAX; ++i) red[t * (N0MAX + 1) + i] = acc[i];
+  red[t * (N0MAX + 1) + N0MAX] = sacc;
+  __syncthreads();
+  float* pp = part + (int64_t)blockIdx.x * ((int64_t)n0 * nl + nl);
+  for (int e = t; e < (n0 + 1) * nlp; e += 256) {
+    const int i = e / nlp, jj = e % nlp;  // i == n0: the column sum
+    if (jj >= nl) continue;
+    const int slot = i == n0 ? N0MAX : i;
+    float v = 0.f;
+    for (int q = 0; q < P; ++q) v += red[(q * nlp + jj) * (N0MAX + 1) + slot];
+    pp[(int64_t)i * nl + jj] = v;
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -124,6 +247,65 @@ extern "C" int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B,
   }
   RS_CHECK_LAUNCH();
   fold_chunks_kernel<<<(unsigned)ceil_div(N, 64), 256, 0, st>>>(part, nchunks, N, db);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" size_t rs_chain_reduce_workspace_size(int64_t B, int32_t n0, int32_t nl) {
+  const int rows = nl == 1 ? kVecRows : kChainRows;
+  return (size_t)ceil_div(B < 1 ? 1 : B, rows) * ((size_t)n0 * nl + nl) * sizeof(float);
+}
+
+extern "C" int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, const float* dy,
+                                   const float* y, int32_t nl, int32_t act, int64_t B, float* out,
+                                   float* g_out, void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(B >= 0 && n0 >= 1 && nl >= 1 && ldx >= n0 && act >= 0 && act <= 2,
+               "rs_chain_reduce: bad arguments");
+  RS_CHECK_ARG(act == 0 || y, "rs_chain_reduce: activation backward needs y");
+  RS_CHECK_ARG((nl == 1 && n0 <= 1024) || (nl <= 256 && n0 <= 32),
+               "rs_chain_reduce: shape outside the kernels (nl == 1 and n0 <= 1024, or nl <= 256 "
+               "and n0 <= 32)");
+  RS_CHECK_ARG(ws_bytes >= rs_chain_reduce_workspace_size(B, n0, nl),
+               "rs_chain_reduce: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int M = n0 * nl + nl;
+  if (B == 0) {
+    RS_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)M * 4, st));
+    return RS_OK;
+  }
+  float* part = static_cast<float*>(workspace);
+  int nchunks = (int)ceil_div(B, kChainRows);
+  if (nl == 1) {
+    RS_CHECK_ARG(n0 % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+                 "rs_chain_reduce: nl == 1 needs n0, ldx multiples of 4 and a 16-B aligned x");
+    nchunks = (int)ceil_div(B, kVecRows);
+    int cgp = 1;
+    while (cgp < n0 / 4) cgp <<= 1;
+    switch (act) {
+      case 0: chain_reduce_vec_kernel<0><<<nchunks, 256, 0, st>>>(x, ldx, n0, cgp, dy, y, B, g_out, part); break;
+      case 1: chain_reduce_vec_kernel<1><<<nchunks, 256, 0, st>>>(x, ldx, n0, cgp, dy, y, B, g_out, part); break;
+      default: chain_reduce_vec_kernel<2><<<nchunks, 256, 0, st>>>(x, ldx, n0, cgp, dy, y, B, g_out, part); break;
+    }
+  } else {
+    int nlp = 1;
+    while (nlp < nl) nlp <<= 1;
+    auto go = [&](auto kern) { kern<<<nchunks, 256, 0, st>>>(x, ldx, n0, dy, y, nl, nlp, B, g_out, part); };
+    if (n0 <= 16) {
+      switch (act) {
+        case 0: go(chain_reduce_outer_kernel<0, 16>); break;
+        case 1: go(chain_reduce_outer_kernel<1, 16>); break;
+        default: go(chain_reduce_outer_kernel<2, 16>); break;
+      }
+    } else {
+      switch (act) {
+        case 0: go(chain_reduce_outer_kernel<0, 32>); break;
+        case 1: go(chain_reduce_outer_kernel<1, 32>); break;
+        default: go(chain_reduce_outer_kernel<2, 32>); break;
+      }
+    }
+  }
+  RS_CHECK_LAUNCH();
+  fold_chunks_kernel<<<(unsigned)ceil_div(M, 64), 256, 0, st>>>(part, nchunks, M, out);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -325,11 +325,16 @@ typedef __attribute__((address_space(1))) const float gfloat;
 // pipelined gathers need no per-row select (a select would keep a lane mask live per row)
 __device__ const float kZeroRow[256] = {};
 
-template <int D, int GREG, int KS, bool SELF, bool SKIP, bool ID64>
+// RANK1: the upstream gradient is rank one, grad row b = gscale[b] * gout[0..gstride) (the
+// factored top-MLP backward's dZ = G ⊗ Q_0): each staged value is the same single fp32 product
+// the materialised dZ would hold, so the results are bit-identical to that path, without the
+// [B, width] write and read.
+template <int D, int GREG, int KS, bool SELF, bool SKIP, bool ID64, bool RANK1 = false>
 __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batch, int F,
                                                      const float* __restrict__ gout,
                                                      int64_t gstride, float* __restrict__ gemb,
-                                                     float* __restrict__ gdense, int epw) {
+                                                     float* __restrict__ gdense, int epw,
+                                                     const float* __restrict__ gscale = nullptr) {
   static_assert(D == 128, "pipelined backward is laid out for D = 128 (4 floats per lane)");
   constexpr int NTILE = 4;
   // per wave: the staged grad row + one zero slot (index ZS) that dropped pairs read
@@ -375,11 +380,22 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
   float gnx[GREG];
   const int glast = (int)gstride - 1;  // reads past the row end are clamped (the values there
                                        // are never used: every index read is < gw)
+  float pv[RANK1 ? GREG : 1];
+  if constexpr (RANK1) {
+#pragma unroll
+    for (int j = 0; j < GREG; ++j) pv[j] = gout[min(lane + 64 * j, glast)];
+  }
   auto load_g = [&](int64_t b, int ln) {  // ln: a lane id (the loop passes the opaque one)
     const int64_t bb = b < last ? b : first;
-    gfloat* grow = (gfloat*)(gout + bb * gstride);
+    if constexpr (RANK1) {
+      const float gsc = gscale[bb];
 #pragma unroll
-    for (int j = 0; j < GREG; ++j) gnx[j] = grow[min(ln + 64 * j, glast)];
+      for (int j = 0; j < GREG; ++j) gnx[j] = gsc * pv[j];
+    } else {
+      gfloat* grow = (gfloat*)(gout + bb * gstride);
+#pragma unroll
+      for (int j = 0; j < GREG; ++j) gnx[j] = grow[min(ln + 64 * j, glast)];
+    }
   };
   // prologue: example `first` in flight, ids of first+1 in flight
   const float* cur = row_of(first, raw_id(first));
@@ -455,7 +471,7 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
 template <int GREG, int KS, bool ID64>
 static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode md,
                           const float* gout, int64_t gstride, float* gemb, float* gdense, int,
-                          hipStream_t st) {
+                          hipStream_t st, const float* gscale = nullptr) {
   auto go = [&](auto kern) {
     static int epw_cached = 0;
     static int64_t batch_cached = -1;
@@ -465,8 +481,12 @@ static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode 
     }
     const int epw = epw_cached;
     kern<<<ceil_div(batch, 4 * (int64_t)epw), 256, 0, st>>>(src, batch, F, gout, gstride, gemb,
-                                                           gdense, epw);
+                                                           gdense, epw, gscale);
   };
+  if (gscale) {  // rank-one upstream gradient: the DLRM layout only (non-self, compact)
+    go(dlrm_bwd_pipe<128, GREG, KS, false, false, ID64, true>);
+    return;
+  }
   if (md.self_interaction) {
     if (md.skip_gather) go(dlrm_bwd_pipe<128, GREG, KS, true, true, ID64>);
     else go(dlrm_bwd_pipe<128, GREG, KS, true, false, ID64>);
@@ -479,11 +499,11 @@ static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode 
 template <int GREG, int KS>
 static void launch_pipe(const GatherSrc& src, int64_t batch, int F, InterMode md,
                         const float* gout, int64_t gstride, float* gemb, float* gdense, int epw,
-                        hipStream_t st) {
+                        hipStream_t st, const float* gscale = nullptr) {
   if (src.id_dtype == RS_ID_I64)
-    launch_pipe_t<GREG, KS, true>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+    launch_pipe_t<GREG, KS, true>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st, gscale);
   else
-    launch_pipe_t<GREG, KS, false>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st);
+    launch_pipe_t<GREG, KS, false>(src, batch, F, md, gout, gstride, gemb, gdense, epw, st, gscale);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -744,6 +764,40 @@ extern "C" int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, i
                                      grad_emb, grad_dense,
                                      al16(table) && al16(dense) && al16(grad_emb) && al16(grad_dense),
                                      as_stream(stream));
+}
+
+extern "C" int32_t rs_dlrm_interaction_bwd_rank1(const float* table, int64_t n_rows, int32_t D,
+                                                 const void* ids, int32_t id_dtype,
+                                                 int32_t n_slots, const int64_t* slot_offsets,
+                                                 const float* dense, int64_t batch,
+                                                 const float* gscale, const float* grad_row,
+                                                 int64_t width, float* grad_emb,
+                                                 float* grad_dense, void* stream) {
+  const int F = n_slots + 1;
+  const InterMode md{0, 0};
+  const int gw = out_width(F, 0, 0) + D;
+  RS_CHECK_ARG(n_slots >= 1 && D >= 1 && batch >= 0, "bad sizes");
+  RS_CHECK_ARG(width >= gw, "width too small");
+  if (batch == 0) return RS_OK;
+  RS_CHECK_ARG(table && ids && dense && gscale && grad_row && grad_emb && grad_dense,
+               "null pointer");
+  if (!(F <= 32 && D == 128 && gw <= 20 * 64 && al16(table) && al16(dense) && al16(grad_emb) &&
+        al16(grad_dense))) {
+    set_error("rs_dlrm_interaction_bwd_rank1: needs D = 128, F <= 32, 16-B aligned buffers");
+    return RS_E_UNSUPPORTED;
+  }
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, nullptr};
+  hipStream_t st = as_stream(stream);
+  const bool k14 = F <= 28;
+  if (gw <= 8 * 64) {
+    if (k14) launch_pipe<8, 14>(src, batch, F, md, grad_row, width, grad_emb, grad_dense, 0, st, gscale);
+    else launch_pipe<8, 16>(src, batch, F, md, grad_row, width, grad_emb, grad_dense, 0, st, gscale);
+  } else {
+    if (k14) launch_pipe<20, 14>(src, batch, F, md, grad_row, width, grad_emb, grad_dense, 0, st, gscale);
+    else launch_pipe<20, 16>(src, batch, F, md, grad_row, width, grad_emb, grad_dense, 0, st, gscale);
+  }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
 }
 
 extern "C" int32_t rs_fm_fwd(const float* emb, int64_t batch, int32_t F, int32_t D, float* out,

@@ -33,12 +33,17 @@ class MLP(nn.Module):
                             generator=generator))
         self.mlp = nn.ModuleList(layers)
 
+    def chain_ready(self, x) -> bool:
+        """True when the forward runs as one linear chain (factored backward)."""
+        layers = list(self.mlp)
+        return (self.factored_backward and x.dim() == 2 and x.is_cuda and torch.is_grad_enabled()
+                and all(l.kernel is not None and l.act_code >= 0 for l in layers)
+                and all(l.act_code == 0 for l in layers[:-1]))
+
     def forward(self, x, rows=None):
         """rows: optional index of first-layer kernel rows the input holds (DLRM compact row)."""
         layers = list(self.mlp)
-        if (self.factored_backward and x.dim() == 2 and x.is_cuda and torch.is_grad_enabled()
-                and all(l.kernel is not None and l.act_code >= 0 for l in layers)
-                and all(l.act_code == 0 for l in layers[:-1])):
+        if self.chain_ready(x):
             return linear_chain(x, layers, rows)
         x = layers[0](x, rows=rows)
         for layer in layers[1:]:

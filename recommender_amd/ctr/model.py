@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from ..embedding import Embedding, SlabEmbedding
-from ..functional import COMPACT_ALIGN, dlrm_interaction, fm_interaction
+from ..functional import COMPACT_ALIGN, dlrm_interaction, dlrm_top, fm_interaction
 from .layers import MLP, DotInteraction
 
 
@@ -106,8 +106,15 @@ class DLRM(nn.Module):
             tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)
             out = self.top_mlp(tmlp_input).squeeze(1)
         else:
-            tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
-            out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)
+            layers = list(self.top_mlp.mlp)
+            if (self._exchanged is None and self.embedding_size == 128 and torch.is_grad_enabled()
+                    and self.top_mlp.chain_ready(bmlp_activation)):
+                # interaction + top MLP as one linear chain: rank-one interaction backward
+                out = dlrm_top(self.embedding_layer, cat_features, bmlp_activation, layers,
+                               self.compact_rows).squeeze(1)
+            else:
+                tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
+                out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)
         # forward kernels are queued: the side-stream sort now runs beside them
         self.embedding_layer.presort(cat_features)
         return out

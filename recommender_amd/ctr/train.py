@@ -73,6 +73,13 @@ class TrainStep:
         frozen into the graph, so capture only with constant-lr SGD."""
         if self._sched is not None or not isinstance(self.opt_sparse, SparseSGD):
             raise RuntimeError("graph capture needs constant-lr SGD (scalars are frozen)")
+        # the graph must join every stream it forks: the sparse update joins inside the step
+        # (a replay is ordered after the previous one as a whole)
+        defer = self.opt_sparse.defer_join
+        self.opt_sparse.defer_join = False
+        torch.cuda.synchronize()
+        for t in self.opt_sparse.tables:
+            t._pending_update = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -84,6 +91,7 @@ class TrainStep:
         with torch.cuda.graph(g):
             loss = self(batch)
         self._graph_loss = loss
+        self.opt_sparse.defer_join = defer
 
         def replay():
             g.replay()

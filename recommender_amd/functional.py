@@ -145,6 +145,57 @@ def dlrm_interaction(table_module, ids, dense, compact: bool = False):
     return _DLRMInteraction.apply(table_module.grad_handle, dense, table_module, ids, compact)
 
 
+class _DLRMTopFn(torch.autograd.Function):
+    """DLRM's fused lookup + interaction (compact row) feeding the top MLP as one linear chain
+    (ctr/model.py:49-57 with the ctr MLP's linear hidden layers, ctr/layers.py:8). Forward:
+    rs_dlrm_interaction_fwd, then the top MLP layer by layer (bit-identical to the unfused
+    path). Backward: rs_chain_reduce over the interaction row gives G = σ'(y)·dy [B], A = Zᵀ·G
+    and Σ G in one pass; every top-MLP gradient follows from them (nn.chain_param_grads); the
+    upstream gradient of the interaction is then the rank-one G ⊗ Q_0 (Q_0 = K_1·K_2·K_3), which
+    rs_dlrm_interaction_bwd_rank1 consumes without materialising the [B, width] rows."""
+
+    @staticmethod
+    def forward(ctx, handle, dense, table_module, ids, layers, rows):
+        from .nn import chain_forward
+
+        dense = dense.contiguous()
+        z = _DLRMInteraction.forward(ctx, handle, dense, table_module, ids, True)
+        y, ks = chain_forward(z, layers, rows)
+        ctx.layers, ctx.rows = layers, rows
+        ctx.save_for_backward(dense, z, y, *ks)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .nn import chain_param_grads, chain_reduce
+
+        dense, z, y, *ks = ctx.saved_tensors
+        layers, rows = ctx.layers, ctx.rows
+        G, A, s = chain_reduce(z, dy.contiguous(), y, layers[-1].act_code, need_g=True)
+        Q = chain_param_grads(layers, rows, ks, A, s)
+        tm = ctx.table_module
+        w = tm.weight
+        ids = ctx.ids
+        B, S = ids.shape
+        D = w.shape[1]
+        grad_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
+        grad_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
+        p = Q[:, 0].contiguous()
+        L.call("rs_dlrm_interaction_bwd_rank1", L.ptr(w), w.shape[0], D, L.ptr(ids),
+               L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, L.ptr(G),
+               L.ptr(p), p.numel(), L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
+        if tm.fused_optimizer is not None:
+            tm.fused_optimizer.apply_async(tm, ids, grad_emb, tm.take_presorted(ids))
+        else:
+            tm.accumulate_grad(ids, grad_emb)
+        return None, grad_dense, None, None, None, None
+
+
+def dlrm_top(table_module, ids, dense, layers, rows):
+    """sigmoid-head top MLP over the compact DLRM interaction row, fused (see _DLRMTopFn)."""
+    return _DLRMTopFn.apply(table_module.grad_handle, dense, table_module, ids, list(layers), rows)
+
+
 class _FM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, emb):

@@ -235,69 +235,97 @@ class _LinearChainFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, handle, layers, rows):
-        h = x
-        last = len(layers) - 1
-        ks = []
-        for i, layer in enumerate(layers):
-            k = layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
-            ks.append(k)
-            h = torch.addmm(layer.bias, h, k) if layer.bias is not None else h @ k
-            if i == last:
-                if layer.act_code == 1:
-                    h = torch.relu_(h)
-                elif layer.act_code == 2:
-                    h = torch.sigmoid_(h)
+        h, ks = chain_forward(x, layers, rows)
         ctx.layers, ctx.rows = layers, rows
         ctx.save_for_backward(h if layers[-1].act_code else None, x, *ks)
         return h
 
     @staticmethod
     def backward(ctx, dy):
-        from . import _lib as L
-
         layers, rows = ctx.layers, ctx.rows
-        n = len(layers)
         y, x, *ks = ctx.saved_tensors
-        last = layers[-1]
-        dy = dy.contiguous()
-        B, fo = dy.shape
-        act = last.act_code
-        G, s = dy, None
-        if act or last.bias is not None:
-            G = torch.empty_like(dy) if act else dy
-            s = torch.empty(fo, device=dy.device, dtype=torch.float32)
-            ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, fo) // 4),
-                             device=dy.device)
-            L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, fo, act, L.ptr(G), L.ptr(s),
-                   L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
-        A = wgrad(x, G)  # xᵀ·G  [n_0, n_L]
-        if n > 1 and s is None:
-            s = G.sum(0)
-        # M_l = h_{l-1}ᵀ·G from A via the affine maps R, c (forward order)
-        Ms, R, c = [], None, None
-        for i in range(n):
-            Ms.append(A if i == 0 else torch.addmm(torch.outer(c, s), R.t(), A))
-            if i < n - 1:
-                b = layers[i].bias
-                R = ks[i] if R is None else R @ ks[i]
-                if c is None:
-                    c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device)
-                else:
-                    c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
-        Q = None  # K_{l+1}···K_L
-        for i in range(n - 1, -1, -1):
-            layer = layers[i]
-            dk = Ms[i] if Q is None else Ms[i] @ Q.t()
-            if i == 0 and rows is not None:
-                full = torch.zeros_like(layer.kernel)
-                full.index_copy_(0, rows, dk)
-                dk = full
-            _accum_grad(layer.kernel, dk)
-            if layer.bias is not None and s is not None:
-                _accum_grad(layer.bias, s if Q is None else s @ Q.t())
-            Q = ks[i] if Q is None else ks[i] @ Q
-        dx = G @ Q.t() if ctx.needs_input_grad[0] else None
+        need_dx = ctx.needs_input_grad[0]
+        G, A, s = chain_reduce(x, dy.contiguous(), y, layers[-1].act_code, need_g=need_dx)
+        Q = chain_param_grads(layers, rows, ks, A, s)
+        dx = G @ Q.t() if need_dx else None
         return dx, None, None, None
+
+
+def chain_reduce(x, dy, y, act, need_g=True):
+    """(G, A = xᵀ·G, s = Σ_b G) of a linear chain's last layer, G = act'(y) ⊙ dy: one fused
+    deterministic pass (rs_chain_reduce) for the narrow shapes of the ctr MLPs, else the
+    act_bwd_colsum kernel + a split-K reduction. G is None unless need_g (fused path)."""
+    from . import _lib as L
+
+    B, n0 = x.shape
+    nl = dy.shape[1]
+    vec_ok = (nl == 1 and n0 <= 1024 and n0 % 4 == 0 and x.stride(0) % 4 == 0
+              and x.data_ptr() % 16 == 0)
+    if x.stride(1) == 1 and (vec_ok or (nl > 1 and nl <= 256 and n0 <= 32)):
+        out = torch.empty(n0 * nl + nl, device=dy.device, dtype=torch.float32)
+        G = torch.empty_like(dy) if need_g else None
+        nb = L.lib().rs_chain_reduce_workspace_size(B, n0, nl)
+        ws = torch.empty(max(1, nb // 4), device=dy.device)
+        L.call("rs_chain_reduce", L.ptr(x), x.stride(0), n0, L.ptr(dy), L.ptr(y), nl, act, B,
+               L.ptr(out), L.ptr(G), L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
+        if G is None and act == 0 and need_g:
+            G = dy
+        return G, out[:n0 * nl].view(n0, nl), out[n0 * nl:]
+    G = dy
+    s = None
+    if act:
+        G = torch.empty_like(dy)
+        s = torch.empty(nl, device=dy.device, dtype=torch.float32)
+        ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, nl) // 4), device=dy.device)
+        L.call("rs_act_bwd_colsum", L.ptr(dy), L.ptr(y), B, nl, act, L.ptr(G), L.ptr(s),
+               L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
+    return G, wgrad(x, G), (s if s is not None else G.sum(0))
+
+
+def chain_param_grads(layers, rows, ks, A, s):
+    """Accumulate every layer's kernel / bias gradient of a linear chain from A = xᵀ·G and
+    s = Σ_b G (see _LinearChainFn); returns Q_0 = K_1···K_L for the input gradient G·Q_0ᵀ."""
+    n = len(layers)
+    Ms, R, c = [], None, None
+    for i in range(n):
+        Ms.append(A if i == 0 else torch.addmm(torch.outer(c, s), R.t(), A))
+        if i < n - 1:
+            b = layers[i].bias
+            R = ks[i] if R is None else R @ ks[i]
+            if c is None:
+                c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device)
+            else:
+                c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
+    Q = None  # K_{l+1}···K_L
+    for i in range(n - 1, -1, -1):
+        layer = layers[i]
+        dk = Ms[i] if Q is None else Ms[i] @ Q.t()
+        if i == 0 and rows is not None:
+            full = torch.zeros_like(layer.kernel)
+            full.index_copy_(0, rows, dk)
+            dk = full
+        _accum_grad(layer.kernel, dk)
+        if layer.bias is not None:
+            _accum_grad(layer.bias, s if Q is None else s @ Q.t())
+        Q = ks[i] if Q is None else ks[i] @ Q
+    return Q
+
+
+def chain_forward(x, layers, rows=None):
+    """Layer-by-layer forward of a linear chain: (y, the kernels as used)."""
+    h = x
+    last = len(layers) - 1
+    ks = []
+    for i, layer in enumerate(layers):
+        k = layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
+        ks.append(k)
+        h = torch.addmm(layer.bias, h, k) if layer.bias is not None else h @ k
+        if i == last:
+            if layer.act_code == 1:
+                h = torch.relu_(h)
+            elif layer.act_code == 2:
+                h = torch.sigmoid_(h)
+    return h, ks
 
 
 def linear_chain(x, layers, rows=None, handle=None):

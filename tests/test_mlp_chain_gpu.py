@@ -96,3 +96,72 @@ def test_factored_backward_matches_oracle(units, act, fin, B, rows, rng):
         if i == 0 and ridx is not None:
             got = got[ridx.cpu().numpy()]
         assert_close_rel(got, ref, 1e-5, bounds[i], f"layerwise dK{i}")
+
+
+def test_rank1_interaction_bwd_bit_identical(rng):
+    """rs_dlrm_interaction_bwd_rank1(G, p) == rs_dlrm_interaction_bwd on the materialised G ⊗ p."""
+    from recommender_amd import _lib as L
+    from recommender_amd.functional import COMPACT_ALIGN
+
+    S, D, B, V = 26, 128, 777, 20000
+    F = S + 1
+    width = (F * (F - 1) // 2 + D + COMPACT_ALIGN - 1) // COMPACT_ALIGN * COMPACT_ALIGN
+    table = torch.from_numpy(rng.standard_normal((V, D)).astype(np.float32)).to(DEV)
+    ids = torch.from_numpy(rng.integers(0, V, (B, S))).to(DEV)
+    dense = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(DEV)
+    G = torch.from_numpy(rng.standard_normal(B).astype(np.float32)).to(DEV)
+    p = torch.from_numpy(rng.standard_normal(width).astype(np.float32)).to(DEV)
+    gmat = (G[:, None] * p[None, :]).contiguous()
+    st = L.stream_ptr(torch.device(DEV))
+    outs = []
+    for rank1 in (False, True):
+        ge = torch.empty(B * S, D, device=DEV)
+        gd = torch.empty(B, D, device=DEV)
+        if rank1:
+            L.call("rs_dlrm_interaction_bwd_rank1", L.ptr(table), V, D, L.ptr(ids), 1, S, None,
+                   L.ptr(dense), B, L.ptr(G), L.ptr(p), width, L.ptr(ge), L.ptr(gd), st)
+        else:
+            L.call("rs_dlrm_interaction_bwd", L.ptr(table), V, D, L.ptr(ids), 1, S, None,
+                   L.ptr(dense), B, 1, L.ptr(gmat), width, L.ptr(ge), L.ptr(gd), st)
+        outs.append((ge, gd))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_dlrm_fused_top_matches_layerwise(rng):
+    """DLRM at D = 128 (the fused interaction + top-MLP chain with the rank-one backward)
+    against the same model with the layer-by-layer MLP backward: logits bit-identical, every
+    gradient within 1e-5 relative to its magnitude."""
+    from recommender_amd.ctr.model import DLRM
+
+    S, D, B, V = 26, 128, 1024, 50000
+    models = []
+    for _ in range(2):
+        g = torch.Generator(device=DEV)
+        g.manual_seed(3)
+        models.append(DLRM([64, D], [64, 32, 1], D, V, S, 13, device=DEV, generator=g))
+    x = {"cat_features": torch.from_numpy(rng.integers(0, V, (B, S))).to(DEV),
+         "int_features": torch.from_numpy(rng.standard_normal((B, 13)).astype(np.float32)).to(DEV)}
+    MLP.factored_backward = True
+    p1 = models[0](x)
+    MLP.factored_backward = False
+    try:
+        p2 = models[1](x)
+    finally:
+        MLP.factored_backward = True
+    assert torch.equal(p1, p2)
+    gy = torch.from_numpy(rng.standard_normal(B).astype(np.float32)).to(DEV)
+    p1.backward(gy)
+    MLP.factored_backward = False
+    try:
+        p2.backward(gy)
+    finally:
+        MLP.factored_backward = True
+    for (n1, a), (_, b) in zip(models[0].named_parameters(), models[1].named_parameters()):
+        if a.grad is None and b.grad is None:
+            continue
+        ga, gb = a.grad.cpu().numpy(), b.grad.cpu().numpy()
+        assert_close_rel(ga, gb, 1e-4, np.abs(gb).max() * 1e-1 + 1e-30, n1)
+    (i1, r1), (i2, r2) = models[0].embedding_layer.take_grad(), models[1].embedding_layer.take_grad()
+    assert torch.equal(i1, i2)
+    r2n = r2.cpu().numpy()
+    assert_close_rel(r1.cpu().numpy(), r2n, 1e-5, np.abs(r2n).max() * 5e-2, "emb grad rows")
