@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-baseline-steps", type=int, default=20)
     ap.add_argument("--cpu-baseline-batch", type=int, default=16384)
-    ap.add_argument("--graph", type=int, default=0, help="1: time HIP-graph replays of the step")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: HIP-graph replays of single steps; 2: one graph per pool of steps "
+                         "(updates overlapped across steps inside the graph)")
     ap.add_argument("--fused", type=int, default=1, help="fused side-stream sparse optimizer")
     ap.add_argument("--prio", type=int, default=0,
                     help="1: run the step on a high-priority HIP stream (side-stream work fills in)")
@@ -264,8 +266,15 @@ def main():
     for i in range(args.warmup):
         step(pool[i % len(pool)])
     runners = [lambda b=b: step(b) for b in pool]
-    if args.graph:
+    per_call = 1
+    if args.graph == 1:
         runners = [step.capture(b) for b in pool]
+    elif args.graph == 2:
+        # the pool's steps as one graph (per-step updates overlapped inside it); a remainder of
+        # steps that does not fill a whole graph runs through single-step graphs
+        runners = [step.capture_sequence(pool)]
+        singles = [step.capture(b) for b in pool]
+        per_call = len(pool)
     timer = L.KernelTimer(WATCH)
     L.set_timer(timer)
     torch.cuda.synchronize()
@@ -275,8 +284,14 @@ def main():
     timer.enabled = True
     t0 = time.perf_counter()
     ev0.record()
-    for i in range(args.steps):
-        loss = runners[i % len(runners)]()
+    if per_call > 1:
+        for _ in range(args.steps // per_call):
+            loss = runners[0]()
+        for i in range(args.steps % per_call):
+            loss = singles[i]()
+    else:
+        for i in range(args.steps):
+            loss = runners[i % len(runners)]()
     ev1.record()
     torch.cuda.synchronize()
     barrier(world)

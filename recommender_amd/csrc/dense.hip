@@ -101,12 +101,13 @@ __device__ __forceinline__ float act_grad(float g, float y) {
 // nl == 1: thread (phase, column group) moves 4 consecutive columns per row (float4); the
 // 256/cgp row phases of a block are folded in phase order through LDS. Every thread forms g_b
 // itself (broadcast loads); the phase's group-0 thread accumulates Σ g and writes g_out.
-constexpr int kVecRows = 64;
+constexpr int kVecRows = 256;
 
 template <int ACT>
 __global__ __launch_bounds__(256) void chain_reduce_vec_kernel(
     const float* __restrict__ x, int64_t ldx, int n0, int cgp, const float* __restrict__ dy,
     const float* __restrict__ y, int64_t B, float* __restrict__ gout, float* __restrict__ part) {
+  constexpr int U = 8;
   __shared__ float4 red[256];
   __shared__ float sred[256];
   const int t = threadIdx.x;
@@ -118,19 +119,29 @@ __global__ __launch_bounds__(256) void chain_reduce_vec_kernel(
   const int64_t r1 = r0 + kVecRows < B ? r0 + kVecRows : B;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float sacc = 0.f;
-#pragma unroll 4
-  for (int64_t b = r0 + ph; b < r1; b += P) {
-    const float g = act_grad<ACT>(dy[b], ACT ? y[b] : 0.f);
-    if (live) {
-      const float4 v = *reinterpret_cast<const float4*>(x + b * ldx + c0);
-      acc.x += v.x * g;
-      acc.y += v.y * g;
-      acc.z += v.z * g;
-      acc.w += v.w * g;
+  for (int64_t b0 = r0 + ph; b0 < r1; b0 += (int64_t)U * P) {
+    float4 v[U];
+    float g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // all U rows' loads in flight before any use
+      const int64_t b = b0 + (int64_t)u * P;
+      const bool in = b < r1;
+      const int64_t bb = in ? b : r0;
+      g[u] = in ? act_grad<ACT>(dy[bb], ACT ? y[bb] : 0.f) : 0.f;
+      v[u] = (live && in) ? *reinterpret_cast<const float4*>(x + bb * ldx + c0)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (cg == 0) {
-      sacc += g;
-      if (gout) gout[b] = g;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc.x += v[u].x * g[u];
+      acc.y += v[u].y * g[u];
+      acc.z += v[u].z * g[u];
+      acc.w += v[u].w * g[u];
+      const int64_t b = b0 + (int64_t)u * P;
+      if (cg == 0 && b < r1) {
+        sacc += g[u];
+        if (gout) gout[b] = g[u];
+      }
     }
   }
   red[t] = acc;

@@ -15,13 +15,14 @@ output [B] (ctr/model.py:27,57), so the loss the reference differentiates is the
 from __future__ import annotations
 
 import argparse
+import contextlib
 import time
 
 import numpy as np
 import torch
 
 from ..functional import binary_crossentropy
-from ..nn import overlapped_weight_grads
+from ..nn import overlapped_param_grads, overlapped_weight_grads
 from ..metrics import AUC
 from ..optim import DLRMScheduler, KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import criteo_batch, criteo_cardinalities
@@ -32,7 +33,8 @@ class TrainStep:
     """One optimizer step of a ctr model: forward, BCE, backward, dense + sparse apply."""
 
     def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
-                 fused=True, overlap_wgrad=False, comm=None, defer_sparse_join=False):
+                 fused=True, overlap_wgrad=False, comm=None, defer_sparse_join=False,
+                 overlap_param_grads=True):
         """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
         all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
         by its owners inside the backward."""
@@ -51,6 +53,9 @@ class TrainStep:
         # measured on MI355X: a weight-grad GEMM beside the interaction backward only
         # time-slices the CUs (no net gain), so the overlap is opt-in
         self.wgrad = overlapped_weight_grads(dense[0].device) if overlap_wgrad else None
+        # the MLP chains' parameter gradients beside the interaction backward / sparse apply
+        self.pgrad = (overlapped_param_grads(dense[0].device) if overlap_param_grads
+                      else contextlib.nullcontext())
         if optimizer == "sgd":
             lr = sched or (lr if lr is not None else 0.01)
             self.opt_dense = torch.optim.SGD(dense, lr=lr if not callable(lr) else lr(0))
@@ -99,6 +104,43 @@ class TrainStep:
 
         return replay
 
+    def capture_sequence(self, batches, warmup: int = 2):
+        """Capture len(batches) consecutive steps into ONE HIP graph (constant-lr SGD): no host
+        launch cost per kernel, and inside the graph each step's sparse update (side stream)
+        overlaps the next step's bottom MLP exactly as the deferred join does eagerly; only the
+        last step's update is joined at the end of the graph. Returns a replay callable that
+        runs all the steps and returns the last loss."""
+        if self._sched is not None or not isinstance(self.opt_sparse, SparseSGD):
+            raise RuntimeError("graph capture needs constant-lr SGD (scalars are frozen)")
+        defer = self.opt_sparse.defer_join
+        self.opt_sparse.defer_join = self.opt_sparse.fused
+        torch.cuda.synchronize()
+        for t in self.opt_sparse.tables:
+            t._pending_update = None
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                for b in batches:
+                    self(b)
+            for t in self.opt_sparse.tables:
+                t.wait_update()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for b in batches:
+                loss = self(b)
+            for t in self.opt_sparse.tables:  # join the last update inside the graph
+                t.wait_update()
+        self.opt_sparse.defer_join = defer
+
+        def replay():
+            g.replay()
+            return loss
+
+        return replay
+
     def __call__(self, batch):
         cat, dense_x, label = batch
         if self._sched is not None:
@@ -108,11 +150,12 @@ class TrainStep:
         p = self.model({"cat_features": cat, "int_features": dense_x})
         self.last_pred = p.detach()
         loss = binary_crossentropy(label, p, reduction=self.loss_reduction)
-        if self.wgrad is not None:
-            with self.wgrad:
+        with self.pgrad:
+            if self.wgrad is not None:
+                with self.wgrad:
+                    loss.backward()
+            else:
                 loss.backward()
-        else:
-            loss.backward()
         if self.comm is not None and self.comm.world > 1:
             self._allreduce_dense()
         self.opt_dense.step()

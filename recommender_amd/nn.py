@@ -6,6 +6,7 @@ lazily on the first call like Keras; the models in this package always pass it.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -282,33 +283,69 @@ def chain_reduce(x, dy, y, act, need_g=True):
     return G, wgrad(x, G), (s if s is not None else G.sum(0))
 
 
+_pgrad_stream: torch.cuda.Stream | None = None
+
+
+class overlapped_param_grads:
+    """Context for a backward pass over linear chains: the parameter gradients (a dozen small
+    products of weight-sized matrices per chain) are formed on a second HIP stream, beside the
+    batch-sized kernels that follow (the interaction backward, the sparse apply); the input
+    gradient's chain stays on the current stream. On exit the current stream waits for it."""
+
+    def __init__(self, device=None):
+        self.stream = torch.cuda.Stream(device=device)
+
+    def __enter__(self):
+        global _pgrad_stream
+        self._prev = _pgrad_stream
+        _pgrad_stream = self.stream
+        return self
+
+    def __exit__(self, *exc):
+        global _pgrad_stream
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+        _pgrad_stream = self._prev
+        return False
+
+
 def chain_param_grads(layers, rows, ks, A, s):
     """Accumulate every layer's kernel / bias gradient of a linear chain from A = xᵀ·G and
-    s = Σ_b G (see _LinearChainFn); returns Q_0 = K_1···K_L for the input gradient G·Q_0ᵀ."""
+    s = Σ_b G (see _LinearChainFn); returns Q_0 = K_1···K_L for the input gradient G·Q_0ᵀ.
+    Qa[i] = K_{i+1}···K_L is formed on the current stream (the input gradient needs it); the
+    rest, with h_{i}ᵀ·G = T_{i+1} + c_i⊗s where T_1 = A, T_{i+1} = K_iᵀ·T_i and
+    c_i = K_iᵀ·c_{i-1} + b_i, runs on the overlapped parameter-gradient stream when one is
+    active (matrix-vector chains when the output width is 1)."""
     n = len(layers)
-    Ms, R, c = [], None, None
-    for i in range(n):
-        Ms.append(A if i == 0 else torch.addmm(torch.outer(c, s), R.t(), A))
-        if i < n - 1:
-            b = layers[i].bias
-            R = ks[i] if R is None else R @ ks[i]
-            if c is None:
-                c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device)
-            else:
-                c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
-    Q = None  # K_{l+1}···K_L
-    for i in range(n - 1, -1, -1):
-        layer = layers[i]
-        dk = Ms[i] if Q is None else Ms[i] @ Q.t()
-        if i == 0 and rows is not None:
-            full = torch.zeros_like(layer.kernel)
-            full.index_copy_(0, rows, dk)
-            dk = full
-        _accum_grad(layer.kernel, dk)
-        if layer.bias is not None:
-            _accum_grad(layer.bias, s if Q is None else s @ Q.t())
-        Q = ks[i] if Q is None else ks[i] @ Q
-    return Q
+    Qa = [None] * n  # Qa[i] = K_{i+1}···K_L (None: identity)
+    for i in range(n - 2, -1, -1):
+        Qa[i] = ks[i + 1] if Qa[i + 1] is None else ks[i + 1] @ Qa[i + 1]
+    Q0 = ks[0] if Qa[0] is None else ks[0] @ Qa[0]
+    side = _pgrad_stream if A.is_cuda else None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(A.device))
+        for t in (A, s, *ks, *[q for q in Qa if q is not None]):
+            t.record_stream(side)
+    with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+        T, c = A, None
+        for i in range(n):
+            M = T if c is None else torch.addr(T, c, s)
+            dk = M if Qa[i] is None else M @ Qa[i].t()
+            layer = layers[i]
+            if i == 0 and rows is not None:
+                full = torch.zeros_like(layer.kernel)
+                full.index_copy_(0, rows, dk)
+                dk = full
+            _accum_grad(layer.kernel, dk)
+            if layer.bias is not None:
+                _accum_grad(layer.bias, s if Qa[i] is None else Qa[i] @ s)
+            if i < n - 1:
+                b = layer.bias
+                T = ks[i].t() @ T
+                if c is None:
+                    c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device)
+                else:
+                    c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
+    return Q0
 
 
 def chain_forward(x, layers, rows=None):
