@@ -406,6 +406,27 @@ def dlrm_path(iters, out):
            tot, per_ex * B, out)
 
 
+def chain(iters, out):
+    """rs_chain_reduce at the DLRM MLP shapes (factored backward): the top MLP's GEMV over the
+    compact interaction row (n0 480, nl 1, sigmoid) and the bottom MLP's 13 x 128 outer
+    reduction (relu). Bytes: x, dy, y read once (+ G written for the top)."""
+    B = 65536
+    for n0, nl, act, gout in ((480, 1, 2, True), (13, 128, 1, False)):
+        x = torch.randn(B, n0, device=DEV)
+        dy = torch.randn(B, nl, device=DEV)
+        y = torch.rand(B, nl, device=DEV)
+        o = torch.empty(n0 * nl + nl, device=DEV)
+        g = torch.empty(B, nl, device=DEV) if gout else None
+        nb = L.lib().rs_chain_reduce_workspace_size(B, n0, nl)
+        ws = torch.empty(nb // 4 + 1, device=DEV)
+        st = L.stream_ptr(torch.device(DEV))
+        fn = lambda: L.call("rs_chain_reduce", L.ptr(x), n0, n0, L.ptr(dy), L.ptr(y), nl, act, B,
+                            L.ptr(o), L.ptr(g), L.ptr(ws), ws.numel() * 4, st)
+        us = timed(fn, iters)
+        by = B * (n0 * 4 + 2 * nl * 4 + (nl * 4 if gout else 0))
+        report("rs_chain_reduce", {"B": B, "n0": n0, "nl": nl, "act": act}, us, by, out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)

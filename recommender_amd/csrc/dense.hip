@@ -101,7 +101,7 @@ __device__ __forceinline__ float act_grad(float g, float y) {
 // nl == 1: thread (phase, column group) moves 4 consecutive columns per row (float4); the
 // 256/cgp row phases of a block are folded in phase order through LDS. Every thread forms g_b
 // itself (broadcast loads); the phase's group-0 thread accumulates Σ g and writes g_out.
-constexpr int kVecRows = 256;
+constexpr int kVecRows = 128;
 
 template <int ACT>
 __global__ __launch_bounds__(256) void chain_reduce_vec_kernel(
@@ -190,16 +190,27 @@ __global__ __launch_bounds__(256) void chain_reduce_outer_kernel(
 #pragma unroll
   for (int i = 0; i < N0MAX; ++i) acc[i] = 0.f;
   float sacc = 0.f;
+  constexpr int U = 8;
   if (j < nl) {
-#pragma unroll 2
-    for (int r = ph; r < nr; r += P) {
-      const int64_t o = (r0 + r) * nl + j;
-      const float g = act_grad<ACT>(dy[o], ACT ? y[o] : 0.f);
+    for (int r0b = ph; r0b < nr; r0b += U * P) {
+      float g[U];
 #pragma unroll
-      for (int i = 0; i < N0MAX; ++i)
-        if (i < n0) acc[i] += xs[r * n0 + i] * g;
-      sacc += g;
-      if (gout) gout[o] = g;
+      for (int u = 0; u < U; ++u) {  // U rows' loads in flight before any use
+        const int r = r0b + u * P;
+        const int64_t o = (r0 + (r < nr ? r : 0)) * nl + j;
+        g[u] = r < nr ? act_grad<ACT>(dy[o], ACT ? y[o] : 0.f) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = r0b + u * P;
+        if (r < nr) {
+#pragma unroll
+          for (int i = 0; i < N0MAX; ++i)
+            if (i < n0) acc[i] += xs[r * n0 + i] * g[u];
+          sacc += g[u];
+          if (gout) gout[(r0 + r) * nl + j] = g[u];
+        }
+      }
     }
   }
 #pragma unroll
@@ -215,6 +226,134 @@ __global__ __launch_bounds__(256) void chain_reduce_outer_kernel(
     for (int q = 0; q < P; ++q) v += red[(q * nlp + jj) * (N0MAX + 1) + slot];
     pp[(int64_t)i * nl + jj] = v;
   }
+}
+
+// nl % 4 == 0, nl <= 256, n0 <= N0MAX: thread (phase, column quad) moves 16 B of dy and of y
+// per row; 256 / (nl / 4) row phases walk the chunk's rows interleaved, 4 rows in flight; the
+// phases are folded in phase order through LDS (one phase per round: deterministic)
+constexpr int kQuadRows = 128;
+
+template <int ACT, int N0MAX>
+__global__ __launch_bounds__(256) void chain_reduce_quad_kernel(
+    const float* __restrict__ x, int64_t ldx, int n0, const float* __restrict__ dy,
+    const float* __restrict__ y, int nl, int64_t B, float* __restrict__ gout,
+    float* __restrict__ part) {
+  __shared__ float xs[kQuadRows * N0MAX];
+  __shared__ float red[(N0MAX + 1) * 256];
+  const int t = threadIdx.x;
+  const int nq = nl / 4;
+  const int P = 256 / nq;
+  const int q = t % nq, ph = t / nq;
+  const int j0 = 4 * q;
+  const int64_t r0 = (int64_t)blockIdx.x * kQuadRows;
+  const int64_t r1 = r0 + kQuadRows < B ? r0 + kQuadRows : B;
+  const int nr = (int)(r1 - r0);
+  for (int e = t; e < nr * n0; e += 256) {
+    const int rr = e / n0;
+    xs[e] = x[(r0 + rr) * ldx + (e - rr * n0)];
+  }
+  __syncthreads();
+  float4 acc[N0MAX];
+#pragma unroll
+  for (int i = 0; i < N0MAX; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int U = 4;
+  if (ph < P) {
+    for (int rb = ph; rb < nr; rb += U * P) {
+      float4 g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = rb + u * P;
+        const int64_t o = (r0 + (r < nr ? r : 0)) * nl + j0;
+        const float4 d = *reinterpret_cast<const float4*>(dy + o);
+        float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ACT) yy = *reinterpret_cast<const float4*>(y + o);
+        g[u] = r < nr ? make_float4(act_grad<ACT>(d.x, yy.x), act_grad<ACT>(d.y, yy.y),
+                                    act_grad<ACT>(d.z, yy.z), act_grad<ACT>(d.w, yy.w))
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = rb + u * P;
+        if (r < nr) {
+#pragma unroll
+          for (int i = 0; i < N0MAX; ++i) {
+            if (i < n0) {
+              const float xv = xs[r * n0 + i];
+              acc[i].x += xv * g[u].x;
+              acc[i].y += xv * g[u].y;
+              acc[i].z += xv * g[u].z;
+              acc[i].w += xv * g[u].w;
+            }
+          }
+          sacc.x += g[u].x;
+          sacc.y += g[u].y;
+          sacc.z += g[u].z;
+          sacc.w += g[u].w;
+          if (gout)
+            *reinterpret_cast<float4*>(gout + (r0 + r) * nl + j0) = g[u];
+        }
+      }
+    }
+  }
+  // fold the phases in order: red[i][column] (i == N0MAX: the column sum)
+  for (int p = 0; p < P; ++p) {
+    if (ph == p) {
+#pragma unroll
+      for (int i = 0; i <= N0MAX; ++i) {
+        if (i < n0 || i == N0MAX) {
+          const float4 v = i == N0MAX ? sacc : acc[i];
+          float* dst = red + i * 256 + j0;
+          if (p == 0) {
+            dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+          } else {
+            dst[0] += v.x; dst[1] += v.y; dst[2] += v.z; dst[3] += v.w;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* pp = part + (int64_t)blockIdx.x * ((int64_t)n0 * nl + nl);
+  for (int e = t; e < (n0 + 1) * nl; e += 256) {
+    const int i = e / nl, j = e - i * nl;
+    pp[(int64_t)i * nl + j] = red[(i == n0 ? N0MAX : i) * 256 + j];
+  }
+}
+
+// first level of a two-level fold for many chunks of a narrow row: block (cx, seg) folds the
+// chunks of its segment (4 waves interleaved, then in wave order) into part2[seg][col]
+__global__ __launch_bounds__(256) void fold_segments_kernel(const float* __restrict__ part,
+                                                            int nchunks, int per_seg, int N,
+                                                            float* __restrict__ part2) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int c0 = blockIdx.y * per_seg;
+  const int c1 = min(c0 + per_seg, nchunks);
+  float s = 0.f;
+  if (col < N) {
+#pragma unroll 4
+    for (int c = c0 + w; c < c1; c += 4) s += part[(int64_t)c * N + col];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < N)
+    part2[(int64_t)blockIdx.y * N + col] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// fixed two-level fold of nchunks partial rows [N] (deterministic for given nchunks)
+static int32_t fold_two_level(const float* part, int nchunks, int N, float* part2, float* out,
+                              hipStream_t st) {
+  constexpr int kSeg = 32;
+  const int per = (int)ceil_div(nchunks, kSeg);
+  const int nseg = (int)ceil_div(nchunks, per);
+  fold_segments_kernel<<<dim3((unsigned)ceil_div(N, 64), (unsigned)nseg), 256, 0, st>>>(
+      part, nchunks, per, N, part2);
+  RS_CHECK_LAUNCH();
+  fold_chunks_kernel<<<(unsigned)ceil_div(N, 64), 256, 0, st>>>(part2, nseg, N, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
 }
 
 }  // namespace rs
@@ -264,7 +403,8 @@ extern "C" int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B,
 
 extern "C" size_t rs_chain_reduce_workspace_size(int64_t B, int32_t n0, int32_t nl) {
   const int rows = nl == 1 ? kVecRows : kChainRows;
-  return (size_t)ceil_div(B < 1 ? 1 : B, rows) * ((size_t)n0 * nl + nl) * sizeof(float);
+  // chunk partials + 32 segment partials of the two-level fold
+  return ((size_t)ceil_div(B < 1 ? 1 : B, rows) + 32) * ((size_t)n0 * nl + nl) * sizeof(float) + 256;
 }
 
 extern "C" int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, const float* dy,
@@ -297,6 +437,24 @@ extern "C" int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, cons
       case 1: chain_reduce_vec_kernel<1><<<nchunks, 256, 0, st>>>(x, ldx, n0, cgp, dy, y, B, g_out, part); break;
       default: chain_reduce_vec_kernel<2><<<nchunks, 256, 0, st>>>(x, ldx, n0, cgp, dy, y, B, g_out, part); break;
     }
+  } else if (nl % 4 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0 &&
+             (!y || (reinterpret_cast<uintptr_t>(y) & 15) == 0) &&
+             (!g_out || (reinterpret_cast<uintptr_t>(g_out) & 15) == 0)) {
+    nchunks = (int)ceil_div(B, kQuadRows);
+    auto go = [&](auto kern) { kern<<<nchunks, 256, 0, st>>>(x, ldx, n0, dy, y, nl, B, g_out, part); };
+    if (n0 <= 16) {
+      switch (act) {
+        case 0: go(chain_reduce_quad_kernel<0, 16>); break;
+        case 1: go(chain_reduce_quad_kernel<1, 16>); break;
+        default: go(chain_reduce_quad_kernel<2, 16>); break;
+      }
+    } else {
+      switch (act) {
+        case 0: go(chain_reduce_quad_kernel<0, 32>); break;
+        case 1: go(chain_reduce_quad_kernel<1, 32>); break;
+        default: go(chain_reduce_quad_kernel<2, 32>); break;
+      }
+    }
   } else {
     int nlp = 1;
     while (nlp < nl) nlp <<= 1;
@@ -316,7 +474,5 @@ extern "C" int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, cons
     }
   }
   RS_CHECK_LAUNCH();
-  fold_chunks_kernel<<<(unsigned)ceil_div(M, 64), 256, 0, st>>>(part, nchunks, M, out);
-  RS_CHECK_LAUNCH();
-  return RS_OK;
+  return fold_two_level(part, nchunks, M, part + (size_t)nchunks * M, out, st);
 }

@@ -34,7 +34,7 @@ class TrainStep:
 
     def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
                  fused=True, overlap_wgrad=False, comm=None, defer_sparse_join=False,
-                 overlap_param_grads=True):
+                 overlap_param_grads=False):
         """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
         all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
         by its owners inside the backward."""
@@ -53,7 +53,8 @@ class TrainStep:
         # measured on MI355X: a weight-grad GEMM beside the interaction backward only
         # time-slices the CUs (no net gain), so the overlap is opt-in
         self.wgrad = overlapped_weight_grads(dense[0].device) if overlap_wgrad else None
-        # the MLP chains' parameter gradients beside the interaction backward / sparse apply
+        # opt-in: the MLP chains' parameter gradients on a second stream (measured: they slow the
+        # co-running interaction backward by as much as they hide, 320 -> 364 us)
         self.pgrad = (overlapped_param_grads(dense[0].device) if overlap_param_grads
                       else contextlib.nullcontext())
         if optimizer == "sgd":

@@ -23,10 +23,18 @@ def _ids_flat(ids: torch.Tensor) -> torch.Tensor:
     return ids
 
 
+def _wait_update(table_module):
+    """Order this stream after a deferred sparse update of the table (Embedding.wait_update);
+    table views without deferred updates (e.g. a sharded exchange's unique rows) have none."""
+    w = getattr(table_module, "wait_update", None)
+    if w is not None:
+        w()
+
+
 class _EmbeddingLookup(torch.autograd.Function):
     @staticmethod
     def forward(ctx, handle, table_module, ids):
-        table_module.wait_update()
+        _wait_update(table_module)
         w = table_module.weight
         L.require_device(w, "embedding table")
         ids = _ids_flat(ids)
@@ -94,7 +102,7 @@ class _DLRMInteraction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, handle, dense, table_module, ids, compact):
-        table_module.wait_update()
+        _wait_update(table_module)
         w = table_module.weight
         L.require_device(w, "embedding table")
         ids = _ids_flat(ids)

@@ -143,12 +143,15 @@ class SparseOptimizer:
     def apply_async(self, table: Embedding, ids, grad_rows, sorted_ids: SortedIds):
         if id(table) in self._applied:
             raise RuntimeError("fused sparse optimizer: a table was looked up twice in one step")
+        self._launch_apply(table, ids, grad_rows, sorted_ids)
+        self._applied.add(id(table))
+
+    def _launch_apply(self, table, ids, grad_rows, sorted_ids):
         main = torch.cuda.current_stream(grad_rows.device)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             self.apply(table, ids, grad_rows, self._params(), sorted_ids=sorted_ids)
         grad_rows.record_stream(self.side)
-        self._applied.add(id(table))
 
     def _params(self) -> L.AdamParams:
         lr = self.lr(self.iterations) if callable(self.lr) else self.lr
