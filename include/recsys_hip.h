@@ -378,6 +378,19 @@ int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, const float* dy
                         int32_t nl, int32_t act, int64_t B, float* out, float* g_out,
                         void* workspace, size_t ws_bytes, void* stream);
 
+/* Parameter gradients of a 3-layer linear chain with a scalar output ([n1, n2, 1], e.g. the
+ * DLRM / DeepFM top MLP) from A = xᵀ·G [n0] and s = Σ G [1] (rs_chain_reduce): kernels
+ * K1 [n_full0, n1] (the input holds rows[n0] of it, inv[n_full0] = position in rows or -1;
+ * both NULL: all rows), K2 [n1, n2], K3 [n2]; biases b1, b2 may be NULL. Writes dK1
+ * [n_full0, n1] (zero rows outside `rows`), db1, dK2 [n1, n2], db2, dK3 [n2], db3 [1] and
+ * p [n0] = K1[rows]·K2·K3 (the input gradient is G ⊗ p). Workspace >= 4·(2·n1 + 2·n2) bytes. */
+int32_t rs_chain3_vec_grads(const float* K1, const int32_t* rows, const int32_t* inv,
+                            int32_t n_full0, int32_t n0, const float* b1, const float* K2,
+                            const float* b2, const float* K3, int32_t n1, int32_t n2,
+                            const float* A, const float* s, float* dK1, float* db1, float* dK2,
+                            float* db2, float* dK3, float* db3, float* p, void* workspace,
+                            size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Keras thresholded AUC (keras.metrics.AUC in ctr/train.py:86,
  * dien/train.py:43-44, esmm/train.py:164). thresholds [n_thresholds] ascending float32 (the

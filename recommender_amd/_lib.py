@@ -112,6 +112,8 @@ _SIGS = {
                                              _i64, _p, _p, _p]),
     "rs_chain_reduce_workspace_size": (_sz, [_i64, _i32, _i32]),
     "rs_chain_reduce": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _sz, _p]),
+    "rs_chain3_vec_grads": (_i32, [_p, _p, _p, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _p,
+                                   _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_vocab_count_masked": (_i32, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
     "rs_kv_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p,
                            _p, _p]),

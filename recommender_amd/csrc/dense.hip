@@ -321,6 +321,137 @@ __global__ __launch_bounds__(256) void chain_reduce_quad_kernel(
   }
 }
 
+// ---- parameter gradients of a 3-layer linear chain with a scalar output --------------------
+// (the DLRM / DeepFM top MLP [n1, n2, 1]; see recommender_amd/nn.py chain_param_grads). With
+// q2 = K3, q1 = K2·q2, T2 = K1[r]ᵀ·A, c2 = K2ᵀ·b1 + b2, T3 = K2ᵀ·T2, p = K1[r]·q1:
+//   dK1[r[a], :] = A[a]·q1 (other rows 0), dK2 = (T2 + b1·s) ⊗ q2, dK3 = T3 + c2·s,
+//   db1 = q1·s, db2 = q2·s, db3 = s, and p = Q_0 (the rank-one input gradient's row).
+// Three launches of fixed-order dot products (deterministic).
+struct Chain3Args {
+  const float* K1;    // [n_full0, n1]
+  const int32_t* r;   // [n0] rows of K1 the input holds (nullptr: identity, n_full0 == n0)
+  const int32_t* inv; // [n_full0] position of each K1 row in r, -1 if absent (nullptr: identity)
+  const float* b1;    // [n1] (nullable)
+  const float* K2;    // [n1, n2]
+  const float* b2;    // [n2] (nullable)
+  const float* K3;    // [n2]
+  const float* A;     // [n0]
+  const float* s;     // [1]
+  int n_full0, n0, n1, n2;
+  float* q1;          // [n1] scratch
+  float* T2;          // [n1] scratch
+  float* c2;          // [n2] scratch
+  float* T3;          // [n2] scratch
+  float* dK1;         // [n_full0, n1]
+  float* db1;         // [n1]
+  float* dK2;         // [n1, n2]
+  float* db2;         // [n2]
+  float* dK3;         // [n2]
+  float* db3;         // [1]
+  float* p;           // [n0]
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// out[i] = Σ_k M[row(i), k] · v[k] (one wave per output, lanes stride k, fixed butterfly)
+__device__ __forceinline__ void rowdot_wave(const float* M, int ld, int i_row, int n,
+                                            const float* v, float* out_i, int lane) {
+  float acc = 0.f;
+  for (int k = lane; k < n; k += 64) acc += M[(int64_t)i_row * ld + k] * v[k];
+  acc = wave_sum(acc);
+  if (lane == 0) *out_i = acc;
+}
+
+// out[c] = Σ_k M[row(k), c] · v[k] (+ add[c]) for a 64-column tile: 4 waves stride k, folded
+// in wave order
+__device__ __forceinline__ void coldot_tile(const float* M, int ld, const int32_t* rowmap, int n,
+                                            int ncol, int c0, const float* v, const float* add,
+                                            float* out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = c0 + lane;
+  float acc = 0.f;
+  if (c < ncol)
+    for (int k = w; k < n; k += 4) acc += M[(int64_t)(rowmap ? rowmap[k] : k) * ld + c] * v[k];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < ncol) {
+    float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    out[c] = add ? t + add[c] : t;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void chain3_stage1(Chain3Args a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nq = (a.n1 + 3) / 4;   // q1 blocks (4 waves each)
+  const int nt = (a.n1 + 63) / 64;  // T2 column tiles
+  int blk = blockIdx.x;
+  if (blk < nq) {
+    const int i = blk * 4 + w;
+    if (i < a.n1) rowdot_wave(a.K2, a.n2, i, a.n2, a.K3, a.q1 + i, lane);
+    return;
+  }
+  blk -= nq;
+  if (blk < nt) {
+    coldot_tile(a.K1, a.n1, a.r, a.n0, a.n1, blk * 64, a.A, nullptr, a.T2);
+    return;
+  }
+  blk -= nt;
+  // c2 = K2ᵀ·b1 + b2
+  if (a.b1) {
+    coldot_tile(a.K2, a.n2, nullptr, a.n1, a.n2, blk * 64, a.b1, a.b2, a.c2);
+  } else if (threadIdx.x < 64) {
+    const int c = blk * 64 + threadIdx.x;
+    if (c < a.n2) a.c2[c] = a.b2 ? a.b2[c] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void chain3_stage2(Chain3Args a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int npb = (a.n0 + 3) / 4;
+  if ((int)blockIdx.x < npb) {
+    const int i = blockIdx.x * 4 + w;
+    if (i < a.n0) rowdot_wave(a.K1, a.n1, a.r ? a.r[i] : i, a.n1, a.q1, a.p + i, lane);
+    return;
+  }
+  coldot_tile(a.K2, a.n2, nullptr, a.n1, a.n2, (blockIdx.x - npb) * 64, a.T2, nullptr, a.T3);
+}
+
+__global__ __launch_bounds__(256) void chain3_stage3(Chain3Args a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const float s = a.s[0];
+  const int64_t n_k1 = (int64_t)a.n_full0 * a.n1, n_k2 = (int64_t)a.n1 * a.n2;
+  if (e < n_k1) {
+    const int row = (int)(e / a.n1), col = (int)(e - (int64_t)row * a.n1);
+    const int ai = a.inv ? a.inv[row] : row;
+    a.dK1[e] = ai >= 0 ? a.A[ai] * a.q1[col] : 0.f;
+    return;
+  }
+  int64_t f = e - n_k1;
+  if (f < n_k2) {
+    const int b = (int)(f / a.n2), d = (int)(f - (int64_t)b * a.n2);
+    const float m2 = a.b1 ? a.T2[b] + a.b1[b] * s : a.T2[b];
+    a.dK2[f] = m2 * a.K3[d];
+    return;
+  }
+  f -= n_k2;
+  if (f < a.n2) {
+    a.dK3[f] = a.T3[f] + a.c2[f] * s;
+    a.db2[f] = a.K3[f] * s;
+    return;
+  }
+  f -= a.n2;
+  if (f < a.n1) {
+    a.db1[f] = a.q1[f] * s;
+    return;
+  }
+  if (f == a.n1) a.db3[0] = s;
+}
+
 // first level of a two-level fold for many chunks of a narrow row: block (cx, seg) folds the
 // chunks of its segment (4 waves interleaved, then in wave order) into part2[seg][col]
 __global__ __launch_bounds__(256) void fold_segments_kernel(const float* __restrict__ part,
@@ -475,4 +606,31 @@ extern "C" int32_t rs_chain_reduce(const float* x, int64_t ldx, int32_t n0, cons
   }
   RS_CHECK_LAUNCH();
   return fold_two_level(part, nchunks, M, part + (size_t)nchunks * M, out, st);
+}
+
+extern "C" int32_t rs_chain3_vec_grads(const float* K1, const int32_t* rows, const int32_t* inv,
+                                       int32_t n_full0, int32_t n0, const float* b1,
+                                       const float* K2, const float* b2, const float* K3,
+                                       int32_t n1, int32_t n2, const float* A, const float* s,
+                                       float* dK1, float* db1, float* dK2, float* db2, float* dK3,
+                                       float* db3, float* p, void* workspace, size_t ws_bytes,
+                                       void* stream) {
+  RS_CHECK_ARG(n0 >= 1 && n1 >= 1 && n2 >= 1 && n_full0 >= n0 && (rows != nullptr) == (inv != nullptr) &&
+                   (rows || n_full0 == n0),
+               "rs_chain3_vec_grads: bad sizes");
+  RS_CHECK_ARG(ws_bytes >= (size_t)(2 * n1 + 2 * n2) * sizeof(float), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* w = static_cast<float*>(workspace);
+  Chain3Args a{K1, rows, inv, b1, K2, b2, K3, A, s, n_full0, n0, n1, n2,
+               w, w + n1, w + 2 * n1, w + 2 * n1 + n2, dK1, db1, dK2, db2, dK3, db3, p};
+  const unsigned g1 = (unsigned)(ceil_div(n1, 4) + ceil_div(n1, 64) + ceil_div(n2, 64));
+  chain3_stage1<<<g1, 256, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  const unsigned g2 = (unsigned)(ceil_div(n0, 4) + ceil_div(n2, 64));
+  chain3_stage2<<<g2, 256, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  const int64_t tot = (int64_t)n_full0 * n1 + (int64_t)n1 * n2 + n2 + n1 + 1;
+  chain3_stage3<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
 }

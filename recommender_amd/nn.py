@@ -316,6 +316,9 @@ def chain_param_grads(layers, rows, ks, A, s):
     c_i = K_iᵀ·c_{i-1} + b_i, runs on the overlapped parameter-gradient stream when one is
     active (matrix-vector chains when the output width is 1)."""
     n = len(layers)
+    if (n == 3 and A.is_cuda and A.shape[1] == 1 and ks[2].shape[1] == 1
+            and all(l.bias is not None for l in layers)):
+        return _chain3_vec_grads(layers, rows, ks, A, s)
     Qa = [None] * n  # Qa[i] = K_{i+1}···K_L (None: identity)
     for i in range(n - 2, -1, -1):
         Qa[i] = ks[i + 1] if Qa[i + 1] is None else ks[i + 1] @ Qa[i + 1]
@@ -346,6 +349,48 @@ def chain_param_grads(layers, rows, ks, A, s):
                 else:
                     c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
     return Q0
+
+
+_inv_cache: dict = {}
+
+
+def _chain3_vec_grads(layers, rows, ks, A, s):
+    """chain_param_grads for a [n1, n2, 1] chain in three launches (rs_chain3_vec_grads)."""
+    from . import _lib as L
+
+    K1, K2, K3 = layers[0].kernel, layers[1].kernel, layers[2].kernel
+    n_full0, n1 = K1.shape
+    n2 = K2.shape[1]
+    n0 = A.shape[0]
+    dev = A.device
+    r = inv = None
+    if rows is not None:
+        key = (rows.data_ptr(), n_full0)
+        hit = _inv_cache.get(key)
+        if hit is None or hit[0] is not rows:
+            r = rows.to(torch.int32).contiguous()
+            inv = torch.full((n_full0,), -1, dtype=torch.int32, device=dev)
+            inv[r.long()] = torch.arange(n0, dtype=torch.int32, device=dev)
+            hit = (rows, r, inv)
+            _inv_cache[key] = hit
+        _, r, inv = hit
+    dK1 = torch.empty_like(K1)
+    dK2 = torch.empty_like(K2)
+    dK3 = torch.empty_like(K3)
+    db1 = torch.empty(n1, device=dev)
+    db2 = torch.empty(n2, device=dev)
+    db3 = torch.empty(1, device=dev)
+    p = torch.empty(n0, 1, device=dev)
+    ws = torch.empty(2 * n1 + 2 * n2, device=dev)
+    L.call("rs_chain3_vec_grads", L.ptr(K1), L.ptr(r), L.ptr(inv), n_full0, n0,
+           L.ptr(layers[0].bias), L.ptr(K2), L.ptr(layers[1].bias), L.ptr(K3), n1, n2,
+           L.ptr(A.contiguous()), L.ptr(s.contiguous()), L.ptr(dK1), L.ptr(db1), L.ptr(dK2),
+           L.ptr(db2), L.ptr(dK3), L.ptr(db3), L.ptr(p), L.ptr(ws), ws.numel() * 4,
+           L.stream_ptr(dev))
+    for layer, dk, db in zip(layers, (dK1, dK2, dK3), (db1, db2, db3)):
+        _accum_grad(layer.kernel, dk)
+        _accum_grad(layer.bias, db)
+    return p
 
 
 def chain_forward(x, layers, rows=None):
