@@ -400,6 +400,16 @@ def dlrm_path(iters, out):
         tot += us
         report(name + " (alone)", {"B": B, "S": S, "D": D, "rows": V, "unique": U}, us,
                kernel_bytes(name, B, S, D, 8, U), out)
+    # what-if: the same apply reading its grad rows in sorted order (contiguous)
+    ident = torch.arange(B * S, dtype=torch.int32, device=DEV)
+
+    def apply_sorted():
+        L.call("rs_embedding_apply", L.RS_OPT_SGD, L.ptr(table), None, None, V, D, L.ptr(s0.rows),
+               L.ptr(ident), B * S, L.ptr(gemb), prm, None, L.ptr(ws), ws.numel(), st)
+
+    us = timed(apply_sorted, iters)
+    report("rs_embedding_apply (grad rows pre-permuted to sorted order, what-if)",
+           {"B": B, "S": S, "D": D, "unique": U}, us, kernel_bytes("rs_embedding_apply", B, S, D, 8, U), out)
     per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
     report("embedding_path (4 launches back to back, alone)",
            {"B": B, "S": S, "D": D, "unique": U, "bytes_per_example": round(per_ex, 1)},
