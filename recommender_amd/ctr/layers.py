@@ -21,6 +21,9 @@ class MLP(nn.Module):
     way and bit-identical between the two."""
 
     factored_backward = True
+    # below this batch the layerwise backward's few GEMMs cost less than the chain's extra
+    # launches (DeepFM cfg1, B 1024: 1.20 ms layerwise vs 1.49 ms factored per step)
+    factored_min_batch = 8192
 
     def __init__(self, units, final_activation, in_features=None, device=None, generator=None):
         super().__init__()
@@ -37,6 +40,7 @@ class MLP(nn.Module):
         """True when the forward runs as one linear chain (factored backward)."""
         layers = list(self.mlp)
         return (self.factored_backward and x.dim() == 2 and x.is_cuda and torch.is_grad_enabled()
+                and x.shape[0] >= self.factored_min_batch
                 and all(l.kernel is not None and l.act_code >= 0 for l in layers)
                 and all(l.act_code == 0 for l in layers[:-1]))
 

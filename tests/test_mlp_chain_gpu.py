@@ -15,6 +15,15 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _factored_at_any_batch():
+    """The production path factors from batch 8192 up; these tests use small batches."""
+    old = MLP.factored_min_batch
+    MLP.factored_min_batch = 0
+    yield
+    MLP.factored_min_batch = old
+
+
 def _make(units, act, fin, seed):
     g = torch.Generator(device=DEV)
     g.manual_seed(seed)

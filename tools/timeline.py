@@ -16,12 +16,14 @@ def short(n):
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "inter_fwd" in r["Kernel_Name"]]
+marker = sys.argv[3] if len(sys.argv) > 3 else "inter_fwd"
+starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 step = int(sys.argv[2]) if len(sys.argv) > 2 else -2
 a, b = starts[step], starts[step + 1]
 # include the bottom-MLP kernels before the interaction: start from the previous step's last
 t_first = int(rows[a]["Start_Timestamp"])
-seg = rows[a - 12:b - 12] if a >= 12 else rows[a:b]
+back = int(sys.argv[4]) if len(sys.argv) > 4 else 12
+seg = rows[a - back:b - back] if a >= back else rows[a:b]
 t0 = int(seg[0]["Start_Timestamp"])
 busy = {}
 for r in seg:
