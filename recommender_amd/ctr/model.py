@@ -107,11 +107,14 @@ class DLRM(nn.Module):
             out = self.top_mlp(tmlp_input).squeeze(1)
         else:
             layers = list(self.top_mlp.mlp)
-            if (self._exchanged is None and self.embedding_size == 128 and torch.is_grad_enabled()
+            if (self.embedding_size == 128 and torch.is_grad_enabled()
                     and self.top_mlp.chain_ready(bmlp_activation)):
                 # interaction + top MLP as one linear chain: rank-one interaction backward
-                out = dlrm_top(self.embedding_layer, cat_features, bmlp_activation, layers,
-                               self.compact_rows).squeeze(1)
+                # (a row-sharded slab hands this step's exchanged unique rows + inverse index)
+                table, ids = self.embedding_layer, cat_features
+                if self._exchanged is not None:
+                    (table, ids), self._exchanged = self._exchanged, None
+                out = dlrm_top(table, ids, bmlp_activation, layers, self.compact_rows).squeeze(1)
             else:
                 tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
                 out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)

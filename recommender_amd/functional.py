@@ -189,10 +189,16 @@ class _DLRMTopFn(torch.autograd.Function):
         grad_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
         grad_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
         p = Q[:, 0].contiguous()
-        L.call("rs_dlrm_interaction_bwd_rank1", L.ptr(w), w.shape[0], D, L.ptr(ids),
-               L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, L.ptr(G),
-               L.ptr(p), p.numel(), L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
-        if tm.fused_optimizer is not None:
+        if all(t.data_ptr() % 16 == 0 for t in (w, dense, grad_emb, grad_dense)):
+            L.call("rs_dlrm_interaction_bwd_rank1", L.ptr(w), w.shape[0], D, L.ptr(ids),
+                   L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, L.ptr(G),
+                   L.ptr(p), p.numel(), L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
+        else:  # unaligned buffers: the same rows, materialised
+            g = (G * p[None, :]).contiguous()
+            L.call("rs_dlrm_interaction_bwd", L.ptr(w), w.shape[0], D, L.ptr(ids),
+                   L.id_dtype_code(ids), S, L.ptr(tm.slot_offsets), L.ptr(dense), B, 1, L.ptr(g),
+                   g.shape[1], L.ptr(grad_emb), L.ptr(grad_dense), L.stream_ptr(w.device))
+        if getattr(tm, "fused_optimizer", None) is not None:
             tm.fused_optimizer.apply_async(tm, ids, grad_emb, tm.take_presorted(ids))
         else:
             tm.accumulate_grad(ids, grad_emb)

@@ -11,18 +11,33 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def test_world1_sharded_dlrm_equals_unsharded():
+@pytest.mark.parametrize("D", [32, 128])
+def test_world1_sharded_dlrm_equals_unsharded(D):
+    """D = 128 with the factored path forced on takes the fused interaction + top chain with the
+    rank-one backward, over the sharded exchange's unique rows."""
+    from recommender_amd.ctr.layers import MLP
     from recommender_amd.ctr.model import DLRM
     from recommender_amd.ctr.train import TrainStep
     from recommender_amd.sharded import Comm, ShardedSlabEmbedding
     from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
 
+    old_min = MLP.factored_min_batch
+    MLP.factored_min_batch = 0 if D == 128 else old_min
+    try:
+        _sharded_vs_unsharded(D, criteo_cardinalities, criteo_batch, DLRM, TrainStep, Comm,
+                              ShardedSlabEmbedding)
+    finally:
+        MLP.factored_min_batch = old_min
+
+
+def _sharded_vs_unsharded(D, criteo_cardinalities, criteo_batch, DLRM, TrainStep, Comm,
+                          ShardedSlabEmbedding):
     cards = criteo_cardinalities(200_000, 26)
     g = torch.Generator(device=DEV)
     g.manual_seed(1)
-    m1 = DLRM([64, 32], [64, 1], 32, sum(cards), 26, 13, device=DEV, slot_cardinalities=cards, generator=g)
-    emb = ShardedSlabEmbedding(cards, 32, Comm(), device=DEV, full_weight=m1.embedding_layer.weight)
-    m2 = DLRM([64, 32], [64, 1], 32, sum(cards), 26, 13, device=DEV, embedding_layer=emb)
+    m1 = DLRM([64, D], [64, 1], D, sum(cards), 26, 13, device=DEV, slot_cardinalities=cards, generator=g)
+    emb = ShardedSlabEmbedding(cards, D, Comm(), device=DEV, full_weight=m1.embedding_layer.weight)
+    m2 = DLRM([64, D], [64, 1], D, sum(cards), 26, 13, device=DEV, embedding_layer=emb)
     sd = {k: v for k, v in m1.state_dict().items() if not k.startswith("embedding_layer")}
     m2.load_state_dict(sd, strict=False)
     s1, s2 = TrainStep(m1, "sgd", lr=0.05), TrainStep(m2, "sgd", lr=0.05)
