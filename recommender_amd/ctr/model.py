@@ -97,10 +97,15 @@ class DLRM(nn.Module):
         cat_features, int_features = x["cat_features"], x["int_features"]
         int_features = int_features.reshape(-1, self.num_int_fea).float()
         cat_features = cat_features.reshape(-1, self.num_cat_fea)
+        pending = None
+        if hasattr(self.embedding_layer, "exchange_begin"):
+            # row-sharded slab: the sort / split-size exchange is queued first (side stream), so
+            # it runs beside the bottom MLP; the host waits for the split sizes only after the
+            # bottom MLP is queued
+            pending = self.embedding_layer.exchange_begin(cat_features)
         bmlp_activation = self.bottom_mlp(int_features)
-        if hasattr(self.embedding_layer, "exchange"):
-            # row-sharded slab: the all-to-all exchange (side stream) overlaps the bottom MLP
-            self._exchanged = self.embedding_layer.exchange(cat_features)
+        if pending is not None:
+            self._exchanged = self.embedding_layer.exchange_finish(pending)
         if not self.compact:
             tmlp_input = self.interact(cat_features, bmlp_activation)
             tmlp_input = tmlp_input.reshape(-1, (self.num_cat_fea + 1) ** 2 + self.embedding_size)

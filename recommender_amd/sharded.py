@@ -121,8 +121,10 @@ class ShardedSlabEmbedding(nn.Module):
         self.optimizer = opt
 
     # ---------------------------------------------------------------- forward
-    def exchange(self, ids: torch.Tensor):
-        """Fetch this step's unique rows; returns (view, inverse ids [B, S] int32)."""
+    def exchange_begin(self, ids: torch.Tensor):
+        """Queue the owner-major sort, the unique / inverse pass and the split-size exchange on
+        the side stream without blocking the host; DLRM calls this before it queues the bottom
+        MLP, so the sort runs beside it (the side stream only waits for work queued so far)."""
         L.require_device(ids, "ids")
         dev = ids.device
         ids = ids.contiguous()
@@ -141,17 +143,40 @@ class ShardedSlabEmbedding(nn.Module):
             L.call("rs_unique_inverse", L.ptr(s.rows), L.ptr(s.pos), n, self.input_dim, W,
                    L.ptr(uniq), L.ptr(inverse), L.ptr(n_unique), L.ptr(counts), L.ptr(w),
                    w.numel(), L.stream_ptr(dev))
-            send_counts = counts.cpu()  # the one host sync of the step (split sizes)
+            staged = self.comm.staged or not dist.is_initialized() or W == 1
+            host = torch.empty(2 * W, dtype=torch.int32, pin_memory=True)
+            if staged:
+                host[:W].copy_(counts, non_blocking=True)
+            else:
+                # receive counts device to device, then ONE copy of both count vectors to the host
+                recv = torch.empty_like(counts)
+                dist.all_to_all_single(recv, counts, group=self.comm.group)
+                host.copy_(torch.cat([counts, recv]), non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(self.side)
+        return dict(ids=ids, s=s, uniq=uniq, inverse=inverse, host=host, ready=ready,
+                    staged=staged, dev=dev)
+
+    def exchange_finish(self, st):
+        """Wait (host) for the split sizes, then the two all-to-alls and the owner gather;
+        returns (view, inverse ids [B, S] int32)."""
+        dev, W = st["dev"], self.world
+        main = torch.cuda.current_stream(dev)
+        st["ready"].synchronize()  # the one host sync of the step (split sizes)
+        send_counts = st["host"][:W].clone()
+        with torch.cuda.stream(self.side):
             U = int(send_counts.sum())
-            if W > 1:
+            if W == 1:
+                recv_counts = send_counts
+            elif st["staged"]:
                 recv_counts = torch.empty(W, dtype=torch.int32)
                 self.comm_counts(recv_counts, send_counts)
             else:
-                recv_counts = send_counts
+                recv_counts = st["host"][W:].clone()
             R = int(recv_counts.sum())
             owner = torch.arange(W, device=dev, dtype=torch.int64).repeat_interleave(
                 send_counts.to(dev, torch.int64), output_size=U)
-            send_rows = (uniq[:U].to(torch.int64) - owner * self.stride).to(torch.int32)
+            send_rows = (st["uniq"][:U].to(torch.int64) - owner * self.stride).to(torch.int32)
             recv_rows = torch.empty(R, dtype=torch.int32, device=dev)
             sc, rc = send_counts.tolist(), recv_counts.tolist()
             self.comm.all_to_all(recv_rows, send_rows, rc, sc)
@@ -159,13 +184,19 @@ class ShardedSlabEmbedding(nn.Module):
                 served = self.shard(recv_rows) if R else torch.empty(0, self.output_dim, device=dev)
             rows = torch.empty(U, self.output_dim, device=dev)
             self.comm.all_to_all(rows, served.detach().contiguous(), sc, rc)
+        inverse = st["inverse"]
         main.wait_stream(self.side)
         for t in (rows, inverse):
             t.record_stream(main)
         self.view.weight = rows
         self.view.input_dim = U
-        self._st = dict(sorted=s, U=U, R=R, send_counts=sc, recv_counts=rc, recv_rows=recv_rows)
-        return self.view, inverse.view(ids.shape)
+        self._st = dict(sorted=st["s"], U=U, R=R, send_counts=sc, recv_counts=rc,
+                        recv_rows=recv_rows)
+        return self.view, inverse.view(st["ids"].shape)
+
+    def exchange(self, ids: torch.Tensor):
+        """Fetch this step's unique rows; returns (view, inverse ids [B, S] int32)."""
+        return self.exchange_finish(self.exchange_begin(ids))
 
     def comm_counts(self, recv_counts: torch.Tensor, send_counts: torch.Tensor):
         if self.comm.staged or not dist.is_initialized():
