@@ -67,6 +67,8 @@ def parse():
                     help="ctr MLP backward: factored linear chain (default) or layer by layer")
     ap.add_argument("--compare-layerwise", type=int, default=1,
                     help="1: after the timed steps, also time the layer-by-layer MLP backward")
+    ap.add_argument("--tuned-gemms", type=int, default=1,
+                    help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py)")
     ap.add_argument("--pmc", type=int, default=1,
                     help="1: measure the roofline kernel's HBM traffic with two rocprofv3 --pmc "
                          "child runs (FETCH_SIZE, WRITE_SIZE) before this process touches the GPU")
@@ -95,7 +97,8 @@ def measure_traffic(args):
              "--cpu-baseline-steps", "0", "--pmc", "0", "--batch", str(args.batch), "--rows",
              str(args.rows), "--dim", str(args.dim), "--slots", str(args.slots), "--optimizer",
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
-             str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd, "--compare-layerwise", "0"]
+             str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd,
+             "--compare-layerwise", "0", "--tuned-gemms", str(args.tuned_gemms)]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -235,6 +238,10 @@ def main():
     L.load()
     if L.lib().rs_device_count() < 1:
         raise SystemExit("no GPU visible to librecsys_hip")
+    if args.tuned_gemms:
+        from recommender_amd.gemm_tuning import use_tuned_gemms
+
+        use_tuned_gemms()
     D, S = args.dim, args.slots
     cards = criteo_cardinalities(args.rows, S)
     g = torch.Generator(device=dev)

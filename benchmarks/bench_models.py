@@ -45,8 +45,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--rows", type=int, default=40_000_000)
+    ap.add_argument("--tuned-gemms", type=int, default=-1,
+                    help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
+                         "-1 (default): on for the fixed-shape models (dien, esmm, mmoe), off for the "
+                         "variable-shape ones (pinsage, eges: 4.6 -> 10.8 ms, 1.16 -> 1.44 ms with it)")
     args = ap.parse_args()
     L.load()
+    if args.tuned_gemms == 1 or (args.tuned_gemms < 0 and args.model in ("dien", "esmm", "mmoe")):
+        from recommender_amd.gemm_tuning import use_tuned_gemms
+
+        use_tuned_gemms()
     dev = "cuda"
     rng = np.random.default_rng(4)
     if args.model == "dien":

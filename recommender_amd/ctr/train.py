@@ -207,6 +207,9 @@ def train(argv=None):
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--steps_per_epoch", type=int, default=50)
     args = ap.parse_args(argv)
+    from ..gemm_tuning import use_tuned_gemms
+
+    use_tuned_gemms()  # committed TunableOp GEMM choices for the fixed dense shapes
     torch.manual_seed(args.seed)
     dev = torch.device("cuda")
     num_int_fea, num_cat_fea = 13, 26

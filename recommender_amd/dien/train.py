@@ -81,6 +81,9 @@ def main(argv=None):
     ap.add_argument("--cat_vocab", type=int, default=801)
     ap.add_argument("--steps_per_epoch", type=int, default=50)
     args = ap.parse_args(argv)
+    from ..gemm_tuning import use_tuned_gemms
+
+    use_tuned_gemms()  # committed TunableOp GEMM choices for the fixed dense shapes
     torch.manual_seed(args.seed)
     kw = dict(item_vocab_size=args.item_vocab, item_embedding_size=18, cat_vocab_size=args.cat_vocab,
               cat_embedding_size=18, mlp_units=[200, 80, 1], device="cuda")

@@ -80,6 +80,9 @@ def train(argv=None):
     ap.add_argument("--steps_per_epoch", type=int, default=50)
     ap.add_argument("--optimizer", default="keras_adam", choices=["keras_adam", "lazy_adam", "sgd"])
     args = ap.parse_args(argv)
+    from ..gemm_tuning import use_tuned_gemms
+
+    use_tuned_gemms()  # committed TunableOp GEMM choices for the fixed dense shapes
     torch.manual_seed(args.seed)
     vocab = scaled_vocab(FEAT_VOCAB, args.rows) if args.rows else dict(FEAT_VOCAB)
     model = build(args.model_type, vocab)
