@@ -134,6 +134,31 @@ int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float* v, int64_
                            int64_t n_ids, const float* grad_out, const rs_adam_params* params,
                            uint32_t* touched_bitmap, void* workspace, size_t ws_bytes,
                            void* stream);
+/* One-call forms (SURVEY §8(b) minimum exports): sort + dedup / sort + apply with one workspace of
+ * rs_sparse_workspace_size(n_ids, dim) bytes; bit-identical to the two-call forms. ids[n_ids]
+ * (id_dtype RS_ID_I32 / RS_ID_I64; slot = position % n_slots when slot_offsets is given);
+ * grad_out[n_ids, dim] in position order. rs_embedding_bwd_dedup writes *n_unique (device). */
+size_t rs_sparse_workspace_size(int64_t n_ids, int32_t dim);
+int32_t rs_embedding_bwd_dedup(const void* ids, int32_t id_dtype, int64_t n_ids,
+                               const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                               const float* grad_out, int32_t dim, uint32_t* uniq_rows,
+                               float* uniq_grad, int32_t* n_unique, int32_t* err_flag,
+                               void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_apply_sgd(float* table, int64_t n_rows, int32_t dim, const void* ids, int32_t id_dtype,
+                     int64_t n_ids, const int64_t* slot_offsets, int32_t n_slots,
+                     const float* grad_out, float lr, int32_t* err_flag, void* workspace,
+                     size_t ws_bytes, void* stream);
+int32_t rs_apply_lazy_adam(float* table, float* m, float* v, int64_t n_rows, int32_t dim,
+                           const void* ids, int32_t id_dtype, int64_t n_ids,
+                           const int64_t* slot_offsets, int32_t n_slots, const float* grad_out,
+                           const rs_adam_params* params, int32_t* err_flag, void* workspace,
+                           size_t ws_bytes, void* stream);
+int32_t rs_apply_keras_dense_adam(float* table, float* m, float* v, int64_t n_rows, int32_t dim,
+                                  const void* ids, int32_t id_dtype, int64_t n_ids,
+                                  const int64_t* slot_offsets, int32_t n_slots,
+                                  const float* grad_out, const rs_adam_params* params,
+                                  uint32_t* touched_bitmap, int32_t* err_flag, void* workspace,
+                                  size_t ws_bytes, void* stream);
 /* dense sweep for RS_OPT_KERAS_ADAM: rows NOT marked in touched_bitmap get
  * m=b1*m, v=b2*v, var -= lr*m/(sqrt(v)+eps); the bitmap is cleared afterwards. */
 int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_rows, int32_t dim,

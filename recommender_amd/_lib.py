@@ -114,6 +114,15 @@ _SIGS = {
     "rs_chain_reduce": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _sz, _p]),
     "rs_chain3_vec_grads": (_i32, [_p, _p, _p, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _p,
                                    _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_sparse_workspace_size": (_sz, [_i64, _i32]),
+    "rs_embedding_bwd_dedup": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _i32, _p, _p, _p, _p, _p,
+                                      _sz, _p]),
+    "rs_apply_sgd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, C.c_float, _p, _p, _sz,
+                            _p]),
+    "rs_apply_lazy_adam": (_i32, [_p, _p, _p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p,
+                                  C.POINTER(AdamParams), _p, _p, _sz, _p]),
+    "rs_apply_keras_dense_adam": (_i32, [_p, _p, _p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p,
+                                         C.POINTER(AdamParams), _p, _p, _p, _sz, _p]),
     "rs_vocab_count_masked": (_i32, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
     "rs_kv_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p, _p,
                            _p, _p]),

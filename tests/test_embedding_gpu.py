@@ -187,3 +187,66 @@ def test_golden_fixture_on_gpu():
         t.accumulate_grad(torch.from_numpy(ids).to(DEV), torch.from_numpy(grad).to(DEV))
         opt.step()
         np.testing.assert_array_equal(t.weight.cpu().numpy(), f[key], err_msg=kind)
+
+
+@pytest.mark.parametrize("kind", ["dedup", "sgd", "lazy_adam", "keras_adam"])
+def test_one_call_sparse_entry_points_match_two_call(kind, rng):
+    """rs_embedding_bwd_dedup / rs_apply_sgd / rs_apply_lazy_adam / rs_apply_keras_dense_adam
+    (SURVEY §8(b) names) are bit-identical to rs_sort_ids + dedup / apply (+ dense sweep)."""
+    card = [50, 3, 4000, 700]
+    so_np = np.concatenate([[0], np.cumsum(card)]).astype(np.int64)
+    V, D, B = int(so_np[-1]), 48, 3000
+    ids = np.stack([rng.integers(0, c, B) for c in card], 1).astype(np.int64)
+    g = rng.standard_normal((B * 4, D)).astype(np.float32)
+    so = torch.from_numpy(so_np).to(DEV)
+    idt, gt = torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV)
+    st = L.stream_ptr(torch.device(DEV))
+    n = ids.size
+    ws = torch.empty(L.lib().rs_sparse_workspace_size(n, D), dtype=torch.uint8, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    prm = L.AdamParams(1e-2, 0.9, 0.999, 0.1, 0.001, 1e-7)
+    if kind == "dedup":
+        ur = torch.empty(n, dtype=torch.int32, device=DEV)
+        ug = torch.empty(n, D, device=DEV)
+        nu = torch.zeros(1, dtype=torch.int32, device=DEV)
+        L.call("rs_embedding_bwd_dedup", L.ptr(idt), 1, n, L.ptr(so), 4, V, L.ptr(gt), D, L.ptr(ur),
+               L.ptr(ug), L.ptr(nu), L.ptr(err), L.ptr(ws), ws.numel(), st)
+        u = int(nu.item())
+        s = SortedIds(idt, V, so)
+        w2 = torch.empty(L.lib().rs_dedup_workspace_size(n, D), dtype=torch.uint8, device=DEV)
+        ur2 = torch.empty(n, dtype=torch.int32, device=DEV)
+        ug2 = torch.empty(n, D, device=DEV)
+        L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(gt), D, V,
+               L.ptr(ur2), L.ptr(ug2), L.ptr(w2), w2.numel(), st)
+        assert u == int(s.n_unique.item())
+        assert torch.equal(ur[:u], ur2[:u]) and torch.equal(ug[:u], ug2[:u])
+        return
+    tabs = [torch.from_numpy(rng.standard_normal((V, D)).astype(np.float32)).to(DEV)]
+    tabs.append(tabs[0].clone())
+    ms = [torch.full((V, D), 0.01, device=DEV) for _ in range(2)]
+    vs = [torch.full((V, D), 0.02, device=DEV) for _ in range(2)]
+    bms = [torch.zeros((V + 31) // 32, dtype=torch.int32, device=DEV) for _ in range(2)]
+    if kind == "sgd":
+        L.call("rs_apply_sgd", L.ptr(tabs[0]), V, D, L.ptr(idt), 1, n, L.ptr(so), 4, L.ptr(gt),
+               0.01, L.ptr(err), L.ptr(ws), ws.numel(), st)
+        opt, m, v, bm = L.RS_OPT_SGD, None, None, None
+        prm = L.AdamParams(0.01, 0, 0, 0, 0, 0)
+    elif kind == "lazy_adam":
+        L.call("rs_apply_lazy_adam", L.ptr(tabs[0]), L.ptr(ms[0]), L.ptr(vs[0]), V, D, L.ptr(idt),
+               1, n, L.ptr(so), 4, L.ptr(gt), prm, L.ptr(err), L.ptr(ws), ws.numel(), st)
+        opt, m, v, bm = L.RS_OPT_LAZY_ADAM, ms[1], vs[1], None
+    else:
+        L.call("rs_apply_keras_dense_adam", L.ptr(tabs[0]), L.ptr(ms[0]), L.ptr(vs[0]), V, D,
+               L.ptr(idt), 1, n, L.ptr(so), 4, L.ptr(gt), prm, L.ptr(bms[0]), L.ptr(err), L.ptr(ws),
+               ws.numel(), st)
+        opt, m, v, bm = L.RS_OPT_KERAS_ADAM, ms[1], vs[1], bms[1]
+    s = SortedIds(idt, V, so)
+    w2 = torch.empty(L.lib().rs_apply_workspace_size(n, D), dtype=torch.uint8, device=DEV)
+    L.call("rs_embedding_apply", opt, L.ptr(tabs[1]), L.ptr(m), L.ptr(v), V, D, L.ptr(s.rows),
+           L.ptr(s.pos), n, L.ptr(gt), prm, L.ptr(bm), L.ptr(w2), w2.numel(), st)
+    if kind == "keras_adam":
+        L.call("rs_keras_adam_dense_sweep", L.ptr(tabs[1]), L.ptr(m), L.ptr(v), V, D, prm,
+               L.ptr(bm), st)
+    assert torch.equal(tabs[0], tabs[1])
+    if m is not None:
+        assert torch.equal(ms[0], ms[1]) and torch.equal(vs[0], vs[1])
