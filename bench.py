@@ -65,8 +65,12 @@ def parse():
                          "(overlaps the next bottom MLP) instead of at the end of the step")
     ap.add_argument("--mlp-bwd", default="factored", choices=["factored", "layerwise"],
                     help="ctr MLP backward: factored linear chain (default) or layer by layer")
+    ap.add_argument("--mlp-fwd", default="composed", choices=["composed", "layerwise"],
+                    help="ctr MLP forward on the chain path: the chain's single affine map "
+                         "(default) or layer by layer")
     ap.add_argument("--compare-layerwise", type=int, default=1,
-                    help="1: after the timed steps, also time the layer-by-layer MLP backward")
+                    help="1: after the timed steps, also time the layer-by-layer MLP forward "
+                         "(factored backward) and the fully layer-by-layer MLP")
     ap.add_argument("--tuned-gemms", type=int, default=1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py)")
     ap.add_argument("--pmc", type=int, default=1,
@@ -98,7 +102,7 @@ def measure_traffic(args):
              str(args.rows), "--dim", str(args.dim), "--slots", str(args.slots), "--optimizer",
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
              str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd,
-             "--compare-layerwise", "0", "--tuned-gemms", str(args.tuned_gemms)]
+             "--mlp-fwd", args.mlp_fwd, "--compare-layerwise", "0", "--tuned-gemms", str(args.tuned_gemms)]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -229,6 +233,7 @@ def cpu_baseline(args, cards):
 def main():
     args = parse()
     MLP.factored_backward = args.mlp_bwd == "factored"
+    MLP.composed_forward = args.mlp_fwd == "composed"
     traffic, traffic_detail = None, None
     if args.pmc and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         traffic, traffic_detail = measure_traffic(args)  # before any GPU initialisation
@@ -313,11 +318,11 @@ def main():
     ms_step = wall / args.steps * 1e3
     value = args.batch * world * args.steps / wall
 
-    # the same steps with the layer-by-layer MLP backward (reference evaluation order), for the
-    # record: same model, same batches, timed the same way
-    layerwise_ms = None
-    if args.compare_layerwise and args.mlp_bwd == "factored" and not args.graph:
-        MLP.factored_backward = False
+    # the same steps with the layer-by-layer MLP forward, and with the MLPs entirely layer by
+    # layer (the reference's evaluation order), for the record: same model, same batches, timed
+    # the same way
+    def time_variant(factored, composed):
+        MLP.factored_backward, MLP.composed_forward = factored, composed
         for i in range(2):
             step(pool[i % len(pool)])
         torch.cuda.synchronize()
@@ -332,8 +337,14 @@ def main():
             tt = torch.tensor([lw], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             lw = float(tt.item())
-        layerwise_ms = round(lw / args.steps * 1e3, 3)
-        MLP.factored_backward = True
+        return round(lw / args.steps * 1e3, 3)
+
+    layerwise_ms = layerwise_fwd_ms = None
+    if args.compare_layerwise and args.mlp_bwd == "factored" and not args.graph:
+        if args.mlp_fwd == "composed":
+            layerwise_fwd_ms = time_variant(True, False)
+        layerwise_ms = time_variant(False, False)
+        MLP.factored_backward, MLP.composed_forward = True, args.mlp_fwd == "composed"
 
     tot = timer.totals_ms()
     kern = {}
@@ -383,12 +394,15 @@ def main():
                        "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
                        "optimizer": args.optimizer,
                        "parallelism": f"row-sharded slab x{world} (RCCL all-to-all) + dp{world} MLPs" if world > 1 else "single"},
-            "mlp_backward": {"mode": args.mlp_bwd,
-                             "note": "ctr MLP hidden layers are linear (ctr/layers.py:8); the factored "
-                                     "backward takes every layer's gradient from the last layer's "
-                                     "(same gradients in exact arithmetic, fp32 summation order differs; "
-                                     "tests/test_mlp_chain_gpu.py); forward is layer by layer",
-                             "ms_per_step_layerwise_bwd": layerwise_ms},
+            "mlp": {"backward": args.mlp_bwd, "forward": args.mlp_fwd,
+                    "note": "ctr MLP hidden layers are linear (ctr/layers.py:8), so each MLP is one "
+                            "affine map: the composed forward evaluates x·K1·K2·K3 + c as x·(K1K2K3) + c "
+                            "and the factored backward takes every layer's gradient from the last "
+                            "layer's. Every layer's parameters are kept and updated; same values in "
+                            "exact arithmetic, fp32 rounding order differs (tests/test_mlp_chain_gpu.py "
+                            "bounds both against a float64 oracle)",
+                    "ms_per_step_layerwise_fwd": layerwise_fwd_ms,
+                    "ms_per_step_layerwise_fwd_bwd": layerwise_ms},
             "roofline": roof, "embedding_path": emb_path, "kernels": kern,
             "cpu_baseline": cpu, "loss": float(loss.item()),
         }

@@ -365,33 +365,43 @@ __device__ __forceinline__ void rowdot_wave(const float* M, int ld, int i_row, i
   if (lane == 0) *out_i = acc;
 }
 
-// out[c] = Σ_k M[row(k), c] · v[k] (+ add[c]) for a 64-column tile: 4 waves stride k, folded
-// in wave order
+// The weight-sized matrix-vector products of the chain: blocks of kC3Waves waves, so the
+// column sums (k up to a few hundred deep) run 16-wide in k with four loads in flight per wave
+// (they are latency-bound, not bandwidth-bound: 4 waves striding k one load at a time took
+// 60 us for K1ᵀ·A at 480 x 512).
+constexpr int kC3Waves = 16;
+
+// out[c] = Σ_k M[row(k), c] · v[k] (+ add[c]) for a 64-column tile: kC3Waves waves stride k,
+// folded in wave order
 __device__ __forceinline__ void coldot_tile(const float* M, int ld, const int32_t* rowmap, int n,
                                             int ncol, int c0, const float* v, const float* add,
                                             float* out) {
-  __shared__ float red[4][64];
+  __shared__ float red[kC3Waves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = c0 + lane;
   float acc = 0.f;
-  if (c < ncol)
-    for (int k = w; k < n; k += 4) acc += M[(int64_t)(rowmap ? rowmap[k] : k) * ld + c] * v[k];
+  if (c < ncol) {
+#pragma unroll 4
+    for (int k = w; k < n; k += kC3Waves) acc += M[(int64_t)(rowmap ? rowmap[k] : k) * ld + c] * v[k];
+  }
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0 && c < ncol) {
-    float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    float t = red[0][lane];
+#pragma unroll
+    for (int j = 1; j < kC3Waves; ++j) t += red[j][lane];
     out[c] = add ? t + add[c] : t;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void chain3_stage1(Chain3Args a) {
+__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage1(Chain3Args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nq = (a.n1 + 3) / 4;   // q1 blocks (4 waves each)
-  const int nt = (a.n1 + 63) / 64;  // T2 column tiles
+  const int nq = (a.n1 + kC3Waves - 1) / kC3Waves;  // q1 blocks (one wave per output)
+  const int nt = (a.n1 + 63) / 64;                   // T2 column tiles
   int blk = blockIdx.x;
   if (blk < nq) {
-    const int i = blk * 4 + w;
+    const int i = blk * kC3Waves + w;
     if (i < a.n1) rowdot_wave(a.K2, a.n2, i, a.n2, a.K3, a.q1 + i, lane);
     return;
   }
@@ -410,11 +420,11 @@ __global__ __launch_bounds__(256) void chain3_stage1(Chain3Args a) {
   }
 }
 
-__global__ __launch_bounds__(256) void chain3_stage2(Chain3Args a) {
+__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage2(Chain3Args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int npb = (a.n0 + 3) / 4;
+  const int npb = (a.n0 + kC3Waves - 1) / kC3Waves;
   if ((int)blockIdx.x < npb) {
-    const int i = blockIdx.x * 4 + w;
+    const int i = blockIdx.x * kC3Waves + w;
     if (i < a.n0) rowdot_wave(a.K1, a.n1, a.r ? a.r[i] : i, a.n1, a.q1, a.p + i, lane);
     return;
   }
@@ -623,11 +633,11 @@ extern "C" int32_t rs_chain3_vec_grads(const float* K1, const int32_t* rows, con
   float* w = static_cast<float*>(workspace);
   Chain3Args a{K1, rows, inv, b1, K2, b2, K3, A, s, n_full0, n0, n1, n2,
                w, w + n1, w + 2 * n1, w + 2 * n1 + n2, dK1, db1, dK2, db2, dK3, db3, p};
-  const unsigned g1 = (unsigned)(ceil_div(n1, 4) + ceil_div(n1, 64) + ceil_div(n2, 64));
-  chain3_stage1<<<g1, 256, 0, st>>>(a);
+  const unsigned g1 = (unsigned)(ceil_div(n1, kC3Waves) + ceil_div(n1, 64) + ceil_div(n2, 64));
+  chain3_stage1<<<g1, kC3Waves * 64, 0, st>>>(a);
   RS_CHECK_LAUNCH();
-  const unsigned g2 = (unsigned)(ceil_div(n0, 4) + ceil_div(n2, 64));
-  chain3_stage2<<<g2, 256, 0, st>>>(a);
+  const unsigned g2 = (unsigned)(ceil_div(n0, kC3Waves) + ceil_div(n2, 64));
+  chain3_stage2<<<g2, kC3Waves * 64, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   const int64_t tot = (int64_t)n_full0 * n1 + (int64_t)n1 * n2 + n2 + n1 + 1;
   chain3_stage3<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(a);

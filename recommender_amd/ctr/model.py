@@ -119,7 +119,8 @@ class DLRM(nn.Module):
                 table, ids = self.embedding_layer, cat_features
                 if self._exchanged is not None:
                     (table, ids), self._exchanged = self._exchanged, None
-                out = dlrm_top(table, ids, bmlp_activation, layers, self.compact_rows).squeeze(1)
+                out = dlrm_top(table, ids, bmlp_activation, layers, self.compact_rows,
+                               composed=self.top_mlp.composed_forward).squeeze(1)
             else:
                 tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
                 out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)

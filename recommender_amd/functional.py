@@ -156,19 +156,19 @@ def dlrm_interaction(table_module, ids, dense, compact: bool = False):
 class _DLRMTopFn(torch.autograd.Function):
     """DLRM's fused lookup + interaction (compact row) feeding the top MLP as one linear chain
     (ctr/model.py:49-57 with the ctr MLP's linear hidden layers, ctr/layers.py:8). Forward:
-    rs_dlrm_interaction_fwd, then the top MLP layer by layer (bit-identical to the unfused
-    path). Backward: rs_chain_reduce over the interaction row gives G = σ'(y)·dy [B], A = Zᵀ·G
+    rs_dlrm_interaction_fwd, then the top MLP as one chain (layer by layer, bit-identical to the
+    unfused path, or composed into its single affine map, nn.chain_forward). Backward: rs_chain_reduce over the interaction row gives G = σ'(y)·dy [B], A = Zᵀ·G
     and Σ G in one pass; every top-MLP gradient follows from them (nn.chain_param_grads); the
     upstream gradient of the interaction is then the rank-one G ⊗ Q_0 (Q_0 = K_1·K_2·K_3), which
     rs_dlrm_interaction_bwd_rank1 consumes without materialising the [B, width] rows."""
 
     @staticmethod
-    def forward(ctx, handle, dense, table_module, ids, layers, rows):
+    def forward(ctx, handle, dense, table_module, ids, layers, rows, composed=False):
         from .nn import chain_forward
 
         dense = dense.contiguous()
         z = _DLRMInteraction.forward(ctx, handle, dense, table_module, ids, True)
-        y, ks = chain_forward(z, layers, rows)
+        y, ks = chain_forward(z, layers, rows, composed)
         ctx.layers, ctx.rows = layers, rows
         ctx.save_for_backward(dense, z, y, *ks)
         return y
@@ -202,12 +202,13 @@ class _DLRMTopFn(torch.autograd.Function):
             tm.fused_optimizer.apply_async(tm, ids, grad_emb, tm.take_presorted(ids))
         else:
             tm.accumulate_grad(ids, grad_emb)
-        return None, grad_dense, None, None, None, None
+        return None, grad_dense, None, None, None, None, None
 
 
-def dlrm_top(table_module, ids, dense, layers, rows):
+def dlrm_top(table_module, ids, dense, layers, rows, composed=False):
     """sigmoid-head top MLP over the compact DLRM interaction row, fused (see _DLRMTopFn)."""
-    return _DLRMTopFn.apply(table_module.grad_handle, dense, table_module, ids, list(layers), rows)
+    return _DLRMTopFn.apply(table_module.grad_handle, dense, table_module, ids, list(layers), rows,
+                            composed)
 
 
 class _FM(torch.autograd.Function):

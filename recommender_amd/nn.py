@@ -221,7 +221,8 @@ class _LinearChainFn(torch.autograd.Function):
     """A chain of Dense layers whose hidden layers are linear (ctr/layers.py:8: the reference's
     ctr MLP puts no activation on hidden layers): h_l = h_{l-1}·K_l + b_l, y = act(h_{L-1}·K_L
     + b_L). The forward is evaluated layer by layer exactly as the layerwise path (bit-identical
-    outputs). The backward uses the chain's linearity twice:
+    outputs) or, composed=True, as the one affine map the chain is (chain_forward). The
+    backward uses the chain's linearity twice:
       * every upstream gradient is the last layer's, G = act'(y)⊙dy, through a fixed matrix:
         g_l = G·Q_lᵀ with Q_l = K_{l+1}···K_L ([n_l, n_L]), so dK_l = (h_{l-1}ᵀ·G)·Q_lᵀ,
         db_l = s·Q_lᵀ (s = Σ_b G) and dx = G·Q_0ᵀ;
@@ -235,8 +236,8 @@ class _LinearChainFn(torch.autograd.Function):
     layerwise oracle."""
 
     @staticmethod
-    def forward(ctx, x, handle, layers, rows):
-        h, ks = chain_forward(x, layers, rows)
+    def forward(ctx, x, handle, layers, rows, composed=False):
+        h, ks = chain_forward(x, layers, rows, composed)
         ctx.layers, ctx.rows = layers, rows
         ctx.save_for_backward(h if layers[-1].act_code else None, x, *ks)
         return h
@@ -247,9 +248,9 @@ class _LinearChainFn(torch.autograd.Function):
         y, x, *ks = ctx.saved_tensors
         need_dx = ctx.needs_input_grad[0]
         G, A, s = chain_reduce(x, dy.contiguous(), y, layers[-1].act_code, need_g=need_dx)
-        Q = chain_param_grads(layers, rows, ks, A, s)
+        Q = chain_param_grads(layers, rows, ks, A, s, need_q0=need_dx)
         dx = G @ Q.t() if need_dx else None
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 def chain_reduce(x, dy, y, act, need_g=True):
@@ -308,17 +309,21 @@ class overlapped_param_grads:
         return False
 
 
-def chain_param_grads(layers, rows, ks, A, s):
+def chain_param_grads(layers, rows, ks, A, s, need_q0=True):
     """Accumulate every layer's kernel / bias gradient of a linear chain from A = xᵀ·G and
-    s = Σ_b G (see _LinearChainFn); returns Q_0 = K_1···K_L for the input gradient G·Q_0ᵀ.
+    s = Σ_b G (see _LinearChainFn); returns Q_0 = K_1···K_L for the input gradient G·Q_0ᵀ
+    (None unless need_q0, narrow-input chains only).
     Qa[i] = K_{i+1}···K_L is formed on the current stream (the input gradient needs it); the
     rest, with h_{i}ᵀ·G = T_{i+1} + c_i⊗s where T_1 = A, T_{i+1} = K_iᵀ·T_i and
     c_i = K_iᵀ·c_{i-1} + b_i, runs on the overlapped parameter-gradient stream when one is
-    active (matrix-vector chains when the output width is 1)."""
+    active (matrix-vector chains when the output width is 1). A chain whose input is narrower
+    than its output (the DLRM bottom MLP, 13 features) goes through _narrow_chain_grads."""
     n = len(layers)
     if (n == 3 and A.is_cuda and A.shape[1] == 1 and ks[2].shape[1] == 1
             and all(l.bias is not None for l in layers)):
         return _chain3_vec_grads(layers, rows, ks, A, s)
+    if n > 1 and A.shape[0] < A.shape[1] and _pgrad_stream is None:
+        return _narrow_chain_grads(layers, rows, ks, A, s, need_q0)
     Qa = [None] * n  # Qa[i] = K_{i+1}···K_L (None: identity)
     for i in range(n - 2, -1, -1):
         Qa[i] = ks[i + 1] if Qa[i + 1] is None else ks[i + 1] @ Qa[i + 1]
@@ -349,6 +354,41 @@ def chain_param_grads(layers, rows, ks, A, s):
                 else:
                     c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
     return Q0
+
+
+def _narrow_chain_grads(layers, rows, ks, A, s, need_q0):
+    """chain_param_grads for a chain whose input width n_0 is below its output width n_L: every
+    batch-deep product is carried on the n_0 side. With R_i = K_1···K_i ([n_0, n_i]),
+    h_iᵀ·G = R_iᵀ·A + c_i⊗s ([n_i, n_L]) and dK_{i+1} = (h_iᵀ·G)·K_Lᵀ···K_{i+2}ᵀ evaluated left
+    to right, so no [n_i, n_L]-by-[n_L, n_{i+1}] chain product (K_{i+1}ᵀ·T_i, K_{i+1}···K_L) is
+    ever formed: for the DLRM bottom MLP 13→512→256→128 that is ≈19 M multiply-adds instead of
+    ≈51 M. Same gradients in exact arithmetic as the T-chain (tests/test_mlp_chain_cpu.py)."""
+    n = len(layers)
+    R = c = None
+    for i in range(n):
+        layer = layers[i]
+        M = A if R is None else torch.addr(R.t() @ A, c, s)
+        dk, db = M, s
+        for j in range(n - 1, i, -1):
+            dk = dk @ ks[j].t()
+            db = ks[j] @ db
+        if i == 0 and rows is not None:
+            full = torch.zeros_like(layer.kernel)
+            full.index_copy_(0, rows, dk)
+            dk = full
+        _accum_grad(layer.kernel, dk)
+        if layer.bias is not None:
+            _accum_grad(layer.bias, db)
+        if i < n - 1:
+            R = ks[0] if R is None else R @ ks[i]
+            b = layer.bias
+            if c is None:
+                c = b if b is not None else torch.zeros(ks[i].shape[1], device=A.device, dtype=A.dtype)
+            else:
+                c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
+    if not need_q0:
+        return None
+    return R @ ks[n - 1]
 
 
 _inv_cache: dict = {}
@@ -393,27 +433,62 @@ def _chain3_vec_grads(layers, rows, ks, A, s):
     return p
 
 
-def chain_forward(x, layers, rows=None):
-    """Layer-by-layer forward of a linear chain: (y, the kernels as used)."""
-    h = x
-    last = len(layers) - 1
-    ks = []
-    for i, layer in enumerate(layers):
-        k = layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
-        ks.append(k)
-        h = torch.addmm(layer.bias, h, k) if layer.bias is not None else h @ k
-        if i == last:
-            if layer.act_code == 1:
-                h = torch.relu_(h)
-            elif layer.act_code == 2:
-                h = torch.sigmoid_(h)
+def chain_compose(layers, ks):
+    """(Q_0, c_L) of a linear chain: its pre-activation output is x·Q_0 + c_L with
+    Q_0 = K_1···K_L and c_L the biases carried through the later kernels. The products run in
+    whichever order is cheaper (left to right for a narrow input, e.g. the DLRM bottom MLP's 13
+    features; right to left for a narrow output, e.g. the top MLP's single logit); every product
+    is weight-sized."""
+    n = len(layers)
+    n0, nl = ks[0].shape[0], ks[-1].shape[1]
+    dev = ks[0].device
+    if n0 <= nl:
+        Q = ks[0]
+        c = (layers[0].bias if layers[0].bias is not None
+             else torch.zeros(ks[0].shape[1], device=dev, dtype=ks[0].dtype))
+        for i in range(1, n):
+            Q = Q @ ks[i]
+            b = layers[i].bias
+            c = torch.addmv(b, ks[i].t(), c) if b is not None else ks[i].t() @ c
+        return Q, c
+    Q = ks[-1]
+    b = layers[-1].bias
+    c = b.clone() if b is not None else torch.zeros(nl, device=dev, dtype=ks[0].dtype)
+    for i in range(n - 2, -1, -1):  # Q = K_{i+1}···K_L here
+        b = layers[i].bias
+        if b is not None:
+            c = torch.addmv(c, Q.t(), b)
+        Q = ks[i] @ Q
+    return Q, c
+
+
+def chain_forward(x, layers, rows=None, composed=False):
+    """Forward of a linear chain: (y, the kernels as used). Layer by layer (composed=False,
+    bit-identical to the layerwise path) or, composed=True, as the single affine map the chain
+    is, y = act(x·Q_0 + c_L) (chain_compose): one batch-deep GEMM of width n_L instead of one
+    per layer. Both are the same function in exact arithmetic; they differ only in fp32
+    rounding order (tests/test_mlp_chain_gpu.py bounds both against a float64 oracle)."""
+    ks = [layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
+          for i, layer in enumerate(layers)]
+    if composed:
+        Q, c = chain_compose(layers, ks)
+        h = torch.addmm(c, x, Q)
+    else:
+        h = x
+        for layer, k in zip(layers, ks):
+            h = torch.addmm(layer.bias, h, k) if layer.bias is not None else h @ k
+    act = layers[-1].act_code
+    if act == 1:
+        h = torch.relu_(h)
+    elif act == 2:
+        h = torch.sigmoid_(h)
     return h, ks
 
 
-def linear_chain(x, layers, rows=None, handle=None):
-    """y of a Dense chain with linear hidden layers (see _LinearChainFn)."""
+def linear_chain(x, layers, rows=None, handle=None, composed=False):
+    """y of a Dense chain with linear hidden layers (see _LinearChainFn; composed: chain_forward)."""
     return _LinearChainFn.apply(x, handle if handle is not None else layers[-1]._handle(),
-                                layers, rows)
+                                layers, rows, composed)
 
 
 class Dense(nn.Module):

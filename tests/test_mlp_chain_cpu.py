@@ -15,7 +15,9 @@ class _Layer:
 
 
 @pytest.mark.parametrize("dims,bias", [([7, 9, 5, 3], True), ([6, 8, 4, 1], True), ([5, 2], True),
-                                       ([4, 6, 3], False), ([13, 32, 16, 8], True)])
+                                       ([4, 6, 3], False), ([13, 32, 16, 8], True),
+                                       # narrow input (n_0 < n_L): _narrow_chain_grads
+                                       ([13, 64, 32, 16], True), ([2, 6, 4, 5], False), ([3, 7], True)])
 def test_chain_param_grads_match_autograd(dims, bias):
     g = torch.Generator().manual_seed(len(dims) * 10 + dims[0])
     B = 64
@@ -57,3 +59,28 @@ def test_chain_param_grads_compact_rows():
     ref[rows] = x.t() @ (G @ k2.t())
     torch.testing.assert_close(layers[0].kernel.grad, ref, rtol=1e-10, atol=1e-10)
     assert (layers[0].kernel.grad[[1, 3, 4, 7]] == 0).all()
+
+
+@pytest.mark.parametrize("dims,bias,act", [([7, 9, 5, 3], True, 0), ([480, 64, 32, 1], True, 2),
+                                           ([13, 64, 32, 16], True, 1), ([4, 6, 3], False, 0),
+                                           ([5, 2], True, 2)])
+def test_composed_forward_matches_layerwise(dims, bias, act):
+    """chain_forward(composed=True), y = act(x·K_1···K_L + c_L), in either product order
+    (narrow input: left to right; narrow output: right to left), equals the layer-by-layer
+    forward in float64, with first-layer rows selected as DLRM's compact row does."""
+    g = torch.Generator().manual_seed(dims[0] * 7 + len(dims))
+    B = 32
+    ks = [torch.randn(dims[i], dims[i + 1], dtype=torch.float64, generator=g) / dims[i] ** 0.5
+          for i in range(len(dims) - 1)]
+    bs = [torch.randn(dims[i + 1], dtype=torch.float64, generator=g) if bias else None
+          for i in range(len(dims) - 1)]
+    layers = [_Layer(k, b) for k, b in zip(ks, bs)]
+    layers[-1].act_code = act
+    for rows in (None, torch.arange(0, dims[0], 2)):
+        width = dims[0] if rows is None else rows.numel()
+        x = torch.randn(B, width, dtype=torch.float64, generator=g)
+        with torch.no_grad():
+            yc, ksc = N.chain_forward(x, layers, rows, composed=True)
+            yl, ksl = N.chain_forward(x, layers, rows, composed=False)
+        torch.testing.assert_close(yc, yl, rtol=1e-12, atol=1e-12)
+        assert all(torch.equal(a, b) for a, b in zip(ksc, ksl))

@@ -1,6 +1,6 @@
 """The ctr MLP's factored backward (nn._LinearChainFn; the reference's hidden Dense layers are
 linear, ctr/layers.py:8) against the layer-by-layer float64 oracle (oracle/ctr.py mlp_backward):
-forward bit-identical to the layerwise path; kernel / bias / input gradients within 1e-5 of the
+forward bit-identical to the layerwise path (or, composed, within 1e-5 of the oracle); kernel / bias / input gradients within 1e-5 of the
 oracle relative to the magnitude bound of the factored products, (|R|ᵀ|x|ᵀ|G| + |c|⊗Σ|G|)·|Q|ᵀ,
 which bounds both evaluation orders."""
 import numpy as np
@@ -41,9 +41,11 @@ def _make(units, act, fin, seed):
     ([32, 1], None, 40, 700, None),            # DeepFM head (linear final)
     ([8], "relu", 5, 333, None),               # single layer
 ])
-def test_factored_backward_matches_oracle(units, act, fin, B, rows, rng):
+@pytest.mark.parametrize("composed", [False, True])
+def test_factored_backward_matches_oracle(units, act, fin, B, rows, composed, rng):
     m_f = _make(units, act, fin, 1)
     m_l = _make(units, act, fin, 1)
+    m_f.composed_forward = composed
     m_l.factored_backward = False
     ridx = None
     width = fin
@@ -54,7 +56,8 @@ def test_factored_backward_matches_oracle(units, act, fin, B, rows, rng):
     xf = torch.from_numpy(x).to(DEV).requires_grad_(True)
     xl = torch.from_numpy(x).to(DEV).requires_grad_(True)
     yf, yl = m_f(xf, rows=ridx), m_l(xl, rows=ridx)
-    assert torch.equal(yf, yl)  # the forward is layerwise in both
+    if not composed:
+        assert torch.equal(yf, yl)  # the forward is layerwise in both
     dy = rng.standard_normal(yf.shape).astype(np.float32)
     yf.backward(torch.from_numpy(dy).to(DEV))
     yl.backward(torch.from_numpy(dy).to(DEV))
@@ -98,6 +101,10 @@ def test_factored_backward_matches_oracle(units, act, fin, B, rows, rng):
         assert_close_rel(m_f.mlp[i].bias.grad.cpu().numpy(), grads[i][1], 1e-5, bscale, f"db{i}")
         absQ = np.abs(layers[i][0]) if absQ is None else np.abs(layers[i][0]) @ absQ
     assert_close_rel(xf.grad.cpu().numpy(), dx, 1e-5, np.abs(G) @ absQ.T, "dx")
+    # the output (composed: x·K_1···K_L + c_L; layerwise: layer by layer) within 1e-5 of the
+    # oracle relative to |x|·|K_1|···|K_L| + |c_L|, which bounds both evaluation orders
+    ybound = np.abs(x.astype(np.float64)) @ absR + absc
+    assert_close_rel(yf.detach().cpu().numpy(), out, 1e-5, ybound, "y")
     # and the layerwise GPU path against the same oracle (the reference's evaluation order)
     for i in range(len(layers)):
         ref = grads[i][0]
@@ -136,12 +143,15 @@ def test_rank1_interaction_bwd_bit_identical(rng):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-def test_dlrm_fused_top_matches_layerwise(rng):
+@pytest.mark.parametrize("composed", [False, True])
+def test_dlrm_fused_top_matches_layerwise(composed, rng, monkeypatch):
     """DLRM at D = 128 (the fused interaction + top-MLP chain with the rank-one backward)
-    against the same model with the layer-by-layer MLP backward: logits bit-identical, every
-    gradient within 1e-5 relative to its magnitude."""
+    against the same model with the layer-by-layer MLP backward: logits bit-identical (layerwise
+    chain forward) or within 1e-5 (composed chain forward), every gradient within 1e-5 relative
+    to its magnitude."""
     from recommender_amd.ctr.model import DLRM
 
+    monkeypatch.setattr(MLP, "composed_forward", composed)
     S, D, B, V = 26, 128, 1024, 50000
     models = []
     for _ in range(2):
@@ -157,7 +167,10 @@ def test_dlrm_fused_top_matches_layerwise(rng):
         p2 = models[1](x)
     finally:
         MLP.factored_backward = True
-    assert torch.equal(p1, p2)
+    if composed:
+        assert_close_rel(p1.detach().cpu().numpy(), p2.detach().cpu().numpy(), 1e-5, 1.0, "p")
+    else:
+        assert torch.equal(p1, p2)
     gy = torch.from_numpy(rng.standard_normal(B).astype(np.float32)).to(DEV)
     p1.backward(gy)
     MLP.factored_backward = False
