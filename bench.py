@@ -30,7 +30,7 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1",
+WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head", "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1",
          "rs_sort_ids", "rs_embedding_apply", "rs_sort_ids_sharded", "rs_embedding_dedup_grad"]
 # the roofline kernel: the embedding-path kernel with the most algorithmic HBM traffic per step
 # (re-gather of every row + grad-row write). It runs on the main stream, so its HIP-event time
@@ -181,6 +181,8 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
     Z = F * (F - 1) // 2 + D
     if name == "rs_dlrm_interaction_fwd":
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z)
+    if name == "rs_dlrm_interaction_fwd_head":  # + the fused top-MLP output y[b]
+        return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + 4)
     if name == "rs_dlrm_interaction_bwd":
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + S * 4 * D + 4 * D)
     if name == "rs_dlrm_interaction_bwd_rank1":  # grad row = G[b] * p: 4 B per example, not 4Z

@@ -198,6 +198,16 @@ int32_t rs_dlrm_interaction_bwd(const float* table, int64_t n_rows, int32_t D, c
                                 const float* grad_out, int64_t grad_stride, float* grad_emb,
                                 float* grad_dense, void* stream);
 
+/* rs_dlrm_interaction_fwd (compact layout, D = 128, F <= 32) with the composed top MLP fused
+ * (ctr/model.py:56 `self.top_mlp(...)` with linear hidden layers): besides writing out[b], the
+ * kernel forms y[b] = act(out[b]·q + c[0]) (q [out_stride], from rs_chain3_vec_compose). */
+int32_t rs_dlrm_interaction_fwd_head(const float* table, int64_t n_rows, int32_t D,
+                                     const void* ids, int32_t id_dtype, int32_t n_slots,
+                                     const int64_t* slot_offsets, const float* dense,
+                                     int64_t batch, float* out, int64_t out_stride,
+                                     const float* q, const float* c, int32_t act, float* y,
+                                     int32_t* err_flag, void* stream);
+
 /* Rank-one upstream gradient (the factored top-MLP backward, recommender_amd/nn.py
  * _LinearChainFn): grad row b = gscale[b] * grad_row[0..width), bit-identical to
  * rs_dlrm_interaction_bwd on the materialised rows; compact layout, D = 128, F <= 32 only
@@ -415,6 +425,43 @@ int32_t rs_chain3_vec_grads(const float* K1, const int32_t* rows, const int32_t*
                             const float* A, const float* s, float* dK1, float* db1, float* dK2,
                             float* db2, float* dK3, float* db3, float* p, void* workspace,
                             size_t ws_bytes, void* stream);
+
+/* Composed forward of a ctr linear chain (hidden Dense layers linear, ctr/layers.py:8; replaces
+ * the layer-by-layer Dense calls of ctr/layers.py:11-14): the chain is the one affine map
+ * y = act(x·Q_0 + c_L).
+ * rs_chain3_vec_compose: [n1, n2, 1] chain (the DLRM / DeepFM top MLP): q [n0] = K1[rows]·K2·K3
+ *   (rows NULL: rows 0..n0) and c [1] = b3 + K3ᵀ·b2 + (K2·K3)ᵀ·b1 (biases may be NULL).
+ *   Workspace >= 4·(n1 + 1) bytes.
+ * rs_chain_aug_product: out [m+1, n] = [M; cin]·K + [0; b] with M [m, k] (row stride ldm, m < 33,
+ *   (m+1)·k <= 16896), cin [k] and b [n] optional; two calls compose a narrow-input chain [K1; b1]·K2 + [0; b2],
+ *   then ·K3 + [0; b3] = [Q_0; c_L].
+ * rs_affine_narrow_fwd: y [B, n] (row stride ldy) = act(x·Qa[0:n0] + Qa[n0]) for x [B, n0]
+ *   (n0 < 33, n <= 256, n % 4 == 0, Qa and y 16-B aligned).
+ * rs_rowdot_act: y [B] = act(x·q + c[0]) for x [B, n0] (n0 <= 1024, n0 % 4 == 0, ldx % 4 == 0,
+ *   x and q 16-B aligned). act: 0 linear, 1 relu, 2 sigmoid. */
+int32_t rs_chain3_vec_compose(const float* K1, const int32_t* rows, int32_t n0, const float* b1,
+                              const float* K2, const float* b2, const float* K3, const float* b3,
+                              int32_t n1, int32_t n2, float* q, float* c, void* workspace,
+                              size_t ws_bytes, void* stream);
+int32_t rs_chain_aug_product(const float* M, int32_t ldm, int32_t m, const float* cin,
+                             const float* K, int32_t k, int32_t n, const float* b, float* out,
+                             void* stream);
+int32_t rs_affine_narrow_fwd(const float* x, int64_t ldx, int64_t B, int32_t n0, const float* Qa,
+                             int32_t n, int32_t act, float* y, int64_t ldy, void* stream);
+int32_t rs_rowdot_act(const float* x, int64_t ldx, int64_t B, int32_t n0, const float* q,
+                      const float* c, int32_t act, float* y, void* stream);
+
+/* Parameter gradients of a narrow-input linear chain from Ã = [xᵀ·G; Σ G] ([n0+1, nL], the
+ * rs_chain_reduce output): P_L = Ã, P_{j-1} = P_j·K_jᵀ, dK_j = R̃_{j-1}ᵀ·P_j, db_j = P_j[n0]
+ * with R̃_j = [K_1···K_j; c_j] (rs_chain_aug_product's outputs; R̃_0 = [I; 0]).
+ * rs_chain_rt_product: out [m+1, n] = P [m+1, k]·Kᵀ for K [n, k] row-major (m < 33,
+ *   (m+1)·k <= 16896).
+ * rs_chain_outer: out [na, nb] = R̃ᵀ·P with R̃ = [R (m rows, row stride ldr); rlast] (rlast
+ *   NULL: zero row), P [m+1, nb] (nb % 4 == 0; P and out 16-B aligned). */
+int32_t rs_chain_rt_product(const float* P, int32_t m, const float* K, int32_t k, int32_t n,
+                            float* out, void* stream);
+int32_t rs_chain_outer(const float* R, int32_t ldr, int32_t m, const float* rlast, int32_t na,
+                       const float* P, int32_t nb, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Keras thresholded AUC (keras.metrics.AUC in ctr/train.py:86,

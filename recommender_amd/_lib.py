@@ -110,6 +110,15 @@ _SIGS = {
     "rs_log_uniform_sample": (_i32, [_p, _i32, _i64, _i32, _i32, _u64, _u32, _p, _p, _p]),
     "rs_dlrm_interaction_bwd_rank1": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p,
                                              _i64, _p, _p, _p]),
+    "rs_dlrm_interaction_fwd_head": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p,
+                                            _i64, _p, _p, _i32, _p, _p, _p]),
+    "rs_chain3_vec_compose": (_i32, [_p, _p, _i32, _p, _p, _p, _p, _p, _i32, _i32, _p, _p, _p,
+                                     _sz, _p]),
+    "rs_chain_aug_product": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p]),
+    "rs_affine_narrow_fwd": (_i32, [_p, _i64, _i64, _i32, _p, _i32, _i32, _p, _i64, _p]),
+    "rs_rowdot_act": (_i32, [_p, _i64, _i64, _i32, _p, _p, _i32, _p, _p]),
+    "rs_chain_rt_product": (_i32, [_p, _i32, _p, _i32, _i32, _p, _p]),
+    "rs_chain_outer": (_i32, [_p, _i32, _i32, _p, _i32, _p, _i32, _p, _p]),
     "rs_chain_reduce_workspace_size": (_sz, [_i64, _i32, _i32]),
     "rs_chain_reduce": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _i64, _p, _p, _p, _sz, _p]),
     "rs_chain3_vec_grads": (_i32, [_p, _p, _p, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _p,

@@ -497,6 +497,289 @@ static int32_t fold_two_level(const float* part, int nchunks, int N, float* part
   return RS_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Composed forward of the ctr linear chains (nn.chain_forward, composed=True): the chain's
+// hidden layers are linear (ctr/layers.py:8), so y = act(x·Q_0 + c_L). The weight-sized
+// composition runs in one or two launches; the batch-deep evaluation is one memory-bound pass.
+// ---------------------------------------------------------------------------------------
+struct VecComposeArgs {
+  const float* K1;   // [n_full0, n1]
+  const int32_t* r;  // [n0] rows of K1 the input holds (nullptr: rows 0..n0)
+  const float* b1;   // [n1] or nullptr
+  const float* K2;   // [n1, n2]
+  const float* b2;   // [n2] or nullptr
+  const float* K3;   // [n2] (one output)
+  const float* b3;   // [1] or nullptr
+  int n0, n1, n2;
+  float* q1;  // [n1] scratch: K2·K3
+  float* cb;  // [1] scratch: K3ᵀ·b2 + b3
+  float* q;   // [n0] out: K1[r]·q1 (= Q_0)
+  float* c;   // [1] out: c_L = b3 + K3ᵀ·b2 + q1ᵀ·b1
+};
+
+__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage1(VecComposeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * kC3Waves + (threadIdx.x >> 6);
+  if (i < a.n1) {
+    rowdot_wave(a.K2, a.n2, i, a.n2, a.K3, a.q1 + i, lane);
+  } else if (i == a.n1) {
+    float acc = 0.f;
+    if (a.b2)
+      for (int k = lane; k < a.n2; k += 64) acc += a.b2[k] * a.K3[k];
+    acc = wave_sum(acc);
+    if (lane == 0) a.cb[0] = a.b3 ? acc + a.b3[0] : acc;
+  }
+}
+
+__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage2(VecComposeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * kC3Waves + (threadIdx.x >> 6);
+  if (i < a.n0) {
+    rowdot_wave(a.K1, a.n1, a.r ? a.r[i] : i, a.n1, a.q1, a.q + i, lane);
+  } else if (i == a.n0) {
+    float acc = 0.f;
+    if (a.b1)
+      for (int k = lane; k < a.n1; k += 64) acc += a.b1[k] * a.q1[k];
+    acc = wave_sum(acc);
+    if (lane == 0) a.c[0] = acc + a.cb[0];
+  }
+}
+
+// Narrow-input product with a bias row: out[i, c] = Σ_k M̃[i, k]·K[k, c] (+ b[c] on row m),
+// M̃ = [M; cin] ([m + 1, k], m < kAugRows). Chained twice it composes [K1; b1]·K2 + [0; b2]
+// and then ·K3 + [0; b3]: rows 0..m-1 of the result are Q = K1·K2·K3, row m is c_L. M̃ is
+// staged in LDS (one coalesced pass, every load in flight at once); a block covers 64 columns,
+// its kC3Waves waves stride k eight loads of K at a time, and are folded in wave order.
+constexpr int kAugRows = 33;
+constexpr int kAugLds = 16896;  // floats of M̃ staged in LDS: (m + 1)·k <= kAugLds
+
+template <int MR>
+__global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
+    const float* __restrict__ M, int ldm, int m, const float* __restrict__ cin,
+    const float* __restrict__ K, int k, int n, const float* __restrict__ b,
+    float* __restrict__ out) {
+  __shared__ float ms[kAugLds];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) {
+    const int i = e / k, kk = e - i * k;
+    ms[e] = i < m ? M[(int64_t)i * ldm + kk] : (cin ? cin[kk] : 0.f);
+  }
+  __syncthreads();
+  const int c = blockIdx.x * 64 + lane;
+  float acc[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) acc[i] = 0.f;
+  if (c < n) {
+    constexpr int U = 8;
+    int kk = w;
+    for (; kk + (U - 1) * kC3Waves < k; kk += U * kC3Waves) {
+      float kv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) kv[u] = K[(int64_t)(kk + u * kC3Waves) * n + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float* mr = ms + kk + u * kC3Waves;
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+          if (i <= m) acc[i] += mr[i * k] * kv[u];
+      }
+    }
+    for (; kk < k; kk += kC3Waves) {
+      const float kv = K[(int64_t)kk * n + c];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        if (i <= m) acc[i] += ms[i * k + kk] * kv;
+    }
+  }
+  // fold: waves [8, 16) park their partials in the (consumed) staging buffer, waves [0, 8)
+  // add them (wave w + w), then every partial row is folded in wave order by output
+  static_assert(kC3Waves == 16 && 8 * MR * 64 <= kAugLds, "fold layout");
+  __syncthreads();
+  float* part = ms;  // [8][MR][64]
+  if (w >= 8) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i) part[((w - 8) * MR + i) * 64 + lane] = acc[i];
+  }
+  __syncthreads();
+  if (w < 8) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i) acc[i] += part[(w * MR + i) * 64 + lane];
+  }
+  __syncthreads();
+  if (w < 8) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i) part[(w * MR + i) * 64 + lane] = acc[i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < (m + 1) * 64; e += kC3Waves * 64) {
+    const int i = e >> 6, cl = e & 63, cc = blockIdx.x * 64 + cl;
+    if (cc >= n) continue;
+    float t = part[i * 64 + cl];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t += part[(j * MR + i) * 64 + cl];
+    if (i == m && b) t += b[cc];
+    out[(int64_t)i * n + cc] = t;
+  }
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float v) {
+  if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
+  if constexpr (ACT == 2) return 1.f / (1.f + expf(-v));
+  return v;
+}
+
+// y[b, :] = act(x[b, :n0]·Q + c) for a narrow input (n0 < kAugRows): Q̃ = [Q; c] and a tile of
+// kNarrowRows input rows are staged in LDS; the block's lanes each own one float4 column and
+// walk the tile's rows (16-byte stores, consecutive lanes consecutive columns).
+constexpr int kNarrowRows = 64;
+
+template <int ACT, int N0MAX>
+__global__ __launch_bounds__(256) void affine_narrow_fwd_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t B, int n0, const float* __restrict__ Qa,
+    int n, float* __restrict__ y, int64_t ldy) {
+  __shared__ float xs[kNarrowRows * N0MAX];
+  const int nq = n >> 2;  // float4 columns (<= 64)
+  const int rpb = 256 / nq;  // rows in flight per pass
+  const int t = threadIdx.x % nq, rl = threadIdx.x / nq;
+  // this lane's column of Q̃ = [Q; c] in registers (the loop below is unrolled over N0MAX)
+  float4 qr[N0MAX + 1];
+#pragma unroll
+  for (int k = 0; k <= N0MAX; ++k)
+    qr[k] = k <= n0 ? reinterpret_cast<const float4*>(Qa)[k * nq + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 cc = qr[0];
+#pragma unroll
+  for (int k = 1; k <= N0MAX; ++k)
+    if (k == n0) cc = qr[k];
+  for (int64_t r0 = (int64_t)blockIdx.x * kNarrowRows; r0 < B;
+       r0 += (int64_t)gridDim.x * kNarrowRows) {
+    const int nr = B - r0 < kNarrowRows ? (int)(B - r0) : kNarrowRows;
+    __syncthreads();  // previous tile consumed
+    for (int e = threadIdx.x; e < nr * n0; e += 256) {
+      const int rr = e / n0, k = e - rr * n0;
+      xs[rr * n0 + k] = x[(r0 + rr) * ldx + k];
+    }
+    __syncthreads();
+    if (rl >= rpb) continue;
+    for (int rr = rl; rr < nr; rr += rpb) {
+      const float* xr = xs + rr * n0;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < N0MAX; ++k) {
+        if (k < n0) {
+          const float xv = xr[k];
+          acc.x += xv * qr[k].x;
+          acc.y += xv * qr[k].y;
+          acc.z += xv * qr[k].z;
+          acc.w += xv * qr[k].w;
+        }
+      }
+      float4 o;
+      o.x = act_fwd<ACT>(acc.x + cc.x);
+      o.y = act_fwd<ACT>(acc.y + cc.y);
+      o.z = act_fwd<ACT>(acc.z + cc.z);
+      o.w = act_fwd<ACT>(acc.w + cc.w);
+      reinterpret_cast<float4*>(y + (r0 + rr) * ldy)[t] = o;
+    }
+  }
+}
+
+// Backward of a narrow-input chain (nn._narrow_chain_grads): with Ã = [xᵀ·G; Σ G] and
+// P_L = Ã, P_{j-1} = P_j·K_jᵀ, every gradient is dK_j = R̃_{j-1}ᵀ·P_j, db_j = P_j[n0]
+// (R̃_j = [K_1···K_j; c_j], the forward composition's rows; R̃_0 = [I; 0]).
+// rt_product: out [m+1, n] = P [m+1, k]·Kᵀ, K [n, k] row-major: P staged in LDS, one wave per
+// output column (lanes stride the contiguous row of K), fixed butterfly per row.
+template <int MR>
+__global__ __launch_bounds__(kC3Waves * 64) void rt_product_kernel(
+    const float* __restrict__ P, int m, const float* __restrict__ K, int k, int n,
+    float* __restrict__ out) {
+  __shared__ float ps[kAugLds];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) ps[e] = P[e];
+  __syncthreads();
+  const int c = blockIdx.x * kC3Waves + w;
+  if (c >= n) return;
+  float acc[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) acc[i] = 0.f;
+  const float* kr = K + (int64_t)c * k;
+#pragma unroll 4
+  for (int kk = lane; kk < k; kk += 64) {
+    const float kv = kr[kk];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+      if (i <= m) acc[i] += ps[i * k + kk] * kv;
+  }
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    if (i > m) break;
+    const float v = wave_sum(acc[i]);
+    if (lane == 0) out[(int64_t)i * n + c] = v;
+  }
+}
+
+// out [na, nb] = R̃ᵀ·P: R̃ = [R (m rows, stride ldr); rlast] ([m+1, na], rlast NULL: a zero
+// row), P [m+1, nb] contiguous; four output columns per thread, r ascending.
+__global__ __launch_bounds__(256) void outer_sum_kernel(const float* __restrict__ R, int ldr, int m,
+                                                        const float* __restrict__ rlast, int na,
+                                                        const float* __restrict__ P, int nb,
+                                                        float* __restrict__ out) {
+  const int nbq = nb >> 2;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)na * nbq) return;
+  const int a = (int)(e / nbq), bq = (int)(e - (int64_t)a * nbq);
+  const float4* P4 = reinterpret_cast<const float4*>(P);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r <= m; ++r) {
+    float rv;
+    if (r < m) rv = R[(int64_t)r * ldr + a];
+    else if (rlast) rv = rlast[a];
+    else break;
+    const float4 pv = P4[(int64_t)r * nbq + bq];
+    acc.x += rv * pv.x;
+    acc.y += rv * pv.y;
+    acc.z += rv * pv.z;
+    acc.w += rv * pv.w;
+  }
+  reinterpret_cast<float4*>(out)[e] = acc;
+}
+
+// y[b] = act(x[b, :n0]·q + c[0]): one wave per row (16-byte loads, q held in registers),
+// rows grid-strided over the waves, fixed butterfly fold.
+template <int ACT>
+__global__ __launch_bounds__(256) void rowdot_act_kernel(const float* __restrict__ x, int64_t ldx,
+                                                         int64_t B, int n0,
+                                                         const float* __restrict__ q,
+                                                         const float* __restrict__ c,
+                                                         float* __restrict__ y) {
+  constexpr int kMaxQ = 4;  // float4 chunks per lane: n0 <= 1024
+  const int lane = threadIdx.x & 63;
+  const int nq = n0 >> 2;
+  float4 qv[kMaxQ];
+#pragma unroll
+  for (int j = 0; j < kMaxQ; ++j) {
+    const int e = lane + 64 * j;
+    qv[j] = e < nq ? reinterpret_cast<const float4*>(q)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float cc = c[0];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < B; row += nw) {
+    const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMaxQ; ++j) {
+      const int e = lane + 64 * j;
+      if (e < nq) {
+        const float4 v = xr[e];
+        acc += v.x * qv[j].x + v.y * qv[j].y + v.z * qv[j].z + v.w * qv[j].w;
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) y[row] = act_fwd<ACT>(acc + cc);
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -641,6 +924,119 @@ extern "C" int32_t rs_chain3_vec_grads(const float* K1, const int32_t* rows, con
   RS_CHECK_LAUNCH();
   const int64_t tot = (int64_t)n_full0 * n1 + (int64_t)n1 * n2 + n2 + n1 + 1;
   chain3_stage3<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_chain3_vec_compose(const float* K1, const int32_t* rows, int32_t n0,
+                                         const float* b1, const float* K2, const float* b2,
+                                         const float* K3, const float* b3, int32_t n1,
+                                         int32_t n2, float* q, float* c, void* workspace,
+                                         size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(n0 >= 1 && n1 >= 1 && n2 >= 1 && K1 && K2 && K3 && q && c,
+               "rs_chain3_vec_compose: bad arguments");
+  RS_CHECK_ARG(ws_bytes >= (size_t)(n1 + 1) * sizeof(float), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* w = static_cast<float*>(workspace);
+  VecComposeArgs a{K1, rows, b1, K2, b2, K3, b3, n0, n1, n2, w, w + n1, q, c};
+  vcompose_stage1<<<(unsigned)ceil_div(n1 + 1, kC3Waves), kC3Waves * 64, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  vcompose_stage2<<<(unsigned)ceil_div(n0 + 1, kC3Waves), kC3Waves * 64, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_chain_aug_product(const float* M, int32_t ldm, int32_t m, const float* cin,
+                                        const float* K, int32_t k, int32_t n, const float* b,
+                                        float* out, void* stream) {
+  RS_CHECK_ARG(m >= 0 && m < kAugRows && k >= 1 && n >= 1 && ldm >= k && K && out &&
+                   (m == 0 || M) && (int64_t)(m + 1) * k <= kAugLds,
+               "rs_chain_aug_product: bad arguments");
+  const unsigned g = (unsigned)ceil_div(n, 64);
+  hipStream_t st = as_stream(stream);
+  if (m < 16)
+    aug_product_kernel<16><<<g, kC3Waves * 64, 0, st>>>(M, ldm, m, cin, K, k, n, b, out);
+  else
+    aug_product_kernel<kAugRows><<<g, kC3Waves * 64, 0, st>>>(M, ldm, m, cin, K, k, n, b, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static int fwd_blocks(int64_t units, int64_t per_block) {
+  const int64_t b = ceil_div(units, per_block);
+  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
+extern "C" int32_t rs_affine_narrow_fwd(const float* x, int64_t ldx, int64_t B, int32_t n0,
+                                        const float* Qa, int32_t n, int32_t act, float* y,
+                                        int64_t ldy, void* stream) {
+  RS_CHECK_ARG(B >= 0 && n0 >= 1 && n0 < kAugRows && n >= 4 && n <= 256 && n % 4 == 0 &&
+                   ldx >= n0 && ldy >= n && ldy % 4 == 0 && act >= 0 && act <= 2,
+               "rs_affine_narrow_fwd: bad sizes");
+  RS_CHECK_ARG(B == 0 || (x && Qa && y), "null pointer");
+  RS_CHECK_ARG((reinterpret_cast<uintptr_t>(Qa) | reinterpret_cast<uintptr_t>(y)) % 16 == 0,
+               "rs_affine_narrow_fwd: Qa and y must be 16-byte aligned");
+  if (B == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  const int g = fwd_blocks(B, kNarrowRows);
+#define RS_NARROW(A, M) affine_narrow_fwd_kernel<A, M><<<g, 256, 0, st>>>(x, ldx, B, n0, Qa, n, y, ldy)
+  if (n0 < 16) {
+    if (act == 0) RS_NARROW(0, 16); else if (act == 1) RS_NARROW(1, 16); else RS_NARROW(2, 16);
+  } else {
+    if (act == 0) RS_NARROW(0, 32); else if (act == 1) RS_NARROW(1, 32); else RS_NARROW(2, 32);
+  }
+#undef RS_NARROW
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_rowdot_act(const float* x, int64_t ldx, int64_t B, int32_t n0,
+                                 const float* q, const float* c, int32_t act, float* y,
+                                 void* stream) {
+  RS_CHECK_ARG(B >= 0 && n0 >= 4 && n0 <= 1024 && n0 % 4 == 0 && ldx >= n0 && ldx % 4 == 0 &&
+                   act >= 0 && act <= 2,
+               "rs_rowdot_act: bad sizes");
+  RS_CHECK_ARG(B == 0 || (x && q && c && y), "null pointer");
+  RS_CHECK_ARG((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(q)) % 16 == 0,
+               "rs_rowdot_act: x and q must be 16-byte aligned");
+  if (B == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  const int g = fwd_blocks(B, 4 * 4);  // 4 rows per wave on average
+  switch (act) {
+    case 0: rowdot_act_kernel<0><<<g, 256, 0, st>>>(x, ldx, B, n0, q, c, y); break;
+    case 1: rowdot_act_kernel<1><<<g, 256, 0, st>>>(x, ldx, B, n0, q, c, y); break;
+    default: rowdot_act_kernel<2><<<g, 256, 0, st>>>(x, ldx, B, n0, q, c, y); break;
+  }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_chain_rt_product(const float* P, int32_t m, const float* K, int32_t k,
+                                       int32_t n, float* out, void* stream) {
+  RS_CHECK_ARG(m >= 0 && m < kAugRows && k >= 1 && n >= 1 && P && K && out &&
+                   (int64_t)(m + 1) * k <= kAugLds,
+               "rs_chain_rt_product: bad arguments");
+  const unsigned g = (unsigned)ceil_div(n, kC3Waves);
+  hipStream_t st = as_stream(stream);
+  if (m < 16)
+    rt_product_kernel<16><<<g, kC3Waves * 64, 0, st>>>(P, m, K, k, n, out);
+  else
+    rt_product_kernel<kAugRows><<<g, kC3Waves * 64, 0, st>>>(P, m, K, k, n, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_chain_outer(const float* R, int32_t ldr, int32_t m, const float* rlast,
+                                  int32_t na, const float* P, int32_t nb, float* out,
+                                  void* stream) {
+  RS_CHECK_ARG(m >= 0 && na >= 1 && nb >= 4 && nb % 4 == 0 && ldr >= na && P && out &&
+                   (m == 0 || R),
+               "rs_chain_outer: bad arguments");
+  RS_CHECK_ARG((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(out)) % 16 == 0,
+               "rs_chain_outer: P and out must be 16-byte aligned");
+  const int64_t tot = (int64_t)na * (nb / 4);
+  outer_sum_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
+      R, ldr, m, rlast, na, P, nb, out);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

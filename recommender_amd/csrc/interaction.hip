@@ -100,9 +100,20 @@ __device__ __forceinline__ const float* shfl_ptr(const float* p, int src) {
 // ---------------------------------------------------------------------------------------
 // forward, MFMA: one wave per sample, 4 waves per block
 // ---------------------------------------------------------------------------------------
-template <int D, class Src, bool DLRM_OUT>
+// HEAD (DLRM, composed top MLP): the top MLP is one affine map of the row (its hidden layers
+// are linear, ctr/layers.py:8), so the wave also forms y[b] = act(row·q + c) from the values it
+// writes (row order, fixed butterfly), and the top MLP's batch-deep GEMM disappears.
+struct FwdHead {
+  const float* q;  // [out_stride] Q_0 over the written row (padding entries multiply zeros)
+  const float* c;  // [1]
+  float* y;        // [batch]
+  int act;         // 0 linear, 1 relu, 2 sigmoid
+};
+
+template <int D, class Src, bool DLRM_OUT, bool HEAD = false>
 __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, int F, InterMode md,
-                                                      float* __restrict__ out, int64_t out_stride) {
+                                                      float* __restrict__ out, int64_t out_stride,
+                                                      FwdHead hd = {}) {
   constexpr int NT = D / 16;  // float4 loads per lane per block-row
   __shared__ float zt[4][32][33];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -110,6 +121,17 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   if (b >= batch) return;
   const int r = lane & 15, g = lane >> 4;
   bool oob = false;
+  // HEAD: this lane's q entries (compact row: pair o = lane + 64t, dense d = lane + 64t), loaded
+  // ahead of the gathers so their latency hides behind the row loads
+  constexpr int kHz = HEAD ? 8 : 1, kHd = HEAD ? (D + 63) / 64 : 1;
+  float qz[kHz], qd[kHd];
+  if constexpr (HEAD) {
+    const int nzc = F * (F - 1) / 2;
+#pragma unroll
+    for (int t = 0; t < kHz; ++t) qz[t] = lane + 64 * t < nzc ? hd.q[lane + 64 * t] : 0.f;
+#pragma unroll
+    for (int t = 0; t < kHd; ++t) qd[t] = lane + 64 * t < D ? hd.q[nzc + lane + 64 * t] : 0.f;
+  }
   // lane k < F resolves row k once; the MFMA lanes fetch the pointers by shuffle
   const float* mine = lane < F ? src.row(b, lane, D, oob) : nullptr;
   const float* p0 = shfl_ptr(mine, r);
@@ -149,7 +171,20 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   __builtin_amdgcn_wave_barrier();
   float* orow = out + b * out_stride;
   const int nz = out_width(F, md.self_interaction, md.skip_gather);
-  if (md.skip_gather) {
+  float hacc = 0.f;  // HEAD: this lane's share of row·q
+  if constexpr (HEAD) {  // compact row only (F <= 32: nz <= 465 < 64·kHz)
+#pragma unroll
+    for (int t = 0; t < kHz; ++t) {
+      const int o = lane + 64 * t;
+      if (o < nz) {
+        int i, j;
+        compact_pair(o, F, false, i, j);
+        const float v = z[i][j];
+        orow[o] = v;
+        hacc += v * qz[t];
+      }
+    }
+  } else if (md.skip_gather) {
     for (int o = lane; o < nz; o += 64) {
       int i = o / F, j = o - i * F;
       orow[o] = keep_pair(i, j, md.self_interaction) ? z[i][j] : 0.f;
@@ -165,7 +200,27 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
     // concat the bottom-MLP output behind Z (ctr/model.py:54)
     const float* dn = src.dense + b * D;
     float* od = orow + nz;
-    for (int d = lane; d < D; d += 64) od[d] = dn[d];
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int t = 0; t < kHd; ++t) {
+        const int d = lane + 64 * t;
+        if (d < D) {
+          const float v = dn[d];
+          od[d] = v;
+          hacc += v * qd[t];
+        }
+      }
+    } else {
+      for (int d = lane; d < D; d += 64) od[d] = dn[d];
+    }
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
+      if (lane == 0) {
+        const float v = hacc + hd.c[0];
+        hd.y[b] = hd.act == 2 ? 1.f / (1.f + expf(-v)) : (hd.act == 1 ? fmaxf(v, 0.f) : v);
+      }
+    }
     // zero the alignment padding of the row (compact layout padded for the GEMM tiles)
     for (int64_t o = nz + D + lane; o < out_stride; o += 64) orow[o] = 0.f;
     if (__any(oob) && lane == 0) flag_oob(src.err_flag);
@@ -817,6 +872,31 @@ extern "C" int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t ba
   RS_CHECK_ARG(emb && grad_out && grad_emb, "null pointer");
   fm_bwd_kernel<<<ceil_div(batch, 4), 256, 0, as_stream(stream)>>>(emb, grad_out, batch, F, D,
                                                                    grad_emb);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_dlrm_interaction_fwd_head(const float* table, int64_t n_rows, int32_t D,
+                                                const void* ids, int32_t id_dtype,
+                                                int32_t n_slots, const int64_t* slot_offsets,
+                                                const float* dense, int64_t batch, float* out,
+                                                int64_t out_stride, const float* q,
+                                                const float* c, int32_t act, float* y,
+                                                int32_t* err_flag, void* stream) {
+  const int F = n_slots + 1;
+  const InterMode md{0, 0};  // compact row
+  RS_CHECK_ARG(n_slots >= 1 && F <= 32 && D == 128 && batch >= 0,
+               "rs_dlrm_interaction_fwd_head: needs D = 128 and at most 31 slots");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(out_stride >= out_width(F, 0, 0) + D, "out_stride too small");
+  RS_CHECK_ARG(act >= 0 && act <= 2, "bad activation");
+  RS_CHECK_ARG(batch == 0 || (table && ids && dense && out && q && c && y), "null pointer");
+  RS_CHECK_ARG(al16(table) && al16(dense), "table and dense must be 16-byte aligned");
+  if (batch == 0) return RS_OK;
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
+  FwdHead hd{q, c, y, act};
+  inter_fwd_mfma<128, GatherSrc, true, true>
+      <<<ceil_div(batch, 4), 256, 0, as_stream(stream)>>>(src, batch, F, md, out, out_stride, hd);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

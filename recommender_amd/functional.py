@@ -164,11 +164,38 @@ class _DLRMTopFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, handle, dense, table_module, ids, layers, rows, composed=False):
-        from .nn import chain_forward
+        from .nn import chain_forward, vec_chain_compose, vec_chain_ready
 
         dense = dense.contiguous()
-        z = _DLRMInteraction.forward(ctx, handle, dense, table_module, ids, True)
-        y, ks = chain_forward(z, layers, rows, composed)
+        w = table_module.weight
+        D = w.shape[1]
+        width = rows.numel() if rows is not None else 0
+        if (composed and D == 128 and ids.shape[-1] + 1 <= 32 and vec_chain_ready(layers, width)
+                and w.data_ptr() % 16 == 0 and dense.data_ptr() % 16 == 0):
+            # the composed top MLP fused into the interaction kernel: y = act(row·q + c) per
+            # example as the row is written (rs_dlrm_interaction_fwd_head)
+            q, c = vec_chain_compose(layers, rows, width)
+            _wait_update(table_module)
+            L.require_device(w, "embedding table")
+            ids = _ids_flat(ids)
+            B, S = ids.shape
+            F = S + 1
+            nz = F * (F - 1) // 2 + D
+            if width != (nz + COMPACT_ALIGN - 1) // COMPACT_ALIGN * COMPACT_ALIGN:
+                raise ValueError(f"compact rows ({width}) do not match the interaction row")
+            if dense.shape != (B, D):
+                raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
+            z = torch.empty(B, width, device=w.device, dtype=torch.float32)
+            y = torch.empty(B, 1, device=w.device, dtype=torch.float32)
+            L.call("rs_dlrm_interaction_fwd_head", L.ptr(w), w.shape[0], D, L.ptr(ids),
+                   L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
+                   L.ptr(z), width, L.ptr(q), L.ptr(c), layers[-1].act_code, L.ptr(y),
+                   L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+            ctx.table_module, ctx.ids, ctx.compact = table_module, ids, 1
+            ks = [l.kernel for l in layers]  # the backward (_chain3_vec_grads) reads rows itself
+        else:
+            z = _DLRMInteraction.forward(ctx, handle, dense, table_module, ids, True)
+            y, ks = chain_forward(z, layers, rows, composed)
         ctx.layers, ctx.rows = layers, rows
         ctx.save_for_backward(dense, z, y, *ks)
         return y

@@ -323,6 +323,8 @@ def chain_param_grads(layers, rows, ks, A, s, need_q0=True):
             and all(l.bias is not None for l in layers)):
         return _chain3_vec_grads(layers, rows, ks, A, s)
     if n > 1 and A.shape[0] < A.shape[1] and _pgrad_stream is None:
+        if rows is None and narrow_chain_hip_ready(layers, A.shape[0]) and A.is_cuda:
+            return _narrow_chain_grads_hip(layers, ks, A, s, need_q0)
         return _narrow_chain_grads(layers, rows, ks, A, s, need_q0)
     Qa = [None] * n  # Qa[i] = K_{i+1}···K_L (None: identity)
     for i in range(n - 2, -1, -1):
@@ -394,6 +396,21 @@ def _narrow_chain_grads(layers, rows, ks, A, s, need_q0):
 _inv_cache: dict = {}
 
 
+def _rows_i32(rows, n_full0):
+    """(rows as int32, inverse map [n_full0] -> position or -1), cached per rows tensor."""
+    if rows is None:
+        return None, None
+    key = (rows.data_ptr(), n_full0)
+    hit = _inv_cache.get(key)
+    if hit is None or hit[0] is not rows:
+        r = rows.to(torch.int32).contiguous()
+        inv = torch.full((n_full0,), -1, dtype=torch.int32, device=rows.device)
+        inv[r.long()] = torch.arange(r.numel(), dtype=torch.int32, device=rows.device)
+        hit = (rows, r, inv)
+        _inv_cache[key] = hit
+    return hit[1], hit[2]
+
+
 def _chain3_vec_grads(layers, rows, ks, A, s):
     """chain_param_grads for a [n1, n2, 1] chain in three launches (rs_chain3_vec_grads)."""
     from . import _lib as L
@@ -403,17 +420,7 @@ def _chain3_vec_grads(layers, rows, ks, A, s):
     n2 = K2.shape[1]
     n0 = A.shape[0]
     dev = A.device
-    r = inv = None
-    if rows is not None:
-        key = (rows.data_ptr(), n_full0)
-        hit = _inv_cache.get(key)
-        if hit is None or hit[0] is not rows:
-            r = rows.to(torch.int32).contiguous()
-            inv = torch.full((n_full0,), -1, dtype=torch.int32, device=dev)
-            inv[r.long()] = torch.arange(n0, dtype=torch.int32, device=dev)
-            hit = (rows, r, inv)
-            _inv_cache[key] = hit
-        _, r, inv = hit
+    r, inv = _rows_i32(rows, n_full0)
     dK1 = torch.empty_like(K1)
     dK2 = torch.empty_like(K2)
     dK3 = torch.empty_like(K3)
@@ -468,6 +475,10 @@ def chain_forward(x, layers, rows=None, composed=False):
     is, y = act(x·Q_0 + c_L) (chain_compose): one batch-deep GEMM of width n_L instead of one
     per layer. Both are the same function in exact arithmetic; they differ only in fp32
     rounding order (tests/test_mlp_chain_gpu.py bounds both against a float64 oracle)."""
+    if composed and x.is_cuda:
+        fast = _composed_forward_hip(x, layers, rows)
+        if fast is not None:
+            return fast
     ks = [layer.kernel if (i > 0 or rows is None) else layer.kernel.index_select(0, rows)
           for i, layer in enumerate(layers)]
     if composed:
@@ -483,6 +494,150 @@ def chain_forward(x, layers, rows=None, composed=False):
     elif act == 2:
         h = torch.sigmoid_(h)
     return h, ks
+
+
+def vec_chain_ready(layers, n0):
+    """A [n1, n2, 1] chain with biases (the ctr top MLPs): the shapes rs_chain3_vec_compose and
+    the rank-one backward (_chain3_vec_grads) take."""
+    return (len(layers) == 3 and layers[2].kernel.shape[1] == 1 and n0 % 4 == 0 and n0 <= 1024
+            and all(l.bias is not None for l in layers))
+
+
+def vec_chain_compose(layers, rows, n0):
+    """(q [n0], c [1]) of a [n1, n2, 1] chain: q = K1[rows]·K2·K3, c = its carried biases
+    (rs_chain3_vec_compose, two launches)."""
+    from . import _lib as L
+
+    K1, K2, K3 = (l.kernel for l in layers)
+    n1, n2 = K2.shape
+    dev = K1.device
+    r, _ = _rows_i32(rows, K1.shape[0])
+    q = torch.empty(n0, device=dev)
+    c = torch.empty(1, device=dev)
+    ws = torch.empty(n1 + 1, device=dev)
+    L.call("rs_chain3_vec_compose", L.ptr(K1), L.ptr(r), n0, L.ptr(layers[0].bias), L.ptr(K2),
+           L.ptr(layers[1].bias), L.ptr(K3), L.ptr(layers[2].bias), n1, n2, L.ptr(q), L.ptr(c),
+           L.ptr(ws), ws.numel() * 4, L.stream_ptr(dev))
+    return q, c
+
+
+_compose_cache: dict = {}
+
+
+def _param_versions(layers):
+    return tuple((l.kernel.data_ptr(), l.kernel._version,
+                  None if l.bias is None else (l.bias.data_ptr(), l.bias._version)) for l in layers)
+
+
+def narrow_chain_compose(layers):
+    """[R̃_2, ..., R̃_n] of a narrow-input chain, R̃_j = [K_1···K_j; c_j] ([n0+1, n_j]; the last
+    is [Q_0; c_L]), by rs_chain_aug_product. Cached until a parameter changes (tensor version
+    counters), so the backward reuses the forward's products."""
+    from . import _lib as L
+
+    key = id(layers[0].kernel)
+    ver = _param_versions(layers)
+    hit = _compose_cache.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    ks = [l.kernel for l in layers]
+    n0 = ks[0].shape[0]
+    dev = ks[0].device
+    st = L.stream_ptr(dev)
+    outs, qa = [], None
+    for i in range(1, len(layers)):
+        k, nn_ = ks[i].shape
+        out = torch.empty(n0 + 1, nn_, device=dev)
+        M, ldm = (ks[0], ks[0].shape[1]) if qa is None else (qa, qa.shape[1])
+        cin = layers[0].bias if qa is None else qa[n0]
+        L.call("rs_chain_aug_product", L.ptr(M), ldm, n0, L.ptr(cin), L.ptr(ks[i]), k, nn_,
+               L.ptr(layers[i].bias), L.ptr(out), st)
+        outs.append(out)
+        qa = out
+    _compose_cache[key] = (ver, outs)
+    return outs
+
+
+def narrow_chain_hip_ready(layers, n0):
+    """Shapes the narrow-chain HIP kernels take: n0 < 33 inputs, fp32, every width a multiple
+    of 4 and (n0 + 1)·width within the LDS staging buffer."""
+    ks = [l.kernel for l in layers]
+    return (len(layers) >= 2 and n0 < 33 and ks[0].is_cuda
+            and all(k.dtype == torch.float32 and k.is_contiguous() for k in ks)
+            and all(k.shape[1] % 4 == 0 and (n0 + 1) * k.shape[0] <= 16896 for k in ks)
+            and all(l.bias is None or l.bias.is_contiguous() for l in layers))
+
+
+def _narrow_chain_grads_hip(layers, ks, A, s, need_q0):
+    """_narrow_chain_grads on the HIP kernels (rs_chain_rt_product, rs_chain_outer): with
+    Ã = [A; s], P_L = Ã and P_{j-1} = P_j·K_jᵀ, dK_j = R̃_{j-1}ᵀ·P_j and db_j = P_j[n0], where
+    R̃_j = [K_1···K_j; c_j] are the forward composition's products (narrow_chain_compose) and
+    R̃_0 = [I; 0]: every contraction is over n0 + 1 rows or a weight's width, ≈4 M multiply-adds
+    for the DLRM bottom MLP instead of ≈19 M."""
+    from . import _lib as L
+
+    n = len(layers)
+    n0, nl = A.shape
+    dev = A.device
+    st = L.stream_ptr(dev)
+    comp = narrow_chain_compose(layers)
+    P = torch.cat([A, s.reshape(1, nl)])
+    for j in range(n - 1, -1, -1):
+        layer = layers[j]
+        n_in, n_out = ks[j].shape
+        if j == 0:
+            dk = P[:n0]
+        else:
+            if j == 1:
+                R, ldr, rl = ks[0], ks[0].shape[1], layers[0].bias
+            else:
+                R = comp[j - 2]
+                ldr, rl = R.shape[1], R[n0]
+            dk = torch.empty(n_in, n_out, device=dev)
+            L.call("rs_chain_outer", L.ptr(R), ldr, n0, L.ptr(rl), n_in, L.ptr(P), n_out,
+                   L.ptr(dk), st)
+        _accum_grad(layer.kernel, dk)
+        if layer.bias is not None:
+            _accum_grad(layer.bias, P[n0])
+        if j > 0:
+            Pn = torch.empty(n0 + 1, n_in, device=dev)
+            L.call("rs_chain_rt_product", L.ptr(P), n0, L.ptr(ks[j]), n_out, n_in, L.ptr(Pn), st)
+            P = Pn
+    return comp[-1][:n0] if need_q0 else None
+
+
+def _composed_forward_hip(x, layers, rows):
+    """chain_forward(composed=True) through the HIP kernels for the two ctr chain shapes:
+    a narrow input (n0 < 33, e.g. the DLRM bottom MLP's 13 features: rs_chain_aug_product
+    composes [Q_0; c_L], rs_affine_narrow_fwd evaluates it) and a [n1, n2, 1] chain (the top
+    MLPs: rs_chain3_vec_compose + rs_rowdot_act). None for other shapes (torch composition)."""
+    from . import _lib as L
+
+    B, n0 = x.shape
+    n = len(layers)
+    nl = layers[-1].kernel.shape[1]
+    act = layers[-1].act_code
+    dev = x.device
+    f32 = x.dtype == torch.float32 and all(l.kernel.dtype == torch.float32 for l in layers)
+    if not f32 or x.stride(1) != 1 or act not in (0, 1, 2):
+        return None
+    st = L.stream_ptr(dev)
+    ks = [l.kernel for l in layers]
+    if rows is None and nl <= 256 and narrow_chain_hip_ready(layers, n0):
+        qa = narrow_chain_compose(layers)[-1]
+        y = torch.empty(B, nl, device=dev)
+        L.call("rs_affine_narrow_fwd", L.ptr(x), x.stride(0), B, n0, L.ptr(qa), nl, act,
+               L.ptr(y), nl, st)
+        return y, ks
+    if (vec_chain_ready(layers, n0) and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0
+            and (rows is None or rows.numel() == n0)):
+        q, c = vec_chain_compose(layers, rows, n0)
+        y = torch.empty(B, 1, device=dev)
+        L.call("rs_rowdot_act", L.ptr(x), x.stride(0), B, n0, L.ptr(q), L.ptr(c), act, L.ptr(y), st)
+        # ks[0] stays the full kernel: the backward of this shape (_chain3_vec_grads) reads the
+        # layers' kernels through rows itself
+        return y, ks
+    return None
 
 
 def linear_chain(x, layers, rows=None, handle=None, composed=False):

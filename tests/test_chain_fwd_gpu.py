@@ -1,0 +1,204 @@
+"""Composed linear-chain forward kernels (nn.chain_forward composed=True; the reference's ctr MLP
+hidden layers are linear, ctr/layers.py:8, so each MLP is y = act(x·Q_0 + c_L)):
+rs_chain_aug_product / rs_affine_narrow_fwd (narrow input, the DLRM bottom MLP),
+rs_chain3_vec_compose / rs_rowdot_act (the [n1, n2, 1] top MLPs) and the top MLP fused into the
+interaction kernel (rs_dlrm_interaction_fwd_head). Checked against the float64 layer-by-layer
+forward (oracle/ctr.py mlp_forward order) within 1e-5 relative to |x|·|K_1|···|K_L| + |c|, the
+magnitude bound of both evaluation orders; the interaction row itself bit-identical to
+rs_dlrm_interaction_fwd."""
+import numpy as np
+import pytest
+import torch
+
+from recommender_amd import _lib as L
+from recommender_amd import nn as N
+from tests.conftest import assert_close_rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class _Layer:
+    def __init__(self, k, b, act=0):
+        self.kernel, self.bias, self.act_code = k, b, act
+
+
+def _chain(dims, bias, act, seed):
+    g = np.random.default_rng(seed)
+    ks = [g.standard_normal((dims[i], dims[i + 1])) / np.sqrt(dims[i]) for i in range(len(dims) - 1)]
+    bs = [g.uniform(-0.1, 0.1, dims[i + 1]) if bias else None for i in range(len(dims) - 1)]
+    layers = [_Layer(torch.tensor(k, dtype=torch.float32, device=DEV),
+                     None if b is None else torch.tensor(b, dtype=torch.float32, device=DEV))
+              for k, b in zip(ks, bs)]
+    layers[-1].act_code = act
+    return ks, bs, layers
+
+
+def _ref(x, ks, bs, act, rows=None):
+    """float64 layer-by-layer forward and the magnitude bound of the composed product."""
+    h = x.astype(np.float64)
+    bound = np.abs(h)
+    for i, (k, b) in enumerate(zip(ks, bs)):
+        k = k if (i > 0 or rows is None) else k[rows]
+        h = h @ k + (b if b is not None else 0.0)
+        bound = bound @ np.abs(k) + (np.abs(b) if b is not None else 0.0)
+    if act == 1:
+        h = np.maximum(h, 0.0)
+    elif act == 2:
+        h = 1.0 / (1.0 + np.exp(-h))
+    return h, bound
+
+
+@pytest.mark.parametrize("dims,bias,act,B", [
+    ([13, 512, 256, 128], True, 1, 4099),   # DLRM bottom MLP (north star)
+    ([13, 64, 16], False, 0, 257),          # no biases
+    ([5, 7, 12], True, 2, 33),              # n % 64 != 0, 3 float4 columns per row
+    ([32, 40, 200], True, 1, 1000),         # widest input; 50 lanes per row (5 rows per pass)
+    ([1, 4, 8], True, 0, 3),                # one feature
+])
+def test_narrow_chain_forward(dims, bias, act, B):
+    ks, bs, layers = _chain(dims, bias, act, sum(dims))
+    x = np.random.default_rng(B).standard_normal((B, dims[0])).astype(np.float32)
+    xt = torch.from_numpy(x).to(DEV)
+    y, used = N.chain_forward(xt, layers, None, composed=True)
+    assert all(u is l.kernel for u, l in zip(used, layers))
+    ref, bound = _ref(x, ks, bs, act)
+    if act == 2:
+        bound = np.full_like(bound, 1.0)
+    assert_close_rel(y.cpu().numpy(), ref, 1e-5, bound, "y")
+    # deterministic: a second evaluation is bit-identical
+    y2, _ = N.chain_forward(xt, layers, None, composed=True)
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("n0,n1,n2,B,act,with_rows", [
+    (480, 512, 256, 4097, 2, True),   # DLRM top MLP on the compact row
+    (428, 512, 256, 1024, 0, False),  # DeepFM-shaped input, linear head
+    (16, 8, 4, 5, 1, False),
+    (1024, 64, 32, 130, 2, False),    # widest rs_rowdot_act row
+])
+def test_vec_chain_forward(n0, n1, n2, B, act, with_rows):
+    full = n0 + 37 if with_rows else n0
+    ks, bs, layers = _chain([full, n1, n2, 1], True, act, n0 + B)
+    rows = np.random.default_rng(1).permutation(full)[:n0] if with_rows else None
+    x = np.random.default_rng(B).standard_normal((B, n0)).astype(np.float32)
+    rt = torch.from_numpy(rows).to(DEV) if with_rows else None
+    y, _ = N.chain_forward(torch.from_numpy(x).to(DEV), layers, rt, composed=True)
+    assert y.shape == (B, 1)
+    ref, bound = _ref(x, ks, bs, act, rows)
+    if act == 2:
+        bound = np.full_like(bound, 1.0)
+    assert_close_rel(y.cpu().numpy(), ref, 1e-5, bound, "y")
+
+
+def test_vec_compose_values():
+    """q = K1[rows]·K2·K3 and c = b3 + K3ᵀ·b2 + (K2·K3)ᵀ·b1 against float64."""
+    ks, bs, layers = _chain([300, 96, 40, 1], True, 0, 7)
+    rows = np.arange(0, 300, 3)
+    q, c = N.vec_chain_compose(layers, torch.from_numpy(rows).to(DEV), rows.size)
+    q1 = ks[1] @ ks[2]
+    qref = (ks[0][rows] @ q1)[:, 0]
+    cref = bs[2][0] + ks[2][:, 0] @ bs[1] + q1[:, 0] @ bs[0]
+    qb = (np.abs(ks[0][rows]) @ np.abs(ks[1]) @ np.abs(ks[2]))[:, 0]
+    assert_close_rel(q.cpu().numpy(), qref, 1e-5, qb, "q")
+    assert abs(float(c) - cref) <= 1e-5 * (abs(bs[2][0]) + np.abs(ks[2][:, 0]) @ np.abs(bs[1])
+                                          + np.abs(q1[:, 0]) @ np.abs(bs[0]))
+
+
+@pytest.mark.parametrize("id64,oob", [(True, False), (False, False), (True, True)])
+def test_interaction_head(id64, oob):
+    """rs_dlrm_interaction_fwd_head: the row bit-identical to rs_dlrm_interaction_fwd, y within
+    1e-5 of act(row·q + c) in float64; an out-of-range id still sets the error flag."""
+    S, D, B, V = 26, 128, 1031, 5000
+    F = S + 1
+    width = 480
+    g = np.random.default_rng(11)
+    table = torch.from_numpy(g.standard_normal((V, D)).astype(np.float32) * 0.1).to(DEV)
+    ids_np = g.integers(0, V, (B, S))
+    if oob:
+        ids_np[7, 3] = V + 5
+    ids = torch.from_numpy(ids_np.astype(np.int64 if id64 else np.int32)).to(DEV)
+    dense = torch.from_numpy(g.standard_normal((B, D)).astype(np.float32)).to(DEV)
+    q = torch.from_numpy(g.standard_normal(width).astype(np.float32) * 0.05).to(DEV)
+    c = torch.tensor([0.3], device=DEV)
+    st = L.stream_ptr(DEV)
+    z0 = torch.empty(B, width, device=DEV)
+    z1 = torch.empty(B, width, device=DEV)
+    y = torch.empty(B, 1, device=DEV)
+    f0 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    f1 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    code = L.RS_ID_I64 if id64 else L.RS_ID_I32
+    L.call("rs_dlrm_interaction_fwd", L.ptr(table), V, D, L.ptr(ids), code, S, None, L.ptr(dense),
+           B, 1, L.ptr(z0), width, L.ptr(f0), st)
+    L.call("rs_dlrm_interaction_fwd_head", L.ptr(table), V, D, L.ptr(ids), code, S, None,
+           L.ptr(dense), B, L.ptr(z1), width, L.ptr(q), L.ptr(c), 2, L.ptr(y), L.ptr(f1), st)
+    assert torch.equal(z0, z1)
+    assert int(f0) == int(f1) == (1 if oob else 0)
+    zz = z1.cpu().numpy().astype(np.float64)
+    ref = 1.0 / (1.0 + np.exp(-(zz @ q.cpu().numpy().astype(np.float64) + 0.3)))
+    assert_close_rel(y.cpu().numpy()[:, 0], ref, 1e-5, np.ones_like(ref), "y")
+    assert F * (F - 1) // 2 + D <= width
+
+
+@pytest.mark.parametrize("dims,bias", [([13, 512, 256, 128], True), ([13, 64, 32, 16, 8], False),
+                                       ([7, 12, 20], True), ([32, 40, 24], True)])
+def test_narrow_chain_backward(dims, bias):
+    """_narrow_chain_grads_hip (P-chain + outer products over n0 + 1 rows) against float64
+    autograd of the layer-by-layer chain, 1e-5 relative to the magnitude of the products."""
+    ks, bs, layers = _chain(dims, bias, 1, 3 * sum(dims))
+    B = 2000
+    g = np.random.default_rng(5)
+    x = g.standard_normal((B, dims[0]))
+    G = g.standard_normal((B, dims[-1]))
+    A = torch.tensor((x.T @ G), dtype=torch.float32, device=DEV)
+    s = torch.tensor(G.sum(0), dtype=torch.float32, device=DEV)
+    for l in layers:
+        l.kernel.grad = None
+        if l.bias is not None:
+            l.bias.grad = None
+    N.chain_forward(torch.tensor(x, dtype=torch.float32, device=DEV), layers, None, composed=True)
+    assert N.narrow_chain_hip_ready(layers, dims[0])
+    q0 = N._narrow_chain_grads_hip(layers, [l.kernel for l in layers], A, s, need_q0=True)
+    # float64 reference
+    kt = [torch.tensor(k, requires_grad=True) for k in ks]
+    bt = [torch.tensor(b, requires_grad=True) if b is not None else None for b in bs]
+    h = torch.tensor(x)
+    for k, b in zip(kt, bt):
+        h = h @ k + (b if b is not None else 0.0)
+    h.backward(torch.tensor(G))
+    absx, absG = np.abs(x), np.abs(G)
+    # magnitude bound: |h_{j-1}|ᵀ·|G|·|Q_j|ᵀ
+    hb = absx
+    for j, l in enumerate(layers):
+        Qb = np.eye(dims[-1])
+        for k in reversed(ks[j + 1:]):
+            Qb = np.abs(k) @ Qb
+        kb = hb.T @ absG @ Qb.T
+        assert_close_rel(l.kernel.grad.cpu().numpy(), kt[j].grad.numpy(), 1e-5, kb, f"dK{j}")
+        if l.bias is not None:
+            assert_close_rel(l.bias.grad.cpu().numpy(), bt[j].grad.numpy(), 1e-5,
+                             absG.sum(0) @ Qb.T, f"db{j}")
+        hb = hb @ np.abs(ks[j]) + (np.abs(bs[j]) if bs[j] is not None else 0.0)
+    Q, Qb = ks[0], np.abs(ks[0])
+    for k in ks[1:]:
+        Q, Qb = Q @ k, Qb @ np.abs(k)
+    assert_close_rel(q0.cpu().numpy(), Q, 1e-5, Qb, "Q0")
+
+
+def test_compose_cache_follows_parameter_updates():
+    """The forward's composition is cached per parameter version: an in-place update (as the
+    optimizer step does) makes the next forward recompose."""
+    dims = [13, 64, 32]
+    ks, bs, layers = _chain(dims, True, 0, 99)
+    x = np.random.default_rng(2).standard_normal((100, 13)).astype(np.float32)
+    xt = torch.from_numpy(x).to(DEV)
+    y1, _ = N.chain_forward(xt, layers, None, composed=True)
+    with torch.no_grad():
+        layers[1].kernel.mul_(0.5)
+        layers[0].bias.add_(1.0)
+    ks[1] = ks[1] * 0.5
+    bs[0] = bs[0] + 1.0
+    y2, _ = N.chain_forward(xt, layers, None, composed=True)
+    ref, bound = _ref(x, ks, bs, 0)
+    assert_close_rel(y2.cpu().numpy(), ref, 1e-5, bound, "y after update")
+    assert not torch.equal(y1, y2)
