@@ -35,6 +35,18 @@ struct RowIO<4> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
+// a read-once stream (the walk's gradient rows): non-temporal, so it does not evict the
+// table rows and tile partials that are read again
+template <int VEC>
+__device__ __forceinline__ void load_stream(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    RowIO<VEC>::load(p, v);
+  }
+}
 template <>
 struct RowIO<2> {
   static __device__ __forceinline__ void load(const float* p, float (&v)[2]) {
@@ -250,7 +262,7 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restric
       for (int c = 0; c < CPL; ++c) {
         int col = (gl + c * lpr) * VEC;
         if (live && col < dim) {
-          RowIO<VEC>::load(grad + p * dim + col, r[u][c]);
+          load_stream<VEC>(grad + p * dim + col, r[u][c]);
         } else {
 #pragma unroll
           for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
