@@ -2,7 +2,7 @@
 # parity tests of the sparse path first, then the isolated north-star path, alternating
 export TMPDIR=/tmp
 L=recommender_amd/_lib
-timeout -k 10 300 python -u -m pytest tests/test_embedding_gpu.py tests/test_sharded_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_embedding_gpu.py tests/test_sharded_gpu.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
 tail -1 gpurun_out/ab_pytest.log
 cp $L/librecsys_hip.so /tmp/new.so; cp $L/librecsys_hip_base.so /tmp/base.so
 for v in new base new base; do
