@@ -1,0 +1,121 @@
+"""Checker for one production DLRM SGD step against oracle/ctr.py, on the step's touched rows.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py; parity unpinned): called by
+tests/test_northstar_gpu.py (full north-star size) and __graft_entry__.smoke() (small size).
+It drives the product path (recommender_amd TrainStep on cuda) and checks it; nothing in the
+product imports this module.
+
+The slab rows the batch references are gathered before the step and the ids are remapped onto
+them monotonically, so the oracle's sort order, tiles and segmented-sum order are exactly those
+of the full slab (reference semantics: ctr/model.py:45-57, ctr/train.py:77-79 SGD path).
+Checks (tolerances are the ones stated here):
+  * loss within 1e-5 relative;
+  * per-example logits: the pre-sigmoid value recovered from p within 1e-5 of its own value
+    plus 1e-6 of its float64 magnitude bound (|row|·|K1|·|K2|·|K3| with |biases|: every fp32
+    rounding of either MLP evaluation order is relative to it), plus the fp32 resolution of p;
+  * grad rows [B*S, D] (position order) within 1e-5 of the oracle's, relative to each element's
+    float64 magnitude bound |dZ + dZᵀ|·|X|;
+  * sorted rows / positions bit-exact;
+  * touched table rows BIT-EXACT against the oracle's segmented sum + SGD fed with the kernel's
+    own grad rows, and within 1e-4 of each row's |Δ| (+2 ulp of w) of the all-oracle update;
+    at least a quarter of the touched elements must actually change (a vacuous update fails);
+  * sampled untouched rows (including the slab's last rows) unchanged.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .ctr import DLRMState, dlrm_sgd_step
+from .embedding import global_rows, segment_sum_tiled
+
+
+def _layers(mlp):
+    return [(l.kernel.detach().cpu().numpy().copy(), l.bias.detach().cpu().numpy().copy())
+            for l in mlp.mlp]
+
+
+def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
+    """Run `step` (a recommender_amd.ctr.train.TrainStep with a fused SparseSGD) on one batch and
+    check it against the oracle; raises AssertionError on a mismatch, returns a summary."""
+    import torch
+
+    emb = model.embedding_layer
+    W = emb.weight
+    dev = W.device
+    V, D = W.shape
+    B, S = cat.shape
+    so = emb.slot_offsets.cpu().numpy() if emb.slot_offsets is not None else None
+    rows = global_rows(cat, V, so).reshape(B, S)
+    assert (rows >= 0).all(), "the checker expects in-range ids"
+    uniq = np.unique(rows)
+    compact = np.searchsorted(uniq, rows).astype(np.int64)  # monotone: same sort order
+    ut = torch.from_numpy(uniq).to(dev)
+    emb.wait_update()
+    torch.cuda.synchronize()
+    before = W[ut].cpu().numpy()
+    probe = np.setdiff1d(np.r_[np.arange(0, V, max(V // 41, 1)), V - 1, V - 2], uniq)
+    pt = torch.from_numpy(probe).to(dev)
+    probe_before = W[pt].cpu().numpy()
+    st = DLRMState(before.copy(), None, _layers(model.bottom_mlp), _layers(model.top_mlp))
+
+    captured = {}
+    opt = step.opt_sparse
+    launch = opt._launch_apply
+
+    def spy(table, ids, grad_rows, sorted_ids):
+        captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
+        return launch(table, ids, grad_rows, sorted_ids)
+
+    opt._launch_apply = spy
+    try:
+        batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
+                 torch.from_numpy(lb).to(dev))
+        loss = float(step(batch).detach())
+    finally:
+        opt._launch_apply = launch
+    emb.wait_update()
+    torch.cuda.synchronize()
+    assert "grad_rows" in captured, "the fused sparse apply did not run"
+    p_gpu = step.last_pred.cpu().numpy().astype(np.float64)
+    after = W[ut].cpu().numpy()
+    g_gpu = captured["grad_rows"].cpu().numpy().reshape(B * S, D)
+    s_rows = captured["sorted"].rows.cpu().numpy().view(np.uint32).astype(np.int64)
+    s_pos = captured["sorted"].pos.cpu().numpy()
+    assert np.array_equal(W[pt].cpu().numpy(), probe_before), "an untouched row changed"
+
+    det: dict = {}
+    ref_loss = dlrm_sgd_step(st, compact, dn, lb, lr, det)
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), f"loss {loss} vs oracle {ref_loss}"
+
+    z_ref = det["logit"].astype(np.float64)
+    pc = np.clip(p_gpu, 1e-30, 1 - 1e-7)
+    z_gpu = np.log(pc) - np.log1p(-pc)
+    res = 2 * np.spacing(p_gpu.astype(np.float32)).astype(np.float64) / (pc * (1 - pc))
+    ztol = 1e-5 * np.abs(z_ref) + 1e-6 * det["logit_bound"] + res
+    zerr = np.abs(z_gpu - z_ref)
+    assert (zerr <= ztol).all(), (
+        f"logit off at example {int(np.argmax(zerr / ztol))}: max err/tol {(zerr / ztol).max():.3g}")
+
+    assert np.array_equal(uniq[det["sorted_rows"].astype(np.int64)], s_rows), "sorted rows differ"
+    assert np.array_equal(det["sorted_pos"], s_pos), "sorted positions differ"
+
+    gerr = np.abs(g_gpu.astype(np.float64) - det["dx"])
+    gtol = 1e-5 * det["dx_bound"] + 1e-38
+    assert (gerr <= gtol).all(), f"grad rows: max err/bound {(gerr / gtol).max():.3g}"
+
+    ur, ug = segment_sum_tiled(det["sorted_rows"], det["sorted_pos"], g_gpu, uniq.size)
+    assert np.array_equal(ur.astype(np.int64), np.arange(uniq.size))
+    expect = before - np.float32(lr) * ug
+    bad = (after != expect).any(1)
+    assert not bad.any(), f"{int(bad.sum())} of {uniq.size} touched rows differ from the oracle apply"
+    changed = float((after != before).mean())
+    assert changed >= 0.25, f"only {changed:.2%} of touched elements changed: vacuous check"
+    d_gpu = after.astype(np.float64) - before
+    d_ref = st.table.astype(np.float64) - before
+    row_scale = np.abs(d_ref).max(1, keepdims=True)
+    assert (np.abs(d_gpu - d_ref) <= 1e-4 * row_scale + 2 * np.spacing(np.abs(before))).all(), \
+        "table update differs from the all-oracle step beyond 1e-4 of the row's |delta|"
+    return {"loss": loss, "oracle_loss": ref_loss, "touched_rows": int(uniq.size),
+            "max_row": int(uniq.max()), "rows_beyond_2^32_elems": int((uniq * D >= (1 << 32)).sum()),
+            "logit_err_over_tol": float((zerr / ztol).max()),
+            "grad_err_over_bound": float((gerr / gtol).max()), "frac_elements_changed": changed}

@@ -16,13 +16,16 @@ from .embedding import global_rows, segment_sum_tiled, sort_ids
 EPS = np.float32(1e-7)
 
 
-def mlp_forward(x, layers, final_activation):
-    """layers = [(kernel [in,out], bias [out]), ...]; returns (out, cache)."""
+def mlp_forward(x, layers, final_activation, pre=None):
+    """layers = [(kernel [in,out], bias [out]), ...]; returns (out, cache). `pre` (a list)
+    receives the last layer's pre-activation values."""
     cache = [x]
     h = x
     for li, (k, b) in enumerate(layers):
         h = h @ k + b
         if li == len(layers) - 1:
+            if pre is not None:
+                pre.append(h)
             if final_activation == "relu":
                 h = np.maximum(h, 0)
             elif final_activation == "sigmoid":
@@ -82,13 +85,29 @@ def dlrm_forward(st: DLRMState, cat, dense_in):
     z = np.matmul(x, x.transpose(0, 2, 1))                           # [B, F, F]
     z = z * np.triu(np.ones((F, F), np.float32), 1)[None]            # strict upper kept
     tin = np.concatenate([z.reshape(B, F * F), bot], axis=1)
-    p, tcache = mlp_forward(tin, st.top, "sigmoid")
-    return p[:, 0], dict(bcache=bcache, tcache=tcache, x=x, rows=rows)
+    pre = []
+    p, tcache = mlp_forward(tin, st.top, "sigmoid", pre)
+    return p[:, 0], dict(bcache=bcache, tcache=tcache, x=x, rows=rows, logit=pre[0][:, 0])
 
 
-def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr):
+def magnitude_chain(x_abs, layers):
+    """Float64 magnitude bound of an MLP chain's pre-activation outputs: every rounding of
+    either evaluation order (layer by layer, or the composed affine map) is bounded relative
+    to this, |x|·|K1|·…·|Kn| with the |biases| carried along."""
+    h = np.asarray(x_abs, np.float64)
+    for k, b in layers:
+        h = h @ np.abs(k).astype(np.float64) + np.abs(b).astype(np.float64)
+    return h
+
+
+def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
     """One DLRM train step: forward, mean BCE, backward, SGD on every parameter (dense: plain
-    SGD; table: deduplicated sparse SGD with the kernel's summation order). Returns loss."""
+    SGD; table: deduplicated sparse SGD with the kernel's summation order). Returns loss.
+
+    detail (a dict, optional) receives the step's intermediates for the full-size parity test:
+    p, logit (pre-sigmoid) and its float64 magnitude bound, the table grad rows dx [B*S, D] in
+    position order and their magnitude bound, the deduplicated (uniq_rows, uniq_grad), the dense
+    gradients and the sorted (rows, pos)."""
     B, S = cat.shape
     D = st.table.shape[1]
     F = S + 1
@@ -101,6 +120,7 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr):
     dx = np.matmul(sm, c["x"])                                       # [B, F, D]
     dbot = dx[:, S, :] + dtin[:, F * F:]
     _, bgrads = mlp_backward(dbot, st.bottom, c["bcache"], "relu", need_dx=False)
+    top_old = list(st.top)
     lr = np.float32(lr)
     for layers, grads in ((st.top, tgrads), (st.bottom, bgrads)):
         for i, ((k, b), (dk, db)) in enumerate(zip(layers, grads)):
@@ -108,5 +128,20 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr):
     sr, sp, _ = sort_ids(cat, st.table.shape[0], st.slot_offsets)
     ur, ug = segment_sum_tiled(sr, sp, dx[:, :S, :].reshape(B * S, D), st.table.shape[0])
     u = ur.astype(np.int64)
+    if detail is not None:
+        tin_abs = np.abs(c["tcache"][0]).astype(np.float64)
+        # |d logit / d tin| chain and the bound of the strict-upper dZ fed to the interaction
+        mag_logit = magnitude_chain(tin_abs, top_old)[:, 0]
+        g_abs = np.abs(dp[:, 0]).astype(np.float64) * 0.25  # |sigma'| <= 1/4
+        q = np.ones((1, 1))
+        for k, _ in reversed(top_old):
+            q = np.abs(k).astype(np.float64) @ q
+        dz_b = (g_abs[:, None] * q[None, : F * F, 0]).reshape(B, F, F)
+        dz_b = dz_b * np.triu(np.ones((F, F)), 1)[None]
+        dx_b = np.matmul(dz_b + dz_b.transpose(0, 2, 1), np.abs(c["x"]).astype(np.float64))
+        detail.update(p=p, logit=c["logit"], logit_bound=mag_logit,
+                      dx=dx[:, :S, :].reshape(B * S, D), dx_bound=dx_b[:, :S, :].reshape(B * S, D),
+                      uniq_rows=u, uniq_grad=ug, top_grads=tgrads, bottom_grads=bgrads,
+                      sorted_rows=sr, sorted_pos=sp)
     st.table[u] = st.table[u] - lr * ug
     return loss
