@@ -30,14 +30,31 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head", "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1",
-         "rs_sort_ids", "rs_embedding_apply", "rs_sort_ids_sharded", "rs_embedding_dedup_grad"]
-# the roofline kernel: the embedding-path kernel with the most algorithmic HBM traffic per step
-# (re-gather of every row + grad-row write). It runs on the main stream, so its HIP-event time
-# is its own; the sort/apply run on the fused optimizer's side stream beside dense GEMMs, so
-# their event spans include co-run time and are reported as such.
-ROOF_KERNELS = ("rs_dlrm_interaction_bwd_rank1", "rs_dlrm_interaction_bwd")  # whichever ran
-SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_sort_ids_sharded", "rs_embedding_dedup_grad"}
+WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head", "rs_dlrm_interaction_fwd_head_dx",
+         "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids",
+         "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
+         "rs_embedding_dedup_grad"]
+# the embedding path of SURVEY §8(d) (lookup fwd + bwd + dedup + apply) as the production step
+# launches it: the fused gather + interaction + unit-backward kernel (main stream), the radix
+# sort and the segmented-sum apply (fused optimizer's side stream, co-running with dense GEMMs:
+# their event spans include that co-run time)
+PATH_KERNELS = ("rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
+                "rs_dlrm_interaction_fwd_head_dx", "rs_dlrm_interaction_bwd",
+                "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids", "rs_sort_ids_sharded",
+                "rs_embedding_apply", "rs_embedding_apply_scaled")
+SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_embedding_apply_scaled",
+               "rs_sort_ids_sharded", "rs_embedding_dedup_grad"}
+# device symbols behind each C-ABI entry (for the PMC passes)
+# (entry, device-symbol regex of its kernels, the one kernel every call launches once)
+PMC_SYMBOLS = [
+    ("rs_dlrm_interaction_fwd_head_dx", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, true>",
+     "inter_fwd_mfma"),
+    ("rs_dlrm_interaction_fwd_head", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, false>",
+     "inter_fwd_mfma"),
+    ("rs_dlrm_interaction_bwd_rank1", r"dlrm_bwd_pipe", "dlrm_bwd_pipe"),
+    ("rs_sort_ids", r"radix_|make_keys|scan_|count_unique", "make_keys"),
+    ("rs_embedding_apply", r"seg_tile|seg_chunk|seg_fixup", "seg_tile"),
+]
 
 
 def parse():
@@ -79,17 +96,19 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = "dlrm_bwd_pipe|inter_bwd_mfma"  # device symbols of rs_dlrm_interaction_bwd
+PMC_KERNEL_REGEX = "inter_fwd_mfma|dlrm_bwd_pipe|radix_|make_keys|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 
 def measure_traffic(args):
-    """HBM bytes per launch of the roofline kernel from PMC counters, collected as the
-    microarchitecture guide prescribes: separate `rocprofv3 --pmc` passes for FETCH_SIZE and
+    """HBM bytes per step of each embedding-path kernel family from PMC counters, collected as
+    the microarchitecture guide prescribes: separate `rocprofv3 --pmc` passes for FETCH_SIZE and
     WRITE_SIZE (they do not fit one pass), kernel-filtered, on a short child run of this same
     benchmark (same config, 1 warm-up + 2 steps). Units are KiB; FETCH_SIZE is doubled (the
-    kernel's gathers are 16 B/lane). Must run before this process initialises the GPU."""
+    path's gathers are 16 B/lane). Must run before this process initialises the GPU.
+    Returns ({C-ABI entry: bytes per call}, detail)."""
     import csv
+    import re
     import shutil
     import subprocess
     import tempfile
@@ -102,7 +121,8 @@ def measure_traffic(args):
              str(args.rows), "--dim", str(args.dim), "--slots", str(args.slots), "--optimizer",
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
              str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd,
-             "--mlp-fwd", args.mlp_fwd, "--compare-layerwise", "0", "--tuned-gemms", str(args.tuned_gemms)]
+             "--mlp-fwd", args.mlp_fwd, "--compare-layerwise", "0", "--tuned-gemms",
+             str(args.tuned_gemms)]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -115,23 +135,34 @@ def measure_traffic(args):
                 return None, {"error": f"{counter} pass timed out"}
             if r.returncode != 0:
                 return None, {"error": f"{counter} pass rc={r.returncode}: {r.stderr[-300:]}"}
-            got = []
+            per, calls = {}, {}
             for root, _, files in os.walk(d):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
                         for row in csv.DictReader(open(os.path.join(root, f))):
-                            if row["Counter_Name"] == counter:
-                                got.append(float(row["Counter_Value"]))
-            if not got:
+                            if row["Counter_Name"] != counter:
+                                continue
+                            name = row.get("Kernel_Name", "")
+                            for entry, pat, main in PMC_SYMBOLS:
+                                if re.search(pat, name):
+                                    per[entry] = per.get(entry, 0.0) + float(row["Counter_Value"])
+                                    if main in name:
+                                        calls[entry] = calls.get(entry, 0) + 1
+                                    break
+            if not per:
                 return None, {"error": f"no {counter} rows"}
-            vals[counter] = sum(got) / len(got) * 1024.0  # KiB → bytes, per launch
-    fetch = vals["FETCH_SIZE"] * FETCH_CORRECTION
-    traffic = fetch + vals["WRITE_SIZE"]
-    return traffic, {"fetch_size_bytes_raw": round(vals["FETCH_SIZE"]),
-                     "fetch_correction": FETCH_CORRECTION, "read_bytes": round(fetch),
-                     "write_bytes": round(vals["WRITE_SIZE"]),
-                     "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                               f"--kernel-include-regex {PMC_KERNEL_REGEX}, avg over launches"}
+            # KiB → bytes per call of the C-ABI entry
+            vals[counter] = {k: v * 1024.0 / max(calls.get(k, 1), 1) for k, v in per.items()}
+    out, detail = {}, {}
+    for k in set(vals["FETCH_SIZE"]) | set(vals["WRITE_SIZE"]):
+        rd = vals["FETCH_SIZE"].get(k, 0.0) * FETCH_CORRECTION
+        wr = vals["WRITE_SIZE"].get(k, 0.0)
+        out[k] = rd + wr
+        detail[k] = {"read_bytes": round(rd), "write_bytes": round(wr)}
+    detail["method"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+                        f"--kernel-include-regex {PMC_KERNEL_REGEX}; per call (family total / "
+                        f"launches of its main kernel), FETCH_SIZE x {FETCH_CORRECTION}")
+    return out, detail
 
 
 def init_dist(args):
@@ -187,8 +218,12 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + S * 4 * D + 4 * D)
     if name == "rs_dlrm_interaction_bwd_rank1":  # grad row = G[b] * p: 4 B per example, not 4Z
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 + S * 4 * D + 4 * D)
+    if name == "rs_dlrm_interaction_fwd_head_dx":  # + the unit gradient rows (S + 1 per example)
+        return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + 4 + S * 4 * D + 4 * D)
     if name == "rs_embedding_apply":
         return N * 8 + N * 4 * D + U * 2 * 4 * D
+    if name == "rs_embedding_apply_scaled":  # + G[b], one scale per example
+        return N * 8 + N * 4 * D + U * 2 * 4 * D + B * 4
     if name == "rs_sort_ids":
         return N * id_bytes + N * 8
     return 0
@@ -358,27 +393,37 @@ def main():
                           "algorithmic_bytes": int(by),
                           "achieved_GBs": round(by / (avg * 1e-3) / 1e9, 1),
                           "stream": "side (co-running)" if (name in SIDE_STREAM and (args.fused or world > 1)) else "main"}
-    dom = next((k for k in ROOF_KERNELS if k in kern), None)
-    roof = None
-    if dom:
-        a = kern[dom]["achieved_GBs"]
-        roof = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBS, 4),
-                "traffic": round(traffic) if traffic else None,
-                "algorithmic_bytes": kern[dom]["algorithmic_bytes"],
-                "traffic_detail": traffic_detail}
-    # whole embedding path per SURVEY §8(d): fwd S(id+8D) + bwd S(id+4D) + (U/B)*8D per example
-    emb_names = [n for n in WATCH if n in kern]
-    emb_us = sum(kern[n]["avg_us"] for n in emb_names)
+    # headline roofline: the whole embedding path of SURVEY §8(d) — fwd S(id+8D) + bwd S(id+4D)
+    # + (U/B)·8D bytes per example at the measured U — over the summed in-step event spans of
+    # the path's kernels (the side-stream spans include co-run time with the dense GEMMs)
     per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / args.batch) * 8 * D
-    emb_path = {"kernels": emb_names,
-                "note": "sum of the four kernels' event spans; side-stream spans include co-run "
-                        "time with dense GEMMs, so this is a lower bound on the path's rate",
-                "us_per_step": round(emb_us, 1),
-                "bytes_per_example": round(per_ex, 1),
-                "achieved_GBs": round(per_ex * args.batch / (emb_us * 1e-6) / 1e9, 1) if emb_us else None,
-                "frac_of_peak": round(per_ex * args.batch / (emb_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if emb_us else None,
-                "unique_rows_per_step": U}
+    path_names = [n for n in PATH_KERNELS if n in kern]
+    path_us = sum(kern[n]["avg_us"] for n in path_names)
+    path_bytes = per_ex * args.batch
+    roof = None
+    if path_us:
+        a = path_bytes / (path_us * 1e-6) / 1e9
+        pmc_key = {"rs_embedding_apply_scaled": "rs_embedding_apply"}
+        per_kernel = {}
+        for n in path_names:
+            k = dict(kern[n])
+            k["frac"] = round(k["achieved_GBs"] / HBM_PEAK_GBS, 4)
+            t = (traffic or {}).get(pmc_key.get(n, n))
+            k["traffic"] = round(t) if t is not None else None
+            per_kernel[n] = k
+        tsum = sum(v["traffic"] for v in per_kernel.values()) if traffic and all(
+            v["traffic"] is not None for v in per_kernel.values()) else None
+        dom = max(path_names, key=lambda n: kern[n]["avg_us"])
+        roof = {"bound": "hbm", "kernel": "embedding_path (" + " + ".join(path_names) + ")",
+                "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": tsum,
+                "algorithmic_bytes": int(path_bytes), "us_per_step": round(path_us, 1),
+                "bytes_per_example": round(per_ex, 1), "unique_rows_per_step": U,
+                "dominant_kernel": dom, "per_kernel": per_kernel,
+                "traffic_detail": traffic_detail,
+                "note": "achieved = SURVEY 8(d) path bytes at measured U / the sum of the path "
+                        "kernels' in-step HIP-event spans; traffic = PMC FETCH+WRITE of the same "
+                        "kernels per call"}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_steps > 0:
@@ -405,7 +450,7 @@ def main():
                             "bounds both against a float64 oracle)",
                     "ms_per_step_layerwise_fwd": layerwise_fwd_ms,
                     "ms_per_step_layerwise_fwd_bwd": layerwise_ms},
-            "roofline": roof, "embedding_path": emb_path, "kernels": kern,
+            "roofline": roof, "kernels": kern,
             "cpu_baseline": cpu, "loss": float(loss.item()),
         }
         print(json.dumps(out), flush=True)

@@ -392,28 +392,42 @@ def dlrm_path(iters, out):
         L.call("rs_embedding_apply", L.RS_OPT_SGD, L.ptr(table), None, None, V, D, L.ptr(s0.rows),
                L.ptr(s0.pos), B * S, L.ptr(gemb), prm, None, L.ptr(ws), ws.numel(), st)
 
+    # the production path (fused forward + unit backward, sort, scaled apply)
+    q = torch.randn(480, device=DEV) * 0.05
+    cc = torch.zeros(1, device=DEV)
+    yv = torch.empty(B, 1, device=DEV)
+    G = torch.randn(B, device=DEV) * 1e-3
+
+    def fwd_dx():
+        L.call("rs_dlrm_interaction_fwd_head_dx", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
+               L.ptr(dense), B, L.ptr(inter), 480, L.ptr(q), L.ptr(cc), 2, L.ptr(yv), L.ptr(gemb),
+               L.ptr(gden), L.ptr(err), st)
+
+    def apply_scaled():
+        L.call("rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(table), None, None, V, D,
+               L.ptr(s0.rows), L.ptr(s0.pos), B * S, L.ptr(gemb), L.ptr(G), S, prm, None,
+               L.ptr(ws), ws.numel(), st)
+
     bwd()
+    cfg = {"B": B, "S": S, "D": D, "rows": V, "unique": U}
+    per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
+    tot = 0.0
+    for name, fn in (("rs_dlrm_interaction_fwd_head_dx", fwd_dx), ("rs_sort_ids", srt),
+                     ("rs_embedding_apply_scaled", apply_scaled)):
+        us = timed(fn, iters)
+        tot += us
+        report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
+    report("embedding_path (production: 3 launches back to back, alone)",
+           dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
+    # the previous path (separate re-gathering backward), for the record
     tot = 0.0
     for name, fn in (("rs_dlrm_interaction_fwd", fwd), ("rs_sort_ids", srt),
                      ("rs_dlrm_interaction_bwd", bwd), ("rs_embedding_apply", apply)):
         us = timed(fn, iters)
         tot += us
-        report(name + " (alone)", {"B": B, "S": S, "D": D, "rows": V, "unique": U}, us,
-               kernel_bytes(name, B, S, D, 8, U), out)
-    # what-if: the same apply reading its grad rows in sorted order (contiguous)
-    ident = torch.arange(B * S, dtype=torch.int32, device=DEV)
-
-    def apply_sorted():
-        L.call("rs_embedding_apply", L.RS_OPT_SGD, L.ptr(table), None, None, V, D, L.ptr(s0.rows),
-               L.ptr(ident), B * S, L.ptr(gemb), prm, None, L.ptr(ws), ws.numel(), st)
-
-    us = timed(apply_sorted, iters)
-    report("rs_embedding_apply (grad rows pre-permuted to sorted order, what-if)",
-           {"B": B, "S": S, "D": D, "unique": U}, us, kernel_bytes("rs_embedding_apply", B, S, D, 8, U), out)
-    per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
-    report("embedding_path (4 launches back to back, alone)",
-           {"B": B, "S": S, "D": D, "unique": U, "bytes_per_example": round(per_ex, 1)},
-           tot, per_ex * B, out)
+        report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
+    report("embedding_path (fwd + re-gathering bwd: 4 launches back to back, alone)",
+           dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
 
 
 def chain(iters, out):

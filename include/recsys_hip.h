@@ -134,6 +134,16 @@ int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float* v, int64_
                            int64_t n_ids, const float* grad_out, const rs_adam_params* params,
                            uint32_t* touched_bitmap, void* workspace, size_t ws_bytes,
                            void* stream);
+/* rs_embedding_apply with the gradient of position p read as row_scale[p / scale_group] *
+ * grad_out[p] (one fp32 multiply, rounded before the segmented sum). The fused DLRM step
+ * (rs_dlrm_interaction_fwd_head_dx) hands its unit interaction gradient and the per-example
+ * scale G[b] (scale_group = n_slots); row_scale NULL = rs_embedding_apply. */
+int32_t rs_embedding_apply_scaled(int32_t opt, float* table, float* m, float* v, int64_t n_rows,
+                                  int32_t dim, const uint32_t* sorted_rows,
+                                  const int32_t* sorted_pos, int64_t n_ids, const float* grad_out,
+                                  const float* row_scale, int32_t scale_group,
+                                  const rs_adam_params* params, uint32_t* touched_bitmap,
+                                  void* workspace, size_t ws_bytes, void* stream);
 /* One-call forms (SURVEY §8(b) minimum exports): sort + dedup / sort + apply with one workspace of
  * rs_sparse_workspace_size(n_ids, dim) bytes; bit-identical to the two-call forms. ids[n_ids]
  * (id_dtype RS_ID_I32 / RS_ID_I64; slot = position % n_slots when slot_offsets is given);
@@ -207,6 +217,20 @@ int32_t rs_dlrm_interaction_fwd_head(const float* table, int64_t n_rows, int32_t
                                      int64_t batch, float* out, int64_t out_stride,
                                      const float* q, const float* c, int32_t act, float* y,
                                      int32_t* err_flag, void* stream);
+
+/* rs_dlrm_interaction_fwd_head plus the example's UNIT interaction gradient, formed while the
+ * gathered rows are in registers (ctr/model.py:49-57 forward; its backward for the rank-one
+ * upstream gradient G[b] ⊗ q of the linear top chain, ctr/layers.py:8): with M the strict-upper
+ * pairs of q, dxu_emb[b*S + i] = ((M + Mᵀ)·X[b])[i] for i < S and dxu_dense[b] = ((M + Mᵀ)·X[b])[S]
+ * + q[F(F-1)/2 ..]. The embedding-row gradient is then G[b] * dxu_emb (rs_embedding_apply_scaled)
+ * and the bottom-MLP gradient G[b] * dxu_dense: the backward needs no re-gather. D = 128, F <= 32. */
+int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n_rows, int32_t D,
+                                        const void* ids, int32_t id_dtype, int32_t n_slots,
+                                        const int64_t* slot_offsets, const float* dense,
+                                        int64_t batch, float* out, int64_t out_stride,
+                                        const float* q, const float* c, int32_t act, float* y,
+                                        float* dxu_emb, float* dxu_dense, int32_t* err_flag,
+                                        void* stream);
 
 /* Rank-one upstream gradient (the factored top-MLP backward, recommender_amd/nn.py
  * _LinearChainFn): grad row b = gscale[b] * grad_row[0..width), bit-identical to

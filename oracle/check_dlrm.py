@@ -62,9 +62,10 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     opt = step.opt_sparse
     launch = opt._launch_apply
 
-    def spy(table, ids, grad_rows, sorted_ids):
+    def spy(table, ids, grad_rows, sorted_ids, row_scale=None):
         captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
-        return launch(table, ids, grad_rows, sorted_ids)
+        captured["row_scale"] = row_scale
+        return launch(table, ids, grad_rows, sorted_ids, row_scale)
 
     opt._launch_apply = spy
     try:
@@ -79,6 +80,10 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     p_gpu = step.last_pred.cpu().numpy().astype(np.float64)
     after = W[ut].cpu().numpy()
     g_gpu = captured["grad_rows"].cpu().numpy().reshape(B * S, D)
+    if captured["row_scale"] is not None:
+        # the fused step hands unit rows + G[b]: the apply's row is their one fp32 product
+        sc = captured["row_scale"].cpu().numpy().astype(np.float32)
+        g_gpu = (np.repeat(sc, S)[:, None] * g_gpu).astype(np.float32)
     s_rows = captured["sorted"].rows.cpu().numpy().view(np.uint32).astype(np.int64)
     s_pos = captured["sorted"].pos.cpu().numpy()
     assert np.array_equal(W[pt].cpu().numpy(), probe_before), "an untouched row changed"

@@ -48,6 +48,8 @@ _SIGS = {
     "rs_apply_workspace_size": (_sz, [_i64, _i32]),
     "rs_embedding_apply": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p,
                                   C.POINTER(AdamParams), _p, _p, _sz, _p]),
+    "rs_embedding_apply_scaled": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _p,
+                                         _i32, C.POINTER(AdamParams), _p, _p, _sz, _p]),
     "rs_keras_adam_dense_sweep": (_i32, [_p, _p, _p, _i64, _i32, C.POINTER(AdamParams), _p, _p]),
     "rs_dot_interaction_fwd": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _p, _i64, _p]),
     "rs_dot_interaction_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _i32, _i64, _p, _p]),
@@ -112,6 +114,8 @@ _SIGS = {
                                              _i64, _p, _p, _p]),
     "rs_dlrm_interaction_fwd_head": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p,
                                             _i64, _p, _p, _i32, _p, _p, _p]),
+    "rs_dlrm_interaction_fwd_head_dx": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64,
+                                               _p, _i64, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "rs_chain3_vec_compose": (_i32, [_p, _p, _i32, _p, _p, _p, _p, _p, _i32, _i32, _p, _p, _p,
                                      _sz, _p]),
     "rs_chain_aug_product": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _p]),

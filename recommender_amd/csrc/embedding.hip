@@ -147,6 +147,11 @@ struct ApplyArgs {
   float* partial;         // [n_tiles][2][dim]
   float* chunk;           // [n_tiles][2][dim] level-1 chunk sums of spanning segments
   uint8_t* tile_flags;    // [n_tiles] bit0: head of a spanning segment, bit1: aligned-group lead
+  // grad row of position p = row_scale[p / scale_group] * grad[p] (null: unscaled). The fused
+  // DLRM step hands the UNIT interaction gradient and the per-example scale G[b]; the product is
+  // one rounded fp32 multiply (__fmul_rn, never contracted into the sum), as if materialised.
+  const float* row_scale;
+  int32_t scale_group;
   // OPT_EMIT (dedup output)
   float* uniq_grad;
   uint32_t* uniq_rows;
@@ -258,11 +263,14 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restric
       kk[u] = valid ? keys[k] : 0xFFFFFFFFu;
       int64_t p = valid ? pos[k] : 0;
       bool live = valid && kk[u] < n_rows;
+      const float sc = (a.row_scale && live) ? a.row_scale[p / a.scale_group] : 1.f;
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         int col = (gl + c * lpr) * VEC;
         if (live && col < dim) {
           load_stream<VEC>(grad + p * dim + col, r[u][c]);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) r[u][c][e] = __fmul_rn(sc, r[u][c][e]);
         } else {
 #pragma unroll
           for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
@@ -630,13 +638,36 @@ extern "C" size_t rs_apply_workspace_size(int64_t n_ids, int32_t dim) {
   return align_up(partial_bytes(n_ids, dim), 256) + 256;
 }
 
+extern "C" int32_t rs_embedding_apply_scaled(int32_t opt, float* table, float* m, float* v,
+                                             int64_t n_rows, int32_t dim,
+                                             const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                             int64_t n_ids, const float* grad_out,
+                                             const float* row_scale, int32_t scale_group,
+                                             const rs_adam_params* params,
+                                             uint32_t* touched_bitmap, void* workspace,
+                                             size_t ws_bytes, void* stream);
+
 extern "C" int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float* v, int64_t n_rows,
                                       int32_t dim, const uint32_t* sorted_rows,
                                       const int32_t* sorted_pos, int64_t n_ids,
                                       const float* grad_out, const rs_adam_params* params,
                                       uint32_t* touched_bitmap, void* workspace, size_t ws_bytes,
                                       void* stream) {
+  return rs_embedding_apply_scaled(opt, table, m, v, n_rows, dim, sorted_rows, sorted_pos, n_ids,
+                                   grad_out, nullptr, 1, params, touched_bitmap, workspace,
+                                   ws_bytes, stream);
+}
+
+extern "C" int32_t rs_embedding_apply_scaled(int32_t opt, float* table, float* m, float* v,
+                                             int64_t n_rows, int32_t dim,
+                                             const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                             int64_t n_ids, const float* grad_out,
+                                             const float* row_scale, int32_t scale_group,
+                                             const rs_adam_params* params,
+                                             uint32_t* touched_bitmap, void* workspace,
+                                             size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(!row_scale || scale_group >= 1, "scale_group must be >= 1");
   RS_CHECK_ARG(params, "params is null");
   RS_CHECK_ARG(opt == RS_OPT_SGD || opt == RS_OPT_LAZY_ADAM || opt == RS_OPT_KERAS_ADAM,
                "unknown optimizer %d", opt);
@@ -655,6 +686,8 @@ extern "C" int32_t rs_embedding_apply(int32_t opt, float* table, float* m, float
   a.dim = dim;
   a.p = *params;
   a.bitmap = touched_bitmap;
+  a.row_scale = row_scale;
+  a.scale_group = scale_group;
   a.partial = static_cast<float*>(workspace);
   a.chunk = chunk_of(a.partial, n_ids, dim);
   a.tile_flags = flags_of(a.partial, n_ids, dim);

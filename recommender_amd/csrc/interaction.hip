@@ -108,14 +108,31 @@ struct FwdHead {
   const float* c;  // [1]
   float* y;        // [batch]
   int act;         // 0 linear, 1 relu, 2 sigmoid
+  // DX: the unit interaction backward of the fused step (see below)
+  float* dxu_emb;    // [batch * n_slots, D]
+  float* dxu_dense;  // [batch, D]
+  int dbg;
 };
 
-template <int D, class Src, bool DLRM_OUT, bool HEAD = false>
+// DX (production DLRM step, D = 128): the top MLP is one linear chain into a sigmoid, so the
+// upstream gradient of the interaction row is rank one, G[b] ⊗ Q_0 (G[b] = σ'(y)·dL/dy, a
+// per-example scalar known only after the loss). dX[b] = G[b] · (M + Mᵀ)·X[b] with M the
+// strict-upper Q_0 pairs, a matrix shared by every example. While X[b] is still in registers
+// the wave also forms the UNIT gradient U[b] = (M + Mᵀ)·X[b] (and U[b, S] + Q_0's dense part for
+// the bottom-MLP row); the sparse apply scales each row by G[b] as it reads it. The backward
+// then never re-gathers the 27 table rows of an example (the 872 MB re-read of the separate
+// backward at the north star). (M + Mᵀ)·X runs on v_mfma_f32_16x16x4_f32 per 16-column tile:
+// the X tile is transposed through 2 KB of LDS (the gather layout puts rows on lane % 16, the
+// B operand wants them on lane / 16).
+
+template <int D, class Src, bool DLRM_OUT, bool HEAD = false, bool DX = false>
 __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, int F, InterMode md,
                                                       float* __restrict__ out, int64_t out_stride,
                                                       FwdHead hd = {}) {
   constexpr int NT = D / 16;  // float4 loads per lane per block-row
+  static_assert(!DX || (HEAD && DLRM_OUT && D == 128), "DX is the fused DLRM head path");
   __shared__ float zt[4][32][33];
+  __shared__ __attribute__((aligned(16))) float xtile[DX ? 4 : 1][32][16];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   if (b >= batch) return;
@@ -123,14 +140,41 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   bool oob = false;
   // HEAD: this lane's q entries (compact row: pair o = lane + 64t, dense d = lane + 64t), loaded
   // ahead of the gathers so their latency hides behind the row loads
+  // Every global load of the example is issued before its first store: vmcnt counts loads and
+  // stores in one in-order counter, so a load issued after the row stores would make its wait
+  // drain those stores too.
   constexpr int kHz = HEAD ? 8 : 1, kHd = HEAD ? (D + 63) / 64 : 1;
-  float qz[kHz], qd[kHd];
+  float qz[kHz], qd[kHd], dnv[kHd], cc = 0.f;
   if constexpr (HEAD) {
     const int nzc = F * (F - 1) / 2;
 #pragma unroll
     for (int t = 0; t < kHz; ++t) qz[t] = lane + 64 * t < nzc ? hd.q[lane + 64 * t] : 0.f;
 #pragma unroll
-    for (int t = 0; t < kHd; ++t) qd[t] = lane + 64 * t < D ? hd.q[nzc + lane + 64 * t] : 0.f;
+    for (int t = 0; t < kHd; ++t) {
+      const bool in = lane + 64 * t < D;
+      qd[t] = in ? hd.q[nzc + lane + 64 * t] : 0.f;
+      dnv[t] = in ? src.dense[b * D + lane + 64 * t] : 0.f;
+    }
+    cc = hd.c[0];
+  }
+  // DX: the A operand (M + Mᵀ)[m = 16 ib + r][k = 4 kk + g] of the unit backward, and this
+  // lane's q dense entries for the bottom row's pass-through (column 16 t + r)
+  constexpr int kSa = DX ? 8 : 1, kQn = DX ? NT : 1;
+  float sa[2][kSa], qdn[kQn];
+  if constexpr (DX) {
+    const int nzc = F * (F - 1) / 2;
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int kk = 0; kk < kSa; ++kk) {
+        const int m = 16 * ib + r, k = 4 * kk + g;
+        const bool in = m < F && k < F && m != k;
+        const int o = in ? compact_index(m < k ? m : k, m < k ? k : m, F, 0) : 0;
+        const float v = hd.q[o];  // unconditional (clamped) load, then select
+        sa[ib][kk] = in ? v : 0.f;
+      }
+#pragma unroll
+    for (int t = 0; t < kQn; ++t) qdn[t] = hd.q[nzc + 16 * t + r];
   }
   // lane k < F resolves row k once; the MFMA lanes fetch the pointers by shuffle
   const float* mine = lane < F ? src.row(b, lane, D, oob) : nullptr;
@@ -205,7 +249,7 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
       for (int t = 0; t < kHd; ++t) {
         const int d = lane + 64 * t;
         if (d < D) {
-          const float v = dn[d];
+          const float v = dnv[t];
           od[d] = v;
           hacc += v * qd[t];
         }
@@ -217,13 +261,55 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
       if (lane == 0) {
-        const float v = hacc + hd.c[0];
+        const float v = hacc + cc;
         hd.y[b] = hd.act == 2 ? 1.f / (1.f + expf(-v)) : (hd.act == 1 ? fmaxf(v, 0.f) : v);
       }
     }
     // zero the alignment padding of the row (compact layout padded for the GEMM tiles)
     for (int64_t o = nz + D + lane; o < out_stride; o += 64) orow[o] = 0.f;
     if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+  }
+  if constexpr (DX) {
+    const int S = src.n_slots;
+    if (hd.dbg & 4) return;
+    float(*xt)[16] = xtile[wave];
+    float* de = hd.dxu_emb + b * S * (int64_t)D;
+    float* dd = hd.dxu_dense + b * D;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      // X[:, 16t .. 16t+15] → LDS as [row][col]; read back with the row on lane / 16
+      *reinterpret_cast<float4*>(&xt[r][4 * g]) = a0[t];
+      *reinterpret_cast<float4*>(&xt[16 + r][4 * g]) = a1[t];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      float bv[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) bv[kk] = xt[4 * kk + g][r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // every read done before the next tile's writes
+      __builtin_amdgcn_wave_barrier();
+      floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+      if (hd.dbg & 2) {
+        d0[0] = bv[0]; d0[1] = bv[1]; d0[2] = bv[2]; d0[3] = bv[3];
+        d1[0] = bv[4]; d1[1] = bv[5]; d1[2] = bv[6]; d1[3] = bv[7];
+      } else {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
+      }
+      }
+      if ((hd.dbg & 1) && d0[0] != 1234.5f) continue;
+      // C layout: lane holds U[4g + reg (+16)][16t + r]
+      const int col = 16 * t + r;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
+        if (i0 < S) de[i0 * D + col] = d0[reg];
+        else if (i0 == S) dd[col] = d0[reg] + qdn[t];  // + the concat pass-through
+        if (i1 < S) de[i1 * D + col] = d1[reg];
+        else if (i1 == S) dd[col] = d1[reg] + qdn[t];
+      }
+    }
   }
 }
 
@@ -519,6 +605,224 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
         *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+  }
+  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused forward + unit backward, software-pipelined (the production DLRM step at D = 128,
+// F <= 28): each wave walks `epw` consecutive examples. Per example b:
+//   Z = X·Xᵀ from the gather registers (as inter_fwd_mfma) → X(b) copied to the wave's LDS
+//   region → the registers are refilled with X(b+1) (its loads fly behind everything below)
+//   → z row + fused head y → U = (M + Mᵀ)·X per 16-column tile from LDS on
+//   v_mfma_f32_16x16x4_f32, written back over the tile → U rows stored whole (a half-wave per
+//   512-B row, as the re-gathering backward stored its grad rows).
+// Per-example arithmetic is that of inter_fwd_mfma<…, HEAD, DX> (same MFMA order, same head
+// butterfly): bit-identical z, y, U. Every global load of an iteration is issued before its
+// stores except X(b+1)'s, which only the next iteration waits for (in-order vmcnt).
+// ---------------------------------------------------------------------------------------
+constexpr int kDxLdx = 144;               // X / U row stride in LDS (floats)
+constexpr int kDxRows = 28;               // LDS rows per wave: F <= 28
+constexpr int kDxZt = 32 * 33;            // Z staging
+
+template <bool ID64>
+__global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t batch, int F,
+                                                        float* __restrict__ out,
+                                                        int64_t out_stride, FwdHead hd, int epw) {
+  constexpr int D = 128, NT = 8;
+  __shared__ __attribute__((aligned(16))) float lds[4][kDxRows * kDxLdx + kDxZt];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
+  if (first >= batch) return;
+  const int64_t last = first + epw < batch ? first + epw : batch;
+  const int r = lane & 15, g = lane >> 4;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int S = src.n_slots;
+  const int nzc = F * (F - 1) / 2;
+  float* X = lds[wave];                       // [kDxRows][kDxLdx]: X, then U in place
+  float(*z)[33] = reinterpret_cast<float(*)[33]>(lds[wave] + kDxRows * kDxLdx);
+  // per-wave constants: head q entries, (M + Mᵀ) operand, q's dense part for the bottom row
+  float qz[8], qd[2], sa[2][8], qdn[4];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) qz[t] = lane + 64 * t < nzc ? hd.q[lane + 64 * t] : 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) qd[t] = hd.q[nzc + lane + 64 * t];
+  const float cc = hd.c[0];
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int m = 16 * ib + r, k = 4 * kk + g;
+      const bool in = m < F && k < F && m != k;
+      const float v = hd.q[in ? compact_index(m < k ? m : k, m < k ? k : m, F, 0) : 0];
+      sa[ib][kk] = in ? v : 0.f;
+    }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) qdn[c] = hd.q[nzc + 4 * r32 + c];
+  // this lane's compact outputs o = lane + 64 t read Z[i][j]: the LDS offsets are the same for
+  // every example (computed once; inverting the pair index costs a sqrt and two loops)
+  int zoff[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int o = lane + 64 * t;
+    int i = 0, j = 0;
+    if (o < nzc) compact_pair(o, F, false, i, j);
+    zoff[t] = o < nzc ? i * 33 + j : -1;
+  }
+  // lane i < S owns slot i: its table range is loaded once
+  int64_t lo = 0, n_ok = src.n_rows;
+  if (lane < S && src.slot_offsets) {
+    lo = src.slot_offsets[lane];
+    n_ok = src.slot_offsets[lane + 1] - lo;
+  }
+  bool oob = false;
+  // every memory op of the loop is issued unconditionally (lanes that have nothing to do load
+  // or store a harmless duplicate), so the compiler can count vmcnt exactly across iterations
+  // instead of draining all stores before each example's MFMAs
+  auto raw_id = [&](int64_t b) -> int64_t {
+    const int64_t bb = b < last ? b : first;
+    const int ln = lane < S ? lane : S - 1;
+    const int64_t v = ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + ln]
+                           : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + ln]);
+    return lane < S ? v : 0;
+  };
+  auto row_of = [&](int64_t b, int64_t id) -> const float* {
+    const bool live = b < last;
+    const bool id_ok = id >= 0 && id < n_ok;
+    if (lane < S && !id_ok && live) oob = true;
+    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
+    return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
+  };
+  floatx4 a0[NT], a1[NT];
+  float dnv[2];
+  auto gather = [&](const float* mine, int64_t b) {
+    const float* p0 = shfl_ptr(mine, r);
+    const float* p1 = shfl_ptr(mine, 16 + r);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a0[t] = *(gfloatx4*)(p0 + 4 * g + 16 * t);
+      a1[t] = *(gfloatx4*)(p1 + 4 * g + 16 * t);
+    }
+    const int64_t bb = b < last ? b : first;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) dnv[t] = *(gfloat*)(src.dense + bb * D + lane + 64 * t);
+  };
+  // prologue: X(first) in flight, ids of first+1 in flight
+  gather(row_of(first, raw_id(first)), first);
+  int64_t id_next = raw_id(first + 1);
+  for (int64_t b = first; b < last; ++b) {
+    // lane-derived values are recomputed per example from an opaque lane id: hoisted out of
+    // the loop, the LDS / store offsets would pin ~100 VGPRs for the whole loop
+    int lanev;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
+    const int r = lanev & 15, g = (lanev >> 4) & 3;
+    const int r32 = lanev & 31, h = (lanev >> 5) & 1;
+    const float* nxt = row_of(b + 1, id_next);
+    id_next = raw_id(b + 2);
+    // (1) Z = X·Xᵀ (three 16x16 blocks), as inter_fwd_mfma
+    floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+    if (hd.dbg & 16) { c00 = a0[0]; c01 = a0[1]; c11 = a1[3]; } else
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a0[t][c], c00, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a1[t][c], c01, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
+      }
+    }
+    // (2) X(b) → LDS rows 0..27 (rows >= F are zeros and never read back as U)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      *reinterpret_cast<floatx4*>(&X[r * kDxLdx + 16 * t + 4 * g]) = a0[t];
+      if (16 + r < kDxRows) *reinterpret_cast<floatx4*>(&X[(16 + r) * kDxLdx + 16 * t + 4 * g]) = a1[t];
+    }
+    float dn_cur[2] = {dnv[0], dnv[1]};
+    // (3) the registers are free: X(b+1) loads fly behind the rest of this example
+    __builtin_amdgcn_sched_barrier(0);
+    gather(nxt, b + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // (4) z row + head, as inter_fwd_mfma<…, HEAD>
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i = 4 * g + reg;
+      z[i][r] = c00[reg];
+      z[i][16 + r] = c01[reg];
+      z[16 + r][i] = c01[reg];
+      z[16 + i][16 + r] = c11[reg];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    float* orow = out + b * out_stride;
+    float hacc = 0.f;
+    const int pad = nzc + D;  // first padding column (zero): lanes past the row write it
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int o = lanev + 64 * t;
+      const bool in = zoff[t] >= 0;
+      const float v = in ? (&z[0][0])[zoff[t]] : 0.f;
+      orow[in ? o : pad] = v;
+      hacc += v * qz[t];
+    }
+    float* od = orow + nzc;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int d = lanev + 64 * t;
+      od[d] = dn_cur[t];
+      hacc += dn_cur[t] * qd[t];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
+    {  // every lane holds the same sum: all store the same y[b]
+      const float v = hacc + cc;
+      hd.y[b] = hd.act == 2 ? 1.f / (1.f + expf(-v)) : (hd.act == 1 ? fmaxf(v, 0.f) : v);
+    }
+    {  // zero padding (out_stride - pad <= 64, checked by the launcher)
+      const int o = pad + lanev;
+      orow[o < out_stride ? o : pad] = 0.f;
+    }
+    // (5) U = (M + Mᵀ)·X per 16-column tile, written back over the tile
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float bv[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int k = 4 * kk + g;
+        bv[kk] = k < kDxRows ? X[k * kDxLdx + 16 * t + r] : 0.f;
+      }
+      floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+      if (hd.dbg & 32) { d0[0] = bv[0]; d0[1] = bv[1]; d1[2] = bv[5]; d1[3] = bv[7]; } else
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // this tile's reads are done before it is overwritten
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
+        X[i0 * kDxLdx + 16 * t + r] = d0[reg];
+        if (i1 < kDxRows) X[i1 * kDxLdx + 16 * t + r] = d1[reg];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // (6) U rows: a half-wave per 512-B row
+    float* de = hd.dxu_emb + b * S * (int64_t)D;
+#pragma unroll
+    for (int s2 = 0; s2 < kDxRows / 2; ++s2) {
+      // rows past S are clamped to S: both halves then store the same bottom row
+      const int i = 2 * s2 + h < S ? 2 * s2 + h : S;
+      floatx4 v = *reinterpret_cast<const floatx4*>(&X[i * kDxLdx + 4 * r32]);
+      const bool emb = i < S;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = emb ? v[c] : v[c] + qdn[c];  // + the concat pass-through
+      float* dst = emb ? de + i * D : hd.dxu_dense + b * D;
+      if (!(hd.dbg & 64) || v[0] == 1234.5f) *reinterpret_cast<floatx4*>(dst + 4 * r32) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the next example's writes follow these reads
+    __builtin_amdgcn_wave_barrier();
   }
   if (__any(oob) && lane == 0) flag_oob(src.err_flag);
 }
@@ -897,6 +1201,51 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head(const float* table, int64_t n_ro
   FwdHead hd{q, c, y, act};
   inter_fwd_mfma<128, GatherSrc, true, true>
       <<<ceil_div(batch, 4), 256, 0, as_stream(stream)>>>(src, batch, F, md, out, out_stride, hd);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n_rows, int32_t D,
+                                                   const void* ids, int32_t id_dtype,
+                                                   int32_t n_slots, const int64_t* slot_offsets,
+                                                   const float* dense, int64_t batch, float* out,
+                                                   int64_t out_stride, const float* q,
+                                                   const float* c, int32_t act, float* y,
+                                                   float* dxu_emb, float* dxu_dense,
+                                                   int32_t* err_flag, void* stream) {
+  const int F = n_slots + 1;
+  const InterMode md{0, 0};  // compact row
+  RS_CHECK_ARG(n_slots >= 1 && F <= 32 && D == 128 && batch >= 0,
+               "rs_dlrm_interaction_fwd_head_dx: needs D = 128 and at most 31 slots");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(out_stride >= out_width(F, 0, 0) + D, "out_stride too small");
+  RS_CHECK_ARG(act >= 0 && act <= 2, "bad activation");
+  RS_CHECK_ARG(batch == 0 || (table && ids && dense && out && q && c && y && dxu_emb && dxu_dense),
+               "null pointer");
+  RS_CHECK_ARG(al16(table) && al16(dense), "table and dense must be 16-byte aligned");
+  if (batch == 0) return RS_OK;
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
+  static int dbg = getenv("RS_DX_DEBUG") ? atoi(getenv("RS_DX_DEBUG")) : 0;
+  FwdHead hd{q, c, y, act, dxu_emb, dxu_dense, dbg};
+  hipStream_t st = as_stream(stream);
+  if (F <= kDxRows && out_stride > out_width(F, 0, 0) + D &&
+      out_stride <= out_width(F, 0, 0) + D + 64 && !(dbg & 8)) {
+    auto go = [&](auto kern) {
+      static int epw_cached = 0;
+      static int64_t batch_cached = -1;
+      if (batch != batch_cached) {
+        epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch);
+        batch_cached = batch;
+      }
+      const int epw = epw_cached;
+      kern<<<ceil_div(batch, 4 * (int64_t)epw), 256, 0, st>>>(src, batch, F, out, out_stride, hd, epw);
+    };
+    if (id_dtype == RS_ID_I64) go(dlrm_fwd_dx_pipe<true>);
+    else go(dlrm_fwd_dx_pipe<false>);
+  } else {
+    inter_fwd_mfma<128, GatherSrc, true, true, true>
+        <<<ceil_div(batch, 4), 256, 0, st>>>(src, batch, F, md, out, out_stride, hd);
+  }
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -160,7 +160,13 @@ class _DLRMTopFn(torch.autograd.Function):
     unfused path, or composed into its single affine map, nn.chain_forward). Backward: rs_chain_reduce over the interaction row gives G = σ'(y)·dy [B], A = Zᵀ·G
     and Σ G in one pass; every top-MLP gradient follows from them (nn.chain_param_grads); the
     upstream gradient of the interaction is then the rank-one G ⊗ Q_0 (Q_0 = K_1·K_2·K_3), which
-    rs_dlrm_interaction_bwd_rank1 consumes without materialising the [B, width] rows."""
+    rs_dlrm_interaction_bwd_rank1 consumes without materialising the [B, width] rows.
+
+    Production path (composed head, D = 128): rs_dlrm_interaction_fwd_head_dx forms each
+    example's UNIT interaction gradient (M + Mᵀ)·X[b] (M = the strict-upper pairs of Q_0) while
+    its rows are in registers, so the backward only scales: the embedding rows' gradient is
+    G[b] · unit rows, handed to the fused sparse optimizer as (unit rows, row_scale = G) and
+    multiplied in its walk; the bottom-MLP gradient is G[b] · unit bottom row. No re-gather."""
 
     @staticmethod
     def forward(ctx, handle, dense, table_module, ids, layers, rows, composed=False):
@@ -187,15 +193,22 @@ class _DLRMTopFn(torch.autograd.Function):
                 raise ValueError(f"bottom-MLP output must be [B, {D}], got {tuple(dense.shape)}")
             z = torch.empty(B, width, device=w.device, dtype=torch.float32)
             y = torch.empty(B, 1, device=w.device, dtype=torch.float32)
-            L.call("rs_dlrm_interaction_fwd_head", L.ptr(w), w.shape[0], D, L.ptr(ids),
+            # the unit interaction gradient of every example, formed while its rows are in
+            # registers (rs_dlrm_interaction_fwd_head_dx): the backward scales it by G[b]
+            dxu_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
+            dxu_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
+            L.call("rs_dlrm_interaction_fwd_head_dx", L.ptr(w), w.shape[0], D, L.ptr(ids),
                    L.id_dtype_code(ids), S, L.ptr(table_module.slot_offsets), L.ptr(dense), B,
                    L.ptr(z), width, L.ptr(q), L.ptr(c), layers[-1].act_code, L.ptr(y),
-                   L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+                   L.ptr(dxu_emb), L.ptr(dxu_dense), L.ptr(table_module.err_flag),
+                   L.stream_ptr(w.device))
             ctx.table_module, ctx.ids, ctx.compact = table_module, ids, 1
+            ctx.dxu = (dxu_emb, dxu_dense)
             ks = [l.kernel for l in layers]  # the backward (_chain3_vec_grads) reads rows itself
         else:
             z = _DLRMInteraction.forward(ctx, handle, dense, table_module, ids, True)
             y, ks = chain_forward(z, layers, rows, composed)
+            ctx.dxu = None
         ctx.layers, ctx.rows = layers, rows
         ctx.save_for_backward(dense, z, y, *ks)
         return y
@@ -213,6 +226,17 @@ class _DLRMTopFn(torch.autograd.Function):
         ids = ctx.ids
         B, S = ids.shape
         D = w.shape[1]
+        if ctx.dxu is not None:
+            # rank-one upstream gradient G ⊗ q: every gradient row is G[b] times the unit one
+            dxu_emb, dxu_dense = ctx.dxu
+            ctx.dxu = None
+            grad_dense = G * dxu_dense
+            if getattr(tm, "fused_optimizer", None) is not None:
+                tm.fused_optimizer.apply_async(tm, ids, dxu_emb, tm.take_presorted(ids),
+                                               row_scale=G.reshape(-1))
+            else:
+                tm.accumulate_grad(ids, (G.reshape(B, 1, 1) * dxu_emb.view(B, S, D)).view(B * S, D))
+            return None, grad_dense, None, None, None, None, None
         grad_emb = torch.empty(B * S, D, device=w.device, dtype=torch.float32)
         grad_dense = torch.empty(B, D, device=w.device, dtype=torch.float32)
         p = Q[:, 0].contiguous()

@@ -140,18 +140,23 @@ class SparseOptimizer:
         ids.record_stream(self.side)
         return s
 
-    def apply_async(self, table: Embedding, ids, grad_rows, sorted_ids: SortedIds):
+    def apply_async(self, table: Embedding, ids, grad_rows, sorted_ids: SortedIds, row_scale=None):
+        """row_scale [B] (optional): the gradient row of position p is row_scale[p // S] *
+        grad_rows[p] with S = ids.shape[-1] (the fused DLRM step's unit rows and G[b])."""
         if id(table) in self._applied:
             raise RuntimeError("fused sparse optimizer: a table was looked up twice in one step")
-        self._launch_apply(table, ids, grad_rows, sorted_ids)
+        self._launch_apply(table, ids, grad_rows, sorted_ids, row_scale)
         self._applied.add(id(table))
 
-    def _launch_apply(self, table, ids, grad_rows, sorted_ids):
+    def _launch_apply(self, table, ids, grad_rows, sorted_ids, row_scale=None):
         main = torch.cuda.current_stream(grad_rows.device)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
-            self.apply(table, ids, grad_rows, self._params(), sorted_ids=sorted_ids)
+            self.apply(table, ids, grad_rows, self._params(), sorted_ids=sorted_ids,
+                       row_scale=row_scale)
         grad_rows.record_stream(self.side)
+        if row_scale is not None:
+            row_scale.record_stream(self.side)
 
     def _params(self) -> L.AdamParams:
         lr = self.lr(self.iterations) if callable(self.lr) else self.lr
@@ -161,16 +166,23 @@ class SparseOptimizer:
         return None, None, None
 
     def apply(self, table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor, params,
-              sorted_ids: SortedIds | None = None):
+              sorted_ids: SortedIds | None = None, row_scale: torch.Tensor | None = None):
         dev = table.weight.device
         s = sorted_ids or SortedIds.for_table(table, ids, self.ws, count_unique=False)
         g = grad_rows.contiguous()
         m, v, bitmap = self._slots(table)
         nbytes = L.lib().rs_apply_workspace_size(s.n, table.output_dim)
         w = self.ws.get("apply", nbytes, dev)
-        L.call("rs_embedding_apply", self.kind, L.ptr(table.weight), L.ptr(m), L.ptr(v),
+        group = 1
+        if row_scale is not None:
+            row_scale = row_scale.contiguous()
+            group = ids.shape[-1] if ids.dim() > 1 else s.n // max(row_scale.numel(), 1)
+            if row_scale.numel() * group != s.n:
+                raise ValueError("row_scale must hold one value per example")
+        L.call("rs_embedding_apply_scaled", self.kind, L.ptr(table.weight), L.ptr(m), L.ptr(v),
                table.input_dim, table.output_dim, L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g),
-               params, L.ptr(bitmap), L.ptr(w), w.numel(), L.stream_ptr(dev))
+               L.ptr(row_scale), group, params, L.ptr(bitmap), L.ptr(w), w.numel(),
+               L.stream_ptr(dev))
         if self.kind == L.RS_OPT_KERAS_ADAM:
             L.call("rs_keras_adam_dense_sweep", L.ptr(table.weight), L.ptr(m), L.ptr(v),
                    table.input_dim, table.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))

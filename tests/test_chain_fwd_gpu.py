@@ -140,6 +140,73 @@ def test_interaction_head(id64, oob):
     assert F * (F - 1) // 2 + D <= width
 
 
+@pytest.mark.parametrize("id64,oob,slots", [(True, False, 26), (False, False, 26), (True, True, 26),
+                                            (True, False, 13), (True, False, 31)])
+def test_interaction_head_dx(id64, oob, slots):
+    """rs_dlrm_interaction_fwd_head_dx: row and y bit-identical to rs_dlrm_interaction_fwd_head;
+    the unit gradient U = (M + Mᵀ)·X (M = strict-upper pairs of q) within 1e-5 of float64,
+    relative to |M + Mᵀ|·|X|; the bottom row carries q's dense part; rows are zero for OOB ids;
+    G[b]·U equals the rank-one backward's rows within the same bound."""
+    S, D, B, V = slots, 128, 517, 5000
+    F = S + 1
+    nzc = F * (F - 1) // 2
+    width = (nzc + D + 15) // 16 * 16
+    g = np.random.default_rng(13)
+    table = torch.from_numpy(g.standard_normal((V, D)).astype(np.float32) * 0.1).to(DEV)
+    ids_np = g.integers(0, V, (B, S))
+    if oob:
+        ids_np[7, 3] = V + 5
+        ids_np[100, 0] = -1
+    ids = torch.from_numpy(ids_np.astype(np.int64 if id64 else np.int32)).to(DEV)
+    dense = torch.from_numpy(g.standard_normal((B, D)).astype(np.float32)).to(DEV)
+    q = torch.from_numpy(g.standard_normal(width).astype(np.float32) * 0.05).to(DEV)
+    c = torch.tensor([0.3], device=DEV)
+    st = L.stream_ptr(DEV)
+    code = L.RS_ID_I64 if id64 else L.RS_ID_I32
+    z0, z1 = torch.empty(B, width, device=DEV), torch.empty(B, width, device=DEV)
+    y0, y1 = torch.empty(B, 1, device=DEV), torch.empty(B, 1, device=DEV)
+    f0, f1 = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    ue = torch.full((B * S, D), float("nan"), device=DEV)
+    ud = torch.full((B, D), float("nan"), device=DEV)
+    L.call("rs_dlrm_interaction_fwd_head", L.ptr(table), V, D, L.ptr(ids), code, S, None,
+           L.ptr(dense), B, L.ptr(z0), width, L.ptr(q), L.ptr(c), 2, L.ptr(y0), L.ptr(f0), st)
+    L.call("rs_dlrm_interaction_fwd_head_dx", L.ptr(table), V, D, L.ptr(ids), code, S, None,
+           L.ptr(dense), B, L.ptr(z1), width, L.ptr(q), L.ptr(c), 2, L.ptr(y1), L.ptr(ue),
+           L.ptr(ud), L.ptr(f1), st)
+    assert torch.equal(z0, z1) and torch.equal(y0, y1)
+    assert int(f0) == int(f1) == (1 if oob else 0)
+    # float64 reference
+    tb = table.cpu().numpy().astype(np.float64)
+    ok = (ids_np >= 0) & (ids_np < V)
+    X = np.zeros((B, F, D))
+    X[:, :S][ok] = tb[ids_np[ok]]
+    X[:, S] = dense.cpu().numpy()
+    qn = q.cpu().numpy().astype(np.float64)
+    Msym = np.zeros((F, F))
+    iu = np.triu_indices(F, 1)
+    Msym[iu] = qn[:nzc]
+    Msym = Msym + Msym.T
+    U = np.einsum("ik,bkd->bid", Msym, X)
+    Ub = np.einsum("ik,bkd->bid", np.abs(Msym), np.abs(X))
+    U[:, S] += qn[nzc:nzc + D]
+    Ub[:, S] += np.abs(qn[nzc:nzc + D])
+    got_e = ue.cpu().numpy().reshape(B, S, D)
+    got_d = ud.cpu().numpy()
+    assert np.isfinite(got_e).all() and np.isfinite(got_d).all()
+    assert_close_rel(got_e, U[:, :S], 1e-5, Ub[:, :S], "unit emb grad")
+    assert_close_rel(got_d, U[:, S], 1e-5, Ub[:, S], "unit dense grad")
+    if S == 26 and not oob:
+        # the rank-one backward's rows (G ⊗ q materialised) vs G[b] * U
+        G = torch.from_numpy(g.standard_normal(B).astype(np.float32)).to(DEV)
+        ge, gd = torch.empty(B * S, D, device=DEV), torch.empty(B, D, device=DEV)
+        L.call("rs_dlrm_interaction_bwd_rank1", L.ptr(table), V, D, L.ptr(ids), code, S, None,
+               L.ptr(dense), B, L.ptr(G), L.ptr(q), width, L.ptr(ge), L.ptr(gd), st)
+        Gn = np.abs(G.cpu().numpy().astype(np.float64))
+        scaled = (G.reshape(B, 1, 1) * ue.view(B, S, D)).cpu().numpy()
+        assert_close_rel(scaled, ge.cpu().numpy().reshape(B, S, D), 2e-5,
+                         Gn[:, None, None] * Ub[:, :S], "G * unit vs rank-one rows")
+
+
 @pytest.mark.parametrize("dims,bias", [([13, 512, 256, 128], True), ([13, 64, 32, 16, 8], False),
                                        ([7, 12, 20], True), ([32, 40, 24], True)])
 def test_narrow_chain_backward(dims, bias):
