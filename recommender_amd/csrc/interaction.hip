@@ -111,7 +111,6 @@ struct FwdHead {
   // DX: the unit interaction backward of the fused step (see below)
   float* dxu_emb;    // [batch * n_slots, D]
   float* dxu_dense;  // [batch, D]
-  int dbg;
 };
 
 // DX (production DLRM step, D = 128): the top MLP is one linear chain into a sigmoid, so the
@@ -271,7 +270,6 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
   }
   if constexpr (DX) {
     const int S = src.n_slots;
-    if (hd.dbg & 4) return;
     float(*xt)[16] = xtile[wave];
     float* de = hd.dxu_emb + b * S * (int64_t)D;
     float* dd = hd.dxu_dense + b * D;
@@ -288,17 +286,11 @@ __global__ __launch_bounds__(256) void inter_fwd_mfma(Src src, int64_t batch, in
       __builtin_amdgcn_s_waitcnt(0xc07f);  // every read done before the next tile's writes
       __builtin_amdgcn_wave_barrier();
       floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-      if (hd.dbg & 2) {
-        d0[0] = bv[0]; d0[1] = bv[1]; d0[2] = bv[2]; d0[3] = bv[3];
-        d1[0] = bv[4]; d1[1] = bv[5]; d1[2] = bv[6]; d1[3] = bv[7];
-      } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
       }
-      }
-      if ((hd.dbg & 1) && d0[0] != 1234.5f) continue;
       // C layout: lane holds U[4g + reg (+16)][16t + r]
       const int col = 16 * t + r;
 #pragma unroll
@@ -621,8 +613,10 @@ __global__ __launch_bounds__(256) void dlrm_bwd_pipe(GatherSrc src, int64_t batc
 // butterfly): bit-identical z, y, U. Every global load of an iteration is issued before its
 // stores except X(b+1)'s, which only the next iteration waits for (in-order vmcnt).
 // ---------------------------------------------------------------------------------------
-constexpr int kDxLdx = 144;               // X / U row stride in LDS (floats)
-constexpr int kDxRows = 28;               // LDS rows per wave: F <= 28
+constexpr int kDxLdx = 136;               // X / U row stride in LDS (floats): every LDS
+                                          // access pattern of the loop is at most 2-way
+                                          // bank-conflicted
+constexpr int kDxRows = 28;               // LDS rows per wave: F <= 28 (a multiple of 4)
 constexpr int kDxZt = 32 * 33;            // Z staging
 
 template <bool ID64>
@@ -721,7 +715,6 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
     id_next = raw_id(b + 2);
     // (1) Z = X·Xᵀ (three 16x16 blocks), as inter_fwd_mfma
     floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-    if (hd.dbg & 16) { c00 = a0[0]; c01 = a0[1]; c11 = a1[3]; } else
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
@@ -751,8 +744,7 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
       z[16 + r][i] = c01[reg];
       z[16 + i][16 + r] = c11[reg];
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // Z staging: the reads below follow the writes in issue order
     float* orow = out + b * out_stride;
     float hacc = 0.f;
     const int pad = nzc + D;  // first padding column (zero): lanes past the row write it
@@ -784,21 +776,20 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
     // (5) U = (M + Mᵀ)·X per 16-column tile, written back over the tile
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      float bv[8];
+      // K = the kDxRows = 28 LDS rows (rows >= F are zeros meeting a zero A operand): 7 k-steps
+      constexpr int KK = kDxRows / 4;
+      float bv[KK];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int k = 4 * kk + g;
-        bv[kk] = k < kDxRows ? X[k * kDxLdx + 16 * t + r] : 0.f;
-      }
+      for (int kk = 0; kk < KK; ++kk) bv[kk] = X[(4 * kk + g) * kDxLdx + 16 * t + r];
       floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-      if (hd.dbg & 32) { d0[0] = bv[0]; d0[1] = bv[1]; d1[2] = bv[5]; d1[3] = bv[7]; } else
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
+      for (int kk = 0; kk < KK; ++kk) {
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // this tile's reads are done before it is overwritten
-      __builtin_amdgcn_wave_barrier();
+      // the U tile overwrites the X tile it was computed from: its values depend on every
+      // lane's reads of that tile (through the MFMA), and one wave's LDS operations execute in
+      // issue order, so no wait is needed; the next tile's reads touch other columns
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
@@ -806,8 +797,7 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
         if (i1 < kDxRows) X[i1 * kDxLdx + 16 * t + r] = d1[reg];
       }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // keep the row reads after the U writes (program order)
     // (6) U rows: a half-wave per 512-B row
     float* de = hd.dxu_emb + b * S * (int64_t)D;
 #pragma unroll
@@ -819,10 +809,9 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] = emb ? v[c] : v[c] + qdn[c];  // + the concat pass-through
       float* dst = emb ? de + i * D : hd.dxu_dense + b * D;
-      if (!(hd.dbg & 64) || v[0] == 1234.5f) *reinterpret_cast<floatx4*>(dst + 4 * r32) = v;
+      *reinterpret_cast<floatx4*>(dst + 4 * r32) = v;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // the next example's writes follow these reads
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // the next example's LDS writes follow these reads
   }
   if (__any(oob) && lane == 0) flag_oob(src.err_flag);
 }
@@ -1225,11 +1214,10 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
   RS_CHECK_ARG(al16(table) && al16(dense), "table and dense must be 16-byte aligned");
   if (batch == 0) return RS_OK;
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
-  static int dbg = getenv("RS_DX_DEBUG") ? atoi(getenv("RS_DX_DEBUG")) : 0;
-  FwdHead hd{q, c, y, act, dxu_emb, dxu_dense, dbg};
+  FwdHead hd{q, c, y, act, dxu_emb, dxu_dense};
   hipStream_t st = as_stream(stream);
   if (F <= kDxRows && out_stride > out_width(F, 0, 0) + D &&
-      out_stride <= out_width(F, 0, 0) + D + 64 && !(dbg & 8)) {
+      out_stride <= out_width(F, 0, 0) + D + 64) {
     auto go = [&](auto kern) {
       static int epw_cached = 0;
       static int64_t batch_cached = -1;
