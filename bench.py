@@ -47,12 +47,11 @@ SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_embedding_apply_scaled",
 # device symbols behind each C-ABI entry (for the PMC passes)
 # (entry, device-symbol regex of its kernels, the one kernel every call launches once)
 PMC_SYMBOLS = [
-    ("rs_dlrm_interaction_fwd_head_dx", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, true>",
-     "inter_fwd_mfma"),
+    ("rs_dlrm_interaction_fwd_head_dx", r"dlrm_fwd_dx_pipe", "dlrm_fwd_dx_pipe"),
     ("rs_dlrm_interaction_fwd_head", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, false>",
      "inter_fwd_mfma"),
     ("rs_dlrm_interaction_bwd_rank1", r"dlrm_bwd_pipe", "dlrm_bwd_pipe"),
-    ("rs_sort_ids", r"radix_|make_keys|scan_|count_unique", "make_keys"),
+    ("rs_sort_ids", r"radix_|scan_|count_unique", "radix_hist_kernel<[0-9]+, true>"),
     ("rs_embedding_apply", r"seg_tile|seg_chunk|seg_fixup", "seg_tile"),
 ]
 
@@ -96,7 +95,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = "inter_fwd_mfma|dlrm_bwd_pipe|radix_|make_keys|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
+PMC_KERNEL_REGEX = "inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 
@@ -146,7 +145,7 @@ def measure_traffic(args):
                             for entry, pat, main in PMC_SYMBOLS:
                                 if re.search(pat, name):
                                     per[entry] = per.get(entry, 0.0) + float(row["Counter_Value"])
-                                    if main in name:
+                                    if re.search(main, name):
                                         calls[entry] = calls.get(entry, 0) + 1
                                     break
             if not per:
@@ -227,6 +226,65 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
     if name == "rs_sort_ids":
         return N * id_bytes + N * 8
     return 0
+
+
+def isolated_path(model, ids, iters=10):
+    """The production embedding path's three launches run alone and back to back on the main
+    stream, after the timed region, on the model's own slab, ids and workspaces: the fused
+    gather + interaction + head + unit-backward kernel, the radix sort, the scaled segmented-sum
+    SGD apply with lr 0 (the table does not move; the same bytes are read and written). Each is
+    timed with HIP events over `iters` launches on the stream it is launched on. In the step the
+    sort and the apply run on the side stream beside other kernels, so their in-step event spans
+    include co-run time; these isolated averages are what the roofline divides by."""
+    torch.cuda.synchronize()  # the last step's deferred side-stream update has landed
+    emb = model.embedding_layer
+    w, so, err = emb.weight, emb.slot_offsets, emb.err_flag
+    V, D = w.shape
+    ids = ids.contiguous()
+    B, S = ids.shape
+    dev = w.device
+    st = L.stream_ptr(dev)
+    width = 512
+    nzc = (S + 1) * S // 2 + D
+    g = torch.Generator(device=dev).manual_seed(7)
+    dense = torch.rand(B, D, device=dev, generator=g)
+    q = torch.randn(nzc, device=dev, generator=g) * 0.05
+    cc = torch.zeros(1, device=dev)
+    z = torch.empty(B, width, device=dev)
+    y = torch.empty(B, 1, device=dev)
+    dxu = torch.empty(B * S, D, device=dev)
+    dxd = torch.empty(B, D, device=dev)
+    G = torch.randn(B, device=dev, generator=g) * 1e-3
+    n = B * S
+    rows = torch.empty(n, dtype=torch.int32, device=dev)
+    pos = torch.empty(n, dtype=torch.int32, device=dev)
+    sws = torch.empty(L.lib().rs_sort_ids_workspace_size(n), dtype=torch.uint8, device=dev)
+    aws = torch.empty(L.lib().rs_apply_workspace_size(n, D), dtype=torch.uint8, device=dev)
+    prm = L.AdamParams(0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+    calls = {
+        "rs_dlrm_interaction_fwd_head_dx": lambda: L.call(
+            "rs_dlrm_interaction_fwd_head_dx", L.ptr(w), V, D, L.ptr(ids), L.id_dtype_code(ids), S,
+            L.ptr(so), L.ptr(dense), B, L.ptr(z), width, L.ptr(q), L.ptr(cc), 2, L.ptr(y),
+            L.ptr(dxu), L.ptr(dxd), L.ptr(err), st),
+        "rs_sort_ids": lambda: L.call(
+            "rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(so), S, V, L.ptr(rows),
+            L.ptr(pos), None, L.ptr(err), L.ptr(sws), sws.numel(), st),
+        "rs_embedding_apply_scaled": lambda: L.call(
+            "rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(w), None, None, V, D, L.ptr(rows),
+            L.ptr(pos), n, L.ptr(dxu), L.ptr(G), S, prm, None, L.ptr(aws), aws.numel(), st),
+    }
+    out = {}
+    for name, fn in calls.items():
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = e0.elapsed_time(e1) / iters * 1e3
+    return out
 
 
 def cpu_baseline(args, cards):
@@ -394,27 +452,29 @@ def main():
                           "achieved_GBs": round(by / (avg * 1e-3) / 1e9, 1),
                           "stream": "side (co-running)" if (name in SIDE_STREAM and (args.fused or world > 1)) else "main"}
     # headline roofline: the whole embedding path of SURVEY §8(d) — fwd S(id+8D) + bwd S(id+4D)
-    # + (U/B)·8D bytes per example at the measured U — over the summed in-step event spans of
-    # the path's kernels (the side-stream spans include co-run time with the dense GEMMs)
+    # + (U/B)·8D bytes per example at the measured U — over the summed isolated launch times of
+    # the production path's three kernels (world 1, fused composed-head path)
     per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / args.batch) * 8 * D
-    path_names = [n for n in PATH_KERNELS if n in kern]
-    path_us = sum(kern[n]["avg_us"] for n in path_names)
     path_bytes = per_ex * args.batch
     roof = None
-    if path_us:
+    if world == 1 and D == 128 and args.fused and args.mlp_fwd == "composed":
+        iso = isolated_path(model, pool[0][0])
+        path_us = sum(iso.values())
         a = path_bytes / (path_us * 1e-6) / 1e9
         pmc_key = {"rs_embedding_apply_scaled": "rs_embedding_apply"}
         per_kernel = {}
-        for n in path_names:
-            k = dict(kern[n])
-            k["frac"] = round(k["achieved_GBs"] / HBM_PEAK_GBS, 4)
-            t = (traffic or {}).get(pmc_key.get(n, n))
-            k["traffic"] = round(t) if t is not None else None
-            per_kernel[n] = k
+        for n_, us in iso.items():
+            by = kernel_bytes(n_, args.batch, S, D, 8, U)
+            t = (traffic or {}).get(pmc_key.get(n_, n_))
+            per_kernel[n_] = {"avg_us": round(us, 2), "algorithmic_bytes": int(by),
+                              "achieved_GBs": round(by / (us * 1e-6) / 1e9, 1),
+                              "frac": round(by / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": round(t) if t is not None else None,
+                              "in_step_span_us": kern.get(n_, {}).get("avg_us")}
         tsum = sum(v["traffic"] for v in per_kernel.values()) if traffic and all(
             v["traffic"] is not None for v in per_kernel.values()) else None
-        dom = max(path_names, key=lambda n: kern[n]["avg_us"])
-        roof = {"bound": "hbm", "kernel": "embedding_path (" + " + ".join(path_names) + ")",
+        dom = max(iso, key=iso.get)
+        roof = {"bound": "hbm", "kernel": "embedding_path (" + " + ".join(iso) + ")",
                 "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(a / HBM_PEAK_GBS, 4), "traffic": tsum,
                 "algorithmic_bytes": int(path_bytes), "us_per_step": round(path_us, 1),
@@ -422,8 +482,10 @@ def main():
                 "dominant_kernel": dom, "per_kernel": per_kernel,
                 "traffic_detail": traffic_detail,
                 "note": "achieved = SURVEY 8(d) path bytes at measured U / the sum of the path "
-                        "kernels' in-step HIP-event spans; traffic = PMC FETCH+WRITE of the same "
-                        "kernels per call"}
+                        "kernels' isolated launch times (HIP events, after the timed region, on "
+                        "the model's slab and ids); in_step_span_us = the same kernel's HIP-event "
+                        "span inside the timed steps (side-stream spans include co-run time); "
+                        "traffic = PMC FETCH+WRITE per call"}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_steps > 0:

@@ -430,6 +430,27 @@ def dlrm_path(iters, out):
            dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
 
 
+def sort_only(iters, out):
+    """rs_sort_ids alone at the north-star batch (26 x 65 536 int64 ids over the 40M-row slab),
+    called straight through the C ABI on preallocated buffers (no Python allocation per call)."""
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    S, B, V = 26, 65536, 40_000_000
+    cards = criteo_cardinalities(V, S)
+    so = torch.tensor(np.concatenate([[0], np.cumsum(cards)]), dtype=torch.int64, device=DEV)
+    ids = torch.from_numpy(criteo_batch(np.random.default_rng(4), B, cards)[0]).to(DEV)
+    n = ids.numel()
+    rows = torch.empty(n, dtype=torch.int32, device=DEV)
+    pos = torch.empty(n, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(L.lib().rs_sort_ids_workspace_size(n), dtype=torch.uint8, device=DEV)
+    st = L.stream_ptr(torch.device(DEV))
+    fn = lambda: L.call("rs_sort_ids", L.ptr(ids), 1, n, L.ptr(so), S, V, L.ptr(rows), L.ptr(pos),
+                        None, L.ptr(err), L.ptr(ws), ws.numel(), st)
+    us = timed(fn, iters)
+    report("rs_sort_ids (raw C call)", {"n_ids": n, "rows": V}, us, n * 8 + n * 8, out)
+
+
 def chain(iters, out):
     """rs_chain_reduce at the DLRM MLP shapes (factored backward): the top MLP's GEMV over the
     compact interaction row (n0 480, nl 1, sigmoid) and the bottom MLP's 13 x 128 outer

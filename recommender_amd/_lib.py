@@ -172,7 +172,8 @@ def load(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # RS_LIB: A/B runs of a variant build (recommender_amd/build.py --variant)
+    p = Path(path) if path else Path(os.environ.get("RS_LIB", LIB_PATH))
     if not p.exists():
         raise RecsysError(f"{p} not built: run `python -m recommender_amd.build` "
                           "(or __graft_entry__.build())")

@@ -76,5 +76,32 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     return LIB
 
 
+def build_variant(name: str, flags: list[str]) -> Path:
+    """A/B helper: the whole library rebuilt with extra -D flags into _lib/variants/<name>.so
+    (loaded by setting RS_LIB=<path>; the product path always loads librecsys_hip.so)."""
+    vdir = OUT_DIR / "variants" / name
+    vdir.mkdir(parents=True, exist_ok=True)
+
+    def one(src: Path) -> Path:
+        obj = vdir / (src.stem + ".o")
+        cmd = [HIPCC, *CFLAGS, *flags, "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+        return obj
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        objs = list(ex.map(one, _sources()))
+    out = OUT_DIR / "variants" / f"{name}.so"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return out
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        build(force="--force" in sys.argv)

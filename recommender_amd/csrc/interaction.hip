@@ -715,6 +715,7 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
     id_next = raw_id(b + 2);
     // (1) Z = X·Xᵀ (three 16x16 blocks), as inter_fwd_mfma
     floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+#ifndef RS_AB_NO_ZMFMA
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
@@ -724,6 +725,10 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
         c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
       }
     }
+#else
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { c00 += a0[t]; c01 += a1[t]; }
+#endif
     // (2) X(b) → LDS rows 0..27 (rows >= F are zeros and never read back as U)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -782,11 +787,16 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) bv[kk] = X[(4 * kk + g) * kDxLdx + 16 * t + r];
       floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#ifndef RS_AB_NO_UMFMA
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
       }
+#else
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) { d0[kk & 3] += bv[kk] * sa[0][kk]; d1[kk & 3] += bv[kk] * sa[1][kk]; }
+#endif
       // the U tile overwrites the X tile it was computed from: its values depend on every
       // lane's reads of that tile (through the MFMA), and one wave's LDS operations execute in
       // issue order, so no wait is needed; the next tile's reads touch other columns
@@ -809,6 +819,9 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] = emb ? v[c] : v[c] + qdn[c];  // + the concat pass-through
       float* dst = emb ? de + i * D : hd.dxu_dense + b * D;
+#ifdef RS_AB_NO_USTORE
+      if (v[0] == 12345.f)
+#endif
       *reinterpret_cast<floatx4*>(dst + 4 * r32) = v;
     }
     __builtin_amdgcn_wave_barrier();  // the next example's LDS writes follow these reads

@@ -13,36 +13,12 @@
 namespace rs {
 
 constexpr int kSortThreads = 256;         // 4 waves
-constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile
+#ifndef RS_SORT_KPL
+#define RS_SORT_KPL 16
+#endif
+constexpr int kSortKeysPerLane = RS_SORT_KPL;  // K: keys per lane per tile
 constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
 constexpr int kMaxBins = 512;
-
-// ---- keys from ids ------------------------------------------------------------------
-// world == 1: key = global row. world > 1 (rows dealt cyclically over ranks): owner-major key
-// = (row % world) * shard_stride + row / world, so sorted unique keys come grouped by owner rank
-// with the owner's local row (key % shard_stride) ascending inside each group.
-__global__ void make_keys_kernel(const void* __restrict__ ids, int32_t dtype, int64_t n,
-                                 const int64_t* __restrict__ slot_offsets, int32_t n_slots,
-                                 int64_t n_rows, int32_t world, int64_t shard_stride,
-                                 int64_t key_space, uint32_t* __restrict__ keys,
-                                 int32_t* __restrict__ vals, int32_t* err_flag) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  bool oob = false;
-  for (; i < n; i += stride) {
-    int64_t r = global_row(ids, dtype, i, slot_offsets, n_slots, n_rows);
-    int64_t k;
-    if (r < 0) {
-      oob = true;
-      k = key_space;  // sentinel: sorts after every valid row
-    } else {
-      k = world == 1 ? r : (r % world) * shard_stride + r / world;
-    }
-    keys[i] = static_cast<uint32_t>(k);
-    vals[i] = static_cast<int32_t>(i);
-  }
-  if (__any(oob) && (threadIdx.x & 63) == 0) flag_oob(err_flag);
-}
 
 // match mask: lanes of this wave whose digit equals mine
 template <int BITS>
@@ -61,93 +37,122 @@ __device__ __forceinline__ uint64_t lanemask_lt64() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// Key source of pass 0: either a key array or the ids themselves (key = slot offset + id, made
+// on the fly by the histogram pass, which also stores it for the later passes).
+struct KeyGen {
+  const void* ids;
+  int32_t dtype;
+  const int64_t* slot_offsets;
+  int32_t n_slots;
+  int64_t n_rows;
+  int32_t world;
+  int64_t shard_stride;
+  int64_t key_space;
+  int32_t* err_flag;
+};
+
+__device__ __forceinline__ uint32_t make_key(const KeyGen& g, int64_t i, bool& oob) {
+  const int64_t r = global_row(g.ids, g.dtype, i, g.slot_offsets, g.n_slots, g.n_rows);
+  if (r < 0) {
+    oob = true;
+    return static_cast<uint32_t>(g.key_space);  // sentinel: sorts after every valid row
+  }
+  return static_cast<uint32_t>(g.world == 1 ? r : (r % g.world) * g.shard_stride + r / g.world);
+}
+
 // histogram: hist[digit * n_tiles + tile]. Equal digits inside a wave are aggregated by a
-// ballot match so skewed (Zipf) keys do not serialise on one LDS counter.
-template <int BITS>
+// ballot match so skewed (Zipf) keys do not serialise on one LDS counter. FROM_IDS: pass 0 of
+// an id sort — the keys are made from the ids here and stored to `keys` for the later passes.
+template <int BITS, bool FROM_IDS>
 __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
-    const uint32_t* __restrict__ keys, int64_t n, int shift, int32_t* __restrict__ hist,
+    uint32_t* __restrict__ keys, KeyGen kg, int64_t n, int shift, int32_t* __restrict__ hist,
     int n_tiles) {
   constexpr int BINS = 1 << BITS;
   __shared__ int32_t cnt[BINS];
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) cnt[d] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  int64_t base = (int64_t)blockIdx.x * kSortTile;
-#pragma unroll 4
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  uint32_t kv[kSortKeysPerLane];
+  bool oob = false;
+#pragma unroll
   for (int k = 0; k < kSortKeysPerLane; ++k) {
-    int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
-    bool valid = i < n;
-    uint32_t d = valid ? (keys[i] >> shift) & (BINS - 1) : 0;
-    uint64_t m = match_digit<BITS>(d, valid);
+    const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+    if (FROM_IDS) {
+      kv[k] = i < n ? make_key(kg, i, oob) : 0u;
+      if (i < n) keys[i] = kv[k];
+    } else {
+      kv[k] = i < n ? keys[i] : 0u;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSortKeysPerLane; ++k) {
+    const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t d = (kv[k] >> shift) & (BINS - 1);
+    const uint64_t m = match_digit<BITS>(d, valid);
     // lowest lane of each match group adds the group size
     if (valid && (m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)))) == 0)
       atomicAdd(&cnt[d], __popcll(m));
   }
+  if (FROM_IDS && __any(oob) && lane == 0) flag_oob(kg.err_flag);
   __syncthreads();
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) hist[(int64_t)d * n_tiles + blockIdx.x] = cnt[d];
 }
 
-// single-block exclusive scan, in place (n up to a few 100k): the 1024 threads sweep the
-// array in coalesced 4096-element stripes; a stripe is scanned in LDS and carried forward.
-__global__ __launch_bounds__(1024) void scan_single_block_kernel(int32_t* __restrict__ a, int64_t n,
-                                                                 int32_t* __restrict__ total) {
-  __shared__ int32_t wsum[16];
-  __shared__ int32_t carry_s;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) carry_s = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 4096) {
-    // each thread owns 4 consecutive elements of the stripe
-    int32_t v[4];
-    int64_t i0 = base + (int64_t)t * 4;
+// per-digit scan over the tiles: one wave per digit turns hist[d][*] into its exclusive
+// prefix in place and writes the digit's total (the scatter adds the digit bases itself)
+constexpr int kColChunks = 8;  // tiles per lane per round: 512 tiles in one round
+__global__ __launch_bounds__(256) void radix_colscan_kernel(int32_t* __restrict__ hist, int n_tiles,
+                                                            int bins, int32_t* __restrict__ totals) {
+  const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (d >= bins) return;
+  int32_t* row = hist + (int64_t)d * n_tiles;
+  int32_t carry = 0;
+  for (int base = 0; base < n_tiles; base += 64 * kColChunks) {
+    int32_t v[kColChunks];
+    // lane owns kColChunks consecutive tiles: the loads of a round are issued together
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (i0 + k < n) ? a[i0 + k] : 0;
-    int32_t s = v[0] + v[1] + v[2] + v[3];
-    // inclusive wave scan
+    for (int c = 0; c < kColChunks; ++c) {
+      const int t = base + lane * kColChunks + c;
+      v[c] = t < n_tiles ? row[t] : 0;
+    }
+    int32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < kColChunks; ++c) s += v[c];
     int32_t x = s;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      int32_t y = __shfl_up(x, off);
+      const int32_t y = __shfl_up(x, off);
       if (lane >= off) x += y;
     }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (t < 16) {
-      int32_t ws = wsum[t];
-      int32_t xs = ws;
+    int32_t run = carry + x - s;
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) {
-        int32_t y = __shfl_up(xs, off, 16);
-        if ((t & 15) >= off) xs += y;
-      }
-      wsum[t] = xs - ws;  // exclusive over waves
+    for (int c = 0; c < kColChunks; ++c) {
+      const int t = base + lane * kColChunks + c;
+      if (t < n_tiles) row[t] = run;
+      run += v[c];
     }
-    __syncthreads();
-    int32_t run = carry_s + wsum[w] + x - s;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (i0 + k < n) a[i0 + k] = run;
-      run += v[k];
-    }
-    __syncthreads();
-    if (t == 1023) carry_s = run;
-    __syncthreads();
+    carry += __shfl(x, 63);
   }
-  if (t == 0 && total) *total = carry_s;
+  if (lane == 0) totals[d] = carry;
 }
 
-// stable scatter
-template <int BITS>
+// stable scatter. The digit bases (exclusive scan of the digit totals) are formed per block
+// in LDS. IOTA_VALS: pass 0 of an id sort — the value of key i is its position i.
+template <int BITS, bool IOTA_VALS>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, int64_t n, int shift,
-    const int32_t* __restrict__ hist_scanned, int n_tiles, uint32_t* __restrict__ keys_out,
-    int32_t* __restrict__ vals_out) {
+    const int32_t* __restrict__ hist_scanned, const int32_t* __restrict__ totals, int n_tiles,
+    uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out) {
   constexpr int BINS = 1 << BITS;
   constexpr int WAVES = kSortThreads / 64;
   __shared__ int32_t wcnt[WAVES][BINS];  // per-wave running counts, then per-wave base offsets
+  __shared__ int32_t dbase[BINS];
+  __shared__ int32_t wsum[WAVES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int d = threadIdx.x; d < WAVES * BINS; d += blockDim.x) (&wcnt[0][0])[d] = 0;
-  __syncthreads();
 
   const int64_t base = (int64_t)blockIdx.x * kSortTile + (int64_t)wave * 64 * kSortKeysPerLane;
   uint32_t key[kSortKeysPerLane];
@@ -158,7 +163,35 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     int64_t i = base + k * 64 + lane;
     bool valid = i < n;
     key[k] = valid ? keys_in[i] : 0u;
-    val[k] = valid ? vals_in[i] : 0;
+    val[k] = IOTA_VALS ? static_cast<int32_t>(i) : (valid ? vals_in[i] : 0);
+  }
+  // digit bases: exclusive scan of the totals (BINS <= 512: each thread owns BINS/256 digits)
+  {
+    constexpr int PER = (BINS + kSortThreads - 1) / kSortThreads;
+    int32_t tv[PER];
+    int32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int d = threadIdx.x * PER + c;
+      tv[c] = d < BINS ? totals[d] : 0;
+      s += tv[c];
+    }
+    int32_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int32_t run = x - s;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int d = threadIdx.x * PER + c;
+      if (d < BINS) dbase[d] = run;
+      run += tv[c];
+    }
   }
   const uint64_t lt = lanemask_lt64();
 #pragma unroll
@@ -176,9 +209,9 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  // convert per-wave counts to absolute bases: global tile offset + earlier waves' counts
+  // convert per-wave counts to absolute bases: digit base + earlier tiles + earlier waves
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) {
-    int32_t run = hist_scanned[(int64_t)d * n_tiles + blockIdx.x];
+    int32_t run = dbase[d] + hist_scanned[(int64_t)d * n_tiles + blockIdx.x];
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) {
       int32_t c = wcnt[w][d];
@@ -289,62 +322,61 @@ int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
                            size_t ws_bytes, hipStream_t st);
 size_t exclusive_scan_ws_size(int64_t n);
 
-// workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles], scan scratch
+// workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles], digit totals[BINS]
 static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int32_t** vals_alt,
-                             int32_t** hist, void** scan_ws) {
+                             int32_t** hist, int32_t** totals) {
   int n_tiles = (int)ceil_div(n_ids, kSortTile);
   *keys_alt = c.take<uint32_t>(n_ids);
   *vals_alt = c.take<int32_t>(n_ids);
   *hist = c.take<int32_t>((size_t)kMaxBins * n_tiles + 1);
-  *scan_ws = c.take<char>(exclusive_scan_ws_size((int64_t)kMaxBins * n_tiles + 1));
+  *totals = c.take<int32_t>(kMaxBins);
   return c.off;
 }
 
-template <int BITS>
-static int32_t launch_pass(const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
-                           int64_t n, int shift, int32_t* hist, void* scan_ws, int n_tiles,
-                           hipStream_t st) {
-  radix_hist_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, n, shift, hist, n_tiles);
+// one LSD pass = 3 launches: tile histograms, per-digit scan over tiles, stable scatter
+template <int BITS, bool FIRST_FROM_IDS>
+static int32_t launch_pass(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                           int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
+                           const KeyGen& kg, hipStream_t st) {
+  radix_hist_kernel<BITS, FIRST_FROM_IDS><<<n_tiles, kSortThreads, 0, st>>>(kin, kg, n, shift, hist,
+                                                                            n_tiles);
   RS_CHECK_LAUNCH();
-  const int64_t hn = (int64_t)(1 << BITS) * n_tiles;
-  int32_t s = exclusive_scan_i32(hist, hist, hn, nullptr, scan_ws, exclusive_scan_ws_size(hn), st);
-  if (s) return s;
-  radix_scatter_kernel<BITS><<<n_tiles, kSortThreads, 0, st>>>(kin, vin, n, shift, hist, n_tiles,
-                                                               kout, vout);
+  constexpr int BINS = 1 << BITS;
+  radix_colscan_kernel<<<(BINS + 3) / 4, 256, 0, st>>>(hist, n_tiles, BINS, totals);
+  RS_CHECK_LAUNCH();
+  radix_scatter_kernel<BITS, FIRST_FROM_IDS><<<n_tiles, kSortThreads, 0, st>>>(
+      kin, vin, n, shift, hist, totals, n_tiles, kout, vout);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
 
-static int32_t dispatch_pass(int bits, const uint32_t* kin, const int32_t* vin, uint32_t* kout,
-                             int32_t* vout, int64_t n, int shift, int32_t* hist, void* scan_ws,
-                             int n_tiles, hipStream_t st) {
+template <bool FIRST_FROM_IDS>
+static int32_t dispatch_pass(int bits, uint32_t* kin, const int32_t* vin, uint32_t* kout,
+                             int32_t* vout, int64_t n, int shift, int32_t* hist, int32_t* totals,
+                             int n_tiles, const KeyGen& kg, hipStream_t st) {
+#define RS_PASS(B) \
+  case B: return launch_pass<B, FIRST_FROM_IDS>(kin, vin, kout, vout, n, shift, hist, totals, n_tiles, kg, st);
   switch (bits) {
-    case 1: return launch_pass<1>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 2: return launch_pass<2>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 3: return launch_pass<3>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 4: return launch_pass<4>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 5: return launch_pass<5>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 6: return launch_pass<6>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 7: return launch_pass<7>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 8: return launch_pass<8>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
-    case 9: return launch_pass<9>(kin, vin, kout, vout, n, shift, hist, scan_ws, n_tiles, st);
+    RS_PASS(1) RS_PASS(2) RS_PASS(3) RS_PASS(4) RS_PASS(5) RS_PASS(6) RS_PASS(7) RS_PASS(8) RS_PASS(9)
   }
+#undef RS_PASS
   set_error("radix pass bits %d unsupported", bits);
   return RS_E_UNSUPPORTED;
 }
 
 // Sort (keys, vals) ascending by key (stable); result ends in keys_out/vals_out.
-// keys_in/vals_in are clobbered.
-int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out,
-                         int32_t* vals_out, int64_t n, int64_t n_rows, void* ws, size_t ws_bytes,
-                         hipStream_t st) {
+// keys_in/vals_in are clobbered. kg != null: the keys are made from ids in pass 0 (keys_in is
+// then only scratch and vals are the positions 0..n-1; vals_in is not read).
+static int32_t radix_sort_impl(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out,
+                               int32_t* vals_out, int64_t n, int64_t n_rows, void* ws,
+                               size_t ws_bytes, const KeyGen* kg, hipStream_t st) {
   SortPlan p = plan_sort(n, n_rows);
   Carver c(ws, ws_bytes);
   uint32_t* kalt;
   int32_t* valt;
   int32_t* hist;
-  void* scan_ws;
-  sort_ws_layout(n, c, &kalt, &valt, &hist, &scan_ws);
+  int32_t* totals;
+  sort_ws_layout(n, c, &kalt, &valt, &hist, &totals);
   if (!c.ok()) {
     set_error("sort workspace too small: need %zu have %zu", c.off, ws_bytes);
     return RS_E_WORKSPACE;
@@ -352,11 +384,15 @@ int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out
   // A = (keys_in, vals_in), B = (kalt, valt): A→B→A… and the last pass writes the output
   uint32_t* ka = keys_in;
   int32_t* va = vals_in;
+  const KeyGen none{};
   for (int pass = 0; pass < p.passes; ++pass) {
     bool last = pass == p.passes - 1;
     uint32_t* kb = last ? keys_out : (ka == keys_in ? kalt : keys_in);
     int32_t* vb = last ? vals_out : (va == vals_in ? valt : vals_in);
-    int32_t s = dispatch_pass(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, scan_ws, p.n_tiles, st);
+    int32_t s = (pass == 0 && kg)
+                    ? dispatch_pass<true>(p.bits, ka, va, kb, vb, n, 0, hist, totals, p.n_tiles, *kg, st)
+                    : dispatch_pass<false>(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, totals,
+                                           p.n_tiles, none, st);
     if (s) return s;
     ka = kb;
     va = vb;
@@ -364,13 +400,68 @@ int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out
   return RS_OK;
 }
 
+int32_t radix_sort_pairs(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out,
+                         int32_t* vals_out, int64_t n, int64_t n_rows, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  return radix_sort_impl(keys_in, vals_in, keys_out, vals_out, n, n_rows, ws, ws_bytes, nullptr, st);
+}
+
 size_t radix_sort_ws_size(int64_t n) {
   Carver c(nullptr, 0);
   uint32_t* a;
   int32_t* b;
   int32_t* h;
-  void* w;
-  return sort_ws_layout(n, c, &a, &b, &h, &w) + 256;
+  int32_t* t;
+  return sort_ws_layout(n, c, &a, &b, &h, &t) + 256;
+}
+
+// single-block exclusive scan, in place (n up to a few 100k): the 1024 threads sweep the
+// array in coalesced 4096-element stripes; a stripe is scanned in LDS and carried forward.
+__global__ __launch_bounds__(1024) void scan_single_block_kernel(int32_t* __restrict__ a, int64_t n,
+                                                                 int32_t* __restrict__ total) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry_s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) carry_s = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 4096) {
+    // each thread owns 4 consecutive elements of the stripe
+    int32_t v[4];
+    int64_t i0 = base + (int64_t)t * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (i0 + k < n) ? a[i0 + k] : 0;
+    int32_t s = v[0] + v[1] + v[2] + v[3];
+    // inclusive wave scan
+    int32_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (t < 16) {
+      int32_t ws = wsum[t];
+      int32_t xs = ws;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        int32_t y = __shfl_up(xs, off, 16);
+        if ((t & 15) >= off) xs += y;
+      }
+      wsum[t] = xs - ws;  // exclusive over waves
+    }
+    __syncthreads();
+    int32_t run = carry_s + wsum[w] + x - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < n) a[i0 + k] = run;
+      run += v[k];
+    }
+    __syncthreads();
+    if (t == 1023) carry_s = run;
+    __syncthreads();
+  }
+  if (t == 0 && total) *total = carry_s;
 }
 
 // ---- device-wide exclusive scan of int32 (3-phase) -----------------------------------
@@ -552,11 +643,10 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
     return RS_E_WORKSPACE;
   }
   int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
-  make_keys_kernel<<<blocks, 256, 0, st>>>(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, world,
-                                           shard_stride, key_space, keys, vals, err_flag);
-  RS_CHECK_LAUNCH();
-  int32_t s = radix_sort_pairs(keys, vals, sorted_rows, sorted_pos, n_ids, key_space,
-                               static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, st);
+  // pass 0 makes the keys from the ids (slot offset + id; owner-major when world > 1)
+  const KeyGen kg{ids, id_dtype, slot_offsets, n_slots, n_rows, world, shard_stride, key_space, err_flag};
+  int32_t s = radix_sort_impl(keys, vals, sorted_rows, sorted_pos, n_ids, key_space,
+                              static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, &kg, st);
   if (s) return s;
   if (n_unique) {
     count_unique_kernel<<<std::min(blocks, 512), 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);

@@ -98,6 +98,11 @@ class DLRM(nn.Module):
         int_features = int_features.reshape(-1, self.num_int_fea).float()
         cat_features = cat_features.reshape(-1, self.num_cat_fea)
         pending = None
+        if not hasattr(self.embedding_layer, "exchange_begin"):
+            # the side-stream radix sort of this step's ids is queued first: it then runs beside
+            # the bottom MLP and the interaction kernels (queued after the forward kernels, the
+            # side stream's wait on the main stream would put it behind them)
+            self.embedding_layer.presort(cat_features)
         if hasattr(self.embedding_layer, "exchange_begin"):
             # row-sharded slab: the sort / split-size exchange is queued first (side stream), so
             # it runs beside the bottom MLP; the host waits for the split sizes only after the
@@ -124,8 +129,6 @@ class DLRM(nn.Module):
             else:
                 tmlp_input = self.interact(cat_features, bmlp_activation, compact=True)
                 out = self.top_mlp(tmlp_input, rows=self.compact_rows).squeeze(1)
-        # forward kernels are queued: the side-stream sort now runs beside them
-        self.embedding_layer.presort(cat_features)
         return out
 
     call = forward
