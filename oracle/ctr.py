@@ -145,3 +145,78 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
                       sorted_rows=sr, sorted_pos=sp)
     st.table[u] = st.table[u] - lr * ug
     return loss
+
+
+# ---- DeepFM (ctr/model.py:6-31) with Keras Adam (ctr/train.py:81-84) ------------------------
+
+def keras_adam_dense(w, m, v, g, c):
+    """Keras Adam _resource_apply_dense [3p TF 2.2] in float32, Keras op order:
+    m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g; w -= lr_t*m/(sqrt(v)+eps)."""
+    f32 = np.float32
+    m2 = (m * c["beta1"] + g * c["one_minus_beta1"]).astype(f32)
+    v2 = (v * c["beta2"] + (g * g) * c["one_minus_beta2"]).astype(f32)
+    w2 = (w - (c["lr"] * m2) / (np.sqrt(v2, dtype=f32) + c["epsilon"])).astype(f32)
+    return w2, m2, v2
+
+
+def deepfm_forward(table, cat, dense_in, layers, slot_offsets=None):
+    """ctr/model.py:15-30: FM second-order term on the [B, S, D] lookups (no first-order term,
+    no bias) plus the linear-hidden MLP over [emb.reshape(B, S*D), int features]; sigmoid."""
+    B, S = cat.shape
+    D = table.shape[1]
+    rows = global_rows(cat, table.shape[0], slot_offsets).reshape(B, S)
+    emb = table[rows]                                                # [B, S, D]
+    s = emb.sum(1)
+    fm = np.float32(0.5) * (s * s - (emb * emb).sum(1)).sum(1)       # ctr/model.py:21-23
+    deep = np.concatenate([emb.reshape(B, S * D), dense_in], axis=1)  # ctr/model.py:25-26
+    out, cache = mlp_forward(deep, layers, None)
+    logit = fm + out[:, 0]
+    p = (1.0 / (1.0 + np.exp(-logit))).astype(np.float32)
+    return p, dict(emb=emb, s=s, cache=cache, logit=logit, rows=rows)
+
+
+def deepfm_keras_adam_step(table, m, v, layers, dense_m, dense_v, cat, dense_in, y, step,
+                           lr=1e-3, slot_offsets=None, grad_rows=None):
+    """One DeepFM train step with Keras Adam on every parameter (mean BCE, ctr/train.py:84-85).
+    `step` is 1-based (Keras local_step = iterations + 1). The table update is the sparse
+    Keras apply: duplicates summed in the tiled order of oracle/embedding.segment_sum_tiled,
+    then dense m/v decay and a dense var update of every row. grad_rows (optional, [B*S, D] in
+    position order) replaces the oracle's own table gradient — the checker feeds the kernel's
+    rows to pin the apply bit for bit. Returns (loss, new state dict, detail dict)."""
+    from .embedding import apply_keras_adam, keras_adam_coefficients
+
+    B, S = cat.shape
+    D = table.shape[1]
+    p, c = deepfm_forward(table, cat, dense_in, layers, slot_offsets)
+    loss = float(bce(y, p).mean())
+    dp = bce_grad(y, p)
+    dlogit = (dp * p * (1 - p)).astype(np.float32)
+    ddeep, grads = mlp_backward(dlogit[:, None], layers, c["cache"], None)
+    d_emb = ddeep[:, : S * D].reshape(B, S, D) + dlogit[:, None, None] * (c["s"][:, None, :] - c["emb"])
+    dx = d_emb.reshape(B * S, D).astype(np.float32)
+    co = keras_adam_coefficients(step, lr)
+    new_layers, nm, nv = [], [], []
+    for (k, b), (dk, db), (mk, mb), (vk, vb) in zip(layers, grads, dense_m, dense_v):
+        k2, mk2, vk2 = keras_adam_dense(k, mk, vk, dk.astype(np.float32), co)
+        b2, mb2, vb2 = keras_adam_dense(b, mb, vb, db.astype(np.float32), co)
+        new_layers.append((k2, b2))
+        nm.append((mk2, mb2))
+        nv.append((vk2, vb2))
+    g_use = dx if grad_rows is None else grad_rows
+    sr, sp, _ = sort_ids(cat, table.shape[0], slot_offsets)
+    ur, ug = segment_sum_tiled(sr, sp, g_use, table.shape[0])
+    t2, m2, v2 = apply_keras_adam(table, m, v, ur.astype(np.int64), ug, co)
+    # float64 magnitude bounds: logit (fm + chain) and the table gradient rows
+    a_emb = np.abs(c["emb"]).astype(np.float64)
+    a_s = a_emb.sum(1)
+    fm_b = 0.5 * (a_s * a_s + (a_emb * a_emb).sum(1)).sum(1)
+    chain_b = magnitude_chain(np.abs(c["cache"][0]), layers)[:, 0]
+    q = np.ones((1, 1))
+    for k, _ in reversed(layers):
+        q = np.abs(k).astype(np.float64) @ q
+    ad = np.abs(dlogit).astype(np.float64)
+    dx_b = ad[:, None, None] * (q[: S * D, 0].reshape(1, S, D) + a_s[:, None, :] + a_emb)
+    detail = dict(p=p, logit=c["logit"], logit_bound=fm_b + chain_b, dx=dx,
+                  dx_bound=dx_b.reshape(B * S, D), sorted_rows=sr, sorted_pos=sp,
+                  dense_grads=grads)
+    return loss, dict(table=t2, m=m2, v=v2, layers=new_layers, dense_m=nm, dense_v=nv), detail

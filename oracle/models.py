@@ -1,0 +1,101 @@
+"""Torch-fp32 restatements of the float-only model families (esmm BASE / ESMM / MMOE) and of
+their Keras-Adam train step — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py; parity
+unpinned: the reference's arithmetic is TF 2.2, absent here).
+
+These are plain torch ops (indexing, matmul, activations, autograd) on copies of a model's
+parameters; nothing here calls recommender_amd. References: esmm/layers.py:4-13 (MLP: relu
+hidden layers, `last_activation` on the last), esmm/esmm.py:15-31 (compute_embedding in input
+order, p_ctcvr = p_ctr * p_cvr), esmm/mmoe.py:19-46 (experts relu-last, softmax gates,
+outputs[1] = outputs[0] * outputs[1]), esmm/base.py:14-19, esmm/train.py:97-106 (mean BCE,
+Adam), Keras binary_crossentropy [3p] (clip to [eps, 1-eps], log(p + eps)).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+EPS = 1e-7
+_ACT = {0: lambda x: x, 1: torch.relu, 2: torch.sigmoid}
+
+
+def _leaf(t):
+    return t.detach().clone().requires_grad_(True)
+
+
+def _mlp(mlp):
+    """[(kernel, bias, act)] leaf copies of an esmm MLP's Dense layers."""
+    return [(_leaf(l.kernel), _leaf(l.bias), l.act_code) for l in mlp.mlp]
+
+
+def esmm_family_params(model) -> dict:
+    kind = type(model).__name__
+    if kind == "ESMM":
+        return {"kind": kind, "ctr": _mlp(model.ctr), "cvr": _mlp(model.cvr)}
+    if kind == "BaseModel":
+        return {"kind": kind, "mlp": _mlp(model.mlp)}
+    return {"kind": kind, "experts": [_mlp(e) for e in model.experts],
+            "gates": [(_leaf(g.kernel), _leaf(g.bias)) for g in model.gates],
+            "towers": [_mlp(t) for t in model.task_towers]}
+
+
+def flat_params(P) -> list:
+    """The leaves in the model's named_parameters order (embedding handle excluded)."""
+    out = []
+    if P["kind"] == "ESMM":
+        mlps = [P["ctr"], P["cvr"]]
+    elif P["kind"] == "BaseModel":
+        mlps = [P["mlp"]]
+    else:
+        out_e = [x for m in P["experts"] for k, b, _ in m for x in (k, b)]
+        out_g = [x for g in P["gates"] for x in g]
+        out_t = [x for m in P["towers"] for k, b, _ in m for x in (k, b)]
+        return out_e + out_g + out_t
+    return [x for m in mlps for k, b, _ in m for x in (k, b)]
+
+
+def _run(mlp, x):
+    for k, b, act in mlp:
+        x = _ACT[act](x @ k + b)
+    return x
+
+
+def esmm_family_forward(P, e):
+    """e: [B, F*D] concatenated embeddings (input-dict order). Returns y [B, 2] ([B, 1] BASE)."""
+    if P["kind"] == "ESMM":
+        c, v = _run(P["ctr"], e), _run(P["cvr"], e)
+        return torch.cat([c, c * v], 1)
+    if P["kind"] == "BaseModel":
+        return _run(P["mlp"], e)
+    ex = torch.stack([_run(m, e) for m in P["experts"]], 1)            # [B, E, H]
+    outs = []
+    for (gk, gb), t in zip(P["gates"], P["towers"]):
+        gw = torch.softmax(e @ gk + gb, -1)                           # [B, E]
+        outs.append(_run(t, (gw.unsqueeze(1) @ ex).squeeze(1)))
+    outs[1] = outs[0] * outs[1]
+    return torch.cat(outs, 1)
+
+
+def keras_bce_mean(y, p):
+    pc = p.clamp(EPS, 1 - EPS)
+    return (-(y * torch.log(pc + EPS) + (1 - y) * torch.log(1 - pc + EPS))).mean()
+
+
+def keras_adam_torch(w, m, v, g, c):
+    """Keras Adam on torch tensors in the op order of oracle/ctr.keras_adam_dense."""
+    m2 = m * c["beta1"] + g * c["one_minus_beta1"]
+    v2 = v * c["beta2"] + (g * g) * c["one_minus_beta2"]
+    return w - (m2 * c["lr"]) / (torch.sqrt(v2) + c["epsilon"]), m2, v2
+
+
+def esmm_family_step(model, table, slot_offsets, feats: dict, label):
+    """Loss, dense gradients (flat_params order) and the table's gradient rows [B*F, D] in
+    position order (p = b*F + f) of one esmm-family step, by torch autograd in fp32."""
+    P = esmm_family_params(model)
+    ids = torch.stack([feats[f].reshape(-1).long() for f in feats], 1)   # [B, F]
+    rows = ids + slot_offsets[:-1].to(ids.device)[None, :]
+    E = table[rows].detach().clone().requires_grad_(True)                 # [B, F, D]
+    y = esmm_family_forward(P, E.reshape(E.shape[0], -1))
+    loss = keras_bce_mean(label, y)
+    leaves = flat_params(P)
+    grads = torch.autograd.grad(loss, leaves + [E])
+    return float(loss), y.detach(), list(grads[:-1]), grads[-1].reshape(-1, table.shape[1])

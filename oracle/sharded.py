@@ -11,7 +11,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .embedding import global_rows, segment_sum_tiled, sort_ids
+from .embedding import (apply_keras_adam, apply_lazy_adam, global_rows, keras_adam_coefficients,
+                        segment_sum_tiled, sort_ids)
 
 
 def owner_keys(rows: np.ndarray, n_rows: int, world: int):
@@ -49,3 +50,47 @@ def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_o
         g_rows = ur.astype(np.int64) * world + o
         out[g_rows] = out[g_rows] - lr_w * ug
     return out
+
+
+def sharded_adam_step(full_table, m, v, per_rank_ids, per_rank_grads, world, step, mode,
+                      lr=1e-3, slot_offsets=None):
+    """One sharded lazy / Keras Adam step (recommender_amd/sharded.py backward_exchange): each
+    owner scales the received per-source unique grads by float32(1/W) (world > 1), folds them
+    with the tiled order and applies Adam (coefficients of 1-based `step`) to its shard. Keras
+    mode is dense: every row of every shard decays m / v and moves, including shards that
+    received no row this step. Returns (table, m, v) in full-slab layout."""
+    V, D = full_table.shape
+    stride = -(-V // world)
+    c = keras_adam_coefficients(step, lr)
+    recv = [[] for _ in range(world)]
+    for r in range(world):
+        rows = global_rows(per_rank_ids[r], V, slot_offsets)
+        keys, _, key_space = owner_keys(rows, V, world)
+        order = np.argsort(keys, kind="stable")
+        sk = keys[order].astype(np.uint32)
+        uk, ug = segment_sum_tiled(sk, order.astype(np.int32), per_rank_grads[r], key_space)
+        uk = uk.astype(np.int64)
+        for o in range(world):
+            sel = (uk // stride) == o
+            recv[o].append((uk[sel] - o * stride, ug[sel]))
+    t, m2, v2 = full_table.copy(), m.copy(), v.copy()
+    for o in range(world):
+        g_all = np.arange(o, V, world)  # this owner's global rows, local order
+        local = np.concatenate([x[0] for x in recv[o]])
+        grads = (np.concatenate([x[1] for x in recv[o]]) if local.size
+                 else np.zeros((0, D), np.float32))
+        if world > 1:
+            grads = grads * np.float32(1.0 / world)
+        shard_rows = g_all.size
+        if local.size:
+            sr, sp, _ = sort_ids(local, shard_rows)
+            ur, ug = segment_sum_tiled(sr, sp, grads, shard_rows)
+            ur = ur.astype(np.int64)
+        else:
+            ur, ug = np.zeros(0, np.int64), np.zeros((0, D), np.float32)
+        fn = apply_keras_adam if mode == "keras" else apply_lazy_adam
+        if mode != "keras" and not ur.size:
+            continue
+        ts, ms, vs = fn(t[g_all], m2[g_all], v2[g_all], ur, ug, c)
+        t[g_all], m2[g_all], v2[g_all] = ts, ms, vs
+    return t, m2, v2

@@ -32,11 +32,18 @@ def build(model_type, feat_vocab, embedding_size=18, device="cuda", generator=No
 
 
 class MultiTaskStep:
-    """train_step of esmm/train.py:97-106: y_pred [B,2], mean BCE, Adam."""
+    """train_step of esmm/train.py:97-106: y_pred [B,2], mean BCE, Adam.
 
-    def __init__(self, model, optimizer="keras_adam", lr=1e-3):
+    comm (a recommender_amd.sharded.Comm, world > 1): data parallel over ranks — the dense
+    gradients are all-reduced and averaged before the dense Adam (MirroredStrategy's sync), and a
+    row-sharded slab applies its owners' update with the gradients scaled 1/W inside the backward,
+    so both halves follow the mean loss over the global batch."""
+
+    def __init__(self, model, optimizer="keras_adam", lr=1e-3, comm=None):
         self.model = model
+        self.comm = comm
         dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
+        self.dense = dense
         slab = model.embedding_layer.slab
         table = getattr(slab, "shard", slab)
         if optimizer == "sgd":
@@ -55,6 +62,8 @@ class MultiTaskStep:
         self.last_pred = y.detach()
         loss = binary_crossentropy(label, y, reduction="mean")
         loss.backward()
+        if self.comm is not None and self.comm.world > 1:
+            self._allreduce_dense()
         self.opt_dense.step()
         if self.sharded:
             self.model.embedding_layer.slab.join()
@@ -62,6 +71,14 @@ class MultiTaskStep:
         else:
             self.opt_sparse.step()
         return loss
+
+    def _allreduce_dense(self):
+        grads = [p.grad for p in self.dense if p.grad is not None]
+        flat = torch._utils._flatten_dense_tensors(grads)
+        self.comm.all_reduce_(flat)
+        flat.mul_(1.0 / self.comm.world)
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
 
 
 def train(argv=None):
@@ -79,15 +96,31 @@ def train(argv=None):
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--steps_per_epoch", type=int, default=50)
     ap.add_argument("--optimizer", default="keras_adam", choices=["keras_adam", "lazy_adam", "sgd"])
+    ap.add_argument("--sharded", action="store_true",
+                    help="row-shard the slab over the torch.distributed ranks (RCCL all-to-all; "
+                         "launch one process per GPU with torch.distributed.run)")
     args = ap.parse_args(argv)
+    comm = None
+    if args.sharded:
+        import os
+
+        import torch.distributed as dist
+
+        from ..sharded import Comm
+
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        comm = Comm()
     from ..gemm_tuning import use_tuned_gemms
 
     use_tuned_gemms()  # committed TunableOp GEMM choices for the fixed dense shapes
     torch.manual_seed(args.seed)
     vocab = scaled_vocab(FEAT_VOCAB, args.rows) if args.rows else dict(FEAT_VOCAB)
-    model = build(args.model_type, vocab)
-    step = MultiTaskStep(model, args.optimizer)
-    rng = np.random.default_rng(args.seed)
+    model = build(args.model_type, vocab, sharded_comm=comm)
+    step = MultiTaskStep(model, args.optimizer, comm=comm)
+    rng = np.random.default_rng([args.seed, comm.rank if comm else 0])
     # ctr and ctcvr AUCs over outputs [ctr, ctcvr] (esmm/train.py:58-61, 10000 thresholds)
     ctr_auc = AUC(num_thresholds=args.auc_num_thresholds)
     ctcvr_auc = AUC(num_thresholds=args.auc_num_thresholds)

@@ -240,15 +240,22 @@ class ShardedSlabEmbedding(nn.Module):
             self.comm.all_to_all(recv_grad, uniq_grad[:U], st["recv_counts"], st["send_counts"])
             if self.optimizer is None:
                 raise RuntimeError("ShardedSlabEmbedding has no optimizer (set_optimizer)")
+            opt = self.optimizer
+            params = opt._params()
             if R:
-                opt = self.optimizer
-                params = opt._params()
                 if self.world > 1:
                     if opt.kind == L.RS_OPT_SGD:
                         params.lr = params.lr / self.world  # same as scaling the gradient
                     else:
                         recv_grad.mul_(1.0 / self.world)
                 opt.apply(self.shard, st["recv_rows"], recv_grad, params)
+            elif opt.kind == L.RS_OPT_KERAS_ADAM:
+                # no row of this shard was touched this step: Keras Adam still decays m / v and
+                # moves every row (the dense half of _resource_apply_sparse)
+                m, v, bitmap = opt._slots(self.shard)
+                t = self.shard
+                L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
+                       t.input_dim, t.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
         g.record_stream(self.side)
         self._st = None
 

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import dien as OD
 from recommender_amd.dien.layers import GRU, DIENAttention, InterestEvolve
 from tests.conftest import assert_close_rel
 
@@ -13,42 +14,7 @@ DEV = "cuda"
 RTOL = 2e-5
 
 
-def ref_gru(x, W, U, bias, mask):
-    B, T, X = x.shape
-    H = U.shape[0]
-    h = torch.zeros(B, H, device=x.device)
-    outs = []
-    for t in range(T):
-        xw = x[:, t] @ W + bias[0]
-        inner = h @ U + bias[1]
-        z = torch.sigmoid(xw[:, :H] + inner[:, :H])
-        r = torch.sigmoid(xw[:, H:2 * H] + inner[:, H:2 * H])
-        hh = torch.tanh(xw[:, 2 * H:] + r * inner[:, 2 * H:])
-        hn = z * h + (1 - z) * hh
-        h = torch.where(mask[:, t:t + 1], hn, h)
-        outs.append(h)
-    return torch.stack(outs, 1)
-
-
-def ref_augru(x, a, ku, bu, kr, br, kh, bh, mask):
-    B, T, X = x.shape
-    H = ku.shape[1]
-    h = torch.zeros(B, H, device=x.device)
-    for t in range(T):
-        c = torch.cat([h, x[:, t]], -1)
-        u = torch.sigmoid(c @ ku + bu)
-        r = torch.sigmoid(c @ kr + br)
-        hh = torch.tanh(torch.cat([x[:, t], r * h], -1) @ kh + bh)
-        u = u * a[:, t]
-        hn = u * hh + (1 - u) * h
-        h = torch.where(mask[:, t:t + 1], hn, h)
-    return h
-
-
-def ref_att(target, hs, K, mask):
-    s = (hs @ K) @ target.transpose(1, 2)
-    s = s + (1.0 - mask.unsqueeze(-1).float()) * -1e9
-    return torch.softmax(s, dim=1)
+ref_gru, ref_augru, ref_att = OD.gru, OD.augru, OD.attention
 
 
 def make_mask(rng, B, T):
@@ -61,9 +27,9 @@ def _close(got, ref, name):
     assert_close_rel(got.detach().cpu().numpy(), r, RTOL, np.abs(r).max() + 1e-30, name)
 
 
-@pytest.mark.parametrize("H,X", [(36, 36), (16, 8), (64, 20)])
-def test_gru_fwd_bwd(H, X, rng):
-    B, T = 96, 23
+@pytest.mark.parametrize("H,X,B,T", [(36, 36, 96, 23), (16, 8, 96, 23), (64, 20, 96, 23),
+                                     (36, 36, 512, 100)])
+def test_gru_fwd_bwd(H, X, B, T, rng):
     g = torch.Generator(device="cpu")
     g.manual_seed(0)
     gru = GRU(H, X, device=DEV, generator=g)
@@ -85,9 +51,9 @@ def test_gru_fwd_bwd(H, X, rng):
         _close(got, r, n)
 
 
-@pytest.mark.parametrize("H", [36, 24])
-def test_augru_fwd_bwd(H, rng):
-    B, T, X = 80, 19, H
+@pytest.mark.parametrize("H,B,T", [(36, 80, 19), (24, 80, 19), (36, 512, 100)])
+def test_augru_fwd_bwd(H, B, T, rng):
+    X = H
     ev = InterestEvolve(H, X, device=DEV)
     c = ev.augru
     with torch.no_grad():
@@ -168,11 +134,7 @@ def test_dien_model_forward_and_train_step(rng):
         rep = ref_augru(hid, sc, c.update_gate.kernel, c.update_gate.bias, c.reset_gate.kernel,
                         c.reset_gate.bias, c.hidden_layer.kernel, c.hidden_layer.bias, mask)
         x = torch.cat([tgt.squeeze(1), rep], -1)
-        bn = m.mlp.bn
-        x = (x - bn.moving_mean) * torch.rsqrt(bn.moving_variance + bn.epsilon) * bn.gamma + bn.beta
-        for l in m.mlp.mlp:
-            x = x @ l.kernel + l.bias
-            x = l.activation(x) if l.activation is not None else x
+        x = _mlp_ref(m, x, False)
     _close(prob, x, "dien prob")
     step = DIENStep(m)
     lab = torch.from_numpy(label).to(DEV)
@@ -180,3 +142,100 @@ def test_dien_model_forward_and_train_step(rng):
     for _ in range(5):
         l1 = float(step(feats, lab)[0])
     assert l1 < l0
+
+
+def _dien_models(kind):
+    from recommender_amd.dien import DIEN, DIN, BaseModel
+
+    g = torch.Generator(device=DEV)
+    g.manual_seed(2)
+    kw = dict(item_vocab_size=3001, item_embedding_size=18, cat_vocab_size=81,
+              cat_embedding_size=18, mlp_units=[200, 80, 1], device=DEV, generator=g)
+    if kind == "DIEN":
+        return DIEN(36, 36, **kw)
+    return (DIN if kind == "DIN" else BaseModel)(**kw)
+
+
+def _emb(m, i, c):
+    return torch.cat([m.item_embedding.weight[i.long()], m.cat_embedding.weight[c.long()]], -1)
+
+
+def _mlp_ref(m, x, training):
+    bn = m.mlp.bn
+    if training:
+        mean, var = x.mean(0), x.var(0, unbiased=False)
+    else:
+        mean, var = bn.moving_mean, bn.moving_variance
+    x = OD.batch_norm_inference(x, mean, var, bn.gamma, bn.beta, bn.epsilon)
+    return OD.dense_stack(x, [(l.kernel, l.bias, "relu") for l in m.mlp.mlp[:-1]]
+                          + [(m.mlp.mlp[-1].kernel, m.mlp.mlp[-1].bias, "sigmoid")])
+
+
+@pytest.mark.parametrize("training", [False, True])
+@pytest.mark.parametrize("kind", ["BASE", "DIN"])
+def test_base_din_forward_vs_oracle(kind, training):
+    """BASE (masked history mean, dien/layers.py:5-17) and DIN (unnormalised local activation,
+    dien/layers.py:34-59) through their MLP (BatchNormalization in the mode `training` selects,
+    dien/model.py:30,47) against oracle/dien.py, 2e-5 relative."""
+    from recommender_amd.dien.train import synthetic_batch
+
+    m = _dien_models(kind)
+    feats, _ = synthetic_batch(np.random.default_rng(1), 256, 50, 3001, 81, negatives=False)
+    feats = {k: torch.from_numpy(v).to(DEV) for k, v in feats.items()}
+    with torch.no_grad():
+        prob = m(feats, training=training)
+        mask = feats["pos_his_item"] != 0
+        tgt = _emb(m, feats["target_item"], feats["target_cat"])
+        his = _emb(m, feats["pos_his_item"], feats["pos_his_cat"])
+        if kind == "BASE":
+            rep = OD.his_average(his, mask)
+        else:
+            lau = m.local_activation_unit
+            rep = OD.local_activation(tgt, his, mask, [(lau.layer_1.kernel, lau.layer_1.bias, "sigmoid"),
+                                                       (lau.layer_2.kernel, lau.layer_2.bias, "sigmoid"),
+                                                       (lau.layer_3.kernel, lau.layer_3.bias, None)])
+        ref = _mlp_ref(m, torch.cat([tgt.squeeze(1), rep], -1), training)
+    _close(prob, ref, f"{kind} prob")
+
+
+def test_base_empty_history_is_nan():
+    """The reference's masked mean divides by Σmask: an all-padding history gives 0/0 = NaN
+    (dien/layers.py:14-16), and BASE's probability for that example is NaN; the others stay
+    finite."""
+    from recommender_amd.dien.train import synthetic_batch
+
+    m = _dien_models("BASE")
+    feats, _ = synthetic_batch(np.random.default_rng(1), 16, 20, 3001, 81, negatives=False)
+    feats["pos_his_item"][3] = 0
+    feats["pos_his_cat"][3] = 0
+    feats = {k: torch.from_numpy(v).to(DEV) for k, v in feats.items()}
+    with torch.no_grad():
+        prob = m(feats).cpu().numpy()
+        mask = feats["pos_his_item"] != 0
+        his = _emb(m, feats["pos_his_item"], feats["pos_his_cat"])
+        ref = OD.his_average(his, mask).cpu().numpy()
+    assert np.isnan(ref[3]).all() and np.isnan(prob[3]).all()
+    assert np.isfinite(np.delete(prob, 3, 0)).all()
+
+
+def test_dien_aux_loss_vs_oracle():
+    """DIEN's auxiliary loss (dien/layers.py:89-108) per example against oracle/dien.py from
+    the model's own GRU states: 1e-5 relative (floor 1e-3 of the largest)."""
+    from recommender_amd.dien.train import synthetic_batch
+
+    m = _dien_models("DIEN")
+    feats, _ = synthetic_batch(np.random.default_rng(3), 512, 100, 3001, 81)
+    feats = {k: torch.from_numpy(v).to(DEV) for k, v in feats.items()}
+    with torch.no_grad():
+        _, aux = m(feats)
+        mask = feats["pos_his_item"] != 0
+        pos = _emb(m, feats["pos_his_item"], feats["pos_his_cat"])
+        neg = _emb(m, feats["neg_his_item"], feats["neg_his_cat"])
+        gr = m.interest_extract_layer.gru
+        hid = OD.gru(pos, gr.kernel, gr.recurrent_kernel, gr.bias, mask)
+        an = m.interest_extract_layer.auxiliary_net.layers
+        ref = OD.aux_loss(hid, pos, neg, mask, [(an[0].kernel, an[0].bias, "sigmoid"),
+                                                (an[1].kernel, an[1].bias, "sigmoid"),
+                                                (an[2].kernel, an[2].bias, None)])
+    assert aux.shape == ref.shape == (512,)
+    assert_close_rel(aux.cpu().numpy(), ref.cpu().numpy(), 1e-5, float(ref.abs().max()) * 1e-3, "aux")

@@ -40,7 +40,7 @@ def _ref_forward(model, feats):
 
 
 @pytest.mark.parametrize("kind", ["ESMM", "MMOE", "BASE"])
-def test_esmm_family_forward_and_step(kind):
+def test_esmm_family_forward(kind):
     vocab = {k: min(v, 5000) for k, v in FEAT_VOCAB.items()}
     g = torch.Generator(device=DEV)
     g.manual_seed(3)
@@ -53,12 +53,208 @@ def test_esmm_family_forward_and_step(kind):
         ref = _ref_forward(model, feats)
     assert y.shape == ref.shape
     assert_close_rel(y.cpu().numpy(), ref.cpu().numpy(), 1e-5, 1e-4, "logits")
+
+
+def _tol_check(got, ref, rtol, msg):
+    got, ref = got.detach().cpu().numpy(), ref.detach().cpu().numpy()
+    assert_close_rel(got, ref, rtol, np.abs(ref).max() * 1e-3 + 1e-30, msg)
+
+
+@pytest.mark.parametrize("kind", ["ESMM", "MMOE", "BASE"])
+def test_esmm_family_keras_adam_step_vs_oracle(kind):
+    """One MultiTaskStep (esmm/train.py:97-106, Keras Adam) against oracle/models.py from the
+    same pre-step state: loss 1e-5; outputs 1e-5 (floor 1e-3 of the largest); dense and table
+    gradients 1e-4 relative (floor 1e-3 of the tensor's largest: fp32 reduction order); dense
+    parameters = Keras Adam of the step's own gradients, bit for bit; table / m / v (all rows:
+    Keras Adam is dense) bit-exact vs the oracle's tiled dedup + Keras apply of the kernel's
+    gradient rows."""
+    from oracle import embedding as OE
+    from oracle.models import esmm_family_step, keras_adam_torch
+
+    vocab = {k: min(v, 5000) for k, v in FEAT_VOCAB.items()}
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    model = build(kind, vocab, 18, DEV, g)
     step = MultiTaskStep(model, "keras_adam")
-    w0 = model.embedding_layer.slab.weight.clone()
-    # BASE trains one tower per task (esmm/train.py:14-91): use the click label
+    slab = model.embedding_layer.slab
+    rng = np.random.default_rng(5)
+    f, lab = aliccp_batch(rng, 512, vocab)
+    feats = {k: torch.from_numpy(v).to(DEV) for k, v in f.items()}
     lab_t = torch.from_numpy(lab[:, :1] if kind == "BASE" else lab).to(DEV)
-    l0 = float(step(feats, lab_t))
-    for _ in range(5):
-        l1 = float(step(feats, lab_t))
-    assert l1 < l0
-    assert not torch.equal(w0, model.embedding_layer.slab.weight)
+    table0 = slab.weight.detach().clone()
+    m_t, v_t, _ = step.opt_sparse._slots(slab)
+    m0, v0 = m_t.detach().cpu().numpy().copy(), v_t.detach().cpu().numpy().copy()
+    dense0 = [p.detach().clone() for p in step.dense]
+    ref_loss, ref_y, ref_dg, ref_rows = esmm_family_step(model, table0, slab.slot_offsets, feats, lab_t)
+
+    cap = {}
+    apply = step.opt_sparse.apply
+
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
+        cap["ids"], cap["rows"] = ids, grad_rows
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
+
+    step.opt_sparse.apply = spy
+    loss = float(step(feats, lab_t))
+    torch.cuda.synchronize()
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    assert_close_rel(step.last_pred.cpu().numpy(), ref_y.cpu().numpy(), 1e-5,
+                     float(ref_y.abs().max()) * 1e-3, "outputs")
+    co = OE.keras_adam_coefficients(1)
+    c = {k: float(v) for k, v in co.items()}
+    for i, (p, p0, rg) in enumerate(zip(step.dense, dense0, ref_dg)):
+        _tol_check(p.grad, rg, 1e-4, f"dense grad {i}")
+        want, _, _ = keras_adam_torch(p0, torch.zeros_like(p0), torch.zeros_like(p0), p.grad, c)
+        assert torch.equal(p.detach(), want), f"dense parameter {i} is not Keras Adam of its gradient"
+    rows_gpu = cap["rows"].reshape(-1, 18)
+    _tol_check(rows_gpu, ref_rows, 1e-4, "table gradient rows")
+    so = slab.slot_offsets.cpu().numpy()
+    ids = cap["ids"].cpu().numpy()
+    sr, sp, _ = OE.sort_ids(ids, slab.input_dim, so)
+    ur, ug = OE.segment_sum_tiled(sr, sp, rows_gpu.cpu().numpy(), slab.input_dim)
+    t2, m2, v2 = OE.apply_keras_adam(table0.cpu().numpy(), m0, v0, ur.astype(np.int64), ug, co)
+    np.testing.assert_array_equal(slab.weight.cpu().numpy(), t2)
+    np.testing.assert_array_equal(m_t.cpu().numpy(), m2)
+    np.testing.assert_array_equal(v_t.cpu().numpy(), v2)
+
+
+def _copy_into_sharded(m1, m2, rank=0, world=1):
+    sd = {k: v for k, v in m1.state_dict().items() if not k.startswith("embedding_layer")}
+    m2.load_state_dict(sd, strict=False)
+    full = m1.embedding_layer.slab.weight
+    m2.embedding_layer.slab.shard.weight.copy_(full[rank::world])
+
+
+@pytest.mark.parametrize("opt", ["keras_adam", "lazy_adam"])
+@pytest.mark.parametrize("kind", ["ESMM", "MMOE"])
+def test_world1_sharded_esmm_equals_unsharded(kind, opt):
+    """cfg4's FeatureTables(sharded_comm=...) path at world 1 (owner-major sort, unique / inverse,
+    exchange, owner apply) is bit-identical to the one-slab model over two Adam steps."""
+    from recommender_amd.sharded import Comm
+
+    vocab = {k: min(v, 5000) for k, v in FEAT_VOCAB.items()}
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    m1 = build(kind, vocab, 18, DEV, g)
+    m2 = build(kind, vocab, 18, DEV, torch.Generator(device=DEV).manual_seed(9), sharded_comm=Comm())
+    _copy_into_sharded(m1, m2)
+    s1, s2 = MultiTaskStep(m1, opt), MultiTaskStep(m2, opt, comm=Comm())
+    rng = np.random.default_rng(5)
+    for _ in range(2):
+        f, lab = aliccp_batch(rng, 512, vocab)
+        feats = {k: torch.from_numpy(v).to(DEV) for k, v in f.items()}
+        lab_t = torch.from_numpy(lab).to(DEV)
+        l1, l2 = float(s1(feats, lab_t)), float(s2(feats, lab_t))
+        assert l1 == l2
+    torch.cuda.synchronize()
+    assert torch.equal(m2.embedding_layer.slab.full_weight(), m1.embedding_layer.slab.weight)
+    p2 = dict(m2.named_parameters())
+    for n, a in m1.named_parameters():
+        if not n.endswith("grad_handle"):
+            assert torch.equal(a, p2[n]), n
+
+
+def _esmm_world2_worker(rank, world, port, q, kind, opt):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import embedding as OE
+        from oracle import sharded as OS
+        from oracle.models import esmm_family_step, keras_adam_torch
+        from recommender_amd.sharded import Comm
+
+        vocab = {k: min(v, 3000) for k, v in FEAT_VOCAB.items()}
+        ref = build(kind, vocab, 18, DEV, torch.Generator(device=DEV).manual_seed(3))
+        model = build(kind, vocab, 18, DEV, torch.Generator(device=DEV).manual_seed(9),
+                      sharded_comm=Comm())
+        _copy_into_sharded(ref, model, rank, world)
+        step = MultiTaskStep(model, opt, comm=Comm())
+        slab = model.embedding_layer.slab
+        so_t = slab.slot_offsets
+        so = so_t.cpu().numpy()
+        table = ref.embedding_layer.slab.weight.detach().clone()   # full slab, oracle state
+        t_np = table.cpu().numpy()
+        V, D = t_np.shape
+        m_np = np.zeros((V, D), np.float32)
+        v_np = np.zeros((V, D), np.float32)
+        cap = {}
+        bex = slab.backward_exchange
+
+        def spy(grad_rows):
+            cap["rows"] = grad_rows.detach().cpu().numpy().copy()
+            return bex(grad_rows)
+
+        slab.backward_exchange = spy
+        rng = np.random.default_rng(5)
+        for it in range(2):
+            f, lab = aliccp_batch(rng, 512, vocab)            # the global batch; rank r: half r
+            half = {k: v[rank * 256:(rank + 1) * 256] for k, v in f.items()}
+            feats = {k: torch.from_numpy(v).to(DEV) for k, v in half.items()}
+            lab_t = torch.from_numpy(lab[rank * 256:(rank + 1) * 256]).to(DEV)
+            dense0 = [p.detach().clone() for p in step.dense]
+            st0 = [dict(step.opt_dense.state.get(p, {})) for p in step.dense]
+            st0 = [(s["m"].clone(), s["v"].clone()) if s else None for s in st0]
+            # oracle dense gradients: each half through oracle/models.py, averaged
+            tcur = torch.from_numpy(t_np).to(DEV)
+            gs = []
+            for r in range(world):
+                fr = {k: torch.from_numpy(v[r * 256:(r + 1) * 256]).to(DEV) for k, v in f.items()}
+                lr_ = torch.from_numpy(lab[r * 256:(r + 1) * 256]).to(DEV)
+                gs.append(esmm_family_step(model, tcur, so_t, fr, lr_)[2])
+            step(feats, lab_t)
+            torch.cuda.synchronize()
+            c = {k: float(v) for k, v in OE.keras_adam_coefficients(it + 1).items()}
+            for i, p in enumerate(step.dense):
+                want_g = (gs[0][i] + gs[1][i]) * 0.5
+                _tol_check(p.grad, want_g, 1e-4, f"all-reduced dense grad {i}")
+                m0, v0 = st0[i] if st0[i] is not None else (torch.zeros_like(p), torch.zeros_like(p))
+                want, _, _ = keras_adam_torch(dense0[i], m0, v0, p.grad, c)
+                assert torch.equal(p.detach(), want), f"dense parameter {i}"
+            # sparse: the oracle's sharded Adam from every rank's own gradient rows
+            ids = np.stack([half[k].reshape(-1) for k in half], 1).astype(np.int64)
+            all_ids = [None] * world
+            all_rows = [None] * world
+            dist.all_gather_object(all_ids, ids)
+            dist.all_gather_object(all_rows, cap["rows"].reshape(-1, D))
+            t_np, m_np, v_np = OS.sharded_adam_step(t_np, m_np, v_np, all_ids, all_rows, world,
+                                                    it + 1, "keras" if opt == "keras_adam" else "lazy",
+                                                    1e-3, so)
+            full = slab.full_weight().cpu().numpy()
+            np.testing.assert_array_equal(full, t_np)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("opt", ["keras_adam", "lazy_adam"])
+def test_world2_sharded_esmm_matches_oracle(opt):
+    """SURVEY cfg4 on two ranks sharing the one GPU (gloo, exchange staged through the host):
+    two MultiTaskStep(comm=...) steps of a row-sharded ESMM. The all-reduced dense gradients
+    match the mean of oracle/models.py's half-batch gradients (1e-4), the dense parameters are
+    Keras Adam of them bit for bit, and the sharded slab equals oracle/sharded.py's sharded Adam
+    of the ranks' own gradient rows bit for bit."""
+    import os
+
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29300 + (os.getpid() % 500) + (7 if opt == "lazy_adam" else 0)
+    ps = [ctx.Process(target=_esmm_world2_worker, args=(r, world, port, q, "ESMM", opt))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res

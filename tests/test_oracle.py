@@ -141,3 +141,41 @@ def test_golden_interaction():
                                        f[f"gx_{si}{sg}"], rtol=1e-12)
     np.testing.assert_allclose(OI.fm(f["fm_e"]), f["fm_out"], rtol=1e-12)
     np.testing.assert_allclose(OI.fm_bwd(f["fm_e"], f["fm_g"]), f["fm_ge"], rtol=1e-12)
+
+
+def test_deepfm_oracle_fm_pairs_and_table_gradient():
+    """oracle/ctr.py DeepFM: the FM term is the sum of the distinct pair dot products
+    (ctr/model.py:21-23), and the table gradient rows match float64 finite differences of the
+    mean BCE loss."""
+    from oracle.ctr import bce, deepfm_forward, deepfm_keras_adam_step
+
+    rng = np.random.default_rng(0)
+    V, D, B, S = 40, 4, 6, 5
+    t = rng.standard_normal((V, D)).astype(np.float32) * 0.3
+    cat = rng.integers(0, V, (B, S))
+    dn = rng.standard_normal((B, 3)).astype(np.float32)
+    y = (rng.random(B) < 0.5).astype(np.float32)
+    layers = [(rng.standard_normal((S * D + 3, 7)).astype(np.float32) * 0.1, np.zeros(7, np.float32)),
+              (rng.standard_normal((7, 1)).astype(np.float32) * 0.1, np.full(1, 0.1, np.float32))]
+    p, c = deepfm_forward(t, cat, dn, layers)
+    e = t[cat].astype(np.float64)
+    fm = sum((e[:, i] * e[:, j]).sum(1) for i in range(S) for j in range(i + 1, S))
+    np.testing.assert_allclose(c["logit"], fm + c["cache"][-1][:, 0], rtol=1e-5, atol=1e-6)
+    zeros = [(np.zeros_like(k), np.zeros_like(b)) for k, b in layers]
+    _, _, det = deepfm_keras_adam_step(t, np.zeros_like(t), np.zeros_like(t), layers, zeros, zeros,
+                                       cat, dn, y, 1)
+    b0, s0 = 2, 3
+    h = 1e-3
+    t64 = t.astype(np.float64)
+
+    def loss_at(delta):
+        tt = t64.copy()
+        tt[cat[b0, s0], 1] += delta
+        pp, _ = deepfm_forward(tt, cat, dn.astype(np.float64), [(k.astype(np.float64), bb.astype(np.float64)) for k, bb in layers])
+        return bce(y.astype(np.float64), pp).mean()
+
+    fd = (loss_at(h) - loss_at(-h)) / (2 * h)
+    # the row's gradient is the sum over every position that looks it up
+    occ = np.flatnonzero(cat.reshape(-1) == cat[b0, s0])
+    got = det["dx"][occ, 1].astype(np.float64).sum()
+    np.testing.assert_allclose(got, fd, rtol=2e-3, atol=1e-7)

@@ -51,7 +51,7 @@ def _sharded_vs_unsharded(D, criteo_cardinalities, criteo_batch, DLRM, TrainStep
     np.testing.assert_array_equal(emb.full_weight().cpu().numpy(), m1.embedding_layer.weight.cpu().numpy())
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, opt="sgd", even=False):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -60,31 +60,50 @@ def _worker(rank, world, port, q):
     try:
         from oracle import embedding as OE
         from oracle import sharded as OS
-        from recommender_amd.optim import SparseSGD
+        from recommender_amd.optim import SparseAdam, SparseSGD
         from recommender_amd.sharded import Comm, ShardedSlabEmbedding
 
-        card = [5, 1, 700, 3000, 40]
+        # even=True: every slot has an even cardinality and offset and every id is even, so all
+        # global rows are even and rank 1 (owner of the odd rows) receives no row at all
+        card = [6, 2, 700, 3000, 40] if even else [5, 1, 700, 3000, 40]
         D, B = 16, 900
         V = sum(card)
         so = np.concatenate([[0], np.cumsum(card)]).astype(np.int64)
         table = np.random.default_rng(9).standard_normal((V, D)).astype(np.float32)
         emb = ShardedSlabEmbedding(card, D, Comm(), device=DEV, full_weight=torch.from_numpy(table))
-        emb.set_optimizer(SparseSGD([emb.shard], lr=0.05))
-        per_ids, per_g = [], []
-        for rr in range(world):
-            rg = np.random.default_rng(100 + rr)
-            ids = np.stack([np.minimum(rg.zipf(1.1, B) - 1, c - 1) for c in card], 1).astype(np.int64)
-            per_ids.append(ids)
-            per_g.append(rg.standard_normal((ids.size, D)).astype(np.float32))
-        ids_t = torch.from_numpy(per_ids[rank]).to(DEV)
-        out = emb(ids_t)
-        np.testing.assert_array_equal(out.detach().cpu().numpy(), OE.embedding_lookup(table, per_ids[rank], so))
-        out.backward(torch.from_numpy(per_g[rank]).to(DEV).view(out.shape))
-        emb.join()
-        full = emb.full_weight().cpu().numpy()
-        if rank == 0:
-            ref = OS.sharded_sgd_step(table, per_ids, per_g, 0.05, world, so)
-            np.testing.assert_array_equal(full, ref)
+        if opt == "sgd":
+            sopt = SparseSGD([emb.shard], lr=0.05)
+        else:
+            sopt = SparseAdam([emb.shard], lr=1e-3, mode=opt)
+        emb.set_optimizer(sopt)
+        m = np.zeros((V, D), np.float32)
+        v = np.zeros((V, D), np.float32)
+        t_ref = table
+        for step in range(2 if opt != "sgd" else 1):
+            per_ids, per_g = [], []
+            for rr in range(world):
+                rg = np.random.default_rng(100 + rr + 10 * step)
+                ids = np.stack([np.minimum(rg.zipf(1.1, B) - 1, c - 1) for c in card], 1).astype(np.int64)
+                if even:
+                    ids = ids - ids % 2
+                per_ids.append(ids)
+                per_g.append(rg.standard_normal((ids.size, D)).astype(np.float32))
+            ids_t = torch.from_numpy(per_ids[rank]).to(DEV)
+            out = emb(ids_t)
+            np.testing.assert_array_equal(out.detach().cpu().numpy(),
+                                          OE.embedding_lookup(t_ref, per_ids[rank], so))
+            out.backward(torch.from_numpy(per_g[rank]).to(DEV).view(out.shape))
+            emb.join()
+            sopt.iterations += 1
+            if opt == "sgd":
+                t_ref = OS.sharded_sgd_step(t_ref, per_ids, per_g, 0.05, world, so)
+            else:
+                t_ref, m, v = OS.sharded_adam_step(t_ref, m, v, per_ids, per_g, world, step + 1,
+                                                   opt, 1e-3, so)
+            full = emb.full_weight().cpu().numpy()
+            np.testing.assert_array_equal(full, t_ref)
+        if even and opt == "keras":
+            assert np.all(full[1::2] != table[1::2])  # rank 1's untouched shard still moved
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover
         import traceback
@@ -94,14 +113,19 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_world2_sharded_embedding_matches_oracle():
+@pytest.mark.parametrize("opt,even", [("sgd", False), ("lazy", False), ("keras", False),
+                                      ("keras", True)])
+def test_world2_sharded_embedding_matches_oracle(opt, even):
+    """Two ranks on the one GPU (gloo staged exchange): lookups, the owner-side SGD / lazy Adam /
+    Keras Adam apply (grads x 1/W) bit-exact vs oracle/sharded.py; `even`: rank 1 owns no row of
+    the batch and its shard still takes Keras Adam's dense update."""
     import torch.multiprocessing as mp
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29700 + (os.getpid() % 1000)
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 29700 + (os.getpid() % 500) + 17 * ["sgd", "lazy", "keras"].index(opt) + (3 if even else 0)
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, opt, even)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
