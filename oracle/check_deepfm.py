@@ -49,22 +49,22 @@ def checked_deepfm_adam_step(model, step, cat, dn, lb) -> dict:
     it = opt.iterations + 1
 
     captured = {}
-    launch = opt._launch_apply
+    apply = opt.apply  # both the fused (side-stream) and the step()-time apply go through it
 
-    def spy(table, ids, grad_rows, sorted_ids, row_scale=None):
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
         captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
-        return launch(table, ids, grad_rows, sorted_ids, row_scale)
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
 
-    opt._launch_apply = spy
+    opt.apply = spy
     try:
         batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
                  torch.from_numpy(lb).to(dev))
         loss = float(step(batch).detach())
     finally:
-        opt._launch_apply = launch
+        del opt.apply
     emb.wait_update()
     torch.cuda.synchronize()
-    assert "grad_rows" in captured, "the fused sparse apply did not run"
+    assert "grad_rows" in captured, "the sparse apply did not run"
     g_gpu = captured["grad_rows"].cpu().numpy().reshape(B * S, D).astype(np.float32)
     p_gpu = step.last_pred.cpu().numpy().astype(np.float64)
 
@@ -78,10 +78,11 @@ def checked_deepfm_adam_step(model, step, cat, dn, lb) -> dict:
     ztol = 1e-5 * np.abs(z_ref) + 1e-6 * det["logit_bound"] + res
     zerr = np.abs(z_gpu - z_ref)
     assert (zerr <= ztol).all(), f"logits: max err/tol {(zerr / ztol).max():.3g}"
-    s_rows = captured["sorted"].rows.cpu().numpy().view(np.uint32).astype(np.int64)
-    s_pos = captured["sorted"].pos.cpu().numpy()
-    assert np.array_equal(det["sorted_rows"].astype(np.int64), s_rows), "sorted rows differ"
-    assert np.array_equal(det["sorted_pos"], s_pos), "sorted positions differ"
+    if captured["sorted"] is not None:  # the fused path's side-stream radix sort
+        s_rows = captured["sorted"].rows.cpu().numpy().view(np.uint32).astype(np.int64)
+        s_pos = captured["sorted"].pos.cpu().numpy()
+        assert np.array_equal(det["sorted_rows"].astype(np.int64), s_rows), "sorted rows differ"
+        assert np.array_equal(det["sorted_pos"], s_pos), "sorted positions differ"
     gerr = np.abs(g_gpu.astype(np.float64) - det["dx"])
     gtol = 1e-5 * det["dx_bound"] + 1e-38
     assert (gerr <= gtol).all(), f"grad rows: max err/bound {(gerr / gtol).max():.3g}"
@@ -93,8 +94,15 @@ def checked_deepfm_adam_step(model, step, cat, dn, lb) -> dict:
                             ("v", _np(v_t), pinned["v"])):
         bad = got != want
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.size} elements differ from the oracle apply"
-    changed = float((_np(W) != table0).mean())
-    assert changed > 0.99, f"Keras Adam moves every row; only {changed:.2%} changed"
+    moved = _np(W) != table0
+    touched = np.unique(det["sorted_rows"].astype(np.int64))
+    changed = float(moved[touched].mean())
+    assert changed >= 0.25, f"only {changed:.2%} of touched elements changed: vacuous check"
+    # the dense half: every row with momentum from earlier steps moves, touched or not
+    carried = (m0 != 0).any(1)
+    if carried.any():
+        frac = float(moved[carried].any(1).mean())
+        assert frac > 0.99, f"Keras Adam's dense update moved only {frac:.2%} of rows with momentum"
     derr = 0.0
     for l, (k0, b0), (k1, b1) in zip(model.mlp.mlp, layers0, ref["layers"]):
         for got, before, want in ((_np(l.kernel), k0, k1), (_np(l.bias), b0, b1)):
@@ -104,4 +112,5 @@ def checked_deepfm_adam_step(model, step, cat, dn, lb) -> dict:
             derr = max(derr, float((e / tol).max()))
     return {"loss": loss, "oracle_loss": ref_loss, "logit_err_over_tol": float((zerr / ztol).max()),
             "grad_err_over_bound": float((gerr / gtol).max()), "dense_err_over_tol": derr,
-            "table_elements_changed": changed}
+            "touched_elements_changed": changed,
+            "rows_with_momentum": int((m0 != 0).any(1).sum())}

@@ -98,4 +98,4 @@ def esmm_family_step(model, table, slot_offsets, feats: dict, label):
     loss = keras_bce_mean(label, y)
     leaves = flat_params(P)
     grads = torch.autograd.grad(loss, leaves + [E])
-    return float(loss), y.detach(), list(grads[:-1]), grads[-1].reshape(-1, table.shape[1])
+    return float(loss.detach()), y.detach(), list(grads[:-1]), grads[-1].reshape(-1, table.shape[1])
