@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ..functional import binary_crossentropy
-from ..nn import overlapped_param_grads, overlapped_weight_grads
+from ..nn import invalidate_compose_cache, overlapped_param_grads, overlapped_weight_grads
 from ..metrics import AUC
 from ..optim import DLRMScheduler, KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import criteo_batch, criteo_cardinalities
@@ -94,13 +94,17 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        invalidate_compose_cache()  # the graph must record the compositions it reads
         with torch.cuda.graph(g):
             loss = self(batch)
+        invalidate_compose_cache()
         self._graph_loss = loss
         self.opt_sparse.defer_join = defer
 
         def replay():
             g.replay()
+            # the replay moved the parameters in place (no version bump): eager steps recompose
+            invalidate_compose_cache()
             return loss
 
         return replay
@@ -129,15 +133,18 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        invalidate_compose_cache()
         with torch.cuda.graph(g):
             for b in batches:
                 loss = self(b)
             for t in self.opt_sparse.tables:  # join the last update inside the graph
                 t.wait_update()
+        invalidate_compose_cache()
         self.opt_sparse.defer_join = defer
 
         def replay():
             g.replay()
+            invalidate_compose_cache()
             return loss
 
         return replay

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import weakref
 
 import torch
 from torch import nn
@@ -524,6 +525,13 @@ def vec_chain_compose(layers, rows, n0):
 _compose_cache: dict = {}
 
 
+def invalidate_compose_cache():
+    """Drop every cached chain composition. Parameter updates replayed inside a HIP graph do not
+    bump the tensors' version counters, so TrainStep calls this around captures and after each
+    replay; eager updates invalidate entries through the version counters."""
+    _compose_cache.clear()
+
+
 def _param_versions(layers):
     return tuple((l.kernel.data_ptr(), l.kernel._version,
                   None if l.bias is None else (l.bias.data_ptr(), l.bias._version)) for l in layers)
@@ -538,7 +546,8 @@ def narrow_chain_compose(layers):
     key = id(layers[0].kernel)
     ver = _param_versions(layers)
     hit = _compose_cache.get(key)
-    if hit is not None and hit[0] == ver:
+    # the entry must belong to THIS kernel tensor (an id can be reused after a model is freed)
+    if hit is not None and hit[0] == ver and hit[2]() is layers[0].kernel:
         return hit[1]
     ks = [l.kernel for l in layers]
     n0 = ks[0].shape[0]
@@ -554,7 +563,7 @@ def narrow_chain_compose(layers):
                L.ptr(layers[i].bias), L.ptr(out), st)
         outs.append(out)
         qa = out
-    _compose_cache[key] = (ver, outs)
+    _compose_cache[key] = (ver, outs, weakref.ref(layers[0].kernel))
     return outs
 
 

@@ -269,3 +269,50 @@ def test_compose_cache_follows_parameter_updates():
     ref, bound = _ref(x, ks, bs, 0)
     assert_close_rel(y2.cpu().numpy(), ref, 1e-5, bound, "y after update")
     assert not torch.equal(y1, y2)
+
+
+def test_graph_replay_then_eager_matches_eager_only():
+    """A HIP-graph replay updates the parameters in place without bumping their version
+    counters: eager steps after replays must recompose the chains (nn.invalidate_compose_cache).
+    capture + replay / eager / forward-only / replay / eager equals the same steps run eagerly,
+    bit for bit (without the invalidation the last eager step reuses the forward-only pass's
+    compositions, made before the second replay's update)."""
+    from recommender_amd.ctr.layers import MLP
+    from recommender_amd.ctr.train import TrainStep, build_model
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    old = MLP.factored_min_batch
+    MLP.factored_min_batch = 0
+    try:
+        cards = criteo_cardinalities(100_000, 26)
+        rng = np.random.default_rng(3)
+        bs = []
+        for _ in range(2):
+            cat, dn, lb = criteo_batch(rng, 512, cards)
+            bs.append(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+        models = []
+        for mode in ("graph", "eager"):
+            g = torch.Generator(device=DEV).manual_seed(5)
+            m = build_model("DLRM", 128, sum(cards), 26, 13, torch.device(DEV), slot_cardinalities=cards,
+                            bottom=[64, 128], top=[64, 32, 1], generator=g)
+            st = TrainStep(m, "sgd", lr=0.05, fused=True, defer_sparse_join=True)
+            def peek():  # an eager forward with no update: caches the current compositions
+                m({"cat_features": bs[1][0], "int_features": bs[1][1]})
+
+            if mode == "graph":
+                replay = st.capture(bs[0], warmup=3)       # 3 eager warm-up steps on bs[0]
+                replay(); st(bs[1]); peek(); replay(); st(bs[1])
+            else:
+                for b in (bs[0],) * 3 + (bs[0], bs[1]):
+                    st(b)
+                peek()
+                st(bs[0]); st(bs[1])
+            m.embedding_layer.wait_update()
+            torch.cuda.synchronize()
+            models.append(m)
+        pa, pb = dict(models[0].named_parameters()), dict(models[1].named_parameters())
+        for n in pa:
+            assert torch.equal(pa[n], pb[n]), n
+        assert torch.equal(models[0].embedding_layer.weight, models[1].embedding_layer.weight)
+    finally:
+        MLP.factored_min_batch = old
