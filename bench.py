@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lazy_adam", "keras_adam"])
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--seed", type=int, default=4)
-    ap.add_argument("--cpu-baseline-steps", type=int, default=20)
-    ap.add_argument("--cpu-baseline-batch", type=int, default=16384)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=50)
+    ap.add_argument("--cpu-baseline-batch", type=int, default=4096)
     ap.add_argument("--graph", type=int, default=0,
                     help="1: HIP-graph replays of single steps; 2: one graph per pool of steps "
                          "(updates overlapped across steps inside the graph)")
@@ -288,11 +288,15 @@ def isolated_path(model, ids, iters=10):
 
 
 def cpu_baseline(args, cards):
-    """The oracle's NumPy DLRM SGD step (oracle/ctr.py) on the host cores, bounded sample."""
-    from threadpoolctl import threadpool_info
+    """The oracle's NumPy DLRM SGD step (oracle/ctr.py) on the host cores, bounded sample
+    (warm-up 5 steps, then the median of 50, on len(sched_getaffinity) cores)."""
+    from threadpoolctl import threadpool_info, threadpool_limits
 
     from oracle.ctr import DLRMState, dlrm_sgd_step
 
+    cores = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(cores, omp) if omp > 0 else cores  # the box caps its CPU share via OMP_NUM_THREADS
     D, S = args.dim, args.slots
     rng = np.random.default_rng(args.seed)
     V = sum(cards)
@@ -311,18 +315,23 @@ def cpu_baseline(args, cards):
     F = S + 1
     st = DLRMState(table, so, mk([512, 256, D], 13), mk([512, 256, 1], F * F + D))
     B = args.cpu_baseline_batch
-    batches = [criteo_batch(rng, B, cards) for _ in range(args.cpu_baseline_steps + 1)]
-    dlrm_sgd_step(st, *batches[0], 0.01)  # warm-up
-    t0 = time.perf_counter()
-    for b in batches[1:]:
-        dlrm_sgd_step(st, *b, 0.01)
-    dt = time.perf_counter() - t0
-    threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-    return {"value": B * args.cpu_baseline_steps / dt, "unit": "examples/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/ctr.py dlrm_sgd_step (NumPy fp32), {args.cpu_baseline_steps} steps of "
-                      f"batch {B} on the same 26x{V}x{D} slab / Zipf ids, after 1 warm-up step; "
-                      f"{dt:.1f} s"}
+    n_warm, n_meas = 5, args.cpu_baseline_steps
+    pool = [criteo_batch(rng, B, cards) for _ in range(4)]
+    times = []
+    with threadpool_limits(threads):
+        used = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+        for i in range(n_warm + n_meas):
+            t0 = time.perf_counter()
+            dlrm_sgd_step(st, *pool[i % len(pool)], 0.01)
+            if i >= n_warm:
+                times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": B / med, "unit": "examples/sec", "cores": int(used),
+            "kind": "port", "host_cpus_visible": cores,
+            "p10_p90_s": [round(float(np.percentile(times, 10)), 4), round(float(np.percentile(times, 90)), 4)],
+            "sample": f"oracle/ctr.py dlrm_sgd_step (NumPy fp32, {used} BLAS threads), batch {B} on "
+                      f"the same 26x{V}x{D} slab / Zipf ids: {n_warm} warm-up steps, then the median "
+                      f"of {n_meas} ({med:.3f} s/step, {sum(times):.1f} s timed)"}
 
 
 def main():

@@ -1,9 +1,12 @@
 """Secondary benchmarks for the BASELINE.json configs other than the north star:
   cfg3 dien  : DIEN train step, B 4096, L 100, Amazon-Electronics-shaped vocab (63 001 / 801)
   cfg4 esmm  : MMOE (or ESMM) train step on 18 tables scaled to --rows, B 65 536 per GPU
-  cfg1 deepfm: DeepFM, 1M-row shared table, B 1024, D 16 (the reference's CPU config, on GPU)
+  cfg1 deepfm: DeepFM, 1M-row shared table, B 1024, D 16 (the reference's CPU config, on GPU),
+              with the oracle's NumPy step timed on the host beside it (cpu_baseline)
+  cfg2 dlrm_cfg2: DLRM, 26 per-slot tables x 10M rows x D 64 in one 66.6 GB slab, B 8192,
+              bottom [512, 256, 64], top [512, 256, 1], Zipf(1.05) ids, --optimizer sgd|lazy_adam|keras_adam
 Prints one JSON line per run with examples/sec and per-kernel HIP-event times.
-Usage: python benchmarks/bench_models.py --model dien|mmoe|esmm|deepfm [--steps K --warmup W]"""
+Usage: python benchmarks/bench_models.py --model dien|mmoe|esmm|deepfm|dlrm_cfg2 [--steps K --warmup W]"""
 from __future__ import annotations
 
 import argparse
@@ -40,7 +43,10 @@ def run(step_fn, batches, steps, warmup, watch):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien", "mmoe", "esmm", "deepfm", "pinsage", "eges"])
+    ap.add_argument("--model", default="dien",
+                    choices=["dien", "mmoe", "esmm", "deepfm", "pinsage", "eges", "dlrm_cfg2"])
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lazy_adam", "keras_adam"],
+                    help="dlrm_cfg2 only (the reference DLRM SGD path or Keras / lazy Adam)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
@@ -128,6 +134,27 @@ def main():
                  "rs_match_logits_bwd", "rs_sort_ids", "rs_embedding_apply",
                  "rs_keras_adam_dense_sweep"]
         cfg = {"workload": "eges_b1024_d160_ns5", "batch": B, "items": n_items}
+    elif args.model == "dlrm_cfg2":
+        from recommender_amd.ctr.train import TrainStep, build_model
+        from recommender_amd.synthetic import criteo_batch
+
+        B = args.batch or 8192
+        S, D, per = 26, 64, 10_000_000
+        cards = [per] * S
+        m = build_model("DLRM", D, per * S, S, 13, torch.device(dev), slot_cardinalities=cards,
+                        bottom=[512, 256, D], top=[512, 256, 1])
+        step0 = TrainStep(m, args.optimizer, lr=0.01 if args.optimizer == "sgd" else 1e-3,
+                          fused=True, defer_sparse_join=True)
+        batches = []
+        for _ in range(4):
+            cat, dn, lb = criteo_batch(rng, B, cards)
+            batches.append(((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
+                             torch.from_numpy(lb).to(dev)),))
+        step = step0
+        watch = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_sort_ids",
+                 "rs_embedding_apply", "rs_keras_adam_dense_sweep"]
+        cfg = {"workload": f"dlrm_criteo_26x{per}x{D}_b{B}", "batch": B, "rows": per * S,
+               "slab_GB": round(per * S * D * 4 / 1e9, 1), "optimizer": args.optimizer}
     else:
         from recommender_amd.ctr.train import TrainStep, build_model
         from recommender_amd.synthetic import criteo_batch
@@ -144,8 +171,53 @@ def main():
                  "rs_keras_adam_dense_sweep"]
         cfg = {"workload": "deepfm_criteo_1M_b1024_d16", "batch": B, "optimizer": "keras_adam"}
     sec, k = run(step, batches, args.steps, args.warmup, watch)
-    print(json.dumps({"model": args.model, "examples_per_sec": round(B / sec, 1),
-                      "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k}))
+    out = {"model": args.model, "examples_per_sec": round(B / sec, 1),
+           "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k}
+    if args.model == "deepfm":
+        out["cpu_baseline"] = deepfm_cpu_baseline(B)
+    print(json.dumps(out))
+
+
+def deepfm_cpu_baseline(B, n_warm=5, n_meas=20):
+    """cfg1 is the reference's CPU-only config: the oracle's NumPy DeepFM Keras-Adam step
+    (oracle/ctr.py deepfm_keras_adam_step, the same 1M x 16 table, MLP [512, 256, 1]) timed on
+    the host cores — warm-up 5, median of 20."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    from oracle.ctr import deepfm_keras_adam_step
+    from recommender_amd.synthetic import criteo_batch
+
+    rng = np.random.default_rng(4)
+    V, D, S = 1_000_000, 16, 26
+    cores = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(cores, omp) if omp > 0 else cores
+    st = {"table": rng.uniform(-0.05, 0.05, (V, D)).astype(np.float32),
+          "m": np.zeros((V, D), np.float32), "v": np.zeros((V, D), np.float32)}
+    fin, layers = S * D + 13, []
+    for u in (512, 256, 1):
+        lim = np.sqrt(6.0 / (fin + u))
+        layers.append((rng.uniform(-lim, lim, (fin, u)).astype(np.float32), np.zeros(u, np.float32)))
+        fin = u
+    st["layers"] = layers
+    st["dense_m"] = [(np.zeros_like(k), np.zeros_like(b)) for k, b in layers]
+    st["dense_v"] = [(np.zeros_like(k), np.zeros_like(b)) for k, b in layers]
+    pool = [criteo_batch(rng, B, [V] * S) for _ in range(4)]
+    times = []
+    with threadpool_limits(threads):
+        used = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+        for i in range(n_warm + n_meas):
+            cat, dn, lb = pool[i % 4]
+            t0 = time.perf_counter()
+            _, st2, _ = deepfm_keras_adam_step(st["table"], st["m"], st["v"], st["layers"],
+                                               st["dense_m"], st["dense_v"], cat % V, dn, lb, i + 1)
+            if i >= n_warm:
+                times.append(time.perf_counter() - t0)
+            st.update(st2)
+    med = float(np.median(times))
+    return {"value": round(B / med, 1), "unit": "examples/sec", "cores": int(used), "kind": "port",
+            "sample": f"oracle/ctr.py deepfm_keras_adam_step, batch {B}, {n_warm} warm-up + median "
+                      f"of {n_meas} ({med * 1e3:.1f} ms/step)"}
 
 
 if __name__ == "__main__":

@@ -61,6 +61,26 @@ def test_sort_ids(n, V, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("per_slot", [10_000_000, 40_000_000])
+def test_sort_ids_large_slab_four_passes(per_slot, rng):
+    """SURVEY cfg2's 26 x 10M-row slab (260M rows: 28 key bits, four 7-bit passes) and a 1.04B-row
+    key space (30 bits, four 8-bit passes): the slab itself is not needed, only its slot offsets.
+    Zipf ids per slot plus out-of-range ones, bit-exact vs the oracle's stable sort."""
+    from recommender_amd.synthetic import criteo_batch
+
+    S, B = 26, 8192
+    cards = [per_slot] * S
+    cat, _, _ = criteo_batch(rng, B, cards)
+    cat[::113, 5] = per_slot + 7  # OOB in slot 5
+    so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+    V = int(so[-1])
+    s = SortedIds(torch.from_numpy(cat).to(DEV), V, torch.from_numpy(so).to(DEV))
+    rows_ref, pos_ref, nu_ref = O.sort_ids(cat, V, so)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
 def test_sort_ids_empty():
     s = SortedIds(torch.zeros(0, dtype=torch.int64, device=DEV), 10)
     assert s.n == 0 and int(s.n_unique.item()) == 0

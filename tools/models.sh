@@ -1,8 +1,6 @@
+# secondary-model benchmarks (run under gpurun): MODELS="deepfm dlrm_cfg2" bash tools/models.sh
 export TMPDIR=/tmp
-: > gpurun_out/models.jsonl
-for m in deepfm dien esmm mmoe pinsage eges; do
-  timeout -k 10 300 python benchmarks/bench_models.py --model $m >> gpurun_out/models.jsonl 2> gpurun_out/models_$m.err || { echo "$m failed"; tail -5 gpurun_out/models_$m.err; exit 1; }
+for m in ${MODELS:-deepfm dlrm_cfg2 dien esmm mmoe pinsage eges}; do
+  timeout -k 10 400 python benchmarks/bench_models.py --model $m ${MODEL_ARGS:-} > gpurun_out/m_$m.jsonl 2> gpurun_out/m_$m.err || { tail -20 gpurun_out/m_$m.err; exit 1; }
+  cat gpurun_out/m_$m.jsonl
 done
-cut -c1-300 gpurun_out/models.jsonl
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dien -o run --output-format csv -- python benchmarks/bench_models.py --model dien --steps 10 --warmup 3 > gpurun_out/prof_dien.log 2>&1 || { echo prof failed; exit 1; }
-echo prof ok
