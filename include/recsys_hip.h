@@ -41,6 +41,7 @@ extern "C" {
 #define RS_ID_I64 1
 
 #define RS_ERRBIT_OOB 1
+#define RS_ERRBIT_FORMAT 2  /* a malformed input record (rs_tfrecord_parse_criteo) */
 
 /* optimizer kinds for rs_embedding_apply */
 #define RS_OPT_SGD 0        /* var[u] -= lr * g_u                         (ctr/train.py:77-79) */
@@ -648,6 +649,29 @@ int32_t rs_dien_encode(const uint64_t* item_hash, const uint64_t* cat_hash,
                        uint64_t seed, int64_t line_base, int32_t* target_item, int32_t* target_cat,
                        int32_t* his_item, int32_t* his_cat, int32_t* neg_item, int32_t* neg_cat,
                        int32_t* err_flag, void* stream);
+
+/* ---- Criteo TFRecord reader (replaces ctr/tfrecord_io.py:78-96
+ * read_tfrecord: tf.data.TFRecordDataset + parse_single_example + parse_tensor) ------------
+ * rs_tfrecord_index (HOST memory, host code): walks the TFRecord framing of data[0, n_bytes)
+ *   (uint64 length, masked CRC32C of it, payload, masked CRC32C of the payload), checking the
+ *   length CRCs when verify_crc; writes up to `capacity` record offsets (of the length field)
+ *   and payload lengths; *n_records = the count. Corrupt framing -> RS_E_INVALID.
+ * rs_tfrecord_parse_criteo (DEVICE memory, stream-ordered): one tf.train.Example per record
+ *   with 'int_features' / 'cat_features' = tf.io.serialize_tensor of float32 [n_int] / int64
+ *   [n_cat] (tensor_content or packed float_val / int64_val) and 'label' = int64_list; any
+ *   field order, unknown fields skipped. verify_crc: the payload CRC32C is checked too.
+ *   Outputs int_features [n, n_int] f32, cat_features [n, n_cat] i64, label [n] i64; a
+ *   malformed record (bad CRC, shape or dtype, missing key, payload > 4096 B) is zeroed and sets
+ *   RS_ERRBIT_FORMAT in err_flag (may be NULL). */
+/* rs_crc32c_masked (HOST memory): the TFRecord masked CRC32C of data[0, n_bytes) (writer side). */
+int32_t rs_crc32c_masked(const uint8_t* data, int64_t n_bytes, uint32_t* out);
+int32_t rs_tfrecord_index(const uint8_t* data, int64_t n_bytes, int32_t verify_crc,
+                          int64_t* offsets, int32_t* lengths, int64_t capacity, int64_t* n_records);
+int32_t rs_tfrecord_parse_criteo(const uint8_t* data, const int64_t* offsets,
+                                 const int32_t* lengths, int64_t n_records, int32_t n_int,
+                                 int32_t n_cat, int32_t verify_crc, float* int_features,
+                                 int64_t* cat_features, int64_t* label, int32_t* err_flag,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@ RS_OPT_LAZY_ADAM = 1
 RS_OPT_KERAS_ADAM = 2
 RS_DEDUP_TILE = 32
 RS_ERRBIT_OOB = 1
+RS_ERRBIT_FORMAT = 2
 
 
 class AdamParams(C.Structure):
@@ -97,6 +98,9 @@ _SIGS = {
     "rs_line_index_workspace_size": (_sz, [_i64]),
     "rs_line_index": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
     "rs_criteo_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
+    "rs_crc32c_masked": (_i32, [_p, _i64, _p]),
+    "rs_tfrecord_index": (_i32, [_p, _i64, _i32, _p, _p, _i64, _p]),
+    "rs_tfrecord_parse_criteo": (_i32, [_p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "rs_vocab_count": (_i32, [_p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),
     "rs_vocab_collect_workspace_size": (_sz, [_i64]),
     "rs_vocab_collect": (_i32, [_p, _p, _p, _i64, _u32, _p, _p, _p, _p, _sz, _p]),

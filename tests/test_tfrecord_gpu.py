@@ -1,0 +1,104 @@
+"""GPU parity of the Criteo TFRecord reader (rs_tfrecord_parse_criteo; ctr/tfrecord_io.py:78-96)
+against oracle/tfrecord.py: bulk files bit-exact, protobuf variants a TF writer may produce
+(any entry / field order, unknown fields, unpacked int64 list, packed float_val, negative label),
+corrupt and malformed records flagged, and the TSV -> vocab -> TFRecord -> device round trip."""
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import tfrecord as OT
+from recommender_amd.data import CriteoVocab, read_tfrecord
+from recommender_amd.data.tfrecord import encode_tsv
+from tests.criteo_text import make_tsv
+
+pytestmark = pytest.mark.gpu
+F, V = OT.field, OT.varint
+
+
+def _arrays(rng, n):
+    ints = np.log1p(rng.geometric(0.01, (n, 13))).astype(np.float32)
+    cats = rng.integers(0, 1_000_000, (n, 26)).astype(np.int64)
+    cats[0, 0] = (1 << 40) + 3
+    labels = (rng.random(n) < 0.25).astype(np.int64)
+    return ints, cats, labels
+
+
+def _check(got, ints, cats, labels):
+    feats, lab = got
+    np.testing.assert_array_equal(feats["int_features"].cpu().numpy(), ints)
+    np.testing.assert_array_equal(feats["cat_features"].cpu().numpy(), cats)
+    np.testing.assert_array_equal(lab.cpu().numpy(), labels)
+
+
+@pytest.mark.parametrize("n", [1, 37, 5000])
+def test_bulk_records_bit_exact(n, rng):
+    ints, cats, labels = _arrays(rng, n)
+    _check(read_tfrecord(OT.write_records(ints, cats, labels)), ints, cats, labels)
+
+
+def test_empty_file():
+    feats, lab = read_tfrecord(b"")
+    assert lab.numel() == 0 and feats["int_features"].shape == (0, 13)
+
+
+def _entry(key, feature):
+    return F(1, 2, F(1, 2, key.encode()) + F(2, 2, feature))
+
+
+def test_protobuf_variants(rng):
+    """Entries in another order, TensorProto fields reordered, an unknown Example field and
+    feature, an unpacked int64 label, float_val (packed) instead of tensor_content, label -1."""
+    ints, cats, _ = _arrays(rng, 3)
+    recs = []
+    # 0: reversed entries + unknown fields; tensor_content before dtype / shape
+    t_int = F(4, 2, ints[0].tobytes()) + F(2, 2, F(2, 2, F(1, 0, V(13)))) + F(1, 0, V(1))
+    t_cat = F(1, 0, V(9)) + F(7, 0, V(5)) + F(2, 2, F(2, 2, F(1, 0, V(26)))) + F(4, 2, cats[0].tobytes())
+    feats = (_entry("label", F(3, 2, F(1, 2, V(1)))) + _entry("zzz", F(2, 2, F(1, 2, b"\0\0\x80?")))
+             + _entry("cat_features", F(1, 2, F(1, 2, t_cat)))
+             + _entry("int_features", F(1, 2, F(1, 2, t_int))))
+    recs.append(OT.frame(F(9, 0, V(3)) + F(1, 2, feats)))
+    # 1: unpacked label (wire type 0) and float_val instead of tensor_content
+    t_int = F(1, 0, V(1)) + F(2, 2, F(2, 2, F(1, 0, V(13)))) + F(5, 2, ints[1].tobytes())
+    feats = (_entry("int_features", F(1, 2, F(1, 2, t_int)))
+             + _entry("cat_features", F(1, 2, F(1, 2, OT.tensor_proto(cats[1]))))
+             + _entry("label", F(3, 2, F(1, 0, V(0)))))
+    recs.append(OT.frame(F(1, 2, feats)))
+    # 2: the canonical layout with label -1 (a ten-byte varint)
+    recs.append(OT.frame(OT.example(ints[2], cats[2], -1)))
+    _check(read_tfrecord(b"".join(recs)), ints, cats, np.array([1, 0, -1]))
+
+
+def test_corrupt_and_malformed_records(rng):
+    ints, cats, labels = _arrays(rng, 4)
+    good = OT.write_records(ints, cats, labels)
+    bad = bytearray(good)
+    rec1 = 16 + len(OT.example(ints[0], cats[0], labels[0]))  # start of record 1
+    bad[rec1 + 12 + 40] ^= 0x10  # a payload byte of record 1
+    with pytest.raises(ValueError):
+        read_tfrecord(bytes(bad))
+    # without the payload CRC the flipped byte is only data: the other rows are intact
+    feats, lab = read_tfrecord(bytes(bad), verify_crc=False)
+    np.testing.assert_array_equal(feats["int_features"][[0, 2, 3]].cpu().numpy(), ints[[0, 2, 3]])
+    # wrong shape (cat_features [25]) and a missing key are malformed
+    for ex in (OT.example(ints[0], cats[0][:25], 1),
+               OT.field(1, 2, _entry("int_features", OT.field(1, 2, OT.field(1, 2, OT.tensor_proto(ints[0])))))):
+        with pytest.raises(ValueError):
+            read_tfrecord(OT.frame(ex))
+
+
+def test_tsv_to_tfrecord_round_trip(rng, tmp_path):
+    """write_tfrecord end to end (tfrecord_io.py:39-75): TSV through the device vocabulary into a
+    TFRecord file, read back on the device = the encoded batch (labels as int64)."""
+    train = make_tsv(rng, 600)
+    v = CriteoVocab.build(train.encode())
+    out = tmp_path / "train.tfrecord"
+    encode_tsv(v, train.encode(), out)
+    cat, dense, label = v.encode(train.encode())
+    feats, lab = read_tfrecord(str(out))
+    assert torch.equal(feats["cat_features"], cat)
+    assert torch.equal(feats["int_features"], dense)
+    assert torch.equal(lab, label.to(torch.int64))
+    a, b, c = OT.read_records(out.read_bytes())
+    np.testing.assert_array_equal(b, cat.cpu().numpy())
