@@ -30,7 +30,8 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head", "rs_dlrm_interaction_fwd_head_dx",
+WATCH = ["rs_dlrm_train_step_fwd", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
+         "rs_dlrm_interaction_fwd_head_dx",
          "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids",
          "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
          "rs_embedding_dedup_grad"]
@@ -38,7 +39,7 @@ WATCH = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head", "rs_dlrm_int
 # launches it: the fused gather + interaction + unit-backward kernel (main stream), the radix
 # sort and the segmented-sum apply (fused optimizer's side stream, co-running with dense GEMMs:
 # their event spans include that co-run time)
-PATH_KERNELS = ("rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
+PATH_KERNELS = ("rs_dlrm_train_step_fwd", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
                 "rs_dlrm_interaction_fwd_head_dx", "rs_dlrm_interaction_bwd",
                 "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids", "rs_sort_ids_sharded",
                 "rs_embedding_apply", "rs_embedding_apply_scaled")
@@ -47,6 +48,7 @@ SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_embedding_apply_scaled",
 # device symbols behind each C-ABI entry (for the PMC passes)
 # (entry, device-symbol regex of its kernels, the one kernel every call launches once)
 PMC_SYMBOLS = [
+    ("rs_dlrm_train_step_fwd", r"dlrm_train_pipe", "dlrm_train_pipe"),
     ("rs_dlrm_interaction_fwd_head_dx", r"dlrm_fwd_dx_pipe", "dlrm_fwd_dx_pipe"),
     ("rs_dlrm_interaction_fwd_head", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, false>",
      "inter_fwd_mfma"),
@@ -95,7 +97,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = "inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
+PMC_KERNEL_REGEX = "dlrm_train_pipe|inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 
@@ -217,12 +219,15 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + S * 4 * D + 4 * D)
     if name == "rs_dlrm_interaction_bwd_rank1":  # grad row = G[b] * p: 4 B per example, not 4Z
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 + S * 4 * D + 4 * D)
+    if name == "rs_dlrm_train_step_fwd":  # ids, rows, bottom row, 13 inputs + label in;
+        # y and the S gradient rows out (the batch sums are weight-sized)
+        return B * (S * id_bytes + S * 4 * D + 4 * D + 13 * 4 + 4 + 4 + S * 4 * D)
     if name == "rs_dlrm_interaction_fwd_head_dx":  # + the unit gradient rows (S + 1 per example)
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + 4 + S * 4 * D + 4 * D)
     if name == "rs_embedding_apply":
         return N * 8 + N * 4 * D + U * 2 * 4 * D
-    if name == "rs_embedding_apply_scaled":  # + G[b], one scale per example
-        return N * 8 + N * 4 * D + U * 2 * 4 * D + B * 4
+    if name == "rs_embedding_apply_scaled":  # the production step hands final rows (no scale)
+        return N * 8 + N * 4 * D + U * 2 * 4 * D
     if name == "rs_sort_ids":
         return N * id_bytes + N * 8
     return 0
@@ -231,8 +236,9 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
 def isolated_path(model, ids, iters=10):
     """The production embedding path's three launches run alone and back to back on the main
     stream, after the timed region, on the model's own slab, ids and workspaces: the fused
-    gather + interaction + head + unit-backward kernel, the radix sort, the scaled segmented-sum
-    SGD apply with lr 0 (the table does not move; the same bytes are read and written). Each is
+    train-step kernel (gather + interaction + head + BCE + gradient rows + batch sums, with its
+    block fold), the radix sort, the segmented-sum SGD apply with lr 0 (the table does not move;
+    the same bytes are read and written). Each is
     timed with HIP events over `iters` launches on the stream it is launched on. In the step the
     sort and the apply run on the side stream beside other kernels, so their in-step event spans
     include co-run time; these isolated averages are what the roofline divides by."""
@@ -244,17 +250,17 @@ def isolated_path(model, ids, iters=10):
     B, S = ids.shape
     dev = w.device
     st = L.stream_ptr(dev)
-    width = 512
     nzc = (S + 1) * S // 2 + D
     g = torch.Generator(device=dev).manual_seed(7)
     dense = torch.rand(B, D, device=dev, generator=g)
     q = torch.randn(nzc, device=dev, generator=g) * 0.05
     cc = torch.zeros(1, device=dev)
-    z = torch.empty(B, width, device=dev)
-    y = torch.empty(B, 1, device=dev)
+    y = torch.empty(B, device=dev)
     dxu = torch.empty(B * S, D, device=dev)
-    dxd = torch.empty(B, D, device=dev)
-    G = torch.randn(B, device=dev, generator=g) * 1e-3
+    xin = torch.rand(B, 13, device=dev, generator=g)
+    lab = (torch.rand(B, device=dev, generator=g) < 0.25).float()
+    sums = torch.empty(512 + 2 + 14 * 128, device=dev)
+    tws = torch.empty(L.lib().rs_dlrm_train_workspace_size(B), dtype=torch.uint8, device=dev)
     n = B * S
     rows = torch.empty(n, dtype=torch.int32, device=dev)
     pos = torch.empty(n, dtype=torch.int32, device=dev)
@@ -262,16 +268,16 @@ def isolated_path(model, ids, iters=10):
     aws = torch.empty(L.lib().rs_apply_workspace_size(n, D), dtype=torch.uint8, device=dev)
     prm = L.AdamParams(0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
     calls = {
-        "rs_dlrm_interaction_fwd_head_dx": lambda: L.call(
-            "rs_dlrm_interaction_fwd_head_dx", L.ptr(w), V, D, L.ptr(ids), L.id_dtype_code(ids), S,
-            L.ptr(so), L.ptr(dense), B, L.ptr(z), width, L.ptr(q), L.ptr(cc), 2, L.ptr(y),
-            L.ptr(dxu), L.ptr(dxd), L.ptr(err), st),
+        "rs_dlrm_train_step_fwd": lambda: L.call(
+            "rs_dlrm_train_step_fwd", L.ptr(w), V, D, L.ptr(ids), L.id_dtype_code(ids), S,
+            L.ptr(so), L.ptr(dense), L.ptr(xin), 13, L.ptr(lab), B, L.ptr(q), L.ptr(cc), 1e-7, 2,
+            L.ptr(y), L.ptr(dxu), L.ptr(sums), L.ptr(tws), tws.numel(), L.ptr(err), st),
         "rs_sort_ids": lambda: L.call(
             "rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(so), S, V, L.ptr(rows),
             L.ptr(pos), None, L.ptr(err), L.ptr(sws), sws.numel(), st),
         "rs_embedding_apply_scaled": lambda: L.call(
             "rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(w), None, None, V, D, L.ptr(rows),
-            L.ptr(pos), n, L.ptr(dxu), L.ptr(G), S, prm, None, L.ptr(aws), aws.numel(), st),
+            L.ptr(pos), n, L.ptr(dxu), None, 1, prm, None, L.ptr(aws), aws.numel(), st),
     }
     out = {}
     for name, fn in calls.items():
@@ -472,7 +478,7 @@ def main():
         a = path_bytes / (path_us * 1e-6) / 1e9
         pmc_key = {"rs_embedding_apply_scaled": "rs_embedding_apply"}
         per_kernel = {}
-        for n_, us in iso.items():
+        for n_, us in iso.items():  # noqa: B007
             by = kernel_bytes(n_, args.batch, S, D, 8, U)
             t = (traffic or {}).get(pmc_key.get(n_, n_))
             per_kernel[n_] = {"avg_us": round(us, 2), "algorithmic_bytes": int(by),

@@ -381,8 +381,13 @@ def dlrm_path(iters, out):
         L.call("rs_dlrm_interaction_fwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
                L.ptr(dense), B, 1, L.ptr(inter), 512, L.ptr(err), st)
 
-    def srt():
-        return SortedIds(ids, V, so, err, count_unique=False)
+    srows = torch.empty(B * S, dtype=torch.int32, device=DEV)
+    spos = torch.empty(B * S, dtype=torch.int32, device=DEV)
+    sws = torch.empty(L.lib().rs_sort_ids_workspace_size(B * S), dtype=torch.uint8, device=DEV)
+
+    def srt():  # raw C call on preallocated buffers (no per-call Python allocation)
+        L.call("rs_sort_ids", L.ptr(ids), 1, B * S, L.ptr(so), S, V, L.ptr(srows), L.ptr(spos),
+               None, L.ptr(err), L.ptr(sws), sws.numel(), st)
 
     def bwd():
         L.call("rs_dlrm_interaction_bwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
@@ -398,6 +403,17 @@ def dlrm_path(iters, out):
     yv = torch.empty(B, 1, device=DEV)
     G = torch.randn(B, device=DEV) * 1e-3
 
+    xin = torch.rand(B, 13, device=DEV)
+    lab = (torch.rand(B, device=DEV) < 0.25).float()
+    sums = torch.empty(512 + 2 + 14 * 128, device=DEV)
+    tws = torch.empty(L.lib().rs_dlrm_train_workspace_size(B), dtype=torch.uint8, device=DEV)
+    yb = torch.empty(B, device=DEV)
+
+    def train_fwd():
+        L.call("rs_dlrm_train_step_fwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
+               L.ptr(dense), L.ptr(xin), 13, L.ptr(lab), B, L.ptr(q), L.ptr(cc), 1e-7, 2,
+               L.ptr(yb), L.ptr(gemb), L.ptr(sums), L.ptr(tws), tws.numel(), L.ptr(err), st)
+
     def fwd_dx():
         L.call("rs_dlrm_interaction_fwd_head_dx", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
                L.ptr(dense), B, L.ptr(inter), 480, L.ptr(q), L.ptr(cc), 2, L.ptr(yv), L.ptr(gemb),
@@ -408,16 +424,30 @@ def dlrm_path(iters, out):
                L.ptr(s0.rows), L.ptr(s0.pos), B * S, L.ptr(gemb), L.ptr(G), S, prm, None,
                L.ptr(ws), ws.numel(), st)
 
+    def apply_final():
+        L.call("rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(table), None, None, V, D,
+               L.ptr(s0.rows), L.ptr(s0.pos), B * S, L.ptr(gemb), None, 1, prm, None,
+               L.ptr(ws), ws.numel(), st)
+
     bwd()
     cfg = {"B": B, "S": S, "D": D, "rows": V, "unique": U}
     per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
+    tot = 0.0
+    for name, fn in (("rs_dlrm_train_step_fwd", train_fwd), ("rs_sort_ids", srt),
+                     ("rs_embedding_apply_scaled", apply_final)):
+        us = timed(fn, iters)
+        tot += us
+        report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
+    report("embedding_path (production: fused train-step kernel, sort, apply; alone)",
+           dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
+    # the previous production path (fused forward + unit backward, scaled apply)
     tot = 0.0
     for name, fn in (("rs_dlrm_interaction_fwd_head_dx", fwd_dx), ("rs_sort_ids", srt),
                      ("rs_embedding_apply_scaled", apply_scaled)):
         us = timed(fn, iters)
         tot += us
         report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
-    report("embedding_path (production: 3 launches back to back, alone)",
+    report("embedding_path (fwd + unit bwd, scaled apply: 3 launches back to back, alone)",
            dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
     # the previous path (separate re-gathering backward), for the record
     tot = 0.0

@@ -673,6 +673,26 @@ int32_t rs_tfrecord_parse_criteo(const uint8_t* data, const int64_t* offsets,
                                  int64_t* cat_features, int64_t* label, int32_t* err_flag,
                                  void* stream);
 
+/* ---- the production DLRM training step's top half in one pass (D = 128, <= 27 slots, 13
+ * dense inputs, sigmoid head, Keras BCE; ctr/model.py:45-57 + ctr/train.py:77-85) ------------
+ * Gathers X = [emb(ids), dense], Z = X·Xᵀ, y = σ(Σ q·[Z_strict_upper, dense] + c) (q, c: the
+ * composed top MLP, rs_chain3_vec_compose), the BCE loss against label (eps clip; reduction
+ * 1 = sum, 2 = mean), G_b = y(1-y)·dL/dy, the table gradient rows G_b·(M + Mᵀ)·X_b (M = the
+ * strict-upper pair weights of q) in position order into grad_emb [B*S, D], y [B], and the
+ * deterministic batch sums (fixed per-wave / per-block / two-level fold order) into
+ * sums [rs_dlrm_train_sums()] = A_top [512] (Σ_b row_b·G_b over the compact row, zero padded)
+ * | s_top = Σ G | loss sum | A_bot [13][128] = Σ_b x_bᵀ·g_b | s_bot [128] = Σ_b g_b, where
+ * g_b = relu'(dense_b) ⊙ G_b·((M + Mᵀ)·X_b + q_dense)[row S] is the bottom MLP's last-layer
+ * gradient and x = xin [B, 13] its input. */
+size_t rs_dlrm_train_workspace_size(int64_t batch);
+int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
+                               int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
+                               const float* dense, const float* xin, int32_t n_in,
+                               const float* label, int64_t batch, const float* q, const float* c,
+                               float eps, int32_t reduction, float* y, float* grad_emb,
+                               float* sums, void* workspace, size_t ws_bytes, int32_t* err_flag,
+                               void* stream);
+
 #ifdef __cplusplus
 }
 #endif

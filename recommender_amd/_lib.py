@@ -99,6 +99,9 @@ _SIGS = {
     "rs_line_index": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
     "rs_criteo_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "rs_crc32c_masked": (_i32, [_p, _i64, _p]),
+    "rs_dlrm_train_workspace_size": (_sz, [_i64]),
+    "rs_dlrm_train_step_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p, _i64,
+                                      _p, _p, C.c_float, _i32, _p, _p, _p, _p, _sz, _p, _p]),
     "rs_tfrecord_index": (_i32, [_p, _i64, _i32, _p, _p, _i64, _p]),
     "rs_tfrecord_parse_criteo": (_i32, [_p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "rs_vocab_count": (_i32, [_p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),

@@ -484,8 +484,8 @@ __global__ __launch_bounds__(256) void fold_segments_kernel(const float* __restr
 }
 
 // fixed two-level fold of nchunks partial rows [N] (deterministic for given nchunks)
-static int32_t fold_two_level(const float* part, int nchunks, int N, float* part2, float* out,
-                              hipStream_t st) {
+int32_t fold_two_level(const float* part, int nchunks, int N, float* part2, float* out,
+                       hipStream_t st) {
   constexpr int kSeg = 32;
   const int per = (int)ceil_div(nchunks, kSeg);
   const int nseg = (int)ceil_div(nchunks, per);

@@ -23,6 +23,11 @@
 
 namespace rs {
 
+// fixed two-level fold of nchunks partial rows [N] into out[N] (csrc/dense.hip); part2 holds
+// 32 x N floats of scratch
+int32_t fold_two_level(const float* part, int nchunks, int N, float* part2, float* out,
+                       hipStream_t st);
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -829,6 +834,301 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
   if (__any(oob) && lane == 0) flag_oob(src.err_flag);
 }
 
+// ---------------------------------------------------------------------------------------
+// The whole top half of the production DLRM training step in one pipelined pass (D = 128,
+// F <= 28, sigmoid head, mean / sum Keras BCE). Per example b, as dlrm_fwd_dx_pipe (Z = X·Xᵀ on
+// MFMA, X(b) to LDS, X(b+1) loads in flight, U = (M + Mᵀ)·X per 16-column tile), plus:
+//   head     y = σ(Σ q·z + Σ q_d·dense + c) straight from the MFMA accumulators (no Z staging:
+//            each lane owns 12 Z entries, their q weights are lane constants);
+//   loss     l_b = keras BCE(label_b, y) (clip to [eps, 1-eps], log(p + eps)), summed;
+//   G        G_b = σ'(y)·dL/dy = y(1-y)·g·d(label, y) (g = 1/B for the mean) — the top MLP
+//            chain's last-layer gradient, known here, so the backward needs no second pass:
+//   A_top    Σ_b z_b·G_b and Σ_b G_b (the factored top-MLP backward's reduction,
+//            nn.chain_reduce) accumulated per lane from the same registers;
+//   rows     the table gradient rows G_b·U_b written whole (position order), ready for the
+//            segmented-sum apply (no row_scale);
+//   bottom   the bottom-MLP row's gradient G_b·(U_b,S + q_d) through the bottom chain's relu
+//            (h > 0), reduced on the spot: A_bot = Σ_b x_bᵀ·G_bot,b ([13, 128]) and Σ_b G_bot,b
+//            (x = the 13 dense input features) — the bottom MLP's factored backward reduction.
+// The z row, the [B, 128] bottom gradient and the BCE / chain-reduce passes are never
+// materialised. Per-wave sums (examples in order) are folded per block in wave order and written
+// as one partial row [kTrainM] per block; rs_dlrm_train_fold folds the blocks in a fixed order.
+// ---------------------------------------------------------------------------------------
+constexpr int kTrainAtop = 512;                       // A_top (compact row, zero padding)
+constexpr int kTrainNI = 13;                          // bottom-MLP inputs (Criteo dense)
+constexpr int kTrainM = kTrainAtop + 2 + kTrainNI * 128 + 128;  // A_top | s_top | loss | A_bot | s_bot
+
+struct TrainArgs {
+  const float* q;      // [nzc + D] Q_0 over the compact row
+  const float* c;      // [1]
+  const float* label;  // [B]
+  const float* xin;    // [B, 13] bottom-MLP input
+  float eps;           // BCE clip
+  float gscale;        // dL/dl_b: 1/B (mean) or 1 (sum)
+  float* y;            // [B] prediction
+  float* grad_emb;     // [B * S, D] table gradient rows
+  float* part;         // [gridDim.x, kTrainM]
+};
+
+template <bool ID64>
+__global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t batch, int F,
+                                                       TrainArgs ta, int epw) {
+  constexpr int D = 128, NT = 8;
+  __shared__ __attribute__((aligned(16))) float lds[4][kDxRows * kDxLdx];
+  // lane constants kept in LDS rather than VGPRs (the accumulators need the registers): the q
+  // weight of each lane's 12 Z entries (0 where the pair is not kept), and q over the row
+  __shared__ __attribute__((aligned(16))) float qlane[64][12];
+  __shared__ __attribute__((aligned(16))) float qsh[kTrainAtop];
+  static_assert(kDxRows * kDxLdx >= kTrainM, "per-wave LDS region holds the wave's partial row");
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
+  const int64_t last = first + epw < batch ? first + epw : batch;
+  const bool active = first < batch;
+  const int r = lane & 15, g = lane >> 4;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int S = src.n_slots;
+  const int nzc = F * (F - 1) / 2;
+  float* X = lds[wave];
+  for (int e = threadIdx.x; e < kTrainAtop; e += 256) qsh[e] = e < nzc + D ? ta.q[e] : 0.f;
+  if (wave == 0) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i0 = 4 * g + reg, j0 = r;            // c00: Z[i0][j0]
+      const int i1 = 4 * g + reg, j1 = 16 + r;       // c01
+      const int i2 = 16 + 4 * g + reg, j2 = 16 + r;  // c11
+      qlane[lane][reg] = (i0 < j0) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
+      qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
+      qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
+    }
+  }
+  float sa[2][8];
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int m = 16 * ib + r, k = 4 * kk + g;
+      const bool in = m < F && k < F && m != k;
+      const float v = ta.q[in ? compact_index(m < k ? m : k, m < k ? k : m, F, 0) : 0];
+      sa[ib][kk] = in ? v : 0.f;
+    }
+  __syncthreads();
+  const float cc = ta.c[0];
+  // accumulators (per lane; the loss and s_top are lane-uniform)
+  float az[12], ad[4], abot[2][kTrainNI], sbot[2];
+  float s_top = 0.f, loss = 0.f;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) az[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ad[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    sbot[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kTrainNI; ++i) abot[k][i] = 0.f;
+  }
+  int64_t lo = 0, n_ok = src.n_rows;
+  if (lane < S && src.slot_offsets) {
+    lo = src.slot_offsets[lane];
+    n_ok = src.slot_offsets[lane + 1] - lo;
+  }
+  bool oob = false;
+  auto raw_id = [&](int64_t b) -> int64_t {
+    const int64_t bb = b < last ? b : first;
+    const int ln = lane < S ? lane : S - 1;
+    const int64_t v = ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + ln]
+                           : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + ln]);
+    return lane < S ? v : 0;
+  };
+  auto row_of = [&](int64_t b, int64_t id) -> const float* {
+    const bool live = b < last;
+    const bool id_ok = id >= 0 && id < n_ok;
+    if (lane < S && !id_ok && live) oob = true;
+    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
+    return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
+  };
+  floatx4 a0[NT], a1[NT];
+  floatx4 dn4;
+  float xv, lab;
+  auto gather = [&](const float* mine, int64_t b) {
+    const float* p0 = shfl_ptr(mine, r);
+    const float* p1 = shfl_ptr(mine, 16 + r);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a0[t] = *(gfloatx4*)(p0 + 4 * g + 16 * t);
+      a1[t] = *(gfloatx4*)(p1 + 4 * g + 16 * t);
+    }
+    const int64_t bb = b < last ? b : first;
+    dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * r32);
+    xv = *(gfloat*)(ta.xin + bb * kTrainNI + (lane < kTrainNI ? lane : 0));
+    lab = *(gfloat*)(ta.label + bb);
+  };
+  if (active) {
+    gather(row_of(first, raw_id(first)), first);
+    int64_t id_next = raw_id(first + 1);
+    for (int64_t b = first; b < last; ++b) {
+      int lanev;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
+      const int r = lanev & 15, g = (lanev >> 4) & 3;
+      const int r32 = lanev & 31, h = (lanev >> 5) & 1;
+      const float* nxt = row_of(b + 1, id_next);
+      id_next = raw_id(b + 2);
+      // (1) Z = X·Xᵀ (three 16x16 blocks)
+      floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a0[t][c], c00, 0, 0, 0);
+          c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a1[t][c], c01, 0, 0, 0);
+          c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
+        }
+      }
+      // (2) X(b) → LDS
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        *reinterpret_cast<floatx4*>(&X[r * kDxLdx + 16 * t + 4 * g]) = a0[t];
+        if (16 + r < kDxRows) *reinterpret_cast<floatx4*>(&X[(16 + r) * kDxLdx + 16 * t + 4 * g]) = a1[t];
+      }
+      const floatx4 dn = dn4;
+      float xb[kTrainNI];  // wave-uniform: scalar registers
+#pragma unroll
+      for (int i = 0; i < kTrainNI; ++i)
+        xb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
+      const float lb = lab;
+      // (3) X(b+1) in flight behind the rest of this example
+      __builtin_amdgcn_sched_barrier(0);
+      gather(nxt, b + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // (4) head, loss, G
+      float zr[12];
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        zr[reg] = c00[reg];
+        zr[4 + reg] = c01[reg];
+        zr[8 + reg] = c11[reg];
+      }
+      float hacc = 0.f;
+      {
+        const floatx4* ql = reinterpret_cast<const floatx4*>(&qlane[lanev & 63][0]);
+#pragma unroll
+        for (int q4 = 0; q4 < 3; ++q4) {
+          const floatx4 qv = ql[q4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hacc += zr[4 * q4 + k] * qv[k];
+        }
+        const floatx4 qd = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * r32]);
+        if (h == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hacc += dn[k] * qd[k];
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
+      const float p = 1.f / (1.f + expf(-(hacc + cc)));
+      if (lanev == 0) ta.y[b] = p;
+      {  // keras binary_crossentropy on probabilities (loss.hip bce_term / bce_bwd_kernel)
+        const float pc = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
+        loss += -(lb * logf(pc + ta.eps) + (1.f - lb) * logf((1.f - pc) + ta.eps));
+      }
+      const bool inside = p >= ta.eps && p <= 1.f - ta.eps;
+      const float pcg = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
+      const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
+      const float dp = inside ? ta.gscale * dbce : 0.f;
+      const float G = dp * (p * (1.f - p));
+      s_top += G;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ad[k] += dn[k] * G;
+      // (5) U = (M + Mᵀ)·X per 16-column tile, written back over the tile
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        constexpr int KK = kDxRows / 4;
+        float bv[KK];
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) bv[kk] = X[(4 * kk + g) * kDxLdx + 16 * t + r];
+        floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
+          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
+          X[i0 * kDxLdx + 16 * t + r] = d0[reg];
+          if (i1 < kDxRows) X[i1 * kDxLdx + 16 * t + r] = d1[reg];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // (6) G·U rows: a half-wave per 512-B row (rows past S are skipped)
+      float* de = ta.grad_emb + b * S * (int64_t)D;
+#pragma unroll
+      for (int s2 = 0; s2 < kDxRows / 2; ++s2) {
+        const int i = 2 * s2 + h;
+        if (i < S) {
+          floatx4 v = *reinterpret_cast<const floatx4*>(&X[i * kDxLdx + 4 * r32]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = __fmul_rn(G, v[c]);
+          *reinterpret_cast<floatx4*>(de + i * D + 4 * r32) = v;
+        }
+      }
+      {  // (7) the bottom-MLP row: this lane's two dims d = 4*r32 + 2h + k get G·(U + q_d)
+         // through the bottom chain's relu (h_d > 0); A_bot += x ⊗ g, s_bot += g
+        const floatx4 v = *reinterpret_cast<const floatx4*>(&X[S * kDxLdx + 4 * r32]);
+        const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * r32]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int c = 2 * h + k;
+          const float gd = __fmul_rn(G, v[c] + qdn[c]);
+          const float gb = dn[c] > 0.f ? gd : 0.f;
+          sbot[k] += gb;
+#pragma unroll
+          for (int ii = 0; ii < kTrainNI; ++ii) abot[k][ii] += xb[ii] * gb;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  // the wave's partial row → its LDS region, then the block folds its four waves in order
+  __syncthreads();
+  for (int e = lane; e < kTrainM; e += 64) X[e] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  if (active) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i0 = 4 * g + reg, j0 = r, i1 = 4 * g + reg, j1 = 16 + r, i2 = 16 + 4 * g + reg, j2 = 16 + r;
+      if (i0 < j0) X[compact_index(i0, j0, F, 0)] = az[reg];
+      if (j1 < F) X[compact_index(i1, j1, F, 0)] = az[4 + reg];
+      if (i2 < j2 && j2 < F) X[compact_index(i2, j2, F, 0)] = az[8 + reg];
+    }
+    if (h == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) X[nzc + 4 * r32 + k] = ad[k];
+    }
+    if (lane == 0) {
+      X[kTrainAtop] = s_top;
+      X[kTrainAtop + 1] = loss;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int d = 4 * r32 + 2 * h + k;
+#pragma unroll
+      for (int ii = 0; ii < kTrainNI; ++ii) X[kTrainAtop + 2 + ii * 128 + d] = abot[k][ii];
+      X[kTrainAtop + 2 + kTrainNI * 128 + d] = sbot[k];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kTrainM; e += 256) {
+    float v = lds[0][e];
+    v += lds[1][e];
+    v += lds[2][e];
+    v += lds[3][e];
+    ta.part[(int64_t)blockIdx.x * kTrainM + e] = v;
+  }
+  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+}
+
 template <int GREG, int KS, bool ID64>
 static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode md,
                           const float* gout, int64_t gstride, float* gemb, float* gdense, int,
@@ -1249,4 +1549,49 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
   }
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
+  // one partial row per block (at most ceil(batch / 4) blocks) + the fold's 32 segment rows
+  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
+}
+
+extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D,
+                                          const void* ids, int32_t id_dtype, int32_t n_slots,
+                                          const int64_t* slot_offsets, const float* dense,
+                                          const float* xin, int32_t n_in, const float* label,
+                                          int64_t batch, const float* q, const float* c,
+                                          float eps, int32_t reduction, float* y,
+                                          float* grad_emb, float* sums, void* workspace,
+                                          size_t ws_bytes, int32_t* err_flag, void* stream) {
+  const int F = n_slots + 1;
+  RS_CHECK_ARG(D == 128 && n_slots >= 1 && F <= kDxRows && n_in == kTrainNI && batch >= 1,
+               "rs_dlrm_train_step_fwd: needs D = 128, at most %d slots, %d dense inputs",
+               kDxRows - 1, kTrainNI);
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(reduction == 1 || reduction == 2, "reduction must be 1 (sum) or 2 (mean)");
+  RS_CHECK_ARG(table && ids && dense && xin && label && q && c && y && grad_emb && sums && workspace,
+               "null pointer");
+  RS_CHECK_ARG(al16(table) && al16(dense) && al16(grad_emb), "table, dense and grad rows must be 16-byte aligned");
+  RS_CHECK_ARG(ws_bytes >= rs_dlrm_train_workspace_size(batch), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
+  float* part = static_cast<float*>(workspace);
+  TrainArgs ta{q, c, label, xin, eps, reduction == 2 ? 1.f / (float)batch : 1.f, y, grad_emb, part};
+  int64_t blocks = 0;
+  auto go = [&](auto kern) {
+    static int epw_cached = 0;
+    static int64_t batch_cached = -1;
+    if (batch != batch_cached) {
+      epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch);
+      batch_cached = batch;
+    }
+    const int epw = epw_cached;
+    blocks = ceil_div(batch, 4 * (int64_t)epw);
+    kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, epw);
+  };
+  if (id_dtype == RS_ID_I64) go(dlrm_train_pipe<true>);
+  else go(dlrm_train_pipe<false>);
+  RS_CHECK_LAUNCH();
+  return fold_two_level(part, (int)blocks, kTrainM, part + (size_t)blocks * kTrainM, sums, st);
 }

@@ -34,10 +34,14 @@ class TrainStep:
 
     def __init__(self, model, optimizer="sgd", lr=None, loss_reduction="mean", sched=None,
                  fused=True, overlap_wgrad=False, comm=None, defer_sparse_join=False,
-                 overlap_param_grads=False):
+                 overlap_param_grads=False, fused_step=True):
         """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
         all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
-        by its owners inside the backward."""
+        by its owners inside the backward.
+        fused_step: the production DLRM step (D = 128, composed / factored MLP chains, fused
+        sparse optimizer, one GPU) runs its forward, loss and backward reductions in one kernel
+        (functional.dlrm_fused_train_forward) instead of autograd over the fused interaction;
+        other configurations take the autograd path."""
         from ..sharded import ShardedSlabEmbedding
 
         self.model = model
@@ -50,6 +54,8 @@ class TrainStep:
         if self.sharded:
             fused = False
         self.loss_reduction = loss_reduction
+        self.fused_step = bool(fused_step)
+        self.overlap_wgrad, self.overlap_pgrad = overlap_wgrad, overlap_param_grads
         # measured on MI355X: a weight-grad GEMM beside the interaction backward only
         # time-slices the CUs (no net gain), so the overlap is opt-in
         self.wgrad = overlapped_weight_grads(dense[0].device) if overlap_wgrad else None
@@ -149,12 +155,45 @@ class TrainStep:
 
         return replay
 
+    def fused_step_ready(self, batch) -> bool:
+        """True when __call__ takes the one-kernel production DLRM step."""
+        from ..embedding import Embedding
+        from ..nn import narrow_chain_hip_ready, vec_chain_ready
+        from .layers import MLP
+        from .model import DLRM
+
+        m = self.model
+        if not (self.fused_step and isinstance(m, DLRM) and m.compact and not self.sharded
+                and self.opt_sparse.fused and (self.comm is None or self.comm.world == 1)
+                and not self.overlap_wgrad and not self.overlap_pgrad
+                and self.loss_reduction in ("mean", "sum") and torch.is_grad_enabled()):
+            return False
+        emb = m.embedding_layer
+        cat, dense_x, _ = batch
+        B = cat.numel() // m.num_cat_fea
+        bl, tl = list(m.bottom_mlp.mlp), list(m.top_mlp.mlp)
+        return (isinstance(emb, Embedding) and emb.output_dim == 128 and m.num_cat_fea <= 27
+                and m.num_int_fea == 13 and cat.is_cuda and emb.weight.data_ptr() % 16 == 0
+                and MLP.factored_backward and MLP.composed_forward and B >= MLP.factored_min_batch
+                and all(l.act_code == 0 for l in bl[:-1] + tl[:-1])
+                and bl[-1].act_code == 1 and tl[-1].act_code == 2
+                and narrow_chain_hip_ready(bl, m.num_int_fea)
+                and vec_chain_ready(tl, m.compact_rows.numel()))
+
     def __call__(self, batch):
         cat, dense_x, label = batch
         if self._sched is not None:
             for g in self.opt_dense.param_groups:
                 g["lr"] = self._sched(self.opt_sparse.iterations)
         self.opt_dense.zero_grad(set_to_none=True)
+        if self.fused_step_ready(batch):
+            from ..functional import dlrm_fused_train_forward
+
+            y, loss = dlrm_fused_train_forward(self.model, cat, dense_x, label, self.loss_reduction)
+            self.last_pred = y
+            self.opt_dense.step()
+            self.opt_sparse.step()
+            return loss
         p = self.model({"cat_features": cat, "int_features": dense_x})
         self.last_pred = p.detach()
         loss = binary_crossentropy(label, p, reduction=self.loss_reduction)

@@ -320,3 +320,75 @@ class _BCE(torch.autograd.Function):
 def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float = 1e-7):
     """Fused keras binary_crossentropy on probabilities (one kernel forward, one backward)."""
     return _BCE.apply(y_pred, y_true, reduction, epsilon)
+
+
+TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
+
+
+def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
+                             epsilon=1e-7):
+    """The production DLRM train step's forward + loss + backward reductions in one kernel
+    (rs_dlrm_train_step_fwd): the reference's DLRM.call (ctr/model.py:45-57) under the mean
+    Keras BCE (ctr/train.py:85) with the SGD path's gradients (ctr/train.py:77-79).
+
+    Runs: the side-stream radix sort of the ids; the bottom MLP as its composed affine map
+    (ctr/layers.py:8: hidden layers linear); the fused kernel (gather, MFMA interaction, composed
+    top MLP head, BCE, G = σ'·dL/dy, the table gradient rows, and the deterministic batch sums
+    A_top, s_top, loss, A_bot, s_bot); every top / bottom MLP parameter gradient from those sums
+    (nn.chain_param_grads: the factored backward's weight-sized products), accumulated into
+    .grad; the segmented-sum sparse update queued on the fused optimizer's side stream.
+    Returns (prediction y [B] (detached), loss scalar tensor (no autograd graph))."""
+    from .nn import _composed_forward_hip, chain_param_grads, vec_chain_compose
+
+    emb = model.embedding_layer
+    S, n_in = model.num_cat_fea, model.num_int_fea
+    ids = _ids_flat(cat_features.reshape(-1, S))
+    emb.presort(ids)  # the sort runs beside the bottom MLP and the fused kernel
+    x = int_features.reshape(-1, n_in).float().contiguous()
+    lab = label.reshape(-1).float().contiguous()
+    B = ids.shape[0]
+    bl = list(model.bottom_mlp.mlp)
+    tl = list(model.top_mlp.mlp)
+    rows = model.compact_rows
+    width = rows.numel()
+    with torch.no_grad():
+        got = _composed_forward_hip(x, bl, None)
+        if got is None:
+            raise RuntimeError("fused DLRM step: the bottom MLP is not a narrow composed chain")
+        h, bks = got
+        q, c = vec_chain_compose(tl, rows, width)
+    w = emb.weight
+    D = w.shape[1]
+    dev = w.device
+    _wait_update(emb)
+    y = torch.empty(B, device=dev, dtype=torch.float32)
+    grad = torch.empty(B * S, D, device=dev, dtype=torch.float32)
+    M = TRAIN_SUMS_ATOP + 2 + n_in * D + D
+    sums = torch.empty(M, device=dev, dtype=torch.float32)
+    ws = _train_ws(B, dev)
+    L.call("rs_dlrm_train_step_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids), L.id_dtype_code(ids), S,
+           L.ptr(emb.slot_offsets), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B, L.ptr(q), L.ptr(c),
+           float(epsilon), 2 if reduction == "mean" else 1, L.ptr(y), L.ptr(grad), L.ptr(sums),
+           L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
+    a = TRAIN_SUMS_ATOP
+    A_top, s_top = sums[:a].view(a, 1)[:width], sums[a:a + 1]
+    loss_sum = sums[a + 1]
+    A_bot = sums[a + 2:a + 2 + n_in * D].view(n_in, D)
+    s_bot = sums[a + 2 + n_in * D:]
+    chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
+    chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
+    emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+    loss = loss_sum / B if reduction == "mean" else loss_sum
+    return y, loss
+
+
+_train_ws_cache: dict = {}
+
+
+def _train_ws(B, dev):
+    nb = L.lib().rs_dlrm_train_workspace_size(B)
+    t = _train_ws_cache.get(dev)
+    if t is None or t.numel() < nb:
+        t = torch.empty(nb, dtype=torch.uint8, device=dev)
+        _train_ws_cache[dev] = t
+    return t

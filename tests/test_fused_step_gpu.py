@@ -1,0 +1,93 @@
+"""The one-kernel production DLRM step (functional.dlrm_fused_train_forward /
+rs_dlrm_train_step_fwd: forward, mean BCE, G, table gradient rows and the MLP chains' batch
+reductions in one pass) against the autograd path over the same kernels (TrainStep
+fused_step=False), and against the CPU oracle on a small slab (oracle/check_dlrm.py; the
+north-star size is tests/test_northstar_gpu.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.check_dlrm import checked_dlrm_sgd_step
+from recommender_amd.ctr.layers import MLP
+from recommender_amd.ctr.train import TrainStep, build_model
+from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+from tests.conftest import assert_close_rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture
+def factored_any_batch():
+    old = MLP.factored_min_batch
+    MLP.factored_min_batch = 0
+    yield
+    MLP.factored_min_batch = old
+
+
+def _model(cards, seed, bottom, top):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return build_model("DLRM", 128, sum(cards), 26, 13, torch.device(DEV), slot_cardinalities=cards,
+                       bottom=bottom, top=top, generator=g)
+
+
+@pytest.mark.parametrize("reduction", ["mean", "sum"])
+@pytest.mark.parametrize("bottom,top", [([64, 128], [64, 32, 1]), ([512, 256, 128], [512, 256, 1])])
+def test_fused_step_matches_autograd_path(factored_any_batch, reduction, bottom, top):
+    cards = criteo_cardinalities(300_000, 26)
+    rng = np.random.default_rng(11)
+    batches = []
+    for _ in range(3):
+        cat, dn, lb = criteo_batch(rng, 2048, cards)
+        batches.append(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+    runs = []
+    for fused in (True, False):
+        m = _model(cards, 3, bottom, top)
+        st = TrainStep(m, "sgd", lr=0.05, loss_reduction=reduction, defer_sparse_join=True,
+                       fused_step=fused)
+        assert st.fused_step_ready(batches[0]) == fused
+        losses, preds = [], []
+        for b in batches:
+            losses.append(float(st(b)))
+            preds.append(st.last_pred.reshape(-1).clone())
+        m.embedding_layer.wait_update()
+        torch.cuda.synchronize()
+        runs.append((m, losses, preds))
+    (mf, lf, pf), (ma, la, pa) = runs
+    for a, b in zip(lf, la):
+        assert abs(a - b) <= 1e-5 * abs(b), (lf, la)
+    for a, b in zip(pf, pa):
+        assert_close_rel(a.cpu().numpy(), b.cpu().numpy(), 1e-5, 1e-3, "predictions")
+    pa_ = dict(ma.named_parameters())
+    for n, p in mf.named_parameters():
+        if n.endswith("grad_handle"):
+            continue
+        # three SGD steps from one init: compare the parameter CHANGE. Both are fp32 batch sums
+        # with cancellation (2048 examples, other orders): 1e-4 relative with a floor of 5% of
+        # the tensor's largest change; the float64-oracle bound checks are
+        # test_fused_step_vs_oracle_small_slab and tests/test_northstar_gpu.py
+        ref = pa_[n].detach()
+        init = dict(_model(cards, 3, bottom, top).named_parameters())[n].detach()
+        d_f, d_a = (p.detach() - init).cpu().numpy(), (ref - init).cpu().numpy()
+        assert_close_rel(d_f, d_a, 1e-4, np.abs(d_a).max() * 5e-2 + 1e-30, n)
+    w0 = _model(cards, 3, bottom, top).embedding_layer.weight
+    d_f = (mf.embedding_layer.weight - w0)
+    d_a = (ma.embedding_layer.weight - w0)
+    touched = (d_a != 0).any(1)
+    assert int(touched.sum()) > 1000
+    assert_close_rel(d_f[touched].cpu().numpy(), d_a[touched].cpu().numpy(), 1e-4,
+                     float(d_a.abs().max()) * 5e-2, "table change")
+
+
+def test_fused_step_vs_oracle_small_slab(factored_any_batch):
+    """oracle/check_dlrm.py on the fused step: loss / logits 1e-5, grad rows 1e-5 of their bound,
+    touched rows bit-exact against the oracle apply of the kernel's rows (two steps)."""
+    cards = criteo_cardinalities(200_000, 26)
+    m = _model(cards, 4, [128, 64, 128], [128, 64, 1])
+    st = TrainStep(m, "sgd", lr=0.05, fused=True, defer_sparse_join=True)
+    rng = np.random.default_rng(4)
+    for _ in range(2):
+        cat, dn, lb = criteo_batch(rng, 1024, cards)
+        assert st.fused_step_ready(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+        r = checked_dlrm_sgd_step(m, st, cat, dn, lb, 0.05)
+        print(r)
