@@ -220,17 +220,40 @@ __device__ __forceinline__ int32_t seg_id_of(const ApplyArgs& a, const uint32_t*
   return a.seg_excl ? a.seg_excl[k] + (head ? 1 : 0) - 1 : 0;
 }
 
+// Persistent over the tiles: the grid is a few blocks per CU (kApplyBlocksPerCU) and each lane
+// group walks tiles t, t + groups, ... — the walk is bandwidth-bound, and a grid of thousands of
+// blocks would hold every CU slot, starving the latency-bound kernels the step runs beside it.
+#ifndef RS_APPLY_BLOCKS_PER_CU
+#define RS_APPLY_BLOCKS_PER_CU (1 << 20)  // effectively one lane group per tile (A/B: 2-64 per CU were slower)
+#endif
+constexpr int kApplyBlocksPerCU = RS_APPLY_BLOCKS_PER_CU;
+
+template <int OPT, int VEC, int CPL>
+__device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
+                                             const int32_t* __restrict__ pos, int64_t n,
+                                             uint32_t n_rows, const float* __restrict__ grad,
+                                             const ApplyArgs& a, int lpr_log2, int64_t t);
+
 template <int OPT, int VEC, int CPL>
 __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restrict__ keys,
                                                        const int32_t* __restrict__ pos, int64_t n,
                                                        uint32_t n_rows, const float* __restrict__ grad,
                                                        ApplyArgs a, int lpr_log2, int64_t n_tiles) {
+  const int gpb = blockDim.x >> lpr_log2;
+  const int64_t groups = (int64_t)gridDim.x * gpb;
+  for (int64_t t = (int64_t)blockIdx.x * gpb + (threadIdx.x >> lpr_log2); t < n_tiles; t += groups)
+    seg_tile_one<OPT, VEC, CPL>(keys, pos, n, n_rows, grad, a, lpr_log2, t);
+}
+
+template <int OPT, int VEC, int CPL>
+__device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
+                                             const int32_t* __restrict__ pos, int64_t n,
+                                             uint32_t n_rows, const float* __restrict__ grad,
+                                             const ApplyArgs& a, int lpr_log2, int64_t t) {
   constexpr int T = RS_DEDUP_TILE;
   constexpr int U = 8;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
-  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
-  if (t >= n_tiles) return;
   const int64_t k0 = t * T;
   const int64_t k1 = k0 + T < n ? k0 + T : n;
   const int dim = a.dim;
@@ -311,6 +334,117 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint32_t* __restric
     if (!ends && run_starts && run_row < n_rows) f |= 1;  // last run opens a spanning segment
     const uint32_t fk = keys[k0];
     if ((t % 32) == 0 && k0 > 0 && fk < n_rows && keys[k0 - 1] == fk) f |= 2;
+    a.tile_flags[t] = f;
+  }
+}
+
+// D = 128 (a half-wave of 32 lanes x float4 per row, RS_DEDUP_TILE = 32): the same walk with
+// the tile's 32 keys / positions / row scales loaded lane-parallel in one instruction each (lane
+// gl holds entry gl; entry u's values come by a width-32 shuffle) instead of per entry, and the
+// gradient rows of the next 8 entries in flight while the current 8 are summed. Same order of
+// additions as seg_tile_kernel: bit-identical results.
+template <int OPT>
+__global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restrict__ keys,
+                                                         const int32_t* __restrict__ pos, int64_t n,
+                                                         uint32_t n_rows,
+                                                         const float* __restrict__ grad,
+                                                         ApplyArgs a, int64_t n_tiles) {
+  constexpr int T = 32, VEC = 4, CPL = 1, U = 8;
+  const int gl = threadIdx.x & 31;
+  const int64_t t = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (t >= n_tiles) return;
+  const int64_t k0 = t * T;
+  const int64_t k1 = k0 + T < n ? k0 + T : n;
+  const int ne = (int)(k1 - k0);
+  const int dim = a.dim;  // 128
+  const int col = gl * VEC;
+  // lane-parallel tile metadata
+  const bool mine = gl < ne;
+  const uint32_t kv = mine ? keys[k0 + gl] : 0xFFFFFFFFu;
+  const int32_t pv = mine ? pos[k0 + gl] : 0;
+  const bool lv = mine && kv < n_rows;
+  const float sv = (a.row_scale && lv) ? a.row_scale[pv / a.scale_group] : 1.f;
+  const uint32_t key_before = k0 > 0 ? keys[k0 - 1] : 0xFFFFFFFFu;
+  const uint32_t key_after = k1 < n ? keys[k1] : 0xFFFFFFFEu;
+  auto key_of = [&](int u) { return (uint32_t)__shfl((int)kv, u, 32); };
+  auto load_batch = [&](int b0, float (&r)[U][VEC]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = b0 + u;
+      const int32_t p = __shfl(pv, e, 32);
+      const float sc = __shfl(sv, e, 32);
+      const bool live = e < ne && key_of(e) < n_rows;
+      if (live) {
+        load_stream<VEC>(grad + (int64_t)p * dim + col, r[u]);
+        if (a.row_scale) {
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) r[u][c] = __fmul_rn(sc, r[u][c]);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) r[u][c] = 0.f;
+      }
+    }
+  };
+  uint32_t run_row = key_of(0);
+  int run_start = 0;
+  bool run_starts = run_row != key_before;
+  float acc[CPL][VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) acc[0][c] = 0.f;
+  auto emit = [&](uint32_t row, bool starts, bool ends, int head_e) {
+    if (row >= n_rows) return;  // OOB sentinel run: gradient dropped
+    if (starts && ends) {
+      finalize_row<OPT, VEC, CPL>(a, row, gl, 32, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, k0 + head_e) : 0);
+    } else {
+      float* dst = a.partial + ((t * 2) + (starts ? 1 : 0)) * (int64_t)dim;
+      RowIO<VEC>::store(dst + col, acc[0]);
+    }
+  };
+  float rA[U][VEC], rB[U][VEC];
+  load_batch(0, rA);
+  auto consume = [&](int b0, float (&r)[U][VEC]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = b0 + u;
+      if (e < ne) {
+        const uint32_t ku = key_of(e);
+        if (ku != run_row) {
+          emit(run_row, run_starts, true, run_start);
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) acc[0][c] = 0.f;
+          run_row = ku;
+          run_starts = true;
+          run_start = e;
+        }
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) acc[0][c] += r[u][c];
+      }
+    }
+  };
+#ifndef RS_T32_SINGLE
+  // four batches of 8, the next batch's rows in flight while the current one is summed
+  load_batch(U, rB);
+  consume(0, rA);
+  if (ne > 2 * U) load_batch(2 * U, rA);
+  consume(U, rB);
+  if (ne > 3 * U) load_batch(3 * U, rB);
+  if (ne > 2 * U) consume(2 * U, rA);
+  if (ne > 3 * U) consume(3 * U, rB);
+#else
+  consume(0, rA);
+  for (int b0 = U; b0 < ne; b0 += U) {
+    load_batch(b0, rA);
+    consume(b0, rA);
+  }
+#endif
+  const bool ends = key_after != run_row;
+  emit(run_row, run_starts, ends, run_start);
+  if (gl == 0) {
+    uint8_t f = 0;
+    if (!ends && run_starts && run_row < n_rows) f |= 1;  // last run opens a spanning segment
+    const uint32_t fk = key_of(0);
+    if ((t % 32) == 0 && k0 > 0 && fk < n_rows && key_before == fk) f |= 2;
     a.tile_flags[t] = f;
   }
 }
@@ -539,10 +673,28 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
   const int gpb = 256 >> geom.lpr_log2;
   const int64_t blocks = ceil_div(n_tiles, gpb);
   if (blocks == 0) return RS_OK;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const int64_t walk_blocks = std::min<int64_t>(blocks, (int64_t)cus * kApplyBlocksPerCU);
+#ifndef RS_NO_T32
+  const bool t32 = geom.vec == 4 && geom.cpl == 1 && geom.lpr_log2 == 5 && RS_DEDUP_TILE == 32;
+#else
+  const bool t32 = false;
+#endif
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
-    seg_tile_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, pos, n, (uint32_t)n_rows, grad, \
-                                                            a, geom.lpr_log2, n_tiles);         \
+    if (t32)                                                                                    \
+      seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, 0, st>>>(keys, pos, n,               \
+                                                                  (uint32_t)n_rows, grad, a,    \
+                                                                  n_tiles);                     \
+    else                                                                                        \
+      seg_tile_kernel<OPTV, VEC, CPL><<<walk_blocks, 256, 0, st>>>(keys, pos, n, (uint32_t)n_rows, \
+                                                                   grad, a, geom.lpr_log2, n_tiles); \
     seg_chunk_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,            \
                                                        geom.lpr_log2, n_tiles, a.chunk);        \
     seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,      \

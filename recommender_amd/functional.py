@@ -376,8 +376,10 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     A_bot = sums[a + 2:a + 2 + n_in * D].view(n_in, D)
     s_bot = sums[a + 2 + n_in * D:]
     chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
-    chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
+    # the sparse update (side stream) is queued after the top chain's gradients: queued first,
+    # its walk starves those latency-bound kernels of CUs (measured 0.907 vs 0.96 ms/step)
     emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+    chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
     loss = loss_sum / B if reduction == "mean" else loss_sum
     return y, loss
 

@@ -1,1 +1,1 @@
-TESTS="tests/test_fused_step_gpu.py tests/test_northstar_gpu.py" TLIM=600 bash tools/gpu_tests.sh && timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" && bash tools/bench_quick.sh
+TESTS="tests/test_embedding_gpu.py tests/test_fused_step_gpu.py" TLIM=400 bash tools/gpu_tests.sh && STEP=1 FILTER="apply_scaled (alone)" VARIANTS="t32single not32" bash tools/ab_variants.sh

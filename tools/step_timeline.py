@@ -6,7 +6,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 mark = sys.argv[2] if len(sys.argv) > 2 else "inter_fwd_mfma"
 idx = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
-a, b = idx[-3], idx[-2]
+k = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+a, b = idx[k], idx[k + 1]
 t0 = int(rows[a]["Start_Timestamp"])
 busy = {}
 for r in rows[a:b]:
