@@ -99,3 +99,38 @@ def esmm_family_step(model, table, slot_offsets, feats: dict, label):
     leaves = flat_params(P)
     grads = torch.autograd.grad(loss, leaves + [E])
     return float(loss.detach()), y.detach(), list(grads[:-1]), grads[-1].reshape(-1, table.shape[1])
+
+
+# ---- EGES / GES / DeepWalk (eges/model.py:20-102, eges/train.py:14-24) ---------------------
+def eges_step(model, inputs, labels):
+    """Loss (sigmoid CE on the 1 + num_ns skip-gram logits, reduce_mean) and, per table, its
+    gradient rows in lookup-position order, by torch autograd in fp32 on gathered copies of the
+    rows: DeepWalk: hidden = Emb_in(q); GES: mean of the id / cat / brand rows; EGES:
+    softmax(Emb_w(q)) · [id, cat, brand] rows; logits = Emb_out(match) · hiddenᵀ.
+    Returns (loss, logits, {table name: (ids [N] int64, rows [N, D])})."""
+    kind = type(model).__name__
+    looked = {}
+
+    def rows(name, ids):
+        E = getattr(model, name).weight[ids.long()].detach().clone().requires_grad_(True)
+        looked[name] = (ids.reshape(-1).long(), E)
+        return E
+
+    if kind == "DeepWalk":
+        q, m = inputs
+        hidden = rows("input_embedding", q)                                   # [B, 1, D]
+    else:
+        q, c, b, m = inputs
+        side = torch.cat([rows("id_embedding", q), rows("cat_embedding", c),
+                          rows("brand_embedding", b)], 1)                     # [B, 3, D]
+        if kind == "EGES":
+            hidden = torch.matmul(torch.softmax(rows("weight_embedding", q), -1), side)
+        else:
+            hidden = (side[:, 0:1] + side[:, 1:2] + side[:, 2:3]) / 3
+    logits = torch.matmul(rows("output_embedding", m), hidden.transpose(1, 2)).squeeze(-1)
+    z, x = labels, logits
+    loss = (torch.clamp(x, min=0) - x * z + torch.log1p(torch.exp(-x.abs()))).mean()
+    names = list(looked)
+    grads = torch.autograd.grad(loss, [looked[n][1] for n in names])
+    out = {n: (looked[n][0], g.reshape(-1, g.shape[-1])) for n, g in zip(names, grads)}
+    return float(loss.detach()), logits.detach(), out

@@ -137,3 +137,54 @@ def test_train_steps_reduce_loss(rng, model_type):
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
     e = model.get_hidden(inp[0] if model_type == "BGE" else tuple(inp[:3]))
     assert e.shape == (512, 1, 32)
+
+
+@pytest.mark.parametrize("model_type", ["BGE", "GES", "EGES"])
+def test_train_step_vs_oracle(rng, model_type):
+    """One EGESStep (eges/train.py:14-24: sigmoid CE mean, Keras Adam on every table) against
+    oracle/models.py eges_step from the same state: loss 1e-5, each table's gradient rows 1e-4
+    (floor 1e-2 of the largest), and every table / m / v BIT-EXACT vs the oracle's tiled dedup +
+    Keras apply of the kernel's own rows (oracle/embedding.py)."""
+    from oracle import embedding as OE
+    from oracle.models import eges_step
+
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    model = build(model_type, 2000, 50, 70, embedding_size=32, generator=gen)
+    step = EGESStep(model, lr=1e-2)
+    *inp, lab = synthetic_batch(rng, 256, 2000, 50, 70)
+    inp = [torch.from_numpy(a).to(DEV) for a in inp]
+    if model_type == "BGE":
+        inp = [inp[0], inp[3]]
+    lab = torch.from_numpy(lab).to(DEV)
+    names = {id(getattr(model, n)): n for n in ("input_embedding", "output_embedding", "id_embedding",
+                                                 "cat_embedding", "brand_embedding", "weight_embedding")
+             if hasattr(model, n)}
+    before = {n: getattr(model, n).weight.detach().cpu().numpy().copy() for n in names.values()}
+    ref_loss, ref_logits, ref_rows = eges_step(model, tuple(inp), lab)
+    cap = {}
+    apply = step.opt.apply
+
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
+        cap[names[id(table)]] = (ids.reshape(-1).long(), grad_rows.reshape(-1, table.output_dim), params)
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
+
+    step.opt.apply = spy
+    loss = float(step(tuple(inp), lab))
+    torch.cuda.synchronize()
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    assert set(cap) == set(ref_rows)
+    co = OE.keras_adam_coefficients(1, 1e-2)
+    for n, (ids, rows, _) in cap.items():
+        rids, rrows = ref_rows[n]
+        assert torch.equal(ids, rids), n
+        assert_close_rel(rows.cpu().numpy(), rrows.cpu().numpy(), 1e-4,
+                         float(rrows.abs().max()) * 1e-2, n)
+        t = getattr(model, n)
+        m_t, v_t, _ = step.opt._slots(t)
+        sr, sp, _ = OE.sort_ids(ids.cpu().numpy(), t.input_dim)
+        ur, ug = OE.segment_sum_tiled(sr, sp, rows.cpu().numpy(), t.input_dim)
+        zeros = np.zeros_like(before[n])
+        w2, m2, v2 = OE.apply_keras_adam(before[n], zeros, zeros, ur.astype(np.int64), ug, co)
+        np.testing.assert_array_equal(t.weight.cpu().numpy(), w2, err_msg=n)
+        np.testing.assert_array_equal(m_t.cpu().numpy(), m2, err_msg=n)
+        np.testing.assert_array_equal(v_t.cpu().numpy(), v2, err_msg=n)
