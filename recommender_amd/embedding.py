@@ -47,6 +47,8 @@ class Embedding(nn.Module):
         # its side stream ahead of the dense forward, the apply inside the backward
         self.fused_optimizer = None
         self._presorted = None
+        # sorts queued ahead for later steps (Embedding.prefetch), keyed by the ids' storage
+        self._prefetched: dict = {}
         # deferred join (SparseOptimizer(defer_join=True)): the event the next table read waits on
         self._pending_update = None
 
@@ -68,13 +70,38 @@ class Embedding(nn.Module):
         return ids != 0 if self.mask_zero else None
 
     # ---- fused-optimizer plumbing ----
+    @staticmethod
+    def _ids_key(ids: torch.Tensor):
+        return (ids.data_ptr(), tuple(ids.shape), ids.dtype, ids.device)
+
+    def prefetch(self, ids: torch.Tensor):
+        """Queue the radix sort of a LATER step's ids now, on the fused optimizer's sort stream
+        (ordered after everything queued so far on the current stream, so `ids` must already be
+        written or queued). Call it before the step that precedes the one using `ids`: the sort
+        then runs beside this step's kernels instead of delaying the next one. The ids must not
+        change until their step has run; a step whose ids match a prefetched sort (same storage,
+        shape and dtype) uses it, any other step sorts as usual."""
+        opt = self.fused_optimizer
+        if opt is None or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing():
+            return
+        key = self._ids_key(ids)
+        if key not in self._prefetched:
+            if len(self._prefetched) >= 4:  # stale entries (steps that never ran)
+                self._prefetched.pop(next(iter(self._prefetched)))
+            # the entry holds the ids (their storage cannot be reused while it waits) and their
+            # version counter (an in-place change before the step voids it)
+            self._prefetched[key] = (ids, ids._version, opt.sort_ahead(self, ids))
+
     def presort(self, ids: torch.Tensor):
         """Queue the radix sort of this step's ids on the fused optimizer's side stream. Call it
         after the step's forward kernels are queued: the host then issues the sort while the
         GPU is busy with the forward, and the sort runs beside it. The lookup's backward reuses
         it (or sorts on the spot when no presort was issued)."""
         if self.fused_optimizer is not None and torch.is_grad_enabled():
-            self._presorted = (ids, self.fused_optimizer.sort_async(self, ids))
+            e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
+            ahead = e[2] if e is not None and e[1] == ids._version else None
+            self._presorted = (ids, ahead if ahead is not None
+                               else self.fused_optimizer.sort_async(self, ids))
 
     def take_presorted(self, ids: torch.Tensor):
         p, self._presorted = self._presorted, None

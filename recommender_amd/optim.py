@@ -125,6 +125,7 @@ class SparseOptimizer:
         self.defer_join = bool(defer_join) and fused
         self.side = None
         self._applied = set()
+        self.sort_stream, self.sort_ws = None, None
         if fused:
             dev = self.tables[0].weight.device
             self.side = torch.cuda.Stream(device=dev)
@@ -140,6 +141,22 @@ class SparseOptimizer:
         ids.record_stream(self.side)
         return s
 
+    def sort_ahead(self, table: Embedding, ids: torch.Tensor) -> SortedIds:
+        """Embedding.prefetch: the sort of a later step's ids on a stream of its own (its own
+        scratch), so it can run while this step's update still reads the current sort."""
+        dev = ids.device
+        if self.sort_stream is None:
+            self.sort_stream = torch.cuda.Stream(device=dev)
+            self.sort_ws = _Workspace()
+        ss = self.sort_stream
+        ss.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(ss):
+            s = SortedIds.for_table(table, ids, self.sort_ws, count_unique=False)
+            s.ready = torch.cuda.Event()
+            s.ready.record(ss)
+        ids.record_stream(ss)
+        return s
+
     def apply_async(self, table: Embedding, ids, grad_rows, sorted_ids: SortedIds, row_scale=None):
         """row_scale [B] (optional): the gradient row of position p is row_scale[p // S] *
         grad_rows[p] with S = ids.shape[-1] (the fused DLRM step's unit rows and G[b])."""
@@ -151,6 +168,11 @@ class SparseOptimizer:
     def _launch_apply(self, table, ids, grad_rows, sorted_ids, row_scale=None):
         main = torch.cuda.current_stream(grad_rows.device)
         self.side.wait_stream(main)
+        ready = getattr(sorted_ids, "ready", None)
+        if ready is not None:  # sorted ahead on the sort stream (Embedding.prefetch)
+            self.side.wait_event(ready)
+            sorted_ids.rows.record_stream(self.side)
+            sorted_ids.pos.record_stream(self.side)
         with torch.cuda.stream(self.side):
             self.apply(table, ids, grad_rows, self._params(), sorted_ids=sorted_ids,
                        row_scale=row_scale)

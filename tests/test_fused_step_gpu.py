@@ -91,3 +91,36 @@ def test_fused_step_vs_oracle_small_slab(factored_any_batch):
         assert st.fused_step_ready(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
         r = checked_dlrm_sgd_step(m, st, cat, dn, lb, 0.05)
         print(r)
+
+
+@pytest.mark.parametrize("fused_step", [True, False])
+def test_prefetched_sort_bit_identical(factored_any_batch, fused_step):
+    """TrainStep.prefetch (the next batch's sort queued one step ahead on its own stream) gives
+    bit-identical parameters and table to plain steps; a batch whose ids change in place after
+    the prefetch is sorted again (the stale sort is dropped)."""
+    cards = criteo_cardinalities(300_000, 26)
+    rng = np.random.default_rng(12)
+    batches = []
+    for _ in range(4):
+        cat, dn, lb = criteo_batch(rng, 2048, cards)
+        batches.append(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+    repl = torch.from_numpy(criteo_batch(rng, 2048, cards)[0]).to(DEV)
+    runs = []
+    for pre in (False, True):
+        m = _model(cards, 5, [512, 256, 128], [512, 256, 1])
+        st = TrainStep(m, "sgd", lr=0.05, defer_sparse_join=True, fused_step=fused_step)
+        bs = [tuple(t.clone() for t in b) for b in batches]
+        for i, b in enumerate(bs):
+            if pre and i + 1 < len(bs):
+                st.prefetch(bs[i + 1])
+            if i == 2:  # batch 2 was prefetched during step 1: change its ids in place now
+                b[0].copy_(repl)
+            st(b)
+        m.embedding_layer.wait_update()
+        torch.cuda.synchronize()
+        assert not m.embedding_layer._prefetched
+        runs.append(m)
+    a, b = runs
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
+    assert torch.equal(a.embedding_layer.weight, b.embedding_layer.weight)
