@@ -57,6 +57,13 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
       nr = xn[H + j];
       nh = xn[2 * H + j];
     }
+    if (!mb[t]) {
+      // masked step (wave-uniform: one example per wave): the state is carried, so the step's
+      // arithmetic is skipped — its result would be discarded; the backward never reads its
+      // saved row (post-padded histories make most of the L steps such steps)
+      if (act) out[(b * L + t) * H + j] = h;
+      continue;
+    }
     float iz = 0.f, ir = 0.f, ih = 0.f;
 #pragma unroll
     for (int k = 0; k < HM; ++k) {
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
     const float z = sigm(xz + iz), r = sigm(xr + ir);
     const float hh = tanhf(xh + r * ih);
     const float hn = z * h + (1.f - z) * hh;
-    if (mb[t]) h = act ? hn : 0.f;
+    h = act ? hn : 0.f;
     if (act) {
       const int64_t o = b * L + t;
       out[o * H + j] = h;
@@ -192,6 +199,16 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
   const float* ab = att + b * L;
   float h = 0.f;
   for (int t = 0; t < L; ++t) {
+    if (!mb[t]) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
+      if (act) {
+        const int64_t o = b * L + t;
+        if (states) states[o * H + j] = h;
+        // r⊙h_prev feeds the caller's candidate-kernel gradient GEMM, whose dxw row is 0 here:
+        // a defined 0 keeps that product exactly 0
+        if (saved) saved[o * 4 * H + 3 * H + j] = 0.f;
+      }
+      continue;
+    }
     const float* x = xb + (int64_t)t * H3;
     const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
     const float a = ab[t];
@@ -210,7 +227,7 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
     const float hh = tanhf(xh + ihh);
     const float ua = u * a;
     const float hn = ua * hh + (1.f - ua) * h;
-    if (mb[t]) h = act ? hn : 0.f;
+    h = act ? hn : 0.f;
     if (act) {
       const int64_t o = b * L + t;
       if (states) states[o * H + j] = h;
