@@ -282,6 +282,27 @@ int32_t rs_dien_attention_fwd(const float* hs, const float* q, const uint8_t* ma
 int32_t rs_dien_attention_bwd(const float* hs, const float* q, const float* a, const float* da,
                               int64_t B, int32_t L, int32_t H, float* dhs, float* dq,
                               void* stream);
+/* a-9  DIEN auxiliary loss (InterestExtract.compute_auxiliary_loss dien/layers.py:89-108 with
+ *      AuxiliaryNet([80, 40, 1]) dien/layers.py:62-73), fused: x = [h_t, e_{t+1}] for
+ *      e = pos / neg history embeddings, z = σ(σ(x·W1+b1)·W2+b2)·W3+b3,
+ *      aux[b] = Σ_t m[b,t+1]·(ce(z_pos,1) + ce(z_neg,0)) / (2·Σ_t m[b,t+1]).
+ *      hidden [B,L,H] (GRU states), pos/neg [B,L,E], mask [B,L] u8; W1 [H+E,80], b1 [80],
+ *      W2 [80,40], b2 [40], W3 [40], b3 [1] (Keras [in, out] kernels). Rows with m = 0 add
+ *      exactly 0 and are not evaluated. Built for (H, E) = (36, 36) and (16, 16); other widths
+ *      return RS_E_UNSUPPORTED. bwd: daux [B] → dhidden [B,L,H], dpos / dneg [B,L,E] (every
+ *      element written) and dparams = [dW1 | db1 | dW2 | db2 | dW3 | db3] (overwritten,
+ *      deterministic); workspace ≥ rs_dien_aux_workspace_size(H, E) bytes. */
+size_t rs_dien_aux_workspace_size(int32_t H, int32_t E);
+int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const float* neg,
+                        const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
+                        const float* W1, const float* b1, const float* W2, const float* b2,
+                        const float* W3, const float* b3, float* aux, void* stream);
+int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const float* neg,
+                        const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
+                        const float* W1, const float* b1, const float* W2, const float* b2,
+                        const float* W3, const float* b3, const float* daux, float* dhidden,
+                        float* dpos, float* dneg, float* dparams, void* workspace,
+                        size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Keras binary_crossentropy on probabilities (ctr/train.py:85, dien/train.py:18,

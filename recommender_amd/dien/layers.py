@@ -318,6 +318,54 @@ class AuxiliaryNet(nn.Module):
         return x.view(*shp[:-1], -1)
 
 
+class _AuxLossFn(torch.autograd.Function):
+    """InterestExtract.compute_auxiliary_loss on the fused kernels (csrc/dien_aux.hip):
+    the aux net is evaluated only on the 16-row tiles that hold a valid (m = 1) row and its
+    [rows, 80] activations never reach HBM; the backward recomputes them."""
+
+    @staticmethod
+    def forward(ctx, hidden, pos, neg, mask_u8, W1, b1, W2, b2, W3, b3):
+        B, Lh, H = hidden.shape
+        E = pos.shape[-1]
+        aux = torch.empty(B, device=hidden.device)
+        ws = (hidden, pos, neg, mask_u8, B, Lh, H, E, W1, b1, W2, b2, W3, b3)
+        L.call("rs_dien_aux_fwd", *[L.ptr(x) if isinstance(x, torch.Tensor) else x for x in ws],
+               L.ptr(aux), L.stream_ptr(hidden.device))
+        ctx.save_for_backward(hidden, pos, neg, mask_u8, W1, b1, W2, b2, W3, b3)
+        return aux
+
+    @staticmethod
+    def backward(ctx, daux):
+        hidden, pos, neg, mask_u8, W1, b1, W2, b2, W3, b3 = ctx.saved_tensors
+        B, Lh, H = hidden.shape
+        E = pos.shape[-1]
+        dev = hidden.device
+        dh = torch.empty_like(hidden)
+        dp = torch.empty_like(pos)
+        dn = torch.empty_like(neg)
+        In, n1, n2 = H + E, W1.shape[1], W2.shape[1]
+        dparams = torch.empty(In * n1 + n1 + n1 * n2 + n2 + n2 + 1, device=dev)
+        nb = L.lib().rs_dien_aux_workspace_size(H, E)
+        ws = _aux_ws.get(dev)
+        if ws is None or ws.numel() < nb:
+            ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+            _aux_ws[dev] = ws
+        args = (hidden, pos, neg, mask_u8, B, Lh, H, E, W1, b1, W2, b2, W3, b3,
+                daux.contiguous(), dh, dp, dn, dparams, ws)
+        L.call("rs_dien_aux_bwd", *[L.ptr(x) if isinstance(x, torch.Tensor) else x for x in args],
+               ws.numel(), L.stream_ptr(dev))
+        o = 0
+        outs = []
+        for shape in (W1.shape, b1.shape, W2.shape, b2.shape, W3.shape, b3.shape):
+            n = int(torch.Size(shape).numel())
+            outs.append(dparams[o:o + n].view(shape))
+            o += n
+        return (dh, dp, dn, None, *outs)
+
+
+_aux_ws: dict = {}
+
+
 def _sigmoid_ce(labels, logits):
     # tf.nn.sigmoid_cross_entropy_with_logits: max(x,0) - x*z + log(1 + exp(-|x|))
     return torch.clamp(logits, min=0) - logits * labels + torch.log1p(torch.exp(-logits.abs()))
@@ -332,8 +380,24 @@ class InterestExtract(nn.Module):
         self.gru = GRU(gru_units, input_dim, device, generator)
         self.auxiliary_net = AuxiliaryNet([80, 40, 1], gru_units + input_dim, device, generator)
 
+    def _fused_aux_ready(self, hidden_state, pos_his):
+        layers = list(self.auxiliary_net.layers)
+        H, E = hidden_state.shape[-1], pos_his.shape[-1]
+        return (hidden_state.is_cuda and (H, E) in ((36, 36), (16, 16))
+                and hidden_state.shape[1] >= 2 and len(layers) == 3
+                and [l.units for l in layers] == [80, 40, 1]
+                and [l.act_code for l in layers] == [2, 2, 0]
+                and all(l.kernel is not None and l.bias is not None for l in layers)
+                and layers[0].kernel.shape[0] == H + E)
+
     def compute_auxiliary_loss(self, inputs, training=False, mask=None):
         hidden_state, pos_his, neg_his = inputs
+        if self._fused_aux_ready(hidden_state, pos_his):
+            l1, l2, l3 = self.auxiliary_net.layers
+            m = _mask_u8(mask, hidden_state.shape[:2], hidden_state.device)
+            return _AuxLossFn.apply(hidden_state.contiguous(), pos_his.contiguous(),
+                                    neg_his.contiguous(), m, l1.kernel, l1.bias, l2.kernel,
+                                    l2.bias, l3.kernel, l3.bias)
         h = hidden_state[:, :-1, :]
         m = mask[:, 1:].to(h.dtype)
         both = torch.cat([torch.cat([h, pos_his[:, 1:, :]], -1),

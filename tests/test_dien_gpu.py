@@ -239,3 +239,54 @@ def test_dien_aux_loss_vs_oracle():
                                                 (an[2].kernel, an[2].bias, None)])
     assert aux.shape == ref.shape == (512,)
     assert_close_rel(aux.cpu().numpy(), ref.cpu().numpy(), 1e-5, float(ref.abs().max()) * 1e-3, "aux")
+
+
+@pytest.mark.parametrize("H,B,L,kind", [(36, 512, 100, "post"), (36, 64, 37, "random"),
+                                        (36, 48, 17, "post"), (16, 96, 50, "random")])
+def test_fused_aux_loss_fwd_bwd_vs_oracle(H, B, L, kind, rng):
+    """The fused aux-net kernels (csrc/dien_aux.hip) forward and backward against
+    oracle/dien.aux_loss under torch autograd: aux and every input / parameter gradient within
+    2e-5 of (|value| + the tensor's largest value) — fp32 sums over different row orders. Masks:
+    post-padded (dien/data_loader.py) or arbitrary; L = 17 puts the last row on a tile edge.
+    One example has a length-1 history: its aux (0 / 0) and every parameter gradient are NaN,
+    as the reference's."""
+    from recommender_amd.dien.layers import InterestExtract
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    ie = InterestExtract(H, H, device=DEV, generator=g)
+    an = ie.auxiliary_net.layers
+    with torch.no_grad():
+        for l in an:
+            l.bias.copy_(torch.randn(l.bias.shape, generator=g, device=DEV) * 0.2)
+    if kind == "post":
+        mask = make_mask(rng, B, L)
+    else:
+        mask = torch.from_numpy(rng.random((B, L)) < 0.3).to(DEV)
+        mask[:, 1] = True
+    x = [torch.from_numpy(rng.standard_normal((B, L, H)).astype(np.float32) * 0.5).to(DEV)
+         for _ in range(3)]
+    daux = torch.from_numpy(rng.standard_normal(B).astype(np.float32)).to(DEV)
+    assert ie._fused_aux_ready(x[0], x[1])
+    got_in = [t.clone().requires_grad_(True) for t in x]
+    aux = ie.compute_auxiliary_loss(tuple(got_in), mask=mask)
+    aux.backward(daux)
+    ref_in = [t.clone().requires_grad_(True) for t in x]
+    params = [p.detach().clone().requires_grad_(True) for l in an for p in (l.kernel, l.bias)]
+    layers = [(params[0], params[1], "sigmoid"), (params[2], params[3], "sigmoid"),
+              (params[4], params[5], None)]
+    ref = OD.aux_loss(ref_in[0], ref_in[1], ref_in[2], mask, layers)
+    ref.backward(daux)
+    _close(aux, ref, "aux")
+    for got, r, n in zip([t.grad for t in got_in] + [p.grad for l in an for p in (l.kernel, l.bias)],
+                         [t.grad for t in ref_in] + [p.grad for p in params],
+                         ["dhidden", "dpos", "dneg", "dW1", "db1", "dW2", "db2", "dW3", "db3"]):
+        _close(got, r, n)
+    # a length-1 history: aux = 0 / 0 and NaN parameter gradients, as the reference
+    mask1 = mask.clone()
+    mask1[5, 1:] = False
+    for p in ie.parameters():
+        p.grad = None
+    aux1 = ie.compute_auxiliary_loss(tuple(t.clone() for t in x), mask=mask1)
+    assert torch.isnan(aux1[5]) and torch.isfinite(aux1[torch.arange(B, device=DEV) != 5]).all()
+    aux1.backward(daux)
+    assert torch.isnan(an[0].kernel.grad).all() and torch.isnan(an[2].bias.grad).all()
