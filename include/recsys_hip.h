@@ -291,8 +291,8 @@ int32_t rs_dien_attention_bwd(const float* hs, const float* q, const float* a, c
  *      exactly 0 and are not evaluated. Built for (H, E) = (36, 36) and (16, 16); other widths
  *      return RS_E_UNSUPPORTED. bwd: daux [B] → dhidden [B,L,H], dpos / dneg [B,L,E] (every
  *      element written) and dparams = [dW1 | db1 | dW2 | db2 | dW3 | db3] (overwritten,
- *      deterministic); workspace ≥ rs_dien_aux_workspace_size(H, E) bytes. */
-size_t rs_dien_aux_workspace_size(int32_t H, int32_t E);
+ *      deterministic); workspace ≥ rs_dien_aux_workspace_size(B, L, H, E) bytes. */
+size_t rs_dien_aux_workspace_size(int64_t B, int32_t L, int32_t H, int32_t E);
 int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const float* neg,
                         const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                         const float* W1, const float* b1, const float* W2, const float* b2,

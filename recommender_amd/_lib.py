@@ -69,7 +69,7 @@ _SIGS = {
     "rs_augru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_dien_attention_fwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p]),
     "rs_dien_attention_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
-    "rs_dien_aux_workspace_size": (_sz, [_i32, _i32]),
+    "rs_dien_aux_workspace_size": (_sz, [_i64, _i32, _i32, _i32]),
     "rs_dien_aux_fwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                _p, _p]),
     "rs_dien_aux_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,

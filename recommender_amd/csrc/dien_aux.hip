@@ -22,12 +22,17 @@
 // Determinism: the backward is a persistent grid with a static item → wave assignment; each wave
 // accumulates its weight gradients in registers (MFMA C tiles), writes one partial row, and the
 // partials are folded in a fixed order (fold_two_level).
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace rs {
 
 int32_t fold_two_level(const float* part, int nchunks, int N, float* part2, float* out,
                        hipStream_t st);
+int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* total, void* ws,
+                           size_t ws_bytes, hipStream_t st);
+size_t exclusive_scan_ws_size(int64_t n);
 
 namespace {
 
@@ -203,12 +208,38 @@ __global__ __launch_bounds__(256) void aux_fwd_kernel(AuxArgs a, float* __restri
 // accumulation order make the per-block partials, and their fold, deterministic.
 // ---------------------------------------------------------------------------------------
 struct AuxGrad {
-  const float* daux;  // [B]
-  float* dhidden;     // [B, L, H]
-  float* dpos;        // [B, L, E]
-  float* dneg;        // [B, L, E]
-  float* part;        // [n_blocks, n_param]
+  const float* daux;       // [B]
+  float* dhidden;          // [B, L, H]
+  float* dpos;             // [B, L, E]
+  float* dneg;             // [B, L, E]
+  float* part;             // [n_blocks, n_param]
+  const int32_t* items;    // live items (tile-major index tile·B + b), in order
+  const int32_t* n_items;  // [1] their count
+  const int32_t* cnt;      // [B] Σ_t m[b, t+1]
 };
+
+// live items: tile·B + b holds a valid row, or example b has none (0/0: NaN, as the reference)
+__global__ __launch_bounds__(256) void aux_live_kernel(AuxArgs a, int NT, int32_t* __restrict__ flag,
+                                                       int32_t* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  const int c = aux_count(a, b, lane);
+  if (lane == 0) cnt[b] = c;
+  for (int tile = 0; tile < NT; ++tile) {
+    const int t = 16 * tile + (lane & 15);
+    const bool m = t <= a.L - 2 && a.mask[b * a.L + t + 1] != 0;
+    const bool live = c == 0 || __ballot(m) != 0;
+    if (lane == 0) flag[(int64_t)tile * a.B + b] = live ? 1 : 0;
+  }
+}
+
+__global__ void aux_compact_kernel(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos,
+                                   int64_t n, int32_t* __restrict__ items) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (flag[i]) items[pos[i]] = (int32_t)i;
+}
 
 __host__ __device__ inline int aux_n_param(int In) {
   return In * kN1 + kN1 + kN1 * kN2 + kN2 + kN2 + 1;
@@ -221,6 +252,7 @@ constexpr int kTilesPerWave = (kTilesW1 + kTilesW2) / kWaves;  // 10
 constexpr int kMaxH = 76;
 
 struct SetTile {
+  float x[16 * kS1];  // [row][feature]: x = [h, e], 1 at feature In (db1), 0 after
   float h1[16 * kS1];
   float dz1[16 * kS1];
   float dz2[16 * kS2];
@@ -253,9 +285,6 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
   const int lane = threadIdx.x & 63, j = lane & 15, kq = lane >> 4, wave = threadIdx.x >> 6;
   constexpr int In = H + E;
   const int L = a.L;
-  const int NT = (L + 15) / 16;  // tiles over every hidden row t < L (rows >= L-1 get zeros)
-  const int64_t n_items = (int64_t)NT * a.B;
-  const int64_t n_pairs = (n_items + 1) / 2;
   const int io = wave >> 1, set = wave & 1;  // this wave's item of the pair, pos / neg
   SetTile& T = S.st[wave];
 
@@ -265,36 +294,28 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
   float vacc = 0.f;  // thread q < 81: dW3[q] (q < 40), db2[q-40] (q < 80), db3 (q = 80)
   __syncthreads();
 
-  for (int64_t pr = blockIdx.x; pr < n_pairs; pr += gridDim.x) {
-    const int64_t it = 2 * pr + io;
-    const bool have = it < n_items;
-    const int tile = have ? (int)(it / a.B) : 0;
-    const int64_t b = have ? it % a.B : 0;
+  const int64_t n_live = *g.n_items;
+  const int64_t n_pairs_live = (n_live + 1) / 2;
+  for (int64_t pr = blockIdx.x; pr < n_pairs_live; pr += gridDim.x) {
+    const int64_t li = 2 * pr + io;
+    const bool live = li < n_live;
+    const int64_t it = live ? g.items[li] : 0;
+    const int tile = (int)(it / a.B);
+    const int64_t b = it % a.B;
     const int t = 16 * tile + j;
-    const int cnt = have ? aux_count(a, b, lane) : 1;
-    const bool m = have && t <= L - 2 && a.mask[b * L + t + 1] != 0;
-    const bool live = have && (cnt == 0 || __ballot(m) != 0);
+    const int cnt = g.cnt[b];
+    const bool m = live && t <= L - 2 && a.mask[b * L + t + 1] != 0;
     const float* e = set == 0 ? a.pos : a.neg;
     float* de = set == 0 ? g.dpos : g.dneg;
-    if (have && tile == 0 && lane == 0) {  // e row 0 is never an aux input: its gradient is 0
-      float* z0 = de + b * L * (int64_t)E;
-      for (int c = 0; c < E; ++c) z0[c] = 0.f;
-    }
     f4 dxh[kT1];
-    if (!live) {
-      if (have) {  // no valid row: zero input gradients only
-        if (set == 0 && t < L)
-          for (int c = 4 * kq; c < H; c += 16)
-            store4(g.dhidden + (b * L + t) * (int64_t)H + c, f4{0.f, 0.f, 0.f, 0.f});
-        if (t <= L - 2)
-          for (int c = 4 * kq; c < E; c += 16)
-            store4(de + (b * L + t + 1) * (int64_t)E + c, f4{0.f, 0.f, 0.f, 0.f});
-      }
-    } else {
+    if (live) {
       // dL/d(loss sum of b) = daux_b / (2·cnt)  (0 rows → inf·0 = NaN, as the reference)
       const float sb = g.daux[b] / ((float)cnt * 2.f);
       float xv[In / 4];
       load_x<H, E>(a, e, b, t, kq, xv);
+#pragma unroll
+      for (int k = 0; k < In / 4; ++k) T.x[j * kS1 + 4 * k + kq] = xv[k];
+      for (int f = In + kq; f < kMaxIn; f += 4) T.x[j * kS1 + f] = f == In ? 1.f : 0.f;
       f4 h1[kT1], h2[kT2];
       const float z = aux_forward<H, E>(a, S.w, xv, j, kq, h1, h2);
       const float d3 = (sb * (m ? 1.f : 0.f)) * (aux_sigm(z) - (set == 0 ? 1.f : 0.f));
@@ -370,21 +391,10 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
         const SetTile& U = S.st[sidx];
         if (tq < kTilesW1) {  // dW1[16x + i][16u + n] += Σ_rows xaug[row][16x + i]·dz1[row][16u + n]
           const int x = tq / kT1, u = tq % kT1;
-          const int64_t it2 = 2 * pr + (sidx >> 1);
-          const int tile2 = (int)(it2 / a.B);
-          const int64_t b2 = it2 % a.B;
-          const float* e2 = (sidx & 1) ? a.neg : a.pos;
-          const int f = 16 * x + j;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int row = 4 * k + kq;
-            const int tr = 16 * tile2 + row;
-            float xa = 0.f;
-            if (f == In) xa = 1.f;  // bias column: db1
-            else if (f < In && tr <= L - 2)
-              xa = f < H ? a.hidden[(b2 * L + tr) * (int64_t)H + f]
-                         : e2[(b2 * L + tr + 1) * (int64_t)E + (f - H)];
-            acc[q] = mfma4(xa, U.dz1[row * kS1 + 16 * u + j], acc[q]);
+            acc[q] = mfma4(U.x[row * kS1 + 16 * x + j], U.dz1[row * kS1 + 16 * u + j], acc[q]);
           }
         } else {  // dW2[16u + i][16m + n] += Σ_rows h1[row][16u + i]·dz2[row][16m + n]
           const int t2 = tq - kTilesW1;
@@ -403,11 +413,14 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
         for (int sidx = 0; sidx < kSets; ++sidx) {
           if (!S.live[sidx]) continue;
           const SetTile& U = S.st[sidx];
-          for (int row = 0; row < 16; ++row) {
-            if (q < kN2) vacc = fmaf(U.h2[row * kS2 + q], U.d3[row], vacc);
-            else if (q < 2 * kN2) vacc += U.dz2[row * kS2 + (q - kN2)];
-            else vacc += U.d3[row];
+          float va[16], vb[16];
+#pragma unroll
+          for (int row = 0; row < 16; ++row) {  // all 32 reads in flight, then the chain
+            va[row] = q < kN2 ? U.h2[row * kS2 + q] : q < 2 * kN2 ? U.dz2[row * kS2 + (q - kN2)] : 1.f;
+            vb[row] = q < kN2 || q == 2 * kN2 ? U.d3[row] : 1.f;
           }
+#pragma unroll
+          for (int row = 0; row < 16; ++row) vacc = fmaf(va[row], vb[row], vacc);
         }
       }
     }
@@ -452,8 +465,8 @@ int device_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
   return cus;
@@ -474,9 +487,31 @@ int32_t check_aux(const AuxArgs& a) {
 
 using namespace rs;
 
-extern "C" size_t rs_dien_aux_workspace_size(int32_t H, int32_t E) {
+namespace rs {
+namespace {
+struct AuxWs {  // workspace carve: partials | fold scratch | flags | positions | items | cnt | n | scan
+  size_t part, part2, flag, pos, items, cnt, n, scan, total;
+};
+AuxWs aux_ws_layout(int64_t B, int32_t L, int32_t H, int32_t E) {
   const size_t np = (size_t)aux_n_param(H + E);
-  return (size_t)bwd_blocks(device_cus()) * np * 4 + 32 * np * 4 + 256;
+  const int64_t ni = (int64_t)((L + 15) / 16) * B;
+  AuxWs w;
+  w.part = 0;
+  w.part2 = align_up(w.part + (size_t)bwd_blocks(device_cus()) * np * 4, 256);
+  w.flag = align_up(w.part2 + 32 * np * 4, 256);
+  w.pos = align_up(w.flag + (size_t)ni * 4, 256);
+  w.items = align_up(w.pos + (size_t)ni * 4, 256);
+  w.cnt = align_up(w.items + (size_t)ni * 4, 256);
+  w.n = align_up(w.cnt + (size_t)B * 4, 256);
+  w.scan = align_up(w.n + 4, 256);
+  w.total = w.scan + exclusive_scan_ws_size(ni);
+  return w;
+}
+}  // namespace
+}  // namespace rs
+
+extern "C" size_t rs_dien_aux_workspace_size(int64_t B, int32_t L, int32_t H, int32_t E) {
+  return aux_ws_layout(B, L, H, E).total;
 }
 
 extern "C" int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const float* neg,
@@ -507,7 +542,7 @@ extern "C" int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const 
   AuxArgs a{hidden, pos, neg, mask, B, L, H, E, W1, b1, W2, b2, W3, b3};
   if (int32_t e = check_aux(a)) return e;
   RS_CHECK_ARG(daux && dhidden && dpos && dneg && dparams && workspace, "null pointer");
-  RS_CHECK_ARG(ws_bytes >= rs_dien_aux_workspace_size(H, E), "workspace too small");
+  RS_CHECK_ARG(ws_bytes >= rs_dien_aux_workspace_size(B, L, H, E), "workspace too small");
   hipStream_t st = as_stream(stream);
   const int np = aux_n_param(H + E);
   if (B == 0) {
@@ -515,10 +550,32 @@ extern "C" int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const 
     return RS_OK;
   }
   const int nb = bwd_blocks(device_cus());
-  float* part = static_cast<float*>(workspace);
-  float* part2 = part + (size_t)nb * np;
+  const AuxWs wl = aux_ws_layout(B, L, H, E);
+  char* wsb = static_cast<char*>(workspace);
+  float* part = reinterpret_cast<float*>(wsb + wl.part);
+  float* part2 = reinterpret_cast<float*>(wsb + wl.part2);
+  int32_t* flag = reinterpret_cast<int32_t*>(wsb + wl.flag);
+  int32_t* ipos = reinterpret_cast<int32_t*>(wsb + wl.pos);
+  int32_t* items = reinterpret_cast<int32_t*>(wsb + wl.items);
+  int32_t* cnt = reinterpret_cast<int32_t*>(wsb + wl.cnt);
+  int32_t* n_live = reinterpret_cast<int32_t*>(wsb + wl.n);
+  const int NT = (L + 15) / 16;  // tiles over every hidden row t < L
+  const int64_t ni = (int64_t)NT * B;
+  RS_CHECK_ARG(ni < (1LL << 31), "too many (tile, example) items");
+  aux_live_kernel<<<(unsigned)ceil_div(B, kWaves), 64 * kWaves, 0, st>>>(a, NT, flag, cnt);
+  RS_CHECK_LAUNCH();
+  if (int32_t e = exclusive_scan_i32(flag, ipos, ni, n_live, wsb + wl.scan,
+                                     exclusive_scan_ws_size(ni), st))
+    return e;
+  aux_compact_kernel<<<(unsigned)std::min<int64_t>(ceil_div(ni, 256), 4096), 256, 0, st>>>(
+      flag, ipos, ni, items);
+  RS_CHECK_LAUNCH();
   const size_t lds = bwd_lds_bytes();
-  AuxGrad g{daux, dhidden, dpos, dneg, part};
+  // input gradients start at 0: the kernel writes only the rows of tiles that hold a valid row
+  RS_CHECK_HIP(hipMemsetAsync(dhidden, 0, (size_t)B * L * H * 4, st));
+  RS_CHECK_HIP(hipMemsetAsync(dpos, 0, (size_t)B * L * E * 4, st));
+  RS_CHECK_HIP(hipMemsetAsync(dneg, 0, (size_t)B * L * E * 4, st));
+  AuxGrad g{daux, dhidden, dpos, dneg, part, items, n_live, cnt};
   auto run = [&](auto kern) -> int32_t {
     RS_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

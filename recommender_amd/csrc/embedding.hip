@@ -562,7 +562,10 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
                                                         int64_t n_tiles,
                                                         const float* __restrict__ chunk) {
   constexpr int T = RS_DEDUP_TILE;
-  constexpr int U = 4;
+  // 16 groups per round trip: the group-leader keys and the group sums are loaded together
+  // (speculatively past the segment's end, discarded there), then added in group order — a hot
+  // row spanning hundreds of groups (e.g. a padding id) costs one load latency per 16 groups
+  constexpr int U = 16;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
   const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
@@ -578,15 +581,19 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
     bool in[U];
     float r[U][CPL][VEC];
     bool more = true;
+    uint32_t k[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t tt = (g + u) * kFixChunk;
-      in[u] = more && tt < n_tiles && keys[tt * T] == row;
-      more = in[u];
+      k[u] = tt < n_tiles ? keys[tt * T] : ~row;
+      if (tt < n_tiles)
+        load_or_zero<VEC, CPL>(chunk + ((g + u) * kFixChunk * 2) * (int64_t)dim, dim, gl, lpr, r[u]);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (in[u]) load_or_zero<VEC, CPL>(chunk + ((g + u) * kFixChunk * 2) * (int64_t)dim, dim, gl, lpr, r[u]);
+    for (int u = 0; u < U; ++u) {
+      in[u] = more && k[u] == row;
+      more = in[u];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (in[u])

@@ -345,7 +345,7 @@ class _AuxLossFn(torch.autograd.Function):
         dn = torch.empty_like(neg)
         In, n1, n2 = H + E, W1.shape[1], W2.shape[1]
         dparams = torch.empty(In * n1 + n1 + n1 * n2 + n2 + n2 + 1, device=dev)
-        nb = L.lib().rs_dien_aux_workspace_size(H, E)
+        nb = L.lib().rs_dien_aux_workspace_size(B, Lh, H, E)
         ws = _aux_ws.get(dev)
         if ws is None or ws.numel() < nb:
             ws = torch.empty(nb, dtype=torch.uint8, device=dev)
