@@ -100,8 +100,11 @@ class Embedding(nn.Module):
         if self.fused_optimizer is not None and torch.is_grad_enabled():
             e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
             ahead = e[2] if e is not None and e[1] == ids._version else None
-            self._presorted = (ids, ahead if ahead is not None
-                               else self.fused_optimizer.sort_async(self, ids))
+            if ahead is None:
+                opt = self.fused_optimizer
+                ahead = (opt.sort_ahead(self, ids) if opt.presort_own_stream
+                         else opt.sort_async(self, ids))
+            self._presorted = (ids, ahead)
 
     def take_presorted(self, ids: torch.Tensor):
         p, self._presorted = self._presorted, None
