@@ -559,7 +559,7 @@ __global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
     const float* __restrict__ M, int ldm, int m, const float* __restrict__ cin,
     const float* __restrict__ K, int k, int n, const float* __restrict__ b,
     float* __restrict__ out) {
-  __shared__ float ms[kAugLds];
+  extern __shared__ float ms[];  // max((m + 1)·k, 8·MR·64) floats (aug_lds_bytes)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) {
     const int i = e / k, kk = e - i * k;
@@ -694,7 +694,7 @@ template <int MR>
 __global__ __launch_bounds__(kC3Waves * 64) void rt_product_kernel(
     const float* __restrict__ P, int m, const float* __restrict__ K, int k, int n,
     float* __restrict__ out) {
-  __shared__ float ps[kAugLds];
+  extern __shared__ float ps[];  // (m + 1)·k floats
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) ps[e] = P[e];
   __syncthreads();
@@ -954,10 +954,14 @@ extern "C" int32_t rs_chain_aug_product(const float* M, int32_t ldm, int32_t m, 
                "rs_chain_aug_product: bad arguments");
   const unsigned g = (unsigned)ceil_div(n, 64);
   hipStream_t st = as_stream(stream);
+  // LDS sized to the product (not the kAugLds maximum): a small block footprint lets these
+  // latency-bound launches find room beside the co-running sparse-update walk
+  const int mr = m < 16 ? 16 : kAugRows;
+  const size_t lds = (size_t)std::max<int64_t>((int64_t)(m + 1) * k, (int64_t)8 * mr * 64) * 4;
   if (m < 16)
-    aug_product_kernel<16><<<g, kC3Waves * 64, 0, st>>>(M, ldm, m, cin, K, k, n, b, out);
+    aug_product_kernel<16><<<g, kC3Waves * 64, lds, st>>>(M, ldm, m, cin, K, k, n, b, out);
   else
-    aug_product_kernel<kAugRows><<<g, kC3Waves * 64, 0, st>>>(M, ldm, m, cin, K, k, n, b, out);
+    aug_product_kernel<kAugRows><<<g, kC3Waves * 64, lds, st>>>(M, ldm, m, cin, K, k, n, b, out);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -1018,10 +1022,11 @@ extern "C" int32_t rs_chain_rt_product(const float* P, int32_t m, const float* K
                "rs_chain_rt_product: bad arguments");
   const unsigned g = (unsigned)ceil_div(n, kC3Waves);
   hipStream_t st = as_stream(stream);
+  const size_t lds = (size_t)(m + 1) * k * 4;
   if (m < 16)
-    rt_product_kernel<16><<<g, kC3Waves * 64, 0, st>>>(P, m, K, k, n, out);
+    rt_product_kernel<16><<<g, kC3Waves * 64, lds, st>>>(P, m, K, k, n, out);
   else
-    rt_product_kernel<kAugRows><<<g, kC3Waves * 64, 0, st>>>(P, m, K, k, n, out);
+    rt_product_kernel<kAugRows><<<g, kC3Waves * 64, lds, st>>>(P, m, K, k, n, out);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

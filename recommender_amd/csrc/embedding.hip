@@ -12,6 +12,8 @@
 // a run cut by a tile edge stores a partial ([tile][0] = continuation, [tile][1] = head part),
 // and a fix-up pass folds the partials of each spanning segment in tile order. The order is
 // therefore fixed by the sorted order alone (oracle/embedding.py:segment_sum_tiled).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace rs {
@@ -651,6 +653,16 @@ __global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restric
 }
 
 // ---- host launchers -------------------------------------------------------------------
+// Opt-in occupancy cap for the D = 128 walk (A/B): unused dynamic LDS per block, so fewer walk
+// blocks fit on a CU and the co-running weight-sized kernels find free wave slots.
+static size_t apply_lds_throttle() {
+  static const size_t v = [] {
+    const char* e = getenv("RS_APPLY_LDS");
+    return e ? (size_t)atol(e) : (size_t)0;
+  }();
+  return v;
+}
+
 template <template <int, int> class K>
 struct Noop {};
 
@@ -696,7 +708,7 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     if (t32)                                                                                    \
-      seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, 0, st>>>(keys, pos, n,               \
+      seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, apply_lds_throttle(), st>>>(keys, pos, n,               \
                                                                   (uint32_t)n_rows, grad, a,    \
                                                                   n_tiles);                     \
     else                                                                                        \
