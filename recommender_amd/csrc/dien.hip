@@ -19,6 +19,22 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+// An example's mask row as wave-uniform bit words (L <= 256); longer rows read the byte.
+struct MaskBits {
+  uint64_t w[4];
+  int L;
+  __device__ __forceinline__ MaskBits(const uint8_t* mb, int L_, int lane) : L(L_) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int t = 64 * q + lane;
+      w[q] = __ballot(t < L && t < 256 && mb[t] != 0);
+    }
+  }
+  __device__ __forceinline__ bool test(const uint8_t* mb, int t) const {
+    return t < 256 ? ((w[t >> 6] >> (t & 63)) & 1ull) != 0 : mb[t] != 0;
+  }
+};
+
 // ---------------------------------------------------------------------------------------
 // GRU (Keras reset_after): xw[b,t] = [x_z, x_r, x_h] = x·W + b_in (caller),
 // inner = h·U + rb; z = σ(x_z+inner_z); r = σ(x_r+inner_r); hh = tanh(x_h + r·inner_h);
@@ -117,27 +133,38 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
     wh[k] = ok ? U[j * H3 + 2 * H + k] : 0.f;
   }
   const uint8_t* mb = mask + b * L;
+  const MaskBits mbits(mb, L, j);
   float dh = 0.f;
+  // step t's operands are loaded one step ahead (t-1's loads are in flight while t computes);
+  // the mask lives in registers (one ballot per 64 steps)
+  float nd = 0.f, nz = 0.f, nr = 0.f, nhh = 0.f, nih = 0.f, nhp = 0.f;
+  auto fetch = [&](int t) {
+    const int64_t o = b * L + t;
+    if (act) nd = dout[o * H + j];
+    if (act && mbits.test(mb, t)) {
+      const float* s = saved + o * 4 * H;
+      nz = s[j];
+      nr = s[H + j];
+      nhh = s[2 * H + j];
+      nih = s[3 * H + j];
+      nhp = t > 0 ? out[(o - 1) * H + j] : 0.f;
+    }
+  };
+  fetch(L - 1);
   for (int t = L - 1; t >= 0; --t) {
     const int64_t o = b * L + t;
-    if (act) dh += dout[o * H + j];
+    const float dcur = nd, z = nz, r = nr, hh = nhh, ih = nih, hp = nhp;
+    const bool valid = mbits.test(mb, t);
+    if (t > 0) fetch(t - 1);
+    if (act) dh += dcur;
     float* dx = dxw + o * H3;
     float* di = dinner + o * H3;
-    if (!mb[t]) {  // state carried: the gradient passes through unchanged
+    if (!valid) {  // state carried: the gradient passes through unchanged
       if (act) {
         dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
         di[j] = di[H + j] = di[2 * H + j] = 0.f;
       }
       continue;
-    }
-    float z = 0.f, r = 0.f, hh = 0.f, ih = 0.f, hp = 0.f;
-    if (act) {
-      const float* s = saved + o * 4 * H;
-      z = s[j];
-      r = s[H + j];
-      hh = s[2 * H + j];
-      ih = s[3 * H + j];
-      hp = t > 0 ? out[(o - 1) * H + j] : 0.f;
     }
     const float dz = dh * (hp - hh);
     const float dph = dh * (1.f - z) * (1.f - hh * hh);
@@ -269,25 +296,35 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
     kh[k] = ok ? Khr[j * H + k] : 0.f;
   }
   const uint8_t* mb = mask + b * L;
+  const MaskBits mbits(mb, L, j);
   const float* ab = att + b * L;
   float dh = act ? dfinal[b * H + j] : 0.f;
+  // the next valid step's operands are loaded while the current one computes
+  float nu = 0.f, nr = 0.f, nhh = 0.f, nhp = 0.f, na = 0.f;
+  auto fetch = [&](int t) {
+    if (!mbits.test(mb, t)) return;
+    const int64_t o = b * L + t;
+    na = ab[t];
+    if (act) {
+      const float* s = saved + o * 4 * H;
+      nu = s[j];
+      nr = s[H + j];
+      nhh = s[2 * H + j];
+      nhp = t > 0 ? states[(o - 1) * H + j] : 0.f;
+    }
+  };
+  fetch(L - 1);
   for (int t = L - 1; t >= 0; --t) {
     const int64_t o = b * L + t;
     float* dx = dxw + o * H3;
-    if (!mb[t]) {
+    if (!mbits.test(mb, t)) {
       if (act) dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
       if (j == 0) datt[o] = 0.f;
+      if (t > 0) fetch(t - 1);
       continue;
     }
-    float u = 0.f, r = 0.f, hh = 0.f, hp = 0.f;
-    if (act) {
-      const float* s = saved + o * 4 * H;
-      u = s[j];
-      r = s[H + j];
-      hh = s[2 * H + j];
-      hp = t > 0 ? states[(o - 1) * H + j] : 0.f;
-    }
-    const float a = ab[t];
+    const float u = nu, r = nr, hh = nhh, hp = nhp, a = na;
+    if (t > 0) fetch(t - 1);
     const float ua = u * a;
     const float dua = dh * (hh - hp);
     float dhp = dh * (1.f - ua);
