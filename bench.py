@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-baseline-steps", type=int, default=50)
     ap.add_argument("--cpu-baseline-batch", type=int, default=4096)
+    ap.add_argument("--defer-decay", type=int, default=0,
+                    help="keras_adam: replay the dense decay per row when it is next read instead "
+                         "of sweeping all rows each step (exact after materialize)")
     ap.add_argument("--prefetch", type=int, default=0,
                     help="1: sort the next batch's ids one step ahead (TrainStep.prefetch); eager "
                          "only. Measured slower on the north star (0.864 vs 0.845 ms/step): the "
@@ -381,7 +384,8 @@ def main():
         model = build_model("DLRM", D, args.rows, S, 13, dev, slot_cardinalities=cards,
                             bottom=[512, 256, D], top=[512, 256, 1], generator=g)
     step = TrainStep(model, args.optimizer, lr=0.01 if args.optimizer == "sgd" else 1e-3,
-                     fused=bool(args.fused), comm=comm, defer_sparse_join=bool(args.defer_join))
+                     fused=bool(args.fused), comm=comm, defer_sparse_join=bool(args.defer_join),
+                     defer_decay=bool(args.defer_decay))
     pool = make_pool(args, cards, rank, dev)
     U = measured_unique(pool, model)
 
@@ -439,6 +443,15 @@ def main():
         tt = torch.tensor([wall], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall = float(tt.item())
+    materialize_ms = None
+    if getattr(step.opt_sparse, "defer_decay", False):
+        # outside the timed region: bring every row up to date (what a checkpoint or an
+        # evaluation pass needs), timed on its own
+        torch.cuda.synchronize()
+        tm0 = time.perf_counter()
+        step.opt_sparse.materialize()
+        torch.cuda.synchronize()
+        materialize_ms = round((time.perf_counter() - tm0) * 1e3, 3)
     ms_step = wall / args.steps * 1e3
     value = args.batch * world * args.steps / wall
 
@@ -530,7 +543,7 @@ def main():
             "config": {"workload": f"dlrm_criteo_{S}x{args.rows}x{D}", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "rows": args.rows, "dim": D, "slots": S,
                        "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
-                       "optimizer": args.optimizer,
+                       "optimizer": args.optimizer + (" (deferred exact decay)" if materialize_ms is not None else ""),
                        "parallelism": f"row-sharded slab x{world} (RCCL all-to-all) + dp{world} MLPs" if world > 1 else "single"},
             "mlp": {"backward": args.mlp_bwd, "forward": args.mlp_fwd,
                     "note": "ctr MLP hidden layers are linear (ctr/layers.py:8), so each MLP is one "
@@ -543,6 +556,7 @@ def main():
                     "ms_per_step_layerwise_fwd_bwd": layerwise_ms},
             "roofline": roof, "kernels": kern,
             "cpu_baseline": cpu, "loss": float(loss.item()),
+            **({"keras_materialize_ms": materialize_ms} if materialize_ms is not None else {}),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -175,6 +175,23 @@ int32_t rs_apply_keras_dense_adam(float* table, float* m, float* v, int64_t n_ro
 int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_rows, int32_t dim,
                                   const rs_adam_params* params, uint32_t* touched_bitmap,
                                   void* stream);
+/* Deferred Keras decay (exact): the dense m/v decay + var update of rows without a gradient is
+ * replayed per row on demand instead of swept over all V rows each step. last [n_rows] int32 =
+ * the last step applied to each row (0 initially); lr_hist[s] = lr_t of step s (1-based, the
+ * host's keras_adam_coefficients(s).lr); beta1 / beta2 / epsilon from params.
+ * rs_keras_adam_catchup: before step `step` reads its rows, each unique row of sorted_rows
+ *   (rs_sort_ids output; entries >= n_rows skipped) replays steps last+1 .. step-1 and is
+ *   marked last = step (the step's sparse apply — rs_embedding_apply with RS_OPT_KERAS_ADAM,
+ *   no dense sweep — updates it next).
+ * rs_keras_adam_materialize: every row replays last+1 .. step; afterwards table / m / v equal
+ *   the per-step dense sweep's state bit for bit (same arithmetic per element and step). */
+int32_t rs_keras_adam_catchup(float* table, float* m, float* v, int32_t* last, int64_t n_rows,
+                              int32_t dim, const int32_t* sorted_rows, int64_t n,
+                              const float* lr_hist, int32_t step, const rs_adam_params* params,
+                              void* stream);
+int32_t rs_keras_adam_materialize(float* table, float* m, float* v, int32_t* last, int64_t n_rows,
+                                  int32_t dim, const float* lr_hist, int32_t step,
+                                  const rs_adam_params* params, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * a-4 DotInteraction(self_interaction, skip_gather) — ctr/layers.py:17-43.

@@ -52,6 +52,10 @@ _SIGS = {
     "rs_embedding_apply_scaled": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p, _p,
                                          _i32, C.POINTER(AdamParams), _p, _p, _sz, _p]),
     "rs_keras_adam_dense_sweep": (_i32, [_p, _p, _p, _i64, _i32, C.POINTER(AdamParams), _p, _p]),
+    "rs_keras_adam_catchup": (_i32, [_p, _p, _p, _p, _i64, _i32, _p, _i64, _p, _i32,
+                                     C.POINTER(AdamParams), _p]),
+    "rs_keras_adam_materialize": (_i32, [_p, _p, _p, _p, _i64, _i32, _p, _i32,
+                                         C.POINTER(AdamParams), _p]),
     "rs_dot_interaction_fwd": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _p, _i64, _p]),
     "rs_dot_interaction_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _i32, _i64, _p, _p]),
     "rs_dlrm_interaction_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _i32, _p,

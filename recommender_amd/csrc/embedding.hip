@@ -618,6 +618,19 @@ __global__ void head_flags_kernel(const uint32_t* __restrict__ keys, int64_t n, 
   }
 }
 
+// One Keras dense-Adam step of an element whose slice holds no gradient (g = 0): m·β1, v·β2,
+// var -= lr_t·m/(√v + ε) [3p TF 2.2 _resource_apply_sparse, untouched rows]. Shared by the dense
+// sweep and the deferred replay below so that both round identically.
+__device__ __forceinline__ void keras_decay(float& w, float& m, float& v, float lr, float b1,
+                                            float b2, float eps) {
+  const float m1 = m * b1;
+  const float v1 = v * b2;
+  const float upd = (lr * m1) / (sqrtf(v1) + eps);
+  m = m1;
+  v = v1;
+  w = w - upd;
+}
+
 // Keras dense sweep over untouched rows (touched rows were fully updated by the sparse pass)
 template <int VEC>
 __global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restrict__ w,
@@ -638,17 +651,72 @@ __global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restric
     RowIO<VEC>::load(m + off, mm);
     RowIO<VEC>::load(v + off, vv);
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      float m1 = mm[e] * p.beta1;
-      float v1 = vv[e] * p.beta2;
-      float upd = (p.lr * m1) / (sqrtf(v1) + p.epsilon);
-      mm[e] = m1;
-      vv[e] = v1;
-      ww[e] = ww[e] - upd;
+    for (int e = 0; e < VEC; ++e) keras_decay(ww[e], mm[e], vv[e], p.lr, p.beta1, p.beta2, p.epsilon);
+    RowIO<VEC>::store(w + off, ww);
+    RowIO<VEC>::store(m + off, mm);
+    RowIO<VEC>::store(v + off, vv);
+  }
+}
+
+// Deferred Keras decay (SparseAdam(mode='keras', defer_decay=True)): instead of sweeping all V
+// rows every step, row r records last[r], the last step applied to it. Before a step s reads
+// its rows, the step's unique rows replay the skipped steps last[r]+1 .. s-1 with the very
+// arithmetic of the sweep (keras_decay, lr_t of each step from lr_hist[step]) and claim step s
+// (its sparse apply follows); materialize replays every row up to the current step. The state
+// after materialize equals the dense-sweep state bit for bit.
+template <int VEC>
+__device__ __forceinline__ void keras_replay_row(float* w, float* m, float* v, int64_t r, int dim,
+                                                 int gl, int lpr, int32_t from, int32_t to,
+                                                 const float* lr_hist, float b1, float b2,
+                                                 float eps) {
+  for (int col = gl * VEC; col < dim; col += lpr * VEC) {
+    const int64_t off = r * dim + col;
+    float ww[VEC], mm[VEC], vv[VEC];
+    RowIO<VEC>::load(w + off, ww);
+    RowIO<VEC>::load(m + off, mm);
+    RowIO<VEC>::load(v + off, vv);
+    for (int32_t st = from; st <= to; ++st) {
+      const float lr = lr_hist[st];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) keras_decay(ww[e], mm[e], vv[e], lr, b1, b2, eps);
     }
     RowIO<VEC>::store(w + off, ww);
     RowIO<VEC>::store(m + off, mm);
     RowIO<VEC>::store(v + off, vv);
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void keras_catchup_kernel(
+    float* __restrict__ w, float* __restrict__ m, float* __restrict__ v, int32_t* __restrict__ last,
+    uint32_t n_rows, int dim, const uint32_t* __restrict__ rows, int64_t n,
+    const float* __restrict__ lr_hist, int32_t step, float b1, float b2, float eps, int lpr_log2) {
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> lpr_log2;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> lpr_log2; i < n; i += stride) {
+    const uint32_t r = rows[i];
+    if (r >= n_rows || (i > 0 && rows[i - 1] == r)) continue;  // one lane group per unique row
+    const int32_t l0 = last[r];
+    if (l0 + 1 <= step - 1)
+      keras_replay_row<VEC>(w, m, v, r, dim, gl, lpr, l0 + 1, step - 1, lr_hist, b1, b2, eps);
+    if (gl == 0) last[r] = step;  // claimed: the step's sparse apply updates the row next
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void keras_materialize_kernel(
+    float* __restrict__ w, float* __restrict__ m, float* __restrict__ v, int32_t* __restrict__ last,
+    int64_t n_rows, int dim, const float* __restrict__ lr_hist, int32_t step, float b1, float b2,
+    float eps, int lpr_log2) {
+  const int lpr = 1 << lpr_log2;
+  const int gl = threadIdx.x & (lpr - 1);
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> lpr_log2;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> lpr_log2; r < n_rows; r += stride) {
+    const int32_t l0 = last[r];
+    if (l0 + 1 <= step)
+      keras_replay_row<VEC>(w, m, v, r, dim, gl, lpr, l0 + 1, step, lr_hist, b1, b2, eps);
+    if (gl == 0) last[r] = step;
   }
 }
 
@@ -871,6 +939,63 @@ extern "C" int32_t rs_embedding_apply_scaled(int32_t opt, float* table, float* m
   RowGeom geom = row_geom(dim, ptrs, 4);
   return launch_segments(opt, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom,
                          as_stream(stream));
+}
+
+static void replay_geom(int dim, const void* const* ptrs, int np, int* vec, int* lpr_log2) {
+  RowGeom g = row_geom(dim, ptrs, np);
+  *vec = g.vec;
+  int lanes = dim / g.vec, l2 = 0;
+  while ((1 << l2) < lanes && l2 < 6) ++l2;
+  *lpr_log2 = l2;
+}
+
+extern "C" int32_t rs_keras_adam_catchup(float* table, float* m, float* v, int32_t* last,
+                                         int64_t n_rows, int32_t dim, const int32_t* sorted_rows,
+                                         int64_t n, const float* lr_hist, int32_t step,
+                                         const rs_adam_params* params, void* stream) {
+  RS_CHECK_ARG(table && m && v && last && lr_hist && params && (n == 0 || sorted_rows),
+               "null pointer");
+  RS_CHECK_ARG(dim > 0 && n_rows > 0 && n_rows <= 0xFFFFFFFFll && n >= 0 && step >= 1,
+               "bad sizes");
+  if (n == 0) return RS_OK;
+  const void* ptrs[3] = {table, m, v};
+  int vec, l2;
+  replay_geom(dim, ptrs, 3, &vec, &l2);
+  const int64_t groups = n, per_block = 256 >> l2;
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(groups, per_block), 4096);
+  hipStream_t st = as_stream(stream);
+  const uint32_t* rows = reinterpret_cast<const uint32_t*>(sorted_rows);
+  const rs_adam_params p = *params;
+  switch (vec) {
+    case 4: keras_catchup_kernel<4><<<blocks, 256, 0, st>>>(table, m, v, last, (uint32_t)n_rows, dim, rows, n, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+    case 2: keras_catchup_kernel<2><<<blocks, 256, 0, st>>>(table, m, v, last, (uint32_t)n_rows, dim, rows, n, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+    default: keras_catchup_kernel<1><<<blocks, 256, 0, st>>>(table, m, v, last, (uint32_t)n_rows, dim, rows, n, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+  }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_keras_adam_materialize(float* table, float* m, float* v, int32_t* last,
+                                             int64_t n_rows, int32_t dim, const float* lr_hist,
+                                             int32_t step, const rs_adam_params* params,
+                                             void* stream) {
+  RS_CHECK_ARG(table && m && v && last && lr_hist && params, "null pointer");
+  RS_CHECK_ARG(dim > 0 && n_rows > 0 && step >= 0, "bad sizes");
+  if (step == 0) return RS_OK;
+  const void* ptrs[3] = {table, m, v};
+  int vec, l2;
+  replay_geom(dim, ptrs, 3, &vec, &l2);
+  const int64_t per_block = 256 >> l2;
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n_rows, per_block), 256 * 64);
+  hipStream_t st = as_stream(stream);
+  const rs_adam_params p = *params;
+  switch (vec) {
+    case 4: keras_materialize_kernel<4><<<blocks, 256, 0, st>>>(table, m, v, last, n_rows, dim, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+    case 2: keras_materialize_kernel<2><<<blocks, 256, 0, st>>>(table, m, v, last, n_rows, dim, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+    default: keras_materialize_kernel<1><<<blocks, 256, 0, st>>>(table, m, v, last, n_rows, dim, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
+  }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
 }
 
 extern "C" int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_rows,

@@ -51,10 +51,22 @@ class Embedding(nn.Module):
         self._prefetched: dict = {}
         # deferred join (SparseOptimizer(defer_join=True)): the event the next table read waits on
         self._pending_update = None
+        # deferred-decay Keras Adam: the step this table's rows were last caught up for
+        self._catchup_step = 0
 
     def wait_update(self):
         """Order the current stream after a deferred sparse update of this table (no-op when
-        none is pending). Every kernel that reads the table calls this first."""
+        none is pending). Every kernel that reads the table calls this first. With a
+        deferred-decay Keras Adam, the rows must have been caught up for this step
+        (Embedding.presort) or the optimizer materialized."""
+        opt = self.fused_optimizer
+        if opt is not None and getattr(opt, "defer_decay", False):
+            if self._catchup_step != opt.iterations + 1 and opt._materialized != opt.iterations:
+                raise RuntimeError("deferred-decay Keras Adam: rows read without presort() for "
+                                   "this step; call the optimizer's materialize() first")
+        self.wait_update_raw()
+
+    def wait_update_raw(self):
         ev, self._pending_update = self._pending_update, None
         if ev is not None:
             torch.cuda.current_stream(self.weight.device).wait_event(ev)
@@ -100,11 +112,17 @@ class Embedding(nn.Module):
         if self.fused_optimizer is not None and torch.is_grad_enabled():
             e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
             ahead = e[2] if e is not None and e[1] == ids._version else None
+            opt = self.fused_optimizer
             if ahead is None:
-                opt = self.fused_optimizer
                 ahead = (opt.sort_ahead(self, ids) if opt.presort_own_stream
                          else opt.sort_async(self, ids))
             self._presorted = (ids, ahead)
+            if getattr(opt, "defer_decay", False):
+                # replay the step's rows' skipped decay on the stream the sort ran on
+                on_sort = getattr(ahead, "ready", None) is not None
+                if on_sort:
+                    opt.sort_stream.wait_event(ahead.ready)
+                opt.catch_up(self, ahead, opt.sort_stream if on_sort else opt.side)
 
     def take_presorted(self, ids: torch.Tensor):
         p, self._presorted = self._presorted, None

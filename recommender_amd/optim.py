@@ -212,7 +212,7 @@ class SparseOptimizer:
                table.input_dim, table.output_dim, L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g),
                L.ptr(row_scale), group, params, L.ptr(bitmap), L.ptr(w), w.numel(),
                L.stream_ptr(dev))
-        if self.kind == L.RS_OPT_KERAS_ADAM:
+        if self.kind == L.RS_OPT_KERAS_ADAM and not getattr(self, "defer_decay", False):
             L.call("rs_keras_adam_dense_sweep", L.ptr(table.weight), L.ptr(m), L.ptr(v),
                    table.input_dim, table.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
 
@@ -231,7 +231,8 @@ class SparseOptimizer:
         for t in self.tables:
             got = t.take_grad()
             if got is None:
-                if self.kind == L.RS_OPT_KERAS_ADAM and id(t) not in applied:
+                if (self.kind == L.RS_OPT_KERAS_ADAM and id(t) not in applied
+                        and not getattr(self, "defer_decay", False)):
                     # Keras still decays m/v and moves var densely when the slice is empty
                     m, v, bitmap = self._slots(t)
                     L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
@@ -254,16 +255,28 @@ class SparseSGD(SparseOptimizer):
 
 class SparseAdam(SparseOptimizer):
     """mode='keras': exact Keras Adam (dense m/v decay + dense var update, 24·V·D bytes/step);
-    mode='lazy': the same update restricted to touched rows."""
+    mode='lazy': the same update restricted to touched rows.
+
+    defer_decay=True (mode='keras', fused=True): the dense decay of rows without a gradient is
+    not swept over all V rows each step; each row records the last step applied to it and
+    replays the skipped steps, with the sweep's own arithmetic, right before a step reads it
+    (Embedding.presort → rs_keras_adam_catchup). `materialize()` brings every row up to date:
+    table, m and v then equal the per-step dense sweep's bit for bit. Reading a table outside
+    the engine's step (evaluation, checkpoints, tests) needs materialize() first;
+    Embedding.wait_update raises otherwise."""
 
     def __init__(self, tables, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, mode="keras",
-                 fused=False, defer_join=False):
+                 fused=False, defer_join=False, defer_decay=False):
         super().__init__(tables, lr, fused=fused, defer_join=defer_join)
         self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
         if mode not in ("keras", "lazy"):
             raise ValueError("mode must be 'keras' or 'lazy'")
         self.kind = L.RS_OPT_KERAS_ADAM if mode == "keras" else L.RS_OPT_LAZY_ADAM
+        self.defer_decay = bool(defer_decay)
+        if self.defer_decay and (self.kind != L.RS_OPT_KERAS_ADAM or not fused):
+            raise ValueError("defer_decay needs mode='keras' and fused=True")
         self.state = {}
+        self.last = {}
         for t in self.tables:
             w = t.weight
             m = torch.zeros_like(w)
@@ -271,9 +284,66 @@ class SparseAdam(SparseOptimizer):
             bitmap = (torch.zeros((t.input_dim + 31) // 32, dtype=torch.int32, device=w.device)
                       if self.kind == L.RS_OPT_KERAS_ADAM else None)
             self.state[id(t)] = (m, v, bitmap)
+            if self.defer_decay:
+                self.last[id(t)] = torch.zeros(t.input_dim, dtype=torch.int32, device=w.device)
+                t._catchup_step = 0
+        self._lr_host = [0.0]  # lr_t of step s at index s (host mirror of _lr_dev)
+        self._lr_dev = None
+        self._materialized = 0
 
     def _slots(self, t):
         return self.state[id(t)]
+
+    def _lr_of_step(self, s):
+        lr = self.lr(s - 1) if callable(self.lr) else self.lr
+        return keras_adam_coefficients(s, lr, self.beta_1, self.beta_2, self.epsilon).lr
+
+    def _lr_hist(self, upto, device):
+        """Device lr_t history covering steps 1..upto (extended 1024 steps at a time)."""
+        if len(self._lr_host) <= upto:
+            end = max(upto + 1, len(self._lr_host) + 1024)
+            self._lr_host += [self._lr_of_step(s) for s in range(len(self._lr_host), end)]
+            self._lr_dev = torch.tensor(self._lr_host, dtype=torch.float32, device=device)
+        return self._lr_dev
+
+    def catch_up(self, table, sorted_ids, stream):
+        """Queue on `stream` (after the sort of this step's ids) the replay of the decay the
+        step's rows skipped; the table's next reader waits for it."""
+        step = self.iterations + 1
+        dev = table.weight.device
+        lr = self._lr_hist(step, dev)
+        m, v, _ = self._slots(table)
+        if self.fused:
+            stream.wait_stream(self.side)  # after the previous step's update of these rows
+        with torch.cuda.stream(stream):
+            L.call("rs_keras_adam_catchup", L.ptr(table.weight), L.ptr(m), L.ptr(v),
+                   L.ptr(self.last[id(table)]), table.input_dim, table.output_dim,
+                   L.ptr(sorted_ids.rows), sorted_ids.n, L.ptr(lr), step, self._params(),
+                   L.stream_ptr(dev))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        table._pending_update = ev
+        table._catchup_step = step
+
+    def materialize(self):
+        """Bring every row of every table up to the last applied step (bit-identical to the
+        per-step dense sweep); a no-op without defer_decay."""
+        if not self.defer_decay or self._materialized == self.iterations:
+            return
+        for t in self.tables:
+            t.wait_update_raw()
+            dev = t.weight.device
+            cur = torch.cuda.current_stream(dev)
+            if self.fused:
+                cur.wait_stream(self.side)
+                if self.sort_stream is not None:
+                    cur.wait_stream(self.sort_stream)
+            lr = self._lr_hist(max(self.iterations, 1), dev)
+            m, v, _ = self._slots(t)
+            L.call("rs_keras_adam_materialize", L.ptr(t.weight), L.ptr(m), L.ptr(v),
+                   L.ptr(self.last[id(t)]), t.input_dim, t.output_dim, L.ptr(lr),
+                   self.iterations, self._params(), L.stream_ptr(dev))
+        self._materialized = self.iterations
 
     def _params(self):
         lr = self.lr(self.iterations) if callable(self.lr) else self.lr
