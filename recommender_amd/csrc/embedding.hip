@@ -344,17 +344,23 @@ __device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
 // the tile's 32 keys / positions / row scales loaded lane-parallel in one instruction each (lane
 // gl holds entry gl; entry u's values come by a width-32 shuffle) instead of per entry, and the
 // gradient rows of the next 8 entries in flight while the current 8 are summed. Same order of
-// additions as seg_tile_kernel: bit-identical results.
+// additions as seg_tile_kernel: bit-identical results. The walk of one tile by one half-wave;
+// a run cut by a tile edge leaves its partial at pbase[(starts ? 1 : 0) * 128 ..] (global tile
+// partials or the group kernel's LDS), and the returned edges say how the tile's runs continue.
+struct Tile32Edges {
+  uint32_t last_row;  // row of the tile's last run
+  bool last_open;     // that run started in this tile and continues into the next (valid row)
+  bool first_cont;    // the tile's first run continues from the previous tile (valid row)
+  uint32_t first_key;
+};
+
 template <int OPT>
-__global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restrict__ keys,
-                                                         const int32_t* __restrict__ pos, int64_t n,
-                                                         uint32_t n_rows,
-                                                         const float* __restrict__ grad,
-                                                         ApplyArgs a, int64_t n_tiles) {
+__device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ keys,
+                                                   const int32_t* __restrict__ pos, int64_t n,
+                                                   uint32_t n_rows, const float* __restrict__ grad,
+                                                   const ApplyArgs& a, int64_t t, float* pbase) {
   constexpr int T = 32, VEC = 4, CPL = 1, U = 8;
   const int gl = threadIdx.x & 31;
-  const int64_t t = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (t >= n_tiles) return;
   const int64_t k0 = t * T;
   const int64_t k1 = k0 + T < n ? k0 + T : n;
   const int ne = (int)(k1 - k0);
@@ -399,8 +405,7 @@ __global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restr
     if (starts && ends) {
       finalize_row<OPT, VEC, CPL>(a, row, gl, 32, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, k0 + head_e) : 0);
     } else {
-      float* dst = a.partial + ((t * 2) + (starts ? 1 : 0)) * (int64_t)dim;
-      RowIO<VEC>::store(dst + col, acc[0]);
+      RowIO<VEC>::store(pbase + (starts ? 1 : 0) * dim + col, acc[0]);
     }
   };
   float rA[U][VEC], rB[U][VEC];
@@ -442,13 +447,96 @@ __global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restr
 #endif
   const bool ends = key_after != run_row;
   emit(run_row, run_starts, ends, run_start);
-  if (gl == 0) {
+  Tile32Edges ed;
+  ed.last_row = run_row;
+  ed.last_open = !ends && run_starts && run_row < n_rows;
+  ed.first_key = key_of(0);
+  ed.first_cont = k0 > 0 && ed.first_key < n_rows && key_before == ed.first_key;
+  return ed;
+}
+
+template <int OPT>
+__global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restrict__ keys,
+                                                         const int32_t* __restrict__ pos, int64_t n,
+                                                         uint32_t n_rows,
+                                                         const float* __restrict__ grad,
+                                                         ApplyArgs a, int64_t n_tiles) {
+  const int64_t t = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (t >= n_tiles) return;
+  const Tile32Edges e = tile32_walk<OPT>(keys, pos, n, n_rows, grad, a, t,
+                                         a.partial + t * 2 * (int64_t)a.dim);
+  if ((threadIdx.x & 31) == 0) {
     uint8_t f = 0;
-    if (!ends && run_starts && run_row < n_rows) f |= 1;  // last run opens a spanning segment
-    const uint32_t fk = key_of(0);
-    if ((t % 32) == 0 && k0 > 0 && fk < n_rows && key_before == fk) f |= 2;
+    if (e.last_open) f |= 1;  // last run opens a spanning segment
+    if ((t % 32) == 0 && e.first_cont) f |= 2;
     a.tile_flags[t] = f;
   }
+}
+
+// The D = 128 walk with the first fix-up level folded in: a block of 32 half-waves walks one
+// ALIGNED group of 32 tiles (= kFixChunk), its cut runs' partials kept in LDS. After a block
+// barrier each segment that spans tiles of the group is folded in tile order from LDS — the
+// level-1 sum of seg_chunk_kernel, same additions in the same order — and finalised on the spot
+// when it also ends inside the group (the level-2 fold of a single group sum is that sum).
+// Only segments that cross a group edge leave global state: the head's group sum
+// (chunk[t][1], tile flag bit 0) and, at a group's first tile, the continuation's group sum
+// (chunk[t][0]); seg_fixup_kernel folds those (level 2). Bit-identical to seg_tile32 + seg_chunk
+// + seg_fixup, one launch fewer and no global partials.
+template <int OPT>
+__global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __restrict__ keys,
+                                                           const int32_t* __restrict__ pos,
+                                                           int64_t n, uint32_t n_rows,
+                                                           const float* __restrict__ grad,
+                                                           ApplyArgs a, int64_t n_tiles) {
+  constexpr int G = 32, D = 128, T = 32;
+  __shared__ __attribute__((aligned(16))) float ps[G][2][D];
+  __shared__ uint32_t fkey[G];
+  const int gi = threadIdx.x >> 5, gl = threadIdx.x & 31;
+  const int64_t t = (int64_t)blockIdx.x * G + gi;
+  const bool live = t < n_tiles;
+  Tile32Edges e{};
+  if (live) e = tile32_walk<OPT>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
+  if (gl == 0) fkey[gi] = live ? e.first_key : 0xFFFFFFFFu;
+  __syncthreads();
+  if (!live) return;
+  const int col = gl * 4;
+  uint8_t gflag = 0;
+  if (e.last_open) {  // head of a spanning segment: its level-1 sum inside this group
+    const uint32_t row = e.last_row;
+    float acc[1][4];
+    {
+      const float4 h = *reinterpret_cast<const float4*>(&ps[gi][1][col]);
+      acc[0][0] = h.x; acc[0][1] = h.y; acc[0][2] = h.z; acc[0][3] = h.w;
+    }
+    int u = gi + 1;
+    for (; u < G && fkey[u] == row; ++u) {
+      const float4 c = *reinterpret_cast<const float4*>(&ps[u][0][col]);
+      acc[0][0] += c.x; acc[0][1] += c.y; acc[0][2] += c.z; acc[0][3] += c.w;
+    }
+    const int64_t tn = ((int64_t)blockIdx.x + 1) * G;  // first tile of the next group
+    const bool crosses = u == G && tn < n_tiles && keys[tn * T] == row;
+    if (crosses) {
+      RowIO<4>::store(a.chunk + (t * 2 + 1) * (int64_t)D + col, acc[0]);
+      gflag = 1;
+    } else {
+      finalize_row<OPT, 4, 1>(a, row, gl, 32, acc,
+                              OPT == OPT_EMIT ? seg_id_of(a, keys, t * T + T - 1) : 0);
+    }
+  }
+  if (gi == 0 && e.first_cont) {  // the group's first tile continues a segment from before
+    const uint32_t fk = e.first_key;
+    float acc[4];
+    {
+      const float4 h = *reinterpret_cast<const float4*>(&ps[0][0][col]);
+      acc[0] = h.x; acc[1] = h.y; acc[2] = h.z; acc[3] = h.w;
+    }
+    for (int u = 1; u < G && fkey[u] == fk; ++u) {
+      const float4 c = *reinterpret_cast<const float4*>(&ps[u][0][col]);
+      acc[0] += c.x; acc[1] += c.y; acc[2] += c.z; acc[3] += c.w;
+    }
+    RowIO<4>::store(a.chunk + (t * 2) * (int64_t)D + col, acc);
+  }
+  if (gl == 0) a.tile_flags[t] = gflag;
 }
 
 // ---- fix-up of segments that span tiles ----------------------------------------------
@@ -773,17 +861,27 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #else
   const bool t32 = false;
 #endif
+#ifndef RS_NO_G32
+  const bool g32 = t32;
+#else
+  const bool g32 = false;
+#endif
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
-    if (t32)                                                                                    \
-      seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, apply_lds_throttle(), st>>>(keys, pos, n,               \
-                                                                  (uint32_t)n_rows, grad, a,    \
-                                                                  n_tiles);                     \
-    else                                                                                        \
-      seg_tile_kernel<OPTV, VEC, CPL><<<walk_blocks, 256, 0, st>>>(keys, pos, n, (uint32_t)n_rows, \
-                                                                   grad, a, geom.lpr_log2, n_tiles); \
-    seg_chunk_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,            \
-                                                       geom.lpr_log2, n_tiles, a.chunk);        \
+    if (g32) {                                                                                  \
+      seg_group32_kernel<OPTV><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(keys, pos, n,            \
+                                                                   (uint32_t)n_rows, grad, a,   \
+                                                                   n_tiles);                    \
+    } else {                                                                                    \
+      if (t32)                                                                                  \
+        seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, apply_lds_throttle(), st>>>(       \
+            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
+      else                                                                                      \
+        seg_tile_kernel<OPTV, VEC, CPL><<<walk_blocks, 256, 0, st>>>(                           \
+            keys, pos, n, (uint32_t)n_rows, grad, a, geom.lpr_log2, n_tiles);                   \
+      seg_chunk_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,          \
+                                                         geom.lpr_log2, n_tiles, a.chunk);      \
+    }                                                                                           \
     seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,      \
                                                              geom.lpr_log2, n_tiles, a.chunk);  \
   }))

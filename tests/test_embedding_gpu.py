@@ -107,6 +107,35 @@ def test_dedup_grad_order(dim, dist, rng):
     np.testing.assert_array_equal(ug.cpu().numpy(), rg)
 
 
+@pytest.mark.parametrize("lens", [
+    [31, 32, 33, 1, 1024, 1023, 1025, 2, 2048 + 7, 5, 32 * 32 * 3, 64],
+    [992, 32, 1, 31, 1024 * 2 - 1, 1, 1056, 7],
+    [1] * 100 + [3000] + [1] * 33,
+])
+def test_segment_runs_across_tile_groups(lens, rng):
+    """D = 128 walk (seg_group32_kernel: tiles of 32 in aligned groups of 32, level-1 fold in
+    LDS, level-2 fold across groups): runs ending on / just past tile and group edges, runs
+    spanning several groups, a group whose first tile continues a run, singletons between.
+    Dedup rows and SGD update bit-exact against the oracle's tiled order."""
+    V, dim = 50_000, 128
+    rows = rng.choice(V, len(lens), replace=False)
+    ids = np.concatenate([np.full(n, r) for n, r in zip(lens, sorted(rows))]).astype(np.int64)
+    ids = ids[rng.permutation(ids.size)]
+    g = rng.standard_normal((ids.size, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV)
+    ur, ug = dedup_grad(t, torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+    sr, sp, _ = O.sort_ids(ids, V)
+    rr, rg = O.segment_sum_tiled(sr, sp, g, V)
+    np.testing.assert_array_equal(ur.cpu().numpy(), rr.astype(np.int64))
+    np.testing.assert_array_equal(ug.cpu().numpy(), rg)
+    w0 = rng.standard_normal((V, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV, weight=torch.from_numpy(w0))
+    opt = SparseSGD(t, lr=0.05)
+    t.accumulate_grad(torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+    opt.step()
+    np.testing.assert_array_equal(t.weight.cpu().numpy(), O.apply_sgd(w0, rr, rg, np.float32(0.05)))
+
+
 @pytest.mark.parametrize("dim", [128, 18])
 def test_sgd_apply_bitexact(dim, rng):
     V, B, S = 30_000, 512, 26
