@@ -647,10 +647,47 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(const uint32_t* __restri
 
 // level 2: one lane group per head tile of a spanning segment
 template <int OPT, int VEC, int CPL>
+__device__ __forceinline__ void fixup_one(const uint32_t* __restrict__ keys, const ApplyArgs& a,
+                                          int lpr_log2, int64_t n_tiles,
+                                          const float* __restrict__ chunk, int64_t t);
+
+template <int OPT, int VEC, int CPL>
 __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                         uint32_t n_rows, ApplyArgs a, int lpr_log2,
                                                         int64_t n_tiles,
                                                         const float* __restrict__ chunk) {
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
+  if (t >= n_tiles - 1) return;
+  if (!(a.tile_flags[t] & 1)) return;  // not the head tile of a spanning segment
+  fixup_one<OPT, VEC, CPL>(keys, a, lpr_log2, n_tiles, chunk, t);
+}
+
+// The level-2 pass after seg_group32_kernel: few tiles head a segment that crosses a group edge,
+// so a small grid sweeps the tile flags instead of one lane group per tile — each half-wave
+// loads the flags of 32 tiles at once and folds the flagged ones (same fold as seg_fixup_kernel).
+template <int OPT>
+__global__ __launch_bounds__(256) void seg_fixup_sweep_kernel(const uint32_t* __restrict__ keys,
+                                                              ApplyArgs a, int64_t n_tiles,
+                                                              const float* __restrict__ chunk) {
+  const int gl = threadIdx.x & 31;
+  const int64_t groups = (int64_t)gridDim.x * 8;
+  for (int64_t t0 = ((int64_t)blockIdx.x * 8 + (threadIdx.x >> 5)) * 32; t0 < n_tiles - 1;
+       t0 += groups * 32) {
+    const int64_t tl = t0 + gl;
+    const bool head = tl < n_tiles - 1 && (a.tile_flags[tl] & 1);
+    uint32_t bits = (uint32_t)(__ballot(head) >> (threadIdx.x & 32));
+    while (bits) {
+      const int u = __builtin_ctz(bits);
+      bits &= bits - 1;
+      fixup_one<OPT, 4, 1>(keys, a, 5, n_tiles, chunk, t0 + u);
+    }
+  }
+}
+
+template <int OPT, int VEC, int CPL>
+__device__ __forceinline__ void fixup_one(const uint32_t* __restrict__ keys, const ApplyArgs& a,
+                                          int lpr_log2, int64_t n_tiles,
+                                          const float* __restrict__ chunk, int64_t t) {
   constexpr int T = RS_DEDUP_TILE;
   // 16 groups per round trip: the group-leader keys and the group sums are loaded together
   // (speculatively past the segment's end, discarded there), then added in group order — a hot
@@ -658,9 +695,6 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
   constexpr int U = 16;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
-  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> lpr_log2) + (threadIdx.x >> lpr_log2);
-  if (t >= n_tiles - 1) return;
-  if (!(a.tile_flags[t] & 1)) return;  // not the head tile of a spanning segment
   const int64_t klast = t * T + T - 1;
   const uint32_t row = keys[klast];
   const int dim = a.dim;
@@ -882,8 +916,12 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
       seg_chunk_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,          \
                                                          geom.lpr_log2, n_tiles, a.chunk);      \
     }                                                                                           \
-    seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,      \
-                                                             geom.lpr_log2, n_tiles, a.chunk);  \
+    if (g32)                                                                                    \
+      seg_fixup_sweep_kernel<OPTV><<<(unsigned)std::min<int64_t>(ceil_div(n_tiles, 256), 1024),  \
+                                     256, 0, st>>>(keys, a, n_tiles, a.chunk);                  \
+    else                                                                                        \
+      seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,    \
+                                                               geom.lpr_log2, n_tiles, a.chunk); \
   }))
   switch (opt) {
     case OPT_SGD: RS_SEG_LAUNCH(OPT_SGD); break;

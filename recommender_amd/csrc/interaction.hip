@@ -981,9 +981,13 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       for (int t = 0; t < NT; ++t) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
+#ifndef RS_AB_TRAIN_NO_ZMFMA
           c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a0[t][c], c00, 0, 0, 0);
           c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a1[t][c], c01, 0, 0, 0);
           c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
+#else  // A/B probe (wrong numbers): the Z chain without its MFMAs
+          c00[c] += a0[t][c]; c01[c] += a1[t][c]; c11[c] += a0[t][c] * a1[t][c];
+#endif
         }
       }
       // (2) X(b) → LDS
@@ -1053,8 +1057,12 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
         floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
+#ifndef RS_AB_TRAIN_NO_UMFMA
           d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
           d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
+#else  // A/B probe (wrong numbers): the U tiles without their MFMAs
+          d0[kk & 3] += bv[kk] * sa[0][kk]; d1[kk & 3] += bv[kk] * sa[1][kk];
+#endif
         }
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
