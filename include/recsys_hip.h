@@ -731,6 +731,48 @@ int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D, co
                                float* sums, void* workspace, size_t ws_bytes, int32_t* err_flag,
                                void* stream);
 
+/* ---- the production DLRM step's dense tail (ctr/train.py:77-79 SGD of every MLP parameter;
+ * ctr/layers.py:5-14 linear hidden layers) ------------------------------------------------
+ * From the train step's sums: every kernel / bias gradient of the top chain [top_n0 rows of
+ * top_k[0] (top_rows / top_inv as rs_chain3_vec_grads) -> n1 -> n2 -> 1] and of the narrow
+ * bottom chain [bot_n0 -> n1 -> n2 -> n3] (P = [A_bot; s_bot], bot_comp2 = the current
+ * [K1·K2; c2] of rs_chain_aug_product), then param -= lr·grad for all twelve parameters
+ * (torch.optim.SGD's foreach update), then the next step's compositions from the updated
+ * parameters: bot_comp2_next = [K1·K2; c2], bot_comp3_next = [K1·K2·K3; c3] (rs_chain_aug_product
+ * x 2) and top_q [n0], top_c [1] (rs_chain3_vec_compose). Bottom gradients: dK3 -> bot_dk3,
+ * dK2 -> bot_dk2, bot_P2 [n0+1, n2] (row n0 = db2), bot_P1 [n0+1, n1] (rows 0..n0-1 = dK1,
+ * row n0 = db1), db3 = P row n0. Six stream-ordered launches; each value equals the separate
+ * rs_chain3_vec_grads / rs_chain_outer / rs_chain_rt_product / rs_chain_aug_product /
+ * rs_chain3_vec_compose calls bit for bit. */
+typedef struct rs_dlrm_tail_args {
+  float* top_k[3];
+  float* top_b[3];
+  const int32_t* top_rows;
+  const int32_t* top_inv;
+  int32_t top_n_full0, top_n0, top_n1, top_n2;
+  const float* top_A; /* [top_n0] */
+  const float* top_s; /* [1] */
+  float* top_dk[3];
+  float* top_db[3];
+  float* top_q; /* [top_n0] next-step composition */
+  float* top_c; /* [1] */
+  float* bot_k[3];
+  float* bot_b[3];
+  int32_t bot_n0, bot_n1, bot_n2, bot_n3;
+  const float* bot_P;     /* [bot_n0 + 1, bot_n3] */
+  const float* bot_comp2; /* [bot_n0 + 1, bot_n2] */
+  float* bot_dk2;         /* [bot_n1, bot_n2] */
+  float* bot_dk3;         /* [bot_n2, bot_n3] */
+  float* bot_P2;          /* [bot_n0 + 1, bot_n2] */
+  float* bot_P1;          /* [bot_n0 + 1, bot_n1] */
+  float* bot_comp2_next;  /* [bot_n0 + 1, bot_n2] */
+  float* bot_comp3_next;  /* [bot_n0 + 1, bot_n3] */
+  float lr;
+} rs_dlrm_tail_args;
+size_t rs_dlrm_dense_tail_workspace_size(int32_t top_n0, int32_t top_n1, int32_t top_n2);
+int32_t rs_dlrm_dense_tail(const rs_dlrm_tail_args* args, void* workspace, size_t ws_bytes,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,20 @@ class AdamParams(C.Structure):
                 ("epsilon", C.c_float)]
 
 
+class DlrmTailArgs(C.Structure):
+    """include/recsys_hip.h rs_dlrm_tail_args."""
+    _fields_ = [("top_k", C.c_void_p * 3), ("top_b", C.c_void_p * 3), ("top_rows", C.c_void_p),
+                ("top_inv", C.c_void_p), ("top_n_full0", C.c_int32), ("top_n0", C.c_int32),
+                ("top_n1", C.c_int32), ("top_n2", C.c_int32), ("top_A", C.c_void_p),
+                ("top_s", C.c_void_p), ("top_dk", C.c_void_p * 3), ("top_db", C.c_void_p * 3),
+                ("top_q", C.c_void_p), ("top_c", C.c_void_p), ("bot_k", C.c_void_p * 3),
+                ("bot_b", C.c_void_p * 3), ("bot_n0", C.c_int32), ("bot_n1", C.c_int32),
+                ("bot_n2", C.c_int32), ("bot_n3", C.c_int32), ("bot_P", C.c_void_p),
+                ("bot_comp2", C.c_void_p), ("bot_dk2", C.c_void_p), ("bot_dk3", C.c_void_p),
+                ("bot_P2", C.c_void_p), ("bot_P1", C.c_void_p), ("bot_comp2_next", C.c_void_p),
+                ("bot_comp3_next", C.c_void_p), ("lr", C.c_float)]
+
+
 _p, _i32, _i64, _sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
 _u32, _u64 = C.c_uint32, C.c_uint64
 _SIGS = {
@@ -109,6 +123,8 @@ _SIGS = {
     "rs_criteo_parse": (_i32, [_p, _i64, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "rs_crc32c_masked": (_i32, [_p, _i64, _p]),
     "rs_dlrm_train_workspace_size": (_sz, [_i64]),
+    "rs_dlrm_dense_tail_workspace_size": (_sz, [_i32, _i32, _i32]),
+    "rs_dlrm_dense_tail": (_i32, [C.POINTER(DlrmTailArgs), _p, _sz, _p]),
     "rs_dlrm_train_step_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p, _i64,
                                       _p, _p, C.c_float, _i32, _p, _p, _p, _p, _sz, _p, _p]),
     "rs_tfrecord_index": (_i32, [_p, _i64, _i32, _p, _p, _i64, _p]),

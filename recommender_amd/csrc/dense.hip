@@ -395,11 +395,12 @@ __device__ __forceinline__ void coldot_tile(const float* M, int ld, const int32_
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage1(Chain3Args a) {
+// Bodies take the (virtual) block index so the grouped dense-tail launches (rs_dlrm_dense_tail)
+// run exactly the arithmetic of the standalone kernels.
+__device__ __forceinline__ void chain3_stage1_body(const Chain3Args& a, int blk) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nq = (a.n1 + kC3Waves - 1) / kC3Waves;  // q1 blocks (one wave per output)
   const int nt = (a.n1 + 63) / 64;                   // T2 column tiles
-  int blk = blockIdx.x;
   if (blk < nq) {
     const int i = blk * kC3Waves + w;
     if (i < a.n1) rowdot_wave(a.K2, a.n2, i, a.n2, a.K3, a.q1 + i, lane);
@@ -419,20 +420,25 @@ __global__ __launch_bounds__(kC3Waves * 64) void chain3_stage1(Chain3Args a) {
     if (c < a.n2) a.c2[c] = a.b2 ? a.b2[c] : 0.f;
   }
 }
+__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage1(Chain3Args a) {
+  chain3_stage1_body(a, blockIdx.x);
+}
 
-__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage2(Chain3Args a) {
+__device__ __forceinline__ void chain3_stage2_body(const Chain3Args& a, int blk) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int npb = (a.n0 + kC3Waves - 1) / kC3Waves;
-  if ((int)blockIdx.x < npb) {
-    const int i = blockIdx.x * kC3Waves + w;
+  if (blk < npb) {
+    const int i = blk * kC3Waves + w;
     if (i < a.n0) rowdot_wave(a.K1, a.n1, a.r ? a.r[i] : i, a.n1, a.q1, a.p + i, lane);
     return;
   }
-  coldot_tile(a.K2, a.n2, nullptr, a.n1, a.n2, (blockIdx.x - npb) * 64, a.T2, nullptr, a.T3);
+  coldot_tile(a.K2, a.n2, nullptr, a.n1, a.n2, (blk - npb) * 64, a.T2, nullptr, a.T3);
+}
+__global__ __launch_bounds__(kC3Waves * 64) void chain3_stage2(Chain3Args a) {
+  chain3_stage2_body(a, blockIdx.x);
 }
 
-__global__ __launch_bounds__(256) void chain3_stage3(Chain3Args a) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void chain3_stage3_body(const Chain3Args& a, int64_t e) {
   const float s = a.s[0];
   const int64_t n_k1 = (int64_t)a.n_full0 * a.n1, n_k2 = (int64_t)a.n1 * a.n2;
   if (e < n_k1) {
@@ -460,6 +466,9 @@ __global__ __launch_bounds__(256) void chain3_stage3(Chain3Args a) {
     return;
   }
   if (f == a.n1) a.db3[0] = s;
+}
+__global__ __launch_bounds__(256) void chain3_stage3(Chain3Args a) {
+  chain3_stage3_body(a, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 // first level of a two-level fold for many chunks of a narrow row: block (cx, seg) folds the
@@ -518,9 +527,9 @@ struct VecComposeArgs {
   float* c;   // [1] out: c_L = b3 + K3ᵀ·b2 + q1ᵀ·b1
 };
 
-__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage1(VecComposeArgs a) {
+__device__ __forceinline__ void vcompose_stage1_body(const VecComposeArgs& a, int blk) {
   const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * kC3Waves + (threadIdx.x >> 6);
+  const int i = blk * kC3Waves + (threadIdx.x >> 6);
   if (i < a.n1) {
     rowdot_wave(a.K2, a.n2, i, a.n2, a.K3, a.q1 + i, lane);
   } else if (i == a.n1) {
@@ -531,10 +540,13 @@ __global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage1(VecComposeArgs 
     if (lane == 0) a.cb[0] = a.b3 ? acc + a.b3[0] : acc;
   }
 }
+__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage1(VecComposeArgs a) {
+  vcompose_stage1_body(a, blockIdx.x);
+}
 
-__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage2(VecComposeArgs a) {
+__device__ __forceinline__ void vcompose_stage2_body(const VecComposeArgs& a, int blk) {
   const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * kC3Waves + (threadIdx.x >> 6);
+  const int i = blk * kC3Waves + (threadIdx.x >> 6);
   if (i < a.n0) {
     rowdot_wave(a.K1, a.n1, a.r ? a.r[i] : i, a.n1, a.q1, a.q + i, lane);
   } else if (i == a.n0) {
@@ -544,6 +556,9 @@ __global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage2(VecComposeArgs 
     acc = wave_sum(acc);
     if (lane == 0) a.c[0] = acc + a.cb[0];
   }
+}
+__global__ __launch_bounds__(kC3Waves * 64) void vcompose_stage2(VecComposeArgs a) {
+  vcompose_stage2_body(a, blockIdx.x);
 }
 
 // Narrow-input product with a bias row: out[i, c] = Σ_k M̃[i, k]·K[k, c] (+ b[c] on row m),
@@ -555,10 +570,10 @@ constexpr int kAugRows = 33;
 constexpr int kAugLds = 16896;  // floats of M̃ staged in LDS: (m + 1)·k <= kAugLds
 
 template <int MR>
-__global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
+__device__ __forceinline__ void aug_product_body(
     const float* __restrict__ M, int ldm, int m, const float* __restrict__ cin,
     const float* __restrict__ K, int k, int n, const float* __restrict__ b,
-    float* __restrict__ out) {
+    float* __restrict__ out, int bx) {
   extern __shared__ float ms[];  // max((m + 1)·k, 8·MR·64) floats (aug_lds_bytes)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) {
@@ -566,7 +581,7 @@ __global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
     ms[e] = i < m ? M[(int64_t)i * ldm + kk] : (cin ? cin[kk] : 0.f);
   }
   __syncthreads();
-  const int c = blockIdx.x * 64 + lane;
+  const int c = bx * 64 + lane;
   float acc[MR];
 #pragma unroll
   for (int i = 0; i < MR; ++i) acc[i] = 0.f;
@@ -613,7 +628,7 @@ __global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
   }
   __syncthreads();
   for (int e = threadIdx.x; e < (m + 1) * 64; e += kC3Waves * 64) {
-    const int i = e >> 6, cl = e & 63, cc = blockIdx.x * 64 + cl;
+    const int i = e >> 6, cl = e & 63, cc = bx * 64 + cl;
     if (cc >= n) continue;
     float t = part[i * 64 + cl];
 #pragma unroll
@@ -621,6 +636,13 @@ __global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
     if (i == m && b) t += b[cc];
     out[(int64_t)i * n + cc] = t;
   }
+}
+template <int MR>
+__global__ __launch_bounds__(kC3Waves * 64) void aug_product_kernel(
+    const float* __restrict__ M, int ldm, int m, const float* __restrict__ cin,
+    const float* __restrict__ K, int k, int n, const float* __restrict__ b,
+    float* __restrict__ out) {
+  aug_product_body<MR>(M, ldm, m, cin, K, k, n, b, out, blockIdx.x);
 }
 
 template <int ACT>
@@ -691,14 +713,14 @@ __global__ __launch_bounds__(256) void affine_narrow_fwd_kernel(
 // rt_product: out [m+1, n] = P [m+1, k]·Kᵀ, K [n, k] row-major: P staged in LDS, one wave per
 // output column (lanes stride the contiguous row of K), fixed butterfly per row.
 template <int MR>
-__global__ __launch_bounds__(kC3Waves * 64) void rt_product_kernel(
-    const float* __restrict__ P, int m, const float* __restrict__ K, int k, int n,
-    float* __restrict__ out) {
+__device__ __forceinline__ void rt_product_body(const float* __restrict__ P, int m,
+                                                const float* __restrict__ K, int k, int n,
+                                                float* __restrict__ out, int bx) {
   extern __shared__ float ps[];  // (m + 1)·k floats
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) ps[e] = P[e];
   __syncthreads();
-  const int c = blockIdx.x * kC3Waves + w;
+  const int c = bx * kC3Waves + w;
   if (c >= n) return;
   float acc[MR];
 #pragma unroll
@@ -718,31 +740,49 @@ __global__ __launch_bounds__(kC3Waves * 64) void rt_product_kernel(
     if (lane == 0) out[(int64_t)i * n + c] = v;
   }
 }
+template <int MR>
+__global__ __launch_bounds__(kC3Waves * 64) void rt_product_kernel(
+    const float* __restrict__ P, int m, const float* __restrict__ K, int k, int n,
+    float* __restrict__ out) {
+  rt_product_body<MR>(P, m, K, k, n, out, blockIdx.x);
+}
 
 // out [na, nb] = R̃ᵀ·P: R̃ = [R (m rows, stride ldr); rlast] ([m+1, na], rlast NULL: a zero
 // row), P [m+1, nb] contiguous; four output columns per thread, r ascending.
-__global__ __launch_bounds__(256) void outer_sum_kernel(const float* __restrict__ R, int ldr, int m,
-                                                        const float* __restrict__ rlast, int na,
-                                                        const float* __restrict__ P, int nb,
-                                                        float* __restrict__ out) {
+// P4: P is 16-byte aligned (one float4 load per row); else four scalar loads, same arithmetic
+template <bool P4 = true>
+__device__ __forceinline__ void outer_sum_body(const float* __restrict__ R, int ldr, int m,
+                                               const float* __restrict__ rlast, int na,
+                                               const float* __restrict__ P, int nb,
+                                               float* __restrict__ out, int64_t e) {
   const int nbq = nb >> 2;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)na * nbq) return;
   const int a = (int)(e / nbq), bq = (int)(e - (int64_t)a * nbq);
-  const float4* P4 = reinterpret_cast<const float4*>(P);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int r = 0; r <= m; ++r) {
     float rv;
     if (r < m) rv = R[(int64_t)r * ldr + a];
     else if (rlast) rv = rlast[a];
     else break;
-    const float4 pv = P4[(int64_t)r * nbq + bq];
+    float4 pv;
+    if constexpr (P4) {
+      pv = reinterpret_cast<const float4*>(P)[(int64_t)r * nbq + bq];
+    } else {
+      const float* pp = P + ((int64_t)r * nbq + bq) * 4;
+      pv = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    }
     acc.x += rv * pv.x;
     acc.y += rv * pv.y;
     acc.z += rv * pv.z;
     acc.w += rv * pv.w;
   }
   reinterpret_cast<float4*>(out)[e] = acc;
+}
+__global__ __launch_bounds__(256) void outer_sum_kernel(const float* __restrict__ R, int ldr, int m,
+                                                        const float* __restrict__ rlast, int na,
+                                                        const float* __restrict__ P, int nb,
+                                                        float* __restrict__ out) {
+  outer_sum_body(R, ldr, m, rlast, na, P, nb, out, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 // y[b] = act(x[b, :n0]·q + c[0]): one wave per row (16-byte loads, q held in registers),
@@ -778,6 +818,110 @@ __global__ __launch_bounds__(256) void rowdot_act_kernel(const float* __restrict
     acc = wave_sum(acc);
     if (lane == 0) y[row] = act_fwd<ACT>(acc + cc);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// The production DLRM step's dense tail (rs_dlrm_dense_tail): every MLP parameter gradient of
+// the [n0 -> n1 -> n2 -> 1] top chain (rs_chain3_vec_grads) and the narrow [m -> n1 -> n2 -> n3]
+// bottom chain (nn._narrow_chain_grads_hip), the SGD update of all twelve parameters, and the
+// next step's compositions (rs_chain_aug_product x 2, rs_chain3_vec_compose) in six launches
+// instead of sixteen. Independent products share a launch (block ranges select the body); the
+// bodies are the standalone kernels' own, so every value is bit-identical to the separate calls.
+// Launch boundaries stay where a product reads another's output (no in-launch grid sync: these
+// launches run beside the HBM-bound sparse-update walk, which holds most CU slots).
+// ---------------------------------------------------------------------------------------
+struct TailOuter {
+  const float* R;
+  int ldr, m;
+  const float* rlast;
+  int na;
+  const float* P;
+  int nb;
+  float* out;
+  int64_t units() const { return (int64_t)na * (nb >> 2); }
+};
+struct TailRt {
+  const float* P;
+  int m;
+  const float* K;
+  int k, n;
+  float* out;
+};
+struct TailAug {
+  const float* M;
+  int ldm, m;
+  const float* cin;
+  const float* K;
+  int k, n;
+  const float* b;
+  float* out;
+};
+constexpr int kTailParams = 12;
+struct TailSgd {
+  float* p[kTailParams];
+  const float* g[kTailParams];
+  int64_t off[kTailParams + 1];  // element offsets of the concatenated parameter space
+  float lr;
+};
+
+// outer units -> 1024-thread blocks (4 virtual 256-thread blocks each)
+template <bool P4>
+__device__ __forceinline__ void tail_outer(const TailOuter& o, int bx) {
+  outer_sum_body<P4>(o.R, o.ldr, o.m, o.rlast, o.na, o.P, o.nb, o.out, (int64_t)bx * 1024 + threadIdx.x);
+}
+
+// grads 1: top stage 1 | bottom dK3 = R~2ᵀ·P | bottom P2 = P·K3ᵀ
+__global__ __launch_bounds__(kC3Waves * 64) void tail_grads1(Chain3Args top, int nb_top, TailOuter o,
+                                                             int nb_o, TailRt r) {
+  int bx = blockIdx.x;
+  if (bx < nb_top) { chain3_stage1_body(top, bx); return; }
+  bx -= nb_top;
+  if (bx < nb_o) { tail_outer<false>(o, bx); return; }
+  rt_product_body<16>(r.P, r.m, r.K, r.k, r.n, r.out, bx - nb_o);
+}
+// grads 2: top stage 2 | bottom dK2 = [K1; b1]ᵀ·P2 | bottom P1 = P2·K2ᵀ (= [dK1; db1])
+__global__ __launch_bounds__(kC3Waves * 64) void tail_grads2(Chain3Args top, int nb_top, TailOuter o,
+                                                             int nb_o, TailRt r) {
+  int bx = blockIdx.x;
+  if (bx < nb_top) { chain3_stage2_body(top, bx); return; }
+  bx -= nb_top;
+  if (bx < nb_o) { tail_outer<true>(o, bx); return; }
+  rt_product_body<16>(r.P, r.m, r.K, r.k, r.n, r.out, bx - nb_o);
+}
+// grads 3: the top chain's elementwise gradients
+__global__ __launch_bounds__(kC3Waves * 64) void tail_grads3(Chain3Args top) {
+  chain3_stage3_body(top, (int64_t)blockIdx.x * 1024 + threadIdx.x);
+}
+// SGD over the concatenated parameters: p = p + (-lr)·g, the update of torch.optim.SGD's
+// foreach path (_foreach_add_(params, grads, alpha=-lr)) with its fused multiply-add
+__global__ __launch_bounds__(256) void tail_sgd(TailSgd a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.off[kTailParams]) return;
+  int j = 0;
+#pragma unroll
+  for (int i = 1; i < kTailParams; ++i) j += e >= a.off[i] ? 1 : 0;
+  const int64_t o = e - a.off[j];
+#ifndef RS_SGD_UNFUSED
+  a.p[j][o] = fmaf(-a.lr, a.g[j][o], a.p[j][o]);
+#else
+  a.p[j][o] = a.p[j][o] + (-a.lr) * a.g[j][o];
+#endif
+}
+// compose 1: bottom R~2' = [K1; b1]·K2 + [0; b2] | top q1 = K2·K3, cb
+__global__ __launch_bounds__(kC3Waves * 64) void tail_compose1(TailAug g, int nb_aug, VecComposeArgs v) {
+  if ((int)blockIdx.x < nb_aug) {
+    aug_product_body<16>(g.M, g.ldm, g.m, g.cin, g.K, g.k, g.n, g.b, g.out, blockIdx.x);
+    return;
+  }
+  vcompose_stage1_body(v, blockIdx.x - nb_aug);
+}
+// compose 2: bottom R~3' = R~2'·K3 + [0; b3] | top q = K1[rows]·q1, c
+__global__ __launch_bounds__(kC3Waves * 64) void tail_compose2(TailAug g, int nb_aug, VecComposeArgs v) {
+  if ((int)blockIdx.x < nb_aug) {
+    aug_product_body<16>(g.M, g.ldm, g.m, g.cin, g.K, g.k, g.n, g.b, g.out, blockIdx.x);
+    return;
+  }
+  vcompose_stage2_body(v, blockIdx.x - nb_aug);
 }
 
 }  // namespace rs
@@ -1042,6 +1186,93 @@ extern "C" int32_t rs_chain_outer(const float* R, int32_t ldr, int32_t m, const 
   const int64_t tot = (int64_t)na * (nb / 4);
   outer_sum_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
       R, ldr, m, rlast, na, P, nb, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" size_t rs_dlrm_dense_tail_workspace_size(int32_t n0, int32_t n1, int32_t n2) {
+  return (size_t)(2 * n1 + 2 * n2 + std::max(n0, n1 + 1)) * sizeof(float);
+}
+
+extern "C" int32_t rs_dlrm_dense_tail(const rs_dlrm_tail_args* t, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  RS_CHECK_ARG(t, "rs_dlrm_dense_tail: null args");
+  const int n0 = t->top_n0, n1 = t->top_n1, n2 = t->top_n2, nf = t->top_n_full0;
+  const int m = t->bot_n0, b1 = t->bot_n1, b2 = t->bot_n2, b3 = t->bot_n3;
+  RS_CHECK_ARG(n0 >= 1 && n1 >= 1 && n2 >= 1 && nf >= n0 && (t->top_rows != nullptr) == (t->top_inv != nullptr) &&
+                   (t->top_rows || nf == n0),
+               "rs_dlrm_dense_tail: bad top chain sizes");
+  RS_CHECK_ARG(m >= 1 && m < 16 && b1 >= 4 && b2 >= 4 && b3 >= 4 && b1 % 4 == 0 && b2 % 4 == 0 &&
+                   b3 % 4 == 0 && (int64_t)(m + 1) * b1 <= kAugLds && (int64_t)(m + 1) * b2 <= kAugLds &&
+                   (int64_t)(m + 1) * b3 <= kAugLds,
+               "rs_dlrm_dense_tail: bad bottom chain sizes");
+  for (int i = 0; i < 3; ++i)
+    RS_CHECK_ARG(t->top_k[i] && t->top_b[i] && t->top_dk[i] && t->top_db[i] && t->bot_k[i] && t->bot_b[i],
+                 "rs_dlrm_dense_tail: null parameter / gradient");
+  RS_CHECK_ARG(t->top_A && t->top_s && t->top_q && t->top_c && t->bot_P && t->bot_comp2 && t->bot_dk2 &&
+                   t->bot_dk3 && t->bot_P2 && t->bot_P1 && t->bot_comp2_next && t->bot_comp3_next,
+               "rs_dlrm_dense_tail: null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_dlrm_dense_tail_workspace_size(n0, n1, n2), "workspace too small");
+  const uintptr_t al = reinterpret_cast<uintptr_t>(t->bot_P2) |
+                       reinterpret_cast<uintptr_t>(t->bot_dk2) | reinterpret_cast<uintptr_t>(t->bot_dk3);
+  RS_CHECK_ARG(al % 16 == 0 && reinterpret_cast<uintptr_t>(t->bot_P) % 4 == 0,
+               "rs_dlrm_dense_tail: bot_P2 / dk2 / dk3 must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  float* w = static_cast<float*>(workspace);
+  // top chain gradients (rs_chain3_vec_grads' stages); p (the input gradient) is not needed
+  Chain3Args top{t->top_k[0], t->top_rows, t->top_inv, t->top_b[0], t->top_k[1], t->top_b[1],
+                 t->top_k[2], t->top_A, t->top_s, nf, n0, n1, n2, w, w + n1, w + 2 * n1,
+                 w + 2 * n1 + n2, t->top_dk[0], t->top_db[0], t->top_dk[1], t->top_db[1],
+                 t->top_dk[2], t->top_db[2], w + 2 * n1 + 2 * n2};
+  // stage 2's p[i] rows (the top chain's input gradient) are a by-product the tail does not
+  // keep: they land in scratch
+  const int g1_top = (int)(ceil_div(n1, kC3Waves) + ceil_div(n1, 64) + ceil_div(n2, 64));
+  const int g2_top = (int)(ceil_div(n0, kC3Waves) + ceil_div(n2, 64));
+  // bottom: P = [A; s] [m+1, b3]; dK3 = R~2ᵀ·P; P2 = P·K3ᵀ [m+1, b2]; dK2 = [K1; b1]ᵀ·P2;
+  // P1 = P2·K2ᵀ [m+1, b1] = [dK1; db1]; db2 = P2[m]; db3 = P[m]
+  TailOuter o1{t->bot_comp2, b2, m, t->bot_comp2 + (size_t)m * b2, b2, t->bot_P, b3, t->bot_dk3};
+  TailRt r1{t->bot_P, m, t->bot_k[2], b3, b2, t->bot_P2};
+  TailOuter o2{t->bot_k[0], b1, m, t->bot_b[0], b1, t->bot_P2, b2, t->bot_dk2};
+  TailRt r2{t->bot_P2, m, t->bot_k[1], b2, b1, t->bot_P1};
+  const int nb_o1 = (int)ceil_div(o1.units(), 1024), nb_o2 = (int)ceil_div(o2.units(), 1024);
+  const int nb_r1 = (int)ceil_div(b2, kC3Waves), nb_r2 = (int)ceil_div(b1, kC3Waves);
+  tail_grads1<<<g1_top + nb_o1 + nb_r1, kC3Waves * 64, (size_t)(m + 1) * b3 * 4, st>>>(top, g1_top, o1, nb_o1, r1);
+  RS_CHECK_LAUNCH();
+  tail_grads2<<<g2_top + nb_o2 + nb_r2, kC3Waves * 64, (size_t)(m + 1) * b2 * 4, st>>>(top, g2_top, o2, nb_o2, r2);
+  RS_CHECK_LAUNCH();
+  const int64_t tot3 = (int64_t)nf * n1 + (int64_t)n1 * n2 + n2 + n1 + 1;
+  tail_grads3<<<(unsigned)ceil_div(tot3, 1024), kC3Waves * 64, 0, st>>>(top);
+  RS_CHECK_LAUNCH();
+  // SGD, parameter order: top K1 b1 K2 b2 K3 b3, bottom K1 b1 K2 b2 K3 b3
+  TailSgd sg{};
+  const int64_t sz[kTailParams] = {(int64_t)nf * n1, n1, (int64_t)n1 * n2, n2, n2, 1,
+                                   (int64_t)m * b1, b1, (int64_t)b1 * b2, b2, (int64_t)b2 * b3, b3};
+  float* ps[kTailParams] = {t->top_k[0], t->top_b[0], t->top_k[1], t->top_b[1], t->top_k[2], t->top_b[2],
+                            t->bot_k[0], t->bot_b[0], t->bot_k[1], t->bot_b[1], t->bot_k[2], t->bot_b[2]};
+  const float* gs[kTailParams] = {t->top_dk[0], t->top_db[0], t->top_dk[1], t->top_db[1], t->top_dk[2],
+                                  t->top_db[2], t->bot_P1, t->bot_P1 + (size_t)m * b1, t->bot_dk2,
+                                  t->bot_P2 + (size_t)m * b2, t->bot_dk3, t->bot_P + (size_t)m * b3};
+  sg.off[0] = 0;
+  for (int i = 0; i < kTailParams; ++i) {
+    sg.p[i] = ps[i];
+    sg.g[i] = gs[i];
+    sg.off[i + 1] = sg.off[i] + sz[i];
+  }
+  sg.lr = t->lr;
+  tail_sgd<<<(unsigned)ceil_div(sg.off[kTailParams], 256), 256, 0, st>>>(sg);
+  RS_CHECK_LAUNCH();
+  // next step's compositions from the updated parameters
+  TailAug a1{t->bot_k[0], b1, m, t->bot_b[0], t->bot_k[1], b1, b2, t->bot_b[1], t->bot_comp2_next};
+  TailAug a2{t->bot_comp2_next, b2, m, t->bot_comp2_next + (size_t)m * b2, t->bot_k[2], b2, b3,
+             t->bot_b[2], t->bot_comp3_next};
+  VecComposeArgs v{t->top_k[0], t->top_rows, t->top_b[0], t->top_k[1], t->top_b[1], t->top_k[2],
+                   t->top_b[2], n0, n1, n2, w, w + n1, t->top_q, t->top_c};
+  const size_t lds1 = (size_t)std::max<int64_t>((int64_t)(m + 1) * b1, 8 * 16 * 64) * 4;
+  const size_t lds2 = (size_t)std::max<int64_t>((int64_t)(m + 1) * b2, 8 * 16 * 64) * 4;
+  const int nb_a1 = (int)ceil_div(b2, 64), nb_a2 = (int)ceil_div(b3, 64);
+  tail_compose1<<<nb_a1 + (int)ceil_div(n1 + 1, kC3Waves), kC3Waves * 64, lds1, st>>>(a1, nb_a1, v);
+  RS_CHECK_LAUNCH();
+  tail_compose2<<<nb_a2 + (int)ceil_div(n0 + 1, kC3Waves), kC3Waves * 64, lds2, st>>>(a2, nb_a2, v);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

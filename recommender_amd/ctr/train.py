@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import os
 import time
 
 import numpy as np
@@ -58,6 +59,9 @@ class TrainStep:
             fused = False
         self.loss_reduction = loss_reduction
         self.fused_step = bool(fused_step)
+        # the fused step's plain-SGD MLP update + next compositions in rs_dlrm_dense_tail
+        # (RS_DENSE_TAIL=0: chain_param_grads + torch.optim.SGD, bit-identical)
+        self.dense_tail = os.environ.get("RS_DENSE_TAIL", "1") == "1"
         self.overlap_wgrad, self.overlap_pgrad = overlap_wgrad, overlap_param_grads
         # measured on MI355X: a weight-grad GEMM beside the interaction backward only
         # time-slices the CUs (no net gain), so the overlap is opt-in
@@ -202,11 +206,15 @@ class TrainStep:
                 g["lr"] = self._sched(self.opt_sparse.iterations)
         self.opt_dense.zero_grad(set_to_none=True)
         if self.fused_step_ready(batch):
-            from ..functional import dlrm_fused_train_forward
+            from ..functional import dense_tail_ready, dlrm_fused_train_forward
 
-            y, loss = dlrm_fused_train_forward(self.model, cat, dense_x, label, self.loss_reduction)
+            tail = self.dense_tail and dense_tail_ready(self.model, self.opt_dense)
+            lr = self.opt_dense.param_groups[0]["lr"] if tail else None
+            y, loss = dlrm_fused_train_forward(self.model, cat, dense_x, label, self.loss_reduction,
+                                               sgd_lr=lr)
             self.last_pred = y
-            self.opt_dense.step()
+            if not tail:
+                self.opt_dense.step()
             self.opt_sparse.step()
             return loss
         p = self.model({"cat_features": cat, "int_features": dense_x})

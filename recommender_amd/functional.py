@@ -6,6 +6,7 @@ upstream rows (position order) and ids to the owning EmbeddingTable, and the spa
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -328,7 +329,7 @@ TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hi
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
-                             epsilon=1e-7):
+                             epsilon=1e-7, sgd_lr=None):
     """The production DLRM train step's forward + loss + backward reductions in one kernel
     (rs_dlrm_train_step_fwd): the reference's DLRM.call (ctr/model.py:45-57) under the mean
     Keras BCE (ctr/train.py:85) with the SGD path's gradients (ctr/train.py:77-79).
@@ -339,8 +340,12 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     A_top, s_top, loss, A_bot, s_bot); every top / bottom MLP parameter gradient from those sums
     (nn.chain_param_grads: the factored backward's weight-sized products), accumulated into
     .grad; the segmented-sum sparse update queued on the fused optimizer's side stream.
+    sgd_lr (float): also apply plain SGD to every MLP parameter and compose the next step's
+    maps, all in rs_dlrm_dense_tail (bit-identical to chain_param_grads + torch.optim.SGD +
+    the next forward's compositions, in six launches instead of sixteen); the caller then skips
+    its dense optimizer step.
     Returns (prediction y [B] (detached), loss scalar tensor (no autograd graph))."""
-    from .nn import _composed_forward_hip, chain_param_grads, vec_chain_compose
+    from .nn import _composed_forward_hip, chain_param_grads, cached_vec_chain_compose
 
     emb = model.embedding_layer
     S, n_in = model.num_cat_fea, model.num_int_fea
@@ -358,7 +363,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         if got is None:
             raise RuntimeError("fused DLRM step: the bottom MLP is not a narrow composed chain")
         h, bks = got
-        q, c = vec_chain_compose(tl, rows, width)
+        q, c = cached_vec_chain_compose(tl, rows, width)
     w = emb.weight
     D = w.shape[1]
     dev = w.device
@@ -384,12 +389,103 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     early = _APPLY_EARLY
     if early:
         emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
-    chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
-    if not early:
-        emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
-    chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
+    if sgd_lr is not None:
+        if not early:
+            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+        _dense_tail_sgd(tl, rows, bl, A_top, s_top, sums[a + 2:].view(n_in + 1, D), sgd_lr)
+    else:
+        chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
+        if not early:
+            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+        chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
     loss = loss_sum / B if reduction == "mean" else loss_sum
     return y, loss
+
+
+def dense_tail_ready(model, opt_dense) -> bool:
+    """rs_dlrm_dense_tail applies: plain SGD (no momentum / dampening / weight decay / nesterov /
+    maximize, one group) over exactly the DLRM's twelve MLP parameters, bottom chain
+    [n0 < 16 -> n1 -> n2 -> n3] and top chain [n0 -> n1 -> n2 -> 1], all with biases."""
+    if not isinstance(opt_dense, torch.optim.SGD) or len(opt_dense.param_groups) != 1:
+        return False
+    g = opt_dense.param_groups[0]
+    if (g.get("momentum", 0) != 0 or g.get("weight_decay", 0) != 0 or g.get("nesterov")
+            or g.get("maximize") or g.get("dampening", 0) != 0 or callable(g["lr"])):
+        return False
+    bl, tl = list(model.bottom_mlp.mlp), list(model.top_mlp.mlp)
+    if len(bl) != 3 or len(tl) != 3 or any(l.bias is None for l in bl + tl):
+        return False
+    params = [t for l in tl + bl for t in (l.kernel, l.bias)]
+    if {id(p) for p in g["params"]} != {id(p) for p in params} or len(g["params"]) != 12:
+        return False
+    n0 = bl[0].kernel.shape[0]
+    return (n0 < 16 and tl[2].kernel.shape[1] == 1
+            and all(p.is_contiguous() and p.dtype == torch.float32 for p in params)
+            and all(l.kernel.shape[1] % 4 == 0 for l in bl)
+            and all((n0 + 1) * l.kernel.shape[0] <= 16896 for l in bl))
+
+
+def _dense_tail_sgd(tl, rows, bl, A_top, s_top, P_bot, lr):
+    """rs_dlrm_dense_tail: gradients into fresh .grad tensors (as chain_param_grads leaves them),
+    SGD on the twelve parameters, next step's compositions into the compose cache."""
+    from .nn import _rows_i32, narrow_chain_compose, store_composed
+
+    dev = A_top.device
+    comp2 = narrow_chain_compose(bl)[0]  # current [K1·K2; c2] (the forward's, cached)
+    n0, n1 = tl[0].kernel.shape[0], tl[0].kernel.shape[1]
+    n2 = tl[1].kernel.shape[1]
+    width = A_top.shape[0]
+    r, inv = _rows_i32(rows, n0)
+    m, b1 = bl[0].kernel.shape
+    b2, b3 = bl[1].kernel.shape[1], bl[2].kernel.shape[1]
+    tdk = [torch.empty_like(l.kernel) for l in tl]
+    tdb = [torch.empty_like(l.bias) for l in tl]
+    P2 = torch.empty(m + 1, b2, device=dev)
+    P1 = torch.empty(m + 1, b1, device=dev)
+    dk2 = torch.empty(b1, b2, device=dev)
+    dk3 = torch.empty(b2, b3, device=dev)
+    comp2n = torch.empty(m + 1, b2, device=dev)
+    comp3n = torch.empty(m + 1, b3, device=dev)
+    q = torch.empty(width, device=dev)
+    c = torch.empty(1, device=dev)
+    ws = _tail_ws(width, n1, n2, dev)
+    a = L.DlrmTailArgs()
+    for i in range(3):
+        a.top_k[i], a.top_b[i] = tl[i].kernel.data_ptr(), tl[i].bias.data_ptr()
+        a.top_dk[i], a.top_db[i] = tdk[i].data_ptr(), tdb[i].data_ptr()
+        a.bot_k[i], a.bot_b[i] = bl[i].kernel.data_ptr(), bl[i].bias.data_ptr()
+    a.top_rows = None if r is None else r.data_ptr()
+    a.top_inv = None if inv is None else inv.data_ptr()
+    a.top_n_full0, a.top_n0, a.top_n1, a.top_n2 = n0, width, n1, n2
+    a.top_A, a.top_s = A_top.data_ptr(), s_top.data_ptr()
+    a.top_q, a.top_c = q.data_ptr(), c.data_ptr()
+    a.bot_n0, a.bot_n1, a.bot_n2, a.bot_n3 = m, b1, b2, b3
+    a.bot_P, a.bot_comp2 = P_bot.data_ptr(), comp2.data_ptr()
+    a.bot_dk2, a.bot_dk3, a.bot_P2, a.bot_P1 = dk2.data_ptr(), dk3.data_ptr(), P2.data_ptr(), P1.data_ptr()
+    a.bot_comp2_next, a.bot_comp3_next = comp2n.data_ptr(), comp3n.data_ptr()
+    a.lr = float(lr)
+    L.call("rs_dlrm_dense_tail", C.byref(a), L.ptr(ws), ws.numel() * 4, L.stream_ptr(dev))
+    grads = list(zip(tdk, tdb)) + [(P1[:m], P1[m]), (dk2, P2[m]), (dk3, P_bot[m])]
+    for layer, (dk, db) in zip(tl + bl, grads):
+        layer.kernel.grad, layer.bias.grad = dk, db
+    # the kernels moved the parameters in place: bump their versions (stale caches of other
+    # consumers miss), then file the next step's compositions under the new versions
+    for l in tl + bl:
+        torch.autograd.graph.increment_version(l.kernel)
+        torch.autograd.graph.increment_version(l.bias)
+    store_composed(bl, [comp2n, comp3n], tl, rows, width, (q, c))
+
+
+_tail_ws_cache: dict = {}
+
+
+def _tail_ws(n0, n1, n2, dev):
+    n = (L.lib().rs_dlrm_dense_tail_workspace_size(n0, n1, n2) + 3) // 4
+    t = _tail_ws_cache.get(dev)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, device=dev)
+        _tail_ws_cache[dev] = t
+    return t
 
 
 _train_ws_cache: dict = {}

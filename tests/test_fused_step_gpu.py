@@ -164,3 +164,38 @@ def test_keras_adam_deferred_decay_bit_exact(factored_any_batch, fused_step):
     # not vacuous: thousands of rows were touched, most of them in only some of the steps, so
     # their skipped steps were replayed (by the next touch's catch-up or by materialize)
     assert int((m0 != 0).any(1).sum()) > 2000
+
+
+@pytest.mark.parametrize("bottom,top", [([512, 256, 128], [512, 256, 1]), ([128, 64, 128], [128, 64, 1])])
+def test_dense_tail_bit_identical(factored_any_batch, bottom, top):
+    """rs_dlrm_dense_tail (the MLP gradients, the SGD update and the next step's compositions in
+    six grouped launches) against chain_param_grads + torch.optim.SGD + the forward's own
+    compositions: parameters, gradients, predictions and table bit-identical over 3 steps."""
+    cards = criteo_cardinalities(300_000, 26)
+    rng = np.random.default_rng(21)
+    batches = []
+    for _ in range(3):
+        cat, dn, lb = criteo_batch(rng, 2048, cards)
+        batches.append(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+    runs = []
+    for tail in (True, False):
+        m = _model(cards, 6, bottom, top)
+        st = TrainStep(m, "sgd", lr=0.05, defer_sparse_join=True)
+        st.dense_tail = tail
+        preds, grads = [], None
+        for b in batches:
+            st(b)
+            preds.append(st.last_pred.clone())
+            grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        m.embedding_layer.wait_update()
+        torch.cuda.synchronize()
+        runs.append((m, preds, grads))
+    (mt, pt, gt), (mr, pr, gr) = runs
+    for a, b in zip(pt, pr):
+        assert torch.equal(a, b)
+    assert gt.keys() == gr.keys() and len(gt) == 12
+    for n in gt:
+        assert torch.equal(gt[n], gr[n]), n
+    for (n, p), q in zip(mt.named_parameters(), mr.parameters()):
+        assert torch.equal(p, q), n
+    assert torch.equal(mt.embedding_layer.weight, mr.embedding_layer.weight)
