@@ -60,20 +60,20 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
 
     captured = {}
     opt = step.opt_sparse
-    launch = opt._launch_apply
+    apply = opt.apply  # the side-stream and the current-stream (apply_now) update both call it
 
-    def spy(table, ids, grad_rows, sorted_ids, row_scale=None):
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
         captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
         captured["row_scale"] = row_scale
-        return launch(table, ids, grad_rows, sorted_ids, row_scale)
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
 
-    opt._launch_apply = spy
+    opt.apply = spy
     try:
         batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
                  torch.from_numpy(lb).to(dev))
         loss = float(step(batch).detach())
     finally:
-        opt._launch_apply = launch
+        del opt.apply
     emb.wait_update()
     torch.cuda.synchronize()
     assert "grad_rows" in captured, "the fused sparse apply did not run"
