@@ -14,7 +14,7 @@ namespace rs {
 
 constexpr int kSortThreads = 256;         // 4 waves
 #ifndef RS_SORT_KPL
-#define RS_SORT_KPL 16
+#define RS_SORT_KPL 8
 #endif
 constexpr int kSortKeysPerLane = RS_SORT_KPL;  // K: keys per lane per tile
 constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
