@@ -54,7 +54,7 @@ PMC_SYMBOLS = [
      "inter_fwd_mfma"),
     ("rs_dlrm_interaction_bwd_rank1", r"dlrm_bwd_pipe", "dlrm_bwd_pipe"),
     ("rs_sort_ids", r"radix_|scan_|count_unique", "radix_hist_kernel<[0-9]+, true>"),
-    ("rs_embedding_apply", r"seg_tile|seg_chunk|seg_fixup", "seg_tile"),
+    ("rs_embedding_apply", r"seg_tile|seg_group|seg_chunk|seg_fixup", "seg_tile|seg_group"),
 ]
 
 
@@ -104,7 +104,8 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = "dlrm_train_pipe|inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|count_unique|seg_tile|seg_chunk|seg_fixup"
+PMC_KERNEL_REGEX = ("dlrm_train_pipe|inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|"
+                    "count_unique|seg_tile|seg_group|seg_chunk|seg_fixup")
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 
