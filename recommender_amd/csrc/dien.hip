@@ -63,17 +63,22 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
   const float rbz = act ? rb[j] : 0.f, rbr = act ? rb[H + j] : 0.f, rbh = act ? rb[2 * H + j] : 0.f;
   const float* xb = xw + b * (int64_t)L * H3;
   const uint8_t* mb = mask + b * L;
+  // the mask row as wave-uniform bits: a step's branch waits on no load (a per-step mask load
+  // put one memory latency on every one of the L steps, masked or not)
+  const MaskBits mbits(mb, L, j);
   float h = 0.f;
-  float nz = act ? xb[j] : 0.f, nr = act ? xb[H + j] : 0.f, nh = act ? xb[2 * H + j] : 0.f;
+  const bool v0 = mbits.test(mb, 0);
+  float nz = act && v0 ? xb[j] : 0.f, nr = act && v0 ? xb[H + j] : 0.f,
+        nh = act && v0 ? xb[2 * H + j] : 0.f;
   for (int t = 0; t < L; ++t) {
     const float xz = nz, xr = nr, xh = nh;
-    if (t + 1 < L && act) {  // prefetch the next step's input projection
+    if (t + 1 < L && act && mbits.test(mb, t + 1)) {  // prefetch the next valid step's x·W
       const float* xn = xb + (int64_t)(t + 1) * H3;
       nz = xn[j];
       nr = xn[H + j];
       nh = xn[2 * H + j];
     }
-    if (!mb[t]) {
+    if (!mbits.test(mb, t)) {
       // masked step (wave-uniform: one example per wave): the state is carried, so the step's
       // arithmetic is skipped — its result would be discarded; the backward never reads its
       // saved row (post-padded histories make most of the L steps such steps)
@@ -223,10 +228,25 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
   }
   const float* xb = xw + b * (int64_t)L * H3;
   const uint8_t* mb = mask + b * L;
+  const MaskBits mbits(mb, L, j);
   const float* ab = att + b * L;
   float h = 0.f;
+  // the next valid step's x·W row and attention weight are loaded while this step computes
+  float nu = 0.f, nr = 0.f, nh = 0.f, na = 0.f;
+  auto fetch = [&](int t) {
+    if (!mbits.test(mb, t)) return;
+    const float* x = xb + (int64_t)t * H3;
+    na = ab[t];
+    if (act) {
+      nu = x[j];
+      nr = x[H + j];
+      nh = x[2 * H + j];
+    }
+  };
+  fetch(0);
   for (int t = 0; t < L; ++t) {
-    if (!mb[t]) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
+    if (!mbits.test(mb, t)) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
+      if (t + 1 < L) fetch(t + 1);
       if (act) {
         const int64_t o = b * L + t;
         if (states) states[o * H + j] = h;
@@ -236,9 +256,9 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
       }
       continue;
     }
-    const float* x = xb + (int64_t)t * H3;
-    const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
-    const float a = ab[t];
+    const float xu = act ? nu : 0.f, xr = act ? nr : 0.f, xh = act ? nh : 0.f;
+    const float a = na;
+    if (t + 1 < L) fetch(t + 1);
     float iu = 0.f, ir = 0.f;
 #pragma unroll
     for (int k = 0; k < HM; ++k) {
