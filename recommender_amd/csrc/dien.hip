@@ -19,6 +19,20 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+// One gate's recurrent weights in LDS (w(k, j) for lane j, row k; 0 outside H x H) instead of
+// VGPRs: with two gates' columns in registers the kernels fit 4 waves per SIMD (<= 128 VGPRs),
+// so the whole batch's waves are resident in one round (at 3 waves per SIMD, B = 4096 examples
+// took 1.33 rounds: the last third of the waves ran a second full recurrence behind the rest).
+// Called by every thread of the block before any wave returns.
+template <int HM, class F>
+__device__ __forceinline__ void stage_gate(float* ws, int H, F w) {
+  for (int e = threadIdx.x; e < HM * 64; e += blockDim.x) {
+    const int k = e >> 6, jj = e & 63;
+    ws[e] = (k < H && jj < H) ? w(k, jj) : 0.f;
+  }
+  __syncthreads();
+}
+
 // An example's mask row as wave-uniform bit words (L <= 256); longer rows read the byte.
 struct MaskBits {
   uint64_t w[4];
@@ -49,16 +63,17 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ saved) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  const int H3 = 3 * H;
+  __shared__ float uh_s[HM * 64];
+  stage_gate<HM>(uh_s, H, [&](int k, int jj) { return U[k * H3 + 2 * H + jj]; });
   if (b >= B) return;
   const bool act = j < H;
-  const int H3 = 3 * H;
-  float uz[HM], ur[HM], uh[HM];
+  float uz[HM], ur[HM];
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
     uz[k] = ok ? U[k * H3 + j] : 0.f;
     ur[k] = ok ? U[k * H3 + H + j] : 0.f;
-    uh[k] = ok ? U[k * H3 + 2 * H + j] : 0.f;
   }
   const float rbz = act ? rb[j] : 0.f, rbr = act ? rb[H + j] : 0.f, rbh = act ? rb[2 * H + j] : 0.f;
   const float* xb = xw + b * (int64_t)L * H3;
@@ -91,7 +106,7 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
       const float hk = bcast(h, k);
       iz = fmaf(hk, uz[k], iz);
       ir = fmaf(hk, ur[k], ir);
-      ih = fmaf(hk, uh[k], ih);
+      ih = fmaf(hk, uh_s[k * 64 + j], ih);
     }
     iz += rbz;
     ir += rbr;
@@ -126,16 +141,17 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ dinner) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  const int H3 = 3 * H;
+  __shared__ float wh_s[HM * 64];
+  stage_gate<HM>(wh_s, H, [&](int k, int jj) { return U[jj * H3 + 2 * H + k]; });
   if (b >= B) return;
   const bool act = j < H;
-  const int H3 = 3 * H;
-  float wz[HM], wr[HM], wh[HM];  // row j of U: U[j][g*H + k]
+  float wz[HM], wr[HM];  // row j of U: U[j][g*H + k]
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
     wz[k] = ok ? U[j * H3 + k] : 0.f;
     wr[k] = ok ? U[j * H3 + H + k] : 0.f;
-    wh[k] = ok ? U[j * H3 + 2 * H + k] : 0.f;
   }
   const uint8_t* mb = mask + b * L;
   const MaskBits mbits(mb, L, j);
@@ -191,7 +207,7 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
     for (int k = 0; k < HM; ++k) {
       acc = fmaf(bcast(dpz, k), wz[k], acc);
       acc = fmaf(bcast(dpr, k), wr[k], acc);
-      acc = fmaf(bcast(dihm, k), wh[k], acc);
+      acc = fmaf(bcast(dihm, k), wh_s[k * 64 + j], acc);
     }
     dh = act ? acc : 0.f;
   }
@@ -215,38 +231,24 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ saved) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  __shared__ float kh_s[HM * 64];
+  stage_gate<HM>(kh_s, H, [&](int k, int jj) { return Khr[k * H + jj]; });
   if (b >= B) return;
   const bool act = j < H;
   const int H3 = 3 * H;
-  float ku[HM], kr[HM], kh[HM];
+  float ku[HM], kr[HM];
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
     ku[k] = ok ? Kuh[k * H + j] : 0.f;
     kr[k] = ok ? Krh[k * H + j] : 0.f;
-    kh[k] = ok ? Khr[k * H + j] : 0.f;
   }
   const float* xb = xw + b * (int64_t)L * H3;
   const uint8_t* mb = mask + b * L;
-  const MaskBits mbits(mb, L, j);
   const float* ab = att + b * L;
   float h = 0.f;
-  // the next valid step's x·W row and attention weight are loaded while this step computes
-  float nu = 0.f, nr = 0.f, nh = 0.f, na = 0.f;
-  auto fetch = [&](int t) {
-    if (!mbits.test(mb, t)) return;
-    const float* x = xb + (int64_t)t * H3;
-    na = ab[t];
-    if (act) {
-      nu = x[j];
-      nr = x[H + j];
-      nh = x[2 * H + j];
-    }
-  };
-  fetch(0);
   for (int t = 0; t < L; ++t) {
-    if (!mbits.test(mb, t)) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
-      if (t + 1 < L) fetch(t + 1);
+    if (!mb[t]) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
       if (act) {
         const int64_t o = b * L + t;
         if (states) states[o * H + j] = h;
@@ -256,9 +258,9 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
       }
       continue;
     }
-    const float xu = act ? nu : 0.f, xr = act ? nr : 0.f, xh = act ? nh : 0.f;
-    const float a = na;
-    if (t + 1 < L) fetch(t + 1);
+    const float* x = xb + (int64_t)t * H3;
+    const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
+    const float a = ab[t];
     float iu = 0.f, ir = 0.f;
 #pragma unroll
     for (int k = 0; k < HM; ++k) {
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
     const float rh = act ? r * h : 0.f;
     float ihh = 0.f;
 #pragma unroll
-    for (int k = 0; k < HM; ++k) ihh = fmaf(bcast(rh, k), kh[k], ihh);
+    for (int k = 0; k < HM; ++k) ihh = fmaf(bcast(rh, k), kh_s[k * 64 + j], ihh);
     const float hh = tanhf(xh + ihh);
     const float ua = u * a;
     const float hn = ua * hh + (1.f - ua) * h;
@@ -304,16 +306,17 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
                                                         float* __restrict__ datt) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  __shared__ float kh_s[HM * 64];
+  stage_gate<HM>(kh_s, H, [&](int k, int jj) { return Khr[jj * H + k]; });
   if (b >= B) return;
   const bool act = j < H;
   const int H3 = 3 * H;
-  float ku[HM], kr[HM], kh[HM];  // rows j
+  float ku[HM], kr[HM];  // rows j
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
     ku[k] = ok ? Kuh[j * H + k] : 0.f;
     kr[k] = ok ? Krh[j * H + k] : 0.f;
-    kh[k] = ok ? Khr[j * H + k] : 0.f;
   }
   const uint8_t* mb = mask + b * L;
   const MaskBits mbits(mb, L, j);
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
     const float dph = act ? dh * ua * (1.f - hh * hh) : 0.f;
     float drh = 0.f;
 #pragma unroll
-    for (int k = 0; k < HM; ++k) drh = fmaf(bcast(dph, k), kh[k], drh);
+    for (int k = 0; k < HM; ++k) drh = fmaf(bcast(dph, k), kh_s[k * 64 + j], drh);
     const float dr = drh * hp;
     dhp = fmaf(drh, r, dhp);
     const float dpr = act ? dr * r * (1.f - r) : 0.f;
