@@ -68,8 +68,15 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     uint32_t* __restrict__ keys, KeyGen kg, int64_t n, int shift, int32_t* __restrict__ hist,
     int n_tiles) {
   constexpr int BINS = 1 << BITS;
+  constexpr int kMaxLdsSlots = 128;
   __shared__ int32_t cnt[BINS];
+  __shared__ int64_t offs[FROM_IDS ? kMaxLdsSlots + 1 : 1];
   for (int d = threadIdx.x; d < BINS; d += blockDim.x) cnt[d] = 0;
+  // pass 0 of an id sort: the slot offsets in LDS and the slot from a 32-bit modulo (n < 2^31)
+  // instead of a 64-bit one and two global loads per key
+  const bool lds_slots = FROM_IDS && kg.slot_offsets && kg.n_slots <= kMaxLdsSlots;
+  if (lds_slots)
+    for (int e = threadIdx.x; e <= kg.n_slots; e += blockDim.x) offs[e] = kg.slot_offsets[e];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -79,8 +86,27 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
   for (int k = 0; k < kSortKeysPerLane; ++k) {
     const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
     if (FROM_IDS) {
-      kv[k] = i < n ? make_key(kg, i, oob) : 0u;
-      if (i < n) keys[i] = kv[k];
+      if (lds_slots) {
+        uint32_t key = 0u;
+        if (i < n) {
+          const int64_t id = load_id(kg.ids, kg.dtype, i);
+          const int sl = (int)((uint32_t)i % (uint32_t)kg.n_slots);
+          const int64_t lo = offs[sl], hi = offs[sl + 1];
+          if (id < 0 || id >= hi - lo) {
+            oob = true;
+            key = static_cast<uint32_t>(kg.key_space);  // sentinel: sorts after every valid row
+          } else {
+            const int64_t r = lo + id;
+            key = static_cast<uint32_t>(kg.world == 1 ? r
+                                                       : (r % kg.world) * kg.shard_stride + r / kg.world);
+          }
+          keys[i] = key;
+        }
+        kv[k] = key;
+      } else {
+        kv[k] = i < n ? make_key(kg, i, oob) : 0u;
+        if (i < n) keys[i] = kv[k];
+      }
     } else {
       kv[k] = i < n ? keys[i] : 0u;
     }
