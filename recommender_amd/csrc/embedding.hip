@@ -662,6 +662,75 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const uint32_t* __restri
   fixup_one<OPT, VEC, CPL>(keys, a, lpr_log2, n_tiles, chunk, t);
 }
 
+// Level 2 with the whole wave on one head tile (the generic-D path): each of the wave's
+// 64/lpr lane groups loads 16 following groups' leader keys and sums, so a hot row spanning
+// hundreds of groups (DIEN's padding id: ~350 groups) costs one load latency per 64 groups
+// instead of per 16; the group sums are then added in group order by shuffling each lane
+// group's values across, so the additions are those of fixup_one, in the same order.
+template <int OPT, int VEC, int CPL>
+__global__ __launch_bounds__(256) void seg_fixup_wave_kernel(const uint32_t* __restrict__ keys,
+                                                             ApplyArgs a, int lpr_log2,
+                                                             int64_t n_tiles,
+                                                             const float* __restrict__ chunk) {
+  constexpr int T = RS_DEDUP_TILE;
+  constexpr int U = 16;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_tiles - 1) return;             // wave-uniform
+  if (!(a.tile_flags[t] & 1)) return;       // not the head tile of a spanning segment
+  const int lane = threadIdx.x & 63;
+  const int lpr = 1 << lpr_log2;
+  const int nlg = 64 >> lpr_log2;           // lane groups per wave (1..64)
+  const int lg = lane >> lpr_log2, gl = lane & (lpr - 1);
+  const int64_t klast = t * T + T - 1;
+  const uint32_t row = keys[klast];
+  const int dim = a.dim;
+  float acc[CPL][VEC];
+  load_or_zero<VEC, CPL>(chunk + (t * 2 + 1) * (int64_t)dim, dim, gl, lpr, acc);
+  const int span = nlg * U < 64 ? nlg * U : 64;  // groups per round (<= 64 continuation bits)
+  for (int64_t g = t / kFixChunk + 1;; g += span) {
+    uint32_t k[U];
+    float r[U][CPL][VEC];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t gg = g + (int64_t)lg * U + u;
+      const int64_t tt = gg * kFixChunk;
+      const bool in = lg * U + u < span && tt < n_tiles;
+      k[u] = in ? keys[tt * T] : ~row;
+      if (in)
+        load_or_zero<VEC, CPL>(chunk + (tt * 2) * (int64_t)dim, dim, gl, lpr, r[u]);
+      else
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
+      mine |= (k[u] == row ? 1u : 0u) << u;
+    }
+    // continuation bits of all lane groups, in group order; the segment covers the leading ones
+    uint64_t w = 0;
+    for (int src = 0; src < nlg && src * U < span; ++src)
+      w |= (uint64_t)(uint32_t)__shfl((int)mine, src * lpr) << (src * U);
+    const int nrun = ~w == 0ull ? 64 : (int)__builtin_ctzll(~w);  // bits >= span are 0
+    for (int src = 0; src < nlg && src * U < nrun; ++src) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float v[CPL][VEC];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[c][e] = __shfl(r[u][c][e], src * lpr + gl);
+        if (src * U + u < nrun)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[c][e] += v[c][e];
+      }
+    }
+    if (nrun < span) break;
+  }
+  if (lg == 0) finalize_row<OPT, VEC, CPL>(a, row, gl, lpr, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, klast) : 0);
+}
+
 // The level-2 pass after seg_group32_kernel: few tiles head a segment that crosses a group edge,
 // so a small grid sweeps the tile flags instead of one lane group per tile — each half-wave
 // loads the flags of 32 tiles at once and folds the flagged ones (same fold as seg_fixup_kernel).
@@ -920,8 +989,8 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
       seg_fixup_sweep_kernel<OPTV><<<(unsigned)std::min<int64_t>(ceil_div(n_tiles, 256), 1024),  \
                                      256, 0, st>>>(keys, a, n_tiles, a.chunk);                  \
     else                                                                                        \
-      seg_fixup_kernel<OPTV, VEC, CPL><<<blocks, 256, 0, st>>>(keys, n, (uint32_t)n_rows, a,    \
-                                                               geom.lpr_log2, n_tiles, a.chunk); \
+      seg_fixup_wave_kernel<OPTV, VEC, CPL><<<(unsigned)ceil_div(n_tiles, 4), 256, 0, st>>>(    \
+          keys, a, geom.lpr_log2, n_tiles, a.chunk);                                            \
   }))
   switch (opt) {
     case OPT_SGD: RS_SEG_LAUNCH(OPT_SGD); break;
