@@ -51,6 +51,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--rows", type=int, default=40_000_000)
+    ap.add_argument("--pinsage-mode", default="graph", choices=["dynamic", "static", "graph"],
+                    help="pinsage: dynamic = host-synced shapes (PinSageStep.__call__); static = "
+                         "capacity-shaped sync-free batches, eager (static_step); graph = the same "
+                         "step captured once and replayed (PinSageStep.capture), sampling eager")
     ap.add_argument("--tuned-gemms", type=int, default=-1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
                          "-1 (default): on for the fixed-shape models (dien, esmm, mmoe), off for the "
@@ -103,12 +107,20 @@ def main():
         m = PinSageModel(g, g.itype, 2, 8, 32, 16)
         train = PinSageStep(m)
         smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
-        ctr = {"step": 0}
+        ctr = {"step": 0, "replay": None}
 
         def step(_):
-            h, p, n = item_pairs(g, B, 4, ctr["step"])
+            it = ctr["step"]
             ctr["step"] += 1
-            return train(*smp.sample_from_item_pairs(h, p, n))
+            if args.pinsage_mode == "dynamic":
+                h, p, n = item_pairs(g, B, 4, it)
+                return train(*smp.sample_from_item_pairs(h, p, n))
+            batch = smp.sample_static(*smp.sample_pairs_static(B, 4, it))
+            if args.pinsage_mode == "static" or it == 0:
+                return train.static_step(*batch)
+            if ctr["replay"] is None:
+                ctr["replay"] = train.capture(batch)
+            return ctr["replay"]()
 
         batches = [(None,)]
         watch = ["rs_item_pairs", "rs_pinsage_neighbors", "rs_unique_first", "rs_pinsage_block",

@@ -387,7 +387,8 @@ int32_t rs_pair_set_build(const int32_t* src, const int32_t* dst, int64_t n, uin
  * traversal is one visit (self-visits count); the num_neighbors most visited (count desc,
  * item id asc — DGL's tie order is unspecified) become in-edges with weight = count; then
  * edges (src, dst=seed) in the exclusion set (excl_capacity 0 = none) are dropped without
- * back-filling. nbr/cnt [n_seeds, num_neighbors], -1/0 in empty slots.
+ * back-filling. nbr/cnt [n_seeds, num_neighbors], -1/0 in empty slots; a seed < 0 (padding
+ * of a capacity-shaped batch) gets k empty slots.
  * Limits: num_walks <= 64, n_traversals <= 8. */
 int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
                              const int64_t* u2i_indptr, const int32_t* u2i_idx,
@@ -437,6 +438,17 @@ int32_t rs_frobenius_normalize_fwd(const float* x, int64_t n, float* y, float* n
                                    void* workspace, size_t ws_bytes, void* stream);
 int32_t rs_frobenius_normalize_bwd(const float* dy, const float* y, const float* norm, int64_t n,
                                    float* dx, void* workspace, size_t ws_bytes, void* stream);
+/* The same over a capacity-shaped [n_cap_rows, row_len] buffer whose first *n_rows (device
+ * int32) rows are live (PinSageStep's sync-free batches): the norm / dot run over the live
+ * rows only (bit-identical to the unpadded call), padding elements of y / dx are written 0.
+ * Workspace: rs_frobenius_workspace_size(n_cap_rows * row_len). */
+int32_t rs_frobenius_normalize_rows_fwd(const float* x, int64_t n_cap_rows, int32_t row_len,
+                                        const int32_t* n_rows, float* y, float* norm,
+                                        void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_frobenius_normalize_rows_bwd(const float* dy, const float* y, const float* norm,
+                                        int64_t n_cap_rows, int32_t row_len,
+                                        const int32_t* n_rows, float* dx, void* workspace,
+                                        size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * EGES / GES / DeepWalk (eges/model.py).

@@ -202,8 +202,9 @@ __global__ __launch_bounds__(256) void neighbors_kernel(
   const int32_t grp = tid >> wshift;
   const int32_t j = tid & (wp - 1);
   const int64_t s = (int64_t)blockIdx.x * (256 >> wshift) + grp;
-  const bool live = s < n_seeds && j < num_walks;
   const int32_t start = s < n_seeds ? seeds[s] : -1;
+  // a padding seed (< 0, capacity-shaped batches) walks nowhere and gets k empty slots
+  const bool live = s < n_seeds && j < num_walks && start >= 0;
   int32_t* mine = cand + tid * T;
   for (int32_t t = 0; t < T; ++t) mine[t] = -1;
   if (live)
@@ -229,6 +230,8 @@ __global__ __launch_bounds__(256) void neighbors_kernel(
       }
       gcc[me] = first ? c : 0;
     }
+  } else if (j < num_walks) {
+    for (int32_t t = 0; t < T; ++t) gcc[j * T + t] = 0;
   }
   __syncthreads();
   if (s >= n_seeds || j != 0) return;
@@ -408,11 +411,23 @@ __device__ __forceinline__ float block_sum(float v, float* sm) {
 }
 
 // partial[b] = Σ a[i] * b[i] over chunk b (b == nullptr: Σ a[i]^2)
+// live length of a capacity-shaped [rows, row_len] buffer: the first *n_rows rows
+// (n_rows == nullptr: all n elements). Elements past it are padding: excluded from the
+// reduction and written as 0.
+__device__ __forceinline__ int64_t live_len(int64_t n, const int32_t* n_rows, int32_t row_len) {
+  if (!n_rows) return n;
+  const int64_t m = (int64_t)*n_rows * row_len;
+  return m < n ? m : n;
+}
+
 __global__ __launch_bounds__(kRedThreads) void dot_partial_kernel(const float* __restrict__ a,
                                                                   const float* __restrict__ b,
-                                                                  int64_t n,
+                                                                  int64_t n_cap,
+                                                                  const int32_t* __restrict__ n_rows,
+                                                                  int32_t row_len,
                                                                   float* __restrict__ partial) {
   __shared__ float sm[kRedThreads];
+  const int64_t n = live_len(n_cap, n_rows, row_len);
   const int64_t base = (int64_t)blockIdx.x * kRedChunk;
   float acc = 0.f;
   for (int64_t i = base + threadIdx.x; i < base + kRedChunk && i < n; i += kRedThreads) {
@@ -435,19 +450,25 @@ __global__ __launch_bounds__(kRedThreads) void fold_partial_kernel(const float* 
 }
 
 __global__ __launch_bounds__(256) void scale_div_kernel(const float* __restrict__ x, int64_t n,
+                                                        const int32_t* __restrict__ n_rows,
+                                                        int32_t row_len,
                                                         const float* __restrict__ norm,
                                                         float* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = x[i] / *norm;
+  if (i >= n) return;
+  y[i] = i < live_len(n, n_rows, row_len) ? x[i] / *norm : 0.f;
 }
 
 __global__ __launch_bounds__(256) void frob_bwd_kernel(const float* __restrict__ dy,
                                                        const float* __restrict__ y, int64_t n,
+                                                       const int32_t* __restrict__ n_rows,
+                                                       int32_t row_len,
                                                        const float* __restrict__ norm,
                                                        const float* __restrict__ dot,
                                                        float* __restrict__ dx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dx[i] = (dy[i] - y[i] * *dot) / *norm;
+  if (i >= n) return;
+  dx[i] = i < live_len(n, n_rows, row_len) ? (dy[i] - y[i] * *dot) / *norm : 0.f;
 }
 
 inline unsigned grid_for(int64_t n, int threads = 256) {
@@ -710,36 +731,68 @@ extern "C" size_t rs_frobenius_workspace_size(int64_t n) {
   return align_up((size_t)(ceil_div(n < 1 ? 1 : n, kRedChunk) + 2) * 4, 256);
 }
 
-extern "C" int32_t rs_frobenius_normalize_fwd(const float* x, int64_t n, float* y, float* norm,
-                                              void* workspace, size_t ws_bytes, void* stream) {
+static int32_t frobenius_fwd(const float* x, int64_t n, const int32_t* n_rows, int32_t row_len,
+                             float* y, float* norm, void* workspace, size_t ws_bytes,
+                             void* stream) {
   RS_CHECK_ARG(n >= 1, "rs_frobenius_normalize_fwd: empty input");
   RS_CHECK_ARG(ws_bytes >= rs_frobenius_workspace_size(n), "rs_frobenius: workspace too small");
   hipStream_t st = as_stream(stream);
   const int64_t nb = ceil_div(n, kRedChunk);
   float* partial = static_cast<float*>(workspace);
-  dot_partial_kernel<<<(unsigned)nb, kRedThreads, 0, st>>>(x, nullptr, n, partial);
+  dot_partial_kernel<<<(unsigned)nb, kRedThreads, 0, st>>>(x, nullptr, n, n_rows, row_len,
+                                                           partial);
   RS_CHECK_LAUNCH();
   fold_partial_kernel<<<1, kRedThreads, 0, st>>>(partial, nb, 0, norm);
   RS_CHECK_LAUNCH();
-  scale_div_kernel<<<grid_for(n), 256, 0, st>>>(x, n, norm, y);
+  scale_div_kernel<<<grid_for(n), 256, 0, st>>>(x, n, n_rows, row_len, norm, y);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
 
-extern "C" int32_t rs_frobenius_normalize_bwd(const float* dy, const float* y, const float* norm,
-                                              int64_t n, float* dx, void* workspace,
-                                              size_t ws_bytes, void* stream) {
+static int32_t frobenius_bwd(const float* dy, const float* y, const float* norm, int64_t n,
+                             const int32_t* n_rows, int32_t row_len, float* dx, void* workspace,
+                             size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(n >= 1, "rs_frobenius_normalize_bwd: empty input");
   RS_CHECK_ARG(ws_bytes >= rs_frobenius_workspace_size(n), "rs_frobenius: workspace too small");
   hipStream_t st = as_stream(stream);
   const int64_t nb = ceil_div(n, kRedChunk);
   float* partial = static_cast<float*>(workspace);
   float* dot = partial + nb;
-  dot_partial_kernel<<<(unsigned)nb, kRedThreads, 0, st>>>(dy, y, n, partial);
+  dot_partial_kernel<<<(unsigned)nb, kRedThreads, 0, st>>>(dy, y, n, n_rows, row_len, partial);
   RS_CHECK_LAUNCH();
   fold_partial_kernel<<<1, kRedThreads, 0, st>>>(partial, nb, 1, dot);
   RS_CHECK_LAUNCH();
-  frob_bwd_kernel<<<grid_for(n), 256, 0, st>>>(dy, y, n, norm, dot, dx);
+  frob_bwd_kernel<<<grid_for(n), 256, 0, st>>>(dy, y, n, n_rows, row_len, norm, dot, dx);
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_frobenius_normalize_fwd(const float* x, int64_t n, float* y, float* norm,
+                                              void* workspace, size_t ws_bytes, void* stream) {
+  return frobenius_fwd(x, n, nullptr, 1, y, norm, workspace, ws_bytes, stream);
+}
+
+extern "C" int32_t rs_frobenius_normalize_bwd(const float* dy, const float* y, const float* norm,
+                                              int64_t n, float* dx, void* workspace,
+                                              size_t ws_bytes, void* stream) {
+  return frobenius_bwd(dy, y, norm, n, nullptr, 1, dx, workspace, ws_bytes, stream);
+}
+
+extern "C" int32_t rs_frobenius_normalize_rows_fwd(const float* x, int64_t n_cap_rows,
+                                                   int32_t row_len, const int32_t* n_rows,
+                                                   float* y, float* norm, void* workspace,
+                                                   size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(row_len >= 1 && n_rows != nullptr, "rs_frobenius_normalize_rows_fwd: bad args");
+  return frobenius_fwd(x, n_cap_rows * row_len, n_rows, row_len, y, norm, workspace, ws_bytes,
+                       stream);
+}
+
+extern "C" int32_t rs_frobenius_normalize_rows_bwd(const float* dy, const float* y,
+                                                   const float* norm, int64_t n_cap_rows,
+                                                   int32_t row_len, const int32_t* n_rows,
+                                                   float* dx, void* workspace, size_t ws_bytes,
+                                                   void* stream) {
+  RS_CHECK_ARG(row_len >= 1 && n_rows != nullptr, "rs_frobenius_normalize_rows_bwd: bad args");
+  return frobenius_bwd(dy, y, norm, n_cap_rows * row_len, n_rows, row_len, dx, workspace,
+                       ws_bytes, stream);
 }

@@ -386,6 +386,74 @@ class KerasAdam(torch.optim.Optimizer):
             torch._foreach_sub_(ps, upd)
 
 
+class GraphKerasAdam:
+    """KerasAdam's update (same arithmetic) over a fixed list of dense tensors, with lr_t read
+    from device memory: a window of lr_t values indexed by a device step counter that the
+    update advances itself. KerasAdam passes lr_t as a host scalar, which a HIP graph would
+    freeze at its capture step; this one can sit inside a graph and be replayed step after
+    step (PinSageStep.capture). Call prepare() on the host before each step (it rolls the
+    window, outside any graph); gradients are passed to apply() explicitly."""
+
+    def __init__(self, params, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, window=4096):
+        self.params = list(params)
+        self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.iterations = 0
+        self.window = int(window)
+        dev = self.params[0].device
+        self._lr = torch.empty(self.window, dtype=torch.float32, device=dev)
+        self._idx = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._base = 0
+        self._fill()
+
+    def _fill(self):
+        vals = [keras_adam_coefficients(self._base + i + 1, self.lr, self.beta_1, self.beta_2,
+                                        self.epsilon).lr for i in range(self.window)]
+        self._lr.copy_(torch.tensor(vals, dtype=torch.float32))
+        self._idx.zero_()
+
+    def prepare(self):
+        """Host side, before a step: start a new lr_t window when this one is used up."""
+        if self.iterations - self._base >= self.window:
+            self._base = self.iterations
+            self._fill()
+
+    @torch.no_grad()
+    def apply(self, grads):
+        """One Keras Adam step of every tensor with `grads` (same order); graph-capturable."""
+        c = keras_adam_coefficients(1, self.lr, self.beta_1, self.beta_2, self.epsilon)
+        lr_t = self._lr.index_select(0, self._idx).reshape(())
+        ms, vs, ps, gs = self.m, self.v, self.params, list(grads)
+        torch._foreach_mul_(ms, c.beta1)
+        torch._foreach_add_(ms, torch._foreach_mul(gs, c.one_minus_beta1))
+        torch._foreach_mul_(vs, c.beta2)
+        torch._foreach_add_(vs, torch._foreach_mul(torch._foreach_mul(gs, gs), c.one_minus_beta2))
+        den = torch._foreach_add(torch._foreach_sqrt(vs), c.epsilon)
+        upd = torch._foreach_div(torch._foreach_mul(ms, lr_t), den)
+        torch._foreach_sub_(ps, upd)
+        self._idx.add_(1)
+
+
+def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
+                 ws: _Workspace | None = None) -> torch.Tensor:
+    """The IndexedSlices gradient as a dense [input_dim, dim] tensor with no host sync:
+    deterministic segmented sum (rs_embedding_dedup_grad, position order per row), rows past
+    the device count of distinct rows aimed at a discarded sentinel row."""
+    ws = ws or _Workspace()
+    dev = table.weight.device
+    s = SortedIds.for_table(table, ids, ws, count_unique=False)
+    n, dim, V = s.n, table.output_dim, table.input_dim
+    uniq_rows = torch.full((n,), V, dtype=torch.int32, device=dev)
+    uniq_grad = torch.empty(n, dim, dtype=torch.float32, device=dev)
+    w = ws.get("dedup", L.lib().rs_dedup_workspace_size(n, dim), dev)
+    L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(grad_rows.contiguous()),
+           dim, V, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
+    dense = torch.zeros(V + 1, dim, dtype=torch.float32, device=dev)
+    dense.index_copy_(0, uniq_rows.to(torch.int64), uniq_grad)
+    return dense[:V]
+
+
 class DLRMScheduler:
     """ctr/util.py:7-37: lr = initial*step/warmup for step <= warmup, else cosine decay to
     alpha over decay_steps."""

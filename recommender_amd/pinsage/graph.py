@@ -80,6 +80,10 @@ class Block:
     n_edges: torch.Tensor     # [1] int32 (device)
     t_indptr: torch.Tensor    # [n_src+1] int32
     t_edge: torch.Tensor      # [cap] int32 edge ids grouped by src
+    # capacity-shaped (sync-free) blocks: live dst / src counts [1] int32 on the device; rows
+    # past them are padding (src id -1, no edges). None: every row is live.
+    n_dst_live: torch.Tensor | None = None
+    n_src_live: torch.Tensor | None = None
 
     @property
     def n_src(self) -> int:
@@ -106,6 +110,10 @@ class PairGraph:
     src: torch.Tensor
     dst: torch.Tensor
     nodes: torch.Tensor
+    # capacity-shaped pair graphs: valid [E] bool (padding pairs have src/dst -1) and the live
+    # count n_valid [1] int32 on the device. None: every edge is live.
+    valid: torch.Tensor | None = None
+    n_valid: torch.Tensor | None = None
 
     @property
     def ndata(self):

@@ -53,15 +53,21 @@ def weighted_mean_agg(u: torch.Tensor, block: Block) -> torch.Tensor:
 
 class _FrobeniusNormalize(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: torch.Tensor):
+    def forward(ctx, x: torch.Tensor, n_rows: torch.Tensor | None):
         L.require_device(x, "x")
         x = x.contiguous()
         n = x.numel()
         y = torch.empty_like(x)
         norm = torch.empty(1, device=x.device)
         ws = torch.empty(L.lib().rs_frobenius_workspace_size(n), dtype=torch.uint8, device=x.device)
-        L.call("rs_frobenius_normalize_fwd", L.ptr(x), n, L.ptr(y), L.ptr(norm), L.ptr(ws),
-               ws.numel(), L.stream_ptr(x.device))
+        if n_rows is None:
+            L.call("rs_frobenius_normalize_fwd", L.ptr(x), n, L.ptr(y), L.ptr(norm), L.ptr(ws),
+                   ws.numel(), L.stream_ptr(x.device))
+        else:
+            L.call("rs_frobenius_normalize_rows_fwd", L.ptr(x), x.shape[0], x.shape[1],
+                   L.ptr(n_rows), L.ptr(y), L.ptr(norm), L.ptr(ws), ws.numel(),
+                   L.stream_ptr(x.device))
+        ctx.n_rows = n_rows
         ctx.save_for_backward(y, norm)
         return y
 
@@ -72,13 +78,20 @@ class _FrobeniusNormalize(torch.autograd.Function):
         n = g.numel()
         dx = torch.empty_like(g)
         ws = torch.empty(L.lib().rs_frobenius_workspace_size(n), dtype=torch.uint8, device=g.device)
-        L.call("rs_frobenius_normalize_bwd", L.ptr(g), L.ptr(y), L.ptr(norm), n, L.ptr(dx),
-               L.ptr(ws), ws.numel(), L.stream_ptr(g.device))
-        return dx
+        if ctx.n_rows is None:
+            L.call("rs_frobenius_normalize_bwd", L.ptr(g), L.ptr(y), L.ptr(norm), n, L.ptr(dx),
+                   L.ptr(ws), ws.numel(), L.stream_ptr(g.device))
+        else:
+            L.call("rs_frobenius_normalize_rows_bwd", L.ptr(g), L.ptr(y), L.ptr(norm), g.shape[0],
+                   g.shape[1], L.ptr(ctx.n_rows), L.ptr(dx), L.ptr(ws), ws.numel(),
+                   L.stream_ptr(g.device))
+        return dx, None
 
 
-def frobenius_normalize(x: torch.Tensor) -> torch.Tensor:
-    return _FrobeniusNormalize.apply(x)
+def frobenius_normalize(x: torch.Tensor, n_rows: torch.Tensor | None = None) -> torch.Tensor:
+    """y = x / ||x||_F. n_rows ([1] int32 device): only the first n_rows rows of the 2-D x are
+    live (capacity-shaped batch); the rest come out 0 and take no part in the norm."""
+    return _FrobeniusNormalize.apply(x, n_rows)
 
 
 class Convolve(nn.Module):
@@ -96,7 +109,7 @@ class Convolve(nn.Module):
         u = self.fc_1(h_src)                              # neighbour transformation
         nv = weighted_mean_agg(u, block)                  # importance pooling
         new = self.fc_2(torch.cat([nv, h_dst], dim=-1))   # concat transformation
-        return frobenius_normalize(new)                   # l2 normalisation (global)
+        return frobenius_normalize(new, block.n_dst_live)  # l2 normalisation (global)
 
 
 class SageNet(nn.Module):
@@ -143,8 +156,10 @@ class FeatureProjector(nn.Module):
     def tables(self):
         return [self.year_embedding, self.genre_embedding, self.id_embedding]
 
-    def forward(self, induces_ids: torch.Tensor) -> torch.Tensor:
+    def forward(self, induces_ids: torch.Tensor, padded: bool = False) -> torch.Tensor:
         ids = induces_ids.to(torch.int64)
+        if padded:  # capacity-shaped block: padding src nodes (-1) read item 0, grad 0
+            ids = ids.clamp_min(0)
         year_embedding = self.year_embedding(self.year.index_select(0, ids))
         genre_embedding = self.genre_embedding(self.genre.index_select(0, ids)).mean(dim=1)
         id_embedding = self.id_embedding(self.item_id.index_select(0, ids))

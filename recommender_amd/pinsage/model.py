@@ -10,13 +10,21 @@ from .layers import FeatureProjector, SageNet
 
 def item2item_scorer(graph: PairGraph, h: torch.Tensor) -> torch.Tensor:
     """apply_edges(u_dot_v) (model.py:14-19): score [E, 1] = h[src] · h[dst]."""
-    s = h.index_select(0, graph.src.to(torch.int64))
-    d = h.index_select(0, graph.dst.to(torch.int64))
+    src, dst = graph.src.to(torch.int64), graph.dst.to(torch.int64)
+    if graph.valid is not None:  # capacity-shaped: padding pairs (-1) score node 0, masked later
+        src, dst = src.clamp_min(0), dst.clamp_min(0)
+    s = h.index_select(0, src)
+    d = h.index_select(0, dst)
     return (s * d).sum(dim=-1, keepdim=True)
 
 
-def margin_loss(pos_score, neg_score, delta: float = 1.0):
-    return torch.clamp(neg_score + delta - pos_score, min=0).mean()
+def margin_loss(pos_score, neg_score, delta: float = 1.0, valid=None, n_valid=None):
+    """mean(max(neg - pos + delta, 0)) (train.py:17-20). valid / n_valid (capacity-shaped
+    batch): the mean over the live pairs, with no host sync."""
+    hinge = torch.clamp(neg_score + delta - pos_score, min=0)
+    if valid is None:
+        return hinge.mean()
+    return (hinge.reshape(-1) * valid).sum() / n_valid.to(hinge.dtype).reshape(())
 
 
 class PinSageModel(nn.Module):
@@ -41,7 +49,8 @@ class PinSageModel(nn.Module):
     call = forward
 
     def get_repr(self, blocks):
-        hidden_src = self.feature_projector(blocks[0].srcdata[NID])
+        hidden_src = self.feature_projector(blocks[0].srcdata[NID],
+                                            padded=blocks[0].n_src_live is not None)
         return self.sagenet(blocks, hidden_src)
 
     def tables(self):

@@ -8,6 +8,12 @@ Every draw is keyed by (seed, step, subject) — pair index for the pair sampler
 layer) for the neighbour walks — so a batch sharded over ranks samples exactly what one rank
 would. Host syncs per step: the valid-pair count, the seed count and each
 layer's src count (tensor shapes).
+
+Sync-free form (`sample_pairs_static` + `sample_static`, used by PinSageStep.capture): every
+tensor is capacity-shaped and lives in the sampler's persistent buffers (same addresses every
+call, so a HIP graph captured over one batch reads the next), the live counts stay on the
+device, and padding is -1 ids / empty CSR rows. Capacities: pairs B, seeds S0 = min(3B, items),
+layer sources min(cap_dst·(1+k), items). The live part equals the dynamic form bit for bit.
 """
 from __future__ import annotations
 
@@ -166,3 +172,119 @@ class PinSageSampler:
         neg_graph = PairGraph(local[:n], local[2 * n:], seeds)
         blocks = self.generate_blocks(seeds, heads, pos_tails, neg_tails)
         return pos_graph, neg_graph, blocks
+
+    # -- capacity-shaped, sync-free batches ----------------------------------------------------
+    def _buf(self, name, shape, dtype):
+        """Persistent device buffer (allocated once per name / shape / dtype)."""
+        if not hasattr(self, "_static"):
+            self._static = {}
+        key = (name, tuple(shape), dtype)
+        t = self._static.get(key)
+        if t is None:
+            t = torch.empty(shape, dtype=dtype, device=self.g.device)
+            self._static[key] = t
+        return t
+
+    def _unique_static(self, name, ids, cap):
+        """rs_unique_first into persistent buffers: (uniq [cap] padded with -1 past the device
+        count, local [n] (-1 for ids < 0), count [1] device)."""
+        n = ids.numel()
+        uniq = self._buf(name + ".uniq", (n,), torch.int32)
+        uniq.fill_(-1)
+        local = self._buf(name + ".local", (n,), torch.int32)
+        count = self._buf(name + ".n", (1,), torch.int32)
+        count.zero_()
+        ws = self.scratch.get("uniq." + name, L.lib().rs_unique_first_workspace_size(
+            self.g.n_items, n), ids.device)
+        L.call("rs_unique_first", L.ptr(ids), n, self.g.n_items, L.ptr(uniq), L.ptr(local),
+               L.ptr(count), L.ptr(self.err_flag), L.ptr(ws), ws.numel(), L.stream_ptr(ids.device))
+        return uniq[:cap], local, count
+
+    def sample_pairs_static(self, batch: int, seed: int, step: int, pair_base: int = 0):
+        """item_pairs without the host read of the valid count: (heads, pos, neg) [batch] with
+        -1 past the device count n_valid [1] (data_loader.py:6-18, dropped pairs at the end)."""
+        dev = self.g.device
+        heads, pos, neg = (self._buf(n, (batch,), torch.int32) for n in ("heads", "pos", "neg"))
+        n_valid = self._buf("n_valid", (1,), torch.int32)
+        n_valid.zero_()
+        ws = self.scratch.get("pairs", L.lib().rs_item_pairs_workspace_size(batch), dev)
+        L.call("rs_item_pairs", *(L.ptr(t) for t in self.g.csr_args()), self.g.n_items, pair_base,
+               batch, seed, step & 0xFFFFFFFF, L.ptr(heads), L.ptr(pos), L.ptr(neg),
+               L.ptr(n_valid), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        pad = self._buf("pair_pad", (batch,), torch.bool)
+        torch.ge(self._arange(batch), n_valid, out=pad)
+        for t in (heads, pos, neg):
+            t.masked_fill_(pad, -1)
+        return heads, pos, neg, n_valid
+
+    def _arange(self, n):
+        key = ("arange", (n,), torch.int32)
+        if not hasattr(self, "_static") or key not in self._static:
+            self._buf("arange", (n,), torch.int32).copy_(
+                torch.arange(n, dtype=torch.int32, device=self.g.device))
+        return self._static[key]
+
+    def sample_static(self, heads, pos_tails, neg_tails, n_valid):
+        """sample_from_item_pairs on a sample_pairs_static batch, with no host sync: pair
+        graphs carry `valid` / `n_valid`, blocks carry `n_dst_live`, padded src nodes are -1.
+        The returned tensors are the sampler's buffers, overwritten by its next call."""
+        B = heads.numel()
+        n_items, k = self.g.n_items, self.num_neighbors
+        ids = self._buf("pair_ids", (3 * B,), torch.int32)
+        torch.cat([heads, pos_tails, neg_tails], out=ids)
+        cap = min(3 * B, n_items)
+        seeds, local, n_seeds = self._unique_static("seeds", ids, cap)
+        valid = self._buf("pair_valid", (B,), torch.bool)
+        torch.ge(heads, 0, out=valid)
+        pos_graph = PairGraph(local[:B], local[B:2 * B], seeds, valid, n_valid)
+        neg_graph = PairGraph(local[:B], local[2 * B:], seeds, valid, n_valid)
+        # leak-edge exclusion set (padding pairs are skipped by the build kernel)
+        esrc = self._buf("excl_src", (2 * B,), torch.int32)
+        edst = self._buf("excl_dst", (2 * B,), torch.int32)
+        torch.cat([heads, heads], out=esrc)
+        torch.cat([pos_tails, neg_tails], out=edst)
+        ecap = _pow2_above(4 * B + 1)
+        table = self._buf("excl_table", (ecap,), torch.int64)
+        table.fill_(-1)
+        L.call("rs_pair_set_build", L.ptr(esrc), L.ptr(edst), 2 * B, L.ptr(table), ecap,
+               L.stream_ptr(self.g.device))
+        blocks = []
+        dst, n_dst = seeds, n_seeds
+        for layer in range(self.num_layers):
+            blocks.insert(0, self._block_static(layer, dst, n_dst, (table, ecap)))
+            dst, n_dst = blocks[0].src_nodes, blocks[0].n_src_live
+        self.step += 1
+        return pos_graph, neg_graph, blocks
+
+    def _block_static(self, layer, dst, n_dst, excl):
+        dev = self.g.device
+        cap_dst, k = dst.numel(), self.num_neighbors
+        pre = f"l{layer}."
+        nbr = self._buf(pre + "nbr", (cap_dst, k), torch.int32)
+        cnt = self._buf(pre + "cnt", (cap_dst, k), torch.int32)
+        table, ecap = excl
+        L.call("rs_pinsage_neighbors", *(L.ptr(t) for t in self.g.csr_args()), L.ptr(dst),
+               cap_dst, self.num_random_walks, self.num_traversals, self.termination_prob,
+               self.seed, self.step & 0xFFFFFFFF, layer, k, L.ptr(table), ecap, L.ptr(nbr),
+               L.ptr(cnt), L.stream_ptr(dev))
+        ids = self._buf(pre + "ids", (cap_dst * (1 + k),), torch.int32)
+        torch.cat([dst, nbr.reshape(-1)], out=ids)
+        cap_src = min(cap_dst * (1 + k), self.g.n_items)
+        src, local, n_src = self._unique_static(pre + "src", ids, cap_src)
+        nbr_local = local[cap_dst:]
+        E = cap_dst * k
+        indptr = self._buf(pre + "indptr", (cap_dst + 1,), torch.int32)
+        edge_src = self._buf(pre + "edge_src", (E,), torch.int32)
+        edge_dst = self._buf(pre + "edge_dst", (E,), torch.int32)
+        edge_w = self._buf(pre + "edge_w", (E,), torch.float32)
+        n_edges = self._buf(pre + "n_edges", (1,), torch.int32)
+        n_edges.zero_()
+        t_indptr = self._buf(pre + "t_indptr", (cap_src + 1,), torch.int32)
+        t_edge = self._buf(pre + "t_edge", (E,), torch.int32)
+        ws = self.scratch.get("block." + pre, L.lib().rs_pinsage_block_workspace_size(cap_dst, k),
+                              dev)
+        L.call("rs_pinsage_block", L.ptr(nbr_local), L.ptr(cnt), cap_dst, k, cap_src,
+               L.ptr(indptr), L.ptr(edge_src), L.ptr(edge_dst), L.ptr(edge_w), L.ptr(n_edges),
+               L.ptr(t_indptr), L.ptr(t_edge), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        return Block(src, cap_dst, indptr, edge_src, edge_dst, edge_w, n_edges, t_indptr, t_edge,
+                     n_dst_live=n_dst, n_src_live=n_src)

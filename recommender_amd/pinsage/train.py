@@ -21,7 +21,7 @@ import time
 import numpy as np
 import torch
 
-from ..optim import KerasAdam, SparseAdam, dedup_grad
+from ..optim import GraphKerasAdam, KerasAdam, SparseAdam, _Workspace, dedup_grad, densify_grad
 from ..synthetic import ML20M, movielens_graph
 from .evaluation import (build_val_test_matrix, get_item_reprs, hit_rate_eval, recommend,
                          train_test_split_by_time)
@@ -74,6 +74,58 @@ class PinSageStep:
             self.opt_dense.step()
             self.opt_sparse.step()
         return loss.detach()
+
+    # -- sync-free step on capacity-shaped batches (PinSageSampler.sample_static) ------------
+    def static_step(self, pos_graph, neg_graph, blocks):
+        """One training step with no host sync, so it can be captured into a HIP graph: masked
+        margin loss over the live pairs, and Keras Adam (GraphKerasAdam: lr_t from device
+        memory) on the dense parameters and on the three tables' densified IndexedSlices
+        gradients — Keras' sparse Adam decays m / v and moves every row anyway
+        (_resource_apply_sparse [3p TF 2.2]), so the dense form is the same update. Equal to
+        __call__ on the unpadded batch up to fp32 rounding order (tests/test_pinsage_gpu.py).
+        Its Adam state (GraphKerasAdam) is its own: do not interleave with __call__."""
+        if self.world > 1:
+            raise ValueError("static_step is single-replica (the sharded step all-reduces)")
+        tables = self.model.tables()
+        if getattr(self, "opt_graph", None) is None:
+            self.opt_graph = GraphKerasAdam(self.dense + [t.weight for t in tables],
+                                            lr=self.opt_dense.param_groups[0]["lr"])
+            self._ws = _Workspace()
+        for p in self.dense:
+            p.grad = None
+        pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
+        loss = margin_loss(pos_score, neg_score, 1.0, pos_graph.valid, pos_graph.n_valid)
+        loss.backward()
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.dense]
+        for t in tables:
+            got = t.take_grad()
+            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
+                         else torch.zeros_like(t.weight))
+        if not torch.cuda.is_current_stream_capturing():
+            self.opt_graph.prepare()
+            self.opt_graph.iterations += 1  # a capture records the step; replay() counts it
+        self.opt_graph.apply(grads)
+        return loss.detach()
+
+    def capture(self, batch):
+        """Record one static_step on `batch` (a PinSageSampler.sample_static batch: the
+        sampler's persistent buffers) into a HIP graph. Returns replay(): one training step on
+        whatever the sampler last wrote into those buffers, and the step's loss tensor. Run at
+        least one eager static_step first (library handles, workspaces)."""
+        opt = self.opt_graph
+        opt.prepare()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self.static_step(*batch)
+        self._graph = g
+
+        def replay():
+            opt.prepare()
+            g.replay()
+            opt.iterations += 1
+            return loss
+        return replay
 
     def _allreduce_and_apply_tables(self):
         """Densify each table's IndexedSlices grad (deterministic segmented sum), bucket it

@@ -446,3 +446,146 @@ def test_world2_pinsage_step_equals_two_sub_batches():
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+# ---- sync-free capacity-shaped step (PinSageSampler.sample_static, PinSageStep.capture) -----
+def _live(t, n):
+    return t[: int(n.item()) if torch.is_tensor(n) else n].cpu().numpy()
+
+
+@pytest.mark.parametrize("batch", [48, 128])
+def test_sample_static_equals_dynamic(batch):
+    """The capacity-shaped batch's live part is the dynamic batch bit for bit (pairs with a
+    dead-end walk dropped, seeds, both blocks' src nodes / CSR / transpose); padding is -1
+    ids, empty CSR rows and k empty neighbour slots per padding seed."""
+    g, _ = small_graph(3, n_users=120, n_items=200, n_edges=1500, dead_items=20)
+    dyn = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    sta = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    for step in range(2):
+        h, p, n = item_pairs(g, batch, 4, step)
+        sh, sp, sn, nv = sta.sample_pairs_static(batch, 4, step)
+        nvalid = int(nv.item())
+        assert nvalid == h.numel() and nvalid < batch  # dead items drop some pairs
+        for a, b in ((sh, h), (sp, p), (sn, n)):
+            np.testing.assert_array_equal(_live(a, nvalid), b.cpu().numpy())
+            assert (a[nvalid:] == -1).all()
+        pg, ng, blocks = dyn.sample_from_item_pairs(h, p, n)
+        spg, sng, sblocks = sta.sample_static(sh, sp, sn, nv)
+        S = pg.nodes.numel()
+        np.testing.assert_array_equal(_live(spg.nodes, S), pg.nodes.cpu().numpy())
+        assert (spg.nodes[S:] == -1).all()
+        np.testing.assert_array_equal(_live(spg.src, nvalid), pg.src.cpu().numpy())
+        np.testing.assert_array_equal(_live(spg.dst, nvalid), pg.dst.cpu().numpy())
+        np.testing.assert_array_equal(_live(sng.dst, nvalid), ng.dst.cpu().numpy())
+        assert int(spg.valid.sum()) == nvalid
+        for b, sb in zip(blocks, sblocks):
+            E = int(b.n_edges.item())
+            assert int(sb.n_edges.item()) == E
+            assert int(sb.n_dst_live.item()) == b.n_dst and int(sb.n_src_live.item()) == b.n_src
+            np.testing.assert_array_equal(_live(sb.src_nodes, b.n_src), b.src_nodes.cpu().numpy())
+            assert (sb.src_nodes[b.n_src:] == -1).all()
+            np.testing.assert_array_equal(_live(sb.indptr, b.n_dst + 1), b.indptr.cpu().numpy())
+            assert (sb.indptr[b.n_dst:] == E).all()  # padding dst rows hold no edges
+            for f in ("edge_src", "edge_dst", "edge_w", "t_edge"):
+                np.testing.assert_array_equal(_live(getattr(sb, f), E),
+                                              getattr(b, f)[:E].cpu().numpy(), err_msg=f)
+            np.testing.assert_array_equal(_live(sb.t_indptr, b.n_src + 1),
+                                          b.t_indptr.cpu().numpy())
+            assert (sb.t_indptr[b.n_src:] == E).all()
+
+
+def test_frobenius_rows_bit_exact_on_live_rows():
+    """rs_frobenius_normalize_rows_*: norm and y / dx over the live rows equal the unpadded
+    call bit for bit; padding rows come out 0."""
+    torch.manual_seed(5)
+    x = torch.randn(700, 16, device=DEV)
+    dy = torch.randn(700, 16, device=DEV)
+    n_live = torch.tensor([513], dtype=torch.int32, device=DEV)
+    xs = x.clone().requires_grad_(True)
+    y = frobenius_normalize(xs, n_live)
+    y.backward(dy)
+    xr = x[:513].clone().requires_grad_(True)
+    yr = frobenius_normalize(xr)
+    yr.backward(dy[:513])
+    assert torch.equal(y[:513], yr) and not y[513:].any()
+    assert torch.equal(xs.grad[:513], xr.grad) and not xs.grad[513:].any()
+
+
+def _pinsage_setup(seed_model=1):
+    g, _ = small_graph(7, n_users=200, n_items=300, n_edges=3000, dead_items=25)
+    gen = torch.Generator(device=DEV).manual_seed(seed_model)
+    model = PinSageModel(g, g.itype, 2, 8, 32, 16, generator=gen)
+    smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    return g, model, smp
+
+
+def test_static_forward_backward_equals_dynamic():
+    """PinSageModel on the capacity-shaped batch: live scores, the masked margin loss and
+    every gradient (dense and densified tables) equal the dynamic batch's up to fp32 rounding
+    order (the GEMMs see more rows); padding contributes exactly nothing."""
+    from recommender_amd.optim import densify_grad
+    from recommender_amd.pinsage.model import margin_loss
+
+    B = 128
+    g, model, dyn = _pinsage_setup()
+    sta = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    h, p, n = item_pairs(g, B, 4, 0)
+    pos, neg = model(*dyn.sample_from_item_pairs(h, p, n))
+    margin_loss(pos, neg).backward()
+    ref = {k: v.grad.clone() for k, v in model.named_parameters() if v.grad is not None}
+    ref_tab = [densify_grad(t, *t.take_grad()) for t in model.tables()]
+    model.zero_grad(set_to_none=True)
+    spg, sng, sblocks = sta.sample_static(*sta.sample_pairs_static(B, 4, 0))
+    spos, sneg = model(spg, sng, sblocks)
+    sloss = margin_loss(spos, sneg, 1.0, spg.valid, spg.n_valid)
+    sloss.backward()
+    nv = h.numel()
+    assert_close_rel(spos[:nv].detach().cpu(), pos.detach().cpu(), RTOL, msg="pos")
+    assert_close_rel(sneg[:nv].detach().cpu(), neg.detach().cpu(), RTOL, msg="neg")
+    rl = margin_loss(pos, neg).item()
+    assert abs(sloss.item() - rl) <= RTOL * abs(rl)
+    for k, v in model.named_parameters():
+        if k in ref:
+            assert_close_rel(v.grad.cpu(), ref[k].cpu(), 1e-4,
+                             scale=float(ref[k].abs().max()) * 1e-2, msg=k)
+    for t, r in zip(model.tables(), ref_tab):
+        d = densify_grad(t, *t.take_grad())
+        assert_close_rel(d.cpu(), r.cpu(), 1e-4, scale=float(r.abs().max()) * 1e-2)
+
+
+def test_static_step_graph_replay_bit_exact_and_matches_dynamic():
+    """Four training steps three ways: (a) the dynamic PinSageStep (host-synced shapes,
+    SparseAdam + KerasAdam), (b) four eager static_steps, (c) one eager static_step, then
+    the step captured once into a HIP graph and replayed three times on freshly sampled
+    batches. (c) equals (b) bit for bit (the lr_t of each replay comes from device memory);
+    (b) equals (a) to fp32 rounding order."""
+    B = 96
+    res = []
+    for mode in ("dynamic", "static", "graph"):
+        g, model, smp = _pinsage_setup()
+        step = PinSageStep(model, lr=1e-2)
+        losses = []
+        replay = None
+        for it in range(4):
+            if mode == "dynamic":
+                h, p, n = item_pairs(g, B, 4, it)
+                losses.append(float(step(*smp.sample_from_item_pairs(h, p, n))))
+                continue
+            batch = smp.sample_static(*smp.sample_pairs_static(B, 4, it))
+            if mode == "static" or it == 0:
+                losses.append(float(step.static_step(*batch)))
+                continue
+            if replay is None:
+                replay = step.capture(batch)
+            losses.append(float(replay()))
+        torch.cuda.synchronize()
+        res.append((losses, _pinsage_params(model)))
+    (l_dyn, p_dyn), (l_sta, p_sta), (l_gr, p_gr) = res
+    assert l_sta == l_gr
+    for a, b in zip(p_sta, p_gr):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(l_sta, l_dyn, rtol=1e-5)
+    for a, b in zip(p_sta, p_dyn):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+    moved = [float((a != b).mean()) for a, b in zip(p_gr, _pinsage_params(_pinsage_setup()[1]))]
+    assert min(moved) > 0.0, moved
