@@ -122,6 +122,27 @@ int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sort
                                 uint32_t* uniq_rows, float* uniq_grad, void* workspace,
                                 size_t ws_bytes, void* stream);
 
+/* Dense gradient of a small table, no sort: grad_dense [n_rows, dim] = Σ over entries n with
+ * ids[n] = v of grad_rows[n, :] (Keras' IndexedSlices gradient densified for a dense Adam step,
+ * pinsage/train/train.py:45-46 on the year / genre tables, layers.py:63-75). Fixed summation
+ * order (per-block LDS lanes, then blocks in order): deterministic, not position order.
+ * Limits: dim a power of two <= 256, n_rows * dim <= 16384. Ids outside [0, n_rows) are
+ * skipped and set RS_ERRBIT_OOB in err_flag (may be NULL). */
+size_t rs_embedding_grad_dense_small_workspace_size(int64_t n_ids, int64_t n_rows, int32_t dim);
+int32_t rs_embedding_grad_dense_small(const void* ids, int32_t id_dtype, int64_t n_ids,
+                                      const float* grad_rows, int32_t dim, int64_t n_rows,
+                                      float* grad_dense, int32_t* err_flag, void* workspace,
+                                      size_t ws_bytes, void* stream);
+
+/* Keras Adam dense update (KerasAdam / [3p TF 2.2] _resource_apply_dense, as pinsage/train/
+ * train.py:45-48 applies it to every variable) over one flat buffer of n floats (n % 4 == 0,
+ * 16-byte aligned), with lr_t read from device memory: lr_t = lr_hist[*step_idx]
+ * (params->lr ignored), so a captured HIP graph replays the right step. Same roundings as the
+ * separate torch ops: m = m*b1 + g*(1-b1); v = v*b2 + (g*g)*(1-b2); var -= (m*lr_t)/(sqrt(v)+eps). */
+int32_t rs_keras_adam_flat(float* var, float* m, float* v, const float* grad, int64_t n,
+                           const float* lr_hist, const int64_t* step_idx,
+                           const rs_adam_params* params, void* stream);
+
 /* a-2 (part 3) fused segmented-sum + optimizer apply on the touched rows
  * (Keras Adam _resource_apply_sparse / SGD _resource_apply_sparse_duplicate_indices,
  * [3p] reached from ctr/train.py:80,84,97 and the commented SGD path ctr/train.py:77-79).

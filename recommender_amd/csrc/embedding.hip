@@ -1222,3 +1222,200 @@ extern "C" int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, i
   RS_CHECK_HIP(hipMemsetAsync(touched_bitmap, 0, (size_t)ceil_div(n_rows, 32) * 4, st));
   return RS_OK;
 }
+
+// ---- small-table dense gradient (no sort) ---------------------------------------------------
+// grad_dense[v, :] = Σ_{n: ids[n] = v} grad_rows[n, :] for a table of V·dim ≤ kSmallVD floats
+// (PinSage's year / genre tables: Keras' IndexedSlices gradient densified, pinsage/train/
+// train.py:45-46). Block b sums entries [b·chunk, (b+1)·chunk): thread (e, d) of E entry lanes
+// × dim columns adds column d of entries e, e+E, … into its own LDS copy of the table, the E
+// copies are folded in lane order and the block partials in block order — a fixed summation
+// order, independent of timing. One pass over the entries, no radix sort, no hot-row fix-up
+// (the genre table's 2 live rows take every entry).
+namespace rs {
+constexpr int64_t kSmallVD = 16384;  // 64 KiB of LDS at E = 1
+
+template <typename Id>
+__global__ __launch_bounds__(256) void dense_small_partial_kernel(
+    const Id* __restrict__ ids, int64_t n, const float* __restrict__ rows, int32_t dim,
+    int32_t dshift, int32_t E, int64_t V, int64_t chunk, float* __restrict__ partial,
+    int32_t* __restrict__ err_flag) {
+  extern __shared__ float acc[];  // [E][V * dim]
+  const int32_t t = threadIdx.x, d = t & (dim - 1), e = t >> dshift;
+  const int64_t VD = V * dim;
+  for (int64_t i = t; i < (int64_t)E * VD; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  float* mine = acc + (int64_t)e * VD;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  // 4 entries' ids and gradient values loaded before their 4 read-modify-writes (same order)
+  int64_t k = lo + e;
+  for (; k + 3 * E < hi; k += 4 * E) {
+    int64_t r[4];
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = (int64_t)ids[k + u * E];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = rows[(k + u * E) * dim + d];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (r[u] < 0 || r[u] >= V) {
+        if (d == 0) flag_oob(err_flag);
+        continue;
+      }
+      mine[r[u] * dim + d] += x[u];
+    }
+  }
+  for (; k < hi; k += E) {
+    const int64_t r = (int64_t)ids[k];
+    if (r < 0 || r >= V) {
+      if (d == 0) flag_oob(err_flag);
+      continue;
+    }
+    mine[r * dim + d] += rows[k * dim + d];
+  }
+  __syncthreads();
+  for (int64_t i = t; i < VD; i += blockDim.x) {
+    float s = 0.f;
+    for (int32_t q = 0; q < E; ++q) s += acc[(int64_t)q * VD + i];
+    partial[(int64_t)blockIdx.x * VD + i] = s;
+  }
+}
+
+// 64 outputs per block x 4 lanes: lane q sums blocks q, q+4, … (8 loads in flight), then the
+// 4 lane sums are added in lane order.
+__global__ __launch_bounds__(256) void dense_small_fold_kernel(const float* __restrict__ partial,
+                                                               int32_t nb, int64_t VD,
+                                                               float* __restrict__ out) {
+  __shared__ float lane_sum[4][64];
+  const int32_t c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (i < VD) {
+    int32_t b = q;
+    for (; b + 28 < nb; b += 32) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = partial[(int64_t)(b + 4 * u) * VD + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += x[u];
+    }
+    for (; b < nb; b += 4) s += partial[(int64_t)b * VD + i];
+  }
+  lane_sum[q][c] = s;
+  __syncthreads();
+  if (q == 0 && i < VD) out[i] = ((lane_sum[0][c] + lane_sum[1][c]) + lane_sum[2][c]) + lane_sum[3][c];
+}
+
+struct SmallGeom {
+  int32_t E, nb;
+  int64_t chunk;
+};
+
+inline SmallGeom small_geom(int64_t n_ids, int64_t n_rows, int32_t dim) {
+  const int64_t VD = n_rows * dim;
+  int32_t E = 256 / dim;
+  while (E > 1 && (int64_t)E * VD > kSmallVD) E >>= 1;
+  SmallGeom g;
+  g.E = E;
+  g.nb = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n_ids, 512)));
+  g.chunk = ceil_div(n_ids < 1 ? 1 : n_ids, g.nb);
+  return g;
+}
+}  // namespace rs
+
+extern "C" size_t rs_embedding_grad_dense_small_workspace_size(int64_t n_ids, int64_t n_rows,
+                                                                int32_t dim) {
+  using namespace rs;
+  if (dim <= 0 || n_rows <= 0) return 256;
+  return align_up((size_t)small_geom(n_ids, n_rows, dim).nb * n_rows * dim * 4, 256);
+}
+
+extern "C" int32_t rs_embedding_grad_dense_small(const void* ids, int32_t id_dtype, int64_t n_ids,
+                                                 const float* grad_rows, int32_t dim,
+                                                 int64_t n_rows, float* grad_dense,
+                                                 int32_t* err_flag, void* workspace,
+                                                 size_t ws_bytes, void* stream) {
+  using namespace rs;
+  RS_CHECK_ARG(dim > 0 && dim <= 256 && (dim & (dim - 1)) == 0,
+               "rs_embedding_grad_dense_small: dim must be a power of two <= 256");
+  RS_CHECK_ARG(n_rows > 0 && n_rows * dim <= kSmallVD,
+               "rs_embedding_grad_dense_small: n_rows * dim must be <= 16384");
+  RS_CHECK_ARG(n_ids >= 0 && id_dtype >= RS_ID_I32 && id_dtype <= RS_ID_I64, "bad ids");
+  RS_CHECK_ARG(grad_dense && (n_ids == 0 || (ids && grad_rows)), "null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_embedding_grad_dense_small_workspace_size(n_ids, n_rows, dim),
+               "rs_embedding_grad_dense_small: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t VD = n_rows * dim;
+  if (n_ids == 0) {
+    RS_CHECK_HIP(hipMemsetAsync(grad_dense, 0, (size_t)VD * 4, st));
+    return RS_OK;
+  }
+  const SmallGeom g = small_geom(n_ids, n_rows, dim);
+  int32_t dshift = 0;
+  while ((1 << dshift) < dim) ++dshift;
+  float* partial = static_cast<float*>(workspace);
+  const size_t lds = (size_t)g.E * VD * 4;
+  const int threads = g.E * dim;
+  if (id_dtype == RS_ID_I32)
+    dense_small_partial_kernel<int32_t><<<g.nb, threads, lds, st>>>(
+        static_cast<const int32_t*>(ids), n_ids, grad_rows, dim, dshift, g.E, n_rows, g.chunk,
+        partial, err_flag);
+  else
+    dense_small_partial_kernel<int64_t><<<g.nb, threads, lds, st>>>(
+        static_cast<const int64_t*>(ids), n_ids, grad_rows, dim, dshift, g.E, n_rows, g.chunk,
+        partial, err_flag);
+  RS_CHECK_LAUNCH();
+  dense_small_fold_kernel<<<(unsigned)ceil_div(VD, 64), 256, 0, st>>>(partial, g.nb, VD,
+                                                                      grad_dense);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+// ---- Keras Adam over one flat buffer, lr_t from device memory ---------------------------------
+// The dense update of KerasAdam (m = m·b1 + g·(1-b1); v = v·b2 + g²·(1-b2);
+// var -= m·lr_t / (√v + eps), each product / sum rounded as the separate torch ops round) for
+// every parameter of a model at once (parameters as views of one buffer), with lr_t =
+// lr_hist[*step_idx]: a HIP graph holding this launch replays the right step each time.
+namespace rs {
+__global__ __launch_bounds__(256) void keras_adam_flat_kernel(
+    float4* __restrict__ var, float4* __restrict__ m, float4* __restrict__ v,
+    const float4* __restrict__ g, int64_t n4, const float* __restrict__ lr_hist,
+    const int64_t* __restrict__ step_idx, rs_adam_params p) {
+  const float lr = lr_hist[*step_idx];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 gi = g[i];
+    float4 mi = m[i], vi = v[i], wi = var[i];
+    float* mf = reinterpret_cast<float*>(&mi);
+    float* vf = reinterpret_cast<float*>(&vi);
+    float* wf = reinterpret_cast<float*>(&wi);
+    const float* gf = reinterpret_cast<const float*>(&gi);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mf[c] = mf[c] * p.beta1 + gf[c] * p.one_minus_beta1;
+      vf[c] = vf[c] * p.beta2 + (gf[c] * gf[c]) * p.one_minus_beta2;
+      wf[c] = wf[c] - (mf[c] * lr) / (sqrtf(vf[c]) + p.epsilon);
+    }
+    m[i] = mi;
+    v[i] = vi;
+    var[i] = wi;
+  }
+}
+}  // namespace rs
+
+extern "C" int32_t rs_keras_adam_flat(float* var, float* m, float* v, const float* grad, int64_t n,
+                                      const float* lr_hist, const int64_t* step_idx,
+                                      const rs_adam_params* params, void* stream) {
+  using namespace rs;
+  RS_CHECK_ARG(var && m && v && grad && lr_hist && step_idx && params, "null pointer");
+  RS_CHECK_ARG(n > 0 && n % 4 == 0, "rs_keras_adam_flat: n must be a positive multiple of 4");
+  RS_CHECK_ARG(((uintptr_t)var | (uintptr_t)m | (uintptr_t)v | (uintptr_t)grad) % 16 == 0,
+               "rs_keras_adam_flat: buffers must be 16-byte aligned");
+  const int64_t n4 = n / 4;
+  const int64_t blocks = std::min<int64_t>(ceil_div(n4, 256), 2048);
+  keras_adam_flat_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<float4*>(var), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
+      reinterpret_cast<const float4*>(grad), n4, lr_hist, step_idx, *params);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}

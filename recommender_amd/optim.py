@@ -387,21 +387,35 @@ class KerasAdam(torch.optim.Optimizer):
 
 
 class GraphKerasAdam:
-    """KerasAdam's update (same arithmetic) over a fixed list of dense tensors, with lr_t read
+    """KerasAdam's update (same roundings) over a fixed list of dense tensors, with lr_t read
     from device memory: a window of lr_t values indexed by a device step counter that the
     update advances itself. KerasAdam passes lr_t as a host scalar, which a HIP graph would
     freeze at its capture step; this one can sit inside a graph and be replayed step after
-    step (PinSageStep.capture). Call prepare() on the host before each step (it rolls the
-    window, outside any graph); gradients are passed to apply() explicitly."""
+    step (PinSageStep.capture). The tensors are re-pointed to views of one flat buffer (the
+    Parameter objects stay), so a step is one gradient concat + one rs_keras_adam_flat launch.
+    Call prepare() on the host before each step (it rolls the window, outside any graph);
+    gradients are passed to apply() explicitly."""
 
     def __init__(self, params, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7, window=4096):
         self.params = list(params)
         self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
-        self.m = [torch.zeros_like(p) for p in self.params]
-        self.v = [torch.zeros_like(p) for p in self.params]
+        dev = self.params[0].device
+        sizes = [p.numel() for p in self.params]
+        pads = [(-n) % 4 for n in sizes]  # each view 16-byte aligned
+        self._segs = []
+        off = 0
+        for n, pad in zip(sizes, pads):
+            self._segs.append((off, n, pad))
+            off += n + pad
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, (o, n, _) in zip(self.params, self._segs):
+                self.flat[o:o + n].copy_(p.reshape(-1))
+                p.data = self.flat[o:o + n].view_as(p)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
         self.iterations = 0
         self.window = int(window)
-        dev = self.params[0].device
         self._lr = torch.empty(self.window, dtype=torch.float32, device=dev)
         self._idx = torch.zeros(1, dtype=torch.int64, device=dev)
         self._base = 0
@@ -422,28 +436,42 @@ class GraphKerasAdam:
     @torch.no_grad()
     def apply(self, grads):
         """One Keras Adam step of every tensor with `grads` (same order); graph-capturable."""
+        parts = []
+        for g, (_, n, pad) in zip(grads, self._segs):
+            parts.append(g.reshape(-1))
+            if pad:
+                parts.append(g.new_zeros(pad))
+        gflat = torch.cat(parts)
         c = keras_adam_coefficients(1, self.lr, self.beta_1, self.beta_2, self.epsilon)
-        lr_t = self._lr.index_select(0, self._idx).reshape(())
-        ms, vs, ps, gs = self.m, self.v, self.params, list(grads)
-        torch._foreach_mul_(ms, c.beta1)
-        torch._foreach_add_(ms, torch._foreach_mul(gs, c.one_minus_beta1))
-        torch._foreach_mul_(vs, c.beta2)
-        torch._foreach_add_(vs, torch._foreach_mul(torch._foreach_mul(gs, gs), c.one_minus_beta2))
-        den = torch._foreach_add(torch._foreach_sqrt(vs), c.epsilon)
-        upd = torch._foreach_div(torch._foreach_mul(ms, lr_t), den)
-        torch._foreach_sub_(ps, upd)
+        dev = self.flat.device
+        L.call("rs_keras_adam_flat", L.ptr(self.flat), L.ptr(self.m), L.ptr(self.v),
+               L.ptr(gflat), self.flat.numel(), L.ptr(self._lr), L.ptr(self._idx), c,
+               L.stream_ptr(dev))
         self._idx.add_(1)
 
 
 def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
                  ws: _Workspace | None = None) -> torch.Tensor:
-    """The IndexedSlices gradient as a dense [input_dim, dim] tensor with no host sync:
-    deterministic segmented sum (rs_embedding_dedup_grad, position order per row), rows past
-    the device count of distinct rows aimed at a discarded sentinel row."""
+    """The IndexedSlices gradient as a dense [input_dim, dim] tensor with no host sync. Small
+    tables (input_dim·dim <= 16384): rs_embedding_grad_dense_small (one pass, fixed block /
+    lane order); others: deterministic segmented sum (rs_embedding_dedup_grad, position order
+    per row), rows past the device count of distinct rows aimed at a discarded sentinel row."""
     ws = ws or _Workspace()
     dev = table.weight.device
+    dim, V = table.output_dim, table.input_dim
+    if V * dim <= 16384 and dim <= 256 and dim & (dim - 1) == 0:
+        # small table (PinSage year / genre): one pass, per-block LDS copies, no sort
+        ids = ids.reshape(-1).contiguous()
+        n = ids.numel()
+        dense = torch.empty(V, dim, dtype=torch.float32, device=dev)
+        w = ws.get("dense_small", L.lib().rs_embedding_grad_dense_small_workspace_size(n, V, dim),
+                   dev)
+        L.call("rs_embedding_grad_dense_small", L.ptr(ids), L.id_dtype_code(ids), n,
+               L.ptr(grad_rows.contiguous()), dim, V, L.ptr(dense), L.ptr(table.err_flag),
+               L.ptr(w), w.numel(), L.stream_ptr(dev))
+        return dense
     s = SortedIds.for_table(table, ids, ws, count_unique=False)
-    n, dim, V = s.n, table.output_dim, table.input_dim
+    n = s.n
     uniq_rows = torch.full((n,), V, dtype=torch.int32, device=dev)
     uniq_grad = torch.empty(n, dim, dtype=torch.float32, device=dev)
     w = ws.get("dedup", L.lib().rs_dedup_workspace_size(n, dim), dev)

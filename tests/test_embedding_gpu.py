@@ -299,3 +299,38 @@ def test_one_call_sparse_entry_points_match_two_call(kind, rng):
     assert torch.equal(tabs[0], tabs[1])
     if m is not None:
         assert torch.equal(ms[0], ms[1]) and torch.equal(vs[0], vs[1])
+
+
+@pytest.mark.parametrize("V,dim,n", [(2, 8, 540_000), (100, 8, 30_000), (2048, 8, 5000),
+                                     (64, 256, 3000), (20, 16, 1), (7, 4, 0)])
+@pytest.mark.parametrize("id_dtype", [np.int32, np.int64])
+def test_grad_dense_small_vs_float64(V, dim, n, id_dtype, rng):
+    """rs_embedding_grad_dense_small (PinSage year / genre tables densified for a sync-free
+    Keras Adam step): equals the float64 segmented sum within fp32 summation error (its order
+    is fixed — per-block LDS lanes, then blocks — not position order), deterministic across
+    calls, OOB ids skipped and flagged."""
+    from recommender_amd.optim import densify_grad
+
+    t = Embedding(V, dim, device=DEV)
+    ids = rng.integers(0, V, n).astype(id_dtype)
+    if V == 2:  # the genre table: two live rows take every entry
+        ids = (rng.random(n) < 0.3).astype(id_dtype)
+    rows = rng.standard_normal((n, dim)).astype(np.float32)
+    ref = np.zeros((V, dim))
+    np.add.at(ref, ids.astype(np.int64), rows.astype(np.float64))
+    gi, gr = torch.from_numpy(ids).to(DEV), torch.from_numpy(rows).to(DEV)
+    got = densify_grad(t, gi, gr)
+    again = densify_grad(t, gi, gr)
+    assert torch.equal(got, again)
+    cnt = np.maximum(np.bincount(ids.astype(np.int64), minlength=V), 1)[:, None]
+    bound = 1e-5 * (np.abs(ref) + np.sqrt(cnt) * 4.0)  # fp32 sum error ~ sqrt(count)·|row|·eps
+    assert (np.abs(got.cpu().numpy() - ref) <= bound).all()
+    assert not t.oob_detected()
+    if n:
+        bad = gi.clone()
+        bad[n // 2] = V  # out of range: skipped, flagged
+        d = densify_grad(t, bad, gr)
+        assert t.oob_detected()
+        ref2 = ref.copy()
+        ref2[ids[n // 2]] -= rows[n // 2]
+        assert (np.abs(d.cpu().numpy() - ref2) <= bound + 1e-5 * np.abs(rows[n // 2]).max()).all()
