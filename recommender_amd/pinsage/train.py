@@ -163,6 +163,9 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--eval_every", type=int, default=1000)
     ap.add_argument("--top_k", type=int, default=10)
+    ap.add_argument("--hip_graph", type=int, default=1,
+                    help="1: sync-free capacity-shaped batches, the model step replayed as one HIP "
+                         "graph (PinSageStep.capture); 0: the DGL-shaped dynamic step")
     args = ap.parse_args(argv)
     num_layers = 2
     embedding_size = 8
@@ -176,10 +179,20 @@ def main(argv=None):
     sampler = PinSageSampler(g, g.itype, g.utype, num_layers, random_walk_length,
                              num_random_walks, termination_prob, num_neighbors, seed=args.seed)
     t0 = time.perf_counter()
+    replay = None
     for step in range(args.steps):
-        heads, pos, neg = item_pairs(g, args.train_batch_size, args.seed, step)
-        batch = sampler.sample_from_item_pairs(heads, pos, neg, g.itype)
-        loss = step_fn(*batch)
+        if args.hip_graph:
+            batch = sampler.sample_static(*sampler.sample_pairs_static(
+                args.train_batch_size, args.seed, step))
+            if step == 0:
+                loss = step_fn.static_step(*batch)
+            else:
+                replay = replay or step_fn.capture(batch)
+                loss = replay()
+        else:
+            heads, pos, neg = item_pairs(g, args.train_batch_size, args.seed, step)
+            batch = sampler.sample_from_item_pairs(heads, pos, neg, g.itype)
+            loss = step_fn(*batch)
         if step % 50 == 0:
             print(f"step {step} step_loss {float(loss):.4f}")
         if args.eval_every and step % args.eval_every == 0:
