@@ -51,10 +51,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--rows", type=int, default=40_000_000)
-    ap.add_argument("--pinsage-mode", default="graph", choices=["dynamic", "static", "graph"],
+    ap.add_argument("--pinsage-mode", default="graph_all",
+                    choices=["dynamic", "static", "graph", "graph_all"],
                     help="pinsage: dynamic = host-synced shapes (PinSageStep.__call__); static = "
                          "capacity-shaped sync-free batches, eager (static_step); graph = the same "
-                         "step captured once and replayed (PinSageStep.capture), sampling eager")
+                         "step captured once and replayed (PinSageStep.capture), sampling eager; "
+                         "graph_all = sampling inside the graph too (capture_with_sampling)")
     ap.add_argument("--tuned-gemms", type=int, default=-1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
                          "-1 (default): on for the fixed-shape models (dien, esmm, mmoe), off for the "
@@ -115,6 +117,10 @@ def main():
             if args.pinsage_mode == "dynamic":
                 h, p, n = item_pairs(g, B, 4, it)
                 return train(*smp.sample_from_item_pairs(h, p, n))
+            if args.pinsage_mode == "graph_all" and it > 0:
+                if ctr["replay"] is None:
+                    ctr["replay"] = train.capture_with_sampling(smp, B, 4, it)
+                return ctr["replay"]()
             batch = smp.sample_static(*smp.sample_pairs_static(B, 4, it))
             if args.pinsage_mode == "static" or it == 0:
                 return train.static_step(*batch)

@@ -396,6 +396,14 @@ int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_idx,
                       int32_t* heads, int32_t* pos_tails, int32_t* neg_tails, int32_t* n_valid,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* rs_item_pairs with the RNG step read from device memory (*step_ptr, uint32): a captured
+ * HIP graph that advances the counter on the device samples the next step's pairs on replay. */
+int32_t rs_item_pairs_at(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                         const int64_t* u2i_indptr, const int32_t* u2i_idx, int32_t n_items,
+                         int64_t pair_base, int32_t batch, uint64_t seed, const uint32_t* step_ptr,
+                         int32_t* heads, int32_t* pos_tails, int32_t* neg_tails, int32_t* n_valid,
+                         void* workspace, size_t ws_bytes, void* stream);
+
 /* Set of (dst, src) item pairs for the leak-edge removal of generate_blocks
  * (pinsage/train/data_loader.py:34-39): table [capacity] uint64, capacity a power of two > n,
  * filled with 0xFF bytes by the caller before the first build. */
@@ -418,6 +426,15 @@ int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
                              uint32_t step, uint32_t layer, int32_t num_neighbors,
                              const uint64_t* excl_table, int64_t excl_capacity, int32_t* nbr,
                              int32_t* cnt, void* stream);
+
+/* rs_pinsage_neighbors with the RNG step read from device memory (*step_ptr). */
+int32_t rs_pinsage_neighbors_at(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                const int32_t* seeds, int64_t n_seeds, int32_t num_walks,
+                                int32_t n_traversals, float restart_prob, uint64_t seed,
+                                const uint32_t* step_ptr, uint32_t layer, int32_t num_neighbors,
+                                const uint64_t* excl_table, int64_t excl_capacity, int32_t* nbr,
+                                int32_t* cnt, void* stream);
 
 /* First-appearance unique (dgl.compact_graphs / dgl.to_block node order,
  * pinsage/train/data_loader.py:40,48): uniq = distinct ids >= 0 in order of first position,

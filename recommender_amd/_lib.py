@@ -103,6 +103,10 @@ _SIGS = {
     "rs_item_pairs_workspace_size": (_sz, [_i32]),
     "rs_item_pairs": (_i32, [_p, _p, _p, _p, _i32, _i64, _i32, _u64, _u32, _p, _p, _p, _p, _p,
                              _sz, _p]),
+    "rs_item_pairs_at": (_i32, [_p, _p, _p, _p, _i32, _i64, _i32, _u64, _p, _p, _p, _p, _p, _p,
+                                _sz, _p]),
+    "rs_pinsage_neighbors_at": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, C.c_float, _u64, _p,
+                                       _u32, _i32, _p, _i64, _p, _p, _p]),
     "rs_pair_set_build": (_i32, [_p, _p, _i64, _p, _i64, _p]),
     "rs_pinsage_neighbors": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, C.c_float, _u64, _u32,
                                     _u32, _i32, _p, _i64, _p, _p, _p]),

@@ -110,11 +110,13 @@ __global__ __launch_bounds__(256) void walk_kernel(Graph g, const int32_t* __res
 // pair_base + i) draws head, neg ~ U[0, n_items) and pos = item after one item→user→item walk.
 __global__ __launch_bounds__(256) void pairs_gen_kernel(Graph g, int32_t n_items,
                                                         int64_t pair_base, int32_t batch,
-                                                        uint64_t seed, uint32_t step,
+                                                        uint64_t seed, uint32_t step_add,
+                                                        const uint32_t* __restrict__ step_ptr,
                                                         int32_t* __restrict__ tmp,
                                                         int32_t* __restrict__ flag) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch) return;
+  const uint32_t step = step_add + (step_ptr ? *step_ptr : 0u);
   const uint32_t gi = (uint32_t)(pair_base + i);
   const U4 r = philox4x32_10(U4{gi, 0u, step, 0u}, (uint32_t)seed,
                              (uint32_t)(seed >> 32) ^ kPurposePair);
@@ -191,9 +193,11 @@ __device__ __forceinline__ bool pair_set_has(const uint64_t* __restrict__ table,
 // exclusion set and writes nbr/cnt [n_seeds, k] (-1 / 0 in empty slots).
 __global__ __launch_bounds__(256) void neighbors_kernel(
     Graph g, const int32_t* __restrict__ seeds, int64_t n_seeds, int32_t num_walks,
-    int32_t wshift, int32_t T, uint32_t stop_thr, uint64_t seed, uint32_t step, uint32_t layer,
-    int32_t k, const uint64_t* __restrict__ excl, uint32_t excl_mask, int32_t* __restrict__ nbr,
+    int32_t wshift, int32_t T, uint32_t stop_thr, uint64_t seed, uint32_t step_add,
+    const uint32_t* __restrict__ step_ptr, uint32_t layer, int32_t k,
+    const uint64_t* __restrict__ excl, uint32_t excl_mask, int32_t* __restrict__ nbr,
     int32_t* __restrict__ cnt) {
+  const uint32_t step = step_add + (step_ptr ? *step_ptr : 0u);
   extern __shared__ int32_t lds[];
   int32_t* cand = lds;                    // [256 * T]
   int32_t* ccount = lds + 256 * T;        // [256 * T]: count at first occurrence, else 0
@@ -526,12 +530,12 @@ extern "C" size_t rs_item_pairs_workspace_size(int32_t batch) {
   return c.off + 256;
 }
 
-extern "C" int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_idx,
-                                 const int64_t* u2i_indptr, const int32_t* u2i_idx,
-                                 int32_t n_items, int64_t pair_base, int32_t batch, uint64_t seed,
-                                 uint32_t step, int32_t* heads, int32_t* pos_tails,
-                                 int32_t* neg_tails, int32_t* n_valid, void* workspace,
-                                 size_t ws_bytes, void* stream) {
+static int32_t item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                          const int64_t* u2i_indptr, const int32_t* u2i_idx, int32_t n_items,
+                          int64_t pair_base, int32_t batch, uint64_t seed, uint32_t step,
+                          const uint32_t* step_ptr, int32_t* heads, int32_t* pos_tails,
+                          int32_t* neg_tails, int32_t* n_valid, void* workspace, size_t ws_bytes,
+                          void* stream) {
   RS_CHECK_ARG(n_items >= 1 && batch >= 0, "rs_item_pairs: bad sizes");
   RS_CHECK_ARG(i2u_indptr && i2u_idx && u2i_indptr && u2i_idx, "rs_item_pairs: null graph");
   hipStream_t st = as_stream(stream);
@@ -550,7 +554,7 @@ extern "C" int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_i
   }
   pairs_gen_kernel<<<grid_for(batch), 256, 0, st>>>(
       make_graph(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx), n_items, pair_base, batch, seed, step,
-      tmp, flag);
+      step_ptr, tmp, flag);
   RS_CHECK_LAUNCH();
   int32_t s = exclusive_scan_i32(flag, offs, batch, n_valid, sws, exclusive_scan_ws_size(batch), st);
   if (s) return s;
@@ -558,6 +562,28 @@ extern "C" int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_i
                                                         neg_tails);
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_item_pairs(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                 const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                 int32_t n_items, int64_t pair_base, int32_t batch, uint64_t seed,
+                                 uint32_t step, int32_t* heads, int32_t* pos_tails,
+                                 int32_t* neg_tails, int32_t* n_valid, void* workspace,
+                                 size_t ws_bytes, void* stream) {
+  return item_pairs(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx, n_items, pair_base, batch, seed,
+                    step, nullptr, heads, pos_tails, neg_tails, n_valid, workspace, ws_bytes,
+                    stream);
+}
+
+extern "C" int32_t rs_item_pairs_at(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                    const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                    int32_t n_items, int64_t pair_base, int32_t batch,
+                                    uint64_t seed, const uint32_t* step_ptr, int32_t* heads,
+                                    int32_t* pos_tails, int32_t* neg_tails, int32_t* n_valid,
+                                    void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(step_ptr != nullptr, "rs_item_pairs_at: null step pointer");
+  return item_pairs(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx, n_items, pair_base, batch, seed, 0u,
+                    step_ptr, heads, pos_tails, neg_tails, n_valid, workspace, ws_bytes, stream);
 }
 
 extern "C" int32_t rs_pair_set_build(const int32_t* src, const int32_t* dst, int64_t n,
@@ -573,14 +599,13 @@ extern "C" int32_t rs_pair_set_build(const int32_t* src, const int32_t* dst, int
   return RS_OK;
 }
 
-extern "C" int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
-                                        const int64_t* u2i_indptr, const int32_t* u2i_idx,
-                                        const int32_t* seeds, int64_t n_seeds,
-                                        int32_t num_walks, int32_t n_traversals,
-                                        float restart_prob, uint64_t seed, uint32_t step,
-                                        uint32_t layer, int32_t num_neighbors,
-                                        const uint64_t* excl_table, int64_t excl_capacity,
-                                        int32_t* nbr, int32_t* cnt, void* stream) {
+static int32_t pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                 const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                 const int32_t* seeds, int64_t n_seeds, int32_t num_walks,
+                                 int32_t n_traversals, float restart_prob, uint64_t seed,
+                                 uint32_t step, const uint32_t* step_ptr, uint32_t layer,
+                                 int32_t num_neighbors, const uint64_t* excl_table,
+                                 int64_t excl_capacity, int32_t* nbr, int32_t* cnt, void* stream) {
   RS_CHECK_ARG(num_walks >= 1 && num_walks <= 64 && n_traversals >= 1 && n_traversals <= 8 &&
                    num_neighbors >= 1 && layer < 65536 && n_seeds >= 0,
                "rs_pinsage_neighbors: need 1<=num_walks<=64, 1<=n_traversals<=8, k>=1");
@@ -595,10 +620,38 @@ extern "C" int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t
   const size_t lds = (size_t)2 * 256 * n_traversals * sizeof(int32_t);
   neighbors_kernel<<<(unsigned)ceil_div(n_seeds, per_block), 256, lds, as_stream(stream)>>>(
       make_graph(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx), seeds, n_seeds, num_walks, wshift,
-      n_traversals, stop_threshold(restart_prob), seed, step, layer, num_neighbors, excl_table,
-      excl_capacity ? (uint32_t)(excl_capacity - 1) : 0u, nbr, cnt);
+      n_traversals, stop_threshold(restart_prob), seed, step, step_ptr, layer, num_neighbors,
+      excl_table, excl_capacity ? (uint32_t)(excl_capacity - 1) : 0u, nbr, cnt);
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_pinsage_neighbors(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                        const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                        const int32_t* seeds, int64_t n_seeds,
+                                        int32_t num_walks, int32_t n_traversals,
+                                        float restart_prob, uint64_t seed, uint32_t step,
+                                        uint32_t layer, int32_t num_neighbors,
+                                        const uint64_t* excl_table, int64_t excl_capacity,
+                                        int32_t* nbr, int32_t* cnt, void* stream) {
+  return pinsage_neighbors(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx, seeds, n_seeds, num_walks,
+                           n_traversals, restart_prob, seed, step, nullptr, layer, num_neighbors,
+                           excl_table, excl_capacity, nbr, cnt, stream);
+}
+
+extern "C" int32_t rs_pinsage_neighbors_at(const int64_t* i2u_indptr, const int32_t* i2u_idx,
+                                           const int64_t* u2i_indptr, const int32_t* u2i_idx,
+                                           const int32_t* seeds, int64_t n_seeds,
+                                           int32_t num_walks, int32_t n_traversals,
+                                           float restart_prob, uint64_t seed,
+                                           const uint32_t* step_ptr, uint32_t layer,
+                                           int32_t num_neighbors, const uint64_t* excl_table,
+                                           int64_t excl_capacity, int32_t* nbr, int32_t* cnt,
+                                           void* stream) {
+  RS_CHECK_ARG(step_ptr != nullptr, "rs_pinsage_neighbors_at: null step pointer");
+  return pinsage_neighbors(i2u_indptr, i2u_idx, u2i_indptr, u2i_idx, seeds, n_seeds, num_walks,
+                           n_traversals, restart_prob, seed, 0u, step_ptr, layer, num_neighbors,
+                           excl_table, excl_capacity, nbr, cnt, stream);
 }
 
 extern "C" size_t rs_unique_first_workspace_size(int64_t n_nodes, int64_t n) {

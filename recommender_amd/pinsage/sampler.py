@@ -200,17 +200,24 @@ class PinSageSampler:
                L.ptr(count), L.ptr(self.err_flag), L.ptr(ws), ws.numel(), L.stream_ptr(ids.device))
         return uniq[:cap], local, count
 
-    def sample_pairs_static(self, batch: int, seed: int, step: int, pair_base: int = 0):
+    def sample_pairs_static(self, batch: int, seed: int, step: int, pair_base: int = 0,
+                            step_dev: torch.Tensor | None = None):
         """item_pairs without the host read of the valid count: (heads, pos, neg) [batch] with
-        -1 past the device count n_valid [1] (data_loader.py:6-18, dropped pairs at the end)."""
+        -1 past the device count n_valid [1] (data_loader.py:6-18, dropped pairs at the end).
+        step_dev ([1] int32 device): the RNG step is read from it instead (`step` ignored)."""
         dev = self.g.device
         heads, pos, neg = (self._buf(n, (batch,), torch.int32) for n in ("heads", "pos", "neg"))
         n_valid = self._buf("n_valid", (1,), torch.int32)
         n_valid.zero_()
         ws = self.scratch.get("pairs", L.lib().rs_item_pairs_workspace_size(batch), dev)
-        L.call("rs_item_pairs", *(L.ptr(t) for t in self.g.csr_args()), self.g.n_items, pair_base,
-               batch, seed, step & 0xFFFFFFFF, L.ptr(heads), L.ptr(pos), L.ptr(neg),
-               L.ptr(n_valid), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        if step_dev is None:
+            L.call("rs_item_pairs", *(L.ptr(t) for t in self.g.csr_args()), self.g.n_items,
+                   pair_base, batch, seed, step & 0xFFFFFFFF, L.ptr(heads), L.ptr(pos),
+                   L.ptr(neg), L.ptr(n_valid), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        else:
+            L.call("rs_item_pairs_at", *(L.ptr(t) for t in self.g.csr_args()), self.g.n_items,
+                   pair_base, batch, seed, L.ptr(step_dev), L.ptr(heads), L.ptr(pos),
+                   L.ptr(neg), L.ptr(n_valid), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
         pad = self._buf("pair_pad", (batch,), torch.bool)
         torch.ge(self._arange(batch), n_valid, out=pad)
         for t in (heads, pos, neg):
@@ -224,10 +231,12 @@ class PinSageSampler:
                 torch.arange(n, dtype=torch.int32, device=self.g.device))
         return self._static[key]
 
-    def sample_static(self, heads, pos_tails, neg_tails, n_valid):
+    def sample_static(self, heads, pos_tails, neg_tails, n_valid, step_dev=None):
         """sample_from_item_pairs on a sample_pairs_static batch, with no host sync: pair
         graphs carry `valid` / `n_valid`, blocks carry `n_dst_live`, padded src nodes are -1.
-        The returned tensors are the sampler's buffers, overwritten by its next call."""
+        The returned tensors are the sampler's buffers, overwritten by its next call.
+        step_dev ([1] int32 device): the walks' RNG step is read from it instead of self.step
+        (self.step still advances on the host)."""
         B = heads.numel()
         n_items, k = self.g.n_items, self.num_neighbors
         ids = self._buf("pair_ids", (3 * B,), torch.int32)
@@ -251,22 +260,28 @@ class PinSageSampler:
         blocks = []
         dst, n_dst = seeds, n_seeds
         for layer in range(self.num_layers):
-            blocks.insert(0, self._block_static(layer, dst, n_dst, (table, ecap)))
+            blocks.insert(0, self._block_static(layer, dst, n_dst, (table, ecap), step_dev))
             dst, n_dst = blocks[0].src_nodes, blocks[0].n_src_live
         self.step += 1
         return pos_graph, neg_graph, blocks
 
-    def _block_static(self, layer, dst, n_dst, excl):
+    def _block_static(self, layer, dst, n_dst, excl, step_dev=None):
         dev = self.g.device
         cap_dst, k = dst.numel(), self.num_neighbors
         pre = f"l{layer}."
         nbr = self._buf(pre + "nbr", (cap_dst, k), torch.int32)
         cnt = self._buf(pre + "cnt", (cap_dst, k), torch.int32)
         table, ecap = excl
-        L.call("rs_pinsage_neighbors", *(L.ptr(t) for t in self.g.csr_args()), L.ptr(dst),
-               cap_dst, self.num_random_walks, self.num_traversals, self.termination_prob,
-               self.seed, self.step & 0xFFFFFFFF, layer, k, L.ptr(table), ecap, L.ptr(nbr),
-               L.ptr(cnt), L.stream_ptr(dev))
+        if step_dev is None:
+            L.call("rs_pinsage_neighbors", *(L.ptr(t) for t in self.g.csr_args()), L.ptr(dst),
+                   cap_dst, self.num_random_walks, self.num_traversals, self.termination_prob,
+                   self.seed, self.step & 0xFFFFFFFF, layer, k, L.ptr(table), ecap, L.ptr(nbr),
+                   L.ptr(cnt), L.stream_ptr(dev))
+        else:
+            L.call("rs_pinsage_neighbors_at", *(L.ptr(t) for t in self.g.csr_args()), L.ptr(dst),
+                   cap_dst, self.num_random_walks, self.num_traversals, self.termination_prob,
+                   self.seed, L.ptr(step_dev), layer, k, L.ptr(table), ecap, L.ptr(nbr),
+                   L.ptr(cnt), L.stream_ptr(dev))
         ids = self._buf(pre + "ids", (cap_dst * (1 + k),), torch.int32)
         torch.cat([dst, nbr.reshape(-1)], out=ids)
         cap_src = min(cap_dst * (1 + k), self.g.n_items)

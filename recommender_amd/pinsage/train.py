@@ -127,6 +127,39 @@ class PinSageStep:
             return loss
         return replay
 
+    def capture_with_sampling(self, sampler, batch_size: int, seed: int, step: int,
+                              pair_base: int = 0):
+        """One HIP graph for the WHOLE step: pair sampling (sample_pairs_static), neighbour
+        walks and blocks (sample_static), forward, backward and Keras Adam. The two RNG steps
+        (the pair sampler's `step` and the sampler's walk step) live in device memory and the
+        graph advances them, so replay k samples exactly what eager step `step` + k would.
+        Returns replay() -> loss tensor. Run at least one eager static_step first."""
+        dev = sampler.g.device
+        pair_step = torch.tensor([step], dtype=torch.int32, device=dev)
+        walk_step = torch.tensor([sampler.step], dtype=torch.int32, device=dev)
+        opt = self.opt_graph
+        opt.prepare()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        host_step = sampler.step
+        with torch.cuda.graph(g):
+            batch = sampler.sample_static(
+                *sampler.sample_pairs_static(batch_size, seed, 0, pair_base, step_dev=pair_step),
+                step_dev=walk_step)
+            loss = self.static_step(*batch)
+            pair_step.add_(1)
+            walk_step.add_(1)
+        sampler.step = host_step  # the capture ran no step
+        self._graph = g
+
+        def replay():
+            opt.prepare()
+            g.replay()
+            opt.iterations += 1
+            sampler.step += 1
+            return loss
+        return replay
+
     def _allreduce_and_apply_tables(self):
         """Densify each table's IndexedSlices grad (deterministic segmented sum), bucket it
         with the dense grads into one all-reduce, average over ranks, then apply the tables

@@ -554,15 +554,16 @@ def test_static_forward_backward_equals_dynamic():
 
 
 def test_static_step_graph_replay_bit_exact_and_matches_dynamic():
-    """Four training steps three ways: (a) the dynamic PinSageStep (host-synced shapes,
+    """Four training steps four ways: (a) the dynamic PinSageStep (host-synced shapes,
     SparseAdam + KerasAdam), (b) four eager static_steps, (c) one eager static_step, then
     the step captured once into a HIP graph and replayed three times on freshly sampled
-    batches. (c) equals (b) to 1e-5 (the lr_t of each replay comes from device memory; a
+    batches, (d) as (c) with the sampling inside the graph (capture_with_sampling: the RNG
+    steps advance in device memory, so each replay samples the next step's batch). (c) equals (b) to 1e-5 (the lr_t of each replay comes from device memory; a
     frozen lr_t would be off by the bias-correction ratio, 0.18 vs 0.32 at step 4); (b) equals (a)
     to fp32 rounding order."""
     B = 96
     res = []
-    for mode in ("dynamic", "static", "graph"):
+    for mode in ("dynamic", "static", "graph", "graph_all"):
         g, model, smp = _pinsage_setup()
         step = PinSageStep(model, lr=1e-2)
         losses = []
@@ -571,6 +572,11 @@ def test_static_step_graph_replay_bit_exact_and_matches_dynamic():
             if mode == "dynamic":
                 h, p, n = item_pairs(g, B, 4, it)
                 losses.append(float(step(*smp.sample_from_item_pairs(h, p, n))))
+                continue
+            if mode == "graph_all" and it > 0:
+                if replay is None:  # sampling inside the graph too, RNG steps on the device
+                    replay = step.capture_with_sampling(smp, B, 4, it)
+                losses.append(float(replay()))
                 continue
             batch = smp.sample_static(*smp.sample_pairs_static(B, 4, it))
             if mode == "static" or it == 0:
@@ -581,7 +587,10 @@ def test_static_step_graph_replay_bit_exact_and_matches_dynamic():
             losses.append(float(replay()))
         torch.cuda.synchronize()
         res.append((losses, _pinsage_params(model)))
-    (l_dyn, p_dyn), (l_sta, p_sta), (l_gr, p_gr) = res
+    (l_dyn, p_dyn), (l_sta, p_sta), (l_gr, p_gr), (l_all, p_all) = res
+    np.testing.assert_allclose(l_all, l_sta, rtol=1e-6)
+    for a, b in zip(p_sta, p_all):
+        np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(l_gr, l_sta, rtol=1e-6)
     for a, b in zip(p_sta, p_gr):
         # measured: ulp-level (1.5e-6 relative) differences in one weight — the library GEMM
