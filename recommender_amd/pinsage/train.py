@@ -197,8 +197,8 @@ def main(argv=None):
     ap.add_argument("--eval_every", type=int, default=1000)
     ap.add_argument("--top_k", type=int, default=10)
     ap.add_argument("--hip_graph", type=int, default=1,
-                    help="1: sync-free capacity-shaped batches, the model step replayed as one HIP "
-                         "graph (PinSageStep.capture); 0: the DGL-shaped dynamic step")
+                    help="1: sync-free capacity-shaped batches, sampling + step replayed as one "
+                         "HIP graph (PinSageStep.capture_with_sampling); 0: the DGL-shaped step")
     args = ap.parse_args(argv)
     num_layers = 2
     embedding_size = 8
@@ -215,12 +215,12 @@ def main(argv=None):
     replay = None
     for step in range(args.steps):
         if args.hip_graph:
-            batch = sampler.sample_static(*sampler.sample_pairs_static(
-                args.train_batch_size, args.seed, step))
             if step == 0:
-                loss = step_fn.static_step(*batch)
-            else:
-                replay = replay or step_fn.capture(batch)
+                loss = step_fn.static_step(*sampler.sample_static(
+                    *sampler.sample_pairs_static(args.train_batch_size, args.seed, step)))
+            else:  # sampling + step in one graph, RNG steps advanced on the device
+                replay = replay or step_fn.capture_with_sampling(
+                    sampler, args.train_batch_size, args.seed, step)
                 loss = replay()
         else:
             heads, pos, neg = item_pairs(g, args.train_batch_size, args.seed, step)
