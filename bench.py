@@ -477,6 +477,21 @@ def main():
             lw = float(tt.item())
         return round(lw / args.steps * 1e3, 3)
 
+    # per-step distribution (after the timed region, same steps): intervals between consecutive
+    # step starts on the main stream (the deferred update overlaps the next step, so this is the
+    # steady-state step time), reported as p10 / median / p90 (SURVEY 8(d) timing method)
+    step_dist = None
+    if per_call == 1 and args.steps >= 4:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        for i in range(args.steps):
+            evs[i].record()
+            loss = runners[i % len(runners)]()
+        evs[-1].record()
+        torch.cuda.synchronize()
+        d = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+        q = lambda f: round(d[min(len(d) - 1, int(f * (len(d) - 1) + 0.5))], 3)  # noqa: E731
+        step_dist = {"p10": q(0.1), "median": q(0.5), "p90": q(0.9), "steps": args.steps}
+
     layerwise_ms = layerwise_fwd_ms = None
     if args.compare_layerwise and args.mlp_bwd == "factored" and not args.graph:
         if args.mlp_fwd == "composed":
@@ -517,18 +532,33 @@ def main():
         tsum = sum(v["traffic"] for v in per_kernel.values()) if traffic and all(
             v["traffic"] is not None for v in per_kernel.values()) else None
         dom = max(iso, key=iso.get)
+        # measured STREAM-copy bandwidth of this GPU: a 4 GiB device-to-device copy
+        src = torch.empty(1 << 30, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(10):
+            dst.copy_(src)
+        c1.record()
+        torch.cuda.synchronize()
+        copy_gbs = 2 * src.numel() * 4 * 10 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        del src, dst
         roof = {"bound": "hbm", "kernel": "embedding_path (" + " + ".join(iso) + ")",
                 "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(a / HBM_PEAK_GBS, 4), "traffic": tsum,
                 "algorithmic_bytes": int(path_bytes), "us_per_step": round(path_us, 1),
                 "bytes_per_example": round(per_ex, 1), "unique_rows_per_step": U,
                 "dominant_kernel": dom, "per_kernel": per_kernel,
+                "measured_copy_GBs": round(copy_gbs, 1),
+                "frac_of_measured_copy": round(a / copy_gbs, 4),
                 "traffic_detail": traffic_detail,
                 "note": "achieved = SURVEY 8(d) path bytes at measured U / the sum of the path "
                         "kernels' isolated launch times (HIP events, after the timed region, on "
                         "the model's slab and ids); in_step_span_us = the same kernel's HIP-event "
                         "span inside the timed steps (side-stream spans include co-run time); "
-                        "traffic = PMC FETCH+WRITE per call"}
+                        "traffic = PMC FETCH+WRITE per call; measured_copy_GBs = torch D2D copy_ "
+                        "of 4 GiB (read + write bytes / time), the STREAM-copy reference"}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_steps > 0:
@@ -540,6 +570,7 @@ def main():
             "value": round(value, 1), "unit": "examples/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "step_ms_distribution": step_dist,
             "data": "synthetic (Criteo-Kaggle-skewed 26-slot slab, bounded Zipf(1.05) ids, seed 4)",
             "config": {"workload": f"dlrm_criteo_{S}x{args.rows}x{D}", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "rows": args.rows, "dim": D, "slots": S,
