@@ -488,9 +488,11 @@ def main():
             loss = runners[i % len(runners)]()
         evs[-1].record()
         torch.cuda.synchronize()
-        d = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+        raw = [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(args.steps)]
+        d = sorted(raw)
         q = lambda f: round(d[min(len(d) - 1, int(f * (len(d) - 1) + 0.5))], 3)  # noqa: E731
-        step_dist = {"p10": q(0.1), "median": q(0.5), "p90": q(0.9), "steps": args.steps}
+        step_dist = {"p10": q(0.1), "median": q(0.5), "p90": q(0.9), "steps": args.steps,
+                     "ms": raw}
 
     layerwise_ms = layerwise_fwd_ms = None
     if args.compare_layerwise and args.mlp_bwd == "factored" and not args.graph:
