@@ -326,6 +326,7 @@ def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float 
 
 
 TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
+_TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
@@ -368,6 +369,15 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     D = w.shape[1]
     dev = w.device
     _wait_update(emb)
+    # the fused kernel is one round of resident blocks: launched while the sort stream's last
+    # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
+    # kernel 0.42 -> 0.62 ms whenever the two overlap). The sort normally ends first (it runs
+    # beside the previous update, which the kernel waits for anyway), so waiting for it costs
+    # at most its tail.
+    ahead = emb._presorted[1] if getattr(emb, "_presorted", None) else None
+    ready = getattr(ahead, "ready", None)
+    if ready is not None and _TRAIN_WAITS_SORT:
+        torch.cuda.current_stream(dev).wait_event(ready)
     y = torch.empty(B, device=dev, dtype=torch.float32)
     grad = torch.empty(B * S, D, device=dev, dtype=torch.float32)
     M = TRAIN_SUMS_ATOP + 2 + n_in * D + D
