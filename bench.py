@@ -61,8 +61,9 @@ PMC_SYMBOLS = [
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # SURVEY 8(d) timing method: warm-up 10, measure 100 steps (0.1 s of GPU time)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch")
     ap.add_argument("--rows", type=int, default=40_000_000)
     ap.add_argument("--dim", type=int, default=128)
