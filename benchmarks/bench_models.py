@@ -57,6 +57,9 @@ def main():
                          "capacity-shaped sync-free batches, eager (static_step); graph = the same "
                          "step captured once and replayed (PinSageStep.capture), sampling eager; "
                          "graph_all = sampling inside the graph too (capture_with_sampling)")
+    ap.add_argument("--eges-mode", default="graph", choices=["eager", "graph"],
+                    help="eges: eager = EGESStep.__call__ (SparseAdam keras); graph = static_step "
+                         "captured once and replayed (EGESStep.capture)")
     ap.add_argument("--tuned-gemms", type=int, default=-1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
                          "-1 (default): on for the fixed-shape models (dien, esmm, mmoe), off for the "
@@ -148,10 +151,27 @@ def main():
             batches.append((tuple(torch.from_numpy(a).to(dev) for a in inp),
                             torch.from_numpy(lab).to(dev)))
         step = train
+        if args.eges_mode == "graph":
+            # static input buffers refilled from the batch pool, then one graph replay per step
+            st_in = tuple(torch.empty_like(a) for a in batches[0][0])
+            st_lab = torch.empty_like(batches[0][1])
+            gctr = {"n": 0, "replay": None}
+
+            def step(inp, lab):
+                for d_, s_ in zip(st_in, inp):
+                    d_.copy_(s_)
+                st_lab.copy_(lab)
+                gctr["n"] += 1
+                if gctr["n"] == 1:
+                    return train.static_step(st_in, st_lab)
+                if gctr["replay"] is None:
+                    gctr["replay"] = train.capture(st_in, st_lab)
+                return gctr["replay"]()
         watch = ["rs_embedding_fwd", "rs_side_pool_fwd", "rs_side_pool_bwd", "rs_match_logits_fwd",
                  "rs_match_logits_bwd", "rs_sort_ids", "rs_embedding_apply",
                  "rs_keras_adam_dense_sweep"]
-        cfg = {"workload": "eges_b1024_d160_ns5", "batch": B, "items": n_items}
+        cfg = {"workload": "eges_b1024_d160_ns5", "batch": B, "items": n_items,
+               "mode": args.eges_mode}
     elif args.model == "dlrm_cfg2":
         from recommender_amd.ctr.train import TrainStep, build_model
         from recommender_amd.synthetic import criteo_batch

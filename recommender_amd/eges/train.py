@@ -15,7 +15,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from ..optim import SparseAdam
+from ..optim import GraphKerasAdam, SparseAdam, _Workspace, densify_grad
 from .model import EGES, GES, DeepWalk
 from .sampler import EGESPairSampler
 
@@ -67,6 +67,51 @@ class EGESStep:
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+    # -- graph-capturable step --------------------------------------------------------------
+    def static_step(self, inputs, labels):
+        """The same step with no host-side per-step scalars, so it can sit in a HIP graph:
+        every table's IndexedSlices gradient densified (densify_grad, no sync) and Keras Adam
+        over all of them with lr_t from device memory (GraphKerasAdam, one launch). Keras'
+        sparse Adam decays m / v and moves every row each step anyway (the dense sweep), so the
+        dense step is the same update. Its Adam state is its own: do not interleave with
+        __call__."""
+        tables = self.model.tables()
+        if getattr(self, "opt_graph", None) is None:
+            self.opt_graph = GraphKerasAdam([t.weight for t in tables], lr=self.opt.lr)
+            self._ws = _Workspace()
+        logits = self.model(inputs)
+        loss = F.binary_cross_entropy_with_logits(logits, labels)
+        loss.backward()
+        grads = []
+        for t in tables:
+            got = t.take_grad()
+            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
+                         else torch.zeros_like(t.weight))
+        if not torch.cuda.is_current_stream_capturing():
+            self.opt_graph.prepare()
+            self.opt_graph.iterations += 1
+        self.opt_graph.apply(grads)
+        return loss.detach()
+
+    def capture(self, inputs, labels):
+        """Record one static_step on (inputs, labels) — static device tensors the caller
+        refills before each replay — into a HIP graph; returns replay() -> loss tensor. Run at
+        least one eager static_step first."""
+        opt = self.opt_graph
+        opt.prepare()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self.static_step(inputs, labels)
+        self._graph = g
+
+        def replay():
+            opt.prepare()
+            g.replay()
+            opt.iterations += 1
+            return loss
+        return replay
 
 
 def build(model_type, n_items, n_cat, n_brand, embedding_size=160, device="cuda", generator=None):

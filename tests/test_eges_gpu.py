@@ -188,3 +188,46 @@ def test_train_step_vs_oracle(rng, model_type):
         np.testing.assert_array_equal(t.weight.cpu().numpy(), w2, err_msg=n)
         np.testing.assert_array_equal(m_t.cpu().numpy(), m2, err_msg=n)
         np.testing.assert_array_equal(v_t.cpu().numpy(), v2, err_msg=n)
+
+
+@pytest.mark.parametrize("model_type", ["BGE", "EGES"])
+def test_static_step_and_graph_replay(rng, model_type):
+    """EGESStep.static_step (tables densified, Keras Adam with lr_t from device memory) equals
+    the SparseAdam(keras) step to fp32 rounding over 3 steps, and the captured graph replayed on
+    refilled input buffers equals the eager static steps (1e-5: the library GEMMs may pick
+    another algorithm under capture)."""
+    batches = []
+    for _ in range(3):
+        *inp, lab = synthetic_batch(rng, 256, 500, 20, 30)
+        inp = [torch.from_numpy(a).to(DEV) for a in inp]
+        if model_type == "BGE":
+            inp = [inp[0], inp[3]]
+        batches.append((tuple(inp), torch.from_numpy(lab).to(DEV)))
+
+    def run(mode):
+        model = build(model_type, 500, 20, 30, embedding_size=32,
+                      generator=torch.Generator(device=DEV).manual_seed(3))
+        step = EGESStep(model, lr=1e-2)
+        st_in = tuple(torch.empty_like(a) for a in batches[0][0])
+        st_lab = torch.empty_like(batches[0][1])
+        replay, losses = None, []
+        for i, (inp, lab) in enumerate(batches):
+            if mode == "eager":
+                losses.append(float(step(inp, lab)))
+            elif mode == "static" or i == 0:
+                losses.append(float(step.static_step(inp, lab)))
+            else:
+                for d_, s_ in zip(st_in, inp):
+                    d_.copy_(s_)
+                st_lab.copy_(lab)
+                replay = replay or step.capture(st_in, st_lab)
+                losses.append(float(replay()))
+        torch.cuda.synchronize()
+        return losses, [t.weight.detach().cpu().numpy().copy() for t in model.tables()]
+
+    (le, pe), (ls, ps), (lg, pg) = run("eager"), run("static"), run("graph")
+    np.testing.assert_allclose(ls, le, rtol=1e-5)
+    np.testing.assert_allclose(lg, ls, rtol=1e-6)
+    for a, b, c in zip(pe, ps, pg):
+        np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(c, b, rtol=1e-5, atol=1e-7)
