@@ -14,7 +14,7 @@ import torch
 
 from ..functional import binary_crossentropy
 from ..metrics import AUC
-from ..optim import GraphKerasAdam, KerasAdam, SparseAdam, _Workspace, densify_grad
+from ..optim import KerasAdam, SparseAdam
 from . import DIEN, DIN, BaseModel
 
 
@@ -65,61 +65,6 @@ class DIENStep:
         self.opt_dense.step()
         self.opt_sparse.step()
         return total, aux
-
-    # -- graph-capturable step --------------------------------------------------------------
-    def static_step(self, feats, label):
-        """__call__ with no host-side per-step scalars, so it can sit in a HIP graph: the two
-        tables' IndexedSlices gradients densified (densify_grad, no sync) and Keras Adam over
-        every parameter with lr_t from device memory (GraphKerasAdam: one launch). Keras'
-        sparse Adam moves every row each step anyway, so the dense step is the same update.
-        Its Adam state is its own: do not interleave with __call__."""
-        tables = [self.model.item_embedding, self.model.cat_embedding]
-        if getattr(self, "opt_graph", None) is None:
-            tw = {id(t.weight) for t in tables}
-            self._gdense = [p for p in self.opt_dense.param_groups[0]["params"]
-                            if id(p) not in tw and p.numel() > 0]
-            self.opt_graph = GraphKerasAdam(self._gdense + [t.weight for t in tables],
-                                            lr=self.opt_dense.param_groups[0]["lr"])
-            self._ws = _Workspace()
-        for p in self._gdense:
-            p.grad = None
-        if self.is_dien:
-            pred, aux = self.model(feats, training=True)
-            aux = aux.mean()
-            total = binary_crossentropy(label, pred, reduction="mean") + aux
-        else:
-            pred = self.model(feats, training=True)
-            total = aux = binary_crossentropy(label, pred, reduction="mean")
-        total.backward()
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self._gdense]
-        for t in tables:
-            got = t.take_grad()
-            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
-                         else torch.zeros_like(t.weight))
-        if not torch.cuda.is_current_stream_capturing():
-            self.opt_graph.prepare()
-            self.opt_graph.iterations += 1
-        self.opt_graph.apply(grads)
-        return total.detach(), aux.detach()
-
-    def capture(self, feats, label):
-        """Record one static_step on (feats, label) — static device tensors the caller refills
-        before each replay — into a HIP graph; returns replay() -> (total, aux). Run at least
-        one eager static_step first."""
-        opt = self.opt_graph
-        opt.prepare()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            out = self.static_step(feats, label)
-        self._graph = g
-
-        def replay():
-            opt.prepare()
-            g.replay()
-            opt.iterations += 1
-            return out
-        return replay
 
 
 def main(argv=None):
