@@ -1,13 +1,18 @@
-"""Checker for one production DLRM SGD step against oracle/ctr.py, on the step's touched rows.
+"""Checker for one production DLRM SGD step against oracle/ctr.py: the touched table rows AND
+the dense half (every MLP parameter gradient and update).
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py; parity unpinned): called by
-tests/test_northstar_gpu.py (full north-star size) and __graft_entry__.smoke() (small size).
-It drives the product path (recommender_amd TrainStep on cuda) and checks it; nothing in the
-product imports this module.
+tests/test_northstar_gpu.py (full north-star size, cfg2) and __graft_entry__.smoke() (small
+size). It drives the product path (recommender_amd TrainStep on cuda) and checks it; nothing in
+the product imports this module.
 
 The slab rows the batch references are gathered before the step and the ids are remapped onto
 them monotonically, so the oracle's sort order, tiles and segmented-sum order are exactly those
 of the full slab (reference semantics: ctr/model.py:45-57, ctr/train.py:77-79 SGD path).
+The oracle carries its OWN MLP state across steps (pass the same `state` dict to every call):
+an error in one step's MLP update then shows up in the next step's logits and gradients instead
+of being absorbed by re-reading the GPU's weights. The table rows are read from the GPU before
+each step (they are checked bit-exact against the oracle apply, so the two tables agree).
 Checks (tolerances are the ones stated here):
   * loss within 1e-5 relative;
   * per-example logits: the pre-sigmoid value recovered from p within 1e-5 of its own value
@@ -15,6 +20,13 @@ Checks (tolerances are the ones stated here):
     rounding of either MLP evaluation order is relative to it), plus the fp32 resolution of p;
   * grad rows [B*S, D] (position order) within 1e-5 of the oracle's, relative to each element's
     float64 magnitude bound |dZ + dZᵀ|·|X|;
+  * every top / bottom MLP kernel and bias gradient within 1e-5 of its float64 magnitude bound
+    (oracle.ctr.chain_grad_bounds: Σ_b |h_b|·|G_b| carried through the chain), plus the bound
+    of the gradient error the logit tolerance above admits (|dG/dz| <= 1/4 per example, through
+    the same chain) and, for the bottom chain, of its upstream gradient's tolerance and of the
+    ReLU outputs whose pre-activation lies within rounding of 0;
+  * every MLP parameter after the step equal to fp32(before - lr·grad) within 1 ulp (the SGD
+    apply) — so it also lies within lr·(gradient tolerance) + 1 ulp of the oracle's update;
   * sorted rows / positions bit-exact;
   * touched table rows BIT-EXACT against the oracle's segmented sum + SGD fed with the kernel's
     own grad rows, and within 1e-4 of each row's |Δ| (+2 ulp of w) of the all-oracle update;
@@ -25,7 +37,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .ctr import DLRMState, dlrm_sgd_step
+from .ctr import DLRMState, chain_grad_bounds, dlrm_sgd_step, magnitude_chain
 from .embedding import global_rows, segment_sum_tiled
 
 
@@ -34,9 +46,71 @@ def _layers(mlp):
             for l in mlp.mlp]
 
 
-def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
+def _grads(mlp):
+    out = []
+    for l in mlp.mlp:
+        assert l.kernel.grad is not None and l.bias.grad is not None, "an MLP gradient is missing"
+        out.append((l.kernel.grad.detach().cpu().numpy().copy(),
+                    l.bias.grad.detach().cpu().numpy().copy()))
+    return out
+
+
+def _check_chain(name, got, ref, tol):
+    """got / ref: [(dk, db)]; tol: [(kernel tol, bias tol)] (float64, same shapes)."""
+    worst = 0.0
+    for i, ((gk, gb), (rk, rb), (tk, tb)) in enumerate(zip(got, ref, tol)):
+        for what, g, r, t in (("kernel", gk, rk, tk), ("bias", gb, rb, tb)):
+            err = np.abs(g.astype(np.float64) - np.asarray(r, np.float64))
+            t = np.asarray(t, np.float64).reshape(err.shape) + 1e-38
+            ratio = err / t
+            if (ratio > 1).any():
+                j = int(np.argmax(ratio))
+                raise AssertionError(
+                    f"{name} layer {i} {what} gradient off at flat index {j}: gpu "
+                    f"{g.reshape(-1)[j]!r} oracle {np.asarray(r).reshape(-1)[j]!r} "
+                    f"(err/tol {ratio.max():.3g})")
+            worst = max(worst, float(ratio.max()))
+    return worst
+
+
+def _check_sgd(name, before, after, grads, lr):
+    """after == fp32(before - lr·g) within 1 ulp (fmaf or mul-then-sub rounding)."""
+    lr = np.float64(np.float32(lr))
+    for i, ((k0, b0), (k1, b1), (gk, gb)) in enumerate(zip(before, after, grads)):
+        for what, p0, p1, g in (("kernel", k0, k1, gk), ("bias", b0, b1, gb)):
+            exact = p0.astype(np.float64) - lr * g.astype(np.float64)
+            err = np.abs(p1.astype(np.float64) - exact)
+            ok = err <= np.spacing(np.abs(p1).astype(np.float32)).astype(np.float64)
+            assert ok.all(), (f"{name} layer {i} {what}: SGD update is not before - lr*grad "
+                              f"({int((~ok).sum())} elements)")
+
+
+def dense_half_tolerances(det, n_examples, mean=True):
+    """Per-element tolerances of the top / bottom chains' parameter gradients (see the module
+    docstring). Returns (top [(tk, tb)], bottom [(tk, tb)])."""
+    scale = 1.0 / n_examples if mean else 1.0
+    z = det["logit"].astype(np.float64)
+    ztol = 1e-5 * np.abs(z) + 1e-6 * det["logit_bound"]
+    tG = np.abs(det["top_G"]).astype(np.float64)                      # [B, 1]
+    dG = 0.25 * ztol[:, None] * scale                                  # |dG/dz| <= 1/4
+    top_tol, _ = chain_grad_bounds(det["top_in"], det["top_layers"], 1e-5 * tG + dG)
+    # bottom chain upstream gradient dbot = (interaction part) + G·Q0[F²:]: its tolerance
+    F2 = det["top_in"].shape[1] - det["bottom_dout"].shape[1]
+    qtail = det["top_Q"][F2:][None, :]
+    ddbot = 1e-5 * det["dbot_interaction_bound"] + (1e-5 * tG + dG) * qtail
+    # ReLU outputs whose pre-activation is within rounding of 0 may go either way
+    pre_bound = magnitude_chain(np.abs(det["bottom_in"]), det["bottom_layers"])
+    amb = np.abs(det["bottom_pre"]) <= 1e-5 * pre_bound
+    bG = np.abs(det["bottom_G"]).astype(np.float64)
+    dGb = ddbot + amb * (np.abs(det["bottom_dout"]) + ddbot)
+    bot_tol, _ = chain_grad_bounds(det["bottom_in"], det["bottom_layers"], 1e-5 * bG + dGb)
+    return top_tol, bot_tol
+
+
+def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr, state=None) -> dict:
     """Run `step` (a recommender_amd.ctr.train.TrainStep with a fused SparseSGD) on one batch and
-    check it against the oracle; raises AssertionError on a mismatch, returns a summary."""
+    check it against the oracle; raises AssertionError on a mismatch, returns a summary.
+    state: a dict reused across consecutive calls; it carries the oracle's own MLP layers."""
     import torch
 
     emb = model.embedding_layer
@@ -56,7 +130,13 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     probe = np.setdiff1d(np.r_[np.arange(0, V, max(V // 41, 1)), V - 1, V - 2], uniq)
     pt = torch.from_numpy(probe).to(dev)
     probe_before = W[pt].cpu().numpy()
-    st = DLRMState(before.copy(), None, _layers(model.bottom_mlp), _layers(model.top_mlp))
+    top0, bot0 = _layers(model.top_mlp), _layers(model.bottom_mlp)
+    if state is None:
+        state = {}
+    if "top" not in state:
+        state["top"] = [(k.copy(), b.copy()) for k, b in top0]
+        state["bottom"] = [(k.copy(), b.copy()) for k, b in bot0]
+    st = DLRMState(before.copy(), None, state["bottom"], state["top"])
 
     captured = {}
     opt = step.opt_sparse
@@ -87,9 +167,12 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     s_rows = captured["sorted"].rows.cpu().numpy().view(np.uint32).astype(np.int64)
     s_pos = captured["sorted"].pos.cpu().numpy()
     assert np.array_equal(W[pt].cpu().numpy(), probe_before), "an untouched row changed"
+    tgrad_gpu, bgrad_gpu = _grads(model.top_mlp), _grads(model.bottom_mlp)
+    top1, bot1 = _layers(model.top_mlp), _layers(model.bottom_mlp)
 
     det: dict = {}
     ref_loss = dlrm_sgd_step(st, compact, dn, lb, lr, det)
+    state["top"], state["bottom"] = st.top, st.bottom
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), f"loss {loss} vs oracle {ref_loss}"
 
     z_ref = det["logit"].astype(np.float64)
@@ -100,6 +183,14 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     zerr = np.abs(z_gpu - z_ref)
     assert (zerr <= ztol).all(), (
         f"logit off at example {int(np.argmax(zerr / ztol))}: max err/tol {(zerr / ztol).max():.3g}")
+
+    # the dense half: twelve parameter gradients against the oracle, then the SGD apply
+    mean = getattr(step, "loss_reduction", "mean") == "mean"
+    top_tol, bot_tol = dense_half_tolerances(det, B, mean)
+    top_ratio = _check_chain("top MLP", tgrad_gpu, det["top_grads"], top_tol)
+    bot_ratio = _check_chain("bottom MLP", bgrad_gpu, det["bottom_grads"], bot_tol)
+    _check_sgd("top MLP", top0, top1, tgrad_gpu, lr)
+    _check_sgd("bottom MLP", bot0, bot1, bgrad_gpu, lr)
 
     assert np.array_equal(uniq[det["sorted_rows"].astype(np.int64)], s_rows), "sorted rows differ"
     assert np.array_equal(det["sorted_pos"], s_pos), "sorted positions differ"
@@ -123,4 +214,6 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr) -> dict:
     return {"loss": loss, "oracle_loss": ref_loss, "touched_rows": int(uniq.size),
             "max_row": int(uniq.max()), "rows_beyond_2^32_elems": int((uniq * D >= (1 << 32)).sum()),
             "logit_err_over_tol": float((zerr / ztol).max()),
-            "grad_err_over_bound": float((gerr / gtol).max()), "frac_elements_changed": changed}
+            "grad_err_over_bound": float((gerr / gtol).max()),
+            "top_mlp_grad_err_over_tol": top_ratio, "bottom_mlp_grad_err_over_tol": bot_ratio,
+            "frac_elements_changed": changed}

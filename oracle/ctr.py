@@ -78,7 +78,8 @@ def dlrm_forward(st: DLRMState, cat, dense_in):
     B, S = cat.shape
     D = st.table.shape[1]
     F = S + 1
-    bot, bcache = mlp_forward(dense_in, st.bottom, "relu")
+    bpre = []
+    bot, bcache = mlp_forward(dense_in, st.bottom, "relu", bpre)
     rows = global_rows(cat, st.table.shape[0], st.slot_offsets).reshape(B, S)
     emb = np.where(rows[..., None] >= 0, st.table[np.maximum(rows, 0)], 0).astype(np.float32)
     x = np.concatenate([emb, bot[:, None, :]], axis=1)               # [B, F, D]
@@ -87,7 +88,8 @@ def dlrm_forward(st: DLRMState, cat, dense_in):
     tin = np.concatenate([z.reshape(B, F * F), bot], axis=1)
     pre = []
     p, tcache = mlp_forward(tin, st.top, "sigmoid", pre)
-    return p[:, 0], dict(bcache=bcache, tcache=tcache, x=x, rows=rows, logit=pre[0][:, 0])
+    return p[:, 0], dict(bcache=bcache, tcache=tcache, x=x, rows=rows, logit=pre[0][:, 0],
+                         bot_pre=bpre[0])
 
 
 def magnitude_chain(x_abs, layers):
@@ -98,6 +100,33 @@ def magnitude_chain(x_abs, layers):
     for k, b in layers:
         h = h @ np.abs(k).astype(np.float64) + np.abs(b).astype(np.float64)
     return h
+
+
+def chain_grad_bounds(x, layers, G):
+    """Float64 magnitude bounds of an MLP chain's parameter gradients for BOTH evaluation
+    orders (layer by layer, or factored from the last layer's G): h_{l-1} = x·R + c, so
+    |h_{l-1}ᵀ·g_l| <= (|R|ᵀ·|x|ᵀ·|G| + |c|⊗Σ|G|)·|Q_l|ᵀ with Q_l = K_{l+1}···K_L.
+    layers = [(kernel [in, out], bias [out])] as the input sees them; G [B, n_L] (its absolute
+    value is taken). Linear in |G|. Returns ([(kernel bound, bias bound)] per layer,
+    dx bound [B, in])."""
+    aG = np.abs(np.asarray(G, np.float64))
+    base = np.abs(np.asarray(x, np.float64)).T @ aG
+    Mb, absR, absc = [], None, None
+    for i, (k, b) in enumerate(layers):
+        k, b = np.asarray(k, np.float64), np.asarray(b, np.float64)
+        Mb.append(base if i == 0 else absR.T @ base + np.outer(absc, aG.sum(0)))
+        absR = np.abs(k) if absR is None else absR @ np.abs(k)
+        absc = np.abs(b) if absc is None else np.abs(k).T @ absc + np.abs(b)
+    out = [None] * len(layers)
+    absQ = None
+    for i in range(len(layers) - 1, -1, -1):
+        kb, bb = Mb[i], aG.sum(0)
+        if absQ is not None:
+            kb, bb = kb @ absQ.T, bb @ absQ.T
+        out[i] = (kb, bb)
+        ak = np.abs(np.asarray(layers[i][0], np.float64))
+        absQ = ak if absQ is None else ak @ absQ
+    return out, aG @ absQ.T
 
 
 def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
@@ -120,7 +149,7 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
     dx = np.matmul(sm, c["x"])                                       # [B, F, D]
     dbot = dx[:, S, :] + dtin[:, F * F:]
     _, bgrads = mlp_backward(dbot, st.bottom, c["bcache"], "relu", need_dx=False)
-    top_old = list(st.top)
+    top_old, bottom_old = list(st.top), list(st.bottom)
     lr = np.float32(lr)
     for layers, grads in ((st.top, tgrads), (st.bottom, bgrads)):
         for i, ((k, b), (dk, db)) in enumerate(zip(layers, grads)):
@@ -142,7 +171,14 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
         detail.update(p=p, logit=c["logit"], logit_bound=mag_logit,
                       dx=dx[:, :S, :].reshape(B * S, D), dx_bound=dx_b[:, :S, :].reshape(B * S, D),
                       uniq_rows=u, uniq_grad=ug, top_grads=tgrads, bottom_grads=bgrads,
-                      sorted_rows=sr, sorted_pos=sp)
+                      sorted_rows=sr, sorted_pos=sp,
+                      # the dense half: each chain's input, its last-layer gradient G (the
+                      # factored backward's only batch-deep operand) and the pre-step layers
+                      top_in=c["tcache"][0], top_G=dp * c["tcache"][-1] * (1 - c["tcache"][-1]),
+                      top_layers=top_old, top_Q=q[:, 0], bottom_in=dense_in,
+                      bottom_G=dbot * (c["bcache"][-1] > 0), bottom_dout=dbot,
+                      bottom_pre=c["bot_pre"], bottom_layers=bottom_old,
+                      dbot_interaction_bound=dx_b[:, S, :])
     st.table[u] = st.table[u] - lr * ug
     return loss
 

@@ -56,25 +56,4 @@ def assert_close_rel(got, ref, rtol=1e-5, scale=None, msg=""):
                              f"(max err/bound {float((err / np.maximum(bound, 1e-300)).max()):.3g})")
 
 
-def chain_grad_bounds(x, layers, G):
-    """Float64 magnitude bounds of an MLP chain's parameter gradients for BOTH evaluation
-    orders (layer by layer, or factored from the last layer's G): h_{l-1} = x·R + c, so
-    |h_{l-1}ᵀ·g_l| <= (|R|ᵀ·|x|ᵀ·|G| + |c|⊗Σ|G|)·|Q_l|ᵀ with Q_l = K_{l+1}···K_L.
-    layers = [(kernel [in, out], bias [out])] as the input sees them (float64); G [B, n_L].
-    Returns ([(kernel bound, bias bound)] per layer, dx bound [B, in])."""
-    aG = np.abs(np.asarray(G, np.float64))
-    base = np.abs(np.asarray(x, np.float64)).T @ aG
-    Mb, absR, absc = [], None, None
-    for i, (k, b) in enumerate(layers):
-        Mb.append(base if i == 0 else absR.T @ base + np.outer(absc, aG.sum(0)))
-        absR = np.abs(k) if absR is None else absR @ np.abs(k)
-        absc = np.abs(b) if absc is None else np.abs(k).T @ absc + np.abs(b)
-    out = [None] * len(layers)
-    absQ = None
-    for i in range(len(layers) - 1, -1, -1):
-        kb, bb = Mb[i], aG.sum(0)
-        if absQ is not None:
-            kb, bb = kb @ absQ.T, bb @ absQ.T
-        out[i] = (kb, bb)
-        absQ = np.abs(layers[i][0]) if absQ is None else np.abs(layers[i][0]) @ absQ
-    return out, aG @ absQ.T
+from oracle.ctr import chain_grad_bounds  # noqa: E402,F401  (shared with oracle/check_dlrm.py)
