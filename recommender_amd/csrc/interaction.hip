@@ -1081,7 +1081,9 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
           floatx4 v = *reinterpret_cast<const floatx4*>(&X[i * kDxLdx + 4 * r32]);
 #pragma unroll
           for (int c = 0; c < 4; ++c) v[c] = __fmul_rn(G, v[c]);
-          *reinterpret_cast<floatx4*>(de + i * D + 4 * r32) = v;
+          // non-temporal: the 872 MB of rows stream past L2 instead of evicting the Zipf-hot
+          // table rows the gather re-reads (the apply reads them back from HBM either way)
+          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 4 * r32));
         }
       }
       {  // (7) the bottom-MLP row: this lane's two dims d = 4*r32 + 2h + k get G·(U + q_d)

@@ -129,11 +129,13 @@ __device__ __forceinline__ bool key_is(const Cursor& k, const char* s, int n) {
 // TensorProto: dtype must be `want_dtype`, shape [want_n] (or a scalar-free 1-D shape of that
 // size); returns the byte offset of tensor_content (size want_n * elem) in the record, or -1.
 // float_val (5) / int64_val (10) packed forms are accepted too (content offset then marks the
-// packed run; `packed` is set).
-__device__ int parse_tensor(Cursor t, int want_dtype, int want_n, int elem, bool& packed) {
+// packed run and `content_len` its byte length; `packed` is set).
+__device__ int parse_tensor(Cursor t, int want_dtype, int want_n, int elem, bool& packed,
+                            int& content_len) {
   int dtype = -1, content = -1, dims = 0;
   int64_t size = -1;
   packed = false;
+  content_len = 0;
   while (t.ok && t.pos < t.end) {
     const uint64_t tag = rd_varint(t);
     const uint32_t f = (uint32_t)(tag >> 3), wt = (uint32_t)(tag & 7);
@@ -161,12 +163,14 @@ __device__ int parse_tensor(Cursor t, int want_dtype, int want_n, int elem, bool
       const uint64_t n = rd_varint(t);
       if (n != (uint64_t)want_n * elem || n > (uint64_t)(t.end - t.pos)) return -1;
       content = t.pos;
+      content_len = (int)n;
       t.pos += (int)n;
     } else if (((f == 5 && want_dtype == 1) || (f == 10 && want_dtype == 9)) && wt == 2) {
       // float_val (fixed 4-byte values, the tensor_content bytes) / int64_val (varints), packed
       const uint64_t n = rd_varint(t);
       if (n > (uint64_t)(t.end - t.pos) || (f == 5 && n != (uint64_t)want_n * 4)) return -1;
       content = t.pos;
+      content_len = (int)n;
       packed = f == 10;
       t.pos += (int)n;
     } else {
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(256) void tfrecord_criteo_kernel(
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (lane == 0) {
     bool ok = fits;
-    int dense_at = -1, cat_at = -1;
+    int dense_at = -1, cat_at = -1, dense_len = 0, cat_len = 0;
     bool dense_pk = false, cat_pk = false;
     int64_t label = 0;
     bool have_label = false;
@@ -285,10 +289,10 @@ __global__ __launch_bounds__(256) void tfrecord_criteo_kernel(
             }
             if (key_is(key, "int_features", 12)) {
               Cursor t = feature_bytes(val);
-              if (t.ok) dense_at = parse_tensor(t, 1 /*DT_FLOAT*/, o.n_int, 4, dense_pk);
+              if (t.ok) dense_at = parse_tensor(t, 1 /*DT_FLOAT*/, o.n_int, 4, dense_pk, dense_len);
             } else if (key_is(key, "cat_features", 12)) {
               Cursor t = feature_bytes(val);
-              if (t.ok) cat_at = parse_tensor(t, 9 /*DT_INT64*/, o.n_cat, 8, cat_pk);
+              if (t.ok) cat_at = parse_tensor(t, 9 /*DT_INT64*/, o.n_cat, 8, cat_pk, cat_len);
             } else if (key_is(key, "label", 5)) {
               have_label = feature_int64(val, label);
             }
@@ -310,13 +314,16 @@ __global__ __launch_bounds__(256) void tfrecord_criteo_kernel(
     meta[wave][3] = cat_pk ? 1 : 0;
     meta[wave][4] = (int)(label & 0xFFFFFFFF);
     meta[wave][5] = (int)(label >> 32);
-    if (ok && cat_pk) {  // varint-packed int64_val: decode in place into a scratch tail
-      Cursor pk{rec[wave], cat_at, len, true};
+    if (ok && cat_pk) {  // varint-packed int64_val: exactly n_cat varints filling the field
+      Cursor pk{rec[wave], cat_at, cat_at + cat_len, true};
       for (int i = 0; i < o.n_cat; ++i) {
         const int64_t v = (int64_t)rd_varint(pk);
         o.cat[r * o.n_cat + i] = pk.ok ? v : 0;
       }
-      if (!pk.ok) meta[wave][0] = 0;
+      if (!pk.ok || pk.pos != pk.end) {
+        meta[wave][0] = 0;
+        for (int i = 0; i < o.n_cat; ++i) o.cat[r * o.n_cat + i] = 0;
+      }
     }
     if (!meta[wave][0] && err_flag) atomicOr(err_flag, RS_ERRBIT_FORMAT);
   }
@@ -367,7 +374,7 @@ extern "C" int32_t rs_tfrecord_index(const uint8_t* data, int64_t n_bytes, int32
   host_crc_init();
   int64_t pos = 0, n = 0;
   while (pos < n_bytes) {
-    if (n_bytes - pos < 12) {
+    if (n_bytes - pos < 16) {  // length (8) + its CRC (4) + the data CRC (4) at the least
       set_error("truncated TFRecord header at byte %lld", (long long)pos);
       return RS_E_INVALID;
     }
@@ -376,7 +383,7 @@ extern "C" int32_t rs_tfrecord_index(const uint8_t* data, int64_t n_bytes, int32
       set_error("TFRecord length CRC mismatch at byte %lld", (long long)pos);
       return RS_E_INVALID;
     }
-    if (len > (uint64_t)(n_bytes - pos - 16) || len > 0x7FFFFFFFull) {
+    if (len > 0x7FFFFFFFull || (int64_t)len > n_bytes - pos - 16) {
       set_error("TFRecord length %llu at byte %lld runs past the data", (unsigned long long)len,
                 (long long)pos);
       return RS_E_INVALID;

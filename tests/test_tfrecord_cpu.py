@@ -48,3 +48,19 @@ def test_index_rejects_corrupt_framing(rng):
     index_records(np.frombuffer(bytes(bad), np.uint8), verify_crc=False)  # unchecked: framing ok
     with pytest.raises(L.RecsysError):
         index_records(np.frombuffer(bytes(good[:-3]), np.uint8))  # truncated
+
+
+@pytest.mark.parametrize("extra", [0, 1, 2, 3, 4])
+def test_index_rejects_file_cut_after_a_record_header(rng, extra):
+    """A file cut just after a record's 12-byte header (+0..4 bytes): the length and its CRC are
+    intact, so only the bounds check stands between the index and an out-of-range record."""
+    from recommender_amd import _lib as L
+    from recommender_amd.data.tfrecord import index_records
+
+    ints, cats, labels = _arrays(rng, 2)
+    good = bytes(OT.write_records(ints, cats, labels))
+    offs, lens = index_records(np.frombuffer(good, np.uint8))
+    cut = good[: int(offs[1]) + 12 + extra]
+    for verify in (True, False):
+        with pytest.raises(L.RecsysError):
+            index_records(np.frombuffer(cut, np.uint8), verify_crc=verify)

@@ -102,3 +102,24 @@ def test_tsv_to_tfrecord_round_trip(rng, tmp_path):
     assert torch.equal(lab, label.to(torch.int64))
     a, b, c = OT.read_records(out.read_bytes())
     np.testing.assert_array_equal(b, cat.cpu().numpy())
+
+
+def test_packed_int64_val_field_bounds(rng):
+    """cat_features as a varint-packed int64_val (TensorProto field 10): exactly 26 varints are
+    decoded; a run one short (the next field's bytes must not be read as ids) or one long is
+    malformed."""
+    ints, cats, labels = _arrays(rng, 1)
+    shape = F(2, 2, F(2, 2, F(1, 0, V(26))))
+
+    def rec(vals, trailer=b""):
+        t_cat = F(1, 0, V(9)) + shape + F(10, 2, b"".join(V(int(v)) for v in vals)) + trailer
+        feats = (_entry("int_features", F(1, 2, F(1, 2, OT.tensor_proto(ints[0]))))
+                 + _entry("cat_features", F(1, 2, F(1, 2, t_cat)))
+                 + _entry("label", F(3, 2, F(1, 2, V(1)))))
+        return OT.frame(F(1, 2, feats))
+
+    _check(read_tfrecord(rec(cats[0])), ints, cats, np.array([1]))
+    # 25 values followed by an unknown varint field (tag 7): its bytes would decode as ids
+    for bad in (rec(cats[0][:25], F(7, 0, V(5))), rec(list(cats[0]) + [7])):
+        with pytest.raises(ValueError):
+            read_tfrecord(bad)
