@@ -168,12 +168,7 @@ __device__ __forceinline__ void finalize_chunk(const ApplyArgs& a, uint32_t row,
   } else if constexpr (OPT == OPT_SGD) {
     float* t = a.table + (int64_t)row * a.dim + col;
     float w[VEC];
-#ifndef RS_AB_NO_TLOAD
     RowIO<VEC>::load(t, w);
-#else
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) w[e] = 0.f;
-#endif
 #pragma unroll
     for (int e = 0; e < VEC; ++e) w[e] = w[e] - a.p.lr * g[e];
     RowIO<VEC>::store(t, w);

@@ -723,7 +723,6 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
     id_next = raw_id(b + 2);
     // (1) Z = X·Xᵀ (three 16x16 blocks), as inter_fwd_mfma
     floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-#ifndef RS_AB_NO_ZMFMA
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
@@ -733,10 +732,6 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
         c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
       }
     }
-#else
-#pragma unroll
-    for (int t = 0; t < NT; ++t) { c00 += a0[t]; c01 += a1[t]; }
-#endif
     // (2) X(b) → LDS rows 0..27 (rows >= F are zeros and never read back as U)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -795,16 +790,11 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) bv[kk] = X[(4 * kk + g) * kDxLdx + 16 * t + r];
       floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-#ifndef RS_AB_NO_UMFMA
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
       }
-#else
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) { d0[kk & 3] += bv[kk] * sa[0][kk]; d1[kk & 3] += bv[kk] * sa[1][kk]; }
-#endif
       // the U tile overwrites the X tile it was computed from: its values depend on every
       // lane's reads of that tile (through the MFMA), and one wave's LDS operations execute in
       // issue order, so no wait is needed; the next tile's reads touch other columns
@@ -827,9 +817,6 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] = emb ? v[c] : v[c] + qdn[c];  // + the concat pass-through
       float* dst = emb ? de + i * D : hd.dxu_dense + b * D;
-#ifdef RS_AB_NO_USTORE
-      if (v[0] == 12345.f)
-#endif
       *reinterpret_cast<floatx4*>(dst + 4 * r32) = v;
     }
     __builtin_amdgcn_wave_barrier();  // the next example's LDS writes follow these reads
@@ -857,6 +844,43 @@ __global__ __launch_bounds__(256) void dlrm_fwd_dx_pipe(GatherSrc src, int64_t b
 // materialised. Per-wave sums (examples in order) are folded per block in wave order and written
 // as one partial row [kTrainM] per block; rs_dlrm_train_fold folds the blocks in a fixed order.
 // ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// x = h + m + l with h, m, l bf16 (v_cvt_pk_bf16_f32, round to nearest): the two residuals are
+// exact in fp32 and l carries x's bits below 2^-16 |x| to 2^-24 |x|. lo / hi: elements 0-3 / 4-7.
+__device__ __forceinline__ void split3(const floatx4& lo, const floatx4& hi, bf16x8& h, bf16x8& m,
+                                       bf16x8& l) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = j < 4 ? lo[j] : hi[j - 4];
+    h[j] = (__bf16)x;
+    const float r1 = x - (float)h[j];
+    m[j] = (__bf16)r1;
+    l[j] = (__bf16)(r1 - (float)m[j]);
+  }
+}
+
+// c + A·B from the split operands: the six products down to 2^-16 |a||b|, smallest first
+__device__ __forceinline__ floatx4 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                         const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
+                                         floatx4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+// LDS rows of the train kernel (per wave): X(b) [32 rows][kTrLdx] fp32, rows >= F zero, then U
+// in place. Rows 8-15 and 24-31 keep their two 16-column halves swapped, so the U product's
+// transposed reads (lanes of groups g = 0 / 1 read rows j / 8 + j of one column) fall on
+// different banks; 4-column groups stay contiguous and 16-byte aligned.
+constexpr int kTrRows = 32, kTrLdx = 136;
+__device__ __forceinline__ float* tr_at(float* X, int row, int col) {
+  return X + row * kTrLdx + (col ^ (((row >> 3) & 1) << 4));
+}
+
 constexpr int kTrainAtop = 512;                       // A_top (compact row, zero padding)
 constexpr int kTrainNI = 13;                          // bottom-MLP inputs (Criteo dense)
 constexpr int kTrainM = kTrainAtop + 2 + kTrainNI * 128 + 128;  // A_top | s_top | loss | A_bot | s_bot
@@ -874,15 +898,16 @@ struct TrainArgs {
 };
 
 template <bool ID64>
-__global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t batch, int F,
+__global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t batch, int F,
                                                        TrainArgs ta, int epw) {
   constexpr int D = 128, NT = 8;
-  __shared__ __attribute__((aligned(16))) float lds[4][kDxRows * kDxLdx];
+  // per wave: X(b) as fp32 rows [32][kTrLdx] (rows >= F zero), then U in place (tr_at)
+  __shared__ __attribute__((aligned(16))) float lds[4][kTrRows * kTrLdx];
   // lane constants kept in LDS rather than VGPRs (the accumulators need the registers): the q
   // weight of each lane's 12 Z entries (0 where the pair is not kept), and q over the row
   __shared__ __attribute__((aligned(16))) float qlane[64][12];
   __shared__ __attribute__((aligned(16))) float qsh[kTrainAtop];
-  static_assert(kDxRows * kDxLdx >= kTrainM, "per-wave LDS region holds the wave's partial row");
+  static_assert(kTrRows * kTrLdx >= kTrainM, "per-wave LDS region holds the wave's partial row");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
   const int64_t last = first + epw < batch ? first + epw : batch;
@@ -904,16 +929,21 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
     }
   }
-  float sa[2][8];
+  // (M + Mᵀ) as the A operand of the U product on v_mfma_f32_16x16x32_bf16, split in three
+  // bf16 parts: lane (r, g) holds row 16 ib + r, k = 8g + j
+  bf16x8 sa[2][3];
 #pragma unroll
-  for (int ib = 0; ib < 2; ++ib)
+  for (int ib = 0; ib < 2; ++ib) {
+    floatx4 v[2];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int m = 16 * ib + r, k = 4 * kk + g;
-      const bool in = m < F && k < F && m != k;
-      const float v = ta.q[in ? compact_index(m < k ? m : k, m < k ? k : m, F, 0) : 0];
-      sa[ib][kk] = in ? v : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const int m = 16 * ib + r, kk = 8 * g + j;
+      const bool in = m < F && kk < F && m != kk;
+      const float q = ta.q[in ? compact_index(m < kk ? m : kk, m < kk ? kk : m, F, 0) : 0];
+      v[j >> 2][j & 3] = in ? q : 0.f;
     }
+    split3(v[0], v[1], sa[ib][0], sa[ib][1], sa[ib][2]);
+  }
   __syncthreads();
   const float cc = ta.c[0];
   // accumulators (per lane; the loss and s_top are lane-uniform)
@@ -949,6 +979,8 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
     if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
     return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
   };
+  // X(b) in the bf16 MFMA's A/B layout: lane (r, g) holds rows r (a0) and 16 + r (a1), columns
+  // 32s + 8g + 4e + c in a0[2s + e][c] (k-step s of v_mfma_f32_16x16x32_bf16, element 4e + c)
   floatx4 a0[NT], a1[NT];
   floatx4 dn4;
   float xv, lab;
@@ -957,8 +989,8 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
     const float* p1 = shfl_ptr(mine, 16 + r);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      a0[t] = *(gfloatx4*)(p0 + 4 * g + 16 * t);
-      a1[t] = *(gfloatx4*)(p1 + 4 * g + 16 * t);
+      a0[t] = *(gfloatx4*)(p0 + 32 * (t >> 1) + 8 * g + 4 * (t & 1));
+      a1[t] = *(gfloatx4*)(p1 + 32 * (t >> 1) + 8 * g + 4 * (t & 1));
     }
     const int64_t bb = b < last ? b : first;
     dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * r32);
@@ -975,26 +1007,28 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       const int r32 = lanev & 31, h = (lanev >> 5) & 1;
       const float* nxt = row_of(b + 1, id_next);
       id_next = raw_id(b + 2);
-      // (1) Z = X·Xᵀ (three 16x16 blocks)
+      // (1) Z = X·Xᵀ (three 16x16 blocks) on v_mfma_f32_16x16x32_bf16: each fp32 value is
+      // split x = h + m + l into three bf16 (round to nearest, the residuals exact), and the
+      // six products h·h, h·m, m·h, m·m, h·l, l·h are accumulated in fp32 (smallest first) —
+      // the dropped m·l, l·m, l·l terms are below 2^-23 of |x||y|, so each dot product keeps
+      // fp32 accuracy at 6 × 16 instead of 8 × 32 matrix cycles per 32-wide k-step
       floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-#ifndef RS_AB_TRAIN_NO_ZMFMA
-          c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a0[t][c], c00, 0, 0, 0);
-          c01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[t][c], a1[t][c], c01, 0, 0, 0);
-          c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[t][c], a1[t][c], c11, 0, 0, 0);
-#else  // A/B probe (wrong numbers): the Z chain without its MFMAs
-          c00[c] += a0[t][c]; c01[c] += a1[t][c]; c11[c] += a0[t][c] * a1[t][c];
-#endif
-        }
+      for (int s = 0; s < NT / 2; ++s) {
+        bf16x8 h0, m0, l0, h1, m1, l1;
+        split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
+        split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
+        c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
+        c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
+        c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);
       }
-      // (2) X(b) → LDS
+      // (2) X(b) → LDS, all 32 rows (rows >= F are the zero row's zeros: the U product's
+      // k-padding); tr_at swizzles the 16-column halves of rows 8-15 / 24-31
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        *reinterpret_cast<floatx4*>(&X[r * kDxLdx + 16 * t + 4 * g]) = a0[t];
-        if (16 + r < kDxRows) *reinterpret_cast<floatx4*>(&X[(16 + r) * kDxLdx + 16 * t + 4 * g]) = a1[t];
+        const int col = 32 * (t >> 1) + 8 * g + 4 * (t & 1);
+        *reinterpret_cast<floatx4*>(tr_at(X, r, col)) = a0[t];
+        *reinterpret_cast<floatx4*>(tr_at(X, 16 + r, col)) = a1[t];
       }
       const floatx4 dn = dn4;
       float xb[kTrainNI];  // wave-uniform: scalar registers
@@ -1047,28 +1081,24 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
 #pragma unroll
       for (int k = 0; k < 4; ++k) ad[k] += dn[k] * G;
-      // (5) U = (M + Mᵀ)·X per 16-column tile, written back over the tile
+      // (5) U = (M + Mᵀ)·X per 16-column tile on the split MFMA: the B operand (rows 8g + j
+      // of column r) read transposed from the fp32 rows and split like X; the tile is written
+      // back over itself (one wave's LDS operations run in issue order)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        constexpr int KK = kDxRows / 4;
-        float bv[KK];
+        floatx4 xv[2];
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) bv[kk] = X[(4 * kk + g) * kDxLdx + 16 * t + r];
+        for (int jj = 0; jj < 8; ++jj) xv[jj >> 2][jj & 3] = *tr_at(X, 8 * g + jj, 16 * t + r);
+        bf16x8 bh, bm, bl;
+        split3(xv[0], xv[1], bh, bm, bl);
         floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-#ifndef RS_AB_TRAIN_NO_UMFMA
-          d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[0][kk], bv[kk], d0, 0, 0, 0);
-          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[1][kk], bv[kk], d1, 0, 0, 0);
-#else  // A/B probe (wrong numbers): the U tiles without their MFMAs
-          d0[kk & 3] += bv[kk] * sa[0][kk]; d1[kk & 3] += bv[kk] * sa[1][kk];
-#endif
-        }
+        d0 = mfma6(sa[0][0], sa[0][1], sa[0][2], bh, bm, bl, d0);
+        d1 = mfma6(sa[1][0], sa[1][1], sa[1][2], bh, bm, bl, d1);
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
           const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
-          X[i0 * kDxLdx + 16 * t + r] = d0[reg];
-          if (i1 < kDxRows) X[i1 * kDxLdx + 16 * t + r] = d1[reg];
+          *tr_at(X, i0, 16 * t + r) = d0[reg];
+          if (i1 < kDxRows) *tr_at(X, i1, 16 * t + r) = d1[reg];
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -1078,7 +1108,7 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       for (int s2 = 0; s2 < kDxRows / 2; ++s2) {
         const int i = 2 * s2 + h;
         if (i < S) {
-          floatx4 v = *reinterpret_cast<const floatx4*>(&X[i * kDxLdx + 4 * r32]);
+          floatx4 v = *reinterpret_cast<const floatx4*>(tr_at(X, i, 4 * r32));
 #pragma unroll
           for (int c = 0; c < 4; ++c) v[c] = __fmul_rn(G, v[c]);
           // non-temporal: the 872 MB of rows stream past L2 instead of evicting the Zipf-hot
@@ -1088,7 +1118,7 @@ __global__ __launch_bounds__(256) void dlrm_train_pipe(GatherSrc src, int64_t ba
       }
       {  // (7) the bottom-MLP row: this lane's two dims d = 4*r32 + 2h + k get G·(U + q_d)
          // through the bottom chain's relu (h_d > 0); A_bot += x ⊗ g, s_bot += g
-        const floatx4 v = *reinterpret_cast<const floatx4*>(&X[S * kDxLdx + 4 * r32]);
+        const floatx4 v = *reinterpret_cast<const floatx4*>(tr_at(X, S, 4 * r32));
         const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * r32]);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {

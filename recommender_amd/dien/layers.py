@@ -243,10 +243,12 @@ class BatchNormalization(nn.Module):
     def forward(self, x, training=False):
         if training:
             mean = x.mean(0)
-            var = x.var(0, unbiased=False)
+            var = x.var(0, unbiased=False)  # tf.nn.moments: the population variance
             with torch.no_grad():
-                self.moving_mean.mul_(self.momentum).add_(mean.detach() * (1 - self.momentum))
-                self.moving_variance.mul_(self.momentum).add_(var.detach() * (1 - self.momentum))
+                # keras _assign_moving_average: var -= (var - value) * (1 - momentum)
+                decay = 1.0 - self.momentum
+                self.moving_mean.sub_((self.moving_mean - mean.detach()) * decay)
+                self.moving_variance.sub_((self.moving_variance - var.detach()) * decay)
         else:
             mean, var = self.moving_mean, self.moving_variance
         return (x - mean) * torch.rsqrt(var + self.epsilon) * self.gamma + self.beta

@@ -1,8 +1,15 @@
 """dien/model.py surface (reference dien/model.py:7-80): item / category tables with
 mask_zero=True (dien/model.py:11-12), flat embeddings item‖cat (:14-19), BASE (masked history
 mean), DIN (local activation), DIEN (GRU + aux loss, attention, AUGRU; returns
-(prob [B,1], aux [B]); its MLP runs BatchNormalization in inference mode because the
-reference calls self.mlp(embedding) without `training` (dien/model.py:79))."""
+(prob [B,1], aux [B])).
+
+DIEN's head BatchNormalization mode (`head_bn_mode`, parity unpinned): the reference calls
+`self.mlp(embedding)` without `training` (dien/model.py:79) inside a model called with
+training=True (dien/train.py:17). TF 2.2's `Layer.__call__` fills an unpassed `training` from the
+enclosing call's context [3p], so during a train step the head BN normalises by the batch
+statistics and updates its moving averages — "propagate", the default. "inference" is the
+literal reading of the line (moving statistics, no update), kept as the alternative; both are
+tested against oracle/dien.py."""
 from __future__ import annotations
 
 import torch
@@ -59,8 +66,12 @@ class DIN(BaseModel):
 
 
 class DIEN(BaseModel):
-    def __init__(self, interest_extract_gru_units, interest_evolve_gru_units, **kwargs):
+    def __init__(self, interest_extract_gru_units, interest_evolve_gru_units,
+                 head_bn_mode="propagate", **kwargs):
         super().__init__(**kwargs)
+        if head_bn_mode not in ("propagate", "inference"):
+            raise ValueError("head_bn_mode must be 'propagate' or 'inference'")
+        self.head_bn_mode = head_bn_mode
         dev, gen = kwargs.get("device"), kwargs.get("generator")
         D = self.embedding_dim
         self.interest_extract_layer = InterestExtract(interest_extract_gru_units, D, dev, gen)
@@ -82,7 +93,9 @@ class DIEN(BaseModel):
         hidden, aux = self.interest_extract_layer((pos, neg), training, mask)
         score = self.attention((target, hidden), training, mask)
         rep = self.interest_evolve((hidden, score), training, mask)
-        prob = self.mlp(torch.cat([target.squeeze(1), rep], -1))  # inference BN (dien/model.py:79)
+        # dien/model.py:79 passes no `training`: TF 2.2 propagates the call's (head_bn_mode)
+        bn_training = bool(training) and self.head_bn_mode == "propagate"
+        prob = self.mlp(torch.cat([target.squeeze(1), rep], -1), training=bn_training)
         return prob, aux
 
     call = forward

@@ -14,7 +14,7 @@ import torch
 
 from ..functional import binary_crossentropy
 from ..metrics import AUC
-from ..optim import KerasAdam, SparseAdam
+from ..optim import GraphKerasAdam, KerasAdam, SparseAdam, _Workspace, densify_grad
 from . import DIEN, DIN, BaseModel
 
 
@@ -65,6 +65,63 @@ class DIENStep:
         self.opt_dense.step()
         self.opt_sparse.step()
         return total, aux
+
+    # -- graph-capturable step --------------------------------------------------------------
+    def static_step(self, feats, label):
+        """__call__ with no host-side per-step scalars, so it can sit in a HIP graph: the two
+        tables' IndexedSlices gradients densified (densify_grad: the same sort + tiled
+        segmented sum as the sparse apply, no sync) and Keras Adam over every variable with
+        lr_t from device memory (GraphKerasAdam, a variable without a gradient skipped as Keras
+        skips it). Keras' sparse Adam decays m / v and moves every row each step anyway, so the
+        dense step is the same update (tests/test_dien_step_gpu.py: equal to __call__ bit for
+        bit). Its Adam state is its own: do not interleave with __call__."""
+        tables = [self.model.item_embedding, self.model.cat_embedding]
+        if getattr(self, "opt_graph", None) is None:
+            tw = {id(t.weight) for t in tables}
+            self._gdense = [p for p in self.opt_dense.param_groups[0]["params"]
+                            if id(p) not in tw and p.numel() > 0]
+            self.opt_graph = GraphKerasAdam(self._gdense + [t.weight for t in tables],
+                                            lr=self.opt_dense.param_groups[0]["lr"])
+            self._ws = _Workspace()
+        for p in self._gdense:
+            p.grad = None
+        if self.is_dien:
+            pred, aux = self.model(feats, training=True)
+            aux = aux.mean()
+            total = binary_crossentropy(label, pred, reduction="mean") + aux
+        else:
+            pred = self.model(feats, training=True)
+            total = aux = binary_crossentropy(label, pred, reduction="mean")
+        self.last_pred = pred.detach()
+        total.backward()
+        grads = [p.grad for p in self._gdense]  # None: Keras skips the variable
+        for t in tables:
+            got = t.take_grad()
+            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None else None)
+        if not torch.cuda.is_current_stream_capturing():
+            self.opt_graph.prepare()
+            self.opt_graph.iterations += 1
+        self.opt_graph.apply(grads)
+        return total.detach(), aux.detach()
+
+    def capture(self, feats, label):
+        """Record one static_step on (feats, label) — static device tensors the caller refills
+        before each replay — into a HIP graph; returns replay() -> (total, aux). Run at least
+        one eager static_step first (it builds the optimizer state the graph reads)."""
+        opt = self.opt_graph
+        opt.prepare()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self.static_step(feats, label)
+        self._graph = g
+
+        def replay():
+            opt.prepare()
+            g.replay()
+            opt.iterations += 1
+            return out
+        return replay
 
 
 def main(argv=None):

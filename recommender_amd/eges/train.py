@@ -87,7 +87,7 @@ class EGESStep:
         for t in tables:
             got = t.take_grad()
             grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
-                         else torch.zeros_like(t.weight))
+                         else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()
             self.opt_graph.iterations += 1

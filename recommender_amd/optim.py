@@ -435,18 +435,34 @@ class GraphKerasAdam:
 
     @torch.no_grad()
     def apply(self, grads):
-        """One Keras Adam step of every tensor with `grads` (same order); graph-capturable."""
-        parts = []
-        for g, (_, n, pad) in zip(grads, self._segs):
-            parts.append(g.reshape(-1))
-            if pad:
-                parts.append(g.new_zeros(pad))
-        gflat = torch.cat(parts)
+        """One Keras Adam step of every tensor with `grads` (same order); graph-capturable.
+        A None gradient skips its tensor, as Keras' apply_gradients skips a variable without a
+        gradient (no m / v decay, no move); a zero gradient still decays m and v and moves the
+        variable by lr_t·m/(√v + ε). The tensors with gradients are updated in runs of
+        contiguous segments, one rs_keras_adam_flat launch per run."""
         c = keras_adam_coefficients(1, self.lr, self.beta_1, self.beta_2, self.epsilon)
         dev = self.flat.device
-        L.call("rs_keras_adam_flat", L.ptr(self.flat), L.ptr(self.m), L.ptr(self.v),
-               L.ptr(gflat), self.flat.numel(), L.ptr(self._lr), L.ptr(self._idx), c,
-               L.stream_ptr(dev))
+        runs, cur = [], None
+        for i, g in enumerate(grads):
+            if g is None:
+                cur = None
+                continue
+            if cur is None:
+                cur = [i, i]
+                runs.append(cur)
+            cur[1] = i
+        for a, b in runs:
+            parts = []
+            for g, (_, n, pad) in zip(grads[a:b + 1], self._segs[a:b + 1]):
+                parts.append(g.reshape(-1))
+                if pad:
+                    parts.append(g.new_zeros(pad))
+            gflat = torch.cat(parts) if len(parts) > 1 else parts[0].contiguous()
+            o = self._segs[a][0]
+            n = gflat.numel()
+            L.call("rs_keras_adam_flat", L.ptr(self.flat[o:]), L.ptr(self.m[o:]),
+                   L.ptr(self.v[o:]), L.ptr(gflat), n, L.ptr(self._lr), L.ptr(self._idx), c,
+                   L.stream_ptr(dev))
         self._idx.add_(1)
 
 

@@ -96,11 +96,11 @@ class PinSageStep:
         pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
         loss = margin_loss(pos_score, neg_score, 1.0, pos_graph.valid, pos_graph.n_valid)
         loss.backward()
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.dense]
+        grads = [p.grad for p in self.dense]  # None: Keras skips the variable
         for t in tables:
             got = t.take_grad()
             grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
-                         else torch.zeros_like(t.weight))
+                         else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()
             self.opt_graph.iterations += 1  # a capture records the step; replay() counts it
@@ -164,7 +164,7 @@ class PinSageStep:
         """Densify each table's IndexedSlices grad (deterministic segmented sum), bucket it
         with the dense grads into one all-reduce, average over ranks, then apply the tables
         as fully-touched slices (identical to Keras' dense m/v decay for untouched rows)."""
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.dense]
+        grads = [p.grad for p in self.dense]  # None: Keras skips the variable
         tables = self.model.tables()
         dense_tab = []
         for t in tables:

@@ -57,3 +57,25 @@ def assert_close_rel(got, ref, rtol=1e-5, scale=None, msg=""):
 
 
 from oracle.ctr import chain_grad_bounds  # noqa: E402,F401  (shared with oracle/check_dlrm.py)
+
+
+def assert_close_f64(got, ref64, ref32, msg="", rtol=1e-5, noise=4.0, floor=1e-7):
+    """Per-element check of an fp32 result against a float64 evaluation of the same function:
+    |got - ref64| <= rtol·|ref64| + noise·max_k|ref32_k - ref64| + floor·max|ref64|, where the
+    ref32_k (one array or a list) are fp32 evaluations of the reference in different summation
+    orders: their errors, element by element, stand for the rounding any fp32 evaluation order
+    may show there; `floor` bounds the elements where those samples happen to be ~0."""
+    def arr(x):
+        x = x.detach().cpu().numpy() if hasattr(x, "detach") else x
+        return np.asarray(x, np.float64)
+    g, r = arr(got), arr(ref64)
+    samples = ref32 if isinstance(ref32, (list, tuple)) else [ref32]
+    spread = np.max([np.abs(arr(s) - r) for s in samples], axis=0)
+    tol = rtol * np.abs(r) + noise * spread + floor * (np.abs(r).max() if r.size else 0.0)
+    err = np.abs(g - r)
+    bad = ~(err <= tol)
+    if bad.any():
+        i = int(np.flatnonzero(bad.reshape(-1))[0])
+        raise AssertionError(f"{msg}: {int(bad.sum())} / {bad.size} elements off; first at {i}: "
+                             f"got {g.reshape(-1)[i]!r} ref {r.reshape(-1)[i]!r} "
+                             f"(max err/tol {float((err / np.maximum(tol, 1e-300)).max()):.3g})")
