@@ -1,7 +1,8 @@
 """North-star benchmark: Criteo-shaped DLRM train step (fwd + bwd + optimizer) on MI355X.
 
-metric: examples/sec fwd+bwd, Criteo-DLRM 26×40M×128 batch 65536 (BASELINE.json), per GPU
-batch 65 536 (weak scaling over ranks). One step = DLRM forward (bottom MLP, fused gather +
+metric: examples/sec fwd+bwd, Criteo-DLRM 26×40M×128 batch 65536 (BASELINE.json): the global
+batch 65 536 split over the ranks (strong scaling, the metric line); --scaling weak keeps 65 536
+per GPU, and N > 1 also reports the weak-scaling rate as a secondary key. One step = DLRM forward (bottom MLP, fused gather +
 MFMA DotInteraction, top MLP), mean BCE, backward (fused re-gather interaction bwd, MLPs),
 dense SGD and the fused sparse SGD apply on the embedding slab (the reference's DLRM SGD path,
 ctr/train.py:77-79). Inputs are pre-generated on device (no host I/O in the timed region).
@@ -64,7 +65,14 @@ def parse():
     # SURVEY 8(d) timing method: warm-up 10, measure 100 steps (0.1 s of GPU time)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="global batch (strong scaling) or per-GPU batch (--scaling weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the global batch is split over the ranks (the metric's fixed "
+                         "global batch); weak: every rank runs --batch")
+    ap.add_argument("--weak-secondary", type=int, default=1,
+                    help="N > 1, strong scaling: also time --batch per GPU (weak scaling) and "
+                         "report it under weak_scaling")
     ap.add_argument("--rows", type=int, default=40_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--slots", type=int, default=26)
@@ -196,11 +204,11 @@ def barrier(world):
         dist.barrier()
 
 
-def make_pool(args, cards, rank, dev):
+def make_pool(args, cards, rank, dev, batch=None):
     rng = np.random.default_rng([args.seed, rank])
     pool = []
     for _ in range(args.pool):
-        cat, dn, lb = criteo_batch(rng, args.batch, cards)
+        cat, dn, lb = criteo_batch(rng, batch or args.batch, cards)
         pool.append((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
                      torch.from_numpy(lb).to(dev)))
     return pool
@@ -357,6 +365,11 @@ def main():
     if args.pmc and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         traffic, traffic_detail = measure_traffic(args)  # before any GPU initialisation
     world, rank, local = init_dist(args)
+    requested_batch = args.batch
+    if args.scaling == "strong":
+        if args.batch % world:
+            raise SystemExit("strong scaling: --batch must be divisible by the number of ranks")
+        args.batch //= world  # from here on args.batch is the per-GPU batch
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     L.load()
@@ -574,6 +587,28 @@ def main():
                         "traffic = PMC FETCH+WRITE per call; measured_copy_GBs = torch D2D copy_ "
                         "of 4 GiB (read + write bytes / time), the STREAM-copy reference"}
 
+    # N > 1 under strong scaling: the same step at --batch per GPU (weak scaling), for the record
+    weak = None
+    if world > 1 and args.scaling == "strong" and args.weak_secondary:
+        wpool = make_pool(args, cards, rank, dev, batch=requested_batch)
+        for i in range(3):
+            step(wpool[i % len(wpool)])
+        torch.cuda.synchronize()
+        barrier(world)
+        tw0 = time.perf_counter()
+        for i in range(args.steps):
+            step(wpool[i % len(wpool)])
+        torch.cuda.synchronize()
+        barrier(world)
+        tw = time.perf_counter() - tw0
+        tt = torch.tensor([tw], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tw = float(tt.item())
+        weak = {"value": round(requested_batch * world * args.steps / tw, 1), "unit": "examples/sec",
+                "per_gpu_batch": requested_batch, "global_batch": requested_batch * world,
+                "ms_per_step": round(tw / args.steps * 1e3, 3), "steps": args.steps}
+        del wpool
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_steps > 0:
         cpu = cpu_baseline(args, cards)
@@ -583,14 +618,16 @@ def main():
             "metric": "examples/sec fwd+bwd, Criteo-DLRM 26×40M×128 batch 65536, 1/2/4/8 GPU",
             "value": round(value, 1), "unit": "examples/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32",
             "step_ms_distribution": step_dist,
             "data": "synthetic (Criteo-Kaggle-skewed 26-slot slab, bounded Zipf(1.05) ids, seed 4)",
             "config": {"workload": f"dlrm_criteo_{S}x{args.rows}x{D}", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "rows": args.rows, "dim": D, "slots": S,
                        "bottom_mlp": [512, 256, D], "top_mlp": [512, 256, 1],
                        "optimizer": args.optimizer + (" (deferred exact decay)" if materialize_ms is not None else ""),
-                       "parallelism": f"row-sharded slab x{world} (RCCL all-to-all) + dp{world} MLPs" if world > 1 else "single"},
+                       "parallelism": (f"row-sharded slab x{world} (RCCL all-to-all of the unique rows and of their "
+                                       f"gradient rows) + dp{world} MLPs (all-reduce of the fused kernel's "
+                                       f"batch sums)") if world > 1 else "single"},
             "mlp": {"backward": args.mlp_bwd, "forward": args.mlp_fwd,
                     "note": "ctr MLP hidden layers are linear (ctr/layers.py:8), so each MLP is one "
                             "affine map: the composed forward evaluates x·K1·K2·K3 + c as x·(K1K2K3) + c "
@@ -601,6 +638,7 @@ def main():
                     "ms_per_step_layerwise_fwd": layerwise_fwd_ms,
                     "ms_per_step_layerwise_fwd_bwd": layerwise_ms},
             "roofline": roof, "kernels": kern,
+            **({"weak_scaling": weak} if weak is not None else {}),
             "cpu_baseline": cpu, "loss": float(loss.item()),
             **({"keras_materialize_ms": materialize_ms} if materialize_ms is not None else {}),
         }

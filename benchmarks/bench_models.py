@@ -57,6 +57,9 @@ def main():
                          "capacity-shaped sync-free batches, eager (static_step); graph = the same "
                          "step captured once and replayed (PinSageStep.capture), sampling eager; "
                          "graph_all = sampling inside the graph too (capture_with_sampling)")
+    ap.add_argument("--dien-mode", default="graph", choices=["eager", "graph"],
+                    help="dien: eager = DIENStep.__call__; graph = static_step captured once and "
+                         "replayed (DIENStep.capture)")
     ap.add_argument("--eges-mode", default="graph", choices=["eager", "graph"],
                     help="eges: eager = EGESStep.__call__ (SparseAdam keras); graph = static_step "
                          "captured once and replayed (EGESStep.capture)")
@@ -84,9 +87,26 @@ def main():
         for _ in range(4):
             f, lab = synthetic_batch(rng, B, 100, 63001, 801)
             batches.append(({k: torch.from_numpy(v).to(dev) for k, v in f.items()}, torch.from_numpy(lab).to(dev)))
+        if args.dien_mode == "graph":
+            st_f = {k: torch.empty_like(v) for k, v in batches[0][0].items()}
+            st_l = torch.empty_like(batches[0][1])
+            dctr = {"n": 0, "replay": None}
+            train_d = step
+
+            def step(f, lab):
+                for k, v in f.items():
+                    st_f[k].copy_(v)
+                st_l.copy_(lab)
+                dctr["n"] += 1
+                if dctr["n"] == 1:
+                    return train_d.static_step(st_f, st_l)
+                if dctr["replay"] is None:
+                    dctr["replay"] = train_d.capture(st_f, st_l)
+                return dctr["replay"]()
         watch = ["rs_gru_fwd", "rs_gru_bwd", "rs_augru_fwd", "rs_augru_bwd", "rs_dien_attention_fwd",
                  "rs_dien_attention_bwd", "rs_embedding_fwd", "rs_embedding_apply", "rs_keras_adam_dense_sweep"]
-        cfg = {"workload": "dien_amazon_b4096_l100", "batch": B, "hist_len": 100, "gru_units": 36}
+        cfg = {"workload": "dien_amazon_b4096_l100", "batch": B, "hist_len": 100, "gru_units": 36,
+               "mode": args.dien_mode}
     elif args.model in ("mmoe", "esmm"):
         from recommender_amd.esmm import FEAT_VOCAB
         from recommender_amd.esmm.train import MultiTaskStep, build

@@ -780,6 +780,18 @@ int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D, co
                                float eps, int32_t reduction, float* y, float* grad_emb,
                                float* sums, void* workspace, size_t ws_bytes, int32_t* err_flag,
                                void* stream);
+/* The same with dL/dl_b given explicitly (`reduction` 2 is loss_scale = 1/batch, 1 is 1): a
+ * data-parallel rank holding `batch` of a global batch of B examples passes 1/B, so G, the
+ * gradient rows and every batch sum are those of the global mean loss and the ranks' sums
+ * add up to the global ones. */
+int32_t rs_dlrm_train_step_fwd_scaled(const float* table, int64_t n_rows, int32_t D,
+                                      const void* ids, int32_t id_dtype, int32_t n_slots,
+                                      const int64_t* slot_offsets, const float* dense,
+                                      const float* xin, int32_t n_in, const float* label,
+                                      int64_t batch, const float* q, const float* c, float eps,
+                                      float loss_scale, float* y, float* grad_emb, float* sums,
+                                      void* workspace, size_t ws_bytes, int32_t* err_flag,
+                                      void* stream);
 
 /* ---- the production DLRM step's dense tail (ctr/train.py:77-79 SGD of every MLP parameter;
  * ctr/layers.py:5-14 linear hidden layers) ------------------------------------------------

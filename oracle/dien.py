@@ -121,7 +121,7 @@ def dien_params(model, dtype):
             for n, p in model.named_parameters() if not n.endswith("grad_handle")}
 
 
-def dien_forward(model, P, E, mask, mlp_training):
+def dien_forward(model, P, E, mask, mlp_training, bn_stats=None):
     """DIEN.call (dien/model.py:67-80) from parameter leaves P and the flat embeddings
     E = {target [B,1,36], pos [B,L,36], neg [B,L,36]}: InterestExtract (GRU + aux loss),
     DIENAttention, InterestEvolve (AUGRU), concat, MLP (BatchNormalization with batch
@@ -141,7 +141,9 @@ def dien_forward(model, P, E, mask, mlp_training):
     x = torch.cat([E["target"].squeeze(1), rep], -1)
     bn = model.mlp.bn
     stats = None
-    if mlp_training:  # batch statistics; the moving averages after the step [3p keras]
+    if mlp_training and bn_stats is not None:  # given batch statistics, held constant
+        mean, var = (t.to(x.dtype) for t in bn_stats)
+    elif mlp_training:  # batch statistics; the moving averages after the step [3p keras]
         mean, var = x.mean(0), x.var(0, unbiased=False)
         d = 1.0 - bn.momentum
         mm = bn.moving_mean.to(x.dtype)
@@ -157,10 +159,13 @@ def dien_forward(model, P, E, mask, mlp_training):
     return dense_stack(x, layers), aux, stats
 
 
-def dien_step(model, feats, label, dtype=torch.float64, mlp_training=None, perm=None):
+def dien_step(model, feats, label, dtype=torch.float64, mlp_training=None, perm=None,
+              bn_stats=None):
     """One DIEN train step's loss and gradients (dien/train.py:14-22: mean Keras BCE + mean aux,
     gradients of every trainable variable) by torch autograd in `dtype` on copies of the model's
     parameters and of the looked-up table rows. mlp_training None: the model's own setting.
+    bn_stats (optional, (mean, var)): training-mode BN with these statistics held constant
+    (the tests' per-chunk magnitude pass).
     perm (optional, a permutation of the batch): evaluate on the permuted batch and map the
     per-example outputs back — the same function in exact arithmetic, another fp32 rounding
     order (the tests sample the fp32 rounding noise this way).
@@ -169,7 +174,7 @@ def dien_step(model, feats, label, dtype=torch.float64, mlp_training=None, perm=
     if perm is not None:
         inv = torch.argsort(perm)
         out = dien_step(model, {k: v[perm] for k, v in feats.items()}, label[perm], dtype,
-                        mlp_training)
+                        mlp_training, bn_stats=bn_stats)
         out["prob"], out["aux"] = out["prob"][inv], out["aux"][inv]
         for k, r in out["rows"].items():
             B = label.shape[0]
@@ -190,12 +195,49 @@ def dien_step(model, feats, label, dtype=torch.float64, mlp_training=None, perm=
     E = {"target": flat("target_item", "target_cat"), "pos": flat("pos_his_item", "pos_his_cat"),
          "neg": flat("neg_his_item", "neg_his_cat")}
     mask = feats["pos_his_item"] != 0
-    prob, aux, stats = dien_forward(model, P, E, mask, mlp_training)
+    prob, aux, stats = dien_forward(model, P, E, mask, mlp_training, bn_stats)
     loss = keras_bce_mean(label.to(dtype), prob) + aux.mean()
     names = list(P)
     keys = [k for _, k in _LOOKUPS]
     g = torch.autograd.grad(loss, [P[n] for n in names] + [leaves[k] for k in keys])
+    if bn_stats is None and mlp_training:
+        bn_stats = tuple(t.detach() for t in _bn_batch_stats(model, P, E, mask))
     return dict(loss=float(loss.detach()), prob=prob.detach(), aux=aux.detach(),
+                bn_batch=bn_stats,
                 grads=dict(zip(names, g[:len(names)])),
                 rows={k: gr.reshape(-1, gr.shape[-1]) for k, gr in zip(keys, g[len(names):])},
                 stats=stats)
+
+
+def _bn_batch_stats(model, P, E, mask):
+    """The head BN's batch mean / variance of this forward (for the magnitude pass)."""
+    with torch.no_grad():
+        pre = "interest_extract_layer."
+        hidden = gru(E["pos"], P[pre + "gru.kernel"], P[pre + "gru.recurrent_kernel"],
+                     P[pre + "gru.bias"], mask)
+        score = attention(E["target"], hidden, P["attention.kernel"], mask)
+        a = "interest_evolve.augru."
+        rep = augru(hidden, score, P[a + "update_gate.kernel"], P[a + "update_gate.bias"],
+                    P[a + "reset_gate.kernel"], P[a + "reset_gate.bias"],
+                    P[a + "hidden_layer.kernel"], P[a + "hidden_layer.bias"], mask)
+        x = torch.cat([E["target"].squeeze(1), rep], -1)
+        return x.mean(0), x.var(0, unbiased=False)
+
+
+def dien_grad_magnitude(model, feats, label, chunks=16, mlp_training=None, bn_stats=None):
+    """Float64 magnitude of every dense gradient over the batch: Σ_k |g_k| over `chunks`
+    contiguous chunks of the batch, g_k = chunk k's contribution to the batch-mean gradient
+    (BN batch statistics of the whole batch held constant). A reduction over the batch in any
+    fp32 order errs by a small multiple of eps·Σ_k |g_k|; the tests use it as the per-element
+    floor of the dense-gradient check."""
+    B = label.shape[0]
+    c = B // chunks
+    mag = None
+    for k in range(chunks):
+        sl = slice(k * c, (k + 1) * c if k < chunks - 1 else B)
+        n = sl.stop - sl.start
+        out = dien_step(model, {f: v[sl] for f, v in feats.items()}, label[sl], torch.float64,
+                        mlp_training, bn_stats=bn_stats)
+        g = {nm: (t * (n / B)).abs() for nm, t in out["grads"].items()}
+        mag = g if mag is None else {nm: mag[nm] + g[nm] for nm in mag}
+    return mag

@@ -22,8 +22,11 @@ def owner_keys(rows: np.ndarray, n_rows: int, world: int):
     return keys, stride, key_space
 
 
-def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_offsets=None):
-    """Returns the updated full table after one sharded SGD step."""
+def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_offsets=None,
+                     global_grads=False):
+    """Returns the updated full table after one sharded SGD step. global_grads: the rows are
+    gradients of the global mean loss (the fused DLRM step), applied with lr as given;
+    otherwise of each rank's local mean, applied with lr/W."""
     V, D = full_table.shape
     stride = -(-V // world)
     recv = [[] for _ in range(world)]  # recv[o] = list of (local rows, grads) from rank 0..W-1
@@ -38,7 +41,8 @@ def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_o
             sel = (uk // stride) == o
             recv[o].append((uk[sel] - o * stride, ug[sel]))
     out = full_table.copy()
-    lr_w = np.float32(float(np.float32(lr)) / world) if world > 1 else np.float32(lr)
+    lr_w = (np.float32(float(np.float32(lr)) / world) if world > 1 and not global_grads
+            else np.float32(lr))
     for o in range(world):
         local = np.concatenate([x[0] for x in recv[o]])
         grads = np.concatenate([x[1] for x in recv[o]]) if local.size else np.zeros((0, D), np.float32)

@@ -1599,6 +1599,13 @@ extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
   return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
 }
 
+extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
+    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
+    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
+    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
+    float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
+    int32_t* err_flag, void* stream);
+
 extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D,
                                           const void* ids, int32_t id_dtype, int32_t n_slots,
                                           const int64_t* slot_offsets, const float* dense,
@@ -1607,12 +1614,26 @@ extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, in
                                           float eps, int32_t reduction, float* y,
                                           float* grad_emb, float* sums, void* workspace,
                                           size_t ws_bytes, int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(reduction == 1 || reduction == 2, "reduction must be 1 (sum) or 2 (mean)");
+  RS_CHECK_ARG(batch >= 1, "rs_dlrm_train_step_fwd: empty batch");
+  return rs_dlrm_train_step_fwd_scaled(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets,
+                                       dense, xin, n_in, label, batch, q, c, eps,
+                                       reduction == 2 ? 1.f / (float)batch : 1.f, y, grad_emb,
+                                       sums, workspace, ws_bytes, err_flag, stream);
+}
+
+extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
+    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
+    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
+    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
+    float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
+    int32_t* err_flag, void* stream) {
   const int F = n_slots + 1;
   RS_CHECK_ARG(D == 128 && n_slots >= 1 && F <= kDxRows && n_in == kTrainNI && batch >= 1,
                "rs_dlrm_train_step_fwd: needs D = 128, at most %d slots, %d dense inputs",
                kDxRows - 1, kTrainNI);
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
-  RS_CHECK_ARG(reduction == 1 || reduction == 2, "reduction must be 1 (sum) or 2 (mean)");
+  RS_CHECK_ARG(loss_scale > 0.f, "loss_scale must be positive");
   RS_CHECK_ARG(table && ids && dense && xin && label && q && c && y && grad_emb && sums && workspace,
                "null pointer");
   RS_CHECK_ARG(al16(table) && al16(dense) && al16(grad_emb), "table, dense and grad rows must be 16-byte aligned");
@@ -1620,7 +1641,7 @@ extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, in
   hipStream_t st = as_stream(stream);
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
   float* part = static_cast<float*>(workspace);
-  TrainArgs ta{q, c, label, xin, eps, reduction == 2 ? 1.f / (float)batch : 1.f, y, grad_emb, part};
+  TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part};
   int64_t blocks = 0;
   auto go = [&](auto kern) {
     static int epw_cached = 0;

@@ -181,18 +181,28 @@ class TrainStep:
         from .layers import MLP
         from .model import DLRM
 
+        from ..sharded import ShardedSlabEmbedding
+
         m = self.model
-        if not (self.fused_step and isinstance(m, DLRM) and m.compact and not self.sharded
-                and self.opt_sparse.fused and (self.comm is None or self.comm.world == 1)
+        emb = m.embedding_layer
+        # one GPU: the fused side-stream sparse optimizer; row-sharded: the owners' apply inside
+        # the backward exchange, with plain SGD (the gradient rows carry the global 1/(B·W))
+        if self.sharded:
+            sparse_ok = (isinstance(emb, ShardedSlabEmbedding) and isinstance(self.opt_sparse, SparseSGD)
+                         and not callable(self.opt_sparse.lr)
+                         and (self.comm is None or self.comm.world == emb.world))
+        else:
+            sparse_ok = (self.opt_sparse.fused and (self.comm is None or self.comm.world == 1)
+                         and isinstance(emb, Embedding) and emb.weight.data_ptr() % 16 == 0)
+        if not (self.fused_step and isinstance(m, DLRM) and m.compact and sparse_ok
                 and not self.overlap_wgrad and not self.overlap_pgrad
                 and self.loss_reduction in ("mean", "sum") and torch.is_grad_enabled()):
             return False
-        emb = m.embedding_layer
         cat, dense_x, _ = batch
         B = cat.numel() // m.num_cat_fea
         bl, tl = list(m.bottom_mlp.mlp), list(m.top_mlp.mlp)
-        return (isinstance(emb, Embedding) and emb.output_dim == 128 and m.num_cat_fea <= 27
-                and m.num_int_fea == 13 and cat.is_cuda and emb.weight.data_ptr() % 16 == 0
+        return (emb.output_dim == 128 and m.num_cat_fea <= 27
+                and m.num_int_fea == 13 and cat.is_cuda
                 and MLP.factored_backward and MLP.composed_forward and B >= MLP.factored_min_batch
                 and all(l.act_code == 0 for l in bl[:-1] + tl[:-1])
                 and bl[-1].act_code == 1 and tl[-1].act_code == 2
@@ -210,12 +220,18 @@ class TrainStep:
 
             tail = self.dense_tail and dense_tail_ready(self.model, self.opt_dense)
             lr = self.opt_dense.param_groups[0]["lr"] if tail else None
+            comm = self.comm if self.sharded else None
+            if comm is None and self.sharded:
+                comm = self.model.embedding_layer.comm
             y, loss = dlrm_fused_train_forward(self.model, cat, dense_x, label, self.loss_reduction,
-                                               sgd_lr=lr)
+                                               sgd_lr=lr, comm=comm)
             self.last_pred = y
             if not tail:
                 self.opt_dense.step()
-            self.opt_sparse.step()
+            if self.sharded:
+                self.opt_sparse.iterations += 1  # the owners applied inside the exchange
+            else:
+                self.opt_sparse.step()
             return loss
         p = self.model({"cat_features": cat, "int_features": dense_x})
         self.last_pred = p.detach()

@@ -81,7 +81,13 @@ class GRU(nn.Module):
         H = self.units
         self.kernel = nn.Parameter(_glorot((input_dim, 3 * H), dev, self._gen))
         rk = torch.empty(3 * H, H)
-        g = self._gen if (self._gen is not None and self._gen.device.type == "cpu") else None
+        # orthogonal init [3p keras] runs on the host (QR): a CPU generator seeded from the
+        # model's generator, so two models built from equal seeds are equal (the global host RNG
+        # made them differ: the round-2 "DIEN graph step" discrepancy)
+        g = self._gen
+        if g is not None and g.device.type != "cpu":
+            seed = int(torch.randint(0, 2 ** 62, (1,), device=g.device, generator=g).item())
+            g = torch.Generator().manual_seed(seed)
         nn.init.orthogonal_(rk, generator=g)
         self.recurrent_kernel = nn.Parameter(rk.t().contiguous().to(dev))
         self.bias = nn.Parameter(torch.zeros(2, 3 * H, device=dev))

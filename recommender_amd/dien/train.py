@@ -137,6 +137,9 @@ def main(argv=None):
     ap.add_argument("--item_vocab", type=int, default=63001)
     ap.add_argument("--cat_vocab", type=int, default=801)
     ap.add_argument("--steps_per_epoch", type=int, default=50)
+    ap.add_argument("--hip_graph", type=int, default=1,
+                    help="1: the step captured once as a HIP graph (DIENStep.capture) and replayed "
+                         "on each batch; 0: the eager step")
     args = ap.parse_args(argv)
     from ..gemm_tuning import use_tuned_gemms
 
@@ -153,6 +156,7 @@ def main(argv=None):
     step = DIENStep(model)
     rng = np.random.default_rng(args.seed)
     auc = AUC(num_thresholds=20000)  # dien/train.py:43-44
+    static, replay = None, None
     for epoch in range(1, args.epochs + 1):
         t0, tot = time.time(), 0.0
         auc.reset_states()
@@ -161,8 +165,24 @@ def main(argv=None):
                                      args.item_vocab, args.cat_vocab, args.model_type == "DIEN")
             feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
             label = torch.from_numpy(lab).cuda()
-            tot += float(step(feats, label)[0])
-            auc.update_state(label, step.last_pred)
+            if args.hip_graph:
+                # static input buffers refilled per batch; the first step runs eagerly (it builds
+                # the optimizer state), the second captures the graph that later steps replay
+                if static is None:
+                    static = ({k: torch.empty_like(v) for k, v in feats.items()}, torch.empty_like(label))
+                for k, v in feats.items():
+                    static[0][k].copy_(v)
+                static[1].copy_(label)
+                if getattr(step, "opt_graph", None) is None:
+                    out = step.static_step(*static)
+                else:
+                    replay = replay or step.capture(*static)
+                    out = replay()
+                tot += float(out[0])
+                auc.update_state(static[1], step.last_pred)
+            else:
+                tot += float(step(feats, label)[0])
+                auc.update_state(label, step.last_pred)
         torch.cuda.synchronize()
         print(f"epoch {epoch} loss {tot / args.steps_per_epoch:.4f} auc {auc.result():.4f} "
               f"{args.steps_per_epoch * args.train_batch_size / (time.time() - t0):.0f} ex/s")

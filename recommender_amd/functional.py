@@ -330,7 +330,7 @@ _TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
-                             epsilon=1e-7, sgd_lr=None):
+                             epsilon=1e-7, sgd_lr=None, comm=None):
     """The production DLRM train step's forward + loss + backward reductions in one kernel
     (rs_dlrm_train_step_fwd): the reference's DLRM.call (ctr/model.py:45-57) under the mean
     Keras BCE (ctr/train.py:85) with the SGD path's gradients (ctr/train.py:77-79).
@@ -345,13 +345,23 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     maps, all in rs_dlrm_dense_tail (bit-identical to chain_param_grads + torch.optim.SGD +
     the next forward's compositions, in six launches instead of sixteen); the caller then skips
     its dense optimizer step.
+    comm (a recommender_amd.sharded.Comm with a row-sharded ShardedSlabEmbedding): the same step
+    on this rank's share of a global batch of B·W examples — the exchange fetches the batch's
+    unique rows from their owners (side stream, beside the bottom MLP), the kernel reads them by
+    the inverse index with dL/dl_b = 1/(B·W), one all-reduce of the batch sums (≈9 KB) makes every
+    rank's dense tail the global step, and the gradient rows go back to the owners' apply.
     Returns (prediction y [B] (detached), loss scalar tensor (no autograd graph))."""
     from .nn import _composed_forward_hip, chain_param_grads, cached_vec_chain_compose
 
     emb = model.embedding_layer
     S, n_in = model.num_cat_fea, model.num_int_fea
     ids = _ids_flat(cat_features.reshape(-1, S))
-    emb.presort(ids)  # the sort runs beside the bottom MLP and the fused kernel
+    sharded = hasattr(emb, "exchange_begin")
+    world = comm.world if (sharded and comm is not None) else 1
+    if sharded:
+        pending = emb.exchange_begin(ids)  # sort / unique / split sizes beside the bottom MLP
+    else:
+        emb.presort(ids)  # the sort runs beside the bottom MLP and the fused kernel
     x = int_features.reshape(-1, n_in).float().contiguous()
     lab = label.reshape(-1).float().contiguous()
     B = ids.shape[0]
@@ -365,33 +375,56 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
             raise RuntimeError("fused DLRM step: the bottom MLP is not a narrow composed chain")
         h, bks = got
         q, c = cached_vec_chain_compose(tl, rows, width)
-    w = emb.weight
-    D = w.shape[1]
-    dev = w.device
-    _wait_update(emb)
-    # the fused kernel is one round of resident blocks: launched while the sort stream's last
-    # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
-    # kernel 0.42 -> 0.62 ms whenever the two overlap). The sort normally ends first (it runs
-    # beside the previous update, which the kernel waits for anyway), so waiting for it costs
-    # at most its tail.
-    ahead = emb._presorted[1] if getattr(emb, "_presorted", None) else None
-    ready = getattr(ahead, "ready", None)
-    if ready is not None and _TRAIN_WAITS_SORT:
-        torch.cuda.current_stream(dev).wait_event(ready)
+    if sharded:
+        view, inv = emb.exchange_finish(pending)  # this step's unique rows + inverse index
+        w, kid, offs, n_rows = view.weight, inv.reshape(-1, S), None, view.input_dim
+        D = emb.output_dim
+        dev = w.device
+    else:
+        w = emb.weight
+        D = w.shape[1]
+        dev = w.device
+        _wait_update(emb)
+        # the fused kernel is one round of resident blocks: launched while the sort stream's last
+        # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
+        # kernel 0.42 -> 0.62 ms whenever the two overlap). The sort normally ends first (it runs
+        # beside the previous update, which the kernel waits for anyway), so waiting for it costs
+        # at most its tail.
+        ahead = emb._presorted[1] if getattr(emb, "_presorted", None) else None
+        ready = getattr(ahead, "ready", None)
+        if ready is not None and _TRAIN_WAITS_SORT:
+            torch.cuda.current_stream(dev).wait_event(ready)
+        kid, offs, n_rows = ids, emb.slot_offsets, w.shape[0]
     y = torch.empty(B, device=dev, dtype=torch.float32)
     grad = torch.empty(B * S, D, device=dev, dtype=torch.float32)
     M = TRAIN_SUMS_ATOP + 2 + n_in * D + D
     sums = torch.empty(M, device=dev, dtype=torch.float32)
     ws = _train_ws(B, dev)
-    L.call("rs_dlrm_train_step_fwd", L.ptr(w), w.shape[0], D, L.ptr(ids), L.id_dtype_code(ids), S,
-           L.ptr(emb.slot_offsets), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B, L.ptr(q), L.ptr(c),
-           float(epsilon), 2 if reduction == "mean" else 1, L.ptr(y), L.ptr(grad), L.ptr(sums),
-           L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
+    n_global = B * world
+    scale = 1.0 / n_global if reduction == "mean" else 1.0
+    L.call("rs_dlrm_train_step_fwd_scaled", L.ptr(w), n_rows, D, L.ptr(kid), L.id_dtype_code(kid),
+           S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B, L.ptr(q), L.ptr(c),
+           float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums), L.ptr(ws), ws.numel(),
+           L.ptr(emb.err_flag), L.stream_ptr(dev))
+    if world > 1:
+        # the dense half of the global step: every MLP gradient is a linear function of these
+        # batch sums, so one all-reduce of ≈9 KB replaces the all-reduce of ≈3 MB of gradients
+        comm.all_reduce_(sums)
     a = TRAIN_SUMS_ATOP
     A_top, s_top = sums[:a].view(a, 1)[:width], sums[a:a + 1]
     loss_sum = sums[a + 1]
     A_bot = sums[a + 2:a + 2 + n_in * D].view(n_in, D)
     s_bot = sums[a + 2 + n_in * D:]
+    if sharded:
+        # the gradient rows (already of the global mean loss) go to their owners' apply
+        emb.backward_exchange(grad, global_grads=True)
+        if sgd_lr is not None:
+            _dense_tail_sgd(tl, rows, bl, A_top, s_top, sums[a + 2:].view(n_in + 1, D), sgd_lr)
+        else:
+            chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
+            chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
+        loss = loss_sum / n_global if reduction == "mean" else loss_sum
+        return y, loss
     # the sparse update (side stream) is queued right after the kernel. With the presort on its
     # own stream this measured 0.841 vs 0.862 ms/step for queueing it after the top chain's
     # gradients (which was the better order while the presort queued behind the update on the

@@ -218,7 +218,10 @@ class ShardedSlabEmbedding(nn.Module):
         pass
 
     # ---------------------------------------------------------------- backward
-    def backward_exchange(self, grad_rows: torch.Tensor):
+    def backward_exchange(self, grad_rows: torch.Tensor, global_grads: bool = False):
+        """global_grads: the rows are gradients of the GLOBAL mean loss (the fused DLRM step's
+        kernel scales by 1/(B·W)), so the owners apply them as they are; otherwise each rank's
+        rows are of its local mean and the update is scaled 1/W."""
         st = self._st
         if st is None:
             raise RuntimeError("backward without a forward exchange")
@@ -243,7 +246,7 @@ class ShardedSlabEmbedding(nn.Module):
             opt = self.optimizer
             params = opt._params()
             if R:
-                if self.world > 1:
+                if self.world > 1 and not global_grads:
                     if opt.kind == L.RS_OPT_SGD:
                         params.lr = params.lr / self.world  # same as scaling the gradient
                     else:

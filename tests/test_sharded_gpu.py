@@ -135,3 +135,108 @@ def test_world2_sharded_embedding_matches_oracle(opt, even):
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def _fused_dlrm_world2_worker(rank, world, port, q):
+    """The production fused DLRM step over a row-sharded slab, two ranks on the one GPU (gloo):
+    every check is against the oracle on the GLOBAL batch (both ranks' examples)."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sharded as OS
+        from oracle.check_dlrm import _check_chain, _check_sgd, _grads, _layers, dense_half_tolerances
+        from oracle.ctr import DLRMState, dlrm_sgd_step
+        from recommender_amd.ctr.layers import MLP
+        from recommender_amd.ctr.model import DLRM
+        from recommender_amd.ctr.train import TrainStep
+        from recommender_amd.sharded import Comm, ShardedSlabEmbedding
+        from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+        MLP.factored_min_batch = 0
+        S, D, B, lr = 26, 128, 1024, 0.05
+        cards = criteo_cardinalities(200_000, S)
+        V = sum(cards)
+        so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+        table = np.random.default_rng(9).uniform(-0.05, 0.05, (V, D)).astype(np.float32)
+        comm = Comm()
+        emb = ShardedSlabEmbedding(cards, D, comm, device=DEV, full_weight=torch.from_numpy(table))
+        g = torch.Generator(device=DEV)
+        g.manual_seed(3)  # the same MLP init on both ranks
+        model = DLRM([128, 64, D], [128, 64, 1], D, V, S, 13, device=DEV, generator=g,
+                     embedding_layer=emb)
+        step = TrainStep(model, "sgd", lr=lr, comm=comm)
+        per = [criteo_batch(np.random.default_rng(40 + r), B, cards) for r in range(world)]
+        cat, dn, lb = per[rank]
+        assert step.fused_step_ready((torch.from_numpy(cat).to(DEV), None, None))
+        top0, bot0 = _layers(model.top_mlp), _layers(model.bottom_mlp)
+        cap = {}
+        bx = emb.backward_exchange
+
+        def spy(grad_rows, global_grads=False):
+            cap["g"] = grad_rows.detach().clone()
+            assert global_grads
+            return bx(grad_rows, global_grads=global_grads)
+
+        emb.backward_exchange = spy
+        batch = tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb))
+        loss = float(step(batch))
+        emb.join()
+        torch.cuda.synchronize()
+        # both ranks' gradient rows, for the sharded-apply oracle
+        gr = [torch.empty_like(cap["g"].cpu()) for _ in range(world)]
+        dist.all_gather(gr, cap["g"].cpu())
+        want = OS.sharded_sgd_step(table, [p[0] for p in per], [x.numpy() for x in gr], lr, world,
+                                   so, global_grads=True)
+        full = emb.full_weight().cpu().numpy()
+        np.testing.assert_array_equal(full, want)
+        assert (full != table).any(1).sum() > 1000
+        # the dense half and the loss against the oracle step on the global batch
+        st = DLRMState(table.copy(), so, [(k.copy(), b.copy()) for k, b in bot0],
+                       [(k.copy(), b.copy()) for k, b in top0])
+        det = {}
+        gcat = np.concatenate([p[0] for p in per])
+        gdn = np.concatenate([p[1] for p in per])
+        glb = np.concatenate([p[2] for p in per])
+        ref_loss = dlrm_sgd_step(st, gcat, gdn, glb, lr, det)
+        assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
+        top_tol, bot_tol = dense_half_tolerances(det, B * world)
+        _check_chain("top MLP", _grads(model.top_mlp), det["top_grads"], top_tol)
+        _check_chain("bottom MLP", _grads(model.bottom_mlp), det["bottom_grads"], bot_tol)
+        _check_sgd("top MLP", top0, _layers(model.top_mlp), _grads(model.top_mlp), lr)
+        _check_sgd("bottom MLP", bot0, _layers(model.bottom_mlp), _grads(model.bottom_mlp), lr)
+        # this rank's gradient rows against the oracle's rows of its examples
+        dx = det["dx"].reshape(world, B * S, D)[rank]
+        dxb = det["dx_bound"].reshape(world, B * S, D)[rank]
+        err = np.abs(cap["g"].cpu().numpy().astype(np.float64) - dx)
+        assert (err <= 1e-5 * dxb + 1e-38).all(), "gradient rows"
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_fused_dlrm_step_matches_oracle():
+    """TrainStep's fused DLRM step on a row-sharded slab at world 2 (gloo, both ranks on the one
+    GPU): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the batch sums
+    are all-reduced (the dense half of the global step); the owners apply the gradient rows.
+    Slab bit-exact vs oracle/sharded.py fed with both ranks' kernel rows; loss, the twelve MLP
+    gradients (per-element bounds) and the SGD apply vs the oracle step on the global batch."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29300 + (os.getpid() % 500)
+    ps = [ctx.Process(target=_fused_dlrm_world2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res
