@@ -31,7 +31,7 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_train_step_fwd", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
+WATCH = ["rs_dlrm_train_step_fwd", "rs_dlrm_train_step_fwd_scaled", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
          "rs_dlrm_interaction_fwd_head_dx",
          "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids",
          "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
@@ -40,7 +40,7 @@ WATCH = ["rs_dlrm_train_step_fwd", "rs_dlrm_interaction_fwd", "rs_dlrm_interacti
 # launches it: the fused gather + interaction + unit-backward kernel (main stream), the radix
 # sort and the segmented-sum apply (fused optimizer's side stream, co-running with dense GEMMs:
 # their event spans include that co-run time)
-PATH_KERNELS = ("rs_dlrm_train_step_fwd", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
+PATH_KERNELS = ("rs_dlrm_train_step_fwd", "rs_dlrm_train_step_fwd_scaled", "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
                 "rs_dlrm_interaction_fwd_head_dx", "rs_dlrm_interaction_bwd",
                 "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids", "rs_sort_ids_sharded",
                 "rs_embedding_apply", "rs_embedding_apply_scaled")
@@ -236,7 +236,7 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + S * 4 * D + 4 * D)
     if name == "rs_dlrm_interaction_bwd_rank1":  # grad row = G[b] * p: 4 B per example, not 4Z
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 + S * 4 * D + 4 * D)
-    if name == "rs_dlrm_train_step_fwd":  # ids, rows, bottom row, 13 inputs + label in;
+    if name in ("rs_dlrm_train_step_fwd", "rs_dlrm_train_step_fwd_scaled"):  # ids, rows, bottom row, 13 inputs + label in;
         # y and the S gradient rows out (the batch sums are weight-sized)
         return B * (S * id_bytes + S * 4 * D + 4 * D + 13 * 4 + 4 + 4 + S * 4 * D)
     if name == "rs_dlrm_interaction_fwd_head_dx":  # + the unit gradient rows (S + 1 per example)
@@ -555,7 +555,7 @@ def main():
                               "achieved_GBs": round(by / (us * 1e-6) / 1e9, 1),
                               "frac": round(by / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                               "traffic": round(t) if t is not None else None,
-                              "in_step_span_us": kern.get(n_, {}).get("avg_us")}
+                              "in_step_span_us": kern.get(n_, kern.get(n_ + "_scaled", {})).get("avg_us")}
         tsum = sum(v["traffic"] for v in per_kernel.values()) if traffic and all(
             v["traffic"] is not None for v in per_kernel.values()) else None
         dom = max(iso, key=iso.get)
