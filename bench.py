@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the global batch is split over the ranks (the metric's fixed "
                          "global batch); weak: every rank runs --batch")
+    ap.add_argument("--keras-line", type=int, default=1,
+                    help="N = 1, SGD: also time the reference's active optimizer (Keras Adam with "
+                         "the deferred exact decay) on the same model and report it under keras_adam")
     ap.add_argument("--weak-secondary", type=int, default=1,
                     help="N > 1, strong scaling: also time --batch per GPU (weak scaling) and "
                          "report it under weak_scaling")
@@ -140,7 +143,7 @@ def measure_traffic(args):
              args.optimizer, "--pool", str(args.pool), "--seed", str(args.seed), "--fused",
              str(args.fused), "--defer-join", str(args.defer_join), "--mlp-bwd", args.mlp_bwd,
              "--mlp-fwd", args.mlp_fwd, "--compare-layerwise", "0", "--tuned-gemms",
-             str(args.tuned_gemms)]
+             str(args.tuned_gemms), "--keras-line", "0"]
     vals = {}
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -587,6 +590,33 @@ def main():
                         "traffic = PMC FETCH+WRITE per call; measured_copy_GBs = torch D2D copy_ "
                         "of 4 GiB (read + write bytes / time), the STREAM-copy reference"}
 
+    # the reference's active ctr optimizer (ctr/train.py:80,84: Keras Adam on every variable) on
+    # the same model and batches, with the deferred exact decay (bit-identical to the per-step
+    # dense sweep after materialize(); tests/test_northstar_gpu.py), for the record
+    keras = None
+    if world == 1 and args.keras_line and args.optimizer == "sgd" and not args.graph:
+        torch.cuda.synchronize()
+        kstep = TrainStep(model, "keras_adam", lr=1e-3, fused=True, defer_sparse_join=True,
+                          defer_decay=True)
+        for i in range(3):
+            kstep(pool[i % len(pool)])
+        torch.cuda.synchronize()
+        tk0 = time.perf_counter()
+        for i in range(args.steps):
+            kstep(pool[i % len(pool)])
+        torch.cuda.synchronize()
+        tk = time.perf_counter() - tk0
+        tm0 = time.perf_counter()
+        kstep.opt_sparse.materialize()
+        torch.cuda.synchronize()
+        keras = {"value": round(args.batch * args.steps / tk, 1), "unit": "examples/sec",
+                 "ms_per_step": round(tk / args.steps * 1e3, 3), "steps": args.steps,
+                 "optimizer": "keras_adam (deferred exact decay)",
+                 "materialize_ms_after_run": round((time.perf_counter() - tm0) * 1e3, 2),
+                 "fused_step": bool(kstep.fused_step_ready(pool[0]))}
+        del kstep
+        torch.cuda.empty_cache()
+
     # N > 1 under strong scaling: the same step at --batch per GPU (weak scaling), for the record
     weak = None
     if world > 1 and args.scaling == "strong" and args.weak_secondary:
@@ -639,6 +669,7 @@ def main():
                     "ms_per_step_layerwise_fwd_bwd": layerwise_ms},
             "roofline": roof, "kernels": kern,
             **({"weak_scaling": weak} if weak is not None else {}),
+            **({"keras_adam": keras} if keras is not None else {}),
             "cpu_baseline": cpu, "loss": float(loss.item()),
             **({"keras_materialize_ms": materialize_ms} if materialize_ms is not None else {}),
         }

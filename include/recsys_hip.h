@@ -202,8 +202,10 @@ int32_t rs_keras_adam_dense_sweep(float* table, float* m, float* v, int64_t n_ro
  * host's keras_adam_coefficients(s).lr); beta1 / beta2 / epsilon from params.
  * rs_keras_adam_catchup: before step `step` reads its rows, each unique row of sorted_rows
  *   (rs_sort_ids output; entries >= n_rows skipped) replays steps last+1 .. step-1 and is
- *   marked last = step (the step's sparse apply — rs_embedding_apply with RS_OPT_KERAS_ADAM,
- *   no dense sweep — updates it next).
+ *   left at last = step - 1 (the step's sparse apply — rs_embedding_apply with
+ *   RS_OPT_KERAS_ADAM, no dense sweep — updates it next, then rs_keras_adam_mark sets
+ *   last = step; a presort whose apply never runs — a forward-only call, an exception —
+ *   leaves that step to a later replay instead of losing it).
  * rs_keras_adam_materialize: every row replays last+1 .. step; afterwards table / m / v equal
  *   the per-step dense sweep's state bit for bit (same arithmetic per element and step). */
 int32_t rs_keras_adam_catchup(float* table, float* m, float* v, int32_t* last, int64_t n_rows,
@@ -213,6 +215,10 @@ int32_t rs_keras_adam_catchup(float* table, float* m, float* v, int32_t* last, i
 int32_t rs_keras_adam_materialize(float* table, float* m, float* v, int32_t* last, int64_t n_rows,
                                   int32_t dim, const float* lr_hist, int32_t step,
                                   const rs_adam_params* params, void* stream);
+/* After step `step`'s sparse apply: its unique rows (the sorted rows the apply walked) are up
+ * to date through that step, last[row] = step. */
+int32_t rs_keras_adam_mark(int32_t* last, int64_t n_rows, const uint32_t* sorted_rows, int64_t n,
+                           int32_t step, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * a-4 DotInteraction(self_interaction, skip_gather) — ctr/layers.py:17-43.

@@ -217,3 +217,110 @@ def checked_dlrm_sgd_step(model, step, cat, dn, lb, lr, state=None) -> dict:
             "grad_err_over_bound": float((gerr / gtol).max()),
             "top_mlp_grad_err_over_tol": top_ratio, "bottom_mlp_grad_err_over_tol": bot_ratio,
             "frac_elements_changed": changed}
+
+
+def checked_dlrm_keras_step(model, step, cat, dn, lb, state) -> dict:
+    """One production DLRM step with the reference's active optimizer, Keras Adam on every
+    variable (ctr/train.py:80,84: tf.keras.optimizers.Adam(); the table's IndexedSlices through
+    _resource_apply_sparse, i.e. dense m / v decay and a dense var update [3p TF 2.2]), checked
+    against the oracle. `step`: a TrainStep(model, "keras_adam", ...) with a fused SparseAdam,
+    deferred decay or not; `state`: a dict reused across consecutive calls.
+
+    Checks: loss, logits, the table gradient rows and the twelve MLP gradients as
+    checked_dlrm_sgd_step; every MLP parameter = Keras Adam of its own gradient from its own
+    m / v, bit for bit; the table, m and v — after SparseAdam.materialize(), on every row any
+    checked step touched (the only rows with non-zero m / v, so the only rows Keras moves) —
+    BIT-EXACT against the oracle's tiled dedup of the kernel's gradient rows + Keras sparse
+    apply, the oracle carrying those rows' w / m / v across the steps itself."""
+    import torch
+
+    from .embedding import apply_keras_adam, keras_adam_coefficients
+    from .models import keras_adam_torch
+
+    emb = model.embedding_layer
+    opt = step.opt_sparse
+    W = emb.weight
+    dev = W.device
+    V, D = W.shape
+    B, S = cat.shape
+    so = emb.slot_offsets.cpu().numpy() if emb.slot_offsets is not None else None
+    rows = global_rows(cat, V, so).reshape(B, S)
+    assert (rows >= 0).all(), "the checker expects in-range ids"
+    opt.materialize()
+    emb.wait_update_raw()
+    torch.cuda.synchronize()
+    m_t, v_t, _ = opt._slots(emb)
+    union = state.get("rows", np.zeros(0, np.int64))
+    new = np.setdiff1d(np.unique(rows), union)
+    nt = torch.from_numpy(new).to(dev)
+    w_new = W[nt].cpu().numpy()
+    assert not m_t[nt].any() and not v_t[nt].any(), "an unchecked row has Adam state"
+    allr = np.union1d(union, new)
+    wu = np.empty((allr.size, D), np.float32)
+    mu = np.zeros((allr.size, D), np.float32)
+    vu = np.zeros((allr.size, D), np.float32)
+    if union.size:
+        at = np.searchsorted(allr, union)
+        wu[at], mu[at], vu[at] = state["w"], state["m"], state["v"]
+    wu[np.searchsorted(allr, new)] = w_new
+    compact = np.searchsorted(allr, rows).astype(np.int64)
+    dense = [p for l in list(model.top_mlp.mlp) + list(model.bottom_mlp.mlp) for p in (l.kernel, l.bias)]
+    d0 = [p.detach().clone() for p in dense]
+    s0 = [{k: v.detach().clone() for k, v in step.opt_dense.state[p].items()} for p in dense]
+    top0, bot0 = _layers(model.top_mlp), _layers(model.bottom_mlp)
+
+    captured = {}
+    apply = opt.apply
+
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
+        captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
+
+    opt.apply = spy
+    try:
+        batch = (torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
+                 torch.from_numpy(lb).to(dev))
+        loss = float(step(batch).detach())
+    finally:
+        del opt.apply
+    opt.materialize()
+    emb.wait_update_raw()
+    torch.cuda.synchronize()
+    assert "grad_rows" in captured, "the fused sparse apply did not run"
+    g_gpu = captured["grad_rows"].cpu().numpy().reshape(B * S, D)
+    p_gpu = step.last_pred.cpu().numpy().astype(np.float64)
+
+    st = DLRMState(wu.copy(), None, [(k.copy(), b.copy()) for k, b in bot0],
+                   [(k.copy(), b.copy()) for k, b in top0])
+    det: dict = {}
+    ref_loss = dlrm_sgd_step(st, compact, dn, lb, 0.0, det)  # lr 0: the step's gradients only
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), f"loss {loss} vs oracle {ref_loss}"
+    z_ref = det["logit"].astype(np.float64)
+    pc = np.clip(p_gpu, 1e-30, 1 - 1e-7)
+    z_gpu = np.log(pc) - np.log1p(-pc)
+    res = 2 * np.spacing(p_gpu.astype(np.float32)).astype(np.float64) / (pc * (1 - pc))
+    ztol = 1e-5 * np.abs(z_ref) + 1e-6 * det["logit_bound"] + res
+    assert (np.abs(z_gpu - z_ref) <= ztol).all(), "logits"
+    gerr = np.abs(g_gpu.astype(np.float64) - det["dx"])
+    assert (gerr <= 1e-5 * det["dx_bound"] + 1e-38).all(), "grad rows"
+    top_tol, bot_tol = dense_half_tolerances(det, B, step.loss_reduction == "mean")
+    _check_chain("top MLP", _grads(model.top_mlp), det["top_grads"], top_tol)
+    _check_chain("bottom MLP", _grads(model.bottom_mlp), det["bottom_grads"], bot_tol)
+    it = step.opt_dense.iterations
+    c = {k: float(x) for k, x in keras_adam_coefficients(it, step.opt_dense.param_groups[0]["lr"]).items()}
+    for i, (p, p0, sd) in enumerate(zip(dense, d0, s0)):
+        want, _, _ = keras_adam_torch(p0, sd.get("m", torch.zeros_like(p0)),
+                                      sd.get("v", torch.zeros_like(p0)), p.grad, c)
+        assert torch.equal(p.detach(), want), f"MLP parameter {i} is not Keras Adam of its gradient"
+
+    ur, ug = segment_sum_tiled(det["sorted_rows"], det["sorted_pos"], g_gpu, allr.size)
+    co = keras_adam_coefficients(opt.iterations, opt.lr)
+    w2, m2, v2 = apply_keras_adam(wu, mu, vu, ur.astype(np.int64), ug, co)
+    at = torch.from_numpy(allr).to(dev)
+    for name, got, want in (("table", W[at], w2), ("m", m_t[at], m2), ("v", v_t[at], v2)):
+        g = got.cpu().numpy()
+        bad = (g != want).any(1)
+        assert not bad.any(), f"{name}: {int(bad.sum())} of {allr.size} rows differ from the oracle"
+    state.update(rows=allr, w=w2, m=m2, v=v2)
+    return {"loss": loss, "oracle_loss": ref_loss, "rows_checked": int(allr.size),
+            "step": int(opt.iterations), "rows_beyond_2^32_elems": int((allr * D >= (1 << 32)).sum())}

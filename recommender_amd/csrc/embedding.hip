@@ -886,7 +886,20 @@ __global__ __launch_bounds__(256) void keras_catchup_kernel(
     const int32_t l0 = last[r];
     if (l0 + 1 <= step - 1)
       keras_replay_row<VEC>(w, m, v, r, dim, gl, lpr, l0 + 1, step - 1, lr_hist, b1, b2, eps);
-    if (gl == 0) last[r] = step;  // claimed: the step's sparse apply updates the row next
+    // caught up through step - 1; the step's sparse apply marks it step once it ran
+    // (rs_keras_adam_mark), so a presort whose apply never runs leaves the step to a replay
+    if (gl == 0) last[r] = step - 1;
+  }
+}
+
+// after the sparse apply of step s: its unique rows are now up to date through s
+__global__ __launch_bounds__(256) void keras_mark_kernel(int32_t* __restrict__ last, uint32_t n_rows,
+                                                          const uint32_t* __restrict__ rows,
+                                                          int64_t n, int32_t step) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rows[i];
+    if (r < n_rows && (i == 0 || rows[i - 1] != r)) last[r] = step;
   }
 }
 
@@ -1171,6 +1184,16 @@ extern "C" int32_t rs_keras_adam_catchup(float* table, float* m, float* v, int32
     case 2: keras_catchup_kernel<2><<<blocks, 256, 0, st>>>(table, m, v, last, (uint32_t)n_rows, dim, rows, n, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
     default: keras_catchup_kernel<1><<<blocks, 256, 0, st>>>(table, m, v, last, (uint32_t)n_rows, dim, rows, n, lr_hist, step, p.beta1, p.beta2, p.epsilon, l2); break;
   }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_keras_adam_mark(int32_t* last, int64_t n_rows, const uint32_t* sorted_rows,
+                                      int64_t n, int32_t step, void* stream) {
+  RS_CHECK_ARG(last && (n == 0 || sorted_rows) && n >= 0 && n_rows > 0, "bad arguments");
+  if (n == 0) return RS_OK;
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+  keras_mark_kernel<<<blocks, 256, 0, as_stream(stream)>>>(last, (uint32_t)n_rows, sorted_rows, n, step);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -39,7 +39,7 @@ class TrainStep:
         """comm: a recommender_amd.sharded.Comm for data-parallel dense parameters (gradients
         all-reduced and averaged over ranks); with a ShardedSlabEmbedding the table is updated
         by its owners inside the backward.
-        fused_step: the production DLRM step (D = 128, composed / factored MLP chains, fused
+        fused_step: the production DLRM step (D = 128 or 64, composed / factored MLP chains, fused
         sparse optimizer, one GPU) runs its forward, loss and backward reductions in one kernel
         (functional.dlrm_fused_train_forward) instead of autograd over the fused interaction;
         other configurations take the autograd path.
@@ -201,7 +201,7 @@ class TrainStep:
         cat, dense_x, _ = batch
         B = cat.numel() // m.num_cat_fea
         bl, tl = list(m.bottom_mlp.mlp), list(m.top_mlp.mlp)
-        return (emb.output_dim == 128 and m.num_cat_fea <= 27
+        return (emb.output_dim in (64, 128) and m.num_cat_fea <= 27
                 and m.num_int_fea == 13 and cat.is_cuda
                 and MLP.factored_backward and MLP.composed_forward and B >= MLP.factored_min_batch
                 and all(l.act_code == 0 for l in bl[:-1] + tl[:-1])

@@ -215,6 +215,10 @@ class SparseOptimizer:
         if self.kind == L.RS_OPT_KERAS_ADAM and not getattr(self, "defer_decay", False):
             L.call("rs_keras_adam_dense_sweep", L.ptr(table.weight), L.ptr(m), L.ptr(v),
                    table.input_dim, table.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
+        elif getattr(self, "defer_decay", False):
+            # the step's rows are now current through it (the catch-up left them one behind)
+            L.call("rs_keras_adam_mark", L.ptr(self.last[id(table)]), table.input_dim,
+                   L.ptr(s.rows), s.n, self.iterations + 1, L.stream_ptr(dev))
 
     def step(self):
         applied = set()

@@ -27,12 +27,13 @@ def factored_any_batch():
 
 def _model(cards, seed, bottom, top):
     g = torch.Generator(device=DEV).manual_seed(seed)
-    return build_model("DLRM", 128, sum(cards), 26, 13, torch.device(DEV), slot_cardinalities=cards,
-                       bottom=bottom, top=top, generator=g)
+    return build_model("DLRM", bottom[-1], sum(cards), 26, 13, torch.device(DEV),
+                       slot_cardinalities=cards, bottom=bottom, top=top, generator=g)
 
 
 @pytest.mark.parametrize("reduction", ["mean", "sum"])
-@pytest.mark.parametrize("bottom,top", [([64, 128], [64, 32, 1]), ([512, 256, 128], [512, 256, 1])])
+@pytest.mark.parametrize("bottom,top", [([64, 128], [64, 32, 1]), ([512, 256, 128], [512, 256, 1]),
+                                        ([512, 256, 64], [512, 256, 1])])
 def test_fused_step_matches_autograd_path(factored_any_batch, reduction, bottom, top):
     cards = criteo_cardinalities(300_000, 26)
     rng = np.random.default_rng(11)
@@ -199,3 +200,33 @@ def test_dense_tail_bit_identical(factored_any_batch, bottom, top):
     for (n, p), q in zip(mt.named_parameters(), mr.parameters()):
         assert torch.equal(p, q), n
     assert torch.equal(mt.embedding_layer.weight, mr.embedding_layer.weight)
+
+
+def test_keras_deferred_decay_presort_without_step(factored_any_batch):
+    """A presort whose step never runs (a forward-only call under grad) must not make its rows
+    skip that step's Keras decay: steps 1, 2, a forward-only call on a batch with other rows,
+    step 3, then materialize() — table / m / v bit-identical to the per-step dense sweep."""
+    cards = criteo_cardinalities(50_000, 26)
+    rng = np.random.default_rng(23)
+    batches = [tuple(torch.from_numpy(x).to(DEV) for x in criteo_batch(rng, 1024, cards))
+               for _ in range(4)]
+    runs = []
+    for defer in (False, True):
+        m = _model(cards, 6, [128, 64, 128], [128, 64, 1])
+        st = TrainStep(m, "keras_adam", lr=1e-2, defer_sparse_join=True, defer_decay=defer)
+        st(batches[0])
+        st(batches[1])
+        if defer:  # the forward alone: presort + catch-up of batch 3's rows, no apply
+            cat = batches[3][0]
+            m.embedding_layer.presort(cat.reshape(-1, 26).contiguous())
+        st(batches[2])
+        emb = m.embedding_layer
+        if defer:
+            st.opt_sparse.materialize()
+        emb.wait_update_raw()
+        torch.cuda.synchronize()
+        mm, vv, _ = st.opt_sparse._slots(emb)
+        runs.append((emb.weight.clone(), mm.clone(), vv.clone()))
+    (w0, m0, v0), (w1, m1, v1) = runs
+    assert torch.equal(m0, m1) and torch.equal(v0, v1)
+    assert torch.equal(w0, w1)

@@ -114,3 +114,36 @@ def test_dense_half_check_trips_on_perturbed_sum(monkeypatch):
     with pytest.raises(AssertionError, match="top MLP layer"):
         checked_dlrm_sgd_step(model, step, cat, dn, lb, lr, state)
     assert calls, "the production step did not run the dense tail"
+
+
+@pytest.mark.timeout(900)
+def test_northstar_keras_adam_deferred_decay():
+    """The reference's active ctr optimizer (ctr/train.py:80,84: Keras Adam on every variable)
+    at full north-star size, with the deferred exact decay: three checked steps
+    (oracle/check_dlrm.py checked_dlrm_keras_step: every row the steps touched bit-exact in
+    table / m / v after materialize(), MLP Keras Adam of its own gradients bit for bit)."""
+    from oracle.check_dlrm import checked_dlrm_keras_step
+    from recommender_amd.ctr.train import TrainStep, build_model
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    S, D, B, V = 26, 128, 65536, 40_000_000
+    dev = torch.device(DEV)
+    cards = criteo_cardinalities(V, S)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    model = build_model("DLRM", D, V, S, 13, dev, slot_cardinalities=cards,
+                        bottom=[512, 256, D], top=[512, 256, 1], generator=g)
+    step = TrainStep(model, "keras_adam", lr=1e-3, fused=True, defer_sparse_join=True,
+                     defer_decay=True)
+    assert step.fused_step_ready((torch.zeros(B, S, dtype=torch.int64, device=dev), None, None))
+    rng = np.random.default_rng(4)
+    state = {}
+    try:
+        for it in range(3):
+            cat, dn, lb = criteo_batch(rng, B, cards)
+            r = checked_dlrm_keras_step(model, step, cat, dn, lb, state)
+            print(f"keras step {it}: {r}")
+            assert r["rows_beyond_2^32_elems"] > 0
+    finally:
+        del step, model
+        torch.cuda.empty_cache()
