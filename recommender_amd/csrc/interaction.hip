@@ -848,15 +848,23 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // x = h + m + l with h, m, l bf16 (v_cvt_pk_bf16_f32, round to nearest): the two residuals are
 // exact in fp32 and l carries x's bits below 2^-16 |x| to 2^-24 |x|. lo / hi: elements 0-3 / 4-7.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split3(const floatx4& lo, const floatx4& hi, bf16x8& h, bf16x8& m,
                                        bf16x8& l) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float x = j < 4 ? lo[j] : hi[j - 4];
-    h[j] = (__bf16)x;
-    const float r1 = x - (float)h[j];
-    m[j] = (__bf16)r1;
-    l[j] = (__bf16)(r1 - (float)m[j]);
+  for (int j = 0; j < 4; ++j) {  // in pairs: one v_cvt_pk_bf16_f32 and one v_pk_add_f32 each
+    const floatx2 x = j < 2 ? floatx2{lo[2 * j], lo[2 * j + 1]} : floatx2{hi[2 * j - 4], hi[2 * j - 3]};
+    const bf16x2 hp = __builtin_convertvector(x, bf16x2);
+    const floatx2 r1 = x - __builtin_convertvector(hp, floatx2);
+    const bf16x2 mp = __builtin_convertvector(r1, bf16x2);
+    const bf16x2 lp = __builtin_convertvector(r1 - __builtin_convertvector(mp, floatx2), bf16x2);
+    h[2 * j] = hp[0];
+    h[2 * j + 1] = hp[1];
+    m[2 * j] = mp[0];
+    m[2 * j + 1] = mp[1];
+    l[2 * j] = lp[0];
+    l[2 * j + 1] = lp[1];
   }
 }
 
@@ -1109,7 +1117,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t
         for (int reg = 0; reg < 4; ++reg) {
           const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
           *tr_at<D>(X, i0, 16 * t + r) = d0[reg];
-          if (i1 < kDxRows) *tr_at<D>(X, i1, 16 * t + r) = d1[reg];
+          *tr_at<D>(X, i1, 16 * t + r) = d1[reg];  // rows 28-31: never read
         }
       }
       __builtin_amdgcn_wave_barrier();
