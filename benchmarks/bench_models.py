@@ -63,6 +63,10 @@ def main():
     ap.add_argument("--eges-mode", default="graph", choices=["eager", "graph"],
                     help="eges: eager = EGESStep.__call__ (SparseAdam keras); graph = static_step "
                          "captured once and replayed (EGESStep.capture)")
+    ap.add_argument("--cfg2-graph", type=int, default=0,
+                    help="dlrm_cfg2 (sgd): 1 = each step a HIP-graph replay (TrainStep.capture); "
+                         "2 = the 4-batch pool as one graph (TrainStep.capture_sequence, updates "
+                         "overlapped across steps), timed per step")
     ap.add_argument("--tuned-gemms", type=int, default=-1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
                          "-1 (default): on for the fixed-shape models (dien, esmm, mmoe), off for the "
@@ -209,10 +213,31 @@ def main():
             batches.append(((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
                              torch.from_numpy(lb).to(dev)),))
         step = step0
-        watch = ["rs_dlrm_interaction_fwd", "rs_dlrm_interaction_bwd", "rs_sort_ids",
-                 "rs_embedding_apply", "rs_keras_adam_dense_sweep"]
+        if args.cfg2_graph and args.optimizer == "sgd":
+            for b in batches:  # eager warm-up (compositions, caches) before capture
+                step0(*b)
+            if args.cfg2_graph == 1:
+                reps = [step0.capture(*b) for b in batches]
+                gc = {"n": 0}
+
+                def step(_):
+                    r = reps[gc["n"] % len(reps)]
+                    gc["n"] += 1
+                    return r()
+            else:
+                seq = step0.capture_sequence([b[0] for b in batches])
+                B_pool = len(batches)
+                batches = [(None,)]
+                args.steps = max(1, args.steps // B_pool)
+                args.warmup = max(1, args.warmup // B_pool)
+
+                def step(_):
+                    return seq()
+        watch = ["rs_dlrm_train_step_fwd_scaled", "rs_sort_ids", "rs_embedding_apply",
+                 "rs_dlrm_dense_tail", "rs_keras_adam_dense_sweep"]
         cfg = {"workload": f"dlrm_criteo_26x{per}x{D}_b{B}", "batch": B, "rows": per * S,
-               "slab_GB": round(per * S * D * 4 / 1e9, 1), "optimizer": args.optimizer}
+               "slab_GB": round(per * S * D * 4 / 1e9, 1), "optimizer": args.optimizer,
+               "graph": args.cfg2_graph if args.optimizer == "sgd" else 0}
     else:
         from recommender_amd.ctr.train import TrainStep, build_model
         from recommender_amd.synthetic import criteo_batch
@@ -229,6 +254,8 @@ def main():
                  "rs_keras_adam_dense_sweep"]
         cfg = {"workload": "deepfm_criteo_1M_b1024_d16", "batch": B, "optimizer": "keras_adam"}
     sec, k = run(step, batches, args.steps, args.warmup, watch)
+    if args.model == "dlrm_cfg2" and args.cfg2_graph == 2 and args.optimizer == "sgd":
+        sec /= B_pool  # one replay = the whole pool of steps
     out = {"model": args.model, "examples_per_sec": round(B / sec, 1),
            "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k}
     if args.model == "deepfm":

@@ -316,3 +316,48 @@ def test_graph_replay_then_eager_matches_eager_only():
         assert torch.equal(models[0].embedding_layer.weight, models[1].embedding_layer.weight)
     finally:
         MLP.factored_min_batch = old
+
+
+@pytest.mark.parametrize("D", [128, 64])
+def test_graph_sequence_matches_eager_fused_step(D):
+    """The graph modes of benchmarks/bench_models.py --cfg2-graph: a pool of fused DLRM steps
+    captured as ONE graph (TrainStep.capture_sequence: each step's sparse update on its side
+    stream overlaps the next step's bottom MLP inside the graph) and replayed twice leaves the
+    slab and every MLP parameter bit-identical to the same steps run eagerly, at D = 128 (the
+    north star) and D = 64 (cfg2)."""
+    from recommender_amd.ctr.layers import MLP
+    from recommender_amd.ctr.train import TrainStep, build_model
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    old = MLP.factored_min_batch
+    MLP.factored_min_batch = 0
+    try:
+        cards = criteo_cardinalities(100_000, 26)
+        rng = np.random.default_rng(11)
+        bs = []
+        for _ in range(3):
+            cat, dn, lb = criteo_batch(rng, 1024, cards)
+            bs.append(tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb)))
+        models = []
+        for mode in ("graph", "eager"):
+            g = torch.Generator(device=DEV).manual_seed(7)
+            m = build_model("DLRM", D, sum(cards), 26, 13, torch.device(DEV), slot_cardinalities=cards,
+                            bottom=[64, D], top=[64, 32, 1], generator=g)
+            st = TrainStep(m, "sgd", lr=0.05, fused=True, defer_sparse_join=True)
+            assert st.fused_step_ready(bs[0])
+            if mode == "graph":
+                replay = st.capture_sequence(bs, warmup=1)   # 1 eager pass over the pool
+                replay()
+                replay()
+            else:
+                for b in bs * 3:
+                    st(b)
+            m.embedding_layer.wait_update()
+            torch.cuda.synchronize()
+            models.append(m)
+        pa, pb = dict(models[0].named_parameters()), dict(models[1].named_parameters())
+        for n in pa:
+            assert torch.equal(pa[n], pb[n]), n
+        assert torch.equal(models[0].embedding_layer.weight, models[1].embedding_layer.weight)
+    finally:
+        MLP.factored_min_batch = old
