@@ -49,6 +49,7 @@ class Embedding(nn.Module):
         self._presorted = None
         # sorts queued ahead for later steps (Embedding.prefetch), keyed by the ids' storage
         self._prefetched: dict = {}
+        self._prefetch_queue: list = []  # prefetched ids whose sort is not launched yet
         # deferred join (SparseOptimizer(defer_join=True)): the event the next table read waits on
         self._pending_update = None
         # deferred-decay Keras Adam: the step this table's rows were last caught up for
@@ -97,7 +98,22 @@ class Embedding(nn.Module):
         if opt is None or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing():
             return
         key = self._ids_key(ids)
-        if key not in self._prefetched:
+        if key in self._prefetched or any(self._ids_key(q) == key for q in self._prefetch_queue):
+            return
+        self._prefetch_queue.append(ids)
+        if not opt.prefetch_after_kernel:
+            self.flush_prefetch()
+
+    def flush_prefetch(self):
+        """Launch the sorts Embedding.prefetch queued. The fused DLRM step calls this right
+        after its train kernel, so the next batch's sort runs beside this step's sparse update
+        and dense tail (the train kernel's resident grid leaves no CU slots for it, and a sort
+        queued at the next step's start would delay that step's kernel); presort() calls it too,
+        when the queue holds its own ids, so a queued sort is never lost."""
+        q, self._prefetch_queue = self._prefetch_queue, []
+        opt = self.fused_optimizer
+        for ids in q:
+            key = self._ids_key(ids)
             if len(self._prefetched) >= 4:  # stale entries (steps that never ran)
                 self._prefetched.pop(next(iter(self._prefetched)))
             # the entry holds the ids (their storage cannot be reused while it waits) and their
@@ -110,6 +126,9 @@ class Embedding(nn.Module):
         GPU is busy with the forward, and the sort runs beside it. The lookup's backward reuses
         it (or sorts on the spot when no presort was issued)."""
         if self.fused_optimizer is not None and torch.is_grad_enabled():
+            if self._prefetch_queue and any(self._ids_key(q) == self._ids_key(ids)
+                                            for q in self._prefetch_queue):
+                self.flush_prefetch()  # this step's own ids were queued but not sorted yet
             e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
             ahead = e[2] if e is not None and e[1] == ids._version else None
             opt = self.fused_optimizer

@@ -406,6 +406,8 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
            S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B, L.ptr(q), L.ptr(c),
            float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums), L.ptr(ws), ws.numel(),
            L.ptr(emb.err_flag), L.stream_ptr(dev))
+    if not sharded and emb._prefetch_queue:
+        emb.flush_prefetch()  # a later batch's sort, beside this step's update and dense tail
     if world > 1:
         # the dense half of the global step: every MLP gradient is a linear function of these
         # batch sums, so one all-reduce of ≈9 KB replaces the all-reduce of ≈3 MB of gradients

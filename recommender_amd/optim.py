@@ -133,11 +133,16 @@ class SparseOptimizer:
         # stream (north star with the early apply: 0.862 -> 0.841 ms/step; RS_PRESORT_STREAM=0
         # restores the side-stream presort)
         self.presort_own_stream = os.environ.get("RS_PRESORT_STREAM", "1") == "1"
+        # Embedding.prefetch: launch the later batch's sort right after the current step's train
+        # kernel (Embedding.flush_prefetch) instead of at the prefetch call
+        self.prefetch_after_kernel = os.environ.get("RS_PREFETCH_AFTER_KERNEL", "1") == "1"
         if fused:
             dev = self.tables[0].weight.device
             self.side = torch.cuda.Stream(device=dev)
             for t in self.tables:
                 t.fused_optimizer = self
+                # sorts another optimizer prefetched belong to its streams and scratch
+                t._prefetched, t._prefetch_queue, t._presorted = {}, [], None
 
     # ---- fused path ----
     def sort_async(self, table: Embedding, ids: torch.Tensor) -> SortedIds:
