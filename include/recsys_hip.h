@@ -337,6 +337,34 @@ int32_t rs_dien_attention_bwd(const float* hs, const float* q, const float* a, c
  *      element written) and dparams = [dW1 | db1 | dW2 | db2 | dW3 | db3] (overwritten,
  *      deterministic); workspace ≥ rs_dien_aux_workspace_size(B, L, H, E) bytes. */
 size_t rs_dien_aux_workspace_size(int64_t B, int32_t L, int32_t H, int32_t E);
+/* a-9 / a-11 the B·L-row products around the recurrences, on the valid (mask != 0) rows only
+ *      (replace the library GEMMs over all B·L rows: dien/layers.py:79,131,161-204 via
+ *      keras GRU / RNN(AUGRUCell); a masked step carries the state, so its projection is never
+ *      read and its gradient rows are 0).
+ *      rs_valid_rows: idx [R] (the valid rows in order, first *count entries), count [1] int32
+ *        on the device; workspace >= rs_valid_rows_workspace_size(R) bytes.
+ *      rs_masked_proj: y[r, :N] = x[r, :K]·W [K,N] + bias[N] (bias may be NULL) for the listed
+ *        rows; other rows of y untouched. K <= 64, N <= 192.
+ *      rs_masked_dx: dx[r, :K] = d[r, :N]·Wᵀ (W [K,N]) for the listed rows (idx / count of
+ *        rs_valid_rows over the same mask), 0 for the rows with mask == 0 (all R rows written).
+ *      rs_masked_wgrad: C [K,N] = Σ_listed A_rᵀ·D[r, :N] and sums [N] = Σ_listed D[r] (may be
+ *        NULL); A_r = A row r, or with shift_L > 0 row r - 1 and zeros where r % shift_L == 0
+ *        (the previous step's state). Fixed row chunks, folded in order: deterministic.
+ *        workspace >= rs_masked_wgrad_workspace_size(K, N) bytes. */
+size_t rs_valid_rows_workspace_size(int64_t R);
+int32_t rs_valid_rows(const uint8_t* mask, int64_t R, int32_t* idx, int32_t* count,
+                      void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_masked_proj(const float* x, int64_t ldx, const float* W, const float* bias,
+                       const int32_t* idx, const int32_t* count, int64_t R, int32_t K, int32_t N,
+                       float* y, int64_t ldy, void* stream);
+int32_t rs_masked_dx(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
+                     const int32_t* idx, const int32_t* count, int64_t R, int32_t K, int32_t N,
+                     float* dx, int64_t lddx, void* stream);
+size_t rs_masked_wgrad_workspace_size(int32_t K, int32_t N);
+int32_t rs_masked_wgrad(const float* A, int64_t lda, int32_t shift_L, const float* D, int64_t ldd,
+                        const int32_t* idx, const int32_t* count, int32_t K, int32_t N, float* C,
+                        float* sums, void* workspace, size_t ws_bytes, void* stream);
+
 int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const float* neg,
                         const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                         const float* W1, const float* b1, const float* W2, const float* b2,

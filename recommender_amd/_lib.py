@@ -91,6 +91,12 @@ _SIGS = {
     "rs_dien_attention_fwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p]),
     "rs_dien_attention_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_dien_aux_workspace_size": (_sz, [_i64, _i32, _i32, _i32]),
+    "rs_valid_rows_workspace_size": (_sz, [_i64]),
+    "rs_valid_rows": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
+    "rs_masked_proj": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "rs_masked_dx": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "rs_masked_wgrad_workspace_size": (_sz, [_i32, _i32]),
+    "rs_masked_wgrad": (_i32, [_p, _i64, _i32, _p, _i64, _p, _p, _i32, _i32, _p, _p, _p, _sz, _p]),
     "rs_dien_aux_fwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                _p, _p]),
     "rs_dien_aux_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,

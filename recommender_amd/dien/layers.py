@@ -31,23 +31,104 @@ def _mask_u8(mask, shape, device):
 
 
 # ---------------------------------------------------------------------------------------------
+# The B·L-row products around the recurrences on the valid (mask != 0) steps only
+# (csrc/dien_proj.hip): a masked step carries the state, so its input projection is never read
+# and its gradient rows are exactly 0 — the library GEMMs over all B·L rows spent ≈1 ms of the
+# cfg3 step on them. Widths beyond the kernels' (input > 64) keep the GEMMs.
+_proj_ws: dict = {}
+
+
+def _ws(name, nbytes, dev):
+    key = (name, dev)
+    b = _proj_ws.get(key)
+    if b is None or b.numel() < nbytes:
+        b = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+        _proj_ws[key] = b
+    return b
+
+
+def _rows_ready(X, H):
+    return X <= 64 and H <= 64
+
+
+def _valid_rows(mask_u8):
+    """(idx [R] int32, count [1] int32) of the rows with mask != 0, in order (on the device)."""
+    dev, R = mask_u8.device, mask_u8.numel()
+    idx = torch.empty(R, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    nb = L.lib().rs_valid_rows_workspace_size(R)
+    ws = _ws("valid_rows", nb, dev)
+    L.call("rs_valid_rows", L.ptr(mask_u8), R, L.ptr(idx), L.ptr(cnt), L.ptr(ws), ws.numel(),
+           L.stream_ptr(dev))
+    return idx, cnt
+
+
+def _ld(t):
+    if t.stride(-1) != 1:
+        raise ValueError("row-major views only")
+    return t.stride(0)
+
+
+def _masked_proj(x2, W, bias, vr):
+    """x2 [R, K]·W [K, N] + bias on the listed rows; other rows of the result are undefined."""
+    R, K = x2.shape
+    N = W.shape[1]
+    y = torch.empty(R, N, device=x2.device)
+    L.call("rs_masked_proj", L.ptr(x2), _ld(x2), L.ptr(W.contiguous()), L.ptr(bias), L.ptr(vr[0]),
+           L.ptr(vr[1]), R, K, N, L.ptr(y), N, L.stream_ptr(x2.device))
+    return y
+
+
+def _masked_dx(d2, W, mask_u8, vr):
+    """d2 [R, N]·Wᵀ (W [K, N]) on the listed rows (vr = _valid_rows(mask_u8)), 0 where the mask
+    is 0."""
+    R, N = d2.shape
+    K = W.shape[0]
+    dx = torch.empty(R, K, device=d2.device)
+    L.call("rs_masked_dx", L.ptr(d2), _ld(d2), L.ptr(W.contiguous()), L.ptr(mask_u8),
+           L.ptr(vr[0]), L.ptr(vr[1]), R, K, N, L.ptr(dx), K, L.stream_ptr(d2.device))
+    return dx
+
+
+def _masked_wgrad(A2, shift_L, D2, vr, sums=True):
+    """(Σ_listed A_rᵀ·D_r [K, N], Σ_listed D_r [N] or None); shift_L > 0: A_r = row r - 1 within
+    each length-shift_L sequence (0 at its first step)."""
+    K, N = A2.shape[1], D2.shape[1]
+    dev = D2.device
+    C = torch.empty(K, N, device=dev)
+    s = torch.empty(N, device=dev) if sums else None
+    nb = L.lib().rs_masked_wgrad_workspace_size(K, N)
+    ws = _ws("masked_wgrad", nb, dev)
+    L.call("rs_masked_wgrad", L.ptr(A2), _ld(A2), shift_L, L.ptr(D2), _ld(D2), L.ptr(vr[0]),
+           L.ptr(vr[1]), K, N, L.ptr(C), L.ptr(s), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+    return C, s
+
+
+# ---------------------------------------------------------------------------------------------
 class _GRUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, recurrent_kernel, bias, mask_u8):
         B, T, X = x.shape
         H = recurrent_kernel.shape[0]
-        xw = torch.addmm(bias[0], x.reshape(-1, X), kernel).view(B, T, 3 * H)
+        rows = _rows_ready(X, H)
+        if rows:
+            vr = _valid_rows(mask_u8)
+            xw = _masked_proj(x.reshape(-1, X), kernel, bias[0], vr).view(B, T, 3 * H)
+        else:
+            vr = (None, None)
+            xw = torch.addmm(bias[0], x.reshape(-1, X), kernel).view(B, T, 3 * H)
         out = torch.empty(B, T, H, device=x.device)
         saved = torch.empty(B, T, 4 * H, device=x.device)
         rk = recurrent_kernel.contiguous()
         L.call("rs_gru_fwd", L.ptr(xw), L.ptr(rk), L.ptr(bias[1].contiguous()), L.ptr(mask_u8), B, T,
                H, L.ptr(out), L.ptr(saved), L.stream_ptr(x.device))
-        ctx.save_for_backward(x, kernel, rk, out, saved, mask_u8)
+        ctx.save_for_backward(x, kernel, rk, out, saved, mask_u8, *vr)
+        ctx.rows = rows
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, kernel, rk, out, saved, mask_u8 = ctx.saved_tensors
+        x, kernel, rk, out, saved, mask_u8, idx, cnt = ctx.saved_tensors
         B, T, X = x.shape
         H = rk.shape[0]
         dout = dout.contiguous()
@@ -56,6 +137,13 @@ class _GRUFn(torch.autograd.Function):
         L.call("rs_gru_bwd", L.ptr(dout), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
                H, L.ptr(dxw), L.ptr(dinner), L.stream_ptr(x.device))
         dxw2, din2 = dxw.view(-1, 3 * H), dinner.view(-1, 3 * H)
+        if ctx.rows:
+            vr = (idx, cnt)
+            m = mask_u8.reshape(-1)
+            dx = _masked_dx(dxw2, kernel, m, vr).view(B, T, X) if ctx.needs_input_grad[0] else None
+            dk, db0 = _masked_wgrad(x.reshape(-1, X), 0, dxw2, vr)
+            drk, db1 = _masked_wgrad(out.view(-1, H), T, din2, vr)
+            return dx, dk, drk, torch.stack([db0, db1]), None
         hp = torch.cat([torch.zeros(B, 1, H, device=x.device), out[:, :-1]], 1).reshape(-1, H)
         dx = (dxw2 @ kernel.t()).view(B, T, X) if ctx.needs_input_grad[0] else None
         dk = wgrad(x.reshape(-1, X), dxw2)
@@ -109,7 +197,14 @@ class _AUGRUFn(torch.autograd.Function):
         # x parts: update/reset kernels take [h, x] (rows H: are x), candidate takes [x, r·h]
         wx = torch.cat([ku[H:], kr[H:], kh[:X]], dim=1)                 # [X, 3H]
         bx = torch.cat([bu, br, bh])
-        xw = torch.addmm(bx, x.reshape(-1, X), wx).view(B, T, 3 * H)
+        rows = _rows_ready(X, H)
+        if rows:
+            vr = _valid_rows(mask_u8)
+            xw = _masked_proj(x.reshape(-1, X), wx, bx, vr).view(B, T, 3 * H)
+        else:
+            vr = (None, None)
+            xw = torch.addmm(bx, x.reshape(-1, X), wx).view(B, T, 3 * H)
+        ctx.rows = rows
         kuh, krh, khr = ku[:H].contiguous(), kr[:H].contiguous(), kh[X:].contiguous()
         final = torch.empty(B, H, device=x.device)
         states = torch.empty(B, T, H, device=x.device)
@@ -118,13 +213,13 @@ class _AUGRUFn(torch.autograd.Function):
         L.call("rs_augru_fwd", L.ptr(xw), L.ptr(a), L.ptr(kuh), L.ptr(krh), L.ptr(khr),
                L.ptr(mask_u8), B, T, H, L.ptr(final), L.ptr(states), L.ptr(saved),
                L.stream_ptr(x.device))
-        ctx.save_for_backward(x, a, wx, kuh, krh, khr, states, saved, mask_u8)
+        ctx.save_for_backward(x, a, wx, kuh, krh, khr, states, saved, mask_u8, *vr)
         ctx.att_shape = att.shape
         return final
 
     @staticmethod
     def backward(ctx, dfinal):
-        x, a, wx, kuh, krh, khr, states, saved, mask_u8 = ctx.saved_tensors
+        x, a, wx, kuh, krh, khr, states, saved, mask_u8, idx, cnt = ctx.saved_tensors
         B, T, X = x.shape
         H = kuh.shape[0]
         dxw = torch.empty(B, T, 3 * H, device=x.device)
@@ -135,6 +230,18 @@ class _AUGRUFn(torch.autograd.Function):
         d2 = dxw.view(-1, 3 * H)
         dpu, dpr, dph = d2[:, :H], d2[:, H:2 * H], d2[:, 2 * H:]
         x2 = x.reshape(-1, X)
+        if ctx.rows:
+            vr = (idx, cnt)
+            dwx, sb = _masked_wgrad(x2, 0, d2, vr)                        # [X, 3H], Σ rows
+            dhur, _ = _masked_wgrad(states.view(-1, H), T, d2[:, :2 * H], vr, sums=False)
+            dkhr, _ = _masked_wgrad(saved.view(-1, 4 * H)[:, 3 * H:], 0, dph, vr, sums=False)
+            dku = torch.cat([dhur[:, :H], dwx[:, :H]], 0)
+            dkr = torch.cat([dhur[:, H:], dwx[:, H:2 * H]], 0)
+            dkh = torch.cat([dwx[:, 2 * H:], dkhr], 0)
+            dx = (_masked_dx(d2, wx, mask_u8.reshape(-1), vr).view(B, T, X)
+                  if ctx.needs_input_grad[0] else None)
+            return (dx, datt.view(ctx.att_shape), dku, sb[:H], dkr, sb[H:2 * H], dkh, sb[2 * H:],
+                    None)
         hp = torch.cat([torch.zeros(B, 1, H, device=x.device), states[:, :-1]], 1).reshape(-1, H)
         rh = saved[:, :, 3 * H:].reshape(-1, H)
         dwx = wgrad(x2, d2)                                               # [X, 3H]
