@@ -68,7 +68,7 @@ def dien(iters, out):
     dxw = torch.empty(B, T, 3 * H, device=DEV)
     din = torch.empty(B, T, 3 * H, device=DEV)
     us = timed(lambda: L.call("rs_gru_bwd", L.ptr(dout), L.ptr(outp), L.ptr(saved), L.ptr(U),
-                              L.ptr(mask), B, T, H, L.ptr(dxw), L.ptr(din), st), iters)
+                              L.ptr(mask), B, T, H, L.ptr(dxw), L.ptr(din), 0, st), iters)
     report("rs_gru_bwd", cfg, us, B * T * (4 * H + 4 * H + 16 * H + 1 + 12 * H + 12 * H), out)
     att = torch.rand(B, T, device=DEV, generator=g)
     kuh = torch.randn(H, H, device=DEV, generator=g) * 0.1
@@ -76,13 +76,13 @@ def dien(iters, out):
     states = torch.empty(B, T, H, device=DEV)
     us = timed(lambda: L.call("rs_augru_fwd", L.ptr(xw), L.ptr(att), L.ptr(kuh), L.ptr(kuh),
                               L.ptr(kuh), L.ptr(mask), B, T, H, L.ptr(final), L.ptr(states),
-                              L.ptr(saved), st), iters)
+                              L.ptr(saved), 0, st), iters)
     report("rs_augru_fwd", cfg, us, B * T * (12 * H + 4 + 1 + 4 * H + 16 * H) + 4 * B * H, out)
     dfinal = torch.randn(B, H, device=DEV, generator=g)
     datt = torch.empty(B, T, device=DEV)
     us = timed(lambda: L.call("rs_augru_bwd", L.ptr(dfinal), L.ptr(att), L.ptr(states),
                               L.ptr(saved), L.ptr(kuh), L.ptr(kuh), L.ptr(kuh), L.ptr(mask), B, T,
-                              H, L.ptr(dxw), L.ptr(datt), st), iters)
+                              H, L.ptr(dxw), L.ptr(datt), 0, st), iters)
     report("rs_augru_bwd", cfg, us, B * T * (4 + 4 * H + 16 * H + 1 + 12 * H + 4) + 4 * B * H, out)
     hs = torch.randn(B, T, H, device=DEV, generator=g)
     q = torch.randn(B, H, device=DEV, generator=g)

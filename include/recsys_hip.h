@@ -92,6 +92,15 @@ int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids, const int6
                     int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
                     void* stream);
 
+/* Masked variant: positions with valid[i] == 0 are excluded — they take the sentinel key (sorted
+ * last, no segment, no OOB flag). For lookups whose masked positions carry no gradient by
+ * construction (DIEN's padded history steps: dien/model.py mask_zero, dien/layers.py GRU / AUGRU
+ * / aux loss all skip them), so the segmented sums below see only the steps that exist. */
+int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t n_ids, const uint8_t* valid,
+                           const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                           uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
+                           int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
+
 /* Row-sharded variant: rows dealt cyclically over `world` ranks
  * (owner = row % world, local row = row / world). Keys are owner-major:
  * key = owner * ceil(n_rows/world) + local row, so the sorted unique keys are grouped by owner
@@ -121,6 +130,14 @@ int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sort
                                 int64_t n_ids, const float* grad_out, int32_t dim, int64_t n_rows,
                                 uint32_t* uniq_rows, float* uniq_grad, void* workspace,
                                 size_t ws_bytes, void* stream);
+
+/* The deduplicated gradient as a dense [n_rows, dim] tensor: rows without ids 0, every other row
+ * its segment sum (same additions, same order as rs_embedding_dedup_grad); dense is fully written.
+ * workspace >= rs_apply_workspace_size(n_ids, dim) bytes. (The graph-captured Keras Adam steps'
+ * densified table gradients: DIEN, EGES, PinSage.) */
+int32_t rs_embedding_grad_dense(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                int64_t n_ids, const float* grad_out, int32_t dim, int64_t n_rows,
+                                float* dense, void* workspace, size_t ws_bytes, void* stream);
 
 /* Dense gradient of a small table, no sort: grad_dense [n_rows, dim] = Σ over entries n with
  * ids[n] = v of grad_rows[n, :] (Keras' IndexedSlices gradient densified for a dense Adam step,
@@ -301,12 +318,16 @@ int32_t rs_fm_bwd(const float* emb, const float* grad_out, int64_t batch, int32_
  * a-9  keras GRU, reset_after (InterestExtract dien/layers.py:79,131):
  *      xw [B,L,3H] = [x_z,x_r,x_h]; U [H,3H] recurrent kernel; rb [3H] recurrent bias;
  *      out [B,L,H] state after every step; saved [B,L,4H] = [z, r, hh, inner_h] (may be NULL).
- *      bwd: dout [B,L,H] → dxw [B,L,3H] (grad of x·W+b), dinner [B,L,3H] (grad of h·U+rb). */
+ *      bwd: dout [B,L,H] → dxw [B,L,3H] (grad of x·W+b), dinner [B,L,3H] (grad of h·U+rb).
+ *      flags: RS_DIEN_SKIP_MASKED_ROWS leaves the masked steps' rows of dxw / dinner (and of the
+ *      AUGRU's dxw and saved r·h_prev) unwritten — for callers that read only the valid rows
+ *      (rs_masked_dx / rs_masked_wgrad); 0 writes them as 0. */
+#define RS_DIEN_SKIP_MASKED_ROWS 1
 int32_t rs_gru_fwd(const float* xw, const float* U, const float* rb, const uint8_t* mask,
                    int64_t B, int32_t L, int32_t H, float* out, float* saved, void* stream);
 int32_t rs_gru_bwd(const float* dout, const float* out, const float* saved, const float* U,
                    const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
-                   float* dinner, void* stream);
+                   float* dinner, int32_t flags, void* stream);
 /* a-11 AUGRUCell under keras RNN (dien/layers.py:161-204): xw = [x·Ku_x+bu, x·Kr_x+br,
  *      x·Kh_x+bh]; Kuh, Krh [H,H] = h rows of the update/reset kernels ([h, x] concat order),
  *      Khr [H,H] = r·h rows of the candidate kernel ([x, r·h] order); att [B,L].
@@ -314,11 +335,11 @@ int32_t rs_gru_bwd(const float* dout, const float* out, const float* saved, cons
  *      bwd: dfinal [B,H] → dxw [B,L,3H], datt [B,L]. */
 int32_t rs_augru_fwd(const float* xw, const float* att, const float* Kuh, const float* Krh,
                      const float* Khr, const uint8_t* mask, int64_t B, int32_t L, int32_t H,
-                     float* final_h, float* states, float* saved, void* stream);
+                     float* final_h, float* states, float* saved, int32_t flags, void* stream);
 int32_t rs_augru_bwd(const float* dfinal, const float* att, const float* states,
                      const float* saved, const float* Kuh, const float* Krh, const float* Khr,
                      const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
-                     float* datt, void* stream);
+                     float* datt, int32_t flags, void* stream);
 /* a-10 DIENAttention (dien/layers.py:145-158): a = softmax_t(h_t·q + (1-m_t)(-1e9)),
  *      q = K·target [B,H] (caller); bwd: da → dhs [B,L,H] (= ds_t q, written), dq [B,H]. */
 int32_t rs_dien_attention_fwd(const float* hs, const float* q, const uint8_t* mask, int64_t B,

@@ -24,6 +24,7 @@ RS_OPT_KERAS_ADAM = 2
 RS_DEDUP_TILE = 32
 RS_ERRBIT_OOB = 1
 RS_ERRBIT_FORMAT = 2
+RS_DIEN_SKIP_MASKED_ROWS = 1
 
 
 class AdamParams(C.Structure):
@@ -55,6 +56,7 @@ _SIGS = {
     "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_sort_ids_masked": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_sort_ids_sharded": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _sz,
                                    _p]),
     "rs_unique_inverse": (_i32, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
@@ -63,6 +65,7 @@ _SIGS = {
     "rs_keras_adam_flat": (_i32, [_p, _p, _p, _p, _i64, _p, _p, C.POINTER(AdamParams), _p]),
     "rs_embedding_grad_dense_small": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _sz, _p]),
     "rs_embedding_dedup_grad": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _p, _sz, _p]),
+    "rs_embedding_grad_dense": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _sz, _p]),
     "rs_apply_workspace_size": (_sz, [_i64, _i32]),
     "rs_embedding_apply": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p,
                                   C.POINTER(AdamParams), _p, _p, _sz, _p]),
@@ -85,9 +88,9 @@ _SIGS = {
     "rs_bce_fwd": (_i32, [_p, _p, _i64, C.c_float, _i32, _p, _p, _sz, _p]),
     "rs_bce_bwd": (_i32, [_p, _p, _i64, C.c_float, _i32, _p, _p, _p]),
     "rs_gru_fwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
-    "rs_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
-    "rs_augru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _p]),
-    "rs_augru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _i32, _p]),
+    "rs_augru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _i32, _p]),
+    "rs_augru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _i32, _p]),
     "rs_dien_attention_fwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p]),
     "rs_dien_attention_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_dien_aux_workspace_size": (_sz, [_i64, _i32, _i32, _i32]),

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ U,
                                                       const uint8_t* __restrict__ mask, int64_t B,
                                                       int L, int H, float* __restrict__ dxw,
-                                                      float* __restrict__ dinner) {
+                                                      float* __restrict__ dinner, bool zero_masked) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   const int H3 = 3 * H;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
     float* dx = dxw + o * H3;
     float* di = dinner + o * H3;
     if (!valid) {  // state carried: the gradient passes through unchanged
-      if (act) {
+      if (act && zero_masked) {
         dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
         di[j] = di[H + j] = di[2 * H + j] = 0.f;
       }
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
                                                         const uint8_t* __restrict__ mask, int64_t B,
                                                         int L, int H, float* __restrict__ final_h,
                                                         float* __restrict__ states,
-                                                        float* __restrict__ saved) {
+                                                        float* __restrict__ saved, bool zero_masked) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   __shared__ float kh_s[HM * 64];
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
         if (states) states[o * H + j] = h;
         // r⊙h_prev feeds the caller's candidate-kernel gradient GEMM, whose dxw row is 0 here:
         // a defined 0 keeps that product exactly 0
-        if (saved) saved[o * 4 * H + 3 * H + j] = 0.f;
+        if (saved && zero_masked) saved[o * 4 * H + 3 * H + j] = 0.f;
       }
       continue;
     }
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
                                                         const float* __restrict__ Khr,
                                                         const uint8_t* __restrict__ mask, int64_t B,
                                                         int L, int H, float* __restrict__ dxw,
-                                                        float* __restrict__ datt) {
+                                                        float* __restrict__ datt, bool zero_masked) {
   const int wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   __shared__ float kh_s[HM * 64];
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
     const int64_t o = b * L + t;
     float* dx = dxw + o * H3;
     if (!mbits.test(mb, t)) {
-      if (act) dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
+      if (act && zero_masked) dx[j] = dx[H + j] = dx[2 * H + j] = 0.f;
       if (j == 0) datt[o] = 0.f;
       if (t > 0) fetch(t - 1);
       continue;
@@ -521,12 +521,13 @@ extern "C" int32_t rs_gru_fwd(const float* xw, const float* U, const float* rb, 
 
 extern "C" int32_t rs_gru_bwd(const float* dout, const float* out, const float* saved, const float* U,
                               const uint8_t* mask, int64_t B, int32_t L, int32_t H, float* dxw,
-                              float* dinner, void* stream) {
+                              float* dinner, int32_t flags, void* stream) {
+  const bool zm = !(flags & RS_DIEN_SKIP_MASKED_ROWS);
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
   if (B == 0) return RS_OK;
   RS_CHECK_ARG(dout && out && saved && U && mask && dxw && dinner, "null pointer");
   hipStream_t st = as_stream(stream);
-  RS_HM_DISPATCH(H, ({ gru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dout, out, saved, U, mask, B, L, H, dxw, dinner); }));
+  RS_HM_DISPATCH(H, ({ gru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dout, out, saved, U, mask, B, L, H, dxw, dinner, zm); }));
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -534,12 +535,13 @@ extern "C" int32_t rs_gru_bwd(const float* dout, const float* out, const float* 
 extern "C" int32_t rs_augru_fwd(const float* xw, const float* att, const float* Kuh, const float* Krh,
                                 const float* Khr, const uint8_t* mask, int64_t B, int32_t L,
                                 int32_t H, float* final_h, float* states, float* saved,
-                                void* stream) {
+                                int32_t flags, void* stream) {
+  const bool zm = !(flags & RS_DIEN_SKIP_MASKED_ROWS);
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
   if (B == 0) return RS_OK;
   RS_CHECK_ARG(xw && att && Kuh && Krh && Khr && mask && final_h, "null pointer");
   hipStream_t st = as_stream(stream);
-  RS_HM_DISPATCH(H, ({ augru_fwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(xw, att, Kuh, Krh, Khr, mask, B, L, H, final_h, states, saved); }));
+  RS_HM_DISPATCH(H, ({ augru_fwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(xw, att, Kuh, Krh, Khr, mask, B, L, H, final_h, states, saved, zm); }));
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -547,13 +549,14 @@ extern "C" int32_t rs_augru_fwd(const float* xw, const float* att, const float* 
 extern "C" int32_t rs_augru_bwd(const float* dfinal, const float* att, const float* states,
                                 const float* saved, const float* Kuh, const float* Krh,
                                 const float* Khr, const uint8_t* mask, int64_t B, int32_t L,
-                                int32_t H, float* dxw, float* datt, void* stream) {
+                                int32_t H, float* dxw, float* datt, int32_t flags, void* stream) {
+  const bool zm = !(flags & RS_DIEN_SKIP_MASKED_ROWS);
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1, "bad sizes");
   if (B == 0) return RS_OK;
   RS_CHECK_ARG(dfinal && att && states && saved && Kuh && Krh && Khr && mask && dxw && datt,
                "null pointer");
   hipStream_t st = as_stream(stream);
-  RS_HM_DISPATCH(H, ({ augru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dfinal, att, states, saved, Kuh, Krh, Khr, mask, B, L, H, dxw, datt); }));
+  RS_HM_DISPATCH(H, ({ augru_bwd_kernel<HM><<<ceil_div(B, 4), 256, 0, st>>>(dfinal, att, states, saved, Kuh, Krh, Khr, mask, B, L, H, dxw, datt, zm); }));
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -137,7 +137,10 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
 }
 
 // ---- a-2: segmented sum + apply -------------------------------------------------------
-enum { OPT_SGD = RS_OPT_SGD, OPT_LAZY = RS_OPT_LAZY_ADAM, OPT_KERAS = RS_OPT_KERAS_ADAM, OPT_EMIT = 100 };
+// OPT_EMIT: segment sums to (uniq_rows, uniq_grad) in segment order; OPT_DENSE: each segment sum
+// stored as row `row` of a dense [n_rows, dim] gradient (a.table)
+enum { OPT_SGD = RS_OPT_SGD, OPT_LAZY = RS_OPT_LAZY_ADAM, OPT_KERAS = RS_OPT_KERAS_ADAM, OPT_EMIT = 100,
+       OPT_DENSE = 101 };
 
 struct ApplyArgs {
   float* table;
@@ -165,6 +168,8 @@ __device__ __forceinline__ void finalize_chunk(const ApplyArgs& a, uint32_t row,
                                                const float (&g)[VEC], int32_t seg_id) {
   if constexpr (OPT == OPT_EMIT) {
     RowIO<VEC>::store(a.uniq_grad + (int64_t)seg_id * a.dim + col, g);
+  } else if constexpr (OPT == OPT_DENSE) {
+    RowIO<VEC>::store(a.table + (int64_t)row * a.dim + col, g);
   } else if constexpr (OPT == OPT_SGD) {
     float* t = a.table + (int64_t)row * a.dim + col;
     float w[VEC];
@@ -1005,6 +1010,7 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
     case OPT_LAZY: RS_SEG_LAUNCH(OPT_LAZY); break;
     case OPT_KERAS: RS_SEG_LAUNCH(OPT_KERAS); break;
     case OPT_EMIT: RS_SEG_LAUNCH(OPT_EMIT); break;
+    case OPT_DENSE: RS_SEG_LAUNCH(OPT_DENSE); break;
     default: set_error("unknown optimizer %d", opt); return RS_E_INVALID;
   }
 #undef RS_SEG_LAUNCH
@@ -1089,6 +1095,31 @@ extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const in
   const void* ptrs[2] = {grad_out, uniq_grad};
   RowGeom geom = row_geom(dim, ptrs, 2);
   return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);
+}
+
+extern "C" int32_t rs_embedding_grad_dense(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                           int64_t n_ids, const float* grad_out, int32_t dim,
+                                           int64_t n_rows, float* dense, void* workspace,
+                                           size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(dense, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_CHECK_HIP(hipMemsetAsync(dense, 0, (size_t)n_rows * dim * sizeof(float), st));
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(sorted_rows && sorted_pos && grad_out, "null pointer");
+  if (ws_bytes < partial_bytes(n_ids, dim)) {
+    set_error("dense-gradient workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  ApplyArgs a{};
+  a.table = dense;
+  a.dim = dim;
+  a.partial = static_cast<float*>(workspace);
+  a.chunk = chunk_of(a.partial, n_ids, dim);
+  a.tile_flags = flags_of(a.partial, n_ids, dim);
+  const void* ptrs[2] = {grad_out, dense};
+  RowGeom geom = row_geom(dim, ptrs, 2);
+  return launch_segments(OPT_DENSE, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);
 }
 
 extern "C" size_t rs_apply_workspace_size(int64_t n_ids, int32_t dim) {

@@ -46,9 +46,11 @@ struct KeyGen {
   int64_t shard_stride;
   int64_t key_space;
   int32_t* err_flag;
+  const uint8_t* valid;  // optional: positions with valid[i] == 0 take the sentinel key, unflagged
 };
 
 __device__ __forceinline__ uint32_t make_key(const KeyGen& g, int64_t i, bool& oob) {
+  if (g.valid && !g.valid[i]) return static_cast<uint32_t>(g.key_space);  // excluded position
   const int64_t r = global_row(g.ids, g.dtype, i, g.slot_offsets, g.n_slots, g.n_rows);
   if (r < 0) {
     oob = true;
@@ -85,7 +87,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     if (FROM_IDS) {
       if (lds_slots) {
         uint32_t key = 0u;
-        if (i < n) {
+        if (i < n && kg.valid && !kg.valid[i]) {
+          key = static_cast<uint32_t>(kg.key_space);  // excluded position: sentinel, unflagged
+          keys[i] = key;
+        } else if (i < n) {
           const int64_t id = load_id(kg.ids, kg.dtype, i);
           const int sl = (int)((uint32_t)i % (uint32_t)kg.n_slots);
           const int64_t lo = offs[sl], hi = offs[sl + 1];
@@ -613,7 +618,7 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                              const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                              int32_t world, uint32_t* sorted_keys, int32_t* sorted_pos,
                              int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
-                             hipStream_t st, int64_t* key_space_out);
+                             hipStream_t st, const uint8_t* valid);
 
 extern "C" size_t rs_sort_ids_workspace_size(int64_t n_ids) {
   Carver c(nullptr, 0);
@@ -628,6 +633,16 @@ extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
                                int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream) {
   return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
                        sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr);
+}
+
+extern "C" int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t n_ids,
+                                      const uint8_t* valid, const int64_t* slot_offsets,
+                                      int32_t n_slots, int64_t n_rows, uint32_t* sorted_rows,
+                                      int32_t* sorted_pos, int32_t* n_unique, int32_t* err_flag,
+                                      void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(valid || n_ids == 0, "valid is null");
+  return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), valid);
 }
 
 extern "C" int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_t n_ids,
@@ -682,7 +697,7 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                              const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                              int32_t world, uint32_t* sorted_rows, int32_t* sorted_pos,
                              int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
-                             hipStream_t st, int64_t*) {
+                             hipStream_t st, const uint8_t* valid) {
   RS_CHECK_ARG(n_ids >= 0 && n_ids < (int64_t(1) << 31), "n_ids out of range");
   RS_CHECK_ARG(n_rows > 0 && n_rows < (int64_t(1) << 31) - 1, "n_rows out of range");
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
@@ -704,7 +719,8 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
   }
   int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
   // pass 0 makes the keys from the ids (slot offset + id; owner-major when world > 1)
-  const KeyGen kg{ids, id_dtype, slot_offsets, n_slots, n_rows, world, shard_stride, key_space, err_flag};
+  const KeyGen kg{ids, id_dtype, slot_offsets, n_slots, n_rows, world, shard_stride, key_space, err_flag,
+                  valid};
   int32_t s = radix_sort_impl(keys, vals, sorted_rows, sorted_pos, n_ids, key_space,
                               static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, &kg, st);
   if (s) return s;

@@ -134,8 +134,10 @@ class _GRUFn(torch.autograd.Function):
         dout = dout.contiguous()
         dxw = torch.empty(B, T, 3 * H, device=x.device)
         dinner = torch.empty(B, T, 3 * H, device=x.device)
+        # the valid-row kernels below read only the valid steps' rows: the masked ones stay unwritten
+        skip = L.RS_DIEN_SKIP_MASKED_ROWS if ctx.rows else 0
         L.call("rs_gru_bwd", L.ptr(dout), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
-               H, L.ptr(dxw), L.ptr(dinner), L.stream_ptr(x.device))
+               H, L.ptr(dxw), L.ptr(dinner), skip, L.stream_ptr(x.device))
         dxw2, din2 = dxw.view(-1, 3 * H), dinner.view(-1, 3 * H)
         if ctx.rows:
             vr = (idx, cnt)
@@ -212,7 +214,7 @@ class _AUGRUFn(torch.autograd.Function):
         a = att.reshape(B, T).contiguous()
         L.call("rs_augru_fwd", L.ptr(xw), L.ptr(a), L.ptr(kuh), L.ptr(krh), L.ptr(khr),
                L.ptr(mask_u8), B, T, H, L.ptr(final), L.ptr(states), L.ptr(saved),
-               L.stream_ptr(x.device))
+               L.RS_DIEN_SKIP_MASKED_ROWS if rows else 0, L.stream_ptr(x.device))
         ctx.save_for_backward(x, a, wx, kuh, krh, khr, states, saved, mask_u8, *vr)
         ctx.att_shape = att.shape
         return final
@@ -226,7 +228,7 @@ class _AUGRUFn(torch.autograd.Function):
         datt = torch.empty(B, T, device=x.device)
         L.call("rs_augru_bwd", L.ptr(dfinal.contiguous()), L.ptr(a), L.ptr(states), L.ptr(saved),
                L.ptr(kuh), L.ptr(krh), L.ptr(khr), L.ptr(mask_u8), B, T, H, L.ptr(dxw),
-               L.ptr(datt), L.stream_ptr(x.device))
+               L.ptr(datt), L.RS_DIEN_SKIP_MASKED_ROWS if ctx.rows else 0, L.stream_ptr(x.device))
         d2 = dxw.view(-1, 3 * H)
         dpu, dpr, dph = d2[:, :H], d2[:, H:2 * H], d2[:, 2 * H:]
         x2 = x.reshape(-1, X)

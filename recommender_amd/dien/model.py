@@ -32,9 +32,12 @@ class BaseModel(nn.Module):
         self.cat_embedding = Embedding(cat_vocab_size, cat_embedding_size, mask_zero=True,
                                        device=device, generator=generator)
 
-    def compute_flat_embedding(self, inputs):
+    def compute_flat_embedding(self, inputs, grad_mask=None):
+        """grad_mask: the history mask when every consumer skips the masked steps (DIEN), so
+        the tables' densified gradients leave those positions out (Embedding grad_mask)."""
         item, cat = inputs
-        return torch.cat([self.item_embedding(item), self.cat_embedding(cat)], dim=-1)
+        return torch.cat([self.item_embedding(item, grad_mask), self.cat_embedding(cat, grad_mask)],
+                         dim=-1)
 
     def compute_prob(self, inputs):
         return self.forward(inputs)
@@ -88,8 +91,11 @@ class DIEN(BaseModel):
     def forward(self, inputs, training=False, mask=None):
         mask = self.item_embedding.compute_mask(inputs["pos_his_item"])
         target = self.compute_flat_embedding((inputs["target_item"], inputs["target_cat"]))
-        pos = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]))
-        neg = self.compute_flat_embedding((inputs["neg_his_item"], inputs["neg_his_cat"]))
+        # masked history steps carry no gradient: the GRU / AUGRU skip them (their input rows'
+        # gradient is written 0), the attention gives them weight exactly 0 and the aux loss
+        # reads pos / neg only at steps t + 1 with m = 1
+        pos = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]), mask)
+        neg = self.compute_flat_embedding((inputs["neg_his_item"], inputs["neg_his_cat"]), mask)
         hidden, aux = self.interest_extract_layer((pos, neg), training, mask)
         score = self.attention((target, hidden), training, mask)
         rep = self.interest_evolve((hidden, score), training, mask)

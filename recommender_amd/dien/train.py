@@ -96,8 +96,9 @@ class DIENStep:
         total.backward()
         grads = [p.grad for p in self._gdense]  # None: Keras skips the variable
         for t in tables:
-            got = t.take_grad()
-            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None else None)
+            got = t.take_grad(with_valid=True)
+            grads.append(densify_grad(t, got[0], got[1], self._ws, valid=got[2])
+                         if got is not None else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()
             self.opt_graph.iterations += 1

@@ -76,8 +76,9 @@ class Embedding(nn.Module):
     def n_slots(self) -> int:
         return 1 if self.slot_offsets is None else self.slot_offsets.numel() - 1
 
-    def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        return embedding_lookup(self, ids)
+    def forward(self, ids: torch.Tensor, grad_mask=None) -> torch.Tensor:
+        """grad_mask: see functional.embedding_lookup (masked positions carry no gradient)."""
+        return embedding_lookup(self, ids, grad_mask)
 
     def compute_mask(self, ids: torch.Tensor):
         return ids != 0 if self.mask_zero else None
@@ -150,23 +151,35 @@ class Embedding(nn.Module):
         return self.fused_optimizer.sort_async(self, ids)
 
     # ---- sparse gradient plumbing ----
-    def accumulate_grad(self, ids: torch.Tensor, grad_rows: torch.Tensor):
-        self._pending.append((ids.reshape(-1), grad_rows.reshape(-1, self.output_dim)))
+    def accumulate_grad(self, ids: torch.Tensor, grad_rows: torch.Tensor, valid=None):
+        """valid (ids' shape, optional): positions flagged 0 carry no gradient (left out by
+        take_grad(with_valid=True)'s consumers)."""
+        v = None if valid is None else valid.reshape(-1).to(torch.uint8)
+        self._pending.append((ids.reshape(-1), grad_rows.reshape(-1, self.output_dim), v))
 
     def has_grad(self) -> bool:
         return bool(self._pending)
 
-    def take_grad(self):
+    def take_grad(self, with_valid: bool = False):
         """(ids [N] flattened in position order, grad rows [N, dim]) of every lookup since the
-        last call, concatenated in call order; clears the pending list."""
+        last call, concatenated in call order; clears the pending list. with_valid: a third
+        entry, the uint8 [N] flags of positions that carry gradient (None when every lookup
+        registered all its positions)."""
         p, self._pending = self._pending, []
         if not p:
             return None
         if len(p) == 1:
-            return p[0]
-        # every lookup holds a multiple of n_slots ids, so position % n_slots stays the slot
-        ids = torch.cat([i.to(torch.int64) for i, _ in p])
-        return ids, torch.cat([g for _, g in p])
+            ids, g, v = p[0]
+        else:
+            # every lookup holds a multiple of n_slots ids, so position % n_slots stays the slot
+            ids = torch.cat([i.to(torch.int64) for i, _, _ in p])
+            g = torch.cat([g for _, g, _ in p])
+            v = None
+            if any(x is not None for _, _, x in p):
+                v = torch.cat([x if x is not None else torch.ones(i.numel(), dtype=torch.uint8,
+                                                                   device=i.device)
+                               for i, _, x in p])
+        return (ids, g, v) if with_valid else (ids, g)
 
     def zero_grad_pending(self):
         self._pending = []

@@ -36,7 +36,7 @@ def _wait_update(table_module):
 
 class _EmbeddingLookup(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, handle, table_module, ids):
+    def forward(ctx, handle, table_module, ids, grad_mask=None):
         _wait_update(table_module)
         w = table_module.weight
         L.require_device(w, "embedding table")
@@ -50,6 +50,7 @@ class _EmbeddingLookup(torch.autograd.Function):
                L.stream_ptr(w.device))
         ctx.table_module = table_module
         ctx.ids = ids
+        ctx.grad_mask = grad_mask
         return out
 
     @staticmethod
@@ -59,12 +60,18 @@ class _EmbeddingLookup(torch.autograd.Function):
         if tm.fused_optimizer is not None:
             tm.fused_optimizer.apply_async(tm, ctx.ids, g.contiguous(), tm.take_presorted(ctx.ids))
         else:
-            tm.accumulate_grad(ctx.ids, g)
-        return None, None, None
+            if ctx.grad_mask is None:
+                tm.accumulate_grad(ctx.ids, g)
+            else:
+                tm.accumulate_grad(ctx.ids, g, valid=ctx.grad_mask)
+        return None, None, None, None
 
 
-def embedding_lookup(table_module, ids: torch.Tensor) -> torch.Tensor:
-    return _EmbeddingLookup.apply(table_module.grad_handle, table_module, ids)
+def embedding_lookup(table_module, ids: torch.Tensor, grad_mask=None) -> torch.Tensor:
+    """grad_mask (bool / uint8, ids' shape, optional): the caller's statement that the lookup's
+    masked positions receive exactly zero gradient (the model skips them); the densified table
+    gradient then leaves them out instead of summing their zero rows (Embedding.take_grad)."""
+    return _EmbeddingLookup.apply(table_module.grad_handle, table_module, ids, grad_mask)
 
 
 class _DotInteraction(torch.autograd.Function):

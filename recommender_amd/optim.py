@@ -54,7 +54,8 @@ class SortedIds:
 
     def __init__(self, ids: torch.Tensor, n_rows: int, slot_offsets: torch.Tensor | None = None,
                  err_flag: torch.Tensor | None = None, ws: _Workspace | None = None,
-                 count_unique: bool = True, world: int = 1):
+                 count_unique: bool = True, world: int = 1, valid: torch.Tensor | None = None):
+        """valid (uint8 [n], optional): positions with 0 are left out (sentinel key, no flag)."""
         ws = ws or _Workspace()
         ids = ids.contiguous()
         L.require_device(ids, "ids")
@@ -67,7 +68,14 @@ class SortedIds:
         n_slots = 1 if slot_offsets is None else slot_offsets.numel() - 1
         nbytes = L.lib().rs_sort_ids_workspace_size(n)
         w = ws.get("sort", nbytes, dev)
-        if world == 1:
+        if valid is not None:
+            if world != 1 or valid.numel() != n or valid.dtype != torch.uint8:
+                raise ValueError("valid: a uint8 flag per id, one GPU")
+            L.call("rs_sort_ids_masked", L.ptr(ids), L.id_dtype_code(ids), n,
+                   L.ptr(valid.contiguous()), L.ptr(slot_offsets), n_slots, int(n_rows),
+                   L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique), L.ptr(err_flag),
+                   L.ptr(w), w.numel(), L.stream_ptr(dev))
+        elif world == 1:
             L.call("rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets), n_slots,
                    int(n_rows), L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique),
                    L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
@@ -78,8 +86,9 @@ class SortedIds:
 
     @classmethod
     def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None,
-                  count_unique: bool = True):
-        return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws, count_unique)
+                  count_unique: bool = True, valid: torch.Tensor | None = None):
+        return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws, count_unique,
+                   valid=valid)
 
 
 def dedup_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
@@ -200,9 +209,12 @@ class SparseOptimizer:
         return None, None, None
 
     def apply(self, table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor, params,
-              sorted_ids: SortedIds | None = None, row_scale: torch.Tensor | None = None):
+              sorted_ids: SortedIds | None = None, row_scale: torch.Tensor | None = None,
+              valid: torch.Tensor | None = None):
+        """valid (uint8 per id, optional): positions flagged 0 carry no gradient and are left out
+        of the segmented sums (Embedding.take_grad(with_valid=True))."""
         dev = table.weight.device
-        s = sorted_ids or SortedIds.for_table(table, ids, self.ws, count_unique=False)
+        s = sorted_ids or SortedIds.for_table(table, ids, self.ws, count_unique=False, valid=valid)
         g = grad_rows.contiguous()
         m, v, bitmap = self._slots(table)
         nbytes = L.lib().rs_apply_workspace_size(s.n, table.output_dim)
@@ -238,7 +250,7 @@ class SparseOptimizer:
             applied, self._applied = self._applied, set()
         params = self._params()
         for t in self.tables:
-            got = t.take_grad()
+            got = t.take_grad(with_valid=True)
             if got is None:
                 if (self.kind == L.RS_OPT_KERAS_ADAM and id(t) not in applied
                         and not getattr(self, "defer_decay", False)):
@@ -248,8 +260,11 @@ class SparseOptimizer:
                            t.input_dim, t.output_dim, params, L.ptr(bitmap),
                            L.stream_ptr(t.weight.device))
                 continue
-            ids, g = got
-            self.apply(t, ids, g, params)
+            ids, g, valid = got
+            if valid is None:
+                self.apply(t, ids, g, params)
+            else:
+                self.apply(t, ids, g, params, valid=valid)
         self.iterations += 1
 
     def zero_grad(self):
@@ -476,15 +491,17 @@ class GraphKerasAdam:
 
 
 def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
-                 ws: _Workspace | None = None) -> torch.Tensor:
+                 ws: _Workspace | None = None, valid: torch.Tensor | None = None) -> torch.Tensor:
     """The IndexedSlices gradient as a dense [input_dim, dim] tensor with no host sync. Small
     tables (input_dim·dim <= 16384): rs_embedding_grad_dense_small (one pass, fixed block /
-    lane order); others: deterministic segmented sum (rs_embedding_dedup_grad, position order
-    per row), rows past the device count of distinct rows aimed at a discarded sentinel row."""
+    lane order); others: deterministic segmented sum (rs_embedding_grad_dense: position order
+    per row, each row's sum stored in place, untouched rows 0). valid (uint8 per id, optional):
+    positions flagged 0 are left out — for lookups whose masked positions carry no gradient
+    (Embedding.accumulate_grad's valid)."""
     ws = ws or _Workspace()
     dev = table.weight.device
     dim, V = table.output_dim, table.input_dim
-    if V * dim <= 16384 and dim <= 256 and dim & (dim - 1) == 0:
+    if valid is None and V * dim <= 16384 and dim <= 256 and dim & (dim - 1) == 0:
         # small table (PinSage year / genre): one pass, per-block LDS copies, no sort
         ids = ids.reshape(-1).contiguous()
         n = ids.numel()
@@ -495,16 +512,13 @@ def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
                L.ptr(grad_rows.contiguous()), dim, V, L.ptr(dense), L.ptr(table.err_flag),
                L.ptr(w), w.numel(), L.stream_ptr(dev))
         return dense
-    s = SortedIds.for_table(table, ids, ws, count_unique=False)
+    s = SortedIds.for_table(table, ids, ws, count_unique=False, valid=valid)
     n = s.n
-    uniq_rows = torch.full((n,), V, dtype=torch.int32, device=dev)
-    uniq_grad = torch.empty(n, dim, dtype=torch.float32, device=dev)
-    w = ws.get("dedup", L.lib().rs_dedup_workspace_size(n, dim), dev)
-    L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(grad_rows.contiguous()),
-           dim, V, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
-    dense = torch.zeros(V + 1, dim, dtype=torch.float32, device=dev)
-    dense.index_copy_(0, uniq_rows.to(torch.int64), uniq_grad)
-    return dense[:V]
+    dense = torch.empty(V, dim, dtype=torch.float32, device=dev)
+    w = ws.get("dense", L.lib().rs_apply_workspace_size(n, dim), dev)
+    L.call("rs_embedding_grad_dense", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(grad_rows.contiguous()),
+           dim, V, L.ptr(dense), L.ptr(w), w.numel(), L.stream_ptr(dev))
+    return dense
 
 
 class DLRMScheduler:

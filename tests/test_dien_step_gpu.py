@@ -105,15 +105,16 @@ def _checked_step(model, step, feats, label):
     cap = {}
     apply = step.opt_sparse.apply
     for k, t in tables.items():
-        def rec(ids, grad_rows, _k=k, _f=acc[k]):
+        def rec(ids, grad_rows, valid=None, _k=k, _f=acc[k]):
             order[_k].append(ids.reshape(-1).clone())
-            return _f(ids, grad_rows)
+            return _f(ids, grad_rows, valid=valid)
         t.accumulate_grad = rec
 
-    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None, valid=None):
         name = "item" if table is tables["item"] else "cat"
-        cap[name] = (ids.clone(), grad_rows.clone())
-        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
+        cap[name] = (ids.clone(), grad_rows.clone(), None if valid is None else valid.clone())
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale,
+                     valid=valid)
 
     step.opt_sparse.apply = spy
     try:
@@ -143,7 +144,7 @@ def _checked_step(model, step, feats, label):
     keys = {"item": ("target_item", "pos_his_item", "neg_his_item"),
             "cat": ("target_cat", "pos_his_cat", "neg_his_cat")}
     for name, t in tables.items():
-        ids, rows = cap[name]
+        ids, rows, valid = cap[name]
         o = 0
         for chunk in order[name]:
             key = [k for k in keys[name] if torch.equal(chunk.long(), feats[k].reshape(-1).long())]
@@ -154,7 +155,13 @@ def _checked_step(model, step, feats, label):
             o += n
         assert o == ids.numel()
         w0, m0, v0 = (x.cpu().numpy() for x in snap[name])
-        sr, sp, _ = OE.sort_ids(ids.cpu().numpy(), t.input_dim)
+        # the history steps the model masks carry no gradient and are left out of the sums
+        # (Embedding grad_mask): the oracle sorts them as out-of-range ids
+        kept = ids.cpu().numpy()
+        if valid is not None:
+            assert bool((rows[valid == 0] == 0).all()), "a left-out position had a gradient"
+            kept = np.where(valid.cpu().numpy() != 0, kept, -1)
+        sr, sp, _ = OE.sort_ids(kept, t.input_dim)
         ur, ug = OE.segment_sum_tiled(sr, sp, rows.cpu().numpy(), t.input_dim)
         cot = OE.keras_adam_coefficients(step.opt_sparse.iterations, step.opt_sparse.lr)
         w2, m2, v2 = OE.apply_keras_adam(w0, m0, v0, ur.astype(np.int64), ug, cot)

@@ -334,3 +334,35 @@ def test_grad_dense_small_vs_float64(V, dim, n, id_dtype, rng):
         ref2 = ref.copy()
         ref2[ids[n // 2]] -= rows[n // 2]
         assert (np.abs(d.cpu().numpy() - ref2) <= bound + 1e-5 * np.abs(rows[n // 2]).max()).all()
+
+
+@pytest.mark.parametrize("dim", [18, 128])
+@pytest.mark.parametrize("frac", [0.12, 0.0, 1.0])
+def test_masked_sort_dense_grad(dim, frac, rng):
+    """densify_grad with a position mask (DIEN's padded history steps): the masked sort gives the
+    left-out positions the sentinel key without flagging them, and rs_embedding_grad_dense writes
+    each kept row's segment sum in place, bit-exact against the oracle's tiled order on the kept
+    positions (left-out ids as out-of-range), every other row 0; the unmasked densify equals the
+    same oracle over all positions."""
+    from recommender_amd.optim import densify_grad
+
+    V, n = 63_001, 40 * 32 + 7
+    ids = zipf_ids(rng, n, V).astype(np.int64)
+    ids[rng.random(n) < 0.3] = 0  # a padding row shared by many positions
+    keep = rng.random(n) < frac
+    g = rng.standard_normal((n, dim)).astype(np.float32)
+    t = Embedding(V, dim, device=DEV)
+    dense = densify_grad(t, torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV),
+                         valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV))
+    assert int(t.err_flag.item()) == 0  # left-out positions are not out-of-range ids
+    sr, sp, _ = O.sort_ids(np.where(keep, ids, -1), V)
+    ref = np.zeros((V, dim), np.float32)
+    rr, rg = O.segment_sum_tiled(sr, sp, g, V)
+    ref[rr.astype(np.int64)] = rg
+    np.testing.assert_array_equal(dense.cpu().numpy(), ref)
+    full = densify_grad(t, torch.from_numpy(ids).to(DEV), torch.from_numpy(g).to(DEV))
+    sr, sp, _ = O.sort_ids(ids, V)
+    ref = np.zeros((V, dim), np.float32)
+    rr, rg = O.segment_sum_tiled(sr, sp, g, V)
+    ref[rr.astype(np.int64)] = rg
+    np.testing.assert_array_equal(full.cpu().numpy(), ref)
