@@ -18,24 +18,25 @@ EPS = 1e-7
 _ACT = {0: lambda x: x, 1: torch.relu, 2: torch.sigmoid}
 
 
-def _leaf(t):
-    return t.detach().clone().requires_grad_(True)
+def _leaf(t, dtype=None):
+    t = t.detach()
+    return (t.to(dtype) if dtype is not None else t).clone().requires_grad_(True)
 
 
-def _mlp(mlp):
+def _mlp(mlp, dtype=None):
     """[(kernel, bias, act)] leaf copies of an esmm MLP's Dense layers."""
-    return [(_leaf(l.kernel), _leaf(l.bias), l.act_code) for l in mlp.mlp]
+    return [(_leaf(l.kernel, dtype), _leaf(l.bias, dtype), l.act_code) for l in mlp.mlp]
 
 
-def esmm_family_params(model) -> dict:
+def esmm_family_params(model, dtype=None) -> dict:
     kind = type(model).__name__
     if kind == "ESMM":
-        return {"kind": kind, "ctr": _mlp(model.ctr), "cvr": _mlp(model.cvr)}
+        return {"kind": kind, "ctr": _mlp(model.ctr, dtype), "cvr": _mlp(model.cvr, dtype)}
     if kind == "BaseModel":
-        return {"kind": kind, "mlp": _mlp(model.mlp)}
-    return {"kind": kind, "experts": [_mlp(e) for e in model.experts],
-            "gates": [(_leaf(g.kernel), _leaf(g.bias)) for g in model.gates],
-            "towers": [_mlp(t) for t in model.task_towers]}
+        return {"kind": kind, "mlp": _mlp(model.mlp, dtype)}
+    return {"kind": kind, "experts": [_mlp(e, dtype) for e in model.experts],
+            "gates": [(_leaf(g.kernel, dtype), _leaf(g.bias, dtype)) for g in model.gates],
+            "towers": [_mlp(t, dtype) for t in model.task_towers]}
 
 
 def flat_params(P) -> list:
@@ -87,18 +88,30 @@ def keras_adam_torch(w, m, v, g, c):
     return w - (m2 * c["lr"]) / (torch.sqrt(v2) + c["epsilon"]), m2, v2
 
 
-def esmm_family_step(model, table, slot_offsets, feats: dict, label):
+def esmm_family_step(model, table, slot_offsets, feats: dict, label, dtype=torch.float32,
+                     perm=None):
     """Loss, dense gradients (flat_params order) and the table's gradient rows [B*F, D] in
-    position order (p = b*F + f) of one esmm-family step, by torch autograd in fp32."""
-    P = esmm_family_params(model)
+    position order (p = b*F + f) of one esmm-family step, by torch autograd in `dtype`
+    (float64: the accuracy reference; float32 with a batch permutation `perm`: a sample of the
+    rounding another fp32 evaluation order shows — the outputs come back in batch order)."""
+    P = esmm_family_params(model, dtype)
     ids = torch.stack([feats[f].reshape(-1).long() for f in feats], 1)   # [B, F]
+    lab = label.to(dtype)
+    if perm is not None:
+        ids, lab = ids[perm], lab[perm]
     rows = ids + slot_offsets[:-1].to(ids.device)[None, :]
-    E = table[rows].detach().clone().requires_grad_(True)                 # [B, F, D]
+    E = table[rows].detach().to(dtype).clone().requires_grad_(True)      # [B, F, D]
     y = esmm_family_forward(P, E.reshape(E.shape[0], -1))
-    loss = keras_bce_mean(label, y)
+    loss = keras_bce_mean(lab, y)
     leaves = flat_params(P)
     grads = torch.autograd.grad(loss, leaves + [E])
-    return float(loss.detach()), y.detach(), list(grads[:-1]), grads[-1].reshape(-1, table.shape[1])
+    gE = grads[-1]
+    y = y.detach()
+    if perm is not None:
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel(), device=perm.device)
+        y, gE = y[inv], gE[inv]
+    return float(loss.detach()), y, list(grads[:-1]), gE.reshape(-1, table.shape[1])
 
 
 # ---- EGES / GES / DeepWalk (eges/model.py:20-102, eges/train.py:14-24) ---------------------

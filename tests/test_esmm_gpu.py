@@ -7,7 +7,7 @@ import torch
 from recommender_amd.esmm import FEAT_VOCAB
 from recommender_amd.esmm.train import MultiTaskStep, build
 from recommender_amd.synthetic import aliccp_batch
-from tests.conftest import assert_close_rel
+from tests.conftest import assert_close_f64, assert_close_rel
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -63,11 +63,12 @@ def _tol_check(got, ref, rtol, msg, floor=1e-3):
 @pytest.mark.parametrize("kind", ["ESMM", "MMOE", "BASE"])
 def test_esmm_family_keras_adam_step_vs_oracle(kind):
     """One MultiTaskStep (esmm/train.py:97-106, Keras Adam) against oracle/models.py from the
-    same pre-step state: loss 1e-5; outputs 1e-5 (floor 1e-3 of the largest); dense and table
-    gradients 1e-4 relative (floor 1e-3 / 1e-2 of the tensor's largest: fp32 reduction order); dense
-    parameters = Keras Adam of the step's own gradients, bit for bit; table / m / v (all rows:
-    Keras Adam is dense) bit-exact vs the oracle's tiled dedup + Keras apply of the kernel's
-    gradient rows."""
+    same pre-step state, evaluated in float64: loss 1e-5; outputs, dense gradients and the
+    per-position table gradient rows per element within 1e-5 relative + 4x the fp32 oracle's own
+    error there (three batch orders) + 1e-7 of the tensor's largest (1e-6 for the table rows;
+    tests/conftest.py assert_close_f64); dense parameters = Keras Adam of the step's own gradients, bit for bit;
+    table / m / v (all rows: Keras Adam is dense) bit-exact vs the oracle's tiled dedup + Keras
+    apply of the kernel's gradient rows."""
     from oracle import embedding as OE
     from oracle.models import esmm_family_step, keras_adam_torch
 
@@ -85,7 +86,12 @@ def test_esmm_family_keras_adam_step_vs_oracle(kind):
     m_t, v_t, _ = step.opt_sparse._slots(slab)
     m0, v0 = m_t.detach().cpu().numpy().copy(), v_t.detach().cpu().numpy().copy()
     dense0 = [p.detach().clone() for p in step.dense]
-    ref_loss, ref_y, ref_dg, ref_rows = esmm_family_step(model, table0, slab.slot_offsets, feats, lab_t)
+    ref_loss, ref_y, ref_dg, ref_rows = esmm_family_step(model, table0, slab.slot_offsets, feats,
+                                                         lab_t, dtype=torch.float64)
+    # fp32 evaluations in three batch orders: their spread is the rounding noise per element
+    g = torch.Generator(device="cpu").manual_seed(3)
+    perms = [None] + [torch.randperm(512, generator=g).to(DEV) for _ in range(2)]
+    r32 = [esmm_family_step(model, table0, slab.slot_offsets, feats, lab_t, perm=p) for p in perms]
 
     cap = {}
     apply = step.opt_sparse.apply
@@ -98,17 +104,18 @@ def test_esmm_family_keras_adam_step_vs_oracle(kind):
     loss = float(step(feats, lab_t))
     torch.cuda.synchronize()
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
-    assert_close_rel(step.last_pred.cpu().numpy(), ref_y.cpu().numpy(), 1e-5,
-                     float(ref_y.abs().max()) * 1e-3, "outputs")
+    assert_close_f64(step.last_pred, ref_y, [r[1] for r in r32], "outputs")
     co = OE.keras_adam_coefficients(1)
     c = {k: float(v) for k, v in co.items()}
     for i, (p, p0, rg) in enumerate(zip(step.dense, dense0, ref_dg)):
-        _tol_check(p.grad, rg, 1e-4, f"dense grad {i}")
+        assert_close_f64(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}")
         want, _, _ = keras_adam_torch(p0, torch.zeros_like(p0), torch.zeros_like(p0), p.grad, c)
         assert torch.equal(p.detach(), want), f"dense parameter {i} is not Keras Adam of its gradient"
     rows_gpu = cap["rows"].reshape(-1, 18)
-    # rows are products through every tower layer (relu masks, cancellations): floor 1e-2
-    _tol_check(rows_gpu, ref_rows, 1e-4, "table gradient rows", floor=1e-2)
+    # rows run back through every tower layer (relu masks, cancellations): a small element's
+    # rounding follows the size of the terms that cancelled there, so its floor is 1e-6 of the
+    # largest row element (was 1e-2)
+    assert_close_f64(rows_gpu, ref_rows, [r[3] for r in r32], "table gradient rows", floor=1e-6)
     so = slab.slot_offsets.cpu().numpy()
     ids = cap["ids"].cpu().numpy()
     sr, sp, _ = OE.sort_ids(ids, slab.input_dim, so)

@@ -17,7 +17,7 @@ from recommender_amd.pinsage.graph import HeteroGraph
 from recommender_amd.pinsage.layers import frobenius_normalize, weighted_mean_agg
 from recommender_amd.pinsage.sampler import item_pairs
 from recommender_amd.pinsage.train import PinSageStep
-from tests.conftest import assert_close_rel
+from tests.conftest import assert_close_rel, assert_close_f64
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -191,9 +191,10 @@ def torch_agg(u, b):
     E = int(b.n_edges.item())
     src = b.edge_src[:E].long()
     dst = b.edge_dst[:E].long()
-    w = b.edge_w[:E]
-    vs = torch.zeros(b.n_dst, u.shape[1], device=u.device).index_add(0, dst, u[src] * w[:, None])
-    ws = torch.zeros(b.n_dst, device=u.device).index_add(0, dst, w)
+    w = b.edge_w[:E].to(u.dtype)
+    vs = torch.zeros(b.n_dst, u.shape[1], device=u.device, dtype=u.dtype).index_add(
+        0, dst, u[src] * w[:, None])
+    ws = torch.zeros(b.n_dst, device=u.device, dtype=u.dtype).index_add(0, dst, w)
     return vs / torch.clamp(ws, min=1)[:, None]
 
 
@@ -242,13 +243,14 @@ def test_frobenius_normalize(shape):
     assert_close_rel(x.grad.cpu(), x2.grad.cpu(), RTOL, scale=nat * 1e-2, msg="frob bwd")
 
 
-def torch_reference_repr(model, blocks):
-    """pinsage/train/layers.py / model.py restated in plain torch (fp32, autograd)."""
+def torch_reference_repr(model, blocks, dtype=torch.float32):
+    """pinsage/train/layers.py / model.py restated in plain torch (autograd; float64: the
+    accuracy reference, float32: a sample of another fp32 evaluation's rounding)."""
     fp = model.feature_projector
     P = {}
 
     def leaf(name, t):
-        P[name] = t.detach().clone().requires_grad_(True)
+        P[name] = t.detach().to(dtype).clone().requires_grad_(True)
         return P[name]
 
     ids = blocks[0].src_nodes.long()
@@ -280,29 +282,35 @@ def test_pinsage_model_forward_backward():
 
     loss = margin_loss(pos, neg)
     loss.backward()
-    rh, P = torch_reference_repr(model, blocks)
-    rpos, rneg = item2item_scorer(pos_g, rh), item2item_scorer(neg_g, rh)
-    rloss = torch.clamp(rneg + 1 - rpos, min=0).mean()
-    rloss.backward()
-    assert_close_rel(pos.detach().cpu(), rpos.detach().cpu(), RTOL, msg="pos score")
-    assert_close_rel(neg.detach().cpu(), rneg.detach().cpu(), RTOL, msg="neg score")
-    assert abs(loss.item() - rloss.item()) <= RTOL * abs(rloss.item())
+    # the restatement in float64 (the reference) and in fp32 (its rounding: the noise sample of
+    # tests/conftest.py assert_close_f64: 1e-5 relative + 4x the fp32 error + 1e-6 of the largest)
+    ref = {}
+    for dt in (torch.float64, torch.float32):
+        rh, P = torch_reference_repr(model, blocks, dt)
+        rpos, rneg = item2item_scorer(pos_g, rh), item2item_scorer(neg_g, rh)
+        rloss = torch.clamp(rneg + 1 - rpos, min=0).mean()
+        rloss.backward()
+        ref[dt] = (rpos.detach(), rneg.detach(), float(rloss), P)
+    (p64, n64, l64, P64), (p32, n32, _, P32) = ref[torch.float64], ref[torch.float32]
+
+    def close(got, name, r64, r32):
+        assert_close_f64(got, r64, r32, name, floor=1e-6)
+
+    close(pos, "pos score", p64, p32)
+    close(neg, "neg score", n64, n32)
+    assert abs(loss.item() - l64) <= 1e-5 * abs(l64)
     s = model.sagenet
     pairs = [(s.fc_2.kernel, "k2"), (s.fc_2.bias, "b2"), (s.fc_1.kernel, "k1"), (s.fc_1.bias, "b1")]
     for li, c in enumerate(s.convolves):
         pairs += [(c.fc_1.kernel, f"c{li}k1"), (c.fc_1.bias, f"c{li}b1"),
                   (c.fc_2.kernel, f"c{li}k2"), (c.fc_2.bias, f"c{li}b2")]
     for prm, name in pairs:
-        ref = P[name].grad
-        assert_close_rel(prm.grad.cpu(), ref.cpu(), 1e-4, scale=float(ref.abs().max()) * 1e-2,
-                         msg=name)
+        close(prm.grad, name, P64[name].grad, P32[name].grad)
     for t, name in zip(model.tables(), ("year", "genre", "id")):
         ids, rows = t.take_grad()
         dense = torch.zeros_like(t.weight).index_add(0, ids.reshape(-1).long(),
                                                      rows.reshape(-1, t.output_dim))
-        ref = P[name].grad
-        assert_close_rel(dense.cpu(), ref.cpu(), 1e-4, scale=float(ref.abs().max()) * 1e-2,
-                         msg=f"table {name}")
+        close(dense, f"table {name}", P64[name].grad, P32[name].grad)
 
 
 def test_pinsage_train_steps_reduce_loss():
@@ -519,18 +527,34 @@ def _pinsage_setup(seed_model=1):
     return g, model, smp
 
 
+def _param_ref_names(model):
+    """named_parameters name -> torch_reference_repr leaf name."""
+    s = model.sagenet
+    out = {}
+    pairs = [(s.fc_2.kernel, "k2"), (s.fc_2.bias, "b2"), (s.fc_1.kernel, "k1"), (s.fc_1.bias, "b1")]
+    for li, c in enumerate(s.convolves):
+        pairs += [(c.fc_1.kernel, f"c{li}k1"), (c.fc_1.bias, f"c{li}b1"),
+                  (c.fc_2.kernel, f"c{li}k2"), (c.fc_2.bias, f"c{li}b2")]
+    ids = {id(p): nm for p, nm in pairs}
+    for k, v in model.named_parameters():
+        if id(v) in ids:
+            out[k] = ids[id(v)]
+    return out
+
+
 def test_static_forward_backward_equals_dynamic():
     """PinSageModel on the capacity-shaped batch: live scores, the masked margin loss and
-    every gradient (dense and densified tables) equal the dynamic batch's up to fp32 rounding
-    order (the GEMMs see more rows); padding contributes exactly nothing."""
+    every gradient (dense and densified tables) — and the dynamic batch's — within fp32 rounding
+    of the float64 restatement per element (padding contributes exactly nothing)."""
     from recommender_amd.optim import densify_grad
-    from recommender_amd.pinsage.model import margin_loss
+    from recommender_amd.pinsage.model import item2item_scorer, margin_loss
 
     B = 128
     g, model, dyn = _pinsage_setup()
     sta = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
     h, p, n = item_pairs(g, B, 4, 0)
-    pos, neg = model(*dyn.sample_from_item_pairs(h, p, n))
+    pg, ng, blocks = dyn.sample_from_item_pairs(h, p, n)
+    pos, neg = model(pg, ng, blocks)
     margin_loss(pos, neg).backward()
     ref = {k: v.grad.clone() for k, v in model.named_parameters() if v.grad is not None}
     ref_tab = [densify_grad(t, *t.take_grad()) for t in model.tables()]
@@ -540,17 +564,32 @@ def test_static_forward_backward_equals_dynamic():
     sloss = margin_loss(spos, sneg, 1.0, spg.valid, spg.n_valid)
     sloss.backward()
     nv = h.numel()
-    assert_close_rel(spos[:nv].detach().cpu(), pos.detach().cpu(), RTOL, msg="pos")
-    assert_close_rel(sneg[:nv].detach().cpu(), neg.detach().cpu(), RTOL, msg="neg")
+    # both batches against the float64 restatement of the dynamic one (the fp32 restatement's
+    # error as the noise sample: tests/conftest.py assert_close_f64)
+    r = {}
+    for dt in (torch.float64, torch.float32):
+        rh, P = torch_reference_repr(model, blocks, dt)
+        rp, rn = item2item_scorer(pg, rh), item2item_scorer(ng, rh)
+        torch.clamp(rn + 1 - rp, min=0).mean().backward()
+        r[dt] = (rp.detach(), rn.detach(), P)
+    (p64, n64, P64), (p32, n32, P32) = r[torch.float64], r[torch.float32]
+    for got, name in ((spos[:nv], "static pos"), (pos, "dynamic pos")):
+        assert_close_f64(got, p64, p32, name, floor=1e-6)
+    for got, name in ((sneg[:nv], "static neg"), (neg, "dynamic neg")):
+        assert_close_f64(got, n64, n32, name, floor=1e-6)
     rl = margin_loss(pos, neg).item()
     assert abs(sloss.item() - rl) <= RTOL * abs(rl)
+    names = _param_ref_names(model)
     for k, v in model.named_parameters():
         if k in ref:
-            assert_close_rel(v.grad.cpu(), ref[k].cpu(), 1e-4,
-                             scale=float(ref[k].abs().max()) * 1e-2, msg=k)
-    for t, r in zip(model.tables(), ref_tab):
+            assert_close_f64(v.grad, P64[names[k]].grad, P32[names[k]].grad, f"static {k}",
+                             floor=1e-6)
+            assert_close_f64(ref[k], P64[names[k]].grad, P32[names[k]].grad, f"dynamic {k}",
+                             floor=1e-6)
+    for t, rt, name in zip(model.tables(), ref_tab, ("year", "genre", "id")):
         d = densify_grad(t, *t.take_grad())
-        assert_close_rel(d.cpu(), r.cpu(), 1e-4, scale=float(r.abs().max()) * 1e-2)
+        assert_close_f64(d, P64[name].grad, P32[name].grad, f"static table {name}", floor=1e-6)
+        assert_close_f64(rt, P64[name].grad, P32[name].grad, f"dynamic table {name}", floor=1e-6)
 
 
 def test_static_step_graph_replay_bit_exact_and_matches_dynamic():
