@@ -87,10 +87,12 @@ def parse():
     ap.add_argument("--defer-decay", type=int, default=0,
                     help="keras_adam: replay the dense decay per row when it is next read instead "
                          "of sweeping all rows each step (exact after materialize)")
-    ap.add_argument("--prefetch", type=int, default=0,
-                    help="1: sort the next batch's ids one step ahead (TrainStep.prefetch); eager "
-                         "only. Measured slower on the north star (0.864 vs 0.845 ms/step): the "
-                         "early sort contends with the previous update and the resident train grid")
+    ap.add_argument("--prefetch", type=int, default=-1,
+                    help="1: the next batch's ids handled one step ahead (TrainStep.prefetch): one "
+                         "GPU, its sort after this step's train kernel; row-sharded (--gpus > 1), "
+                         "the exchange's sort / unique / split sizes, so the step's one host sync "
+                         "waits on work queued a step earlier. -1 (default): on for --gpus > 1, off "
+                         "for one GPU (measured: 0.745 vs 0.707 ms/step there, host-bound)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: HIP-graph replays of single steps; 2: one graph per pool of steps "
                          "(updates overlapped across steps inside the graph)")
@@ -412,6 +414,8 @@ def main():
         hp.wait_stream(torch.cuda.current_stream(dev))
         torch.cuda.set_stream(hp)
     P = len(pool)
+    if args.prefetch < 0:
+        args.prefetch = 1 if world > 1 else 0
     if args.prefetch and not args.graph:
         # the loader's next batch is on the device a step early: its sort is queued one step
         # ahead (TrainStep.prefetch), beside the current step's kernels
@@ -657,7 +661,8 @@ def main():
                        "optimizer": args.optimizer + (" (deferred exact decay)" if materialize_ms is not None else ""),
                        "parallelism": (f"row-sharded slab x{world} (RCCL all-to-all of the unique rows and of their "
                                        f"gradient rows) + dp{world} MLPs (all-reduce of the fused kernel's "
-                                       f"batch sums)") if world > 1 else "single"},
+                                       f"batch sums)") if world > 1 else "single",
+                       "prefetch": bool(args.prefetch)},
             "mlp": {"backward": args.mlp_bwd, "forward": args.mlp_fwd,
                     "note": "ctr MLP hidden layers are linear (ctr/layers.py:8), so each MLP is one "
                             "affine map: the composed forward evaluates x·K1·K2·K3 + c as x·(K1K2K3) + c "

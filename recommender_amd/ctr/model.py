@@ -107,7 +107,9 @@ class DLRM(nn.Module):
             # row-sharded slab: the sort / split-size exchange is queued first (side stream), so
             # it runs beside the bottom MLP; the host waits for the split sizes only after the
             # bottom MLP is queued
-            pending = self.embedding_layer.exchange_begin(cat_features)
+            pending = self.embedding_layer.take_prefetched(cat_features.contiguous())
+            if pending is None:
+                pending = self.embedding_layer.exchange_begin(cat_features)
         bmlp_activation = self.bottom_mlp(int_features)
         if pending is not None:
             self._exchanged = self.embedding_layer.exchange_finish(pending)

@@ -164,15 +164,21 @@ class TrainStep:
         return replay
 
     def prefetch(self, batch):
-        """Sort a LATER batch's ids now (Embedding.prefetch, fused sparse optimizer only): call
+        """Sort a LATER batch's ids now (Embedding.prefetch, fused sparse optimizer; on a
+        row-sharded slab the exchange's first half, ShardedSlabEmbedding.prefetch): call
         it before the step that precedes the batch's own step, e.g.
         `step.prefetch(batches[i + 1]); step(batches[i])` — the data pipeline's prefetch of the
         next batch. The batch's ids must already be on the device and must not change before
         their step runs."""
         emb = self.model.embedding_layer
-        if self.sharded or not self.opt_sparse.fused or not hasattr(emb, "prefetch"):
+        ids = batch[0].reshape(-1, self.model.num_cat_fea).contiguous()
+        if self.sharded:
+            # row-sharded slab: the exchange's sort, unique pass and split sizes a step ahead
+            emb.prefetch(ids)
             return
-        emb.prefetch(batch[0].reshape(-1, self.model.num_cat_fea).contiguous())
+        if not self.opt_sparse.fused or not hasattr(emb, "prefetch"):
+            return
+        emb.prefetch(ids)
 
     def fused_step_ready(self, batch) -> bool:
         """True when __call__ takes the one-kernel production DLRM step."""

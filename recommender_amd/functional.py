@@ -366,7 +366,10 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     sharded = hasattr(emb, "exchange_begin")
     world = comm.world if (sharded and comm is not None) else 1
     if sharded:
-        pending = emb.exchange_begin(ids)  # sort / unique / split sizes beside the bottom MLP
+        # sort / unique / split sizes beside the bottom MLP (or queued a step ahead: prefetch)
+        pending = emb.take_prefetched(ids)
+        if pending is None:
+            pending = emb.exchange_begin(ids)
     else:
         emb.presort(ids)  # the sort runs beside the bottom MLP and the fused kernel
     x = int_features.reshape(-1, n_in).float().contiguous()

@@ -110,6 +110,7 @@ class ShardedSlabEmbedding(nn.Module):
         self.side = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.optimizer: SparseOptimizer | None = None
         self._st = None  # per-step exchange state
+        self._prefetched: dict = {}  # exchange_begin states queued ahead (prefetch)
 
     @property
     def n_slots(self):
@@ -157,6 +158,31 @@ class ShardedSlabEmbedding(nn.Module):
         return dict(ids=ids, s=s, uniq=uniq, inverse=inverse, host=host, ready=ready,
                     staged=staged, dev=dev)
 
+    @staticmethod
+    def _ids_key(ids):
+        return (ids.data_ptr(), tuple(ids.shape), ids.dtype)
+
+    def prefetch(self, ids: torch.Tensor):
+        """Queue the first half of a LATER step's exchange now (owner-major sort, unique /
+        inverse, split sizes: exchange_begin) so that step's exchange_finish finds its split
+        sizes already on the host: the one host sync of a sharded step then waits on work queued
+        a step earlier instead of stalling the device (every rank must prefetch the same steps,
+        in the same order: the split-size exchange is a collective). The ids must not change
+        before their step (an in-place change voids the entry)."""
+        key = self._ids_key(ids)
+        if key in self._prefetched or torch.cuda.is_current_stream_capturing():
+            return
+        if len(self._prefetched) >= 4:  # stale entries (steps that never ran)
+            self._prefetched.pop(next(iter(self._prefetched)))
+        self._prefetched[key] = (ids._version, self.exchange_begin(ids))
+
+    def take_prefetched(self, ids: torch.Tensor):
+        """The prefetched exchange_begin state of these ids, or None."""
+        e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
+        if e is None or e[0] != ids._version:
+            return None
+        return e[1]
+
     def exchange_finish(self, st):
         """Wait (host) for the split sizes, then the two all-to-alls and the owner gather;
         returns (view, inverse ids [B, S] int32)."""
@@ -196,7 +222,8 @@ class ShardedSlabEmbedding(nn.Module):
 
     def exchange(self, ids: torch.Tensor):
         """Fetch this step's unique rows; returns (view, inverse ids [B, S] int32)."""
-        return self.exchange_finish(self.exchange_begin(ids))
+        st = self.take_prefetched(ids.contiguous())
+        return self.exchange_finish(st if st is not None else self.exchange_begin(ids))
 
     def comm_counts(self, recv_counts: torch.Tensor, send_counts: torch.Tensor):
         if self.comm.staged or not dist.is_initialized():

@@ -240,3 +240,77 @@ def test_world2_fused_dlrm_step_matches_oracle():
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def _prefetch_world2_worker(rank, world, port, q):
+    """The row-sharded fused DLRM step with the exchange's first half queued a step ahead
+    (TrainStep.prefetch -> ShardedSlabEmbedding.prefetch) equals the same steps without it, bit for
+    bit (slab and MLP), over 3 steps; a prefetched batch whose ids change in place is exchanged
+    again."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommender_amd.ctr.layers import MLP
+        from recommender_amd.ctr.model import DLRM
+        from recommender_amd.ctr.train import TrainStep
+        from recommender_amd.sharded import Comm, ShardedSlabEmbedding
+        from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+        MLP.factored_min_batch = 0
+        S, D, B = 26, 128, 512
+        cards = criteo_cardinalities(100_000, S)
+        V = sum(cards)
+        table = torch.from_numpy(np.random.default_rng(9).uniform(-0.05, 0.05, (V, D)).astype(np.float32))
+        rng = np.random.default_rng(50 + rank)
+        batches = [tuple(torch.from_numpy(x).to(DEV) for x in criteo_batch(rng, B, cards)) for _ in range(3)]
+        repl = torch.from_numpy(criteo_batch(rng, B, cards)[0]).to(DEV)
+        comm = Comm()
+        res = []
+        for pre in (False, True):
+            emb = ShardedSlabEmbedding(cards, D, comm, device=DEV, full_weight=table)
+            g = torch.Generator(device=DEV)
+            g.manual_seed(3)
+            model = DLRM([128, 64, D], [128, 64, 1], D, V, S, 13, device=DEV, generator=g,
+                         embedding_layer=emb)
+            step = TrainStep(model, "sgd", lr=0.05, comm=comm)
+            bs = [tuple(t.clone() for t in b) for b in batches]
+            for i, b in enumerate(bs):
+                if pre and i + 1 < len(bs):
+                    step.prefetch(bs[i + 1])
+                if i == 2:  # prefetched during step 1, then changed in place
+                    b[0].copy_(repl)
+                step(b)
+            emb.join()
+            torch.cuda.synchronize()
+            assert not emb._prefetched
+            res.append((emb.full_weight().cpu(), [p.detach().cpu() for p in model.parameters()]))
+        (wa, pa), (wb, pb) = res
+        assert torch.equal(wa, wb)
+        for x, y in zip(pa, pb):
+            assert torch.equal(x, y)
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_prefetched_exchange_bit_identical():
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + (os.getpid() % 500)
+    ps = [ctx.Process(target=_prefetch_world2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res
