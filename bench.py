@@ -567,16 +567,20 @@ def main():
             v["traffic"] is not None for v in per_kernel.values()) else None
         dom = max(iso, key=iso.get)
         # measured STREAM-copy bandwidth of this GPU: a 4 GiB device-to-device copy
-        src = torch.empty(1 << 30, dtype=torch.float32, device=dev)
+        # with 16-byte accesses (rs_stream_copy; torch's copy_ measured ≈4.7 TB/s on the same
+        # boxes, below the float4 copy's ≈6.3 TB/s the guide lists)
+        src = torch.zeros(1 << 30, dtype=torch.float32, device=dev)
         dst = torch.empty_like(src)
-        dst.copy_(src)
+        nb = src.numel() * 4
+        st_ = L.stream_ptr(dev)
+        L.call("rs_stream_copy", L.ptr(src), L.ptr(dst), nb, st_)
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         c0.record()
         for _ in range(10):
-            dst.copy_(src)
+            L.call("rs_stream_copy", L.ptr(src), L.ptr(dst), nb, st_)
         c1.record()
         torch.cuda.synchronize()
-        copy_gbs = 2 * src.numel() * 4 * 10 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        copy_gbs = 2 * nb * 10 / (c0.elapsed_time(c1) * 1e-3) / 1e9
         del src, dst
         roof = {"bound": "hbm", "kernel": "embedding_path (" + " + ".join(iso) + ")",
                 "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -591,8 +595,9 @@ def main():
                         "kernels' isolated launch times (HIP events, after the timed region, on "
                         "the model's slab and ids); in_step_span_us = the same kernel's HIP-event "
                         "span inside the timed steps (side-stream spans include co-run time); "
-                        "traffic = PMC FETCH+WRITE per call; measured_copy_GBs = torch D2D copy_ "
-                        "of 4 GiB (read + write bytes / time), the STREAM-copy reference"}
+                        "traffic = PMC FETCH+WRITE per call; measured_copy_GBs = a 4 GiB "
+                        "device copy with 16-byte accesses (rs_stream_copy; read + write bytes / "
+                        "time), the STREAM-copy reference"}
 
     # the reference's active ctr optimizer (ctr/train.py:80,84: Keras Adam on every variable) on
     # the same model and batches, with the deferred exact decay (bit-identical to the per-step

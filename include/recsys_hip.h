@@ -62,6 +62,9 @@ const char* rs_last_error(void);
 int32_t rs_version(void);
 /* number of gfx950 devices visible; 0 when no GPU (used by loaders to fail loudly) */
 int32_t rs_device_count(void);
+/* STREAM-style device copy (16-byte accesses): the measured HBM-bandwidth reference of the
+ * bench's roofline; bytes a multiple of 16, both buffers 16-byte aligned. */
+int32_t rs_stream_copy(const void* src, void* dst, size_t bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * a-1  Embedding forward (multi-slot gather).

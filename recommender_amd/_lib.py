@@ -53,6 +53,7 @@ _SIGS = {
     "rs_last_error": (C.c_char_p, []),
     "rs_version": (_i32, []),
     "rs_device_count": (_i32, []),
+    "rs_stream_copy": (_i32, [_p, _p, _sz, _p]),
     "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
