@@ -414,6 +414,19 @@ def dlrm_path(iters, out):
                L.ptr(dense), L.ptr(xin), 13, L.ptr(lab), B, L.ptr(q), L.ptr(cc), 1e-7, 2,
                L.ptr(yb), L.ptr(gemb), L.ptr(sums), L.ptr(tws), tws.numel(), L.ptr(err), st)
 
+    gb = torch.empty(B, device=DEV)
+
+    def train_unit():
+        L.call("rs_dlrm_train_step_fwd_unit", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
+               L.ptr(dense), L.ptr(xin), 13, L.ptr(lab), B, L.ptr(q), L.ptr(cc), 1e-7, 1.0 / B,
+               L.ptr(yb), L.ptr(gemb), L.ptr(gb), L.ptr(sums), L.ptr(tws), tws.numel(), L.ptr(err),
+               st)
+
+    def apply_unit():
+        L.call("rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(table), None, None, V, D,
+               L.ptr(s0.rows), L.ptr(s0.pos), B * S, L.ptr(gemb), L.ptr(gb), S, prm, None,
+               L.ptr(ws), ws.numel(), st)
+
     def fwd_dx():
         L.call("rs_dlrm_interaction_fwd_head_dx", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
                L.ptr(dense), B, L.ptr(inter), 480, L.ptr(q), L.ptr(cc), 2, L.ptr(yv), L.ptr(gemb),
@@ -439,6 +452,15 @@ def dlrm_path(iters, out):
         tot += us
         report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
     report("embedding_path (production: fused train-step kernel, sort, apply; alone)",
+           dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
+    # the chunked train kernel (unit rows + G, scaled apply)
+    tot = 0.0
+    for name, fn in (("rs_dlrm_train_step_fwd_unit", train_unit), ("rs_sort_ids", srt),
+                     ("rs_embedding_apply_scaled", apply_unit)):
+        us = timed(fn, iters)
+        tot += us
+        report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
+    report("embedding_path (chunked train kernel, sort, scaled apply; alone)",
            dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
     # the previous production path (fused forward + unit backward, scaled apply)
     tot = 0.0

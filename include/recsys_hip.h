@@ -850,6 +850,21 @@ int32_t rs_dlrm_train_step_fwd_scaled(const float* table, int64_t n_rows, int32_
                                       float loss_scale, float* y, float* grad_emb, float* sums,
                                       void* workspace, size_t ws_bytes, int32_t* err_flag,
                                       void* stream);
+/* The same step with the table gradient rows written UNIT-scaled: unit_rows[b, i] = U_b[i] (the
+ * interaction backward's (M + Mᵀ)·X_b row) and g_rows[b] = G_b, so the gradient row of position
+ * p is g_rows[p / n_slots] * unit_rows[p] — hand both to rs_embedding_apply_scaled (row_scale =
+ * g_rows, scale_group = n_slots), which forms that product with the same fmul_rn as
+ * rs_dlrm_train_step_fwd_scaled. y and sums as rs_dlrm_train_step_fwd_scaled. The kernel computes
+ * the interaction chunk by chunk (U written before the head's G is known), which is why the rows
+ * leave it unscaled. Replaces the same reference call as rs_dlrm_train_step_fwd. */
+int32_t rs_dlrm_train_step_fwd_unit(const float* table, int64_t n_rows, int32_t D,
+                                    const void* ids, int32_t id_dtype, int32_t n_slots,
+                                    const int64_t* slot_offsets, const float* dense,
+                                    const float* xin, int32_t n_in, const float* label,
+                                    int64_t batch, const float* q, const float* c, float eps,
+                                    float loss_scale, float* y, float* unit_rows, float* g_rows,
+                                    float* sums, void* workspace, size_t ws_bytes,
+                                    int32_t* err_flag, void* stream);
 
 /* ---- the production DLRM step's dense tail (ctr/train.py:77-79 SGD of every MLP parameter;
  * ctr/layers.py:5-14 linear hidden layers) ------------------------------------------------

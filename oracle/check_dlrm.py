@@ -274,6 +274,7 @@ def checked_dlrm_keras_step(model, step, cat, dn, lb, state) -> dict:
 
     def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
         captured["grad_rows"], captured["sorted"] = grad_rows, sorted_ids
+        captured["row_scale"] = row_scale
         return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
 
     opt.apply = spy
@@ -288,6 +289,9 @@ def checked_dlrm_keras_step(model, step, cat, dn, lb, state) -> dict:
     torch.cuda.synchronize()
     assert "grad_rows" in captured, "the fused sparse apply did not run"
     g_gpu = captured["grad_rows"].cpu().numpy().reshape(B * S, D)
+    if captured["row_scale"] is not None:  # unit rows + G[b]: the apply's row is their product
+        sc = captured["row_scale"].cpu().numpy().astype(np.float32)
+        g_gpu = (np.repeat(sc, S)[:, None] * g_gpu).astype(np.float32)
     p_gpu = step.last_pred.cpu().numpy().astype(np.float64)
 
     st = DLRMState(wu.copy(), None, [(k.copy(), b.copy()) for k, b in bot0],

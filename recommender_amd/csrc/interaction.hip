@@ -1191,6 +1191,356 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t
   if (__any(oob) && lane == 0) flag_oob(src.err_flag);
 }
 
+// ---------------------------------------------------------------------------------------
+// The train step with the interaction computed chunk by chunk (round 3): per 32-column chunk s
+// of X(b) (rows r / 16 + r of the bf16 MFMA operand layout, already in registers),
+//   split   x = h + m + l (split3), once — the same three parts feed both products;
+//   Z       the chunk's k-step of Z = X·Xᵀ (three 16x16 blocks, mfma6);
+//   loads   X(b+1)'s chunk s is issued into the registers just freed, so every chunk's loads
+//           have a whole example of latency cover (no second register set);
+//   image   the six bf16x8 parts go to a 6 KB per-wave LDS image [part][32 rows][32 columns]
+//           (the two 16-column halves of rows 8-15 / 24-31 swapped: conflict-free transposed
+//           reads), read back column-major with ds_read_b64_tr_b16 as the A operand of
+//   Uᵀ      Uᵀ = Xᵀ·(M + Mᵀ) for the chunk's two 16-column tiles: the MFMA result puts four
+//           consecutive columns of one U row in each lane, so the rows go straight to HBM.
+// U is written UNSCALED (the head's G needs all of Z, known only after the last chunk) and G[b]
+// goes to g_rows: the apply multiplies each gradient row by its example's G
+// (rs_embedding_apply_scaled, row_scale = g_rows, scale_group = n_slots) with the same fmul_rn,
+// so the table update is the one dlrm_train_pipe's G·U rows give. Against dlrm_train_pipe: no
+// second split of X for U (≈0.3 k VALU per example), no fp32 X / U round trip through LDS, 6 KB
+// instead of 17 KB of LDS per wave.
+// ---------------------------------------------------------------------------------------
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
+
+// the Uᵀ product: c + Xᵀ·S from the split operands, the six products in dlrm_train_pipe's U
+// order (X as A, S as B: m·m, l·h, h·l, m·h, h·m, h·h)
+__device__ __forceinline__ floatx4 mfma6_xs(const bf16x8& xh, const bf16x8& xm, const bf16x8& xl,
+                                            const bf16x8& sh, const bf16x8& sm, const bf16x8& sl,
+                                            floatx4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xm, sm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, sh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, sl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xm, sh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, sm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, sh, c, 0, 0, 0);
+}
+
+constexpr int kChPlane = 32 * 32 * 2;  // one part of the chunk image: 32 rows x 32 bf16
+constexpr int kChImage = 3 * kChPlane;  // bytes
+// byte offset of (row, 8-column group) in a plane: halves of rows 8-15 / 24-31 swapped
+__device__ __forceinline__ int ch_off(int row, int col) {
+  return row * 64 + 2 * (col ^ (((row >> 3) & 1) << 4));
+}
+constexpr int kChStageLd = 36;  // fp32 U staging rows [32][36]: 32 columns + 4 of padding
+template <int D>
+constexpr int chunk_region_floats() {
+  return (kChImage / 4 + 32 * kChStageLd + D) > train_m<D>() ? (kChImage / 4 + 32 * kChStageLd + D)
+                                                             : train_m<D>();
+}
+
+#ifndef RS_TRAIN_CHUNK_OCC
+#define RS_TRAIN_CHUNK_OCC 2
+#endif
+template <int D, bool ID64>
+__global__ __launch_bounds__(256, RS_TRAIN_CHUNK_OCC) void dlrm_train_chunk(GatherSrc src, int64_t batch, int F,
+                                                        TrainArgs ta, float* g_rows, int epw) {
+  static_assert(D == 64 || D == 128, "train kernel laid out for D = 64 or 128");
+  constexpr int NT = D / 16, NC = D / 32, DL = D / 4, RPI = 64 / DL, DPL = D / 64;
+  constexpr int TM = train_m<D>();
+  constexpr int RW = chunk_region_floats<D>();
+  // per wave: the chunk image (kChImage bytes) + U's bottom row [D]; the partial row at the end
+  __shared__ __attribute__((aligned(16))) float lds[4][RW];
+  __shared__ __attribute__((aligned(16))) float qlane[64][12];
+  __shared__ __attribute__((aligned(16))) float qsh[kTrainAtop];
+  // S's split parts (the Uᵀ product's B operands), read per chunk: 24 VGPRs the loop needs more
+  __shared__ __attribute__((aligned(16))) bf16x8 sash[2][3][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
+  const int64_t last = first + epw < batch ? first + epw : batch;
+  const bool active = first < batch;
+  const int r = lane & 15, g = lane >> 4;
+  const int S = src.n_slots;
+  const int nzc = F * (F - 1) / 2;
+  char* img = reinterpret_cast<char*>(lds[wave]);
+  float* stg = lds[wave] + kChImage / 4;          // the chunk's U columns, row-major
+  float* ubot = stg + 32 * kChStageLd;
+  for (int e = threadIdx.x; e < kTrainAtop; e += 256) qsh[e] = e < nzc + D ? ta.q[e] : 0.f;
+  if (wave == 0) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i0 = 4 * g + reg, j0 = r;
+      const int i1 = 4 * g + reg, j1 = 16 + r;
+      const int i2 = 16 + 4 * g + reg, j2 = 16 + r;
+      qlane[lane][reg] = (i0 < j0) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
+      qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
+      qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
+    }
+  }
+  // S = M + Mᵀ as the B operand of Uᵀ = Xᵀ·S: lane (r, g) holds S[8g + j][16 ib + r], which by
+  // symmetry is dlrm_train_pipe's A operand S[16 ib + r][8g + j]
+  if (wave == 1) {
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      floatx4 v[2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = 16 * ib + r, kk = 8 * g + j;
+        const bool in = m < F && kk < F && m != kk;
+        const float q = ta.q[in ? compact_index(m < kk ? m : kk, m < kk ? kk : m, F, 0) : 0];
+        v[j >> 2][j & 3] = in ? q : 0.f;
+      }
+      split3(v[0], v[1], sash[ib][0][lane], sash[ib][1][lane], sash[ib][2][lane]);
+    }
+  }
+  __syncthreads();
+  const float cc = ta.c[0];
+  float az[12], ad[4], abot[DPL][kTrainNI], sbot[DPL];
+  float s_top = 0.f, loss = 0.f;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) az[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ad[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < DPL; ++k) {
+    sbot[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kTrainNI; ++i) abot[k][i] = 0.f;
+  }
+  int64_t lo = 0, n_ok = src.n_rows;
+  if (lane < S && src.slot_offsets) {
+    lo = src.slot_offsets[lane];
+    n_ok = src.slot_offsets[lane + 1] - lo;
+  }
+  bool oob = false;
+  auto raw_id = [&](int64_t b) -> int64_t {
+    const int64_t bb = b < last ? b : first;
+    const int ln = lane < S ? lane : S - 1;
+    const int64_t v = ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + ln]
+                           : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + ln]);
+    return lane < S ? v : 0;
+  };
+  auto row_of = [&](int64_t b, int64_t id) -> const float* {
+    const bool live = b < last;
+    const bool id_ok = id >= 0 && id < n_ok;
+    if (lane < S && !id_ok && live) oob = true;
+    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
+    return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
+  };
+  floatx4 a0[NT], a1[NT];
+  floatx4 dn4;
+  float xv, lab;
+  const float* p0 = nullptr;
+  const float* p1 = nullptr;
+  auto load_chunk = [&](int s) {
+    a0[2 * s] = *(gfloatx4*)(p0 + 32 * s + 8 * g);
+    a0[2 * s + 1] = *(gfloatx4*)(p0 + 32 * s + 8 * g + 4);
+    a1[2 * s] = *(gfloatx4*)(p1 + 32 * s + 8 * g);
+    a1[2 * s + 1] = *(gfloatx4*)(p1 + 32 * s + 8 * g + 4);
+  };
+  auto load_side = [&](int64_t b) {
+    const int cl = lane & (DL - 1);
+    const int64_t bb = b < last ? b : first;
+    dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * cl);
+    xv = *(gfloat*)(ta.xin + bb * kTrainNI + (lane < kTrainNI ? lane : 0));
+    lab = *(gfloat*)(ta.label + bb);
+  };
+  if (active) {
+    {
+      const float* mine = row_of(first, raw_id(first));
+      p0 = shfl_ptr(mine, r);
+      p1 = shfl_ptr(mine, 16 + r);
+      load_side(first);
+#pragma unroll
+      for (int s = 0; s < NC; ++s) load_chunk(s);
+    }
+    int64_t id_next = raw_id(first + 1);
+    for (int64_t b = first; b < last; ++b) {
+      int lanev;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
+      const int r = lanev & 15, g = (lanev >> 4) & 3;
+      // X(b+1)'s rows: the chunk loads below go there
+      {
+        const float* nxt = row_of(b + 1, id_next);
+        p0 = shfl_ptr(nxt, r);
+        p1 = shfl_ptr(nxt, 16 + r);
+      }
+      id_next = raw_id(b + 2);
+      const floatx4 dn = dn4;
+      float xb[kTrainNI];
+#pragma unroll
+      for (int i = 0; i < kTrainNI; ++i)
+        xb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
+      const float lb = lab;
+      load_side(b + 1);
+      float* de = ta.grad_emb + b * S * (int64_t)D;
+      floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+      // transposed-read addresses (lane 4q + p of group g: row 8g + 4h + q, columns 4p.. of
+      // 16-column tile tt, halves swapped on the odd 8-row groups)
+      const int q = (lanev >> 2) & 3, p4 = lanev & 3;
+#pragma unroll
+      for (int s = 0; s < NC; ++s) {
+        bf16x8 sa[2][3];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) sa[ib][pt] = sash[ib][pt][lanev & 63];
+        bf16x8 h0, m0, l0, h1, m1, l1;
+        split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
+        split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunk(s);  // X(b+1), chunk s: in flight for a whole example
+        __builtin_amdgcn_sched_barrier(0);
+        c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
+        c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
+        c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);
+        // the parts → the chunk image (rows r and 16 + r, columns 8g .. 8g + 7)
+        *reinterpret_cast<bf16x8*>(img + 0 * kChPlane + ch_off(r, 8 * g)) = h0;
+        *reinterpret_cast<bf16x8*>(img + 1 * kChPlane + ch_off(r, 8 * g)) = m0;
+        *reinterpret_cast<bf16x8*>(img + 2 * kChPlane + ch_off(r, 8 * g)) = l0;
+        *reinterpret_cast<bf16x8*>(img + 0 * kChPlane + ch_off(16 + r, 8 * g)) = h1;
+        *reinterpret_cast<bf16x8*>(img + 1 * kChPlane + ch_off(16 + r, 8 * g)) = m1;
+        *reinterpret_cast<bf16x8*>(img + 2 * kChPlane + ch_off(16 + r, 8 * g)) = l1;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          bf16x8 xp[3];
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) {
+            const int o0 = pt * kChPlane + (8 * g + q) * 64 + 32 * (tt ^ (g & 1)) + 8 * p4;
+            const shortx4 lo4 =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o0));
+            const shortx4 hi4 =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o0 + 4 * 64));
+            const shortx8 v8 = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
+            xp[pt] = __builtin_bit_cast(bf16x8, v8);
+          }
+          floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+          d0 = mfma6_xs(xp[0], xp[1], xp[2], sa[0][0], sa[0][1], sa[0][2], d0);
+          d1 = mfma6_xs(xp[0], xp[1], xp[2], sa[1][0], sa[1][1], sa[1][2], d1);
+          // lane (r, g): U[16 ib + r][32 s + 16 tt + 4g ..+3] → the staging rows (and U's row S,
+          // the bottom-MLP row, to ubot)
+          const int col = 16 * tt + 4 * g;
+          *reinterpret_cast<floatx4*>(stg + r * kChStageLd + col) = d0;
+          *reinterpret_cast<floatx4*>(stg + (16 + r) * kChStageLd + col) = d1;
+          if (r == S) *reinterpret_cast<floatx4*>(ubot + 32 * s + col) = d0;
+          if (16 + r == S) *reinterpret_cast<floatx4*>(ubot + 32 * s + col) = d1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the chunk's 128-B row segments to HBM: 8 rows per store, 8 lanes per row (a 64-B
+        // segment per row and store measured half the rate: tools/microbench_gather.hip)
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const int i = 8 * pp + (lanev >> 3), c8 = lanev & 7;
+          const floatx4 v = *reinterpret_cast<const floatx4*>(stg + i * kChStageLd + 4 * c8);
+          if (i < S)
+            __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 32 * s + 4 * c8));
+        }
+        __builtin_amdgcn_wave_barrier();  // the next chunk's image / staging writes follow
+      }
+      // head, loss, G (dlrm_train_pipe (4))
+      const int cl = lanev & (DL - 1), rg = (lanev / DL) & (RPI - 1);
+      float zr[12];
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        zr[reg] = c00[reg];
+        zr[4 + reg] = c01[reg];
+        zr[8 + reg] = c11[reg];
+      }
+      float hacc = 0.f;
+      {
+        const floatx4* ql = reinterpret_cast<const floatx4*>(&qlane[lanev & 63][0]);
+#pragma unroll
+        for (int q4 = 0; q4 < 3; ++q4) {
+          const floatx4 qv = ql[q4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hacc += zr[4 * q4 + k] * qv[k];
+        }
+        const floatx4 qd = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
+        if (rg == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hacc += dn[k] * qd[k];
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
+      const float p = 1.f / (1.f + expf(-(hacc + cc)));
+      {
+        const float pc = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
+        loss += -(lb * logf(pc + ta.eps) + (1.f - lb) * logf((1.f - pc) + ta.eps));
+      }
+      const bool inside = p >= ta.eps && p <= 1.f - ta.eps;
+      const float pcg = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
+      const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
+      const float dp = inside ? ta.gscale * dbce : 0.f;
+      const float G = dp * (p * (1.f - p));
+      if (lanev == 0) {
+        ta.y[b] = p;
+        g_rows[b] = G;
+      }
+      s_top += G;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ad[k] += dn[k] * G;
+      {  // the bottom-MLP row (dlrm_train_pipe (7)) from U's row S
+        const floatx4 v = *reinterpret_cast<const floatx4*>(ubot + 4 * cl);
+        const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+          const int c = DPL * rg + k;
+          const float gd = __fmul_rn(G, v[c] + qdn[c]);
+          const float gb = dn[c] > 0.f ? gd : 0.f;
+          sbot[k] += gb;
+#pragma unroll
+          for (int ii = 0; ii < kTrainNI; ++ii) abot[k][ii] += xb[ii] * gb;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // the next example's ubot writes follow these reads
+    }
+  }
+  // the wave's partial row → its LDS region, then the block folds its four waves in order
+  __syncthreads();
+  float* X = lds[wave];
+  for (int e = lane; e < TM; e += 64) X[e] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  if (active) {
+    const int cl = lane & (DL - 1), rg = lane / DL;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i0 = 4 * g + reg, j0 = r, i1 = 4 * g + reg, j1 = 16 + r, i2 = 16 + 4 * g + reg, j2 = 16 + r;
+      if (i0 < j0) X[compact_index(i0, j0, F, 0)] = az[reg];
+      if (j1 < F) X[compact_index(i1, j1, F, 0)] = az[4 + reg];
+      if (i2 < j2 && j2 < F) X[compact_index(i2, j2, F, 0)] = az[8 + reg];
+    }
+    if (rg == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) X[nzc + 4 * cl + k] = ad[k];
+    }
+    if (lane == 0) {
+      X[kTrainAtop] = s_top;
+      X[kTrainAtop + 1] = loss;
+    }
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) {
+      const int d = 4 * cl + DPL * rg + k;
+#pragma unroll
+      for (int ii = 0; ii < kTrainNI; ++ii) X[kTrainAtop + 2 + ii * D + d] = abot[k][ii];
+      X[kTrainAtop + 2 + kTrainNI * D + d] = sbot[k];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TM; e += 256) {
+    float v = lds[0][e];
+    v += lds[1][e];
+    v += lds[2][e];
+    v += lds[3][e];
+    ta.part[(int64_t)blockIdx.x * TM + e] = v;
+  }
+  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
+}
+
 template <int GREG, int KS, bool ID64>
 static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode md,
                           const float* gout, int64_t gstride, float* gemb, float* gdense, int,
@@ -1641,12 +1991,12 @@ extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, in
                                        sums, workspace, ws_bytes, err_flag, stream);
 }
 
-extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
+static int32_t train_step_launch(
     const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
     int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
     int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
     float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
-    int32_t* err_flag, void* stream) {
+    int32_t* err_flag, void* stream, float* g_rows) {
   const int F = n_slots + 1;
   RS_CHECK_ARG((D == 128 || D == 64) && n_slots >= 1 && F <= kDxRows && n_in == kTrainNI &&
                    batch >= 1,
@@ -1677,9 +2027,20 @@ extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
     }
     const int epw = epw_cached;
     blocks = ceil_div(batch, 4 * (int64_t)epw);
-    kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, epw);
+    if constexpr (std::is_same_v<decltype(kern), decltype(&dlrm_train_pipe<128, true>)>)
+      kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, epw);
+    else
+      kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw);
   };
-  if (D == 128) {
+  if (g_rows) {  // unit rows U + G[b] (dlrm_train_chunk)
+    if (D == 128) {
+      if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<128, true>);
+      else go(dlrm_train_chunk<128, false>);
+    } else {
+      if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<64, true>);
+      else go(dlrm_train_chunk<64, false>);
+    }
+  } else if (D == 128) {
     if (id_dtype == RS_ID_I64) go(dlrm_train_pipe<128, true>);
     else go(dlrm_train_pipe<128, false>);
   } else {
@@ -1689,4 +2050,27 @@ extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
   RS_CHECK_LAUNCH();
   const int tm = D == 128 ? train_m<128>() : train_m<64>();
   return fold_two_level(part, (int)blocks, tm, part + (size_t)blocks * tm, sums, st);
+}
+
+extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
+    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
+    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
+    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
+    float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
+    int32_t* err_flag, void* stream) {
+  return train_step_launch(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets, dense, xin,
+                           n_in, label, batch, q, c, eps, loss_scale, y, grad_emb, sums,
+                           workspace, ws_bytes, err_flag, stream, nullptr);
+}
+
+extern "C" int32_t rs_dlrm_train_step_fwd_unit(
+    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
+    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
+    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
+    float loss_scale, float* y, float* unit_rows, float* g_rows, float* sums, void* workspace,
+    size_t ws_bytes, int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(g_rows, "null pointer");
+  return train_step_launch(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets, dense, xin,
+                           n_in, label, batch, q, c, eps, loss_scale, y, unit_rows, sums,
+                           workspace, ws_bytes, err_flag, stream, g_rows);
 }

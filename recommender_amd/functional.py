@@ -7,6 +7,7 @@ upstream rows (position order) and ids to the owning EmbeddingTable, and the spa
 from __future__ import annotations
 
 import ctypes as C
+import contextlib
 import os
 
 import torch
@@ -334,6 +335,11 @@ def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float 
 
 TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
 _TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
+# the chunked train kernel (rs_dlrm_train_step_fwd_unit: unit rows + G, the apply scales them);
+# RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows (the row-sharded step always takes those)
+_TRAIN_UNIT = os.environ.get("RS_TRAIN_UNIT", "1") != "0"
+# the train kernel on the fused optimizer's update stream, right before the apply
+_TRAIN_ON_SIDE = os.environ.get("RS_TRAIN_ON_SIDE", "0") == "1"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
@@ -364,6 +370,8 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     S, n_in = model.num_cat_fea, model.num_int_fea
     ids = _ids_flat(cat_features.reshape(-1, S))
     sharded = hasattr(emb, "exchange_begin")
+    side_ctx = contextlib.ExitStack()
+    main = None
     world = comm.world if (sharded and comm is not None) else 1
     if sharded:
         # sort / unique / split sizes beside the bottom MLP (or queued a step ahead: prefetch)
@@ -394,6 +402,14 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         w = emb.weight
         D = w.shape[1]
         dev = w.device
+        if _TRAIN_ON_SIDE and _APPLY_EARLY and getattr(emb.fused_optimizer, "side", None) is not None:
+            # the train kernel and the apply back to back on the update stream: no cross-queue
+            # hop between them, and the dense tail / next bottom MLP (main stream) run beside the
+            # apply; main waits only for the train kernel
+            side = emb.fused_optimizer.side
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)  # h, q, c and the batch
+            side_ctx.enter_context(torch.cuda.stream(side))
         _wait_update(emb)
         # the fused kernel is one round of resident blocks: launched while the sort stream's last
         # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
@@ -412,10 +428,22 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     ws = _train_ws(B, dev)
     n_global = B * world
     scale = 1.0 / n_global if reduction == "mean" else 1.0
-    L.call("rs_dlrm_train_step_fwd_scaled", L.ptr(w), n_rows, D, L.ptr(kid), L.id_dtype_code(kid),
-           S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B, L.ptr(q), L.ptr(c),
-           float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums), L.ptr(ws), ws.numel(),
-           L.ptr(emb.err_flag), L.stream_ptr(dev))
+    g_rows = None
+    if _TRAIN_UNIT and not sharded:
+        g_rows = torch.empty(B, device=dev, dtype=torch.float32)
+        L.call("rs_dlrm_train_step_fwd_unit", L.ptr(w), n_rows, D, L.ptr(kid),
+               L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
+               L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(g_rows),
+               L.ptr(sums), L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
+    else:
+        L.call("rs_dlrm_train_step_fwd_scaled", L.ptr(w), n_rows, D, L.ptr(kid),
+               L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
+               L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums),
+               L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
+    ev_train = None
+    if main is not None:
+        ev_train = torch.cuda.Event()
+        ev_train.record()
     if not sharded and emb._prefetch_queue:
         emb.flush_prefetch()  # a later batch's sort, beside this step's update and dense tail
     if world > 1:
@@ -443,15 +471,20 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     # side stream: 0.907 vs 0.96); RS_APPLY_EARLY=0 restores it
     early = _APPLY_EARLY
     if early:
-        emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+        emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids), row_scale=g_rows)
+    if main is not None:  # back on the main stream, after the train kernel only
+        side_ctx.close()
+        main.wait_event(ev_train)
+        y.record_stream(main)
+        sums.record_stream(main)
     if sgd_lr is not None:
         if not early:
-            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids), row_scale=g_rows)
         _dense_tail_sgd(tl, rows, bl, A_top, s_top, sums[a + 2:].view(n_in + 1, D), sgd_lr)
     else:
         chain_param_grads(tl, rows, [l.kernel for l in tl], A_top, s_top)
         if not early:
-            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids))
+            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids), row_scale=g_rows)
         chain_param_grads(bl, None, bks, A_bot, s_bot, need_q0=False)
     loss = loss_sum / B if reduction == "mean" else loss_sum
     return y, loss

@@ -186,15 +186,13 @@ int main(int argc, char** argv) {
     const double by = (read ? (double)B * (S * 4 + 27 * 512.0) : 0) + (write ? (double)B * S * 512 : 0);
     printf("%-44s blocks/CU %d  %7.1f us  %5.2f TB/s\n", name, blocks_per_cu, us, by / us / 1e6);
   };
-  for (int bpc : {1, 2, 3}) {
+  for (int bpc : {1, 2, 3, 4}) {
+    run("zipf  d1 rd only", pattern_k<1, 0, 0>, zipf, bpc, false);
+    run("zipf  d2 rd only", pattern_k<2, 0, 0>, zipf, bpc, false);
     run("zipf  d1 rd+wr nt", pattern_k<1, 0, 3>, zipf, bpc, true);
-    run("zipf  d1 rd+wr nt +208mfma", pattern_k<1, 208, 3>, zipf, bpc, true);
-    run("zipf  d2 rd+wr nt +208mfma", pattern_k<2, 208, 3>, zipf, bpc, true);
-    run("zipf  d1 rd+wr nt +84mfma", pattern_k<1, 84, 3>, zipf, bpc, true);
-    run("zipf  d2 rd+wr nt +84mfma", pattern_k<2, 84, 3>, zipf, bpc, true);
+    run("zipf  d2 rd+wr nt", pattern_k<2, 0, 3>, zipf, bpc, true);
+    run("zipf  d1 rd+wr 64B rows", pattern_k<1, 0, 1>, zipf, bpc, true);
     run("zipf  d1 rd+wr nt +84mfma +300valu", pattern_k<1, 84, 3, true, 300>, zipf, bpc, true);
-    run("zipf  d2 rd+wr nt +84mfma +300valu", pattern_k<2, 84, 3, true, 300>, zipf, bpc, true);
-    run("zipf  d1 rd+wr nt +600valu", pattern_k<1, 0, 3, true, 600>, zipf, bpc, true);
   }
   return 0;
 }
