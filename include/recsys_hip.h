@@ -133,6 +133,14 @@ int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sort
                                 int64_t n_ids, const float* grad_out, int32_t dim, int64_t n_rows,
                                 uint32_t* uniq_rows, float* uniq_grad, void* workspace,
                                 size_t ws_bytes, void* stream);
+/* rs_embedding_dedup_grad with the gradient of position p read as row_scale[p / scale_group] *
+ * grad_out[p] (one fmul_rn, as rs_embedding_apply_scaled): the row-sharded DLRM step's unit rows
+ * and G[b] (rs_dlrm_train_step_fwd_unit). row_scale NULL = rs_embedding_dedup_grad. */
+int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                       int64_t n_ids, const float* grad_out,
+                                       const float* row_scale, int32_t scale_group, int32_t dim,
+                                       int64_t n_rows, uint32_t* uniq_rows, float* uniq_grad,
+                                       void* workspace, size_t ws_bytes, void* stream);
 
 /* The deduplicated gradient as a dense [n_rows, dim] tensor: rows without ids 0, every other row
  * its segment sum (same additions, same order as rs_embedding_dedup_grad); dense is fully written.

@@ -1072,11 +1072,29 @@ extern "C" size_t rs_dedup_workspace_size(int64_t n_ids, int32_t dim) {
          exclusive_scan_ws_size(n_ids) + 256;
 }
 
+extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
+                                                  const int32_t* sorted_pos, int64_t n_ids,
+                                                  const float* grad_out, const float* row_scale,
+                                                  int32_t scale_group, int32_t dim, int64_t n_rows,
+                                                  uint32_t* uniq_rows, float* uniq_grad,
+                                                  void* workspace, size_t ws_bytes, void* stream);
+
 extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const int32_t* sorted_pos,
                                            int64_t n_ids, const float* grad_out, int32_t dim,
                                            int64_t n_rows, uint32_t* uniq_rows, float* uniq_grad,
                                            void* workspace, size_t ws_bytes, void* stream) {
+  return rs_embedding_dedup_grad_scaled(sorted_rows, sorted_pos, n_ids, grad_out, nullptr, 1, dim,
+                                        n_rows, uniq_rows, uniq_grad, workspace, ws_bytes, stream);
+}
+
+extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
+                                                  const int32_t* sorted_pos, int64_t n_ids,
+                                                  const float* grad_out, const float* row_scale,
+                                                  int32_t scale_group, int32_t dim, int64_t n_rows,
+                                                  uint32_t* uniq_rows, float* uniq_grad,
+                                                  void* workspace, size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(!row_scale || scale_group >= 1, "scale_group must be >= 1");
   if (n_ids == 0) return RS_OK;
   RS_CHECK_ARG(sorted_rows && sorted_pos && grad_out && uniq_rows && uniq_grad, "null pointer");
   if (ws_bytes < rs_dedup_workspace_size(n_ids, dim)) {
@@ -1101,6 +1119,8 @@ extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const in
   a.uniq_grad = uniq_grad;
   a.uniq_rows = uniq_rows;
   a.seg_excl = seg;
+  a.row_scale = row_scale;
+  a.scale_group = scale_group;
   const void* ptrs[2] = {grad_out, uniq_grad};
   RowGeom geom = row_geom(dim, ptrs, 2);
   return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);

@@ -1199,10 +1199,11 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t
 //   loads   X(b+1)'s chunk s is issued into the registers just freed, so every chunk's loads
 //           have a whole example of latency cover (no second register set);
 //   image   the six bf16x8 parts go to a 6 KB per-wave LDS image [part][32 rows][32 columns]
-//           (the two 16-column halves of rows 8-15 / 24-31 swapped: conflict-free transposed
-//           reads), read back column-major with ds_read_b64_tr_b16 as the A operand of
+//           (chunk-swizzled, ch_off: conflict-free writes and transposed reads), read back
+//           column-major with ds_read_b64_tr_b16 as the A operand of
 //   Uᵀ      Uᵀ = Xᵀ·(M + Mᵀ) for the chunk's two 16-column tiles: the MFMA result puts four
-//           consecutive columns of one U row in each lane, so the rows go straight to HBM.
+//           consecutive columns of one U row in each lane; a 4.5 KB staging tile turns them
+//           into 128-B row segments for the stores (64-B segments measured half the rate).
 // U is written UNSCALED (the head's G needs all of Z, known only after the last chunk) and G[b]
 // goes to g_rows: the apply multiplies each gradient row by its example's G
 // (rs_embedding_apply_scaled, row_scale = g_rows, scale_group = n_slots) with the same fmul_rn,
@@ -1229,9 +1230,14 @@ __device__ __forceinline__ floatx4 mfma6_xs(const bf16x8& xh, const bf16x8& xm, 
 
 constexpr int kChPlane = 32 * 32 * 2;  // one part of the chunk image: 32 rows x 32 bf16
 constexpr int kChImage = 3 * kChPlane;  // bytes
-// byte offset of (row, 8-column group) in a plane: halves of rows 8-15 / 24-31 swapped
+// byte offset of (row, column) in a plane: 64-B rows of four 16-B chunks (8 columns each), the
+// chunk index XOR-swizzled by row bits 1-2 and 3. Conflict-free both ways (MI355X_MICROARCH
+// §LDS): a ds_write_b128 group (8 lanes = 8 consecutive rows, one logical chunk) covers 32
+// distinct banks mod 32, and a ds_read_b64_tr_b16 half-wave (rows 4h + q and 8 + 4h + q, one
+// 16-column tile) gets rows 8 apart on the other chunk pair: 64 distinct banks mod 64
 __device__ __forceinline__ int ch_off(int row, int col) {
-  return row * 64 + 2 * (col ^ (((row >> 3) & 1) << 4));
+  const int chunk = (col >> 3) ^ ((row >> 1) & 3) ^ (((row >> 3) & 1) << 1);
+  return row * 64 + 16 * chunk + 2 * (col & 7);
 }
 constexpr int kChStageLd = 36;  // fp32 U staging rows [32][36]: 32 columns + 4 of padding
 template <int D>
@@ -1377,7 +1383,7 @@ __global__ __launch_bounds__(256, RS_TRAIN_CHUNK_OCC) void dlrm_train_chunk(Gath
       float* de = ta.grad_emb + b * S * (int64_t)D;
       floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
       // transposed-read addresses (lane 4q + p of group g: row 8g + 4h + q, columns 4p.. of
-      // 16-column tile tt, halves swapped on the odd 8-row groups)
+      // 16-column tile tt, through ch_off's swizzle)
       const int q = (lanev >> 2) & 3, p4 = lanev & 3;
 #pragma unroll
       for (int s = 0; s < NC; ++s) {
@@ -1408,11 +1414,12 @@ __global__ __launch_bounds__(256, RS_TRAIN_CHUNK_OCC) void dlrm_train_chunk(Gath
           bf16x8 xp[3];
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
-            const int o0 = pt * kChPlane + (8 * g + q) * 64 + 32 * (tt ^ (g & 1)) + 8 * p4;
+            const int o0 = pt * kChPlane + ch_off(8 * g + q, 16 * tt + 4 * p4);
+            const int o1 = pt * kChPlane + ch_off(8 * g + 4 + q, 16 * tt + 4 * p4);
             const shortx4 lo4 =
                 __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o0));
             const shortx4 hi4 =
-                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o0 + 4 * 64));
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o1));
             const shortx8 v8 = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
             xp[pt] = __builtin_bit_cast(bf16x8, v8);
           }

@@ -336,7 +336,7 @@ def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float 
 TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
 _TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
 # the chunked train kernel (rs_dlrm_train_step_fwd_unit: unit rows + G, the apply scales them);
-# RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows (the row-sharded step always takes those)
+# RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows
 _TRAIN_UNIT = os.environ.get("RS_TRAIN_UNIT", "1") != "0"
 # the train kernel on the fused optimizer's update stream, right before the apply
 _TRAIN_ON_SIDE = os.environ.get("RS_TRAIN_ON_SIDE", "0") == "1"
@@ -429,7 +429,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     n_global = B * world
     scale = 1.0 / n_global if reduction == "mean" else 1.0
     g_rows = None
-    if _TRAIN_UNIT and not sharded:
+    if _TRAIN_UNIT:
         g_rows = torch.empty(B, device=dev, dtype=torch.float32)
         L.call("rs_dlrm_train_step_fwd_unit", L.ptr(w), n_rows, D, L.ptr(kid),
                L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
@@ -457,7 +457,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     s_bot = sums[a + 2 + n_in * D:]
     if sharded:
         # the gradient rows (already of the global mean loss) go to their owners' apply
-        emb.backward_exchange(grad, global_grads=True)
+        emb.backward_exchange(grad, global_grads=True, row_scale=g_rows)
         if sgd_lr is not None:
             _dense_tail_sgd(tl, rows, bl, A_top, s_top, sums[a + 2:].view(n_in + 1, D), sgd_lr)
         else:

@@ -245,10 +245,13 @@ class ShardedSlabEmbedding(nn.Module):
         pass
 
     # ---------------------------------------------------------------- backward
-    def backward_exchange(self, grad_rows: torch.Tensor, global_grads: bool = False):
+    def backward_exchange(self, grad_rows: torch.Tensor, global_grads: bool = False,
+                          row_scale: torch.Tensor | None = None):
         """global_grads: the rows are gradients of the GLOBAL mean loss (the fused DLRM step's
         kernel scales by 1/(B·W)), so the owners apply them as they are; otherwise each rank's
-        rows are of its local mean and the update is scaled 1/W."""
+        rows are of its local mean and the update is scaled 1/W. row_scale [B] (optional): the
+        row of position p is row_scale[p // S] * grad_rows[p] (the fused step's unit rows and
+        G[b]), formed inside the local segmented sum."""
         st = self._st
         if st is None:
             raise RuntimeError("backward without a forward exchange")
@@ -263,9 +266,17 @@ class ShardedSlabEmbedding(nn.Module):
             uniq_grad = torch.empty(max(s.n, 1), D, dtype=torch.float32, device=dev)
             if s.n:
                 w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(s.n, D), dev)
-                L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g), D,
-                       self.key_space, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(),
-                       L.stream_ptr(dev))
+                if row_scale is None:
+                    L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g),
+                           D, self.key_space, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w),
+                           w.numel(), L.stream_ptr(dev))
+                else:
+                    if row_scale.numel() * self.n_slots != s.n:
+                        raise ValueError("row_scale must hold one value per example")
+                    L.call("rs_embedding_dedup_grad_scaled", L.ptr(s.rows), L.ptr(s.pos), s.n,
+                           L.ptr(g), L.ptr(row_scale), self.n_slots, D, self.key_space,
+                           L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(),
+                           L.stream_ptr(dev))
             recv_grad = torch.empty(R, D, dtype=torch.float32, device=dev)
             self.comm.all_to_all(recv_grad, uniq_grad[:U], st["recv_counts"], st["send_counts"])
             if self.optimizer is None:
@@ -287,6 +298,8 @@ class ShardedSlabEmbedding(nn.Module):
                 L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
                        t.input_dim, t.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
         g.record_stream(self.side)
+        if row_scale is not None:
+            row_scale.record_stream(self.side)
         self._st = None
 
     def join(self):

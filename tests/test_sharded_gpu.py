@@ -175,10 +175,13 @@ def _fused_dlrm_world2_worker(rank, world, port, q):
         cap = {}
         bx = emb.backward_exchange
 
-        def spy(grad_rows, global_grads=False):
-            cap["g"] = grad_rows.detach().clone()
+        def spy(grad_rows, global_grads=False, row_scale=None):
+            g_ = grad_rows.detach().clone()
+            if row_scale is not None:  # unit rows + G[b]: the rows the dedup forms (fmul_rn)
+                g_ = row_scale.repeat_interleave(S)[:, None] * g_
+            cap["g"] = g_
             assert global_grads
-            return bx(grad_rows, global_grads=global_grads)
+            return bx(grad_rows, global_grads=global_grads, row_scale=row_scale)
 
         emb.backward_exchange = spy
         batch = tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb))
