@@ -209,9 +209,9 @@ __device__ __forceinline__ void finalize_row(const ApplyArgs& a, uint32_t row, i
     int col = (gl + c * lpr) * VEC;
     if (col < a.dim) finalize_chunk<OPT, VEC>(a, row, col, acc[c], seg_id);
   }
-  if constexpr (OPT == OPT_KERAS) {
-    if (gl == 0) atomicOr(a.bitmap + (row >> 5), 1u << (row & 31));
-  }
+  // (Keras' touched-row bitmap is marked by keras_bitmap_mark_kernel after the walk: an atomic
+  // here, inlined into every emit of the unrolled walk, took the Keras walk past 128 VGPRs —
+  // 495 spilled registers, 1.6 ms per apply instead of ≈0.3)
   if constexpr (OPT == OPT_EMIT) {
     if (gl == 0) a.uniq_rows[seg_id] = row;
   }
@@ -966,6 +966,17 @@ struct Noop {};
     }                                                                     \
   } while (0)
 
+// Keras Adam's touched-row bitmap: every distinct valid row of the sorted keys (the rows the
+// walk finalised), one atomicOr per segment head; OR is order-free, so the bitmap is exact
+__global__ __launch_bounds__(256) void keras_bitmap_mark_kernel(const uint32_t* __restrict__ keys,
+                                                               int64_t n, uint32_t n_rows,
+                                                               uint32_t* __restrict__ bitmap) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    const uint32_t row = keys[k];
+    if (row < n_rows && (k == 0 || keys[k - 1] != row)) atomicOr(bitmap + (row >> 5), 1u << (row & 31));
+  }
+}
+
 static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos, int64_t n,
                                int64_t n_rows, const float* grad, const ApplyArgs& a,
                                const RowGeom& geom, hipStream_t st) {
@@ -1017,7 +1028,11 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
   switch (opt) {
     case OPT_SGD: RS_SEG_LAUNCH(OPT_SGD); break;
     case OPT_LAZY: RS_SEG_LAUNCH(OPT_LAZY); break;
-    case OPT_KERAS: RS_SEG_LAUNCH(OPT_KERAS); break;
+    case OPT_KERAS:
+      RS_SEG_LAUNCH(OPT_KERAS);
+      keras_bitmap_mark_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 2048), 256, 0, st>>>(
+          keys, n, (uint32_t)n_rows, a.bitmap);
+      break;
     case OPT_EMIT: RS_SEG_LAUNCH(OPT_EMIT); break;
     case OPT_DENSE: RS_SEG_LAUNCH(OPT_DENSE); break;
     default: set_error("unknown optimizer %d", opt); return RS_E_INVALID;
