@@ -1246,11 +1246,8 @@ constexpr int chunk_region_floats() {
                                                              : train_m<D>();
 }
 
-#ifndef RS_TRAIN_CHUNK_OCC
-#define RS_TRAIN_CHUNK_OCC 2
-#endif
 template <int D, bool ID64>
-__global__ __launch_bounds__(256, RS_TRAIN_CHUNK_OCC) void dlrm_train_chunk(GatherSrc src, int64_t batch, int F,
+__global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_t batch, int F,
                                                         TrainArgs ta, float* g_rows, int epw) {
   static_assert(D == 64 || D == 128, "train kernel laid out for D = 64 or 128");
   constexpr int NT = D / 16, NC = D / 32, DL = D / 4, RPI = 64 / DL, DPL = D / 64;

@@ -7,7 +7,6 @@ upstream rows (position order) and ids to the owning EmbeddingTable, and the spa
 from __future__ import annotations
 
 import ctypes as C
-import contextlib
 import os
 
 import torch
@@ -338,8 +337,6 @@ _TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
 # the chunked train kernel (rs_dlrm_train_step_fwd_unit: unit rows + G, the apply scales them);
 # RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows
 _TRAIN_UNIT = os.environ.get("RS_TRAIN_UNIT", "1") != "0"
-# the train kernel on the fused optimizer's update stream, right before the apply
-_TRAIN_ON_SIDE = os.environ.get("RS_TRAIN_ON_SIDE", "0") == "1"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
@@ -370,8 +367,6 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     S, n_in = model.num_cat_fea, model.num_int_fea
     ids = _ids_flat(cat_features.reshape(-1, S))
     sharded = hasattr(emb, "exchange_begin")
-    side_ctx = contextlib.ExitStack()
-    main = None
     world = comm.world if (sharded and comm is not None) else 1
     if sharded:
         # sort / unique / split sizes beside the bottom MLP (or queued a step ahead: prefetch)
@@ -402,14 +397,6 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         w = emb.weight
         D = w.shape[1]
         dev = w.device
-        if _TRAIN_ON_SIDE and _APPLY_EARLY and getattr(emb.fused_optimizer, "side", None) is not None:
-            # the train kernel and the apply back to back on the update stream: no cross-queue
-            # hop between them, and the dense tail / next bottom MLP (main stream) run beside the
-            # apply; main waits only for the train kernel
-            side = emb.fused_optimizer.side
-            main = torch.cuda.current_stream(dev)
-            side.wait_stream(main)  # h, q, c and the batch
-            side_ctx.enter_context(torch.cuda.stream(side))
         _wait_update(emb)
         # the fused kernel is one round of resident blocks: launched while the sort stream's last
         # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
@@ -440,10 +427,6 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
                L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
                L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums),
                L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
-    ev_train = None
-    if main is not None:
-        ev_train = torch.cuda.Event()
-        ev_train.record()
     if not sharded and emb._prefetch_queue:
         emb.flush_prefetch()  # a later batch's sort, beside this step's update and dense tail
     if world > 1:
@@ -472,11 +455,6 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     early = _APPLY_EARLY
     if early:
         emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids), row_scale=g_rows)
-    if main is not None:  # back on the main stream, after the train kernel only
-        side_ctx.close()
-        main.wait_event(ev_train)
-        y.record_stream(main)
-        sums.record_stream(main)
     if sgd_lr is not None:
         if not early:
             emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids), row_scale=g_rows)
