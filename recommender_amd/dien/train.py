@@ -83,6 +83,7 @@ class DIENStep:
             self.opt_graph = GraphKerasAdam(self._gdense + [t.weight for t in tables],
                                             lr=self.opt_dense.param_groups[0]["lr"])
             self._ws = _Workspace()
+            self.opt_sparse.release_state()  # the graph path's Adam state is opt_graph's
         for p in self._gdense:
             p.grad = None
         if self.is_dien:
@@ -95,9 +96,11 @@ class DIENStep:
         self.last_pred = pred.detach()
         total.backward()
         grads = [p.grad for p in self._gdense]  # None: Keras skips the variable
-        for t in tables:
+        nd = len(self._gdense)
+        for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
             got = t.take_grad(with_valid=True)
-            grads.append(densify_grad(t, got[0], got[1], self._ws, valid=got[2])
+            grads.append(densify_grad(t, got[0], got[1], self._ws, valid=got[2],
+                                      out=self.opt_graph.grad_view(nd + i))
                          if got is not None else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()

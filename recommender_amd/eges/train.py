@@ -80,13 +80,15 @@ class EGESStep:
         if getattr(self, "opt_graph", None) is None:
             self.opt_graph = GraphKerasAdam([t.weight for t in tables], lr=self.opt.lr)
             self._ws = _Workspace()
+            self.opt.release_state()  # the graph path's Adam state is opt_graph's
         logits = self.model(inputs)
         loss = F.binary_cross_entropy_with_logits(logits, labels)
         loss.backward()
         grads = []
-        for t in tables:
+        for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
             got = t.take_grad()
-            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
+            grads.append(densify_grad(t, got[0], got[1], self._ws,
+                                      out=self.opt_graph.grad_view(i)) if got is not None
                          else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()

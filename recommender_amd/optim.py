@@ -316,7 +316,16 @@ class SparseAdam(SparseOptimizer):
         self._materialized = 0
 
     def _slots(self, t):
+        if self.state is None:
+            raise RuntimeError("SparseAdam state released (the step's graph path owns the Adam "
+                               "state: GraphKerasAdam); do not interleave the two paths")
         return self.state[id(t)]
+
+    def release_state(self):
+        """Free m / v / bitmaps: a static (graph-capturable) step keeps its own Keras Adam state
+        (GraphKerasAdam), so these would be 2x the tables' memory held for nothing."""
+        self.state = None
+        self.last = {}
 
     def _lr_of_step(self, s):
         lr = self.lr(s - 1) if callable(self.lr) else self.lr
@@ -438,6 +447,10 @@ class GraphKerasAdam:
                 p.data = self.flat[o:o + n].view_as(p)
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
+        # the step's gradients in the same layout (padding stays 0): a table's densified gradient
+        # is written straight into its view (densify_grad(out=grad_view(i))), other gradients
+        # are copied in — no per-step concat of every gradient
+        self.grad_flat = torch.zeros_like(self.flat)
         self.iterations = 0
         self.window = int(window)
         self._lr = torch.empty(self.window, dtype=torch.float32, device=dev)
@@ -456,6 +469,11 @@ class GraphKerasAdam:
         if self.iterations - self._base >= self.window:
             self._base = self.iterations
             self._fill()
+
+    def grad_view(self, i: int) -> torch.Tensor:
+        """Parameter i's slice of the flat gradient buffer, shaped like the parameter."""
+        o, n, _ = self._segs[i]
+        return self.grad_flat[o:o + n].view_as(self.params[i])
 
     @torch.no_grad()
     def apply(self, grads):
@@ -476,36 +494,40 @@ class GraphKerasAdam:
                 runs.append(cur)
             cur[1] = i
         for a, b in runs:
-            parts = []
-            for g, (_, n, pad) in zip(grads[a:b + 1], self._segs[a:b + 1]):
-                parts.append(g.reshape(-1))
-                if pad:
-                    parts.append(g.new_zeros(pad))
-            gflat = torch.cat(parts) if len(parts) > 1 else parts[0].contiguous()
+            for i in range(a, b + 1):
+                dst = self.grad_view(i)
+                if grads[i].data_ptr() != dst.data_ptr():
+                    dst.copy_(grads[i].reshape(dst.shape))
             o = self._segs[a][0]
-            n = gflat.numel()
+            ob, nb, pb = self._segs[b]
+            n = ob + nb + pb - o
             L.call("rs_keras_adam_flat", L.ptr(self.flat[o:]), L.ptr(self.m[o:]),
-                   L.ptr(self.v[o:]), L.ptr(gflat), n, L.ptr(self._lr), L.ptr(self._idx), c,
-                   L.stream_ptr(dev))
+                   L.ptr(self.v[o:]), L.ptr(self.grad_flat[o:]), n, L.ptr(self._lr),
+                   L.ptr(self._idx), c, L.stream_ptr(dev))
         self._idx.add_(1)
 
 
 def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
-                 ws: _Workspace | None = None, valid: torch.Tensor | None = None) -> torch.Tensor:
+                 ws: _Workspace | None = None, valid: torch.Tensor | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
     """The IndexedSlices gradient as a dense [input_dim, dim] tensor with no host sync. Small
     tables (input_dim·dim <= 16384): rs_embedding_grad_dense_small (one pass, fixed block /
     lane order); others: deterministic segmented sum (rs_embedding_grad_dense: position order
     per row, each row's sum stored in place, untouched rows 0). valid (uint8 per id, optional):
     positions flagged 0 are left out — for lookups whose masked positions carry no gradient
-    (Embedding.accumulate_grad's valid)."""
+    (Embedding.accumulate_grad's valid). out (optional, contiguous fp32 [input_dim, dim]): the
+    gradient is written there (every element) instead of into a new tensor."""
     ws = ws or _Workspace()
     dev = table.weight.device
     dim, V = table.output_dim, table.input_dim
+    if out is not None and (tuple(out.shape) != (V, dim) or out.dtype != torch.float32
+                            or not out.is_contiguous()):
+        raise ValueError("out must be a contiguous fp32 [input_dim, dim] tensor")
     if valid is None and V * dim <= 16384 and dim <= 256 and dim & (dim - 1) == 0:
         # small table (PinSage year / genre): one pass, per-block LDS copies, no sort
         ids = ids.reshape(-1).contiguous()
         n = ids.numel()
-        dense = torch.empty(V, dim, dtype=torch.float32, device=dev)
+        dense = out if out is not None else torch.empty(V, dim, dtype=torch.float32, device=dev)
         w = ws.get("dense_small", L.lib().rs_embedding_grad_dense_small_workspace_size(n, V, dim),
                    dev)
         L.call("rs_embedding_grad_dense_small", L.ptr(ids), L.id_dtype_code(ids), n,
@@ -514,7 +536,7 @@ def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
         return dense
     s = SortedIds.for_table(table, ids, ws, count_unique=False, valid=valid)
     n = s.n
-    dense = torch.empty(V, dim, dtype=torch.float32, device=dev)
+    dense = out if out is not None else torch.empty(V, dim, dtype=torch.float32, device=dev)
     w = ws.get("dense", L.lib().rs_apply_workspace_size(n, dim), dev)
     L.call("rs_embedding_grad_dense", L.ptr(s.rows), L.ptr(s.pos), n, L.ptr(grad_rows.contiguous()),
            dim, V, L.ptr(dense), L.ptr(w), w.numel(), L.stream_ptr(dev))

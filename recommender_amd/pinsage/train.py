@@ -91,15 +91,18 @@ class PinSageStep:
             self.opt_graph = GraphKerasAdam(self.dense + [t.weight for t in tables],
                                             lr=self.opt_dense.param_groups[0]["lr"])
             self._ws = _Workspace()
+            self.opt_sparse.release_state()  # the graph path's Adam state is opt_graph's
         for p in self.dense:
             p.grad = None
         pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
         loss = margin_loss(pos_score, neg_score, 1.0, pos_graph.valid, pos_graph.n_valid)
         loss.backward()
         grads = [p.grad for p in self.dense]  # None: Keras skips the variable
-        for t in tables:
+        nd = len(self.dense)
+        for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
             got = t.take_grad()
-            grads.append(densify_grad(t, got[0], got[1], self._ws) if got is not None
+            grads.append(densify_grad(t, got[0], got[1], self._ws,
+                                      out=self.opt_graph.grad_view(nd + i)) if got is not None
                          else None)
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()
