@@ -213,6 +213,7 @@ def main():
             batches.append(((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev),
                              torch.from_numpy(lb).to(dev)),))
         step = step0
+        cfg2_batches = list(batches)
         if args.cfg2_graph and args.optimizer == "sgd":
             for b in batches:  # eager warm-up (compositions, caches) before capture
                 step0(*b)
@@ -260,6 +261,20 @@ def main():
            "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k}
     if args.model == "deepfm":
         out["cpu_baseline"] = deepfm_cpu_baseline(B)
+    if args.model == "dlrm_cfg2":
+        # SURVEY 8(d)'s path bytes per step at the measured unique-row count (fwd S(id + 8D) +
+        # bwd S(id + 4D) + (U/B)·8D per example) over the WHOLE step time (dense half included:
+        # a lower bound on the path's own fraction, which graph replay does not time apart)
+        S_, D_ = 26, 64
+        offs = torch.arange(S_, device=dev, dtype=torch.int64) * per
+        Us = [int(torch.unique(b[0][0].reshape(-1, S_).to(torch.int64) + offs).numel())
+              for b in cfg2_batches]
+        U = sum(Us) / len(Us)
+        by = B * (S_ * (8 + 8 * D_) + S_ * (8 + 4 * D_)) + U * 8 * D_
+        gbs = by / sec / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                           "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
+                           "unique_rows_per_step": U, "note": "path bytes / whole step time"}
     print(json.dumps(out))
 
 
