@@ -13,8 +13,13 @@
 namespace rs {
 
 constexpr int kSortThreads = 256;         // 4 waves
-constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile
+constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile (large sorts)
 constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
+// small sorts (cfg2's 213k ids, DeepFM's 27k, DIEN's tables) take 1024-key tiles: 4x the blocks
+// per launch for a latency-bound pass that would otherwise run on a few dozen CUs
+constexpr int kSortKeysPerLaneSmall = 4;
+constexpr int64_t kSortSmallN = 1 << 20;
+static inline int sort_kpl(int64_t n) { return n < kSortSmallN ? kSortKeysPerLaneSmall : kSortKeysPerLane; }
 constexpr int kMaxBins = 512;
 
 // match mask: lanes of this wave whose digit equals mine
@@ -62,7 +67,7 @@ __device__ __forceinline__ uint32_t make_key(const KeyGen& g, int64_t i, bool& o
 // histogram: hist[digit * n_tiles + tile]. Equal digits inside a wave are aggregated by a
 // ballot match so skewed (Zipf) keys do not serialise on one LDS counter. FROM_IDS: pass 0 of
 // an id sort — the keys are made from the ids here and stored to `keys` for the later passes.
-template <int BITS, bool FROM_IDS>
+template <int BITS, bool FROM_IDS, int KPL = kSortKeysPerLane>
 __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     uint32_t* __restrict__ keys, KeyGen kg, int64_t n, int shift, int32_t* __restrict__ hist,
     int n_tiles) {
@@ -78,11 +83,11 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     for (int e = threadIdx.x; e <= kg.n_slots; e += blockDim.x) offs[e] = kg.slot_offsets[e];
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  uint32_t kv[kSortKeysPerLane];
+  const int64_t base = (int64_t)blockIdx.x * (kSortThreads * KPL);
+  uint32_t kv[KPL];
   bool oob = false;
 #pragma unroll
-  for (int k = 0; k < kSortKeysPerLane; ++k) {
+  for (int k = 0; k < KPL; ++k) {
     const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
     if (FROM_IDS) {
       if (lds_slots) {
@@ -114,7 +119,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     }
   }
 #pragma unroll
-  for (int k = 0; k < kSortKeysPerLane; ++k) {
+  for (int k = 0; k < KPL; ++k) {
     const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
     const bool valid = i < n;
     const uint32_t d = (kv[k] >> shift) & (BINS - 1);
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(256) void radix_colscan_kernel(int32_t* __restrict_
 // out in that order: consecutive lanes store consecutive addresses of one digit's run instead of
 // each lane storing to its own bin (measured before the reorder: pass 0, whose low digits are
 // spread over all 512 bins, 31 us; the same pass as direct per-lane stores).
-template <int BITS, bool IOTA_VALS>
+template <int BITS, bool IOTA_VALS, int KPL = kSortKeysPerLane>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, int64_t n, int shift,
     const int32_t* __restrict__ hist_scanned, const int32_t* __restrict__ totals, int n_tiles,
@@ -185,18 +190,18 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   __shared__ int32_t lstart[BINS];       // digit start inside the tile's reordered keys
   __shared__ int32_t doff[BINS];         // global destination of reordered slot j = doff[d] + j
   __shared__ int32_t wsum[2][WAVES];
-  __shared__ uint32_t sk[kSortTile];
-  __shared__ int32_t sv[kSortTile];
+  __shared__ uint32_t sk[kSortThreads * KPL];
+  __shared__ int32_t sv[kSortThreads * KPL];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int d = threadIdx.x; d < WAVES * BINS; d += blockDim.x) (&wcnt[0][0])[d] = 0;
 
-  const int64_t tile0 = (int64_t)blockIdx.x * kSortTile;
-  const int64_t base = tile0 + (int64_t)wave * 64 * kSortKeysPerLane;
-  uint32_t key[kSortKeysPerLane];
-  int32_t val[kSortKeysPerLane];
-  int32_t rank[kSortKeysPerLane];
+  const int64_t tile0 = (int64_t)blockIdx.x * (kSortThreads * KPL);
+  const int64_t base = tile0 + (int64_t)wave * 64 * KPL;
+  uint32_t key[KPL];
+  int32_t val[KPL];
+  int32_t rank[KPL];
 #pragma unroll
-  for (int k = 0; k < kSortKeysPerLane; ++k) {
+  for (int k = 0; k < KPL; ++k) {
     int64_t i = base + k * 64 + lane;
     bool valid = i < n;
     key[k] = valid ? keys_in[i] : 0u;
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   __syncthreads();  // wcnt zeroed
   const uint64_t lt = lanemask_lt64();
 #pragma unroll
-  for (int k = 0; k < kSortKeysPerLane; ++k) {
+  for (int k = 0; k < KPL; ++k) {
     int64_t i = base + k * 64 + lane;
     bool valid = i < n;
     uint32_t d = (key[k] >> shift) & (BINS - 1);
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   __syncthreads();
   // reorder the tile by digit in LDS (stable)
 #pragma unroll
-  for (int k = 0; k < kSortKeysPerLane; ++k) {
+  for (int k = 0; k < KPL; ++k) {
     int64_t i = base + k * 64 + lane;
     if (i < n) {
       const uint32_t d = (key[k] >> shift) & (BINS - 1);
@@ -288,7 +293,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     }
   }
   __syncthreads();
-  const int tile_n = (int)(n - tile0 < kSortTile ? n - tile0 : kSortTile);
+  const int tile_n = (int)(n - tile0 < kSortThreads * KPL ? n - tile0 : kSortThreads * KPL);
   for (int j = threadIdx.x; j < tile_n; j += kSortThreads) {
     const uint32_t k = sk[j];
     const int32_t dst = doff[(k >> shift) & (BINS - 1)] + j;
@@ -371,6 +376,7 @@ static int key_bits_for(int64_t n_rows) {
 struct SortPlan {
   int passes;
   int bits;   // per pass
+  int kpl;    // keys per lane per tile
   int n_tiles;
 };
 
@@ -379,7 +385,8 @@ static SortPlan plan_sort(int64_t n_ids, int64_t n_rows) {
   int kb = key_bits_for(n_rows);
   p.passes = (kb + 8) / 9;  // digits of <= 9 bits (512 bins): 3 passes for 40M rows
   p.bits = (kb + p.passes - 1) / p.passes;
-  p.n_tiles = (int)ceil_div(n_ids, kSortTile);
+  p.kpl = sort_kpl(n_ids);
+  p.n_tiles = (int)ceil_div(n_ids, (int64_t)kSortThreads * p.kpl);
   return p;
 }
 
@@ -390,7 +397,7 @@ size_t exclusive_scan_ws_size(int64_t n);
 // workspace: keys_alt[n], vals_alt[n], hist[BINS * n_tiles], digit totals[BINS]
 static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int32_t** vals_alt,
                              int32_t** hist, int32_t** totals) {
-  int n_tiles = (int)ceil_div(n_ids, kSortTile);
+  int n_tiles = (int)ceil_div(n_ids, (int64_t)kSortThreads * sort_kpl(n_ids));
   *keys_alt = c.take<uint32_t>(n_ids);
   *vals_alt = c.take<int32_t>(n_ids);
   *hist = c.take<int32_t>((size_t)kMaxBins * n_tiles + 1);
@@ -399,20 +406,31 @@ static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int3
 }
 
 // one LSD pass = 3 launches: tile histograms, per-digit scan over tiles, stable scatter
-template <int BITS, bool FIRST_FROM_IDS>
-static int32_t launch_pass(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
-                           int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
-                           const KeyGen& kg, hipStream_t st) {
-  radix_hist_kernel<BITS, FIRST_FROM_IDS><<<n_tiles, kSortThreads, 0, st>>>(kin, kg, n, shift, hist,
-                                                                            n_tiles);
+template <int BITS, bool FIRST_FROM_IDS, int KPL>
+static int32_t launch_pass_k(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                             int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
+                             const KeyGen& kg, hipStream_t st) {
+  radix_hist_kernel<BITS, FIRST_FROM_IDS, KPL><<<n_tiles, kSortThreads, 0, st>>>(kin, kg, n, shift,
+                                                                                 hist, n_tiles);
   RS_CHECK_LAUNCH();
   constexpr int BINS = 1 << BITS;
   radix_colscan_kernel<<<(BINS + 3) / 4, 256, 0, st>>>(hist, n_tiles, BINS, totals);
   RS_CHECK_LAUNCH();
-  radix_scatter_kernel<BITS, FIRST_FROM_IDS><<<n_tiles, kSortThreads, 0, st>>>(
+  radix_scatter_kernel<BITS, FIRST_FROM_IDS, KPL><<<n_tiles, kSortThreads, 0, st>>>(
       kin, vin, n, shift, hist, totals, n_tiles, kout, vout);
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+template <int BITS, bool FIRST_FROM_IDS>
+static int32_t launch_pass(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                           int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
+                           const KeyGen& kg, hipStream_t st) {
+  if (sort_kpl(n) == kSortKeysPerLaneSmall)
+    return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLaneSmall>(kin, vin, kout, vout, n, shift,
+                                                                      hist, totals, n_tiles, kg, st);
+  return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLane>(kin, vin, kout, vout, n, shift, hist,
+                                                               totals, n_tiles, kg, st);
 }
 
 template <bool FIRST_FROM_IDS>
