@@ -74,3 +74,31 @@ def test_criteo_cardinalities_and_ids():
     cat, dn, lb = criteo_batch(rng, 4096, c)
     assert cat.shape == (4096, 26) and (cat >= 0).all() and (cat < np.array(c)).all()
     assert dn.shape == (4096, 13) and abs(lb.mean() - 0.256) < 0.03
+
+
+def test_graph_keras_adam_flat_layout_cpu():
+    """GraphKerasAdam's flat buffers (host logic only, no kernel call): every parameter becomes a
+    16-byte-aligned view of `flat` with its values kept, and grad_view(i) is the same slice of
+    `grad_flat`, so a densified gradient written there lands where rs_keras_adam_flat reads it
+    and the padding between parameters stays 0."""
+    import torch
+
+    from recommender_amd.optim import GraphKerasAdam
+
+    ps = [torch.nn.Parameter(torch.arange(n, dtype=torch.float32).reshape(shape))
+          for n, shape in ((6, (2, 3)), (5, (5,)), (8, (4, 2)))]
+    want = [p.detach().clone() for p in ps]
+    opt = GraphKerasAdam(ps, lr=1e-3, window=4)
+    for i, (p, w) in enumerate(zip(ps, want)):
+        assert torch.equal(p.detach(), w)
+        o, n, pad = opt._segs[i]
+        assert o % 4 == 0 and (n + pad) % 4 == 0
+        assert p.data_ptr() == opt.flat[o:].data_ptr()
+        gv = opt.grad_view(i)
+        assert gv.shape == p.shape and gv.data_ptr() == opt.grad_flat[o:].data_ptr()
+        gv.fill_(float(i + 1))
+    pad_mask = torch.ones_like(opt.grad_flat, dtype=torch.bool)
+    for i, (o, n, _) in enumerate(opt._segs):
+        assert torch.all(opt.grad_flat[o:o + n] == float(i + 1))
+        pad_mask[o:o + n] = False
+    assert torch.all(opt.grad_flat[pad_mask] == 0)
