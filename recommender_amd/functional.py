@@ -333,10 +333,13 @@ def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float 
 
 
 TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
-_TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "1") != "0"
 # the chunked train kernel (rs_dlrm_train_step_fwd_unit: unit rows + G, the apply scales them);
 # RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows
 _TRAIN_UNIT = os.environ.get("RS_TRAIN_UNIT", "1") != "0"
+# the train kernel waiting for the presort's completion (below): right for dlrm_train_pipe, off
+# for the chunked kernel (interleaved A/B, 3 x 100 steps: 0.695-0.699 vs 0.700-0.704 ms/step,
+# p90 0.698-0.700 vs 0.704-0.707); RS_TRAIN_WAITS_SORT=1 restores the wait
+_TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "0" if _TRAIN_UNIT else "1") != "0"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
@@ -399,10 +402,9 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         dev = w.device
         _wait_update(emb)
         # the fused kernel is one round of resident blocks: launched while the sort stream's last
-        # scatter still holds CU slots, some of its blocks are placed a round late (measured: the
-        # kernel 0.42 -> 0.62 ms whenever the two overlap). The sort normally ends first (it runs
-        # beside the previous update, which the kernel waits for anyway), so waiting for it costs
-        # at most its tail.
+        # scatter still holds CU slots, some of dlrm_train_pipe's blocks were placed a round late
+        # (measured: 0.42 -> 0.62 ms whenever the two overlapped), so that kernel waits for the
+        # sort; the chunked kernel measured better without the wait (_TRAIN_WAITS_SORT above).
         ahead = emb._presorted[1] if getattr(emb, "_presorted", None) else None
         ready = getattr(ahead, "ready", None)
         if ready is not None and _TRAIN_WAITS_SORT:
