@@ -17,9 +17,14 @@ constexpr int kSortKeysPerLane = 16;      // K: keys per lane per tile (large so
 constexpr int kSortTile = kSortThreads * kSortKeysPerLane;  // 4096 keys per tile
 // small sorts (cfg2's 213k ids, DeepFM's 27k, DIEN's tables) take 1024-key tiles: 4x the blocks
 // per launch for a latency-bound pass that would otherwise run on a few dozen CUs
+// and sorts under 2^17 ids (DeepFM's, EGES' and PinSage's tables) 512-key tiles
 constexpr int kSortKeysPerLaneSmall = 4;
+constexpr int kSortKeysPerLaneTiny = 2;
 constexpr int64_t kSortSmallN = 1 << 20;
-static inline int sort_kpl(int64_t n) { return n < kSortSmallN ? kSortKeysPerLaneSmall : kSortKeysPerLane; }
+constexpr int64_t kSortTinyN = 1 << 17;
+static inline int sort_kpl(int64_t n) {
+  return n < kSortTinyN ? kSortKeysPerLaneTiny : (n < kSortSmallN ? kSortKeysPerLaneSmall : kSortKeysPerLane);
+}
 constexpr int kMaxBins = 512;
 
 // match mask: lanes of this wave whose digit equals mine
@@ -426,6 +431,9 @@ template <int BITS, bool FIRST_FROM_IDS>
 static int32_t launch_pass(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
                            int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
                            const KeyGen& kg, hipStream_t st) {
+  if (sort_kpl(n) == kSortKeysPerLaneTiny)
+    return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLaneTiny>(kin, vin, kout, vout, n, shift,
+                                                                     hist, totals, n_tiles, kg, st);
   if (sort_kpl(n) == kSortKeysPerLaneSmall)
     return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLaneSmall>(kin, vin, kout, vout, n, shift,
                                                                       hist, totals, n_tiles, kg, st);
