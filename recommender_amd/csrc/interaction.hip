@@ -17,6 +17,9 @@
 // [Z (F*F, skip_gather), dense (D)] (ctr/model.py:51-55), so the [B,S,D] embedding tensor
 // is never materialised in HBM; the backward re-gathers the rows instead of re-reading a
 // saved copy (one 512-B read instead of a write + a read per row).
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <type_traits>
 
 #include "common.hpp"
@@ -442,14 +445,11 @@ constexpr int kPipeEPW = 16;  // upper bound; the launch sizes it to the occupan
 #define RS_PIPE_ROUNDS 2
 #endif
 constexpr int kPipeRounds = RS_PIPE_ROUNDS;
-static int pipe_epw(const void* kernel, int64_t batch, int rounds = kPipeRounds) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
+static int pipe_epw_uncached(const void* kernel, int dev, int64_t batch, int rounds) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus < 1)
+    cus = 256;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
       per_cu < 1)
@@ -457,6 +457,25 @@ static int pipe_epw(const void* kernel, int64_t batch, int rounds = kPipeRounds)
   const int64_t slots = (int64_t)cus * per_cu * 4 * rounds;  // waves over all rounds
   const int64_t e = ceil_div(batch, slots);
   return (int)(e < 1 ? 1 : (e > 64 ? 64 : e));
+}
+
+// cached per (device, kernel, batch, rounds): occupancy depends on the device, and several host
+// threads may launch at once (one per GPU), so the cache is shared and locked
+static int pipe_epw(const void* kernel, int64_t batch, int rounds = kPipeRounds) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, int64_t, int>, int> cache;
+  const auto key = std::make_tuple(dev, kernel, batch, rounds);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  const int e = pipe_epw_uncached(kernel, dev, batch, rounds);
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = e;
+  return e;
 }
 
 typedef __attribute__((address_space(1))) const floatx4 gfloatx4;
@@ -1550,13 +1569,7 @@ static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode 
                           const float* gout, int64_t gstride, float* gemb, float* gdense, int,
                           hipStream_t st, const float* gscale = nullptr) {
   auto go = [&](auto kern) {
-    static int epw_cached = 0;
-    static int64_t batch_cached = -1;
-    if (batch != batch_cached) {
-      epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch);
-      batch_cached = batch;
-    }
-    const int epw = epw_cached;
+    const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch);
     kern<<<ceil_div(batch, 4 * (int64_t)epw), 256, 0, st>>>(src, batch, F, gout, gstride, gemb,
                                                            gdense, epw, gscale);
   };
@@ -1948,13 +1961,7 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
   if (F <= kDxRows && out_stride > out_width(F, 0, 0) + D &&
       out_stride <= out_width(F, 0, 0) + D + 64) {
     auto go = [&](auto kern) {
-      static int epw_cached = 0;
-      static int64_t batch_cached = -1;
-      if (batch != batch_cached) {
-        epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch);
-        batch_cached = batch;
-      }
-      const int epw = epw_cached;
+      const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch);
       kern<<<ceil_div(batch, 4 * (int64_t)epw), 256, 0, st>>>(src, batch, F, out, out_stride, hd, epw);
     };
     if (id_dtype == RS_ID_I64) go(dlrm_fwd_dx_pipe<true>);
@@ -2018,18 +2025,10 @@ static int32_t train_step_launch(
   TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part};
   int64_t blocks = 0;
   auto go = [&](auto kern) {
-    static int epw_cached = 0;
-    static int64_t batch_cached = -1;
-    static const void* kern_cached = nullptr;
-    if (batch != batch_cached || reinterpret_cast<const void*>(kern) != kern_cached) {
-      // ONE round of resident blocks: the side-stream sort then only fills the resources the
-      // kernel leaves free instead of taking CU slots between rounds (A/B on one box: kernel
-      // 458 -> 448 us alone, step 0.878 -> 0.848 ms; four rounds 0.912)
-      epw_cached = pipe_epw(reinterpret_cast<const void*>(kern), batch, 1);
-      batch_cached = batch;
-      kern_cached = reinterpret_cast<const void*>(kern);
-    }
-    const int epw = epw_cached;
+    // ONE round of resident blocks: the side-stream sort then only fills the resources the
+    // kernel leaves free instead of taking CU slots between rounds (A/B on one box: kernel
+    // 458 -> 448 us alone, step 0.878 -> 0.848 ms; four rounds 0.912)
+    const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch, 1);
     blocks = ceil_div(batch, 4 * (int64_t)epw);
     if constexpr (std::is_same_v<decltype(kern), decltype(&dlrm_train_pipe<128, true>)>)
       kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, epw);

@@ -50,6 +50,8 @@ class Embedding(nn.Module):
         # sorts queued ahead for later steps (Embedding.prefetch), keyed by the ids' storage
         self._prefetched: dict = {}
         self._prefetch_queue: list = []  # prefetched ids whose sort is not launched yet
+        self._prefetch_gen: list = []  # the presort count when each queued entry arrived
+        self._presort_gen = 0
         # deferred join (SparseOptimizer(defer_join=True)): the event the next table read waits on
         self._pending_update = None
         # deferred-decay Keras Adam: the step this table's rows were last caught up for
@@ -101,7 +103,10 @@ class Embedding(nn.Module):
         key = self._ids_key(ids)
         if key in self._prefetched or any(self._ids_key(q) == key for q in self._prefetch_queue):
             return
+        if len(self._prefetch_queue) >= 4:  # bounded like _prefetched: launch what waits
+            self.flush_prefetch()
         self._prefetch_queue.append(ids)
+        self._prefetch_gen.append(self._presort_gen)
         if not opt.prefetch_after_kernel:
             self.flush_prefetch()
 
@@ -111,7 +116,7 @@ class Embedding(nn.Module):
         and dense tail (the train kernel's resident grid leaves no CU slots for it, and a sort
         queued at the next step's start would delay that step's kernel); presort() calls it too,
         when the queue holds its own ids, so a queued sort is never lost."""
-        q, self._prefetch_queue = self._prefetch_queue, []
+        q, self._prefetch_queue, self._prefetch_gen = self._prefetch_queue, [], []
         opt = self.fused_optimizer
         for ids in q:
             key = self._ids_key(ids)
@@ -127,9 +132,14 @@ class Embedding(nn.Module):
         GPU is busy with the forward, and the sort runs beside it. The lookup's backward reuses
         it (or sorts on the spot when no presort was issued)."""
         if self.fused_optimizer is not None and torch.is_grad_enabled():
-            if self._prefetch_queue and any(self._ids_key(q) == self._ids_key(ids)
-                                            for q in self._prefetch_queue):
-                self.flush_prefetch()  # this step's own ids were queued but not sorted yet
+            self._presort_gen += 1
+            if self._prefetch_queue and (
+                    any(self._ids_key(q) == self._ids_key(ids) for q in self._prefetch_queue)
+                    or self._prefetch_gen[0] < self._presort_gen - 1):
+                # this step's own ids were queued but not sorted yet, or an entry has waited a
+                # whole step: paths without the fused DLRM kernel (which flushes right after its
+                # train kernel) flush here, so a queued sort never waits more than one step
+                self.flush_prefetch()
             e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
             ahead = e[2] if e is not None and e[1] == ids._version else None
             opt = self.fused_optimizer

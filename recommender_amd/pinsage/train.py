@@ -167,7 +167,12 @@ class PinSageStep:
         """Densify each table's IndexedSlices grad (deterministic segmented sum), bucket it
         with the dense grads into one all-reduce, average over ranks, then apply the tables
         as fully-touched slices (identical to Keras' dense m/v decay for untouched rows)."""
-        grads = [p.grad for p in self.dense]  # None: Keras skips the variable
+        # every rank must hand the all-reduce the same bucket layout: a parameter without a
+        # gradient on this rank contributes zeros, and a has-gradient flag rides along in the
+        # bucket so a parameter no rank produced a gradient for stays None (Keras skips it)
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.dense]
+        dev = self.dense[0].device if self.dense else self.model.tables()[0].weight.device
+        has = torch.tensor([0.0 if p.grad is None else 1.0 for p in self.dense], device=dev)
         tables = self.model.tables()
         dense_tab = []
         for t in tables:
@@ -177,13 +182,14 @@ class PinSageStep:
                 rows, ug = dedup_grad(t, got[0], got[1])
                 g.index_copy_(0, rows, ug)
             dense_tab.append(g)
-        bucket = grads + dense_tab
+        bucket = grads + dense_tab + [has]
         flat = torch._utils._flatten_dense_tensors(bucket)
         self.comm.all_reduce_(flat)
         flat.mul_(1.0 / self.world)
         out = torch._utils._unflatten_dense_tensors(flat, bucket)
-        for p, g in zip(self.dense, out[: len(self.dense)]):
-            p.grad = g
+        any_grad = (out[-1] > 0).tolist()
+        for p, g, present in zip(self.dense, out[: len(self.dense)], any_grad):
+            p.grad = g if present else None
         params = self.opt_sparse._params()
         for t, g in zip(tables, out[len(self.dense):]):
             ids = torch.arange(t.input_dim, device=g.device, dtype=torch.int32)

@@ -110,7 +110,7 @@ class ShardedSlabEmbedding(nn.Module):
         self.side = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.optimizer: SparseOptimizer | None = None
         self._st = None  # per-step exchange state
-        self._prefetched: dict = {}  # exchange_begin states queued ahead (prefetch)
+        self._prefetched: list = []  # exchange_begin states queued ahead, FIFO (prefetch)
 
     @property
     def n_slots(self):
@@ -166,22 +166,29 @@ class ShardedSlabEmbedding(nn.Module):
         """Queue the first half of a LATER step's exchange now (owner-major sort, unique /
         inverse, split sizes: exchange_begin) so that step's exchange_finish finds its split
         sizes already on the host: the one host sync of a sharded step then waits on work queued
-        a step earlier instead of stalling the device (every rank must prefetch the same steps,
-        in the same order: the split-size exchange is a collective). The ids must not change
-        before their step (an in-place change voids the entry)."""
-        key = self._ids_key(ids)
-        if key in self._prefetched or torch.cuda.is_current_stream_capturing():
+        a step earlier instead of stalling the device. The split-size exchange is a collective,
+        so every rank must prefetch the same steps in the same order. Entries are kept in queue
+        order: a step takes its own entry and drops the older ones (steps that never ran), a
+        step with no entry exchanges afresh, and a step whose entry's ids changed in place
+        raises instead of re-exchanging (which one rank alone might do, pairing the ranks'
+        collectives wrongly)."""
+        if torch.cuda.is_current_stream_capturing():
             return
         if len(self._prefetched) >= 4:  # stale entries (steps that never ran)
-            self._prefetched.pop(next(iter(self._prefetched)))
-        self._prefetched[key] = (ids._version, self.exchange_begin(ids))
+            self._prefetched.pop(0)
+        self._prefetched.append((self._ids_key(ids), ids._version, self.exchange_begin(ids)))
 
     def take_prefetched(self, ids: torch.Tensor):
-        """The prefetched exchange_begin state of these ids, or None."""
-        e = self._prefetched.pop(self._ids_key(ids), None) if self._prefetched else None
-        if e is None or e[0] != ids._version:
-            return None
-        return e[1]
+        """The prefetched exchange_begin state of these ids (older entries dropped), or None."""
+        key = self._ids_key(ids)
+        for i, (k, version, st) in enumerate(self._prefetched):
+            if k == key:
+                del self._prefetched[: i + 1]
+                if version != ids._version:
+                    raise RuntimeError("ShardedSlabEmbedding: a prefetched batch's ids were "
+                                       "changed in place before their step")
+                return st
+        return None
 
     def exchange_finish(self, st):
         """Wait (host) for the split sizes, then the two all-to-alls and the owner gather;

@@ -61,6 +61,28 @@ def test_sort_ids(n, V, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("n", [(1 << 17) - 1, 1 << 17, (1 << 20) - 1, 1 << 20])
+@pytest.mark.parametrize("masked", [False, True])
+def test_sort_ids_tile_size_switch_points(n, masked, rng):
+    """The sort's keys per lane (tile size) switch at n = 2^17 (512 -> 1024-key tiles) and 2^20
+    (1024 -> 4096): both sides of each switch, plain and masked (left-out positions take the
+    sentinel key), rows / positions / unique count bit-exact vs the oracle's stable sort."""
+    V = 40_000_000
+    ids = zipf_ids(rng, n, V).astype(np.int64)
+    ids[::101] = V + 5  # OOB
+    dev_ids = torch.from_numpy(ids).to(DEV)
+    if masked:
+        keep = rng.random(n) < 0.4
+        s = SortedIds(dev_ids, V, valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV))
+        rows_ref, pos_ref, nu_ref = O.sort_ids(np.where(keep, ids, -1), V)
+    else:
+        s = SortedIds(dev_ids, V)
+        rows_ref, pos_ref, nu_ref = O.sort_ids(ids, V)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
 @pytest.mark.parametrize("per_slot", [10_000_000, 40_000_000])
 def test_sort_ids_large_slab_four_passes(per_slot, rng):
     """SURVEY cfg2's 26 x 10M-row slab (260M rows: 28 key bits, four 7-bit passes) and a 1.04B-row

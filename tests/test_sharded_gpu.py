@@ -285,6 +285,15 @@ def _prefetch_world2_worker(rank, world, port, q):
                     step.prefetch(bs[i + 1])
                 if i == 2:  # prefetched during step 1, then changed in place
                     b[0].copy_(repl)
+                    if pre:
+                        # the prefetched exchange no longer matches: loud, on every rank (the
+                        # collectives stay paired), then the step exchanges afresh
+                        try:
+                            step(b)
+                        except RuntimeError as e:
+                            assert "prefetched" in str(e)
+                        else:
+                            raise AssertionError("a changed prefetched batch must raise")
                 step(b)
             emb.join()
             torch.cuda.synchronize()
