@@ -56,16 +56,18 @@ def sharded_sgd_step(full_table, per_rank_ids, per_rank_grads, lr, world, slot_o
     return out
 
 
-def sharded_adam_step(full_table, m, v, per_rank_ids, per_rank_grads, world, step, mode,
-                      lr=1e-3, slot_offsets=None):
-    """One sharded lazy / Keras Adam step (recommender_amd/sharded.py backward_exchange): each
-    owner scales the received per-source unique grads by float32(1/W) (world > 1), folds them
-    with the tiled order and applies Adam (coefficients of 1-based `step`) to its shard. Keras
-    mode is dense: every row of every shard decays m / v and moves, including shards that
-    received no row this step. Returns (table, m, v) in full-slab layout."""
-    V, D = full_table.shape
+def sharded_owner_grads(per_rank_ids, per_rank_grads, world, n_rows, slot_offsets=None,
+                        scale=True):
+    """The owners' side of one sharded step (recommender_amd/sharded.py backward_exchange)
+    before the optimizer: each rank folds its gradient rows per owner-major key with the tiled
+    order, each owner receives the per-source (local row, grad) lists rank-major, scales them by
+    float32(1/W) (world > 1, `scale`: rows of each rank's local mean loss) and folds them with
+    the same tiled order over its shard. Returns, per owner o, (the shard's local rows that got a
+    gradient, sorted; their folded gradients). Depends on the ids and gradient rows only, so a
+    test can apply it to any compacted copy of the touched rows' optimizer state."""
+    V = n_rows
+    D = per_rank_grads[0].shape[1]
     stride = -(-V // world)
-    c = keras_adam_coefficients(step, lr)
     recv = [[] for _ in range(world)]
     for r in range(world):
         rows = global_rows(per_rank_ids[r], V, slot_offsets)
@@ -77,21 +79,37 @@ def sharded_adam_step(full_table, m, v, per_rank_ids, per_rank_grads, world, ste
         for o in range(world):
             sel = (uk // stride) == o
             recv[o].append((uk[sel] - o * stride, ug[sel]))
-    t, m2, v2 = full_table.copy(), m.copy(), v.copy()
+    out = []
     for o in range(world):
-        g_all = np.arange(o, V, world)  # this owner's global rows, local order
         local = np.concatenate([x[0] for x in recv[o]])
         grads = (np.concatenate([x[1] for x in recv[o]]) if local.size
                  else np.zeros((0, D), np.float32))
-        if world > 1:
+        if world > 1 and scale:
             grads = grads * np.float32(1.0 / world)
-        shard_rows = g_all.size
+        shard_rows = (V - o + world - 1) // world
         if local.size:
             sr, sp, _ = sort_ids(local, shard_rows)
             ur, ug = segment_sum_tiled(sr, sp, grads, shard_rows)
-            ur = ur.astype(np.int64)
+            out.append((ur.astype(np.int64), ug))
         else:
-            ur, ug = np.zeros(0, np.int64), np.zeros((0, D), np.float32)
+            out.append((np.zeros(0, np.int64), np.zeros((0, D), np.float32)))
+    return out
+
+
+def sharded_adam_step(full_table, m, v, per_rank_ids, per_rank_grads, world, step, mode,
+                      lr=1e-3, slot_offsets=None):
+    """One sharded lazy / Keras Adam step (recommender_amd/sharded.py backward_exchange): each
+    owner scales the received per-source unique grads by float32(1/W) (world > 1), folds them
+    with the tiled order and applies Adam (coefficients of 1-based `step`) to its shard. Keras
+    mode is dense: every row of every shard decays m / v and moves, including shards that
+    received no row this step. Returns (table, m, v) in full-slab layout."""
+    V, D = full_table.shape
+    c = keras_adam_coefficients(step, lr)
+    owners = sharded_owner_grads(per_rank_ids, per_rank_grads, world, V, slot_offsets)
+    t, m2, v2 = full_table.copy(), m.copy(), v.copy()
+    for o in range(world):
+        g_all = np.arange(o, V, world)  # this owner's global rows, local order
+        ur, ug = owners[o]
         fn = apply_keras_adam if mode == "keras" else apply_lazy_adam
         if mode != "keras" and not ur.size:
             continue

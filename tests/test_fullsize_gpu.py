@@ -1,0 +1,379 @@
+"""BASELINE configs 3, 4 and 5 at their stated sizes against the oracle.
+
+* cfg3 — the whole DIEN train step (dien/train.py:14-22) at B 4096, L 100, 63 001 items, 801
+  cats, both head-BN modes: tests/test_dien_step_gpu.py's per-step check (loss, predictions and
+  every gradient per element vs the float64 autograd oracle, dense Keras Adam and both tables /
+  m / v bit-exact).
+* cfg4 — ESMM and MMOE (esmm/esmm.py, esmm/mmoe.py) on 18 tables scaled to 40M rows, D 18,
+  B 65 536, Keras Adam, two steps at world 1; and a row-sharded ESMM step on two gloo ranks
+  sharing the GPU (global batch 65 536). The oracle's optimizer state is compacted onto the rows
+  that matter (every row the steps touched plus a random sample of the others; Keras' sparse
+  Adam is row-wise, so a compacted apply is the full one restricted to those rows) and compared
+  bit for bit.
+* cfg5 — PinSage sampling on the ML-20M-shaped graph (138 493 users, 26 744 items, 20 000 263
+  edges, hub items of 10^4+ ratings): a 4096-pair batch, pairs / seeds / both blocks bit-exact
+  vs oracle/pinsage.py, and one model forward + backward vs the float64 restatement.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import embedding as OE
+from tests.conftest import assert_close_f64
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+# ------------------------------------------------------------------------------------- cfg3
+@pytest.mark.parametrize("mode", ["propagate", "inference"])
+def test_cfg3_dien_full_size_step_vs_oracle(mode):
+    from recommender_amd.dien import DIEN
+    from recommender_amd.dien.train import DIENStep, synthetic_batch
+    from tests.test_dien_step_gpu import _checked_step
+
+    IV, CV, B, L = 63_001, 801, 4096, 100
+    g = torch.Generator(device=DEV)
+    g.manual_seed(4)
+    model = DIEN(36, 36, head_bn_mode=mode, item_vocab_size=IV, item_embedding_size=18,
+                 cat_vocab_size=CV, cat_embedding_size=18, mlp_units=[200, 80, 1], device=DEV,
+                 generator=g)
+    step = DIENStep(model, lr=1e-3)
+    r = np.random.default_rng(4)
+    for _ in range(2):
+        f, lab = synthetic_batch(r, B, L, IV, CV)
+        feats = {k: torch.from_numpy(v).to(DEV) for k, v in f.items()}
+        _checked_step(model, step, feats, torch.from_numpy(lab).to(DEV))
+
+
+# ------------------------------------------------------------------------------------- cfg4
+CFG4_ROWS, CFG4_BATCH = 40_000_000, 65_536
+
+
+def _cfg4_vocab():
+    from recommender_amd.esmm import FEAT_VOCAB
+    from recommender_amd.synthetic import scaled_vocab
+
+    return scaled_vocab(FEAT_VOCAB, CFG4_ROWS)
+
+
+def _compact_keras_check(rows_sel, w_gpu, m_gpu, v_gpu, w0, m0, v0, ur, ug, co, msg):
+    """The oracle's Keras Adam apply on the compacted rows `rows_sel` (sorted; every touched row
+    included) vs the GPU's table / m / v at those rows. w0 / m0 / v0: the pre-step state at
+    rows_sel (numpy); ur / ug: the oracle's folded rows (global) and gradients."""
+    idx = np.searchsorted(rows_sel, ur)
+    assert np.array_equal(rows_sel[idx], ur), "a touched row is missing from the compaction"
+    t2, m2, v2 = OE.apply_keras_adam(w0, m0, v0, idx, ug, co)
+    sel = torch.from_numpy(rows_sel).to(DEV)
+    np.testing.assert_array_equal(w_gpu[sel].cpu().numpy(), t2, err_msg=f"{msg} table")
+    np.testing.assert_array_equal(m_gpu[sel].cpu().numpy(), m2, err_msg=f"{msg} m")
+    np.testing.assert_array_equal(v_gpu[sel].cpu().numpy(), v2, err_msg=f"{msg} v")
+
+
+@pytest.mark.parametrize("kind", ["ESMM", "MMOE"])
+def test_cfg4_full_size_keras_adam_steps_vs_oracle(kind):
+    """Two MultiTaskStep Keras-Adam steps of cfg4 at its size: loss 1e-5 of the float64 oracle,
+    outputs / dense gradients / per-position table gradient rows per element
+    (tests/conftest.py assert_close_f64: 1e-5 relative + 4x the fp32 oracle's own error over
+    three batch orders + a floor of the tensor's largest), dense parameters = Keras Adam of their
+    gradients bit for bit, and the 40M-row slab / m / v bit-exact at every touched row and at
+    200 000 random other rows (Keras' dense decay included)."""
+    from oracle.models import esmm_family_step, keras_adam_torch
+    from recommender_amd.esmm.train import MultiTaskStep, build
+    from recommender_amd.synthetic import aliccp_batch
+
+    vocab = _cfg4_vocab()
+    assert sum(vocab.values()) == CFG4_ROWS
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    model = build(kind, vocab, 18, DEV, g)
+    step = MultiTaskStep(model, "keras_adam")
+    slab = model.embedding_layer.slab
+    V = slab.input_dim
+    so = slab.slot_offsets.cpu().numpy()
+    m_t, v_t, _ = step.opt_sparse._slots(slab)
+    rng = np.random.default_rng(5)
+    others = np.random.default_rng(11).choice(V, 200_000, replace=False)
+    touched_before = np.zeros(0, np.int64)
+    cap = {}
+    apply = step.opt_sparse.apply
+
+    def spy(table, ids, grad_rows, params, sorted_ids=None, row_scale=None):
+        cap["ids"], cap["rows"] = ids, grad_rows
+        return apply(table, ids, grad_rows, params, sorted_ids=sorted_ids, row_scale=row_scale)
+
+    step.opt_sparse.apply = spy
+    try:
+        for it in range(1, 3):
+            f, lab = aliccp_batch(rng, CFG4_BATCH, vocab)
+            feats = {k: torch.from_numpy(v).to(DEV) for k, v in f.items()}
+            lab_t = torch.from_numpy(lab).to(DEV)
+            w0_full = slab.weight.detach().clone()
+            m0_full, v0_full = m_t.detach().clone(), v_t.detach().clone()
+            dense0 = [p.detach().clone() for p in step.dense]
+            st0 = [dict(step.opt_dense.state.get(p, {})) for p in step.dense]
+            st0 = [(s["m"].clone(), s["v"].clone()) if s else None for s in st0]
+            ref_loss, ref_y, ref_dg, ref_rows = esmm_family_step(
+                model, w0_full, slab.slot_offsets, feats, lab_t, dtype=torch.float64)
+            gp = torch.Generator(device="cpu").manual_seed(3)
+            perms = [None] + [torch.randperm(CFG4_BATCH, generator=gp).to(DEV) for _ in range(2)]
+            r32 = [esmm_family_step(model, w0_full, slab.slot_offsets, feats, lab_t, perm=p)
+                   for p in perms]
+            loss = float(step(feats, lab_t))
+            torch.cuda.synchronize()
+            assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
+            assert_close_f64(step.last_pred, ref_y, [r[1] for r in r32], "outputs")
+            c = {k: float(x) for k, x in OE.keras_adam_coefficients(it).items()}
+            for i, (p, p0, rg) in enumerate(zip(step.dense, dense0, ref_dg)):
+                assert_close_f64(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}")
+                m0, v0 = st0[i] if st0[i] is not None else (torch.zeros_like(p0),) * 2
+                want, _, _ = keras_adam_torch(p0, m0, v0, p.grad, c)
+                assert torch.equal(p.detach(), want), f"dense parameter {i}"
+            rows_gpu = cap["rows"].reshape(-1, 18)
+            assert_close_f64(rows_gpu, ref_rows, [r[3] for r in r32], "table gradient rows",
+                             floor=1e-6)
+            ids = cap["ids"].cpu().numpy()
+            sr, sp, _ = OE.sort_ids(ids, V, so)
+            ur, ug = OE.segment_sum_tiled(sr, sp, rows_gpu.cpu().numpy(), V)
+            ur = ur.astype(np.int64)
+            sel = np.union1d(np.union1d(ur, touched_before), others)
+            st = torch.from_numpy(sel).to(DEV)
+            _compact_keras_check(sel, slab.weight, m_t, v_t, w0_full[st].cpu().numpy(),
+                                 m0_full[st].cpu().numpy(), v0_full[st].cpu().numpy(), ur, ug,
+                                 OE.keras_adam_coefficients(it), f"step {it}")
+            touched_before = np.union1d(touched_before, ur)
+            del w0_full, m0_full, v0_full
+    finally:
+        del step.opt_sparse.apply
+    assert touched_before.size > 100_000  # the batch reaches far into the 40M rows
+
+
+def _cfg4_world2_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sharded as OS
+        from oracle.models import esmm_family_step, keras_adam_torch
+        from recommender_amd.esmm.train import MultiTaskStep, build
+        from recommender_amd.sharded import Comm
+        from recommender_amd.synthetic import aliccp_batch
+
+        vocab = _cfg4_vocab()
+        # every rank builds the same full slab (seed 3) and keeps its cyclic share of it
+        ref = build("ESMM", vocab, 18, DEV, torch.Generator(device=DEV).manual_seed(3))
+        table_init = ref.embedding_layer.slab.weight.detach()
+        model = build("ESMM", vocab, 18, DEV, torch.Generator(device=DEV).manual_seed(9),
+                      sharded_comm=Comm())
+        sd = {k: v for k, v in ref.state_dict().items() if not k.startswith("embedding_layer")}
+        model.load_state_dict(sd, strict=False)
+        slab = model.embedding_layer.slab
+        slab.shard.weight.copy_(table_init[rank::world])
+        step = MultiTaskStep(model, "keras_adam", comm=Comm())
+        so_t = slab.slot_offsets
+        so = so_t.cpu().numpy()
+        V, D = slab.input_dim, 18
+        m_t, v_t, _ = step.opt_sparse._slots(slab.shard)
+        # the oracle's state, compacted: rows touched so far (sorted) and their table / m / v
+        rows_s = np.zeros(0, np.int64)
+        t_s = np.zeros((0, D), np.float32)
+        m_s = np.zeros((0, D), np.float32)
+        v_s = np.zeros((0, D), np.float32)
+        cap = {}
+        bex = slab.backward_exchange
+
+        def spy(grad_rows):
+            cap["rows"] = grad_rows.detach().cpu().numpy().copy()
+            return bex(grad_rows)
+
+        slab.backward_exchange = spy
+        half_b = CFG4_BATCH // world
+        rng = np.random.default_rng(5)
+        others = np.random.default_rng(11).choice(V, 100_000, replace=False)
+        for it in range(1, 3):
+            f, lab = aliccp_batch(rng, CFG4_BATCH, vocab)  # the global batch; rank r: part r
+            part = {k: v[rank * half_b:(rank + 1) * half_b] for k, v in f.items()}
+            feats = {k: torch.from_numpy(v).to(DEV) for k, v in part.items()}
+            lab_t = torch.from_numpy(lab[rank * half_b:(rank + 1) * half_b]).to(DEV)
+            dense0 = [p.detach().clone() for p in step.dense]
+            st0 = [dict(step.opt_dense.state.get(p, {})) for p in step.dense]
+            st0 = [(s["m"].clone(), s["v"].clone()) if s else None for s in st0]
+            # the oracle's dense gradients need the slab as it stands: rows of the touched set
+            # from the oracle state, every other row still at its initial value
+            tcur = table_init.clone()
+            if rows_s.size:
+                tcur[torch.from_numpy(rows_s).to(DEV)] = torch.from_numpy(t_s).to(DEV)
+            gs = []
+            for r in range(world):
+                fr = {k: torch.from_numpy(v[r * half_b:(r + 1) * half_b]).to(DEV)
+                      for k, v in f.items()}
+                lr_ = torch.from_numpy(lab[r * half_b:(r + 1) * half_b]).to(DEV)
+                gs.append(esmm_family_step(model, tcur, so_t, fr, lr_, dtype=torch.float64)[2])
+            del tcur
+            step(feats, lab_t)
+            torch.cuda.synchronize()
+            c = {k: float(x) for k, x in OE.keras_adam_coefficients(it).items()}
+            for i, p in enumerate(step.dense):
+                want_g = ((gs[0][i] + gs[1][i]) * 0.5).to(torch.float32)
+                # float64 oracle of the all-reduced mean gradient: 1e-4 of the largest entry
+                err = (p.grad - want_g).abs().max().item()
+                assert err <= 1e-4 * max(want_g.abs().max().item(), 1e-30), (i, err)
+                m0, v0 = st0[i] if st0[i] is not None else (torch.zeros_like(p),) * 2
+                want, _, _ = keras_adam_torch(dense0[i], m0, v0, p.grad, c)
+                assert torch.equal(p.detach(), want), f"dense parameter {i}"
+            ids = np.stack([part[k].reshape(-1) for k in part], 1).astype(np.int64)
+            all_ids, all_rows = [None] * world, [None] * world
+            dist.all_gather_object(all_ids, ids)
+            dist.all_gather_object(all_rows, cap["rows"].reshape(-1, D))
+            owners = OS.sharded_owner_grads(all_ids, all_rows, world, V, so)
+            ur = np.concatenate([o_rows * world + o for o, (o_rows, _) in enumerate(owners)])
+            ug = np.concatenate([g_ for _, g_ in owners])
+            order = np.argsort(ur)
+            ur, ug = ur[order], ug[order]
+            # grow the compacted state by the newly touched rows (initial values, m = v = 0:
+            # an untouched row's Keras decay leaves it exactly as it was)
+            new = np.setdiff1d(ur, rows_s)
+            allr = np.union1d(rows_s, new)
+            t2 = np.empty((allr.size, D), np.float32)
+            m2 = np.zeros((allr.size, D), np.float32)
+            v2 = np.zeros((allr.size, D), np.float32)
+            at = np.searchsorted(allr, rows_s)
+            t2[at], m2[at], v2[at] = t_s, m_s, v_s
+            t2[np.searchsorted(allr, new)] = table_init[torch.from_numpy(new).to(DEV)].cpu().numpy()
+            rows_s = allr
+            t_s, m_s, v_s = OE.apply_keras_adam(t2, m2, v2, np.searchsorted(rows_s, ur), ug,
+                                                OE.keras_adam_coefficients(it))
+            # this rank's shard at the rows it owns: touched rows vs the oracle, sampled others
+            # unchanged (m = v = 0, no move)
+            mine = rows_s % world == rank
+            loc = torch.from_numpy(rows_s[mine] // world).to(DEV)
+            np.testing.assert_array_equal(slab.shard.weight[loc].cpu().numpy(), t_s[mine])
+            np.testing.assert_array_equal(m_t[loc].cpu().numpy(), m_s[mine])
+            np.testing.assert_array_equal(v_t[loc].cpu().numpy(), v_s[mine])
+            oth = np.setdiff1d(others[others % world == rank], rows_s)
+            ol = torch.from_numpy(oth // world).to(DEV)
+            assert torch.equal(slab.shard.weight[ol], table_init[torch.from_numpy(oth).to(DEV)])
+            assert not bool(m_t[ol].any()) and not bool(v_t[ol].any())
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cfg4_world2_sharded_esmm_full_size_vs_oracle():
+    """cfg4's row-sharded ESMM on two gloo ranks sharing the GPU, global batch 65 536 over the
+    40M-row slab, two Keras-Adam steps: all-reduced dense gradients vs the float64 oracle's mean
+    of the two halves, dense parameters Keras Adam of them bit for bit, each rank's shard / m / v
+    bit-exact vs oracle/sharded.py's owner folds + Keras apply at every touched row, sampled
+    untouched rows unchanged."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30300 + (os.getpid() % 500)
+    ps = [ctx.Process(target=_cfg4_world2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res
+
+
+# ------------------------------------------------------------------------------------- cfg5
+@pytest.fixture(scope="module")
+def ml20m():
+    from oracle import pinsage as OP
+    from recommender_amd.pinsage.graph import HeteroGraph
+    from recommender_amd.synthetic import ML20M, movielens_graph
+
+    rng = np.random.default_rng(4)
+    users, items, year, genre = movielens_graph(rng, **ML20M)
+    g = HeteroGraph(users, items, ML20M["n_users"], ML20M["n_items"], device=DEV,
+                    item_data={"year": year, "genre": genre})
+    og = OP.BipartiteGraph.from_edges(users, items, ML20M["n_users"], ML20M["n_items"])
+    return g, og
+
+
+def test_cfg5_ml20m_sampling_bit_exact(ml20m):
+    """A 4096-pair batch on the ML-20M-shaped graph: item pairs, compacted seeds, pair edges
+    and both blocks (src nodes, CSR by dst, weights, transpose) bit-exact vs oracle/pinsage.py,
+    with hub items (10^4+ users) among the seeds."""
+    from oracle import pinsage as OP
+    from recommender_amd.pinsage import PinSageSampler
+    from recommender_amd.pinsage.sampler import item_pairs
+    from recommender_amd.synthetic import ML20M
+    from tests.test_pinsage_gpu import check_block
+
+    g, og = ml20m
+    assert og.i2u.size == ML20M["n_edges"]
+    deg = np.diff(og.i2u_indptr)
+    assert deg.max() >= 10_000
+    smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    for step in range(2):
+        h, p, n = item_pairs(g, 4096, 4, step)
+        rh, rp, rn = OP.item_pairs(og, 0, 4096, 4, step)
+        np.testing.assert_array_equal(h.cpu().numpy(), rh)
+        np.testing.assert_array_equal(p.cpu().numpy(), rp)
+        np.testing.assert_array_equal(n.cpu().numpy(), rn)
+        smp.step = step
+        pos_g, neg_g, blocks = smp.sample_from_item_pairs(h, p, n)
+        seeds, pe, ne, rblocks = OP.sample_from_item_pairs(og, rh, rp, rn, 2, 4, 2, 0.0, 3, 4, step)
+        np.testing.assert_array_equal(pos_g.nodes.cpu().numpy(), seeds)
+        np.testing.assert_array_equal(pos_g.src.cpu().numpy(), pe[0])
+        np.testing.assert_array_equal(pos_g.dst.cpu().numpy(), pe[1])
+        np.testing.assert_array_equal(neg_g.dst.cpu().numpy(), ne[1])
+        for b, rb in zip(blocks, rblocks):
+            check_block(b, rb)
+        assert (deg[seeds] >= 10_000).any(), "no hub item among the seeds"
+
+
+def test_cfg5_ml20m_model_step_vs_float64(ml20m):
+    """One PinSage forward + backward (pinsage/train/train.py:40-48: scores, margin loss,
+    gradients of every dense parameter and table) on a 4096-pair ML-20M batch vs the float64
+    torch restatement of pinsage/train/layers.py / model.py (tests/test_pinsage_gpu.py)."""
+    from recommender_amd.pinsage import PinSageModel, PinSageSampler
+    from recommender_amd.pinsage.model import item2item_scorer, margin_loss
+    from recommender_amd.pinsage.sampler import item_pairs
+    from tests.test_pinsage_gpu import torch_reference_repr
+
+    g, _ = ml20m
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    model = PinSageModel(g, g.itype, 2, 8, 32, 16, generator=gen)
+    smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    h, p, n = item_pairs(g, 4096, 4, 0)
+    pos_g, neg_g, blocks = smp.sample_from_item_pairs(h, p, n)
+    pos, neg = model(pos_g, neg_g, blocks)
+    loss = margin_loss(pos, neg)
+    loss.backward()
+    ref = {}
+    for dt in (torch.float64, torch.float32):
+        rh, P = torch_reference_repr(model, blocks, dt)
+        rpos, rneg = item2item_scorer(pos_g, rh), item2item_scorer(neg_g, rh)
+        rloss = torch.clamp(rneg + 1 - rpos, min=0).mean()
+        rloss.backward()
+        ref[dt] = (rpos.detach(), rneg.detach(), float(rloss), P)
+    (p64, n64, l64, P64), (p32, n32, _, P32) = ref[torch.float64], ref[torch.float32]
+    assert_close_f64(pos, p64, p32, "pos score", floor=1e-6)
+    assert_close_f64(neg, n64, n32, "neg score", floor=1e-6)
+    assert abs(loss.item() - l64) <= 1e-5 * abs(l64)
+    s = model.sagenet
+    pairs = [(s.fc_2.kernel, "k2"), (s.fc_2.bias, "b2"), (s.fc_1.kernel, "k1"), (s.fc_1.bias, "b1")]
+    for li, c in enumerate(s.convolves):
+        pairs += [(c.fc_1.kernel, f"c{li}k1"), (c.fc_1.bias, f"c{li}b1"),
+                  (c.fc_2.kernel, f"c{li}k2"), (c.fc_2.bias, f"c{li}b2")]
+    for prm, name in pairs:
+        assert_close_f64(prm.grad, P64[name].grad, P32[name].grad, name, floor=1e-6)
+    for t, name in zip(model.tables(), ("year", "genre", "id")):
+        ids, rows = t.take_grad()
+        dense = torch.zeros_like(t.weight).index_add(0, ids.reshape(-1).long(),
+                                                     rows.reshape(-1, t.output_dim))
+        assert_close_f64(dense, P64[name].grad, P32[name].grad, f"table {name}", floor=1e-6)
