@@ -114,6 +114,25 @@ def esmm_family_step(model, table, slot_offsets, feats: dict, label, dtype=torch
     return float(loss.detach()), y, list(grads[:-1]), gE.reshape(-1, table.shape[1])
 
 
+def esmm_grad_magnitude(model, table, slot_offsets, feats: dict, label, chunks=32):
+    """Float64 magnitude of every dense gradient over the batch: Σ_k |g_k| over `chunks`
+    contiguous chunks of the batch, g_k = chunk k's contribution to the batch-mean gradient.
+    Any fp32 reduction over the batch errs by a small multiple of eps·Σ_k |g_k| (the chunks still
+    cancel inside); the tests use it as the per-element floor of the dense-gradient check where
+    the gradient itself is a near-cancelling sum of 10^5 terms."""
+    B = label.shape[0]
+    c = B // chunks
+    mag = None
+    for k in range(chunks):
+        sl = slice(k * c, (k + 1) * c if k < chunks - 1 else B)
+        n = sl.stop - sl.start
+        g = esmm_family_step(model, table, slot_offsets, {f: v[sl] for f, v in feats.items()},
+                             label[sl], dtype=torch.float64)[2]
+        g = [(t * (n / B)).abs() for t in g]
+        mag = g if mag is None else [a + b for a, b in zip(mag, g)]
+    return mag
+
+
 # ---- EGES / GES / DeepWalk (eges/model.py:20-102, eges/train.py:14-24) ---------------------
 def eges_step(model, inputs, labels):
     """Loss (sigmoid CE on the 1 + num_ns skip-gram logits, reduce_mean) and, per table, its

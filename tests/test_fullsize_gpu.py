@@ -80,9 +80,10 @@ def test_cfg4_full_size_keras_adam_steps_vs_oracle(kind):
     three batch orders + a floor of the tensor's largest), dense parameters = Keras Adam of their
     gradients bit for bit, and the 40M-row slab / m / v bit-exact at every touched row and at
     200 000 random other rows (Keras' dense decay included)."""
-    from oracle.models import esmm_family_step, keras_adam_torch
+    from oracle.models import esmm_family_step, esmm_grad_magnitude, keras_adam_torch
     from recommender_amd.esmm.train import MultiTaskStep, build
     from recommender_amd.synthetic import aliccp_batch
+    from tests.test_dien_step_gpu import assert_close_f64 as assert_close_mag
 
     vocab = _cfg4_vocab()
     assert sum(vocab.values()) == CFG4_ROWS
@@ -121,13 +122,17 @@ def test_cfg4_full_size_keras_adam_steps_vs_oracle(kind):
             perms = [None] + [torch.randperm(CFG4_BATCH, generator=gp).to(DEV) for _ in range(2)]
             r32 = [esmm_family_step(model, w0_full, slab.slot_offsets, feats, lab_t, perm=p)
                    for p in perms]
+            mag = esmm_grad_magnitude(model, w0_full, slab.slot_offsets, feats, lab_t)
             loss = float(step(feats, lab_t))
             torch.cuda.synchronize()
             assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
             assert_close_f64(step.last_pred, ref_y, [r[1] for r in r32], "outputs")
             c = {k: float(x) for k, x in OE.keras_adam_coefficients(it).items()}
             for i, (p, p0, rg) in enumerate(zip(step.dense, dense0, ref_dg)):
-                assert_close_f64(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}")
+                # + 1e-5 of the float64 batch-reduction magnitude: at B 65 536 a dense gradient
+                # element is a near-cancelling sum of 10^5 terms, whose fp32 rounding in the
+                # GPU's reduction order the three sampled orders need not span
+                assert_close_mag(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}", mag[i])
                 m0, v0 = st0[i] if st0[i] is not None else (torch.zeros_like(p0),) * 2
                 want, _, _ = keras_adam_torch(p0, m0, v0, p.grad, c)
                 assert torch.equal(p.detach(), want), f"dense parameter {i}"
