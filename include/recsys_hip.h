@@ -122,6 +122,23 @@ int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos
                           int32_t* n_unique, int32_t* owner_counts, void* workspace,
                           size_t ws_bytes, void* stream);
 
+/* Capacity-bounded exchange of the row-sharded slab (recommender_amd/sharded.py; replaces the
+ * MirroredStrategy replicas of ctr/train.py:71-97 with row sharding). Every rank
+ * gives every owner `capacity` row slots: unique u (sorted owner-major, from rs_unique_inverse)
+ * of owner o takes slot o*capacity + (u - first unique of o); send_ids[world*capacity] = the
+ * owner-local rows (-1 = padding), slot_of_unique[u] = its slot (-1 past capacity: *overflow
+ * is set), inverse_slot[p] = slot of position p's unique row (-1 for OOB ids / past capacity).
+ * Both all-to-alls then move equal [world, capacity] blocks: no host sync on the counts. */
+int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_unique,
+                         const int32_t* owner_counts, int32_t world, int64_t shard_stride,
+                         int64_t capacity, const int32_t* inverse, int64_t n_ids,
+                         int32_t* send_ids, int32_t* slot_of_unique, int32_t* inverse_slot,
+                         int32_t* overflow, void* stream);
+/* The owner's side of the exchange: out[i] = shard[ids[i]], a zero row where ids[i] < 0
+ * (padding) or out of range; no error flag (padding is expected). */
+int32_t rs_gather_rows_padded(const float* shard, int64_t n_rows, int32_t dim, const int32_t* ids,
+                              int64_t n, float* out, void* stream);
+
 /* a-2 (part 2) deduplicated gradient: uniq_rows[u], uniq_grad[u, dim] for the n_unique
  * distinct valid rows (count from rs_sort_ids), uniq_grad[u] = Σ grad_out[p] over the
  * positions p of row u. Summation order: sequential over sorted positions inside tiles of
@@ -141,6 +158,15 @@ int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows, const int32_
                                        const float* row_scale, int32_t scale_group, int32_t dim,
                                        int64_t n_rows, uint32_t* uniq_rows, float* uniq_grad,
                                        void* workspace, size_t ws_bytes, void* stream);
+/* rs_embedding_dedup_grad_scaled writing segment s's sum to uniq_grad row seg_map[s] (skipped
+ * when < 0): the row-sharded step's per-owner padded send buffer (rs_exchange_pack's
+ * slot_of_unique). uniq_rows[s] as before. */
+int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                       int64_t n_ids, const float* grad_out,
+                                       const float* row_scale, int32_t scale_group, int32_t dim,
+                                       int64_t n_rows, const int32_t* seg_map, uint32_t* uniq_rows,
+                                       float* uniq_grad, void* workspace, size_t ws_bytes,
+                                       void* stream);
 
 /* The deduplicated gradient as a dense [n_rows, dim] tensor: rows without ids 0, every other row
  * its segment sum (same additions, same order as rs_embedding_dedup_grad); dense is fully written.

@@ -161,13 +161,17 @@ struct ApplyArgs {
   float* uniq_grad;
   uint32_t* uniq_rows;
   const int32_t* seg_excl;  // exclusive scan of head flags
+  // OPT_EMIT: segment s's sum goes to uniq_grad row seg_map[s] (skipped when < 0) instead of
+  // row s (the row-sharded exchange's padded per-owner send buffer, rs_exchange_pack)
+  const int32_t* seg_map;
 };
 
 template <int OPT, int VEC>
 __device__ __forceinline__ void finalize_chunk(const ApplyArgs& a, uint32_t row, int col,
                                                const float (&g)[VEC], int32_t seg_id) {
   if constexpr (OPT == OPT_EMIT) {
-    RowIO<VEC>::store(a.uniq_grad + (int64_t)seg_id * a.dim + col, g);
+    const int32_t dst = a.seg_map ? a.seg_map[seg_id] : seg_id;
+    if (dst >= 0) RowIO<VEC>::store(a.uniq_grad + (int64_t)dst * a.dim + col, g);
   } else if constexpr (OPT == OPT_DENSE) {
     RowIO<VEC>::store(a.table + (int64_t)row * a.dim + col, g);
   } else if constexpr (OPT == OPT_SGD) {
@@ -1102,12 +1106,32 @@ extern "C" int32_t rs_embedding_dedup_grad(const uint32_t* sorted_rows, const in
                                         n_rows, uniq_rows, uniq_grad, workspace, ws_bytes, stream);
 }
 
+extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
+                                                  const int32_t* sorted_pos, int64_t n_ids,
+                                                  const float* grad_out, const float* row_scale,
+                                                  int32_t scale_group, int32_t dim, int64_t n_rows,
+                                                  const int32_t* seg_map, uint32_t* uniq_rows,
+                                                  float* uniq_grad, void* workspace,
+                                                  size_t ws_bytes, void* stream);
+
 extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
                                                   const int32_t* sorted_pos, int64_t n_ids,
                                                   const float* grad_out, const float* row_scale,
                                                   int32_t scale_group, int32_t dim, int64_t n_rows,
                                                   uint32_t* uniq_rows, float* uniq_grad,
                                                   void* workspace, size_t ws_bytes, void* stream) {
+  return rs_embedding_dedup_grad_mapped(sorted_rows, sorted_pos, n_ids, grad_out, row_scale,
+                                        scale_group, dim, n_rows, nullptr, uniq_rows, uniq_grad,
+                                        workspace, ws_bytes, stream);
+}
+
+extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
+                                                  const int32_t* sorted_pos, int64_t n_ids,
+                                                  const float* grad_out, const float* row_scale,
+                                                  int32_t scale_group, int32_t dim, int64_t n_rows,
+                                                  const int32_t* seg_map, uint32_t* uniq_rows,
+                                                  float* uniq_grad, void* workspace,
+                                                  size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
   RS_CHECK_ARG(!row_scale || scale_group >= 1, "scale_group must be >= 1");
   if (n_ids == 0) return RS_OK;
@@ -1136,6 +1160,7 @@ extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
   a.seg_excl = seg;
   a.row_scale = row_scale;
   a.scale_group = scale_group;
+  a.seg_map = seg_map;
   const void* ptrs[2] = {grad_out, uniq_grad};
   RowGeom geom = row_geom(dim, ptrs, 2);
   return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);

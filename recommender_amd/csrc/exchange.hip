@@ -1,0 +1,137 @@
+// exchange.hip — the row-sharded slab's capacity-bounded exchange (BASELINE north
+// star "tables shard row-wise across the 8 GPUs of one node with RCCL all-to-all over xGMI").
+//
+// Every rank sends every owner a fixed `capacity` C of row slots per step, so both all-to-alls
+// of a step (row ids out, rows back; gradient rows out) move [world, C] blocks with EQUAL split
+// sizes: no host sync on the counts, and the whole step can be stream-ordered and graph-captured.
+// A rank's unique rows (owner-major sorted keys, rs_unique_inverse) are dealt to the slots in
+// key order: unique u of owner o goes to slot o·C + (u − first unique of o). Slots left over are
+// padding (id −1: the owner gathers a zero row and its apply leaves the slot out). A rank with
+// more than C unique rows for one owner sets `overflow` (the rows past C are not exchanged; the
+// host raises before trusting the step: recommender_amd/sharded.py).
+#include "common.hpp"
+
+namespace rs {
+
+// ostart[o] = first unique of owner o: an exclusive scan of owner_counts, made per block in LDS
+constexpr int kMaxWorld = 1024;
+
+__device__ __forceinline__ void owner_starts(const int32_t* counts, int world, int32_t* ostart) {
+  if (threadIdx.x == 0) {
+    int32_t run = 0;
+    for (int o = 0; o < world; ++o) {
+      ostart[o] = run;
+      run += counts[o];
+    }
+  }
+  __syncthreads();
+}
+
+// unique u → padded slot (or −1 past capacity), and the send buffer's row ids
+__global__ __launch_bounds__(256) void exchange_slots_kernel(
+    const uint32_t* __restrict__ uniq, const int32_t* __restrict__ n_unique,
+    const int32_t* __restrict__ counts, int world, int64_t stride, int64_t cap, int64_t n_max,
+    int32_t* __restrict__ send_ids, int32_t* __restrict__ slot_of, int32_t* __restrict__ overflow) {
+  __shared__ int32_t ostart[kMaxWorld];
+  owner_starts(counts, world, ostart);
+  const int64_t U = *n_unique;
+  bool over = false;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_max;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    if (u >= U) break;
+    const int64_t key = uniq[u];
+    const int o = (int)(key / stride);
+    const int64_t j = u - ostart[o];
+    if (j < cap) {
+      const int64_t slot = (int64_t)o * cap + j;
+      send_ids[slot] = (int32_t)(key - (int64_t)o * stride);
+      slot_of[u] = (int32_t)slot;
+    } else {
+      slot_of[u] = -1;
+      over = true;
+    }
+  }
+  if (__any(over) && (threadIdx.x & 63) == 0) atomicOr(overflow, 1);
+}
+
+// position p → the padded slot of its unique row (−1: OOB id or a row past capacity)
+__global__ __launch_bounds__(256) void exchange_inverse_kernel(const int32_t* __restrict__ inverse,
+                                                               const int32_t* __restrict__ slot_of,
+                                                               int64_t n,
+                                                               int32_t* __restrict__ inv_slot) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = inverse[p];
+    inv_slot[p] = u >= 0 ? slot_of[u] : -1;
+  }
+}
+
+// the owner's side: out[i] = shard[ids[i]] for ids in range, a zero row for padding (ids < 0).
+// A half-wave (32 lanes x float4) per row at D = 128; rows of other widths by float lanes.
+__global__ __launch_bounds__(256) void gather_padded_kernel(const float* __restrict__ shard,
+                                                            int64_t n_rows, int dim,
+                                                            const int32_t* __restrict__ ids,
+                                                            int64_t n, float* __restrict__ out) {
+  const bool vec = (dim & 3) == 0;
+  const int lanes = vec ? (dim / 4 < 64 ? dim / 4 : 64) : (dim < 64 ? dim : 64);
+  const int per_block = 256 / lanes;
+  const int sub = threadIdx.x / lanes, l = threadIdx.x % lanes;
+  if (sub >= per_block) return;
+  for (int64_t i = blockIdx.x * (int64_t)per_block + sub; i < n;
+       i += (int64_t)gridDim.x * per_block) {
+    const int32_t r = ids[i];
+    const bool ok = r >= 0 && r < n_rows;
+    float* dst = out + i * dim;
+    if (vec) {
+      const float4* src = reinterpret_cast<const float4*>(shard + (ok ? (int64_t)r * dim : 0));
+      for (int c = l; c < dim / 4; c += lanes)
+        reinterpret_cast<float4*>(dst)[c] = ok ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      for (int c = l; c < dim; c += lanes) dst[c] = ok ? shard[(int64_t)r * dim + c] : 0.f;
+    }
+  }
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_unique,
+                                    const int32_t* owner_counts, int32_t world, int64_t shard_stride,
+                                    int64_t capacity, const int32_t* inverse, int64_t n_ids,
+                                    int32_t* send_ids, int32_t* slot_of_unique,
+                                    int32_t* inverse_slot, int32_t* overflow, void* stream) {
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld, "world out of range");
+  RS_CHECK_ARG(shard_stride > 0 && capacity > 0 && n_ids >= 0, "bad sizes");
+  RS_CHECK_ARG((int64_t)world * capacity < (int64_t(1) << 31), "world x capacity out of range");
+  RS_CHECK_ARG(send_ids && n_unique && owner_counts && overflow, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_CHECK_HIP(hipMemsetAsync(send_ids, 0xFF, (size_t)world * capacity * sizeof(int32_t), st));
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(uniq_keys && inverse && slot_of_unique && inverse_slot, "null pointer");
+  const int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 2048);
+  exchange_slots_kernel<<<blocks, 256, 0, st>>>(uniq_keys, n_unique, owner_counts, world,
+                                                shard_stride, capacity, n_ids, send_ids,
+                                                slot_of_unique, overflow);
+  RS_CHECK_LAUNCH();
+  exchange_inverse_kernel<<<blocks, 256, 0, st>>>(inverse, slot_of_unique, n_ids, inverse_slot);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_gather_rows_padded(const float* shard, int64_t n_rows, int32_t dim,
+                                         const int32_t* ids, int64_t n, float* out, void* stream) {
+  RS_CHECK_ARG(dim > 0 && n >= 0 && n_rows >= 0, "bad sizes");
+  if (n == 0) return RS_OK;
+  RS_CHECK_ARG(ids && out && (shard || n_rows == 0), "null pointer");
+  RS_CHECK_ARG((dim & 3) != 0 || ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(shard)) & 15) == 0,
+               "rows of a multiple-of-4 width must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const bool vec = (dim & 3) == 0;
+  const int lanes = vec ? (dim / 4 < 64 ? dim / 4 : 64) : (dim < 64 ? dim : 64);
+  const int64_t per_block = 256 / lanes;
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, per_block), 4096);
+  gather_padded_kernel<<<blocks, 256, 0, st>>>(shard, n_rows, dim, ids, n, out);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}

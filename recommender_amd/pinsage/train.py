@@ -83,9 +83,19 @@ class PinSageStep:
         gradients — Keras' sparse Adam decays m / v and moves every row anyway
         (_resource_apply_sparse [3p TF 2.2]), so the dense form is the same update. Equal to
         __call__ on the unpadded batch up to fp32 rounding order (tests/test_pinsage_gpu.py).
-        Its Adam state (GraphKerasAdam) is its own: do not interleave with __call__."""
-        if self.world > 1:
-            raise ValueError("static_step is single-replica (the sharded step all-reduces)")
+        Its Adam state (GraphKerasAdam) is its own: do not interleave with __call__.
+
+        world > 1 (pairs sharded over the ranks, graph and tables replicated):
+        every gradient lands in GraphKerasAdam's one flat gradient buffer, which is all-reduced
+        (one collective: RCCL under nccl, so the sharded step captures into a HIP graph too) and
+        scaled 1/W before the Adam launch — MirroredStrategy's mean of the replicas' gradients
+        (pinsage/train/train.py:40-48), as __call__ does eagerly. The layout is fixed, so every
+        parameter must have a gradient on every rank (capacity-shaped batches look up every
+        table)."""
+        if (self.world > 1 and getattr(self.comm, "staged", False)
+                and torch.cuda.is_current_stream_capturing()):
+            raise ValueError("a gloo-staged all-reduce cannot be captured: capture the sharded "
+                             "step under RCCL (nccl)")
         tables = self.model.tables()
         if getattr(self, "opt_graph", None) is None:
             self.opt_graph = GraphKerasAdam(self.dense + [t.weight for t in tables],
@@ -104,6 +114,18 @@ class PinSageStep:
             grads.append(densify_grad(t, got[0], got[1], self._ws,
                                       out=self.opt_graph.grad_view(nd + i)) if got is not None
                          else None)
+        if self.world > 1:
+            if any(g is None for g in grads):
+                raise ValueError("sharded static_step: a parameter has no gradient on this rank; "
+                                 "the all-reduce needs the same flat layout on every rank")
+            opt = self.opt_graph
+            for i, g in enumerate(grads):
+                dst = opt.grad_view(i)
+                if g.data_ptr() != dst.data_ptr():
+                    dst.copy_(g.reshape(dst.shape))
+            self.comm.all_reduce_(opt.grad_flat)
+            opt.grad_flat.mul_(1.0 / self.world)
+            grads = [opt.grad_view(i) for i in range(len(grads))]
         if not torch.cuda.is_current_stream_capturing():
             self.opt_graph.prepare()
             self.opt_graph.iterations += 1  # a capture records the step; replay() counts it

@@ -5,19 +5,27 @@ Layout: global row g lives on rank g % W at local row g // W (cyclic deal, so th
 rows of every slot spread over all ranks). Per step, on each rank:
 
   forward   sort ids by owner-major key (rs_sort_ids_sharded) → unique keys + inverse map +
-            per-owner counts (rs_unique_inverse) → all-to-all of the unique local rows each
-            owner must serve → owners gather them (rs_embedding_fwd on the shard) → all-to-all
-            of the rows back. The step's kernels then read rows from the unique-row buffer by
-            the inverse index, so nothing downstream changes.
-  backward  grad rows (position order) → tiled segmented sum per unique row
-            (rs_embedding_dedup_grad) → all-to-all to owners → each owner sorts the received
-            (local row, source-rank-major) list and applies the optimizer with the same tiled
-            fold (rs_sort_ids + rs_embedding_apply); the update is scaled 1/W (the global loss
-            is the mean over W local batches).
+            per-owner counts (rs_unique_inverse) → capacity-bounded packing (rs_exchange_pack:
+            unique row u of owner o takes slot o·C + its rank among o's rows in a [W, C] block,
+            every position the slot of its row) → all-to-all of the row ids (equal C-row blocks)
+            → owners gather them (rs_gather_rows_padded; padding slots read zero rows) →
+            all-to-all of the rows back. The step's kernels read rows from the [W·C, D] block
+            by the slot index, so nothing downstream changes.
+  backward  grad rows (position order) → tiled segmented sum per unique row written straight
+            into its slot (rs_embedding_dedup_grad_mapped) → all-to-all to owners (equal
+            blocks) → each owner sorts the received (local row, source-rank-major) slots,
+            padding left out (masked sort), and applies the optimizer with the same tiled fold;
+            rows of each rank's local mean are scaled 1/W, the fused DLRM step's rows (of the
+            global mean) are applied as they are.
 
-The exchange chain runs on a side HIP stream; RCCL all-to-all runs on its own stream, so the
-exchange overlaps the bottom MLP on the main stream. One host sync per step reads the W owner
-counts (the all-to-all split sizes).
+The capacity C (row slots per (rank, owner) pair) is calibrated once, on the first exchanged
+batch (the largest per-owner unique count over all ranks x capacity_factor + 256), so every
+later all-to-all has fixed equal split sizes: no host sync per step, and the whole sharded step
+is stream-ordered (graph-capturable under RCCL). A batch with more than C unique rows for one
+owner sets an overflow flag that the host raises on (check_overflow) — loud, never silent.
+The exchange runs on a side HIP stream (RCCL all-to-alls on their own), overlapping the bottom
+MLP on the main stream; its first half (sort … row-id all-to-all) reads no table state and can
+be queued a step ahead (prefetch).
 """
 from __future__ import annotations
 
@@ -40,16 +48,19 @@ class Comm:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
+        """Splits None: equal blocks (the sharded slab's capacity-bounded exchange)."""
         if self.world == 1:
             out.copy_(inp)
             return
+        osp = None if out_splits is None else list(out_splits)
+        isp = None if in_splits is None else list(in_splits)
         if self.staged:
             o = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(o, inp.cpu(), list(out_splits), list(in_splits), group=self.group)
+            dist.all_to_all_single(o, inp.cpu(), osp, isp, group=self.group)
             out.copy_(o)
         else:
-            dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.group)
+            dist.all_to_all_single(out, inp, osp, isp, group=self.group)
 
     def all_reduce_(self, t: torch.Tensor):
         if self.world == 1:
@@ -86,7 +97,8 @@ class _UniqueRows:
 
 class ShardedSlabEmbedding(nn.Module):
     def __init__(self, cardinalities, dim: int, comm: Comm | None = None, device=None,
-                 generator: torch.Generator | None = None, full_weight: torch.Tensor | None = None):
+                 generator: torch.Generator | None = None, full_weight: torch.Tensor | None = None,
+                 capacity: int | None = None, capacity_factor: float = 1.5):
         super().__init__()
         self.comm = comm or Comm()
         W, r = self.comm.world, self.comm.rank
@@ -111,6 +123,11 @@ class ShardedSlabEmbedding(nn.Module):
         self.optimizer: SparseOptimizer | None = None
         self._st = None  # per-step exchange state
         self._prefetched: list = []  # exchange_begin states queued ahead, FIFO (prefetch)
+        # exchange capacity: row slots per (rank, owner) pair; None = calibrated on the first
+        # batch (_calibrate), then fixed
+        self.capacity = capacity
+        self.capacity_factor = float(capacity_factor)
+        self._overflow_checks: list = []  # (event, pinned flag) of packed exchanges
 
     @property
     def n_slots(self):
@@ -122,15 +139,34 @@ class ShardedSlabEmbedding(nn.Module):
         self.optimizer = opt
 
     # ---------------------------------------------------------------- forward
+    def _calibrate(self, counts: torch.Tensor):
+        """The exchange capacity (row slots per (rank, owner) pair, the same on every rank): the
+        largest per-owner unique count of the first exchanged batch over all ranks, times
+        capacity_factor, + 256, rounded up to 256. The only host sync of the exchange; every
+        later step moves fixed [world, capacity] blocks."""
+        mx = counts.max().to(torch.int64).reshape(1)
+        if self.world > 1:
+            if self.comm.staged:
+                c = mx.cpu()
+                dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.comm.group)
+                mx = c
+            else:
+                dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.comm.group)
+        need = int(mx.item())
+        self.capacity = -(-(int(need * self.capacity_factor) + 256) // 256) * 256
+
     def exchange_begin(self, ids: torch.Tensor):
-        """Queue the owner-major sort, the unique / inverse pass and the split-size exchange on
-        the side stream without blocking the host; DLRM calls this before it queues the bottom
-        MLP, so the sort runs beside it (the side stream only waits for work queued so far)."""
+        """Queue the first half of a step's exchange on the side stream: owner-major sort, unique
+        / inverse + per-owner counts, the capacity-bounded packing (rs_exchange_pack: every
+        unique row gets a fixed slot in a [world, capacity] send block, each position the slot
+        of its row) and the all-to-all of the row ids. Nothing here reads the table, so it may
+        run a step ahead (prefetch); no host sync once the capacity is known."""
         L.require_device(ids, "ids")
         dev = ids.device
         ids = ids.contiguous()
         main = torch.cuda.current_stream(dev)
         self.side.wait_stream(main)
+        self.check_overflow(block=False)
         W = self.world
         with torch.cuda.stream(self.side):
             s = SortedIds(ids, self.input_dim, self.slot_offsets, self.err_flag, self.ws,
@@ -144,34 +180,57 @@ class ShardedSlabEmbedding(nn.Module):
             L.call("rs_unique_inverse", L.ptr(s.rows), L.ptr(s.pos), n, self.input_dim, W,
                    L.ptr(uniq), L.ptr(inverse), L.ptr(n_unique), L.ptr(counts), L.ptr(w),
                    w.numel(), L.stream_ptr(dev))
-            staged = self.comm.staged or not dist.is_initialized() or W == 1
-            host = torch.empty(2 * W, dtype=torch.int32, pin_memory=True)
-            if staged:
-                host[:W].copy_(counts, non_blocking=True)
-            else:
-                # receive counts device to device, then ONE copy of both count vectors to the host
-                recv = torch.empty_like(counts)
-                dist.all_to_all_single(recv, counts, group=self.comm.group)
-                host.copy_(torch.cat([counts, recv]), non_blocking=True)
-            ready = torch.cuda.Event()
-            ready.record(self.side)
-        return dict(ids=ids, s=s, uniq=uniq, inverse=inverse, host=host, ready=ready,
-                    staged=staged, dev=dev)
+            if self.capacity is None:
+                self._calibrate(counts)
+            C = self.capacity
+            send_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
+            slot_of = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            inv_slot = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            L.call("rs_exchange_pack", L.ptr(uniq), L.ptr(n_unique), L.ptr(counts), W,
+                   self.stride, C, L.ptr(inverse), n, L.ptr(send_ids), L.ptr(slot_of),
+                   L.ptr(inv_slot), L.ptr(overflow), L.stream_ptr(dev))
+            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            host.copy_(overflow, non_blocking=True)
+            ovf_ready = torch.cuda.Event()
+            ovf_ready.record(self.side)
+            recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
+            self.comm.all_to_all(recv_ids, send_ids)
+        self._overflow_checks.append((ovf_ready, host))
+        return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot[:n], recv_ids=recv_ids,
+                    capacity=C, dev=dev)
+
+    def check_overflow(self, block: bool = True):
+        """Raise if a packed exchange had more unique rows for one owner than the capacity (the
+        rows past it were not exchanged, so that step's results are wrong). block=False only
+        looks at packings whose flag has reached the host; exchange_begin calls it so, join()
+        with block=True."""
+        keep = []
+        for ev, host in self._overflow_checks:
+            if not block and not ev.query():
+                keep.append((ev, host))
+                continue
+            ev.synchronize()
+            if int(host.item()):
+                self._overflow_checks = []
+                raise RuntimeError(
+                    f"ShardedSlabEmbedding: a rank had more unique rows for one owner than the "
+                    f"exchange capacity ({self.capacity}); rebuild with a larger capacity_factor "
+                    f"(now {self.capacity_factor}) or an explicit capacity")
+        self._overflow_checks = keep
 
     @staticmethod
     def _ids_key(ids):
         return (ids.data_ptr(), tuple(ids.shape), ids.dtype)
 
     def prefetch(self, ids: torch.Tensor):
-        """Queue the first half of a LATER step's exchange now (owner-major sort, unique /
-        inverse, split sizes: exchange_begin) so that step's exchange_finish finds its split
-        sizes already on the host: the one host sync of a sharded step then waits on work queued
-        a step earlier instead of stalling the device. The split-size exchange is a collective,
-        so every rank must prefetch the same steps in the same order. Entries are kept in queue
-        order: a step takes its own entry and drops the older ones (steps that never ran), a
-        step with no entry exchanges afresh, and a step whose entry's ids changed in place
-        raises instead of re-exchanging (which one rank alone might do, pairing the ranks'
-        collectives wrongly)."""
+        """Queue the first half of a LATER step's exchange now (exchange_begin: sort, unique,
+        packing, the row-id all-to-all) so it runs beside the current step; that step then
+        starts from the owners' gather. The all-to-all is a collective, so every rank must
+        prefetch the same steps in the same order. Entries are kept in queue order: a step
+        takes its own entry and drops the older ones (steps that never ran), a step with no
+        entry exchanges afresh, and a step whose entry's ids changed in place raises instead of
+        re-exchanging (which one rank alone might do, pairing the ranks' collectives wrongly)."""
         if torch.cuda.is_current_stream_capturing():
             return
         if len(self._prefetched) >= 4:  # stale entries (steps that never ran)
@@ -191,55 +250,32 @@ class ShardedSlabEmbedding(nn.Module):
         return None
 
     def exchange_finish(self, st):
-        """Wait (host) for the split sizes, then the two all-to-alls and the owner gather;
-        returns (view, inverse ids [B, S] int32)."""
-        dev, W = st["dev"], self.world
+        """The second half, on the side stream after the previous step's owner apply: the owners
+        gather the requested rows (rs_gather_rows_padded: padding slots read zero rows) and the
+        rows go back in one all-to-all of equal [capacity, D] blocks. Returns (view: the
+        [world * capacity, D] rows, inverse ids [B, S] int32 = each position's slot)."""
+        dev, W, C = st["dev"], self.world, st["capacity"]
         main = torch.cuda.current_stream(dev)
-        st["ready"].synchronize()  # the one host sync of the step (split sizes)
-        send_counts = st["host"][:W].clone()
+        D = self.output_dim
         with torch.cuda.stream(self.side):
-            U = int(send_counts.sum())
-            if W == 1:
-                recv_counts = send_counts
-            elif st["staged"]:
-                recv_counts = torch.empty(W, dtype=torch.int32)
-                self.comm_counts(recv_counts, send_counts)
-            else:
-                recv_counts = st["host"][W:].clone()
-            R = int(recv_counts.sum())
-            owner = torch.arange(W, device=dev, dtype=torch.int64).repeat_interleave(
-                send_counts.to(dev, torch.int64), output_size=U)
-            send_rows = (st["uniq"][:U].to(torch.int64) - owner * self.stride).to(torch.int32)
-            recv_rows = torch.empty(R, dtype=torch.int32, device=dev)
-            sc, rc = send_counts.tolist(), recv_counts.tolist()
-            self.comm.all_to_all(recv_rows, send_rows, rc, sc)
-            with torch.no_grad():
-                served = self.shard(recv_rows) if R else torch.empty(0, self.output_dim, device=dev)
-            rows = torch.empty(U, self.output_dim, device=dev)
-            self.comm.all_to_all(rows, served.detach().contiguous(), sc, rc)
-        inverse = st["inverse"]
+            served = torch.empty(W * C, D, device=dev)
+            L.call("rs_gather_rows_padded", L.ptr(self.shard.weight), self.shard.input_dim, D,
+                   L.ptr(st["recv_ids"]), W * C, L.ptr(served), L.stream_ptr(dev))
+            rows = torch.empty(W * C, D, device=dev)
+            self.comm.all_to_all(rows, served)
         main.wait_stream(self.side)
+        inverse = st["inv_slot"]
         for t in (rows, inverse):
             t.record_stream(main)
         self.view.weight = rows
-        self.view.input_dim = U
-        self._st = dict(sorted=st["s"], U=U, R=R, send_counts=sc, recv_counts=rc,
-                        recv_rows=recv_rows)
+        self.view.input_dim = W * C
+        self._st = dict(sorted=st["s"], slot_of=st["slot_of"], recv_ids=st["recv_ids"], capacity=C)
         return self.view, inverse.view(st["ids"].shape)
 
     def exchange(self, ids: torch.Tensor):
         """Fetch this step's unique rows; returns (view, inverse ids [B, S] int32)."""
         st = self.take_prefetched(ids.contiguous())
         return self.exchange_finish(st if st is not None else self.exchange_begin(ids))
-
-    def comm_counts(self, recv_counts: torch.Tensor, send_counts: torch.Tensor):
-        if self.comm.staged or not dist.is_initialized():
-            dist.all_to_all_single(recv_counts, send_counts.clone(), group=self.comm.group)
-        else:
-            d = send_counts.to(self.slot_offsets.device)
-            r = torch.empty_like(d)
-            dist.all_to_all_single(r, d, group=self.comm.group)
-            recv_counts.copy_(r.cpu())
 
     def forward(self, ids):
         """Plain lookup [.., D] (DeepFM / ESMM style): exchange, then expand by the inverse."""
@@ -258,7 +294,10 @@ class ShardedSlabEmbedding(nn.Module):
         kernel scales by 1/(B·W)), so the owners apply them as they are; otherwise each rank's
         rows are of its local mean and the update is scaled 1/W. row_scale [B] (optional): the
         row of position p is row_scale[p // S] * grad_rows[p] (the fused step's unit rows and
-        G[b]), formed inside the local segmented sum."""
+        G[b]), formed inside the local segmented sum. The per-unique-row sums go straight into
+        their slots of the [world, capacity] send block (rs_embedding_dedup_grad_mapped), one
+        all-to-all of equal blocks, then each owner applies the received rows in (source rank,
+        slot) order, padding slots left out of its masked sort."""
         st = self._st
         if st is None:
             raise RuntimeError("backward without a forward exchange")
@@ -266,52 +305,44 @@ class ShardedSlabEmbedding(nn.Module):
         main = torch.cuda.current_stream(dev)
         self.side.wait_stream(main)
         s = st["sorted"]
+        W, C, D = self.world, st["capacity"], self.output_dim
         with torch.cuda.stream(self.side):
-            U, R, D = st["U"], st["R"], self.output_dim
             g = grad_rows.contiguous()
+            send_grad = torch.empty(W * C, D, dtype=torch.float32, device=dev)
             uniq_rows = torch.empty(max(s.n, 1), dtype=torch.int32, device=dev)
-            uniq_grad = torch.empty(max(s.n, 1), D, dtype=torch.float32, device=dev)
             if s.n:
                 w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(s.n, D), dev)
-                if row_scale is None:
-                    L.call("rs_embedding_dedup_grad", L.ptr(s.rows), L.ptr(s.pos), s.n, L.ptr(g),
-                           D, self.key_space, L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w),
-                           w.numel(), L.stream_ptr(dev))
-                else:
-                    if row_scale.numel() * self.n_slots != s.n:
-                        raise ValueError("row_scale must hold one value per example")
-                    L.call("rs_embedding_dedup_grad_scaled", L.ptr(s.rows), L.ptr(s.pos), s.n,
-                           L.ptr(g), L.ptr(row_scale), self.n_slots, D, self.key_space,
-                           L.ptr(uniq_rows), L.ptr(uniq_grad), L.ptr(w), w.numel(),
-                           L.stream_ptr(dev))
-            recv_grad = torch.empty(R, D, dtype=torch.float32, device=dev)
-            self.comm.all_to_all(recv_grad, uniq_grad[:U], st["recv_counts"], st["send_counts"])
+                if row_scale is not None and row_scale.numel() * self.n_slots != s.n:
+                    raise ValueError("row_scale must hold one value per example")
+                L.call("rs_embedding_dedup_grad_mapped", L.ptr(s.rows), L.ptr(s.pos), s.n,
+                       L.ptr(g), L.ptr(row_scale), self.n_slots if row_scale is not None else 1,
+                       D, self.key_space, L.ptr(st["slot_of"]), L.ptr(uniq_rows),
+                       L.ptr(send_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
+            recv_grad = torch.empty(W * C, D, dtype=torch.float32, device=dev)
+            self.comm.all_to_all(recv_grad, send_grad)
             if self.optimizer is None:
                 raise RuntimeError("ShardedSlabEmbedding has no optimizer (set_optimizer)")
             opt = self.optimizer
             params = opt._params()
-            if R:
-                if self.world > 1 and not global_grads:
-                    if opt.kind == L.RS_OPT_SGD:
-                        params.lr = params.lr / self.world  # same as scaling the gradient
-                    else:
-                        recv_grad.mul_(1.0 / self.world)
-                opt.apply(self.shard, st["recv_rows"], recv_grad, params)
-            elif opt.kind == L.RS_OPT_KERAS_ADAM:
-                # no row of this shard was touched this step: Keras Adam still decays m / v and
-                # moves every row (the dense half of _resource_apply_sparse)
-                m, v, bitmap = opt._slots(self.shard)
-                t = self.shard
-                L.call("rs_keras_adam_dense_sweep", L.ptr(t.weight), L.ptr(m), L.ptr(v),
-                       t.input_dim, t.output_dim, params, L.ptr(bitmap), L.stream_ptr(dev))
+            recv_ids = st["recv_ids"]
+            valid = (recv_ids >= 0).to(torch.uint8)
+            if self.world > 1 and not global_grads:
+                if opt.kind == L.RS_OPT_SGD:
+                    params.lr = params.lr / self.world  # same as scaling the gradient
+                else:
+                    recv_grad.mul_(1.0 / self.world)
+            # every owner applies (an owner no rank sent a row to still runs Keras' dense decay)
+            opt.apply(self.shard, recv_ids, recv_grad, params, valid=valid)
         g.record_stream(self.side)
         if row_scale is not None:
             row_scale.record_stream(self.side)
         self._st = None
 
     def join(self):
-        """Make the current stream wait for the exchange / apply chain."""
+        """Make the current stream wait for the exchange / apply chain (and raise if a finished
+        exchange overflowed its capacity)."""
         torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+        self.check_overflow(block=False)
 
     def full_weight(self) -> torch.Tensor:
         """Gather the whole slab (tests / checkpoints): [V, D] with row g from rank g % W."""

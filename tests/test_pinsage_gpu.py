@@ -664,3 +664,129 @@ def test_graph_keras_adam_equals_keras_adam():
         ga.iterations += 1
         for x, y in zip(a, b):
             assert torch.equal(x, y), it
+
+
+def _pinsage_world2_static_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommender_amd.optim import dedup_grad
+        from recommender_amd.pinsage.model import margin_loss
+        from recommender_amd.sharded import Comm
+
+        B = 64
+        g, _ = small_graph(7, n_users=200, n_items=300, n_edges=3000)
+
+        def fresh():
+            return PinSageModel(g, g.itype, 2, 8, 32, 16,
+                                generator=torch.Generator(device=DEV).manual_seed(1))
+
+        # (a) eager sharded step with a dense parameter that has no gradient on rank 1 only, and
+        # one that has none on any rank: same bucket layout on both ranks, the
+        # first moves by the mean (rank 0's gradient / 2), the second is skipped as Keras does
+        model = fresh()
+        step = PinSageStep(model, lr=1e-2, comm=Comm())
+        smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+        dense = model.dense_parameters()
+        x, y = dense[0], dense[1]
+        x0, y0 = x.detach().clone(), y.detach().clone()
+        if rank == 1:
+            x.requires_grad_(False)
+        y.requires_grad_(False)
+        h, p, n = item_pairs(g, B, 4, 0, pair_base=rank * B)
+        step(*smp.sample_from_item_pairs(h, p, n))
+        torch.cuda.synchronize()
+        x.requires_grad_(True)
+        y.requires_grad_(True)
+        assert torch.equal(y, y0), "a parameter without a gradient on every rank must not move"
+        assert not torch.equal(x, x0)
+        mine = _pinsage_params(model)
+        allp = [None] * world
+        dist.all_gather_object(allp, mine)
+        for a, b in zip(allp[0], allp[1]):
+            np.testing.assert_array_equal(a, b)
+
+        # (b) the sync-free static step sharded (flat-buffer all-reduce inside static_step) vs
+        # one process averaging the two sub-batches' gradients (the dynamic step's arithmetic)
+        model = fresh()
+        step = PinSageStep(model, lr=1e-2, comm=Comm())
+        smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+        if rank == 0:
+            ref = fresh()
+            rstep = PinSageStep(ref, lr=1e-2)
+            rsmp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+        for it in range(2):
+            smp.step = it
+            step.static_step(*smp.sample_static(*smp.sample_pairs_static(B, 4, it, rank * B)))
+            if rank == 0:
+                buckets = []
+                for r in range(world):
+                    rstep.opt_dense.zero_grad(set_to_none=True)
+                    rsmp.step = it
+                    hr, pr, nr = item_pairs(g, B, 4, it, pair_base=r * B)
+                    ps, ns = ref(*rsmp.sample_from_item_pairs(hr, pr, nr))
+                    margin_loss(ps, ns, delta=1.0).backward()
+                    grads = [t.grad for t in rstep.dense]
+                    tabs = []
+                    for t in ref.tables():
+                        got = t.take_grad()
+                        d = torch.zeros(t.input_dim, t.output_dim, device=DEV)
+                        rows, ug = dedup_grad(t, got[0], got[1])
+                        d.index_copy_(0, rows, ug)
+                        tabs.append(d)
+                    buckets.append(grads + tabs)
+                avg = [(a + b) * (1.0 / world) for a, b in zip(*buckets)]
+                for t, gavg in zip(rstep.dense, avg[: len(rstep.dense)]):
+                    t.grad = gavg
+                rstep.opt_dense.step()
+                prm = rstep.opt_sparse._params()
+                for t, gavg in zip(ref.tables(), avg[len(rstep.dense):]):
+                    ids = torch.arange(t.input_dim, device=DEV, dtype=torch.int32)
+                    rstep.opt_sparse.apply(t, ids, gavg, prm)
+                rstep.opt_sparse.iterations += 1
+        torch.cuda.synchronize()
+        mine = _pinsage_params(model)
+        allp = [None] * world
+        dist.all_gather_object(allp, mine)
+        if rank == 0:
+            for a, b in zip(allp[0], allp[1]):
+                np.testing.assert_array_equal(a, b)  # the replicas stay identical
+            for a, b in zip(mine, _pinsage_params(ref)):
+                # static vs dynamic batches: fp32 rounding order (as the world-1 comparison)
+                np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_pinsage_static_step_and_missing_gradients():
+    """cfg5's sync-free (graph-capturable) step sharded over two gloo ranks: pairs split by
+    global pair index, the flat gradient buffer all-reduced inside static_step, two steps equal
+    one process averaging the two sub-batches (1e-4: static vs dynamic rounding), replicas
+    bit-identical; and the eager sharded step with a parameter lacking a gradient on one rank
+    (moves by the mean) or on every rank (skipped, as Keras skips it)."""
+    import os
+
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31300 + (os.getpid() % 500)
+    ps = [ctx.Process(target=_pinsage_world2_static_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res

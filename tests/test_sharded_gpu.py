@@ -326,3 +326,32 @@ def test_world2_prefetched_exchange_bit_identical():
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def test_exchange_capacity_overflow_raises():
+    """A batch with more unique rows for one owner than the exchange capacity must not train
+    silently: the packing flags it and the next host check raises. The calibrated capacity of
+    the same slab holds the batch."""
+    from recommender_amd.sharded import Comm, ShardedSlabEmbedding
+    from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
+
+    cards = criteo_cardinalities(100_000, 26)
+    cat, _, _ = criteo_batch(np.random.default_rng(3), 256, cards)
+    ids = torch.from_numpy(cat).to(DEV)
+    tiny = ShardedSlabEmbedding(cards, 16, Comm(), device=DEV, capacity=64)
+    with torch.no_grad():
+        tiny(ids)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="capacity"):
+        tiny.check_overflow()
+    ok = ShardedSlabEmbedding(cards, 16, Comm(), device=DEV)
+    with torch.no_grad():
+        out = ok(ids)
+    torch.cuda.synchronize()
+    ok.check_overflow()
+    assert ok.capacity >= 256
+    # the lookup itself: every position's row from the slab
+    full = ok.full_weight()
+    so = ok.slot_offsets
+    rows = ids.long() + so[:-1][None, :]
+    assert torch.equal(out.reshape(-1, 16), full[rows.reshape(-1)])
