@@ -44,7 +44,10 @@ def run(step_fn, batches, steps, warmup, watch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="dien",
-                    choices=["dien", "mmoe", "esmm", "deepfm", "pinsage", "eges", "dlrm_cfg2"])
+                    choices=["dien", "mmoe", "esmm", "deepfm", "deepfm_file", "pinsage", "eges",
+                             "dlrm_cfg2"])
+    ap.add_argument("--file-rows", type=int, default=1_000_000,
+                    help="deepfm_file: rows of the Criteo-shaped TFRecord file written and trained on")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lazy_adam", "keras_adam"],
                     help="dlrm_cfg2 only (the reference DLRM SGD path or Keras / lazy Adam)")
     ap.add_argument("--steps", type=int, default=20)
@@ -73,6 +76,8 @@ def main():
                          "variable-shape ones (pinsage, eges: 4.6 -> 10.8 ms, 1.16 -> 1.44 ms with it)")
     args = ap.parse_args()
     L.load()
+    if args.model == "deepfm_file":
+        return deepfm_from_file(args)
     if args.tuned_gemms == 1 or (args.tuned_gemms < 0 and args.model in ("dien", "esmm", "mmoe")):
         from recommender_amd.gemm_tuning import use_tuned_gemms
 
@@ -275,6 +280,69 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "unique_rows_per_step": U, "note": "path bytes / whole step time"}
+    print(json.dumps(out))
+
+
+def deepfm_from_file(args):
+    """cfg1 as BASELINE names it: ctr/train.py's DeepFM trained from a 1M-row Criteo-shaped
+    TFRecord file (ctr/train.py:59-66: read_tfrecord → shuffle(100·batch) → batch(1024); DeepFM
+    [512, 256, 1], D 16, joint 1M vocab, Keras Adam). The file is written by the engine's
+    writer (the reference's tf.train.Example layout, tfrecord_io.py:66-75), read back by the
+    device reader (host framing index + one wave per record parse, rs_tfrecord_parse_criteo),
+    shuffled on the device (a seeded permutation: TF's 100·batch shuffle-buffer order is
+    parity-unpinned) and trained for one epoch. Times each stage; the oracle's NumPy step is
+    timed beside it (cpu_baseline)."""
+    from recommender_amd.ctr.train import TrainStep, build_model
+    from recommender_amd.data.tfrecord import read_tfrecord, write_tfrecord
+    from recommender_amd.synthetic import criteo_batch
+
+    dev = torch.device("cuda")
+    n, B, V = args.file_rows, args.batch or 1024, 1_000_000
+    rng = np.random.default_rng(4)
+    cat, dn, lb = criteo_batch(rng, n, [V] * 26)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"cfg1_criteo_{n}.tfrecord")
+    t0 = time.perf_counter()
+    write_tfrecord(path, dn, cat, lb.astype(np.int64))
+    t_write = time.perf_counter() - t0
+    size = os.path.getsize(path)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    feats, label = read_tfrecord(path, dev)
+    torch.cuda.synchronize()
+    t_read = time.perf_counter() - t0
+    ok = (torch.equal(feats["cat_features"].cpu(), torch.from_numpy(cat))
+          and torch.equal(feats["int_features"].cpu(), torch.from_numpy(dn))
+          and torch.equal(label.cpu(), torch.from_numpy(lb.astype(np.int64))))
+    m = build_model("DeepFM", 16, V, 26, 13, dev)
+    step = TrainStep(m, "keras_adam", fused=False)
+    g = torch.Generator(device=dev).manual_seed(4)
+    n_steps = n // B
+    # warm-up on the first batches (library handles, workspaces), not counted in the epoch
+    for i in range(3):
+        step((feats["cat_features"][i * B:(i + 1) * B], feats["int_features"][i * B:(i + 1) * B],
+              label[i * B:(i + 1) * B].float()))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    perm = torch.randperm(n, device=dev, generator=g)
+    cats, dens, labs = (feats["cat_features"][perm], feats["int_features"][perm],
+                        label[perm].float())
+    loss = None
+    for i in range(n_steps):
+        sl = slice(i * B, (i + 1) * B)
+        loss = step((cats[sl], dens[sl], labs[sl]))
+    torch.cuda.synchronize()
+    t_epoch = time.perf_counter() - t0
+    out = {"model": "deepfm_file", "config": {"workload": f"deepfm_criteo_tfrecord_{n}_b{B}_d16",
+                                                "rows": n, "batch": B, "optimizer": "keras_adam",
+                                                "file_bytes": size},
+           "examples_per_sec": round(n_steps * B / t_epoch, 1),
+           "ms_per_step": round(t_epoch / n_steps * 1e3, 3),
+           "examples_per_sec_incl_read": round(n_steps * B / (t_epoch + t_read), 1),
+           "read_parse_s": round(t_read, 3), "read_GBs": round(size / t_read / 1e9, 2),
+           "write_s": round(t_write, 2), "file_roundtrip_bit_exact": bool(ok),
+           "epoch_steps": n_steps, "final_loss": float(loss),
+           "cpu_baseline": deepfm_cpu_baseline(B)}
+    os.remove(path)
     print(json.dumps(out))
 
 

@@ -121,9 +121,65 @@ def encode_records(int_features, cat_features, labels) -> bytes:
     return b"".join(out)
 
 
+def _crc32c_table() -> np.ndarray:
+    t = np.arange(256, dtype=np.uint32)
+    for _ in range(8):
+        t = np.where(t & 1, (t >> 1) ^ np.uint32(0x82F63B78), t >> 1).astype(np.uint32)
+    return t
+
+
+_CRC_TABLE = None
+
+
+def _masked_crc_rows(rows: np.ndarray) -> np.ndarray:
+    """Masked CRC32C (the TFRecord framing checksum) of every row of a [n, m] uint8 array,
+    vectorised over the rows: the byte loop runs over the m columns."""
+    global _CRC_TABLE
+    if _CRC_TABLE is None:
+        _CRC_TABLE = _crc32c_table()
+    crc = np.full(rows.shape[0], 0xFFFFFFFF, np.uint32)
+    for j in range(rows.shape[1]):
+        crc = _CRC_TABLE[(crc ^ rows[:, j]) & 0xFF] ^ (crc >> np.uint32(8))
+    crc ^= np.uint32(0xFFFFFFFF)
+    return (((crc >> np.uint32(15)) | (crc << np.uint32(17))) + np.uint32(0xA282EAD8)).astype(np.uint32)
+
+
+def encode_records_fixed(int_features, cat_features, labels) -> bytes:
+    """encode_records for a whole batch at once, bit-identical: with n_int floats, n_cat int64
+    ids and a label in 0..127 every record has the same byte layout, so one template record is
+    tiled and the data bytes and payload CRCs are filled column-wise (a 1M-row file in seconds
+    instead of a per-record Python loop)."""
+    ints = np.ascontiguousarray(np.asarray(int_features, "<f4"))
+    cats = np.ascontiguousarray(np.asarray(cat_features, "<i8"))
+    labs = np.asarray(labels, np.int64).reshape(-1)
+    n = labs.size
+    if ints.ndim != 2 or cats.ndim != 2 or not (ints.shape[0] == cats.shape[0] == n):
+        raise ValueError("int_features [n, a], cat_features [n, b], labels [n]")
+    if n == 0:
+        return b""
+    if labs.min() < 0 or labs.max() > 127:
+        return encode_records(ints, cats, labs)  # varint labels of other widths
+    a, b = ints.shape[1], cats.shape[1]
+    # a template whose data fields are findable: distinct sentinel values, label 0 vs 1
+    si = (np.arange(a, dtype=np.float32) + np.float32(0.3141)).reshape(1, a)
+    sc = (np.arange(b, dtype=np.int64) + 0x5EED_0000_0000).reshape(1, b)
+    t0 = np.frombuffer(encode_records(si, sc, [0]), np.uint8)
+    t1 = np.frombuffer(encode_records(si, sc, [1]), np.uint8)
+    rec = t0.size
+    io = bytes(t0).find(si.tobytes())
+    co = bytes(t0).find(sc.tobytes())
+    lo = int(np.flatnonzero(t0[12:rec - 4] != t1[12:rec - 4])[0]) + 12
+    out = np.tile(t0, (n, 1))
+    out[:, io:io + 4 * a] = ints.view(np.uint8).reshape(n, 4 * a)
+    out[:, co:co + 8 * b] = cats.view(np.uint8).reshape(n, 8 * b)
+    out[:, lo] = labs.astype(np.uint8)
+    out[:, rec - 4:] = _masked_crc_rows(out[:, 12:rec - 4]).astype("<u4").view(np.uint8).reshape(n, 4)
+    return out.tobytes()
+
+
 def write_tfrecord(path, int_features, cat_features, labels):
     with open(path, "wb") as f:
-        f.write(encode_records(int_features, cat_features, labels))
+        f.write(encode_records_fixed(int_features, cat_features, labels))
 
 
 def encode_tsv(vocab, tsv_src, out_path, device="cuda"):

@@ -129,10 +129,13 @@ def test_cfg4_full_size_keras_adam_steps_vs_oracle(kind):
             assert_close_f64(step.last_pred, ref_y, [r[1] for r in r32], "outputs")
             c = {k: float(x) for k, x in OE.keras_adam_coefficients(it).items()}
             for i, (p, p0, rg) in enumerate(zip(step.dense, dense0, ref_dg)):
-                # + 1e-5 of the float64 batch-reduction magnitude: at B 65 536 a dense gradient
-                # element is a near-cancelling sum of 10^5 terms, whose fp32 rounding in the
-                # GPU's reduction order the three sampled orders need not span
-                assert_close_mag(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}", mag[i])
+                # + 1e-4 of the float64 batch-reduction magnitude (32 chunks): at B 65 536 a
+                # dense gradient element is a near-cancelling sum of 65 536 terms, formed by fp32
+                # GEMMs accumulating 8 192-deep K chunks in sequence (nn.wgrad) — Higham's bound
+                # for that is 8192·u·Σ|terms| ≈ 5e-4 of the TERM magnitude, which the chunked
+                # magnitude only bounds from below; the three sampled orders need not span it
+                assert_close_mag(p.grad, rg, [r[2][i] for r in r32], f"dense grad {i}",
+                                 mag[i] * 10.0)
                 m0, v0 = st0[i] if st0[i] is not None else (torch.zeros_like(p0),) * 2
                 want, _, _ = keras_adam_torch(p0, m0, v0, p.grad, c)
                 assert torch.equal(p.detach(), want), f"dense parameter {i}"
@@ -370,15 +373,18 @@ def test_cfg5_ml20m_model_step_vs_float64(ml20m):
     assert_close_f64(pos, p64, p32, "pos score", floor=1e-6)
     assert_close_f64(neg, n64, n32, "neg score", floor=1e-6)
     assert abs(loss.item() - l64) <= 1e-5 * abs(l64)
+    # the weight gradients sum over ~10^4 nodes of the 4096-pair batch: one fp32 restatement
+    # order undersamples the rounding spread of such sums, so their floor is 1e-5 of the
+    # tensor's largest element (1e-6 at the small graphs of tests/test_pinsage_gpu.py)
     s = model.sagenet
     pairs = [(s.fc_2.kernel, "k2"), (s.fc_2.bias, "b2"), (s.fc_1.kernel, "k1"), (s.fc_1.bias, "b1")]
     for li, c in enumerate(s.convolves):
         pairs += [(c.fc_1.kernel, f"c{li}k1"), (c.fc_1.bias, f"c{li}b1"),
                   (c.fc_2.kernel, f"c{li}k2"), (c.fc_2.bias, f"c{li}b2")]
     for prm, name in pairs:
-        assert_close_f64(prm.grad, P64[name].grad, P32[name].grad, name, floor=1e-6)
+        assert_close_f64(prm.grad, P64[name].grad, P32[name].grad, name, floor=1e-5)
     for t, name in zip(model.tables(), ("year", "genre", "id")):
         ids, rows = t.take_grad()
         dense = torch.zeros_like(t.weight).index_add(0, ids.reshape(-1).long(),
                                                      rows.reshape(-1, t.output_dim))
-        assert_close_f64(dense, P64[name].grad, P32[name].grad, f"table {name}", floor=1e-6)
+        assert_close_f64(dense, P64[name].grad, P32[name].grad, f"table {name}", floor=1e-5)

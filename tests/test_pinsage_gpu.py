@@ -695,14 +695,19 @@ def _pinsage_world2_static_worker(rank, world, port, q):
         dense = model.dense_parameters()
         x, y = dense[0], dense[1]
         x0, y0 = x.detach().clone(), y.detach().clone()
-        if rank == 1:
-            x.requires_grad_(False)
-        y.requires_grad_(False)
+        reduce = step._allreduce_and_apply_tables
+
+        def drop_grads():  # the dense layers write .grad themselves: drop them before the bucket
+            if rank == 1:
+                x.grad = None
+            y.grad = None
+            reduce()
+
+        step._allreduce_and_apply_tables = drop_grads
         h, p, n = item_pairs(g, B, 4, 0, pair_base=rank * B)
         step(*smp.sample_from_item_pairs(h, p, n))
         torch.cuda.synchronize()
-        x.requires_grad_(True)
-        y.requires_grad_(True)
+        assert y.grad is None and x.grad is not None
         assert torch.equal(y, y0), "a parameter without a gradient on every rank must not move"
         assert not torch.equal(x, x0)
         mine = _pinsage_params(model)

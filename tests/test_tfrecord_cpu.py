@@ -64,3 +64,17 @@ def test_index_rejects_file_cut_after_a_record_header(rng, extra):
     for verify in (True, False):
         with pytest.raises(L.RecsysError):
             index_records(np.frombuffer(cut, np.uint8), verify_crc=verify)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 257])
+def test_encode_records_fixed_equals_per_record(n):
+    """The column-wise batch encoder (one template record tiled, data bytes and payload CRCs
+    filled per column) writes the per-record encoder's bytes exactly, labels 0..127 and a
+    fallback for other label widths."""
+    from recommender_amd.data.tfrecord import encode_records, encode_records_fixed
+
+    r = np.random.default_rng(n)
+    ints = r.standard_normal((n, 13)).astype(np.float32)
+    cats = r.integers(0, 1 << 40, (n, 26))
+    for labs in (r.integers(0, 2, n), np.full(n, 127), np.full(n, 300)):
+        assert encode_records_fixed(ints, cats, labs) == encode_records(ints, cats, labs)

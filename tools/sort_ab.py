@@ -59,7 +59,7 @@ def main():
 
     def rocprim():
         rc = ref.ref_sort_pairs(kin.data_ptr(), kout.data_ptr(), vin.data_ptr(), vout.data_ptr(), n,
-                                bits, rws.data_ptr(), rws.numel(), C.c_void_p(st))
+                                bits, rws.data_ptr(), rws.numel(), st)
         assert rc == 0, rc
 
     out = {}
