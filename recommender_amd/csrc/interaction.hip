@@ -1369,6 +1369,16 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
     lab = *(gfloat*)(ta.label + bb);
   };
   if (active) {
+#ifdef RS_TRAIN_STAGGER
+    // A/B probe: the second half of the grid (the partner blocks on each CU) starts late
+    if (blockIdx.x >= gridDim.x / 2) {
+#pragma unroll
+      for (int z = 0; z < RS_TRAIN_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
+#ifdef RS_TRAIN_PRIO
+    if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     {
       const float* mine = row_of(first, raw_id(first));
       p0 = shfl_ptr(mine, r);
@@ -1411,9 +1421,13 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
         bf16x8 h0, m0, l0, h1, m1, l1;
         split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
         split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
+#ifndef RS_TRAIN_NO_SB
         __builtin_amdgcn_sched_barrier(0);
+#endif
         load_chunk(s);  // X(b+1), chunk s: in flight for a whole example
+#ifndef RS_TRAIN_NO_SB
         __builtin_amdgcn_sched_barrier(0);
+#endif
         c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
         c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
         c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);

@@ -98,7 +98,7 @@ class _UniqueRows:
 class ShardedSlabEmbedding(nn.Module):
     def __init__(self, cardinalities, dim: int, comm: Comm | None = None, device=None,
                  generator: torch.Generator | None = None, full_weight: torch.Tensor | None = None,
-                 capacity: int | None = None, capacity_factor: float = 1.5):
+                 capacity: int | None = None, capacity_factor: float = 1.25):
         super().__init__()
         self.comm = comm or Comm()
         W, r = self.comm.world, self.comm.rank
