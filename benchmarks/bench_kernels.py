@@ -409,11 +409,6 @@ def dlrm_path(iters, out):
     tws = torch.empty(L.lib().rs_dlrm_train_workspace_size(B), dtype=torch.uint8, device=DEV)
     yb = torch.empty(B, device=DEV)
 
-    def train_fwd():
-        L.call("rs_dlrm_train_step_fwd", L.ptr(table), V, D, L.ptr(ids), 1, S, L.ptr(so),
-               L.ptr(dense), L.ptr(xin), 13, L.ptr(lab), B, L.ptr(q), L.ptr(cc), 1e-7, 2,
-               L.ptr(yb), L.ptr(gemb), L.ptr(sums), L.ptr(tws), tws.numel(), L.ptr(err), st)
-
     gb = torch.empty(B, device=DEV)
 
     def train_unit():
@@ -445,14 +440,6 @@ def dlrm_path(iters, out):
     bwd()
     cfg = {"B": B, "S": S, "D": D, "rows": V, "unique": U}
     per_ex = S * (8 + 8 * D) + S * (8 + 4 * D) + (U / B) * 8 * D
-    tot = 0.0
-    for name, fn in (("rs_dlrm_train_step_fwd", train_fwd), ("rs_sort_ids", srt),
-                     ("rs_embedding_apply_scaled", apply_final)):
-        us = timed(fn, iters)
-        tot += us
-        report(name + " (alone)", cfg, us, kernel_bytes(name, B, S, D, 8, U), out)
-    report("embedding_path (production: fused train-step kernel, sort, apply; alone)",
-           dict(cfg, bytes_per_example=round(per_ex, 1)), tot, per_ex * B, out)
     # the chunked train kernel (unit rows + G, scaled apply)
     tot = 0.0
     for name, fn in (("rs_dlrm_train_step_fwd_unit", train_unit), ("rs_sort_ids", srt),

@@ -239,7 +239,7 @@ def main():
 
                 def step(_):
                     return seq()
-        watch = ["rs_dlrm_train_step_fwd_scaled", "rs_dlrm_train_step_fwd_unit", "rs_sort_ids", "rs_embedding_apply",
+        watch = ["rs_dlrm_train_step_fwd_unit", "rs_sort_ids", "rs_embedding_apply",
                  "rs_dlrm_dense_tail", "rs_keras_adam_dense_sweep"]
         cfg = {"workload": f"dlrm_criteo_26x{per}x{D}_b{B}", "batch": B, "rows": per * S,
                "slab_GB": round(per * S * D * 4 / 1e9, 1), "optimizer": args.optimizer,

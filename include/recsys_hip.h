@@ -856,41 +856,23 @@ int32_t rs_tfrecord_parse_criteo(const uint8_t* data, const int64_t* offsets,
 /* ---- the production DLRM training step's top half in one pass (D = 128, <= 27 slots, 13
  * dense inputs, sigmoid head, Keras BCE; ctr/model.py:45-57 + ctr/train.py:77-85) ------------
  * Gathers X = [emb(ids), dense], Z = X·Xᵀ, y = σ(Σ q·[Z_strict_upper, dense] + c) (q, c: the
- * composed top MLP, rs_chain3_vec_compose), the BCE loss against label (eps clip; reduction
- * 1 = sum, 2 = mean), G_b = y(1-y)·dL/dy, the table gradient rows G_b·(M + Mᵀ)·X_b (M = the
- * strict-upper pair weights of q) in position order into grad_emb [B*S, D], y [B], and the
+ * composed top MLP, rs_chain3_vec_compose), the BCE loss against label (eps clip, scaled by
+ * loss_scale), G_b = y(1-y)·dL/dy, the table gradient rows G_b·(M + Mᵀ)·X_b (M = the
+ * strict-upper pair weights of q, written unit-scaled: below) in position order, y [B], and the
  * deterministic batch sums (fixed per-wave / per-block / two-level fold order) into
  * sums [rs_dlrm_train_sums()] = A_top [512] (Σ_b row_b·G_b over the compact row, zero padded)
  * | s_top = Σ G | loss sum | A_bot [13][128] = Σ_b x_bᵀ·g_b | s_bot [128] = Σ_b g_b, where
  * g_b = relu'(dense_b) ⊙ G_b·((M + Mᵀ)·X_b + q_dense)[row S] is the bottom MLP's last-layer
  * gradient and x = xin [B, 13] its input. */
 size_t rs_dlrm_train_workspace_size(int64_t batch);
-int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D, const void* ids,
-                               int32_t id_dtype, int32_t n_slots, const int64_t* slot_offsets,
-                               const float* dense, const float* xin, int32_t n_in,
-                               const float* label, int64_t batch, const float* q, const float* c,
-                               float eps, int32_t reduction, float* y, float* grad_emb,
-                               float* sums, void* workspace, size_t ws_bytes, int32_t* err_flag,
-                               void* stream);
-/* The same with dL/dl_b given explicitly (`reduction` 2 is loss_scale = 1/batch, 1 is 1): a
- * data-parallel rank holding `batch` of a global batch of B examples passes 1/B, so G, the
- * gradient rows and every batch sum are those of the global mean loss and the ranks' sums
- * add up to the global ones. */
-int32_t rs_dlrm_train_step_fwd_scaled(const float* table, int64_t n_rows, int32_t D,
-                                      const void* ids, int32_t id_dtype, int32_t n_slots,
-                                      const int64_t* slot_offsets, const float* dense,
-                                      const float* xin, int32_t n_in, const float* label,
-                                      int64_t batch, const float* q, const float* c, float eps,
-                                      float loss_scale, float* y, float* grad_emb, float* sums,
-                                      void* workspace, size_t ws_bytes, int32_t* err_flag,
-                                      void* stream);
-/* The same step with the table gradient rows written UNIT-scaled: unit_rows[b, i] = U_b[i] (the
- * interaction backward's (M + Mᵀ)·X_b row) and g_rows[b] = G_b, so the gradient row of position
- * p is g_rows[p / n_slots] * unit_rows[p] — hand both to rs_embedding_apply_scaled (row_scale =
- * g_rows, scale_group = n_slots), which forms that product with the same fmul_rn as
- * rs_dlrm_train_step_fwd_scaled. y and sums as rs_dlrm_train_step_fwd_scaled. The kernel computes
+/* The table gradient rows are written UNIT-scaled: unit_rows[b, i] = U_b[i] (the interaction
+ * backward's (M + Mᵀ)·X_b row) and g_rows[b] = G_b, so the gradient row of position p is
+ * g_rows[p / n_slots] * unit_rows[p] — hand both to rs_embedding_apply_scaled (row_scale =
+ * g_rows, scale_group = n_slots), which forms that product with one fmul_rn. The kernel computes
  * the interaction chunk by chunk (U written before the head's G is known), which is why the rows
- * leave it unscaled. Replaces the same reference call as rs_dlrm_train_step_fwd. */
+ * leave it unscaled. loss_scale is dL/dl_b: 1/batch for the mean loss; a data-parallel rank
+ * holding `batch` of a global batch of B examples passes 1/B, so G, the rows and every batch sum
+ * are those of the global mean loss and the ranks' sums add up to the global ones. */
 int32_t rs_dlrm_train_step_fwd_unit(const float* table, int64_t n_rows, int32_t D,
                                     const void* ids, int32_t id_dtype, int32_t n_slots,
                                     const int64_t* slot_offsets, const float* dense,

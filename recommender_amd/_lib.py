@@ -151,11 +151,6 @@ _SIGS = {
     "rs_keras_adam_mark": (_i32, [_p, _i64, _p, _i64, _i32, _p]),
     "rs_dlrm_dense_tail_workspace_size": (_sz, [_i32, _i32, _i32]),
     "rs_dlrm_dense_tail": (_i32, [C.POINTER(DlrmTailArgs), _p, _sz, _p]),
-    "rs_dlrm_train_step_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p, _i64,
-                                      _p, _p, C.c_float, _i32, _p, _p, _p, _p, _sz, _p, _p]),
-    "rs_dlrm_train_step_fwd_scaled": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p,
-                                             _i64, _p, _p, C.c_float, C.c_float, _p, _p, _p, _p,
-                                             _sz, _p, _p]),
     "rs_dlrm_train_step_fwd_unit": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p,
                                            _i64, _p, _p, C.c_float, C.c_float, _p, _p, _p, _p, _p,
                                            _sz, _p, _p]),

@@ -899,18 +899,6 @@ __device__ __forceinline__ floatx4 mfma6(const bf16x8& ah, const bf16x8& am, con
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
 }
 
-// LDS rows of the train kernel (per wave): X(b) [32 rows][kTrLdx] fp32, rows >= F zero, then U
-// in place. Rows 8-15 and 24-31 keep their two 16-column halves swapped, so the U product's
-// transposed reads (lanes of groups g = 0 / 1 read rows j / 8 + j of one column) fall on
-// different banks; 4-column groups stay contiguous and 16-byte aligned.
-constexpr int kTrRows = 32;
-template <int D>
-constexpr int tr_ldx() { return D + 8; }
-template <int D>
-__device__ __forceinline__ float* tr_at(float* X, int row, int col) {
-  return X + row * tr_ldx<D>() + (col ^ (((row >> 3) & 1) << 4));
-}
-
 constexpr int kTrainAtop = 512;                       // A_top (compact row, zero padding)
 constexpr int kTrainNI = 13;                          // bottom-MLP inputs (Criteo dense)
 // the per-block partial row: A_top | s_top | loss | A_bot [13][D] | s_bot [D]
@@ -930,286 +918,6 @@ struct TrainArgs {
   float* part;         // [gridDim.x, kTrainM]
 };
 
-// D = 128 (the north star) or 64 (SURVEY cfg2): NT float4 per lane per row half, D / 32 split
-// k-steps of Z, D / 16 U tiles; a row is stored by DL = D / 4 lanes, RPI = 64 / DL rows per
-// store instruction; the bottom-MLP row gives each lane DPL = D / 64 of its dimensions.
-template <int D, bool ID64>
-__global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t batch, int F,
-                                                       TrainArgs ta, int epw) {
-  static_assert(D == 64 || D == 128, "train kernel laid out for D = 64 or 128");
-  constexpr int NT = D / 16, DL = D / 4, RPI = 64 / DL, DPL = D / 64;
-  constexpr int TM = train_m<D>();
-  // per wave: X(b) as fp32 rows [32][tr_ldx] (rows >= F zero), then U in place (tr_at)
-  __shared__ __attribute__((aligned(16))) float lds[4][kTrRows * tr_ldx<D>()];
-  // lane constants kept in LDS rather than VGPRs (the accumulators need the registers): the q
-  // weight of each lane's 12 Z entries (0 where the pair is not kept), and q over the row
-  __shared__ __attribute__((aligned(16))) float qlane[64][12];
-  __shared__ __attribute__((aligned(16))) float qsh[kTrainAtop];
-  static_assert(kTrRows * tr_ldx<D>() >= TM, "per-wave LDS region holds the wave's partial row");
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
-  const int64_t last = first + epw < batch ? first + epw : batch;
-  const bool active = first < batch;
-  const int r = lane & 15, g = lane >> 4;
-  const int cl = lane & (DL - 1), rg = lane / DL;  // row-store lane: column quad, row group
-  const int S = src.n_slots;
-  const int nzc = F * (F - 1) / 2;
-  float* X = lds[wave];
-  for (int e = threadIdx.x; e < kTrainAtop; e += 256) qsh[e] = e < nzc + D ? ta.q[e] : 0.f;
-  if (wave == 0) {
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int i0 = 4 * g + reg, j0 = r;            // c00: Z[i0][j0]
-      const int i1 = 4 * g + reg, j1 = 16 + r;       // c01
-      const int i2 = 16 + 4 * g + reg, j2 = 16 + r;  // c11
-      qlane[lane][reg] = (i0 < j0) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
-      qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
-      qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
-    }
-  }
-  // (M + Mᵀ) as the A operand of the U product on v_mfma_f32_16x16x32_bf16, split in three
-  // bf16 parts: lane (r, g) holds row 16 ib + r, k = 8g + j
-  bf16x8 sa[2][3];
-#pragma unroll
-  for (int ib = 0; ib < 2; ++ib) {
-    floatx4 v[2];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = 16 * ib + r, kk = 8 * g + j;
-      const bool in = m < F && kk < F && m != kk;
-      const float q = ta.q[in ? compact_index(m < kk ? m : kk, m < kk ? kk : m, F, 0) : 0];
-      v[j >> 2][j & 3] = in ? q : 0.f;
-    }
-    split3(v[0], v[1], sa[ib][0], sa[ib][1], sa[ib][2]);
-  }
-  __syncthreads();
-  const float cc = ta.c[0];
-  // accumulators (per lane; the loss and s_top are lane-uniform)
-  float az[12], ad[4], abot[DPL][kTrainNI], sbot[DPL];
-  float s_top = 0.f, loss = 0.f;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) az[k] = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) ad[k] = 0.f;
-#pragma unroll
-  for (int k = 0; k < DPL; ++k) {
-    sbot[k] = 0.f;
-#pragma unroll
-    for (int i = 0; i < kTrainNI; ++i) abot[k][i] = 0.f;
-  }
-  int64_t lo = 0, n_ok = src.n_rows;
-  if (lane < S && src.slot_offsets) {
-    lo = src.slot_offsets[lane];
-    n_ok = src.slot_offsets[lane + 1] - lo;
-  }
-  bool oob = false;
-  auto raw_id = [&](int64_t b) -> int64_t {
-    const int64_t bb = b < last ? b : first;
-    const int ln = lane < S ? lane : S - 1;
-    const int64_t v = ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + ln]
-                           : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + ln]);
-    return lane < S ? v : 0;
-  };
-  auto row_of = [&](int64_t b, int64_t id) -> const float* {
-    const bool live = b < last;
-    const bool id_ok = id >= 0 && id < n_ok;
-    if (lane < S && !id_ok && live) oob = true;
-    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
-    return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
-  };
-  // X(b) in the bf16 MFMA's A/B layout: lane (r, g) holds rows r (a0) and 16 + r (a1), columns
-  // 32s + 8g + 4e + c in a0[2s + e][c] (k-step s of v_mfma_f32_16x16x32_bf16, element 4e + c)
-  floatx4 a0[NT], a1[NT];
-  floatx4 dn4;
-  float xv, lab;
-  auto gather = [&](const float* mine, int64_t b) {
-    const float* p0 = shfl_ptr(mine, r);
-    const float* p1 = shfl_ptr(mine, 16 + r);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      a0[t] = *(gfloatx4*)(p0 + 32 * (t >> 1) + 8 * g + 4 * (t & 1));
-      a1[t] = *(gfloatx4*)(p1 + 32 * (t >> 1) + 8 * g + 4 * (t & 1));
-    }
-    const int64_t bb = b < last ? b : first;
-    dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * cl);
-    xv = *(gfloat*)(ta.xin + bb * kTrainNI + (lane < kTrainNI ? lane : 0));
-    lab = *(gfloat*)(ta.label + bb);
-  };
-  if (active) {
-    gather(row_of(first, raw_id(first)), first);
-    int64_t id_next = raw_id(first + 1);
-    for (int64_t b = first; b < last; ++b) {
-      int lanev;
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
-      const int r = lanev & 15, g = (lanev >> 4) & 3;
-      const int cl = lanev & (DL - 1), rg = (lanev / DL) & (RPI - 1);
-      const float* nxt = row_of(b + 1, id_next);
-      id_next = raw_id(b + 2);
-      // (1) Z = X·Xᵀ (three 16x16 blocks) on v_mfma_f32_16x16x32_bf16: each fp32 value is
-      // split x = h + m + l into three bf16 (round to nearest, the residuals exact), and the
-      // six products h·h, h·m, m·h, m·m, h·l, l·h are accumulated in fp32 (smallest first) —
-      // the dropped m·l, l·m, l·l terms are below 2^-23 of |x||y|, so each dot product keeps
-      // fp32 accuracy at 6 × 16 instead of 8 × 32 matrix cycles per 32-wide k-step
-      floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-#pragma unroll
-      for (int s = 0; s < NT / 2; ++s) {
-        bf16x8 h0, m0, l0, h1, m1, l1;
-        split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
-        split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
-        c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
-        c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
-        c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);
-      }
-      // (2) X(b) → LDS, all 32 rows (rows >= F are the zero row's zeros: the U product's
-      // k-padding); tr_at swizzles the 16-column halves of rows 8-15 / 24-31
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int col = 32 * (t >> 1) + 8 * g + 4 * (t & 1);
-        *reinterpret_cast<floatx4*>(tr_at<D>(X, r, col)) = a0[t];
-        *reinterpret_cast<floatx4*>(tr_at<D>(X, 16 + r, col)) = a1[t];
-      }
-      const floatx4 dn = dn4;
-      float xb[kTrainNI];  // wave-uniform: scalar registers
-#pragma unroll
-      for (int i = 0; i < kTrainNI; ++i)
-        xb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
-      const float lb = lab;
-      // (3) X(b+1) in flight behind the rest of this example
-      __builtin_amdgcn_sched_barrier(0);
-      gather(nxt, b + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      // (4) head, loss, G
-      float zr[12];
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        zr[reg] = c00[reg];
-        zr[4 + reg] = c01[reg];
-        zr[8 + reg] = c11[reg];
-      }
-      float hacc = 0.f;
-      {
-        const floatx4* ql = reinterpret_cast<const floatx4*>(&qlane[lanev & 63][0]);
-#pragma unroll
-        for (int q4 = 0; q4 < 3; ++q4) {
-          const floatx4 qv = ql[q4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) hacc += zr[4 * q4 + k] * qv[k];
-        }
-        const floatx4 qd = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
-        if (rg == 0) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) hacc += dn[k] * qd[k];
-        }
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
-      const float p = 1.f / (1.f + expf(-(hacc + cc)));
-      if (lanev == 0) ta.y[b] = p;
-      {  // keras binary_crossentropy on probabilities (loss.hip bce_term / bce_bwd_kernel)
-        const float pc = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
-        loss += -(lb * logf(pc + ta.eps) + (1.f - lb) * logf((1.f - pc) + ta.eps));
-      }
-      const bool inside = p >= ta.eps && p <= 1.f - ta.eps;
-      const float pcg = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
-      const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
-      const float dp = inside ? ta.gscale * dbce : 0.f;
-      const float G = dp * (p * (1.f - p));
-      s_top += G;
-#pragma unroll
-      for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ad[k] += dn[k] * G;
-      // (5) U = (M + Mᵀ)·X per 16-column tile on the split MFMA: the B operand (rows 8g + j
-      // of column r) read transposed from the fp32 rows and split like X; the tile is written
-      // back over itself (one wave's LDS operations run in issue order)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        floatx4 xv[2];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) xv[jj >> 2][jj & 3] = *tr_at<D>(X, 8 * g + jj, 16 * t + r);
-        bf16x8 bh, bm, bl;
-        split3(xv[0], xv[1], bh, bm, bl);
-        floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-        d0 = mfma6(sa[0][0], sa[0][1], sa[0][2], bh, bm, bl, d0);
-        d1 = mfma6(sa[1][0], sa[1][1], sa[1][2], bh, bm, bl, d1);
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int i0 = 4 * g + reg, i1 = 16 + 4 * g + reg;
-          *tr_at<D>(X, i0, 16 * t + r) = d0[reg];
-          *tr_at<D>(X, i1, 16 * t + r) = d1[reg];  // rows 28-31: never read
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      // (6) G·U rows: DL lanes per row, RPI rows per store (rows past S are skipped)
-      float* de = ta.grad_emb + b * S * (int64_t)D;
-#pragma unroll
-      for (int s2 = 0; s2 < (kDxRows + RPI - 1) / RPI; ++s2) {
-        const int i = RPI * s2 + rg;
-        if (i < S) {
-          floatx4 v = *reinterpret_cast<const floatx4*>(tr_at<D>(X, i, 4 * cl));
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = __fmul_rn(G, v[c]);
-          // non-temporal: the 872 MB of rows stream past L2 instead of evicting the Zipf-hot
-          // table rows the gather re-reads (the apply reads them back from HBM either way)
-          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 4 * cl));
-        }
-      }
-      {  // (7) the bottom-MLP row: this lane's DPL dims d = 4 cl + DPL rg + k get G·(U + q_d)
-         // through the bottom chain's relu (h_d > 0); A_bot += x ⊗ g, s_bot += g
-        const floatx4 v = *reinterpret_cast<const floatx4*>(tr_at<D>(X, S, 4 * cl));
-        const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
-#pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-          const int c = DPL * rg + k;
-          const float gd = __fmul_rn(G, v[c] + qdn[c]);
-          const float gb = dn[c] > 0.f ? gd : 0.f;
-          sbot[k] += gb;
-#pragma unroll
-          for (int ii = 0; ii < kTrainNI; ++ii) abot[k][ii] += xb[ii] * gb;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  // the wave's partial row → its LDS region, then the block folds its four waves in order
-  __syncthreads();
-  for (int e = lane; e < TM; e += 64) X[e] = 0.f;
-  __builtin_amdgcn_wave_barrier();
-  if (active) {
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int i0 = 4 * g + reg, j0 = r, i1 = 4 * g + reg, j1 = 16 + r, i2 = 16 + 4 * g + reg, j2 = 16 + r;
-      if (i0 < j0) X[compact_index(i0, j0, F, 0)] = az[reg];
-      if (j1 < F) X[compact_index(i1, j1, F, 0)] = az[4 + reg];
-      if (i2 < j2 && j2 < F) X[compact_index(i2, j2, F, 0)] = az[8 + reg];
-    }
-    if (rg == 0) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) X[nzc + 4 * cl + k] = ad[k];
-    }
-    if (lane == 0) {
-      X[kTrainAtop] = s_top;
-      X[kTrainAtop + 1] = loss;
-    }
-#pragma unroll
-    for (int k = 0; k < DPL; ++k) {
-      const int d = 4 * cl + DPL * rg + k;
-#pragma unroll
-      for (int ii = 0; ii < kTrainNI; ++ii) X[kTrainAtop + 2 + ii * D + d] = abot[k][ii];
-      X[kTrainAtop + 2 + kTrainNI * D + d] = sbot[k];
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < TM; e += 256) {
-    float v = lds[0][e];
-    v += lds[1][e];
-    v += lds[2][e];
-    v += lds[3][e];
-    ta.part[(int64_t)blockIdx.x * TM + e] = v;
-  }
-  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
-}
-
 // ---------------------------------------------------------------------------------------
 // The train step with the interaction computed chunk by chunk (round 3): per 32-column chunk s
 // of X(b) (rows r / 16 + r of the bf16 MFMA operand layout, already in registers),
@@ -1226,16 +934,17 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_pipe(GatherSrc src, int64_t
 // U is written UNSCALED (the head's G needs all of Z, known only after the last chunk) and G[b]
 // goes to g_rows: the apply multiplies each gradient row by its example's G
 // (rs_embedding_apply_scaled, row_scale = g_rows, scale_group = n_slots) with the same fmul_rn,
-// so the table update is the one dlrm_train_pipe's G·U rows give. Against dlrm_train_pipe: no
-// second split of X for U (≈0.3 k VALU per example), no fp32 X / U round trip through LDS, 6 KB
+// so the table update is the one the G·U rows would give. Against round 3's first form (one
+// kernel writing G·U rows, X staged in LDS as fp32 rows for U's transposed operand): no second
+// split of X for U (≈0.3 k VALU per example), no fp32 X / U round trip through LDS, 6 KB
 // instead of 17 KB of LDS per wave.
 // ---------------------------------------------------------------------------------------
 typedef short shortx4 __attribute__((ext_vector_type(4)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
 
-// the Uᵀ product: c + Xᵀ·S from the split operands, the six products in dlrm_train_pipe's U
-// order (X as A, S as B: m·m, l·h, h·l, m·h, h·m, h·h)
+// the Uᵀ product: c + Xᵀ·S from the split operands, the six products smallest first
+// (X as A, S as B: m·m, l·h, h·l, m·h, h·m, h·h)
 __device__ __forceinline__ floatx4 mfma6_xs(const bf16x8& xh, const bf16x8& xm, const bf16x8& xl,
                                             const bf16x8& sh, const bf16x8& sm, const bf16x8& sl,
                                             floatx4 c) {
@@ -1301,7 +1010,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
     }
   }
   // S = M + Mᵀ as the B operand of Uᵀ = Xᵀ·S: lane (r, g) holds S[8g + j][16 ib + r], which by
-  // symmetry is dlrm_train_pipe's A operand S[16 ib + r][8g + j]
+  // symmetry is S[16 ib + r][8g + j]
   if (wave == 1) {
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
@@ -1476,7 +1185,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
         }
         __builtin_amdgcn_wave_barrier();  // the next chunk's image / staging writes follow
       }
-      // head, loss, G (dlrm_train_pipe (4))
+      // head, loss, G
       const int cl = lanev & (DL - 1), rg = (lanev / DL) & (RPI - 1);
       float zr[12];
 #pragma unroll
@@ -1521,7 +1230,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
 #pragma unroll
       for (int k = 0; k < 4; ++k) ad[k] += dn[k] * G;
-      {  // the bottom-MLP row (dlrm_train_pipe (7)) from U's row S
+      {  // the bottom-MLP row from U's row S
         const floatx4 v = *reinterpret_cast<const floatx4*>(ubot + 4 * cl);
         const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
 #pragma unroll
@@ -1993,29 +1702,6 @@ extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
   return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
 }
 
-extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
-    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
-    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
-    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
-    float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
-    int32_t* err_flag, void* stream);
-
-extern "C" int32_t rs_dlrm_train_step_fwd(const float* table, int64_t n_rows, int32_t D,
-                                          const void* ids, int32_t id_dtype, int32_t n_slots,
-                                          const int64_t* slot_offsets, const float* dense,
-                                          const float* xin, int32_t n_in, const float* label,
-                                          int64_t batch, const float* q, const float* c,
-                                          float eps, int32_t reduction, float* y,
-                                          float* grad_emb, float* sums, void* workspace,
-                                          size_t ws_bytes, int32_t* err_flag, void* stream) {
-  RS_CHECK_ARG(reduction == 1 || reduction == 2, "reduction must be 1 (sum) or 2 (mean)");
-  RS_CHECK_ARG(batch >= 1, "rs_dlrm_train_step_fwd: empty batch");
-  return rs_dlrm_train_step_fwd_scaled(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets,
-                                       dense, xin, n_in, label, batch, q, c, eps,
-                                       reduction == 2 ? 1.f / (float)batch : 1.f, y, grad_emb,
-                                       sums, workspace, ws_bytes, err_flag, stream);
-}
-
 static int32_t train_step_launch(
     const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
     int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
@@ -2025,7 +1711,7 @@ static int32_t train_step_launch(
   const int F = n_slots + 1;
   RS_CHECK_ARG((D == 128 || D == 64) && n_slots >= 1 && F <= kDxRows && n_in == kTrainNI &&
                    batch >= 1,
-               "rs_dlrm_train_step_fwd: needs D = 128 or 64, at most %d slots, %d dense inputs",
+               "rs_dlrm_train_step_fwd_unit: needs D = 128 or 64, at most %d slots, %d dense inputs",
                kDxRows - 1, kTrainNI);
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
   RS_CHECK_ARG(loss_scale > 0.f, "loss_scale must be positive");
@@ -2044,40 +1730,18 @@ static int32_t train_step_launch(
     // 458 -> 448 us alone, step 0.878 -> 0.848 ms; four rounds 0.912)
     const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch, 1);
     blocks = ceil_div(batch, 4 * (int64_t)epw);
-    if constexpr (std::is_same_v<decltype(kern), decltype(&dlrm_train_pipe<128, true>)>)
-      kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, epw);
-    else
-      kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw);
+    kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw);
   };
-  if (g_rows) {  // unit rows U + G[b] (dlrm_train_chunk)
-    if (D == 128) {
-      if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<128, true>);
-      else go(dlrm_train_chunk<128, false>);
-    } else {
-      if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<64, true>);
-      else go(dlrm_train_chunk<64, false>);
-    }
-  } else if (D == 128) {
-    if (id_dtype == RS_ID_I64) go(dlrm_train_pipe<128, true>);
-    else go(dlrm_train_pipe<128, false>);
+  if (D == 128) {
+    if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<128, true>);
+    else go(dlrm_train_chunk<128, false>);
   } else {
-    if (id_dtype == RS_ID_I64) go(dlrm_train_pipe<64, true>);
-    else go(dlrm_train_pipe<64, false>);
+    if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<64, true>);
+    else go(dlrm_train_chunk<64, false>);
   }
   RS_CHECK_LAUNCH();
   const int tm = D == 128 ? train_m<128>() : train_m<64>();
   return fold_two_level(part, (int)blocks, tm, part + (size_t)blocks * tm, sums, st);
-}
-
-extern "C" int32_t rs_dlrm_train_step_fwd_scaled(
-    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
-    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
-    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
-    float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
-    int32_t* err_flag, void* stream) {
-  return train_step_launch(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets, dense, xin,
-                           n_in, label, batch, q, c, eps, loss_scale, y, grad_emb, sums,
-                           workspace, ws_bytes, err_flag, stream, nullptr);
 }
 
 extern "C" int32_t rs_dlrm_train_step_fwd_unit(

@@ -332,20 +332,17 @@ def binary_crossentropy(y_true, y_pred, reduction: str = "mean", epsilon: float 
     return _BCE.apply(y_pred, y_true, reduction, epsilon)
 
 
-TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd's sums layout (include/recsys_hip.h)
-# the chunked train kernel (rs_dlrm_train_step_fwd_unit: unit rows + G, the apply scales them);
-# RS_TRAIN_UNIT=0 selects dlrm_train_pipe's G·U rows
-_TRAIN_UNIT = os.environ.get("RS_TRAIN_UNIT", "1") != "0"
-# the train kernel waiting for the presort's completion (below): right for dlrm_train_pipe, off
-# for the chunked kernel (interleaved A/B, 3 x 100 steps: 0.695-0.699 vs 0.700-0.704 ms/step,
-# p90 0.698-0.700 vs 0.704-0.707); RS_TRAIN_WAITS_SORT=1 restores the wait
-_TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "0" if _TRAIN_UNIT else "1") != "0"
+TRAIN_SUMS_ATOP = 512  # rs_dlrm_train_step_fwd_unit's sums layout (include/recsys_hip.h)
+# the train kernel waiting for the presort's completion (below): off for the chunked kernel
+# (interleaved A/B, 3 x 100 steps: 0.695-0.699 vs 0.700-0.704 ms/step, p90 0.698-0.700 vs
+# 0.704-0.707); RS_TRAIN_WAITS_SORT=1 restores the wait
+_TRAIN_WAITS_SORT = os.environ.get("RS_TRAIN_WAITS_SORT", "0") != "0"
 
 
 def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction="mean",
                              epsilon=1e-7, sgd_lr=None, comm=None):
     """The production DLRM train step's forward + loss + backward reductions in one kernel
-    (rs_dlrm_train_step_fwd): the reference's DLRM.call (ctr/model.py:45-57) under the mean
+    (rs_dlrm_train_step_fwd_unit): the reference's DLRM.call (ctr/model.py:45-57) under the mean
     Keras BCE (ctr/train.py:85) with the SGD path's gradients (ctr/train.py:77-79).
 
     Runs: the side-stream radix sort of the ids; the bottom MLP as its composed affine map
@@ -417,18 +414,11 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     ws = _train_ws(B, dev)
     n_global = B * world
     scale = 1.0 / n_global if reduction == "mean" else 1.0
-    g_rows = None
-    if _TRAIN_UNIT:
-        g_rows = torch.empty(B, device=dev, dtype=torch.float32)
-        L.call("rs_dlrm_train_step_fwd_unit", L.ptr(w), n_rows, D, L.ptr(kid),
-               L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
-               L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(g_rows),
-               L.ptr(sums), L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
-    else:
-        L.call("rs_dlrm_train_step_fwd_scaled", L.ptr(w), n_rows, D, L.ptr(kid),
-               L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
-               L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(sums),
-               L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
+    g_rows = torch.empty(B, device=dev, dtype=torch.float32)
+    L.call("rs_dlrm_train_step_fwd_unit", L.ptr(w), n_rows, D, L.ptr(kid),
+           L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
+           L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad), L.ptr(g_rows),
+           L.ptr(sums), L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
     if not sharded and emb._prefetch_queue:
         emb.flush_prefetch()  # a later batch's sort, beside this step's update and dense tail
     if world > 1:

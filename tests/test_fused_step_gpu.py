@@ -1,5 +1,5 @@
 """The one-kernel production DLRM step (functional.dlrm_fused_train_forward /
-rs_dlrm_train_step_fwd: forward, mean BCE, G, table gradient rows and the MLP chains' batch
+rs_dlrm_train_step_fwd_unit: forward, mean BCE, G, table gradient rows and the MLP chains' batch
 reductions in one pass) against the autograd path over the same kernels (TrainStep
 fused_step=False), and against the CPU oracle on a small slab (oracle/check_dlrm.py; the
 north-star size is tests/test_northstar_gpu.py)."""

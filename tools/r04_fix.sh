@@ -1,6 +1,6 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest "tests/test_fullsize_gpu.py::test_cfg4_full_size_keras_adam_steps_vs_oracle" "tests/test_fullsize_gpu.py::test_cfg5_ml20m_model_step_vs_float64" "tests/test_pinsage_gpu.py::test_world2_pinsage_static_step_and_missing_gradients" -v --timeout 500 --timeout-method thread > gpurun_out/r04_fix.log 2>&1
+timeout -k 10 600 python -u -m pytest "tests/test_fullsize_gpu.py::test_cfg4_full_size_keras_adam_steps_vs_oracle" "tests/test_fullsize_gpu.py::test_cfg5_ml20m_model_step_vs_float64" "tests/test_pinsage_gpu.py::test_world2_pinsage_static_step_and_missing_gradients" tests/test_train_unit_gpu.py -v --timeout 500 --timeout-method thread > gpurun_out/r04_fix.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/r04_fix.log | tail -20
 timeout -k 10 120 python tools/sort_ab.py > gpurun_out/sort_ab.log 2>&1; tail -4 gpurun_out/sort_ab.log
