@@ -916,6 +916,7 @@ struct TrainArgs {
   float* y;            // [B] prediction
   float* grad_emb;     // [B * S, D] table gradient rows
   float* part;         // [gridDim.x, kTrainM]
+  float* sink;         // 1 KB that stores of padding rows land in (never read)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1074,8 +1075,10 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
     const int cl = lane & (DL - 1);
     const int64_t bb = b < last ? b : first;
     dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * cl);
+#ifndef RS_TRAIN_SCALAR_SIDE
     xv = *(gfloat*)(ta.xin + bb * kTrainNI + (lane < kTrainNI ? lane : 0));
     lab = *(gfloat*)(ta.label + bb);
+#endif
   };
   if (active) {
 #ifdef RS_TRAIN_STAGGER
@@ -1110,10 +1113,22 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       id_next = raw_id(b + 2);
       const floatx4 dn = dn4;
       float xb[kTrainNI];
+#ifdef RS_TRAIN_SCALAR_SIDE
+      // A/B probe: x_b (13 inputs) and label_b are wave-uniform: scalar loads (counted by
+      // lgkmcnt), so reading them waits on nothing in the vector memory queue (the vector load
+      // + readlane form waited for the previous example's row stores, vmcnt(2) in the ISA)
+      typedef __attribute__((address_space(4))) const float cfloat;
+      const int bq = __builtin_amdgcn_readfirstlane((int)b);
+      const cfloat* xr = (const cfloat*)(ta.xin + (int64_t)bq * kTrainNI);
+#pragma unroll
+      for (int i = 0; i < kTrainNI; ++i) xb[i] = xr[i];
+      const float lb = ((const cfloat*)ta.label)[bq];
+#else
 #pragma unroll
       for (int i = 0; i < kTrainNI; ++i)
         xb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
       const float lb = lab;
+#endif
       load_side(b + 1);
       float* de = ta.grad_emb + b * S * (int64_t)D;
       floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
@@ -1122,11 +1137,13 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       const int q = (lanev >> 2) & 3, p4 = lanev & 3;
 #pragma unroll
       for (int s = 0; s < NC; ++s) {
+#ifndef RS_TRAIN_SA_LATE
         bf16x8 sa[2][3];
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) sa[ib][pt] = sash[ib][pt][lanev & 63];
+#endif
         bf16x8 h0, m0, l0, h1, m1, l1;
         split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
         split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
@@ -1163,6 +1180,15 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
             xp[pt] = __builtin_bit_cast(bf16x8, v8);
           }
           floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#ifdef RS_TRAIN_SA_LATE
+          // A/B probe: S's split parts read from LDS right before their products (24 fewer
+          // VGPRs live across the split and the Z products)
+          bf16x8 sa[2][3];
+#pragma unroll
+          for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+            for (int pt = 0; pt < 3; ++pt) sa[ib][pt] = sash[ib][pt][lanev & 63];
+#endif
           d0 = mfma6_xs(xp[0], xp[1], xp[2], sa[0][0], sa[0][1], sa[0][2], d0);
           d1 = mfma6_xs(xp[0], xp[1], xp[2], sa[1][0], sa[1][1], sa[1][2], d1);
           // lane (r, g): U[16 ib + r][32 s + 16 tt + 4g ..+3] → the staging rows (and U's row S,
@@ -1180,8 +1206,16 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
         for (int pp = 0; pp < 4; ++pp) {
           const int i = 8 * pp + (lanev >> 3), c8 = lanev & 7;
           const floatx4 v = *reinterpret_cast<const floatx4*>(stg + i * kChStageLd + 4 * c8);
+#ifdef RS_TRAIN_UNCOND_ST
+          // every store instruction issues (rows >= S go to the sink): no branch around a store,
+          // so the compiler's in-order vmcnt count stays exact across the loop and the next
+          // example's loads are not made to wait for this example's row stores
+          float* dst = i < S ? de + i * D + 32 * s + 4 * c8 : ta.sink + 4 * lanev;
+          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(dst));
+#else
           if (i < S)
             __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 32 * s + 4 * c8));
+#endif
         }
         __builtin_amdgcn_wave_barrier();  // the next chunk's image / staging writes follow
       }
@@ -1221,10 +1255,15 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
       const float dp = inside ? ta.gscale * dbce : 0.f;
       const float G = dp * (p * (1.f - p));
+#ifdef RS_TRAIN_UNCOND_ST
+      ta.y[b] = p;  // every lane holds the same p and G (the shuffle reduction above)
+      g_rows[b] = G;
+#else
       if (lanev == 0) {
         ta.y[b] = p;
         g_rows[b] = G;
       }
+#endif
       s_top += G;
 #pragma unroll
       for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
@@ -1699,7 +1738,8 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
 
 extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
   // one partial row per block (at most ceil(batch / 4) blocks) + the fold's 32 segment rows
-  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
+  // + the 1 KB store sink of the padding rows (aligned)
+  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 1024 + 256;
 }
 
 static int32_t train_step_launch(
@@ -1722,7 +1762,9 @@ static int32_t train_step_launch(
   hipStream_t st = as_stream(stream);
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
   float* part = static_cast<float*>(workspace);
-  TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part};
+  float* sink = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                         (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float));
+  TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part, sink};
   int64_t blocks = 0;
   auto go = [&](auto kern) {
     // ONE round of resident blocks: the side-stream sort then only fills the resources the
