@@ -916,7 +916,6 @@ struct TrainArgs {
   float* y;            // [B] prediction
   float* grad_emb;     // [B * S, D] table gradient rows
   float* part;         // [gridDim.x, kTrainM]
-  float* sink;         // 1 KB that stores of padding rows land in (never read)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1005,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       const int i0 = 4 * g + reg, j0 = r;
       const int i1 = 4 * g + reg, j1 = 16 + r;
       const int i2 = 16 + 4 * g + reg, j2 = 16 + r;
-      qlane[lane][reg] = (i0 < j0) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
+      qlane[lane][reg] = (i0 < j0 && j0 < F) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
       qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
       qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
     }
@@ -1062,7 +1061,6 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
   };
   floatx4 a0[NT], a1[NT];
   floatx4 dn4;
-  float xv, lab;
   const float* p0 = nullptr;
   const float* p1 = nullptr;
   auto load_chunk = [&](int s) {
@@ -1075,22 +1073,8 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
     const int cl = lane & (DL - 1);
     const int64_t bb = b < last ? b : first;
     dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * cl);
-#ifndef RS_TRAIN_SCALAR_SIDE
-    xv = *(gfloat*)(ta.xin + bb * kTrainNI + (lane < kTrainNI ? lane : 0));
-    lab = *(gfloat*)(ta.label + bb);
-#endif
   };
   if (active) {
-#ifdef RS_TRAIN_STAGGER
-    // A/B probe: the second half of the grid (the partner blocks on each CU) starts late
-    if (blockIdx.x >= gridDim.x / 2) {
-#pragma unroll
-      for (int z = 0; z < RS_TRAIN_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
-#ifdef RS_TRAIN_PRIO
-    if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     {
       const float* mine = row_of(first, raw_id(first));
       p0 = shfl_ptr(mine, r);
@@ -1113,22 +1097,15 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       id_next = raw_id(b + 2);
       const floatx4 dn = dn4;
       float xb[kTrainNI];
-#ifdef RS_TRAIN_SCALAR_SIDE
-      // A/B probe: x_b (13 inputs) and label_b are wave-uniform: scalar loads (counted by
-      // lgkmcnt), so reading them waits on nothing in the vector memory queue (the vector load
-      // + readlane form waited for the previous example's row stores, vmcnt(2) in the ISA)
+      // x_b (13 inputs) and label_b are wave-uniform: scalar loads, counted by lgkmcnt, so
+      // reading them waits on nothing in the vector memory queue (a vector load + readlane
+      // waited for the previous example's row stores: vmcnt(2) in the ISA; -3 % measured)
       typedef __attribute__((address_space(4))) const float cfloat;
       const int bq = __builtin_amdgcn_readfirstlane((int)b);
       const cfloat* xr = (const cfloat*)(ta.xin + (int64_t)bq * kTrainNI);
 #pragma unroll
       for (int i = 0; i < kTrainNI; ++i) xb[i] = xr[i];
       const float lb = ((const cfloat*)ta.label)[bq];
-#else
-#pragma unroll
-      for (int i = 0; i < kTrainNI; ++i)
-        xb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
-      const float lb = lab;
-#endif
       load_side(b + 1);
       float* de = ta.grad_emb + b * S * (int64_t)D;
       floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
@@ -1137,23 +1114,17 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       const int q = (lanev >> 2) & 3, p4 = lanev & 3;
 #pragma unroll
       for (int s = 0; s < NC; ++s) {
-#ifndef RS_TRAIN_SA_LATE
         bf16x8 sa[2][3];
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) sa[ib][pt] = sash[ib][pt][lanev & 63];
-#endif
         bf16x8 h0, m0, l0, h1, m1, l1;
         split3(a0[2 * s], a0[2 * s + 1], h0, m0, l0);
         split3(a1[2 * s], a1[2 * s + 1], h1, m1, l1);
-#ifndef RS_TRAIN_NO_SB
         __builtin_amdgcn_sched_barrier(0);
-#endif
         load_chunk(s);  // X(b+1), chunk s: in flight for a whole example
-#ifndef RS_TRAIN_NO_SB
         __builtin_amdgcn_sched_barrier(0);
-#endif
         c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
         c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
         c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);
@@ -1180,15 +1151,6 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
             xp[pt] = __builtin_bit_cast(bf16x8, v8);
           }
           floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
-#ifdef RS_TRAIN_SA_LATE
-          // A/B probe: S's split parts read from LDS right before their products (24 fewer
-          // VGPRs live across the split and the Z products)
-          bf16x8 sa[2][3];
-#pragma unroll
-          for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-            for (int pt = 0; pt < 3; ++pt) sa[ib][pt] = sash[ib][pt][lanev & 63];
-#endif
           d0 = mfma6_xs(xp[0], xp[1], xp[2], sa[0][0], sa[0][1], sa[0][2], d0);
           d1 = mfma6_xs(xp[0], xp[1], xp[2], sa[1][0], sa[1][1], sa[1][2], d1);
           // lane (r, g): U[16 ib + r][32 s + 16 tt + 4g ..+3] → the staging rows (and U's row S,
@@ -1206,16 +1168,8 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
         for (int pp = 0; pp < 4; ++pp) {
           const int i = 8 * pp + (lanev >> 3), c8 = lanev & 7;
           const floatx4 v = *reinterpret_cast<const floatx4*>(stg + i * kChStageLd + 4 * c8);
-#ifdef RS_TRAIN_UNCOND_ST
-          // every store instruction issues (rows >= S go to the sink): no branch around a store,
-          // so the compiler's in-order vmcnt count stays exact across the loop and the next
-          // example's loads are not made to wait for this example's row stores
-          float* dst = i < S ? de + i * D + 32 * s + 4 * c8 : ta.sink + 4 * lanev;
-          __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(dst));
-#else
           if (i < S)
             __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 32 * s + 4 * c8));
-#endif
         }
         __builtin_amdgcn_wave_barrier();  // the next chunk's image / staging writes follow
       }
@@ -1255,15 +1209,10 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
       const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
       const float dp = inside ? ta.gscale * dbce : 0.f;
       const float G = dp * (p * (1.f - p));
-#ifdef RS_TRAIN_UNCOND_ST
-      ta.y[b] = p;  // every lane holds the same p and G (the shuffle reduction above)
-      g_rows[b] = G;
-#else
       if (lanev == 0) {
         ta.y[b] = p;
         g_rows[b] = G;
       }
-#endif
       s_top += G;
 #pragma unroll
       for (int k = 0; k < 12; ++k) az[k] += zr[k] * G;
@@ -1295,7 +1244,7 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int i0 = 4 * g + reg, j0 = r, i1 = 4 * g + reg, j1 = 16 + r, i2 = 16 + 4 * g + reg, j2 = 16 + r;
-      if (i0 < j0) X[compact_index(i0, j0, F, 0)] = az[reg];
+      if (i0 < j0 && j0 < F) X[compact_index(i0, j0, F, 0)] = az[reg];
       if (j1 < F) X[compact_index(i1, j1, F, 0)] = az[4 + reg];
       if (i2 < j2 && j2 < F) X[compact_index(i2, j2, F, 0)] = az[8 + reg];
     }
@@ -1738,8 +1687,7 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
 
 extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
   // one partial row per block (at most ceil(batch / 4) blocks) + the fold's 32 segment rows
-  // + the 1 KB store sink of the padding rows (aligned)
-  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 1024 + 256;
+  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float);
 }
 
 static int32_t train_step_launch(
@@ -1762,9 +1710,7 @@ static int32_t train_step_launch(
   hipStream_t st = as_stream(stream);
   GatherSrc src{table, n_rows, ids, id_dtype, n_slots, slot_offsets, dense, err_flag};
   float* part = static_cast<float*>(workspace);
-  float* sink = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                         (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float));
-  TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part, sink};
+  TrainArgs ta{q, c, label, xin, eps, loss_scale, y, grad_emb, part};
   int64_t blocks = 0;
   auto go = [&](auto kern) {
     // ONE round of resident blocks: the side-stream sort then only fills the resources the
