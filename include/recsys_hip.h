@@ -79,6 +79,13 @@ int32_t rs_stream_copy(const void* src, void* dst, size_t bytes, void* stream);
 int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t dim, const void* ids,
                          int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
                          int32_t n_slots, float* out, int32_t* err_flag, void* stream);
+/* rs_embedding_fwd with the rows written at a row stride out_ld >= dim (floats): a column block
+ * of a wider row-major output. DIEN's flat embedding item ‖ category (dien/model.py:14-19,
+ * tf.concat of the two lookups) is two of these into one [n, 36] tensor, no concat pass. */
+int32_t rs_embedding_fwd_strided(const float* table, int64_t n_rows, int32_t dim, const void* ids,
+                                 int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
+                                 int32_t n_slots, float* out, int64_t out_ld, int32_t* err_flag,
+                                 void* stream);
 
 /* ------------------------------------------------------------------------------------
  * a-2 (part 1) Duplicate-index coalescing: the IndexedSlices gradient's `unique` +
@@ -405,6 +412,9 @@ size_t rs_dien_aux_workspace_size(int64_t B, int32_t L, int32_t H, int32_t E);
  *        rows; other rows of y untouched. K <= 64, N <= 192.
  *      rs_masked_dx: dx[r, :K] = d[r, :N]·Wᵀ (W [K,N]) for the listed rows (idx / count of
  *        rs_valid_rows over the same mask), 0 for the rows with mask == 0 (all R rows written).
+ *      rs_masked_dx_acc: the same with an addend (add may be NULL): dx = add + d·Wᵀ on the listed
+ *        rows, dx = add on the masked ones — a second consumer's gradient of the same input
+ *        (the aux loss's of the positive history, dien/layers.py:89-108) summed in the kernel.
  *      rs_masked_wgrad: C [K,N] = Σ_listed A_rᵀ·D[r, :N] and sums [N] = Σ_listed D[r] (may be
  *        NULL); A_r = A row r, or with shift_L > 0 row r - 1 and zeros where r % shift_L == 0
  *        (the previous step's state). Fixed row chunks, folded in order: deterministic.
@@ -418,6 +428,9 @@ int32_t rs_masked_proj(const float* x, int64_t ldx, const float* W, const float*
 int32_t rs_masked_dx(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
                      const int32_t* idx, const int32_t* count, int64_t R, int32_t K, int32_t N,
                      float* dx, int64_t lddx, void* stream);
+int32_t rs_masked_dx_acc(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
+                         const int32_t* idx, const int32_t* count, int64_t R, int32_t K, int32_t N,
+                         const float* add, int64_t ldadd, float* dx, int64_t lddx, void* stream);
 size_t rs_masked_wgrad_workspace_size(int32_t K, int32_t N);
 int32_t rs_masked_wgrad(const float* A, int64_t lda, int32_t shift_L, const float* D, int64_t ldd,
                         const int32_t* idx, const int32_t* count, int32_t K, int32_t N, float* C,
@@ -433,6 +446,14 @@ int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const float* neg,
                         const float* W3, const float* b3, const float* daux, float* dhidden,
                         float* dpos, float* dneg, float* dparams, void* workspace,
                         size_t ws_bytes, void* stream);
+/* rs_dien_aux_bwd with acc_hidden = 1: dhidden holds the hidden states' upstream gradient (the
+ * attention's + the AUGRU's) and the aux loss's part is added in place (no fill, no add pass). */
+int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, const float* neg,
+                            const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
+                            const float* W1, const float* b1, const float* W2, const float* b2,
+                            const float* W3, const float* b3, const float* daux, float* dhidden,
+                            int32_t acc_hidden, float* dpos, float* dneg, float* dparams,
+                            void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Keras binary_crossentropy on probabilities (ctr/train.py:85, dien/train.py:18,

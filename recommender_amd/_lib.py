@@ -55,6 +55,7 @@ _SIGS = {
     "rs_device_count": (_i32, []),
     "rs_stream_copy": (_i32, [_p, _p, _sz, _p]),
     "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
+    "rs_embedding_fwd_strided": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _i64, _p, _p]),
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_sort_ids_masked": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
@@ -105,12 +106,16 @@ _SIGS = {
     "rs_valid_rows": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
     "rs_masked_proj": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
     "rs_masked_dx": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "rs_masked_dx_acc": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p, _i64,
+                                _p]),
     "rs_masked_wgrad_workspace_size": (_sz, [_i32, _i32]),
     "rs_masked_wgrad": (_i32, [_p, _i64, _i32, _p, _i64, _p, _p, _i32, _i32, _p, _p, _p, _sz, _p]),
     "rs_dien_aux_fwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                _p, _p]),
     "rs_dien_aux_bwd": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_dien_aux_bwd_acc": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
+                                   _p, _p, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_act_bwd_colsum_workspace_size": (_sz, [_i64, _i32]),
     "rs_act_bwd_colsum": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
     "rs_philox4x32_10": (_i32, [_p, _i64, _u32, _u32, _p, _p]),

@@ -160,8 +160,9 @@ __device__ __forceinline__ float sig_ce(float z, float y) {
 }
 
 // ---------------------------------------------------------------------------------------
-// forward: one wave per (example, set); the block's waves are 2 examples × {pos, neg}, summed
-// in LDS; aux[b] as dien/layers.py:105-108
+// forward: persistent blocks (the 42 KB of weights staged once per block, not once per two
+// examples: staging was most of the kernel's time); each round the block's waves are 2 examples
+// × {pos, neg}, summed in LDS; aux[b] as dien/layers.py:105-108
 // ---------------------------------------------------------------------------------------
 template <int H, int E>
 __global__ __launch_bounds__(256) void aux_fwd_kernel(AuxArgs a, float* __restrict__ aux) {
@@ -170,33 +171,37 @@ __global__ __launch_bounds__(256) void aux_fwd_kernel(AuxArgs a, float* __restri
   stage_weights(a, s);
   __syncthreads();
   const int lane = threadIdx.x & 63, j = lane & 15, kq = lane >> 4, wave = threadIdx.x >> 6;
-  const int64_t b = (int64_t)blockIdx.x * (kWaves / 2) + (wave >> 1);
   const int set = wave & 1;
-  float total = 0.f;
-  int cnt = 1;
-  if (b < a.B) {
-    cnt = aux_count(a, b, lane);
-    const int NT = (a.L - 1 + 15) / 16;
-    const float* e = set == 0 ? a.pos : a.neg;
-    for (int tile = 0; tile < NT; ++tile) {
-      const int t = 16 * tile + j;
-      const bool m = t <= a.L - 2 && a.mask[b * a.L + t + 1] != 0;
-      if (__ballot(m) == 0) continue;  // no valid row: the tile adds exactly 0
-      float xv[(H + E) / 4];
-      load_x<H, E>(a, e, b, t, kq, xv);
-      f4 h1[kT1], h2[kT2];
-      const float z = aux_forward<H, E>(a, s, xv, j, kq, h1, h2);
-      float tl = m ? sig_ce(z, set == 0 ? 1.f : 0.f) : 0.f;
-      // row sum of the tile (rows j of each kq lane group, fixed butterfly order)
+  const int NT = (a.L - 1 + 15) / 16;
+  const float* e = set == 0 ? a.pos : a.neg;
+  const int64_t n_rounds = (a.B + kWaves / 2 - 1) / (kWaves / 2);
+  for (int64_t rd = blockIdx.x; rd < n_rounds; rd += gridDim.x) {
+    const int64_t b = rd * (kWaves / 2) + (wave >> 1);
+    float total = 0.f;
+    int cnt = 1;
+    if (b < a.B) {
+      cnt = aux_count(a, b, lane);
+      for (int tile = 0; tile < NT; ++tile) {
+        const int t = 16 * tile + j;
+        const bool m = t <= a.L - 2 && a.mask[b * a.L + t + 1] != 0;
+        if (__ballot(m) == 0) continue;  // no valid row: the tile adds exactly 0
+        float xv[(H + E) / 4];
+        load_x<H, E>(a, e, b, t, kq, xv);
+        f4 h1[kT1], h2[kT2];
+        const float z = aux_forward<H, E>(a, s, xv, j, kq, h1, h2);
+        float tl = m ? sig_ce(z, set == 0 ? 1.f : 0.f) : 0.f;
+        // row sum of the tile (rows j of each kq lane group, fixed butterfly order)
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) tl += __shfl_xor(tl, off);
-      total += tl;
+        for (int off = 1; off < 16; off <<= 1) tl += __shfl_xor(tl, off);
+        total += tl;
+      }
     }
+    if (lane == 0) sums[wave] = total;
+    __syncthreads();
+    if (b < a.B && set == 0 && lane == 0)
+      aux[b] = (sums[wave] + sums[wave + 1]) / ((float)cnt * 2.f);
+    __syncthreads();  // sums is rewritten next round
   }
-  if (lane == 0) sums[wave] = total;
-  __syncthreads();
-  if (b < a.B && set == 0 && lane == 0)
-    aux[b] = (sums[wave] + sums[wave + 1]) / ((float)cnt * 2.f);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -216,6 +221,7 @@ struct AuxGrad {
   const int32_t* items;    // live items (tile-major index tile·B + b), in order
   const int32_t* n_items;  // [1] their count
   const int32_t* cnt;      // [B] Σ_t m[b, t+1]
+  int acc_hidden;          // 1: dhidden += this loss's part (the caller's upstream gradient kept)
 };
 
 // live items: tile·B + b holds a valid row, or example b has none (0/0: NaN, as the reference)
@@ -376,8 +382,9 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
         const int f0 = 16 * x + 4 * kq;
         if (f0 < H) {
           const float* o = S.dxh[io] + j * kMaxH + f0;
-          store4(g.dhidden + (b * L + t) * (int64_t)H + f0,
-                 dxh[x] + f4{o[0], o[1], o[2], o[3]});
+          float* dst = g.dhidden + (b * L + t) * (int64_t)H + f0;
+          const f4 v = dxh[x] + f4{o[0], o[1], o[2], o[3]};
+          store4(dst, g.acc_hidden ? *reinterpret_cast<const f4*>(dst) + v : v);
         }
       }
     }
@@ -523,7 +530,8 @@ extern "C" int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const 
   if (int32_t e = check_aux(a)) return e;
   RS_CHECK_ARG(aux, "null pointer");
   if (B == 0) return RS_OK;
-  const unsigned grid = (unsigned)ceil_div(B, kWaves / 2);
+  // 3 resident blocks per CU (42 KB of LDS each), persistent over the example pairs
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(B, kWaves / 2), 3 * device_cus());
   hipStream_t st = as_stream(stream);
   if (H == 36 && E == 36) aux_fwd_kernel<36, 36><<<grid, 64 * kWaves, 0, st>>>(a, aux);
   else if (H == 16 && E == 16) aux_fwd_kernel<16, 16><<<grid, 64 * kWaves, 0, st>>>(a, aux);
@@ -532,6 +540,14 @@ extern "C" int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const 
   return RS_OK;
 }
 
+extern "C" int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, const float* neg,
+                                       const uint8_t* mask, int64_t B, int32_t L, int32_t H,
+                                       int32_t E, const float* W1, const float* b1, const float* W2,
+                                       const float* b2, const float* W3, const float* b3,
+                                       const float* daux, float* dhidden, int32_t acc_hidden,
+                                       float* dpos, float* dneg, float* dparams, void* workspace,
+                                       size_t ws_bytes, void* stream);
+
 extern "C" int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const float* neg,
                                    const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                                    const float* W1, const float* b1, const float* W2,
@@ -539,6 +555,20 @@ extern "C" int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const 
                                    const float* daux, float* dhidden, float* dpos, float* dneg,
                                    float* dparams, void* workspace, size_t ws_bytes,
                                    void* stream) {
+  return rs_dien_aux_bwd_acc(hidden, pos, neg, mask, B, L, H, E, W1, b1, W2, b2, W3, b3, daux,
+                             dhidden, 0, dpos, dneg, dparams, workspace, ws_bytes, stream);
+}
+
+// acc_hidden = 1: dhidden holds the upstream gradient of the hidden states (attention + AUGRU)
+// and this loss's part is added to it in place (rows of tiles without a valid step untouched):
+// no zero fill and no separate add pass
+extern "C" int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, const float* neg,
+                                       const uint8_t* mask, int64_t B, int32_t L, int32_t H,
+                                       int32_t E, const float* W1, const float* b1, const float* W2,
+                                       const float* b2, const float* W3, const float* b3,
+                                       const float* daux, float* dhidden, int32_t acc_hidden,
+                                       float* dpos, float* dneg, float* dparams, void* workspace,
+                                       size_t ws_bytes, void* stream) {
   AuxArgs a{hidden, pos, neg, mask, B, L, H, E, W1, b1, W2, b2, W3, b3};
   if (int32_t e = check_aux(a)) return e;
   RS_CHECK_ARG(daux && dhidden && dpos && dneg && dparams && workspace, "null pointer");
@@ -572,10 +602,10 @@ extern "C" int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const 
   RS_CHECK_LAUNCH();
   const size_t lds = bwd_lds_bytes();
   // input gradients start at 0: the kernel writes only the rows of tiles that hold a valid row
-  RS_CHECK_HIP(hipMemsetAsync(dhidden, 0, (size_t)B * L * H * 4, st));
+  if (!acc_hidden) RS_CHECK_HIP(hipMemsetAsync(dhidden, 0, (size_t)B * L * H * 4, st));
   RS_CHECK_HIP(hipMemsetAsync(dpos, 0, (size_t)B * L * E * 4, st));
   RS_CHECK_HIP(hipMemsetAsync(dneg, 0, (size_t)B * L * E * 4, st));
-  AuxGrad g{daux, dhidden, dpos, dneg, part, items, n_live, cnt};
+  AuxGrad g{daux, dhidden, dpos, dneg, part, items, n_live, cnt, acc_hidden ? 1 : 0};
   auto run = [&](auto kern) -> int32_t {
     RS_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -142,7 +142,8 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
                                                         const int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ count, int64_t R,
                                                         int K, int N, float* __restrict__ dx,
-                                                        int64_t lddx) {
+                                                        int64_t lddx, const float* __restrict__ add,
+                                                        int64_t ldadd) {
   constexpr int NQ = (NM + 63) / 64;  // d elements per lane per row
   __shared__ __attribute__((aligned(16))) float ds[4][16][NM];
   __shared__ float wsh[64 * NM];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
     const uint64_t zm = __ballot(lane < 16 && rl < R && mask[rl] == 0);
     for (int e = lane; e < 16 * K; e += 64) {
       const int i = e / K, k = e - i * K;
-      if ((zm >> i) & 1ull) dx[(r0 + i) * lddx + k] = 0.f;
+      if ((zm >> i) & 1ull) dx[(r0 + i) * lddx + k] = add ? add[(r0 + i) * ldadd + k] : 0.f;
     }
   }
   const int64_t cnt = *count;
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
       acc = fmaf(v[2], w[4 * n4 + 2], acc);
       acc = fmaf(v[3], w[4 * n4 + 3], acc);
     }
-    if (lane < K) dx[(int64_t)row * lddx + lane] = acc;
+    if (lane < K)
+      dx[(int64_t)row * lddx + lane] = add ? add[(int64_t)row * ldadd + lane] + acc : acc;
   }
 }
 
@@ -367,21 +369,30 @@ extern "C" int32_t rs_masked_proj(const float* x, int64_t ldx, const float* W, c
   return RS_OK;
 }
 
-extern "C" int32_t rs_masked_dx(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
-                                const int32_t* idx, const int32_t* count, int64_t R, int32_t K,
-                                int32_t N, float* dx, int64_t lddx, void* stream) {
+extern "C" int32_t rs_masked_dx_acc(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
+                                    const int32_t* idx, const int32_t* count, int64_t R, int32_t K,
+                                    int32_t N, const float* add, int64_t ldadd, float* dx,
+                                    int64_t lddx, void* stream) {
   RS_CHECK_ARG(R >= 0 && K >= 1 && K <= 64 && N >= 1 && N <= 192, "bad sizes (K <= 64, N <= 192)");
-  RS_CHECK_ARG(ldd >= N && lddx >= K, "bad leading dimensions");
+  RS_CHECK_ARG(ldd >= N && lddx >= K && (!add || ldadd >= K), "bad leading dimensions");
   if (R == 0) return RS_OK;
   RS_CHECK_ARG(d && W && mask && idx && count && dx, "null pointer");
   hipStream_t st = as_stream(stream);
   const int grid = (int)ceil_div(R, 64);  // one wave per 16 rows (and per 16 listed rows)
-  if (N <= 64) masked_dx_kernel<64><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx);
-  else if (N <= 112) masked_dx_kernel<112><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx);
-  else if (N <= 128) masked_dx_kernel<128><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx);
-  else masked_dx_kernel<192><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx);
+#define RS_DX(NM) masked_dx_kernel<NM><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx, add, ldadd)
+  if (N <= 64) RS_DX(64);
+  else if (N <= 112) RS_DX(112);
+  else if (N <= 128) RS_DX(128);
+  else RS_DX(192);
+#undef RS_DX
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_masked_dx(const float* d, int64_t ldd, const float* W, const uint8_t* mask,
+                                const int32_t* idx, const int32_t* count, int64_t R, int32_t K,
+                                int32_t N, float* dx, int64_t lddx, void* stream) {
+  return rs_masked_dx_acc(d, ldd, W, mask, idx, count, R, K, N, nullptr, 0, dx, lddx, stream);
 }
 
 extern "C" size_t rs_masked_wgrad_workspace_size(int32_t K, int32_t N) {

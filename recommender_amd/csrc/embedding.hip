@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
                                                      int32_t dtype, int64_t n_ids,
                                                      const int64_t* __restrict__ slot_offsets,
                                                      int32_t n_slots, float* __restrict__ out,
-                                                     int32_t* err_flag, int lpr_log2) {
+                                                     int32_t* err_flag, int lpr_log2, int64_t out_ld) {
   constexpr int U = 4;
   const int lpr = 1 << lpr_log2;
   const int gl = threadIdx.x & (lpr - 1);
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
           int col = (gl + c * lpr) * VEC;
-          if (col < dim) RowIO<VEC>::store(out + p * dim + col, v[u][c]);
+          if (col < dim) RowIO<VEC>::store(out + p * out_ld + col, v[u][c]);
         }
       }
     }
@@ -1050,24 +1050,41 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 
 using namespace rs;
 
+extern "C" int32_t rs_embedding_fwd_strided(const float* table, int64_t n_rows, int32_t dim,
+                                            const void* ids, int32_t id_dtype, int64_t n_ids,
+                                            const int64_t* slot_offsets, int32_t n_slots, float* out,
+                                            int64_t out_ld, int32_t* err_flag, void* stream);
+
 extern "C" int32_t rs_embedding_fwd(const float* table, int64_t n_rows, int32_t dim, const void* ids,
                                     int32_t id_dtype, int64_t n_ids, const int64_t* slot_offsets,
                                     int32_t n_slots, float* out, int32_t* err_flag, void* stream) {
+  return rs_embedding_fwd_strided(table, n_rows, dim, ids, id_dtype, n_ids, slot_offsets, n_slots,
+                                  out, dim, err_flag, stream);
+}
+
+// the gathered rows written at a row stride: out[p * out_ld + c] (a column block of a wider
+// row-major tensor, e.g. the item ‖ category halves of DIEN's flat embedding, no concat)
+extern "C" int32_t rs_embedding_fwd_strided(const float* table, int64_t n_rows, int32_t dim,
+                                            const void* ids, int32_t id_dtype, int64_t n_ids,
+                                            const int64_t* slot_offsets, int32_t n_slots, float* out,
+                                            int64_t out_ld, int32_t* err_flag, void* stream) {
   RS_CHECK_ARG(dim > 0, "dim must be > 0");
+  RS_CHECK_ARG(out_ld >= dim, "out_ld must be >= dim");
   RS_CHECK_ARG(n_ids >= 0, "n_ids must be >= 0");
   RS_CHECK_ARG(n_slots >= 1, "n_slots must be >= 1");
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
   RS_CHECK_ARG(n_ids == 0 || (table && ids && out), "null pointer");
   if (n_ids == 0) return RS_OK;
-  const void* ptrs[2] = {table, out};
-  RowGeom geom = row_geom(dim, ptrs, 2);
+  // a row stride that breaks the vector width's alignment downgrades it like a base pointer
+  const void* ptrs[3] = {table, out, reinterpret_cast<const void*>((uintptr_t)(out_ld * 4))};
+  RowGeom geom = row_geom(dim, ptrs, 3);
   hipStream_t st = as_stream(stream);
   const int gpb = 256 >> geom.lpr_log2;
   int64_t blocks = std::min<int64_t>(ceil_div(n_ids, gpb * 4), 256 * 16);
   RS_DISPATCH_VEC_CPL(geom, ({
     gather_kernel<VEC, CPL><<<blocks, 256, 0, st>>>(table, n_rows, dim, ids, id_dtype, n_ids,
                                                     slot_offsets, n_slots, out, err_flag,
-                                                    geom.lpr_log2);
+                                                    geom.lpr_log2, out_ld);
   }));
   RS_CHECK_LAUNCH();
   return RS_OK;

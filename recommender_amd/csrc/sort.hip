@@ -307,15 +307,27 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   }
 }
 
-// count distinct valid rows in a sorted key array (one atomic per block)
+// count distinct valid rows in a sorted key array (one atomic per block). Each thread takes 4
+// consecutive keys in one 16-byte load (the key before them from the previous thread's group, an
+// L1 hit), grid-strided: the whole array is in flight at once (the one-key-per-iteration loop it
+// replaces walked 13 dependent loads per thread: 12.7 us at the north star's 1.7 M keys)
 __global__ __launch_bounds__(256) void count_unique_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                            uint32_t n_rows, int32_t* __restrict__ n_unique) {
   __shared__ int32_t red[4];
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int32_t c = 0;
-  for (; i < n; i += stride) {
-    uint32_t k = keys[i];
+  const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const uint4 k = reinterpret_cast<const uint4*>(keys)[q];
+    const uint32_t prev = q > 0 ? keys[4 * q - 1] : ~0u;
+    c += (k.x < n_rows && (q == 0 || k.x != prev)) ? 1 : 0;
+    c += (k.y < n_rows && k.y != k.x) ? 1 : 0;
+    c += (k.z < n_rows && k.z != k.y) ? 1 : 0;
+    c += (k.w < n_rows && k.w != k.z) ? 1 : 0;
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t k = keys[i];
     c += (k < n_rows && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
   }
   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
@@ -751,7 +763,8 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                               static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, &kg, st);
   if (s) return s;
   if (n_unique) {
-    count_unique_kernel<<<std::min(blocks, 512), 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);
+    const int cblocks = (int)std::min<int64_t>(ceil_div(ceil_div(n_ids, 4), 256), 2048);
+    count_unique_kernel<<<cblocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);
     RS_CHECK_LAUNCH();
   }
   return RS_OK;

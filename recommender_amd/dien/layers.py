@@ -462,11 +462,7 @@ class _AuxLossFn(torch.autograd.Function):
         dn = torch.empty_like(neg)
         In, n1, n2 = H + E, W1.shape[1], W2.shape[1]
         dparams = torch.empty(In * n1 + n1 + n1 * n2 + n2 + n2 + 1, device=dev)
-        nb = L.lib().rs_dien_aux_workspace_size(B, Lh, H, E)
-        ws = _aux_ws.get(dev)
-        if ws is None or ws.numel() < nb:
-            ws = torch.empty(nb, dtype=torch.uint8, device=dev)
-            _aux_ws[dev] = ws
+        ws = _aux_workspace(B, Lh, H, E, dev)
         args = (hidden, pos, neg, mask_u8, B, Lh, H, E, W1, b1, W2, b2, W3, b3,
                 daux.contiguous(), dh, dp, dn, dparams, ws)
         L.call("rs_dien_aux_bwd", *[L.ptr(x) if isinstance(x, torch.Tensor) else x for x in args],
@@ -481,6 +477,90 @@ class _AuxLossFn(torch.autograd.Function):
 
 
 _aux_ws: dict = {}
+
+
+def _aux_workspace(B, Lh, H, E, dev):
+    nb = L.lib().rs_dien_aux_workspace_size(B, Lh, H, E)
+    ws = _aux_ws.get(dev)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        _aux_ws[dev] = ws
+    return ws
+
+
+class _InterestExtractFn(torch.autograd.Function):
+    """InterestExtract (dien/layers.py:76-133) as one autograd node: the GRU over the positive
+    history and the auxiliary loss on its states. Same kernels as _GRUFn + _AuxLossFn; the
+    backward sums the two consumers' gradients inside the kernels instead of in separate passes:
+    the aux loss's part of dL/dh is added in place to the upstream dL/dh (rs_dien_aux_bwd_acc: no
+    zero fill, no add), and its part of dL/dpos is the addend of the GRU's input gradient
+    (rs_masked_dx_acc: no add)."""
+
+    @staticmethod
+    def forward(ctx, pos, neg, mask_u8, kernel, recurrent_kernel, bias, W1, b1, W2, b2, W3, b3):
+        B, T, X = pos.shape
+        H = recurrent_kernel.shape[0]
+        E = neg.shape[-1]
+        dev = pos.device
+        vr = _valid_rows(mask_u8)
+        xw = _masked_proj(pos.reshape(-1, X), kernel, bias[0], vr).view(B, T, 3 * H)
+        out = torch.empty(B, T, H, device=dev)
+        saved = torch.empty(B, T, 4 * H, device=dev)
+        rk = recurrent_kernel.contiguous()
+        st = L.stream_ptr(dev)
+        L.call("rs_gru_fwd", L.ptr(xw), L.ptr(rk), L.ptr(bias[1].contiguous()), L.ptr(mask_u8), B, T,
+               H, L.ptr(out), L.ptr(saved), st)
+        aux = torch.empty(B, device=dev)
+        L.call("rs_dien_aux_fwd", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H, E,
+               L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(aux), st)
+        ctx.save_for_backward(pos, neg, kernel, rk, out, saved, mask_u8, *vr, W1, b1, W2, b2, W3, b3)
+        return out, aux
+
+    @staticmethod
+    def backward(ctx, dhidden, daux):
+        (pos, neg, kernel, rk, out, saved, mask_u8, idx, cnt,
+         W1, b1, W2, b2, W3, b3) = ctx.saved_tensors
+        B, T, X = pos.shape
+        H = rk.shape[0]
+        E = neg.shape[-1]
+        dev = pos.device
+        st = L.stream_ptr(dev)
+        # dL/dh: the upstream gradient (owned by this node: summed by autograd or handed over by
+        # its one consumer), the aux loss's part added in place below
+        if dhidden is None:
+            dh = torch.zeros(B, T, H, device=dev)
+        elif dhidden.is_contiguous():
+            dh = dhidden
+        else:
+            dh = dhidden.contiguous()
+        da = torch.zeros(B, device=dev) if daux is None else daux.contiguous()
+        dp_aux = torch.empty_like(pos)
+        dneg = torch.empty_like(neg)
+        In, n1, n2 = H + E, W1.shape[1], W2.shape[1]
+        dparams = torch.empty(In * n1 + n1 + n1 * n2 + n2 + n2 + 1, device=dev)
+        ws = _aux_workspace(B, T, H, E, dev)
+        L.call("rs_dien_aux_bwd_acc", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H,
+               E, L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(da),
+               L.ptr(dh), 1, L.ptr(dp_aux), L.ptr(dneg), L.ptr(dparams), L.ptr(ws), ws.numel(), st)
+        dxw = torch.empty(B, T, 3 * H, device=dev)
+        dinner = torch.empty(B, T, 3 * H, device=dev)
+        L.call("rs_gru_bwd", L.ptr(dh), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
+               H, L.ptr(dxw), L.ptr(dinner), L.RS_DIEN_SKIP_MASKED_ROWS, st)
+        dxw2, din2 = dxw.view(-1, 3 * H), dinner.view(-1, 3 * H)
+        vr = (idx, cnt)
+        m = mask_u8.reshape(-1)
+        dpos = torch.empty_like(pos)
+        L.call("rs_masked_dx_acc", L.ptr(dxw2), _ld(dxw2), L.ptr(kernel.contiguous()), L.ptr(m),
+               L.ptr(idx), L.ptr(cnt), B * T, X, 3 * H, L.ptr(dp_aux), X, L.ptr(dpos), X, st)
+        dk, db0 = _masked_wgrad(pos.reshape(-1, X), 0, dxw2, vr)
+        drk, db1 = _masked_wgrad(out.view(-1, H), T, din2, vr)
+        o = 0
+        outs = []
+        for shape in (W1.shape, b1.shape, W2.shape, b2.shape, W3.shape, b3.shape):
+            n = int(torch.Size(shape).numel())
+            outs.append(dparams[o:o + n].view(shape))
+            o += n
+        return (dpos, dneg, None, dk, drk, torch.stack([db0, db1]), *outs)
 
 
 def _sigmoid_ce(labels, logits):
@@ -528,6 +608,19 @@ class InterestExtract(nn.Module):
 
     def forward(self, inputs, training=False, mask=None):
         pos_history, neg_history = inputs
+        g = self.gru
+        if g.kernel is None:
+            g.build(pos_history.shape[-1], pos_history.device)
+        H, X = g.units, pos_history.shape[-1]
+        if (_rows_ready(X, H) and pos_history.is_cuda and neg_history.shape == pos_history.shape
+                and pos_history.shape[1] >= 2
+                and self._fused_aux_ready(pos_history.new_empty(1, 2, H), pos_history)):
+            # the GRU and its aux loss as one node (_InterestExtractFn)
+            l1, l2, l3 = self.auxiliary_net.layers
+            m = _mask_u8(mask, pos_history.shape[:2], pos_history.device)
+            return _InterestExtractFn.apply(pos_history.contiguous(), neg_history.contiguous(), m,
+                                            g.kernel, g.recurrent_kernel, g.bias, l1.kernel,
+                                            l1.bias, l2.kernel, l2.bias, l3.kernel, l3.bias)
         hidden_state = self.gru(pos_history, mask=mask)
         aux = self.compute_auxiliary_loss((hidden_state, pos_history, neg_history), training, mask)
         return hidden_state, aux

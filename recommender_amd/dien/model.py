@@ -16,6 +16,7 @@ import torch
 from torch import nn
 
 from ..embedding import Embedding
+from ..functional import embedding_lookup_concat
 from .layers import (MLP, DIENAttention, InterestEvolve, InterestExtract, LocalActivationUnit,
                      compute_his_average)
 
@@ -36,8 +37,8 @@ class BaseModel(nn.Module):
         """grad_mask: the history mask when every consumer skips the masked steps (DIEN), so
         the tables' densified gradients leave those positions out (Embedding grad_mask)."""
         item, cat = inputs
-        return torch.cat([self.item_embedding(item, grad_mask), self.cat_embedding(cat, grad_mask)],
-                         dim=-1)
+        # one output, each lookup gathering into its column block (no concat pass)
+        return embedding_lookup_concat(self.item_embedding, item, self.cat_embedding, cat, grad_mask)
 
     def compute_prob(self, inputs):
         return self.forward(inputs)

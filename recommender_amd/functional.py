@@ -55,16 +55,66 @@ class _EmbeddingLookup(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        tm = ctx.table_module
         g = grad_out.reshape(-1, grad_out.shape[-1])
-        if tm.fused_optimizer is not None:
-            tm.fused_optimizer.apply_async(tm, ctx.ids, g.contiguous(), tm.take_presorted(ctx.ids))
-        else:
-            if ctx.grad_mask is None:
-                tm.accumulate_grad(ctx.ids, g)
-            else:
-                tm.accumulate_grad(ctx.ids, g, valid=ctx.grad_mask)
+        _lookup_backward(ctx.table_module, ctx.ids, g, ctx.grad_mask)
         return None, None, None, None
+
+
+def _lookup_backward(tm, ids, g, grad_mask):
+    """A lookup's upstream rows g [N, dim] (possibly a strided column block) to its table."""
+    if tm.fused_optimizer is not None:
+        tm.fused_optimizer.apply_async(tm, ids, g.contiguous(), tm.take_presorted(ids))
+    elif grad_mask is None:
+        tm.accumulate_grad(ids, g)
+    else:
+        tm.accumulate_grad(ids, g, valid=grad_mask)
+
+
+class _EmbeddingLookupConcat(torch.autograd.Function):
+    """tf.concat([table_a(ids_a), table_b(ids_b)], -1) in one output: each lookup gathers into its
+    column block (rs_embedding_fwd_strided), no concat pass; the backward hands each table its
+    column block of the upstream gradient as strided rows (the table's take_grad concatenates
+    lookups in one copy anyway)."""
+
+    @staticmethod
+    def forward(ctx, handle_a, handle_b, ta, tb, ids_a, ids_b, grad_mask=None):
+        _wait_update(ta)
+        _wait_update(tb)
+        ids_a, ids_b = _ids_flat(ids_a), _ids_flat(ids_b)
+        if ids_a.shape != ids_b.shape:
+            raise ValueError("the two lookups must have the same ids shape")
+        wa, wb = ta.weight, tb.weight
+        L.require_device(wa, "embedding table")
+        L.require_device(wb, "embedding table")
+        da, db = wa.shape[1], wb.shape[1]
+        out = torch.empty(*ids_a.shape, da + db, device=wa.device, dtype=torch.float32)
+        st = L.stream_ptr(wa.device)
+        for t, ids, col, d in ((ta, ids_a, 0, da), (tb, ids_b, da, db)):
+            so = t.slot_offsets
+            n_slots = 1 if so is None else so.numel() - 1
+            L.call("rs_embedding_fwd_strided", L.ptr(t.weight), t.weight.shape[0], d, L.ptr(ids),
+                   L.id_dtype_code(ids), ids.numel(), L.ptr(so), n_slots,
+                   L.ptr(out.narrow(-1, col, d)), da + db, L.ptr(t.err_flag), st)
+        ctx.tables = (ta, tb)
+        ctx.ids = (ids_a, ids_b)
+        ctx.grad_mask = grad_mask
+        ctx.da = da
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        g = grad_out.reshape(-1, grad_out.shape[-1])
+        da = ctx.da
+        (ta, tb), (ia, ib) = ctx.tables, ctx.ids
+        _lookup_backward(ta, ia, g[:, :da], ctx.grad_mask)
+        _lookup_backward(tb, ib, g[:, da:], ctx.grad_mask)
+        return None, None, None, None, None, None, None
+
+
+def embedding_lookup_concat(table_a, ids_a, table_b, ids_b, grad_mask=None) -> torch.Tensor:
+    """[table_a(ids_a) ‖ table_b(ids_b)] along the last axis (grad_mask: embedding_lookup)."""
+    return _EmbeddingLookupConcat.apply(table_a.grad_handle, table_b.grad_handle, table_a,
+                                        table_b, ids_a, ids_b, grad_mask)
 
 
 def embedding_lookup(table_module, ids: torch.Tensor, grad_mask=None) -> torch.Tensor:

@@ -32,6 +32,46 @@ def test_gather_shared_table(dim, id_dtype, rng):
     assert not t.oob_detected()
 
 
+@pytest.mark.parametrize("da,db", [(18, 18), (16, 7), (64, 128)])
+def test_concat_lookup_matches_cat_of_lookups(da, db, rng):
+    """functional.embedding_lookup_concat (two strided gathers into one [.., da + db] output,
+    dien/model.py:14-19's tf.concat) == torch.cat of the two lookups, forward bit for bit; its
+    backward hands each table its column block (with the grad mask), so the densified table
+    gradients equal the two-lookup path's bit for bit; an out-of-range id flags its own table."""
+    from recommender_amd.functional import embedding_lookup_concat
+    from recommender_amd.optim import densify_grad, _Workspace
+
+    Va, Vb, B, Lh = 3000, 40, 33, 17
+    wa = torch.from_numpy(rng.standard_normal((Va, da)).astype(np.float32))
+    wb = torch.from_numpy(rng.standard_normal((Vb, db)).astype(np.float32))
+    ia = torch.from_numpy(rng.integers(0, Va, (B, Lh)).astype(np.int32)).to(DEV)
+    ib = torch.from_numpy(rng.integers(0, Vb, (B, Lh)).astype(np.int32)).to(DEV)
+    ib[5, 3] = Vb + 2  # out of range for table b only
+    mask = ia != 0
+    mask[::3, 10:] = False
+    up = torch.from_numpy(rng.standard_normal((B, Lh, da + db)).astype(np.float32)).to(DEV)
+    grads = []
+    for fused in (True, False):
+        ta = Embedding(Va, da, device=DEV, weight=wa)
+        tb = Embedding(Vb, db, device=DEV, weight=wb)
+        if fused:
+            out = embedding_lookup_concat(ta, ia, tb, ib, mask)
+        else:
+            out = torch.cat([ta(ia, mask), tb(ib, mask)], -1)
+        (out * up).sum().backward()
+        torch.cuda.synchronize()
+        assert not ta.oob_detected() and tb.oob_detected()
+        ws = _Workspace()
+        g = []
+        for t in (ta, tb):
+            ids, rows, valid = t.take_grad(with_valid=True)
+            g.append(densify_grad(t, ids, rows, ws, valid=valid).cpu())
+        grads.append((out.detach().cpu(), g))
+    (o1, g1), (o2, g2) = grads
+    assert torch.equal(o1, o2)
+    assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
+
+
 def test_gather_slab_and_oob(rng):
     card = [7, 1, 300, 50]
     dim = 64

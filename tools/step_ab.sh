@@ -1,0 +1,28 @@
+# A/B of the north-star step's stream schedule (run under gpurun): each variant is one bench.py
+# run without the PMC / secondary lines; prints ms/step (median, p10) and the in-step spans.
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() {  # name, env..., -- bench args
+  name=$1; shift
+  envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+  env "${envs[@]}" timeout -k 10 300 python bench.py --pmc 0 --keras-line 0 --weak-secondary 0 \
+    --compare-layerwise 0 --cpu-baseline-steps 0 --steps 200 "$@" > gpurun_out/stepab_$name.json 2> gpurun_out/stepab_$name.err || { echo "$name failed"; tail -5 gpurun_out/stepab_$name.err; return 1; }
+  python - "$name" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/stepab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+k = d["kernels"]
+print(f"{sys.argv[1]:14s} ms/step {d['ms_per_step']:.4f} median {d['step_ms_distribution']['median']} "
+      f"p10 {d['step_ms_distribution']['p10']} | " +
+      " ".join(f"{n.replace('rs_', '')[:18]} {v['avg_us']}" for n, v in k.items()))
+PY
+}
+for rep in ${REPS:-1 2}; do
+  for v in ${VARIANTS:-base mainapply}; do
+    case $v in
+      base) run base RS_MAIN_APPLY=0 -- --prefetch 0 || exit 1 ;;
+      mainapply) run mainapply RS_MAIN_APPLY=1 -- --prefetch 1 || exit 1 ;;
+      mainapply_graph2) run mainapply_g2 RS_MAIN_APPLY=1 -- --prefetch 1 --graph 2 || exit 1 ;;
+      graph2) run graph2 RS_MAIN_APPLY=0 -- --prefetch 0 --graph 2 || exit 1 ;;
+    esac
+  done
+done
