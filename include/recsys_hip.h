@@ -436,6 +436,23 @@ int32_t rs_masked_wgrad(const float* A, int64_t lda, int32_t shift_L, const floa
                         const int32_t* idx, const int32_t* count, int32_t K, int32_t N, float* C,
                         float* sums, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * fp32 GEMM of the Keras Dense layers on the bf16 matrix cores at fp32 accuracy (split-bf16,
+ * six part products; csrc/gemm.hip): C[b] = act(op(A[b])·op(B[b]) + bias[b]) for b < batch,
+ * op(A)[m][k] = ta ? A[k*lda + m] : A[m*lda + k], op(B)[k][n] = tb ? B[n*ldb + k] : B[k*ldb + n],
+ * per-batch strides sA / sB / sC / sbias (floats); act 0 none, 1 relu, 2 sigmoid; bias may be
+ * NULL. Replaces the Dense layers' tf.matmul / BiasAdd / activation (esmm/layers.py:4-13,
+ * esmm/mmoe.py:8-109, ctr/layers.py:5-14, dien/layers.py:20-31) forward (ta 0, tb 0), dgrad
+ * (dz·Wᵀ: ta 0, tb 1) and wgrad (xᵀ·dz: ta 1, tb 0) products. splits > 1 divides K into that many
+ * ranges (multiples of 32) whose partials are folded in order (deterministic);
+ * workspace >= rs_gemm_x3_workspace_size(M, N, batch, splits). M, N, K, lda, ldb, sA, sB multiples
+ * of 4; A, B 16-byte aligned. */
+size_t rs_gemm_x3_workspace_size(int64_t M, int64_t N, int32_t batch, int32_t splits);
+int32_t rs_gemm_x3(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
+                   int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float* C,
+                   int64_t ldc, int64_t sC, int32_t batch, const float* bias, int64_t sbias,
+                   int32_t act, int32_t splits, void* workspace, size_t ws_bytes, void* stream);
+
 int32_t rs_dien_aux_fwd(const float* hidden, const float* pos, const float* neg,
                         const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                         const float* W1, const float* b1, const float* W2, const float* b2,

@@ -106,6 +106,9 @@ _SIGS = {
     "rs_valid_rows": (_i32, [_p, _i64, _p, _p, _p, _sz, _p]),
     "rs_masked_proj": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
     "rs_masked_dx": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "rs_gemm_x3_workspace_size": (_sz, [_i64, _i64, _i32, _i32]),
+    "rs_gemm_x3": (_i32, [_i32, _i32, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i64,
+                          _i64, _i32, _p, _i64, _i32, _i32, _p, _sz, _p]),
     "rs_masked_dx_acc": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _p, _i64,
                                 _p]),
     "rs_masked_wgrad_workspace_size": (_sz, [_i32, _i32]),

@@ -149,14 +149,25 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
   __shared__ float wsh[64 * NM];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
-  // (A) zeros for the masked rows of this wave's 16 rows
+  // (A) the masked rows of this wave's 16 rows: 0, or the addend (its loads issued together)
   {
     const int64_t r0 = gw * 16;
     const int64_t rl = r0 + (lane & 15);
     const uint64_t zm = __ballot(lane < 16 && rl < R && mask[rl] == 0);
-    for (int e = lane; e < 16 * K; e += 64) {
-      const int i = e / K, k = e - i * K;
-      if ((zm >> i) & 1ull) dx[(r0 + i) * lddx + k] = add ? add[(r0 + i) * ldadd + k] : 0.f;
+    if (zm) {
+      float v[16];
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int e = lane + 64 * it;
+        const int i = e / K, k = e - i * K;
+        v[it] = (add && e < 16 * K && ((zm >> i) & 1ull)) ? add[(r0 + i) * ldadd + k] : 0.f;
+      }
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int e = lane + 64 * it;
+        const int i = e / K, k = e - i * K;
+        if (e < 16 * K && ((zm >> i) & 1ull)) dx[(r0 + i) * lddx + k] = v[it];
+      }
     }
   }
   const int64_t cnt = *count;
@@ -177,6 +188,13 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
       const int n = lane + 64 * q;
       t[i][q] = (row >= 0 && n < N) ? src[n] : 0.f;
     }
+  }
+  // the addend of the listed rows (lane = output column), loaded with the d rows
+  float av[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = __builtin_amdgcn_readlane(rr, i);
+    av[i] = (add && row >= 0 && lane < K) ? add[(int64_t)row * ldadd + lane] : 0.f;
   }
   float w[NM];
 #pragma unroll
@@ -201,8 +219,7 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
       acc = fmaf(v[2], w[4 * n4 + 2], acc);
       acc = fmaf(v[3], w[4 * n4 + 3], acc);
     }
-    if (lane < K)
-      dx[(int64_t)row * lddx + lane] = add ? add[(int64_t)row * ldadd + lane] + acc : acc;
+    if (lane < K) dx[(int64_t)row * lddx + lane] = add ? av[i] + acc : acc;
   }
 }
 
