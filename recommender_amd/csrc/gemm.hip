@@ -151,6 +151,8 @@ struct GemmArgs {
   int act;  // 0 none, 1 relu, 2 sigmoid
 };
 
+// two blocks per CU (210 VGPRs, 48 KB LDS each): one block's split-and-store phase runs under the
+// other's products (a two-stage register prefetch at one block per CU measured 1.3-1.9x slower)
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[6 * kPlane];  // A parts | B parts (48 KB)
@@ -172,21 +174,12 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  Slice<!TA> sa;  // op(A) rows = m: k-contiguous unless transposed
+  Slice<!TA> sa;  // op(A) rows = m: k-contiguous unless A is given transposed
   Slice<TB> sb;   // op(B) rows = n: k-contiguous when B is given as [n][k]
-  // op(A)[m][k]: TA -> A[k*lda + m] (row-contiguous slice over m), else A[m*lda + k]
   sa.load(A, g.lda, m0, g.M, kb, ke);
   sb.load(B, g.ldb, n0, g.N, kb, ke);
   const int r = lane & 15, kg = lane >> 4;
-  for (int64_t k0 = kb; k0 < ke; k0 += kBK) {
-    __syncthreads();  // the previous step's fragments are read
-    sa.store(la);
-    sb.store(lb);
-    __syncthreads();
-    if (k0 + kBK < ke) {  // the next slice flies under this step's products
-      sa.load(A, g.lda, m0, g.M, k0 + kBK, ke);
-      sb.load(B, g.ldb, n0, g.N, k0 + kBK, ke);
-    }
+  auto products = [&]() {
     bf8 bh[4], bm[4], bl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -204,6 +197,17 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma6(ah, am, al, bh[j], bm[j], bl[j], acc[i][j]);
     }
+  };
+  for (int64_t k0 = kb; k0 < ke; k0 += kBK) {
+    __syncthreads();  // the previous step's fragments are read
+    sa.store(la);
+    sb.store(lb);
+    __syncthreads();
+    if (k0 + kBK < ke) {  // the next slice flies under this step's products
+      sa.load(A, g.lda, m0, g.M, k0 + kBK, ke);
+      sb.load(B, g.ldb, n0, g.N, k0 + kBK, ke);
+    }
+    products();
   }
   // C[m][n]: lane (r, kg) of tile (i, j) holds rows 4 kg + q, column r
   float* C = g.C + (g.splits > 1 ? (int64_t)z * g.M * g.N : batch * g.sC);

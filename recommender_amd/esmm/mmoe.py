@@ -44,12 +44,13 @@ class MMOE(nn.Module):
         l0 = [m[0] for m in layers]
         k0 = torch.cat([l.kernel for l in l0], dim=1)             # [in, E*H0]
         b0 = torch.cat([l.bias for l in l0])
-        h = torch.relu(linear(x, k0, b0)).view(x.shape[0], E, -1).transpose(0, 1)  # [E,B,H0]
+        # relu in the GEMM epilogues (and its mask with the bias gradient in one backward pass)
+        h = linear(x, k0, b0, act=1).view(x.shape[0], E, -1).transpose(0, 1)  # [E,B,H0]
         h = h.contiguous()
         for j in range(1, len(layers[0])):
             k = torch.stack([m[j].kernel for m in layers])           # [E, Hin, Hout]
             b = torch.stack([m[j].bias for m in layers])[:, None, :]
-            h = torch.relu(batched_linear(h, k, b))
+            h = batched_linear(h, k, b, act=1)
         return h.transpose(0, 1)                                     # [B, E, H]
 
     def _towers(self, x):

@@ -32,6 +32,44 @@ def get_activation(act):
     return _ACTS[act]
 
 
+# The Dense products on the bf16 matrix cores (csrc/gemm.hip rs_gemm_x3: split-bf16, six part
+# products, fp32-class error per element: tests/test_gemm_gpu.py) — OFF by default, opt in with
+# RS_GEMM_X3=1. Measured (tools/gemm_bench.py, B = 65 536): forward with its bias + relu epilogue
+# 1.06-1.29x the library fp32 GEMM for out >= 200, dgrad 1.12-1.30x for in >= 200, MMOE's batched
+# expert forward 1.21x; whole steps ESMM 2.72 -> 2.65 ms, MMOE 5.21 -> 5.01 ms. Not the default
+# because the parity gates do not hold with it: the cfg4 full-size dense gradients (sums over
+# 65 536 examples) land up to 7x outside their 1e-4-of-magnitude bound, and the layerwise MLP
+# forward is no longer bit-identical to the chain path (tests/test_mlp_chain_gpu.py).
+_GEMM_X3 = __import__("os").environ.get("RS_GEMM_X3", "0") == "1"
+_X3_MIN_N, _X3_MIN_K = 128, 160
+
+
+def _x3_ready(*ts, n=0, k=0, batched=False):
+    if not _GEMM_X3 or (not batched and (n < _X3_MIN_N or k < _X3_MIN_K)):
+        return False
+    return all(t is not None and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+               and t.data_ptr() % 16 == 0 and t.dim() >= 2 and t.shape[-1] % 4 == 0
+               and t.shape[-2] % 4 == 0 for t in ts)
+
+
+def gemm_x3(a, b, tb=False, bias=None, act=0):
+    """act(a·op(b) + bias) by rs_gemm_x3: a [M, K] (or [E, M, K]), b [K, N] (tb: [N, K]) or
+    batched [E, ...]; bias [N] / [E, N] or None; act 0 none, 1 relu, 2 sigmoid."""
+    from . import _lib as L
+
+    batched = a.dim() == 3
+    E = a.shape[0] if batched else 1
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-2] if tb else b.shape[-1]
+    out = torch.empty(*((E,) if batched else ()), M, N, device=a.device, dtype=torch.float32)
+    sA = M * K if batched else 0
+    sB = b.shape[-2] * b.shape[-1] if batched else 0
+    sbias = N if (bias is not None and batched) else 0
+    L.call("rs_gemm_x3", 0, int(tb), M, N, K, L.ptr(a), K, sA, L.ptr(b), b.shape[-1], sB,
+           L.ptr(out), N, M * N, E, L.ptr(bias), sbias, act, 1, None, 0, L.stream_ptr(a.device))
+    return out
+
+
 def _splitk_plan(K: int, fan_in: int, fan_out: int, batches: int = 1):
     """(chunks, rows per chunk) for a K-deep weight-gradient GEMM [in, K]·[K, out]: hipBLASLt's
     single-pass fp32 kernels for K >= 8k run at 7-64 TF/s (tiny-N tiles over a huge K); a
@@ -80,45 +118,94 @@ def bwgrad(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _act_bwd(g, y, act, want_db):
+    """(dz = act'(y)⊙g, Σ_rows dz or None) for act 0 / 1 (relu) / 2 (sigmoid) on [R, N] rows
+    (rs_act_bwd_colsum: one pass for both)."""
+    from . import _lib as L
+
+    if act == 0:
+        return g, (g.sum(0) if want_db else None)
+    R, N = g.shape
+    dz = torch.empty_like(g)
+    db = torch.empty(N, device=g.device, dtype=torch.float32)
+    ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(R, N) // 4), device=g.device)
+    L.call("rs_act_bwd_colsum", L.ptr(g), L.ptr(y), R, N, act, L.ptr(dz), L.ptr(db), L.ptr(ws),
+           ws.numel() * 4, L.stream_ptr(g.device))
+    return dz, (db if want_db else None)
+
+
 class _LinearFn(torch.autograd.Function):
-    """y = x·k (+ b); backward with the split-K weight gradient."""
+    """y = act(x·k (+ b)), act 0 / 1 (relu) / 2 (sigmoid); backward with the split-K weight
+    gradient (and the activation's mask with the bias gradient in one pass)."""
 
     @staticmethod
-    def forward(ctx, x, k, b):
-        ctx.save_for_backward(x, k)
-        ctx.has_b = b is not None
-        return torch.addmm(b, x, k) if b is not None else x @ k
+    def forward(ctx, x, k, b, act=0):
+        x = x.contiguous()
+        if _x3_ready(x, k, n=k.shape[1], k=k.shape[0]) and (b is None or b.is_contiguous()):
+            y = gemm_x3(x, k, bias=b, act=act)
+        else:
+            y = torch.addmm(b, x, k) if b is not None else x @ k
+            if act == 1:
+                y = torch.relu_(y)
+            elif act == 2:
+                y = torch.sigmoid_(y)
+        ctx.save_for_backward(x, k, y if act else None)
+        ctx.has_b, ctx.act = b is not None, act
+        return y
 
     @staticmethod
     def backward(ctx, g):
-        x, k = ctx.saved_tensors
+        x, k, y = ctx.saved_tensors
         g = g.contiguous()
-        dx = g @ k.t() if ctx.needs_input_grad[0] else None
-        return dx, wgrad(x, g), (g.sum(0) if ctx.has_b else None)
+        dz, db = _act_bwd(g, y, ctx.act, ctx.has_b)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (gemm_x3(dz, k, tb=True) if _x3_ready(dz, k, n=k.shape[0], k=k.shape[1])
+                  else dz @ k.t())
+        return dx, wgrad(x, dz), db, None
 
 
-def linear(x: torch.Tensor, k: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
-    return _LinearFn.apply(x, k, b)
+def linear(x: torch.Tensor, k: torch.Tensor, b: torch.Tensor | None = None,
+           act: int = 0) -> torch.Tensor:
+    return _LinearFn.apply(x, k, b, act)
 
 
 class _BatchedLinearFn(torch.autograd.Function):
-    """y[e] = x[e]·k[e] + b[e] for x [E, B, in], k [E, in, out], b [E, 1, out]."""
+    """y[e] = act(x[e]·k[e] + b[e]) for x [E, B, in], k [E, in, out], b [E, 1, out]."""
 
     @staticmethod
-    def forward(ctx, x, k, b):
-        ctx.save_for_backward(x, k)
-        return torch.baddbmm(b, x, k)
+    def forward(ctx, x, k, b, act=0):
+        x = x.contiguous()
+        if _x3_ready(x, k, batched=True) and b.is_contiguous():
+            y = gemm_x3(x, k, bias=b.reshape(b.shape[0], -1), act=act)
+        else:
+            y = torch.baddbmm(b, x, k)
+            if act == 1:
+                y = torch.relu_(y)
+            elif act == 2:
+                y = torch.sigmoid_(y)
+        ctx.save_for_backward(x, k, y if act else None)
+        ctx.act = act
+        return y
 
     @staticmethod
     def backward(ctx, g):
-        x, k = ctx.saved_tensors
+        x, k, y = ctx.saved_tensors
         g = g.contiguous()
-        dx = torch.bmm(g, k.transpose(1, 2)) if ctx.needs_input_grad[0] else None
-        return dx, bwgrad(x, g), g.sum(1, keepdim=True)
+        E = g.shape[0]
+        if ctx.act:
+            # per expert: the mask and its bias-gradient column sums in one pass each
+            parts = [_act_bwd(g[e], y[e], ctx.act, True) for e in range(E)]
+            dz = torch.stack([p[0] for p in parts])
+            db = torch.stack([p[1] for p in parts]).unsqueeze(1)
+        else:
+            dz, db = g, g.sum(1, keepdim=True)
+        dx = torch.bmm(dz, k.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        return dx, bwgrad(x, dz), db, None
 
 
-def batched_linear(x, k, b):
-    return _BatchedLinearFn.apply(x, k, b)
+def batched_linear(x, k, b, act: int = 0):
+    return _BatchedLinearFn.apply(x, k, b, act)
 
 
 _ACT_CODE = {"relu": 1, "sigmoid": 2}
@@ -166,14 +253,18 @@ class _DenseFn(torch.autograd.Function):
     def forward(ctx, x, handle, layer, rows, act=None):
         k = layer.kernel if rows is None else layer.kernel.index_select(0, rows)
         b = layer.bias
-        z = torch.addmm(b, x, k) if b is not None else x @ k
         act = layer.act_code if act is None else act
-        if act == 1:
-            y = torch.relu_(z)
-        elif act == 2:
-            y = torch.sigmoid_(z)
+        x = x.contiguous()
+        if _x3_ready(x, k, n=k.shape[1], k=k.shape[0]) and (b is None or b.is_contiguous()):
+            y = gemm_x3(x, k, bias=b, act=act)  # bias + activation in the epilogue
         else:
-            y = z
+            z = torch.addmm(b, x, k) if b is not None else x @ k
+            if act == 1:
+                y = torch.relu_(z)
+            elif act == 2:
+                y = torch.sigmoid_(z)
+            else:
+                y = z
         ctx.layer, ctx.rows, ctx.act = layer, rows, act
         ctx.save_for_backward(x, k, y if act else None)
         return y
@@ -198,7 +289,10 @@ class _DenseFn(torch.autograd.Function):
                    L.ptr(ws), ws.numel() * 4, L.stream_ptr(dy.device))
         else:
             dz = dy
-        dx = dz @ k.t() if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (gemm_x3(dz, k.contiguous(), tb=True)
+                  if _x3_ready(dz, k, n=k.shape[0], k=k.shape[1]) else dz @ k.t())
         side = _wgrad_stream
         if side is not None:
             side.wait_stream(main)
