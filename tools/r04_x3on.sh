@@ -1,0 +1,11 @@
+# split-bf16 GEMM after the K-step re-accumulation: bias probe, parity with RS_GEMM_X3=1, benches
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 200 python tools/gemm_bias_probe.py || exit 1
+export RS_GEMM_X3=1
+timeout -k 10 900 python -u -m pytest tests/test_gemm_gpu.py tests/test_esmm_gpu.py tests/test_deepfm_gpu.py tests/test_mlp_chain_gpu.py tests/test_dien_step_gpu.py "tests/test_fullsize_gpu.py::test_cfg4_full_size_keras_adam_steps_vs_oracle" -q --maxfail 5 --timeout 600 --timeout-method thread > gpurun_out/x3on_t.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED|Error:|max err" gpurun_out/x3on_t.log | head -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for m in esmm mmoe; do timeout -k 10 300 python benchmarks/bench_models.py --model $m --steps 20 --warmup 3 2>/dev/null | tail -1 | cut -c1-160; done
+timeout -k 10 300 python tools/gemm_bench.py 2>/dev/null | cut -c1-200
