@@ -643,6 +643,17 @@ int32_t rs_side_pool_fwd(const float* side, const float* weight_logits, int64_t 
 int32_t rs_side_pool_bwd(const float* side, const float* attn, const float* grad_hidden,
                          int64_t batch, int32_t n_side, int32_t dim, float* grad_side,
                          float* grad_weight_logits, void* stream);
+/* The same over side rows at any layout: row s of example b at side + b*side_bstride +
+ * s*side_sstride (floats; grad_side written at the same layout) — MMOE pools its experts' outputs
+ * in the [E, B, H] order of the batched expert GEMMs (esmm/mmoe.py:88-96), no transpose pass.
+ * A layout other than [batch, n_side, dim] needs dim % 4 == 0, dim <= 128, 16-byte rows. */
+int32_t rs_side_pool_fwd_strided(const float* side, int64_t side_bstride, int64_t side_sstride,
+                                 const float* weight_logits, int64_t batch, int32_t n_side,
+                                 int32_t dim, float* hidden, float* attn, void* stream);
+int32_t rs_side_pool_bwd_strided(const float* side, int64_t side_bstride, int64_t side_sstride,
+                                 const float* attn, const float* grad_hidden, int64_t batch,
+                                 int32_t n_side, int32_t dim, float* grad_side,
+                                 float* grad_weight_logits, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Factored linear-chain backward of a ctr MLP (hidden Dense layers linear, ctr/layers.py:8):

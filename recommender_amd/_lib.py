@@ -148,6 +148,8 @@ _SIGS = {
     "rs_frobenius_normalize_rows_bwd": (_i32, [_p, _p, _p, _i64, _i32, _p, _p, _p, _sz, _p]),
     "rs_match_logits_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _i64, _p, _p, _p]),
     "rs_match_logits_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p, _p]),
+    "rs_side_pool_fwd_strided": (_i32, [_p, _i64, _i64, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_side_pool_bwd_strided": (_i32, [_p, _i64, _i64, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_fwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_auc_update": (_i32, [_p, _p, _i64, _p, _i32, _p, _p, _p]),

@@ -142,6 +142,94 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_bwd_kernel(
     for (int s = 0; s < S; ++s) grad_w[b * S + s] = a[s] * (ga[s] - dot);
 }
 
+// Row widths D = 4k <= 128: a 32-lane half-wave per example, lane c on the float4 column c, the
+// S side rows' loads in flight together (the one-float-per-lane form above left lanes 16-63 idle
+// on the second pass at D = 80 and ran at 1.5 TB/s: MMOE's gate pooling, 4 launches per step).
+// Any layout: side row s of example b at side + b * sb + s * ss (MMOE pools its experts' outputs
+// in the [E, B, H] order the batched expert GEMMs leave them). The forward sums in the same order
+// as the scalar kernel (bit-identical); the backward's <g, side_s> folds over the half-wave.
+typedef float pf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 32);
+  return v;
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_vec_kernel(
+    const float* __restrict__ side, int64_t sb, int64_t ss, const float* __restrict__ wlogits,
+    int64_t B, int32_t S, int32_t D, float* __restrict__ hidden, float* __restrict__ attn) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (b >= B) return;
+  float a[kMaxSide];
+  if (wlogits) {
+    float mx = -INFINITY;
+    for (int s = 0; s < S; ++s) mx = fmaxf(mx, wlogits[b * S + s]);
+    float sum = 0.f;
+    for (int s = 0; s < S; ++s) {
+      a[s] = expf(wlogits[b * S + s] - mx);
+      sum += a[s];
+    }
+    for (int s = 0; s < S; ++s) a[s] = a[s] / sum;
+    if (attn && c < S) {
+      for (int s = 0; s < S; ++s)
+        if (s == c) attn[b * S + s] = a[s];
+    }
+  }
+  if (4 * c >= D) return;
+  const float* x = side + b * sb + 4 * c;
+  pf4 v[kMaxSide];
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s)
+    if (s < S) v[s] = *reinterpret_cast<const pf4*>(x + s * ss);
+  pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s) {
+    if (s < S) {
+      if (wlogits) acc += a[s] * v[s];
+      else acc += v[s];
+    }
+  }
+  if (!wlogits) acc = acc / (float)S;
+  *reinterpret_cast<pf4*>(hidden + b * D + 4 * c) = acc;
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_bwd_vec_kernel(
+    const float* __restrict__ side, int64_t sb, int64_t ss, const float* __restrict__ attn,
+    const float* __restrict__ g, int64_t B, int32_t S, int32_t D, float* __restrict__ grad_side,
+    float* __restrict__ grad_w) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (b >= B) return;  // a whole half-wave: its shuffles below stay within its own 32 lanes
+  const bool on = 4 * c < D;
+  const pf4 gd = on ? *reinterpret_cast<const pf4*>(g + b * D + 4 * c) : pf4{0.f, 0.f, 0.f, 0.f};
+  if (!attn) {
+    if (on)
+      for (int s = 0; s < S; ++s)
+        *reinterpret_cast<pf4*>(grad_side + b * sb + s * ss + 4 * c) = gd / (float)S;
+    return;
+  }
+  float a[kMaxSide], ga[kMaxSide];
+  for (int s = 0; s < S; ++s) a[s] = attn[b * S + s];
+  pf4 v[kMaxSide];
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s)
+    if (s < S) v[s] = on ? *reinterpret_cast<const pf4*>(side + b * sb + s * ss + 4 * c)
+                         : pf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s) {
+    if (s < S) {
+      if (on) *reinterpret_cast<pf4*>(grad_side + b * sb + s * ss + 4 * c) = a[s] * gd;
+      const pf4 p = gd * v[s];
+      ga[s] = half_sum((p[0] + p[1]) + (p[2] + p[3]));
+    }
+  }
+  float dot = 0.f;
+  for (int s = 0; s < S; ++s) dot += a[s] * ga[s];
+  if (grad_w && c == 0)
+    for (int s = 0; s < S; ++s) grad_w[b * S + s] = a[s] * (ga[s] - dot);
+}
+
 // ---- training-pair sampler (eges/data_loader.py:28-62) -------------
 // walk i (global index walk_base + i) starts at 1 + U[0, n_items - 1) (:30, item 0 is OOV) and
 // takes `length` weighted steps (dgl.sampling.random_walk(prob='weight') [3p]: out-edge e of
@@ -323,28 +411,70 @@ extern "C" int32_t rs_match_logits_bwd(const float* table, int64_t n_rows, int32
   return RS_OK;
 }
 
-extern "C" int32_t rs_side_pool_fwd(const float* side, const float* weight_logits, int64_t batch,
-                                    int32_t n_side, int32_t dim, float* hidden, float* attn,
-                                    void* stream) {
+static bool pool_vec_ok(const void* side, const void* a, const void* b, int32_t dim, int64_t sb,
+                        int64_t ss) {
+  return dim % 4 == 0 && dim <= 128 && sb % 4 == 0 && ss % 4 == 0 &&
+         ((reinterpret_cast<uintptr_t>(side) | reinterpret_cast<uintptr_t>(a) |
+           reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+}
+
+extern "C" int32_t rs_side_pool_fwd_strided(const float* side, int64_t side_bstride,
+                                            int64_t side_sstride, const float* weight_logits,
+                                            int64_t batch, int32_t n_side, int32_t dim,
+                                            float* hidden, float* attn, void* stream) {
   RS_CHECK_ARG(n_side >= 1 && n_side <= kMaxSide && dim >= 1 && batch >= 0,
                "rs_side_pool_fwd: need 1 <= n_side <= %d", kMaxSide);
   if (batch == 0) return RS_OK;
-  pool_fwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
-      side, weight_logits, batch, n_side, dim, hidden, attn);
+  RS_CHECK_ARG(side && hidden, "null pointer");
+  const bool dense = side_bstride == (int64_t)n_side * dim && side_sstride == dim;
+  if (pool_vec_ok(side, hidden, side, dim, side_bstride, side_sstride)) {
+    pool_fwd_vec_kernel<<<waves_grid(ceil_div(batch, 2)), kWave * kWavesPerBlock, 0,
+                          as_stream(stream)>>>(side, side_bstride, side_sstride, weight_logits,
+                                               batch, n_side, dim, hidden, attn);
+  } else {
+    RS_CHECK_ARG(dense, "rs_side_pool_fwd: strided side rows need dim % 4 == 0, dim <= 128");
+    pool_fwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
+        side, weight_logits, batch, n_side, dim, hidden, attn);
+  }
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_side_pool_bwd_strided(const float* side, int64_t side_bstride,
+                                            int64_t side_sstride, const float* attn,
+                                            const float* grad_hidden, int64_t batch,
+                                            int32_t n_side, int32_t dim, float* grad_side,
+                                            float* grad_weight_logits, void* stream) {
+  RS_CHECK_ARG(n_side >= 1 && n_side <= kMaxSide && dim >= 1 && batch >= 0,
+               "rs_side_pool_bwd: need 1 <= n_side <= %d", kMaxSide);
+  if (batch == 0) return RS_OK;
+  RS_CHECK_ARG(side && grad_hidden && grad_side, "null pointer");
+  const bool dense = side_bstride == (int64_t)n_side * dim && side_sstride == dim;
+  if (pool_vec_ok(side, grad_hidden, grad_side, dim, side_bstride, side_sstride)) {
+    pool_bwd_vec_kernel<<<waves_grid(ceil_div(batch, 2)), kWave * kWavesPerBlock, 0,
+                          as_stream(stream)>>>(side, side_bstride, side_sstride, attn, grad_hidden,
+                                               batch, n_side, dim, grad_side, grad_weight_logits);
+  } else {
+    RS_CHECK_ARG(dense, "rs_side_pool_bwd: strided side rows need dim % 4 == 0, dim <= 128");
+    pool_bwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
+        side, attn, grad_hidden, batch, n_side, dim, grad_side, grad_weight_logits);
+  }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_side_pool_fwd(const float* side, const float* weight_logits, int64_t batch,
+                                    int32_t n_side, int32_t dim, float* hidden, float* attn,
+                                    void* stream) {
+  return rs_side_pool_fwd_strided(side, (int64_t)n_side * dim, dim, weight_logits, batch, n_side,
+                                  dim, hidden, attn, stream);
 }
 
 extern "C" int32_t rs_side_pool_bwd(const float* side, const float* attn, const float* grad_hidden,
                                     int64_t batch, int32_t n_side, int32_t dim, float* grad_side,
                                     float* grad_weight_logits, void* stream) {
-  RS_CHECK_ARG(n_side >= 1 && n_side <= kMaxSide && dim >= 1 && batch >= 0,
-               "rs_side_pool_bwd: need 1 <= n_side <= %d", kMaxSide);
-  if (batch == 0) return RS_OK;
-  pool_bwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
-      side, attn, grad_hidden, batch, n_side, dim, grad_side, grad_weight_logits);
-  RS_CHECK_LAUNCH();
-  return RS_OK;
+  return rs_side_pool_bwd_strided(side, (int64_t)n_side * dim, dim, attn, grad_hidden, batch,
+                                  n_side, dim, grad_side, grad_weight_logits, stream);
 }
 
 extern "C" int32_t rs_eges_walks(const int64_t* indptr, const int32_t* indices, const double* cumw,

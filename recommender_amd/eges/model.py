@@ -58,11 +58,22 @@ def match_logits(table: Embedding, match: torch.Tensor, hidden: torch.Tensor) ->
     return _MatchLogits.apply(hidden, table.grad_handle, table, match)
 
 
+def _pool_layout_ok(side):
+    """side [B, S, D] read in place: contiguous, or rows of D = 4k <= 128 contiguous floats at
+    16-byte aligned strides (e.g. MMOE's [E, B, H] expert outputs seen as [B, E, H])."""
+    if side.is_contiguous():
+        return True
+    B, S, D = side.shape
+    return (side.stride(2) == 1 and D % 4 == 0 and D <= 128 and side.stride(0) % 4 == 0
+            and side.stride(1) % 4 == 0 and side.data_ptr() % 16 == 0)
+
+
 class _SidePool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, side, wlogits):
         L.require_device(side, "side")
-        side = side.contiguous()
+        if not _pool_layout_ok(side):
+            side = side.contiguous()
         B, S, D = side.shape
         hidden = torch.empty(B, D, device=side.device)
         attn = None
@@ -70,8 +81,8 @@ class _SidePool(torch.autograd.Function):
         if wlogits is not None:
             wl = wlogits.reshape(B, S).contiguous()
             attn = torch.empty(B, S, device=side.device)
-        L.call("rs_side_pool_fwd", L.ptr(side), L.ptr(wl), B, S, D, L.ptr(hidden), L.ptr(attn),
-               L.stream_ptr(side.device))
+        L.call("rs_side_pool_fwd_strided", L.ptr(side), side.stride(0), side.stride(1), L.ptr(wl),
+               B, S, D, L.ptr(hidden), L.ptr(attn), L.stream_ptr(side.device))
         ctx.has_w = wlogits is not None
         ctx.wshape = None if wlogits is None else wlogits.shape
         ctx.save_for_backward(side, attn)
@@ -82,10 +93,12 @@ class _SidePool(torch.autograd.Function):
         side, attn = ctx.saved_tensors
         B, S, D = side.shape
         g = g.reshape(B, D).contiguous()
-        gs = torch.empty_like(side)
+        gs = torch.empty_like(side)  # the side's layout (preserve_format keeps the permutation)
+        if gs.stride() != side.stride():
+            raise RuntimeError("side pool: gradient layout differs from the side rows'")
         gw = torch.empty(B, S, device=side.device) if ctx.has_w else None
-        L.call("rs_side_pool_bwd", L.ptr(side), L.ptr(attn), L.ptr(g), B, S, D, L.ptr(gs),
-               L.ptr(gw), L.stream_ptr(side.device))
+        L.call("rs_side_pool_bwd_strided", L.ptr(side), side.stride(0), side.stride(1),
+               L.ptr(attn), L.ptr(g), B, S, D, L.ptr(gs), L.ptr(gw), L.stream_ptr(side.device))
         return gs, (gw.reshape(ctx.wshape) if gw is not None else None)
 
 

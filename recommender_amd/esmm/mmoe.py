@@ -54,7 +54,9 @@ class MMOE(nn.Module):
         return h.transpose(0, 1)                                     # [B, E, H]
 
     def _towers(self, x):
-        ex = self.experts_outputs(x).contiguous()                     # [B, E, H]
+        # [B, E, H] seen over the [E, B, H] expert outputs: rs_side_pool reads (and writes the
+        # gradient of) that layout in place, no transpose pass either way
+        ex = self.experts_outputs(x)
         outs = []
         for i in range(self.num_tasks):
             # softmax gate (Dense(E, softmax)) · experts, fused: rs_side_pool applies the

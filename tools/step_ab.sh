@@ -10,19 +10,20 @@ run() {  # name, env..., -- bench args
   python - "$name" <<'PY'
 import json, sys
 d = json.loads(open(f"gpurun_out/stepab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
-k = d["kernels"]
-print(f"{sys.argv[1]:14s} ms/step {d['ms_per_step']:.4f} median {d['step_ms_distribution']['median']} "
-      f"p10 {d['step_ms_distribution']['p10']} | " +
+k = d.get("kernels") or {}
+dist = d.get("step_ms_distribution") or {}
+print(f"{sys.argv[1]:14s} ms/step {d['ms_per_step']:.4f} median {dist.get('median')} "
+      f"p10 {dist.get('p10')} | " +
       " ".join(f"{n.replace('rs_', '')[:18]} {v['avg_us']}" for n, v in k.items()))
 PY
 }
 for rep in ${REPS:-1 2}; do
-  for v in ${VARIANTS:-base mainapply}; do
+  for v in ${VARIANTS:-base afterfold}; do
     case $v in
-      base) run base RS_MAIN_APPLY=0 -- --prefetch 0 || exit 1 ;;
-      mainapply) run mainapply RS_MAIN_APPLY=1 -- --prefetch 1 || exit 1 ;;
-      mainapply_graph2) run mainapply_g2 RS_MAIN_APPLY=1 -- --prefetch 1 --graph 2 || exit 1 ;;
-      graph2) run graph2 RS_MAIN_APPLY=0 -- --prefetch 0 --graph 2 || exit 1 ;;
+      base) run base X=1 -- || exit 1 ;;
+      afterfold) run afterfold RS_APPLY_AFTER_KERNEL=0 -- || exit 1 ;;
+      graph2) run graph2 X=1 -- --graph 2 || exit 1 ;;
+      graph2_afterfold) run graph2_af RS_APPLY_AFTER_KERNEL=0 -- --graph 2 || exit 1 ;;
     esac
   done
 done
