@@ -133,16 +133,16 @@ def bwgrad(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _act_bwd(g, y, act, want_db):
+def _act_bwd(g, y, act, want_db, dz=None, db=None):
     """(dz = act'(y)⊙g, Σ_rows dz or None) for act 0 / 1 (relu) / 2 (sigmoid) on [R, N] rows
-    (rs_act_bwd_colsum: one pass for both)."""
+    (rs_act_bwd_colsum: one pass for both); dz / db: optional contiguous outputs to write."""
     from . import _lib as L
 
     if act == 0:
         return g, (g.sum(0) if want_db else None)
     R, N = g.shape
-    dz = torch.empty_like(g)
-    db = torch.empty(N, device=g.device, dtype=torch.float32)
+    dz = torch.empty_like(g) if dz is None else dz
+    db = torch.empty(N, device=g.device, dtype=torch.float32) if db is None else db
     ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(R, N) // 4), device=g.device)
     L.call("rs_act_bwd_colsum", L.ptr(g), L.ptr(y), R, N, act, L.ptr(dz), L.ptr(db), L.ptr(ws),
            ws.numel() * 4, L.stream_ptr(g.device))
@@ -202,10 +202,12 @@ class _BatchedLinearFn(torch.autograd.Function):
         g = g.contiguous()
         E = g.shape[0]
         if ctx.act:
-            # per expert: the mask and its bias-gradient column sums in one pass each
-            parts = [_act_bwd(g[e], y[e], ctx.act, True) for e in range(E)]
-            dz = torch.stack([p[0] for p in parts])
-            db = torch.stack([p[1] for p in parts]).unsqueeze(1)
+            # per expert: the mask and its bias-gradient column sums in one pass each, written in
+            # place into the batched gradients
+            dz = torch.empty_like(g)
+            db = torch.empty(E, 1, g.shape[2], device=g.device, dtype=torch.float32)
+            for e in range(E):
+                _act_bwd(g[e], y[e], ctx.act, True, dz=dz[e], db=db[e, 0])
         else:
             dz, db = g, g.sum(1, keepdim=True)
         dx = torch.bmm(dz, k.transpose(1, 2)) if ctx.needs_input_grad[0] else None

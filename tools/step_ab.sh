@@ -18,12 +18,12 @@ print(f"{sys.argv[1]:14s} ms/step {d['ms_per_step']:.4f} median {dist.get('media
 PY
 }
 for rep in ${REPS:-1 2}; do
-  for v in ${VARIANTS:-base afterfold}; do
+  for v in ${VARIANTS:-base graph2}; do
     case $v in
       base) run base X=1 -- || exit 1 ;;
-      afterfold) run afterfold RS_APPLY_AFTER_KERNEL=0 -- || exit 1 ;;
       graph2) run graph2 X=1 -- --graph 2 || exit 1 ;;
-      graph2_afterfold) run graph2_af RS_APPLY_AFTER_KERNEL=0 -- --graph 2 || exit 1 ;;
+      prefetch) run prefetch X=1 -- --prefetch 1 || exit 1 ;;
+      waitsort) run waitsort RS_TRAIN_WAITS_SORT=1 -- || exit 1 ;;
     esac
   done
 done
