@@ -43,6 +43,9 @@ def get_activation(act):
 # keeps the library default.
 _GEMM_X3 = __import__("os").environ.get("RS_GEMM_X3", "0") == "1"
 _X3_MIN_N, _X3_MIN_K = 128, 160
+# relu layers: hipBLASLt's bias + relu epilogue (torch._addmm_activation) instead of a separate
+# in-place relu pass; RS_RELU_EPILOGUE=0 restores the pass
+_RELU_EPILOGUE = __import__("os").environ.get("RS_RELU_EPILOGUE", "1") == "1"
 
 
 def _x3_ready(*ts, n=0, k=0, batched=False):
@@ -77,6 +80,8 @@ def _affine(x, k, b, act):
     layer-by-layer evaluation goes through here, so they stay bit-identical to each other."""
     if _x3_ready(x, k, n=k.shape[1], k=k.shape[0]) and (b is None or b.is_contiguous()):
         return gemm_x3(x, k, bias=b, act=act)
+    if act == 1 and b is not None and _RELU_EPILOGUE and x.is_cuda:
+        return torch._addmm_activation(b, x, k)  # relu in the library GEMM's epilogue
     z = torch.addmm(b, x, k) if b is not None else x @ k
     if act == 1:
         return torch.relu_(z)
