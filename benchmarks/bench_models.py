@@ -60,6 +60,9 @@ def main():
                          "capacity-shaped sync-free batches, eager (static_step); graph = the same "
                          "step captured once and replayed (PinSageStep.capture), sampling eager; "
                          "graph_all = sampling inside the graph too (capture_with_sampling)")
+    ap.add_argument("--deepfm-mode", default="graph", choices=["eager", "graph"],
+                    help="deepfm: graph = the Keras-Adam step captured once as a HIP graph and replayed "
+                         "(TrainStep.capture_static); eager: TrainStep.__call__")
     ap.add_argument("--dien-mode", default="graph", choices=["eager", "graph"],
                     help="dien: eager = DIENStep.__call__; graph = static_step captured once and "
                          "replayed (DIENStep.capture)")
@@ -256,9 +259,25 @@ def main():
             cat, dn, lb = criteo_batch(rng, B, [1_000_000] * 26)
             batches.append(((torch.from_numpy(cat).to(dev), torch.from_numpy(dn).to(dev), torch.from_numpy(lb).to(dev)),))
         step = step0
+        if args.deepfm_mode == "graph":
+            # the launch-bound B = 1024 step as one HIP graph (TrainStep.capture_static), replayed
+            # on static input buffers refilled per batch
+            static = tuple(torch.empty_like(t) for t in batches[0][0])
+            fctr = {"n": 0, "replay": None}
+
+            def step(b):
+                for d, s_ in zip(static, b):
+                    d.copy_(s_)
+                fctr["n"] += 1
+                if fctr["n"] == 1:
+                    return step0.static_step(static)
+                if fctr["replay"] is None:
+                    fctr["replay"] = step0.capture_static(static)
+                return fctr["replay"]()
         watch = ["rs_embedding_fwd", "rs_fm_fwd", "rs_fm_bwd", "rs_sort_ids", "rs_embedding_apply",
                  "rs_keras_adam_dense_sweep"]
-        cfg = {"workload": "deepfm_criteo_1M_b1024_d16", "batch": B, "optimizer": "keras_adam"}
+        cfg = {"workload": "deepfm_criteo_1M_b1024_d16", "batch": B, "optimizer": "keras_adam",
+               "mode": args.deepfm_mode}
     sec, k = run(step, batches, args.steps, args.warmup, watch)
     if args.model == "dlrm_cfg2" and args.cfg2_graph == 2 and args.optimizer == "sgd":
         sec /= B_pool  # one replay = the whole pool of steps
@@ -314,9 +333,25 @@ def deepfm_from_file(args):
           and torch.equal(feats["int_features"].cpu(), torch.from_numpy(dn))
           and torch.equal(label.cpu(), torch.from_numpy(lb.astype(np.int64))))
     m = build_model("DeepFM", 16, V, 26, 13, dev)
-    step = TrainStep(m, "keras_adam", fused=False)
+    train = TrainStep(m, "keras_adam", fused=False)
     g = torch.Generator(device=dev).manual_seed(4)
     n_steps = n // B
+    first = (feats["cat_features"][:B], feats["int_features"][:B], label[:B].float())
+    if args.deepfm_mode == "graph":
+        # the step captured once as a HIP graph (TrainStep.capture_static) and replayed on static
+        # buffers refilled from each batch of the file
+        static = tuple(torch.empty_like(t) for t in first)
+        for d, s_ in zip(static, first):
+            d.copy_(s_)
+        train.static_step(static)
+        replay = train.capture_static(static)
+
+        def step(b):
+            for d, s_ in zip(static, b):
+                d.copy_(s_)
+            return replay()
+    else:
+        step = train
     # warm-up on the first batches (library handles, workspaces), not counted in the epoch
     for i in range(3):
         step((feats["cat_features"][i * B:(i + 1) * B], feats["int_features"][i * B:(i + 1) * B],
@@ -334,7 +369,7 @@ def deepfm_from_file(args):
     t_epoch = time.perf_counter() - t0
     out = {"model": "deepfm_file", "config": {"workload": f"deepfm_criteo_tfrecord_{n}_b{B}_d16",
                                                 "rows": n, "batch": B, "optimizer": "keras_adam",
-                                                "file_bytes": size},
+                                                "file_bytes": size, "mode": args.deepfm_mode},
            "examples_per_sec": round(n_steps * B / t_epoch, 1),
            "ms_per_step": round(t_epoch / n_steps * 1e3, 3),
            "examples_per_sec_incl_read": round(n_steps * B / (t_epoch + t_read), 1),

@@ -22,6 +22,7 @@ import time
 import numpy as np
 import torch
 
+from .. import _lib as L
 from ..functional import binary_crossentropy
 from ..nn import invalidate_compose_cache, overlapped_param_grads, overlapped_weight_grads
 from ..metrics import AUC
@@ -161,6 +162,70 @@ class TrainStep:
             invalidate_compose_cache()
             return loss
 
+        return replay
+
+    # -- graph-capturable Keras-Adam step (non-fused tables: DeepFM, cfg1) -------------------
+    def static_step(self, batch):
+        """One Keras-Adam step with no host-side per-step scalars, so it can sit in a HIP graph
+        (as DIENStep.static_step): the table's IndexedSlices gradient densified (densify_grad:
+        the sort + tiled segmented sum of the sparse apply, no sync) into the flat gradient buffer
+        and Keras Adam over every variable with lr_t from device memory (GraphKerasAdam). Keras'
+        sparse Adam decays m / v and moves every row each step anyway, so this dense step is the
+        same update as __call__'s sparse apply + dense sweep (tests/test_deepfm_gpu.py: bit for
+        bit). Its Adam state is its own: do not interleave with __call__."""
+        from ..optim import GraphKerasAdam, _Workspace, densify_grad
+
+        if (not isinstance(self.opt_sparse, SparseAdam) or self.opt_sparse.kind != L.RS_OPT_KERAS_ADAM
+                or self.opt_sparse.fused or self.sharded):
+            raise RuntimeError("static_step: Keras Adam on non-fused, unsharded tables only")
+        tables = list(self.opt_sparse.tables)
+        if getattr(self, "opt_graph", None) is None:
+            tw = {id(t.weight) for t in tables}
+            self._gdense = [p for p in self.dense if id(p) not in tw and p.numel() > 0]
+            self.opt_graph = GraphKerasAdam(self._gdense + [t.weight for t in tables],
+                                            lr=self.opt_dense.param_groups[0]["lr"])
+            self._gws = _Workspace()
+            self.opt_sparse.release_state()  # the graph path's Adam state is opt_graph's
+        for p in self._gdense:
+            p.grad = None
+        cat, dense_x, label = batch
+        pred = self.model({"cat_features": cat, "int_features": dense_x})
+        self.last_pred = pred.detach()
+        loss = binary_crossentropy(label, pred, reduction=self.loss_reduction)
+        loss.backward()
+        grads = [p.grad for p in self._gdense]  # None: Keras skips the variable
+        nd = len(self._gdense)
+        for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
+            got = t.take_grad(with_valid=True)
+            grads.append(densify_grad(t, got[0], got[1], self._gws, valid=got[2],
+                                      out=self.opt_graph.grad_view(nd + i))
+                         if got is not None else None)
+        if not torch.cuda.is_current_stream_capturing():
+            self.opt_graph.prepare()
+            self.opt_graph.iterations += 1
+        self.opt_graph.apply(grads)
+        return loss.detach()
+
+    def capture_static(self, batch):
+        """Record one static_step on `batch` (static device tensors the caller refills before
+        each replay) into a HIP graph; returns replay() -> loss. Run one eager static_step first
+        (it builds the optimizer state the graph reads)."""
+        opt = self.opt_graph
+        opt.prepare()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        invalidate_compose_cache()  # the graph must record the compositions it reads
+        with torch.cuda.graph(g):
+            out = self.static_step(batch)
+        invalidate_compose_cache()
+        self._static_graph = g
+
+        def replay():
+            opt.prepare()
+            g.replay()
+            opt.iterations += 1
+            invalidate_compose_cache()  # the replay moved the parameters in place
+            return out
         return replay
 
     def prefetch(self, batch):
