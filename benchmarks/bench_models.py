@@ -69,9 +69,10 @@ def main():
     ap.add_argument("--eges-mode", default="graph", choices=["eager", "graph"],
                     help="eges: eager = EGESStep.__call__ (SparseAdam keras); graph = static_step "
                          "captured once and replayed (EGESStep.capture)")
-    ap.add_argument("--cfg2-graph", type=int, default=0,
-                    help="dlrm_cfg2 (sgd): 1 = each step a HIP-graph replay (TrainStep.capture); "
-                         "2 = the 4-batch pool as one graph (TrainStep.capture_sequence, updates "
+    ap.add_argument("--cfg2-graph", type=int, default=2,
+                    help="dlrm_cfg2 (sgd): 0 = eager steps; 1 = each step a HIP-graph replay "
+                         "(TrainStep.capture); 2 (default, as the other launch-bound configs) = "
+                         "the 4-batch pool as one graph (TrainStep.capture_sequence, updates "
                          "overlapped across steps), timed per step")
     ap.add_argument("--tuned-gemms", type=int, default=-1,
                     help="1: replay the committed TunableOp GEMM choices (recommender_amd/gemm_tuning.py); "
