@@ -107,9 +107,8 @@ def main():
             train_d = step
 
             def step(f, lab):
-                for k, v in f.items():
-                    st_f[k].copy_(v)
-                st_l.copy_(lab)
+                # the feed's refill of the static buffers: one multi-tensor copy
+                torch._foreach_copy_([st_f[k] for k in f] + [st_l], list(f.values()) + [lab])
                 dctr["n"] += 1
                 if dctr["n"] == 1:
                     return train_d.static_step(st_f, st_l)
@@ -191,9 +190,7 @@ def main():
             gctr = {"n": 0, "replay": None}
 
             def step(inp, lab):
-                for d_, s_ in zip(st_in, inp):
-                    d_.copy_(s_)
-                st_lab.copy_(lab)
+                torch._foreach_copy_(list(st_in) + [st_lab], list(inp) + [lab])
                 gctr["n"] += 1
                 if gctr["n"] == 1:
                     return train.static_step(st_in, st_lab)
@@ -267,8 +264,7 @@ def main():
             fctr = {"n": 0, "replay": None}
 
             def step(b):
-                for d, s_ in zip(static, b):
-                    d.copy_(s_)
+                torch._foreach_copy_(list(static), list(b))
                 fctr["n"] += 1
                 if fctr["n"] == 1:
                     return step0.static_step(static)
@@ -348,8 +344,7 @@ def deepfm_from_file(args):
         replay = train.capture_static(static)
 
         def step(b):
-            for d, s_ in zip(static, b):
-                d.copy_(s_)
+            torch._foreach_copy_(list(static), list(b))
             return replay()
     else:
         step = train

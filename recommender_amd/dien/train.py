@@ -174,9 +174,8 @@ def main(argv=None):
                 # the optimizer state), the second captures the graph that later steps replay
                 if static is None:
                     static = ({k: torch.empty_like(v) for k, v in feats.items()}, torch.empty_like(label))
-                for k, v in feats.items():
-                    static[0][k].copy_(v)
-                static[1].copy_(label)
+                torch._foreach_copy_([static[0][k] for k in feats] + [static[1]],
+                                     list(feats.values()) + [label])
                 if getattr(step, "opt_graph", None) is None:
                     out = step.static_step(*static)
                 else:

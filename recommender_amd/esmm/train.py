@@ -77,8 +77,7 @@ class MultiTaskStep:
         flat = torch._utils._flatten_dense_tensors(grads)
         self.comm.all_reduce_(flat)
         flat.mul_(1.0 / self.comm.world)
-        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-            g.copy_(f)
+        torch._foreach_copy_(grads, list(torch._utils._unflatten_dense_tensors(flat, grads)))
 
 
 def train(argv=None):

@@ -476,6 +476,22 @@ class GraphKerasAdam:
         return self.grad_flat[o:o + n].view_as(self.params[i])
 
     @torch.no_grad()
+    def collect(self, grads):
+        """Copy the given gradients (None skipped) into their views of grad_flat, those not
+        already written there, in one multi-tensor copy: one launch where per-tensor copies were
+        one ~4 us memcpy node each (~25 per DIEN step)."""
+        dsts, srcs = [], []
+        for i, g in enumerate(grads):
+            if g is None:
+                continue
+            dst = self.grad_view(i)
+            if g.data_ptr() != dst.data_ptr():
+                dsts.append(dst)
+                srcs.append(g.reshape(dst.shape))
+        if dsts:
+            torch._foreach_copy_(dsts, srcs)
+
+    @torch.no_grad()
     def apply(self, grads):
         """One Keras Adam step of every tensor with `grads` (same order); graph-capturable.
         A None gradient skips its tensor, as Keras' apply_gradients skips a variable without a
@@ -493,11 +509,8 @@ class GraphKerasAdam:
                 cur = [i, i]
                 runs.append(cur)
             cur[1] = i
+        self.collect(grads)
         for a, b in runs:
-            for i in range(a, b + 1):
-                dst = self.grad_view(i)
-                if grads[i].data_ptr() != dst.data_ptr():
-                    dst.copy_(grads[i].reshape(dst.shape))
             o = self._segs[a][0]
             ob, nb, pb = self._segs[b]
             n = ob + nb + pb - o

@@ -119,10 +119,7 @@ class PinSageStep:
                 raise ValueError("sharded static_step: a parameter has no gradient on this rank; "
                                  "the all-reduce needs the same flat layout on every rank")
             opt = self.opt_graph
-            for i, g in enumerate(grads):
-                dst = opt.grad_view(i)
-                if g.data_ptr() != dst.data_ptr():
-                    dst.copy_(g.reshape(dst.shape))
+            opt.collect(grads)
             self.comm.all_reduce_(opt.grad_flat)
             opt.grad_flat.mul_(1.0 / self.world)
             grads = [opt.grad_view(i) for i in range(len(grads))]
