@@ -183,6 +183,19 @@ int32_t rs_embedding_grad_dense(const uint32_t* sorted_rows, const int32_t* sort
                                 int64_t n_ids, const float* grad_out, int32_t dim, int64_t n_rows,
                                 float* dense, void* workspace, size_t ws_bytes, void* stream);
 
+/* rs_embedding_grad_dense with the gradient rows in n_segs (1..4) host-listed segments instead of
+ * one [n_ids, dim] array: position p of segment i (seg_n[i] rows, p counted from the segment's
+ * start) is the row at seg_ptrs[i] + p * seg_ld[i] (seg_ld >= dim, e.g. a column block of a
+ * wider row). Σ seg_n = n_ids; same additions in the same order as over the concatenation. The
+ * host arrays are read during the call. (A table looked up several times in one step — DIEN's
+ * item table: target, positive and negative histories — without a concatenation pass; replaces
+ * the concat of the IndexedSlices parts Keras does in tf.IndexedSlices aggregation.) */
+int32_t rs_embedding_grad_dense_segs(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                     int64_t n_ids, int32_t n_segs, const float* const* seg_ptrs,
+                                     const int64_t* seg_n, const int64_t* seg_ld, int32_t dim,
+                                     int64_t n_rows, float* dense, void* workspace,
+                                     size_t ws_bytes, void* stream);
+
 /* Dense gradient of a small table, no sort: grad_dense [n_rows, dim] = Σ over entries n with
  * ids[n] = v of grad_rows[n, :] (Keras' IndexedSlices gradient densified for a dense Adam step,
  * pinsage/train/train.py:45-46 on the year / genre tables, layers.py:63-75). Fixed summation
@@ -463,8 +476,12 @@ int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const float* neg,
                         const float* W3, const float* b3, const float* daux, float* dhidden,
                         float* dpos, float* dneg, float* dparams, void* workspace,
                         size_t ws_bytes, void* stream);
-/* rs_dien_aux_bwd with acc_hidden = 1: dhidden holds the hidden states' upstream gradient (the
- * attention's + the AUGRU's) and the aux loss's part is added in place (no fill, no add pass). */
+/* rs_dien_aux_bwd with acc_hidden bit 0 set: dhidden holds the hidden states' upstream gradient
+ * (the attention's + the AUGRU's) and the aux loss's part is added in place (no fill, no add
+ * pass). Bit 1 set: the caller discards the input gradients at masked history steps (its pos /
+ * neg lookups carry the mask as their gradient mask): dpos / dneg are written at every step
+ * that can carry gradient (step 0 zeroed, steps t + 1 of the tiles holding a valid step) and
+ * left unwritten at the masked steps of the other tiles — no zero fill of the whole arrays. */
 int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, const float* neg,
                             const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                             const float* W1, const float* b1, const float* W2, const float* b2,
@@ -491,6 +508,31 @@ int32_t rs_bce_bwd(const float* p, const float* y, int64_t n, float eps, int32_t
 size_t rs_act_bwd_colsum_workspace_size(int64_t B, int32_t N);
 int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N, int32_t act,
                           float* dz, float* db, void* workspace, size_t ws_bytes, void* stream);
+/* The same on row-strided operands (ld_* >= N elements between rows): a column block of a
+ * wider [B, ld] activation — the two ESMM towers' first layers evaluated as one GEMM over the
+ * shared input (esmm/esmm.py:27-28), each tower's block masked from its own gradient. */
+int32_t rs_act_bwd_colsum_ld(const float* dy, int64_t ld_dy, const float* y, int64_t ld_y,
+                             int64_t B, int32_t N, int32_t act, float* dz, int64_t ld_dz, float* db,
+                             void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * keras.layers.BatchNormalization on [B, C] rows (the DIEN / DIN / BASE MLP head's input,
+ * dien/layers.py:20-31). training = 1: batch mean and population variance (tf.nn.moments),
+ * y = ((x - mean)·rsqrt(var + epsilon))·gamma + beta, moving statistics updated in place by
+ * Keras' m -= (m - value)·(1 - momentum); training = 0: the moving statistics, none updated.
+ * save_mean / save_invstd [C] (the statistics used) feed the backward: dbeta = Σ dy,
+ * dgamma = Σ dy·x̂, dx = gamma·r·(dy - dbeta/B - x̂·dgamma/B) (training) or gamma·r·dy.
+ * Deterministic (fixed 64-row chunks merged in order). workspace >= rs_batch_norm_workspace_size
+ * (unused by an inference forward). */
+size_t rs_batch_norm_workspace_size(int64_t B, int32_t C);
+int32_t rs_batch_norm_fwd(const float* x, int64_t B, int32_t C, const float* gamma,
+                          const float* beta, float epsilon, float momentum, int32_t training,
+                          float* moving_mean, float* moving_var, float* y, float* save_mean,
+                          float* save_invstd, void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_batch_norm_bwd(const float* dy, const float* x, int64_t B, int32_t C,
+                          const float* save_mean, const float* save_invstd, const float* gamma,
+                          int32_t training, float* dx, float* dgamma, float* dbeta,
+                          void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * PinSage sampling + aggregation. The graph is the bipartite
@@ -654,6 +696,24 @@ int32_t rs_side_pool_bwd_strided(const float* side, int64_t side_bstride, int64_
                                  const float* attn, const float* grad_hidden, int64_t batch,
                                  int32_t n_side, int32_t dim, float* grad_side,
                                  float* grad_weight_logits, void* stream);
+/* n_tasks (1..4) softmax poolings of the same side rows (MMOE: one gate per task over the same
+ * expert outputs, esmm/mmoe.py:36-46), the side rows read once: hidden[t] [batch, dim] =
+ * Σ_s softmax(weight_logits[t][b, :])[s] · side[b, s, :], attn[t] [batch, n_side] the weights
+ * (logits rows logits_ld apart). Per task the same arithmetic as rs_side_pool_fwd. Side rows as
+ * rs_side_pool_fwd_strided (16-byte aligned, dim % 4 == 0, dim <= 128). The task arrays are host
+ * arrays read during the call. */
+int32_t rs_side_pool_fwd_multi(const float* side, int64_t side_bstride, int64_t side_sstride,
+                               int64_t batch, int32_t n_side, int32_t dim, int32_t n_tasks,
+                               const float* const* weight_logits, int64_t logits_ld,
+                               float* const* hidden, float* const* attn, void* stream);
+/* Backward of rs_side_pool_fwd_multi: grad_side = Σ_t attn[t][s] · grad_hidden[t] (task order,
+ * each product rounded: the sum of n_tasks rs_side_pool_bwd results), grad_logits[t] as
+ * rs_side_pool_bwd's (rows grad_logits_ld apart). One pass over the side rows. */
+int32_t rs_side_pool_bwd_multi(const float* side, int64_t side_bstride, int64_t side_sstride,
+                               int64_t batch, int32_t n_side, int32_t dim, int32_t n_tasks,
+                               const float* const* attn, const float* const* grad_hidden,
+                               float* grad_side, float* const* grad_logits,
+                               int64_t grad_logits_ld, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Factored linear-chain backward of a ctr MLP (hidden Dense layers linear, ctr/layers.py:8):

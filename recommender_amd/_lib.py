@@ -74,6 +74,8 @@ _SIGS = {
     "rs_exchange_pack": (_i32, [_p, _p, _p, _i32, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p]),
     "rs_gather_rows_padded": (_i32, [_p, _i64, _i32, _p, _i64, _p, _p]),
     "rs_embedding_grad_dense": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _sz, _p]),
+    "rs_embedding_grad_dense_segs": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _i64, _p, _p,
+                                            _sz, _p]),
     "rs_apply_workspace_size": (_sz, [_i64, _i32]),
     "rs_embedding_apply": (_i32, [_i32, _p, _p, _p, _i64, _i32, _p, _p, _i64, _p,
                                   C.POINTER(AdamParams), _p, _p, _sz, _p]),
@@ -120,7 +122,13 @@ _SIGS = {
     "rs_dien_aux_bwd_acc": (_i32, [_p, _p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_act_bwd_colsum_workspace_size": (_sz, [_i64, _i32]),
+    "rs_batch_norm_workspace_size": (_sz, [_i64, _i32]),
+    "rs_batch_norm_fwd": (_i32, [_p, _i64, _i32, _p, _p, C.c_float, C.c_float, _i32, _p, _p,
+                                 _p, _p, _p, _p, _sz, _p]),
+    "rs_batch_norm_bwd": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_act_bwd_colsum": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
+    "rs_act_bwd_colsum_ld": (_i32, [_p, _i64, _p, _i64, _i64, _i32, _i32, _p, _i64, _p, _p,
+                                    _sz, _p]),
     "rs_philox4x32_10": (_i32, [_p, _i64, _u32, _u32, _p, _p]),
     "rs_metapath_walk": (_i32, [_p, _p, _p, _p, _p, _i64, _i32, _i32, C.c_float, _u64, _u32,
                                 _u32, _p, _p]),
@@ -150,6 +158,10 @@ _SIGS = {
     "rs_match_logits_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p, _p]),
     "rs_side_pool_fwd_strided": (_i32, [_p, _i64, _i64, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd_strided": (_i32, [_p, _i64, _i64, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_side_pool_fwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _i64, _p, _p,
+                                      _p]),
+    "rs_side_pool_bwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p,
+                                      _i64, _p]),
     "rs_side_pool_fwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd": (_i32, [_p, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_auc_update": (_i32, [_p, _p, _i64, _p, _i32, _p, _p, _p]),

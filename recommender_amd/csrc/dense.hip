@@ -16,7 +16,9 @@ template <int ACT, int VEC>
 __global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const float* __restrict__ dy,
                                                              const float* __restrict__ y, int64_t B,
                                                              int N, float* __restrict__ dz,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part,
+                                                             int64_t ldg, int64_t ldy,
+                                                             int64_t ldz) {
   __shared__ float red[16][16 * VEC + 1];
   const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int col0 = (blockIdx.x * 16 + cl) * VEC;
@@ -28,18 +30,18 @@ __global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const float* __rest
   if (col0 < N) {
 #pragma unroll 4
     for (int64_t r = r0 + rl; r < r1; r += 16) {
-      const int64_t o = r * N + col0;
+      const int64_t og = r * ldg + col0, oy = r * ldy + col0, o = r * ldz + col0;
       float g[VEC], yy[VEC];
       if constexpr (VEC == 4) {
-        float4 t = *reinterpret_cast<const float4*>(dy + o);
+        float4 t = *reinterpret_cast<const float4*>(dy + og);
         g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
         if constexpr (ACT != 0) {
-          float4 u = *reinterpret_cast<const float4*>(y + o);
+          float4 u = *reinterpret_cast<const float4*>(y + oy);
           yy[0] = u.x; yy[1] = u.y; yy[2] = u.z; yy[3] = u.w;
         }
       } else {
-        g[0] = dy[o];
-        if constexpr (ACT != 0) yy[0] = y[o];
+        g[0] = dy[og];
+        if constexpr (ACT != 0) yy[0] = y[oy];
       }
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
@@ -932,11 +934,13 @@ extern "C" size_t rs_act_bwd_colsum_workspace_size(int64_t B, int32_t N) {
   return (size_t)ceil_div(B, kColRows) * N * sizeof(float);
 }
 
-extern "C" int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N,
-                                     int32_t act, float* dz, float* db, void* workspace,
-                                     size_t ws_bytes, void* stream) {
+extern "C" int32_t rs_act_bwd_colsum_ld(const float* dy, int64_t ld_dy, const float* y,
+                                        int64_t ld_y, int64_t B, int32_t N, int32_t act, float* dz,
+                                        int64_t ld_dz, float* db, void* workspace, size_t ws_bytes,
+                                        void* stream) {
   RS_CHECK_ARG(B >= 0 && N >= 1 && act >= 0 && act <= 2, "bad arguments");
   RS_CHECK_ARG(act == 0 || (y && dz), "activation backward needs y and dz");
+  RS_CHECK_ARG(ld_dy >= N && (act == 0 || (ld_y >= N && ld_dz >= N)), "row strides must be >= N");
   RS_CHECK_ARG(ws_bytes >= rs_act_bwd_colsum_workspace_size(B, N), "workspace too small");
   hipStream_t st = as_stream(stream);
   if (B == 0) {
@@ -945,28 +949,36 @@ extern "C" int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B,
   }
   const int nchunks = (int)ceil_div(B, kColRows);
   float* part = static_cast<float*>(workspace);
-  const bool v4 = N % 4 == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0 &&
-                  (!y || (reinterpret_cast<uintptr_t>(y) & 15) == 0) &&
-                  (!dz || (reinterpret_cast<uintptr_t>(dz) & 15) == 0);
+  auto al16 = [](const void* p, int64_t ld) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
+  };
+  const bool v4 = N % 4 == 0 && al16(dy, ld_dy) && (act == 0 || (al16(y, ld_y) && al16(dz, ld_dz)));
+  if (act == 0) ld_y = ld_dz = N;  // y / dz unread
   if (v4) {
     dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nchunks);
     switch (act) {
-      case 0: act_bwd_colsum_kernel<0, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
-      case 1: act_bwd_colsum_kernel<1, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
-      default: act_bwd_colsum_kernel<2, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
+      case 0: act_bwd_colsum_kernel<0, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
+      case 1: act_bwd_colsum_kernel<1, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
+      default: act_bwd_colsum_kernel<2, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
     }
   } else {
     dim3 grid((unsigned)ceil_div(N, 16), (unsigned)nchunks);
     switch (act) {
-      case 0: act_bwd_colsum_kernel<0, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
-      case 1: act_bwd_colsum_kernel<1, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
-      default: act_bwd_colsum_kernel<2, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part); break;
+      case 0: act_bwd_colsum_kernel<0, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
+      case 1: act_bwd_colsum_kernel<1, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
+      default: act_bwd_colsum_kernel<2, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, ld_dy, ld_y, ld_dz); break;
     }
   }
   RS_CHECK_LAUNCH();
   fold_chunks_kernel<<<(unsigned)ceil_div(N, 64), 256, 0, st>>>(part, nchunks, N, db);
   RS_CHECK_LAUNCH();
   return RS_OK;
+}
+
+extern "C" int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N,
+                                     int32_t act, float* dz, float* db, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  return rs_act_bwd_colsum_ld(dy, N, y, N, B, N, act, dz, N, db, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t rs_chain_reduce_workspace_size(int64_t B, int32_t n0, int32_t nl) {

@@ -230,6 +230,95 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_bwd_vec_kernel(
     for (int s = 0; s < S; ++s) grad_w[b * S + s] = a[s] * (ga[s] - dot);
 }
 
+// ---- several softmax poolings of the same side rows (MMOE: one gate per task over the same
+// expert outputs, esmm/mmoe.py:36-46) ---------------------------------------------------------
+// The side rows are read once for all T tasks; per task the arithmetic is pool_*_vec_kernel's
+// (same order), and the backward's side gradient is Σ_t attn_t[s]·g_t summed in task order,
+// each product rounded (contraction is off) — the sum autograd forms over T separate poolings.
+constexpr int kMaxPoolTasks = 4;
+struct PoolTasks {
+  const float* wl[kMaxPoolTasks];  // [B, S] gate logits of task t, row stride wl_ld
+  float* hidden[kMaxPoolTasks];    // forward: [B, D] pooled rows
+  float* attn[kMaxPoolTasks];      // [B, S] softmax weights (forward out, backward in)
+  const float* g[kMaxPoolTasks];   // backward: [B, D] upstream gradient of hidden
+  float* gw[kMaxPoolTasks];        // backward: [B, S] logit gradient, row stride gw_ld
+  int64_t wl_ld, gw_ld;
+  int T;
+};
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_multi_kernel(
+    const float* __restrict__ side, int64_t sb, int64_t ss, int64_t B, int32_t S, int32_t D,
+    PoolTasks pt) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (b >= B) return;
+  const bool on = 4 * c < D;
+  pf4 v[kMaxSide];
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s)
+    if (s < S) v[s] = on ? *reinterpret_cast<const pf4*>(side + b * sb + s * ss + 4 * c)
+                         : pf4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < pt.T; ++t) {
+    const float* wl = pt.wl[t] + b * pt.wl_ld;
+    float a[kMaxSide];
+    float mx = -INFINITY;
+    for (int s = 0; s < S; ++s) mx = fmaxf(mx, wl[s]);
+    float sum = 0.f;
+    for (int s = 0; s < S; ++s) {
+      a[s] = expf(wl[s] - mx);
+      sum += a[s];
+    }
+    for (int s = 0; s < S; ++s) a[s] = a[s] / sum;
+    if (c < S) {
+      for (int s = 0; s < S; ++s)
+        if (s == c) pt.attn[t][b * S + s] = a[s];
+    }
+    pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s)
+      if (s < S) acc += a[s] * v[s];
+    if (on) *reinterpret_cast<pf4*>(pt.hidden[t] + b * D + 4 * c) = acc;
+  }
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_bwd_multi_kernel(
+    const float* __restrict__ side, int64_t sb, int64_t ss, int64_t B, int32_t S, int32_t D,
+    float* __restrict__ grad_side, PoolTasks pt) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if (b >= B) return;  // a whole half-wave: its shuffles stay within its own 32 lanes
+  const bool on = 4 * c < D;
+  pf4 v[kMaxSide], gs[kMaxSide];
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s)
+    if (s < S) v[s] = on ? *reinterpret_cast<const pf4*>(side + b * sb + s * ss + 4 * c)
+                         : pf4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < pt.T; ++t) {
+    const pf4 gd = on ? *reinterpret_cast<const pf4*>(pt.g[t] + b * D + 4 * c)
+                      : pf4{0.f, 0.f, 0.f, 0.f};
+    float a[kMaxSide], ga[kMaxSide];
+    for (int s = 0; s < S; ++s) a[s] = pt.attn[t][b * S + s];
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s) {
+      if (s < S) {
+        const pf4 q = a[s] * gd;
+        gs[s] = t == 0 ? q : gs[s] + q;
+        const pf4 p = gd * v[s];
+        ga[s] = half_sum((p[0] + p[1]) + (p[2] + p[3]));
+      }
+    }
+    float dot = 0.f;
+    for (int s = 0; s < S; ++s) dot += a[s] * ga[s];
+    if (c == 0)
+      for (int s = 0; s < S; ++s) pt.gw[t][b * pt.gw_ld + s] = a[s] * (ga[s] - dot);
+  }
+  if (on) {
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s)
+      if (s < S) *reinterpret_cast<pf4*>(grad_side + b * sb + s * ss + 4 * c) = gs[s];
+  }
+}
+
 // ---- training-pair sampler (eges/data_loader.py:28-62) -------------
 // walk i (global index walk_base + i) starts at 1 + U[0, n_items - 1) (:30, item 0 is OOV) and
 // takes `length` weighted steps (dgl.sampling.random_walk(prob='weight') [3p]: out-edge e of
@@ -459,6 +548,74 @@ extern "C" int32_t rs_side_pool_bwd_strided(const float* side, int64_t side_bstr
     pool_bwd_kernel<<<waves_grid(batch), kWave * kWavesPerBlock, 0, as_stream(stream)>>>(
         side, attn, grad_hidden, batch, n_side, dim, grad_side, grad_weight_logits);
   }
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+static int32_t check_pool_multi(const float* side, int64_t sb, int64_t ss, int64_t batch,
+                                int32_t n_side, int32_t dim, int32_t n_tasks) {
+  RS_CHECK_ARG(n_side >= 1 && n_side <= kMaxSide && dim >= 1 && dim <= 128 && dim % 4 == 0 &&
+                   batch >= 0 && n_tasks >= 1 && n_tasks <= kMaxPoolTasks,
+               "rs_side_pool_multi: need 1 <= n_side <= %d, dim % 4 == 0 and <= 128, 1 <= tasks "
+               "<= %d", kMaxSide, kMaxPoolTasks);
+  RS_CHECK_ARG(side && (reinterpret_cast<uintptr_t>(side) & 15) == 0 && sb % 4 == 0 && ss % 4 == 0,
+               "rs_side_pool_multi: side rows must be 16-byte aligned");
+  return RS_OK;
+}
+
+extern "C" int32_t rs_side_pool_fwd_multi(const float* side, int64_t side_bstride,
+                                          int64_t side_sstride, int64_t batch, int32_t n_side,
+                                          int32_t dim, int32_t n_tasks,
+                                          const float* const* weight_logits, int64_t logits_ld,
+                                          float* const* hidden, float* const* attn, void* stream) {
+  if (int32_t e = check_pool_multi(side, side_bstride, side_sstride, batch, n_side, dim, n_tasks))
+    return e;
+  RS_CHECK_ARG(weight_logits && hidden && attn && logits_ld >= n_side, "bad task arrays");
+  if (batch == 0) return RS_OK;
+  PoolTasks pt{};
+  pt.T = n_tasks;
+  pt.wl_ld = logits_ld;
+  for (int t = 0; t < n_tasks; ++t) {
+    RS_CHECK_ARG(weight_logits[t] && hidden[t] && attn[t] &&
+                     (reinterpret_cast<uintptr_t>(hidden[t]) & 15) == 0,
+                 "task %d: null or unaligned pointer", t);
+    pt.wl[t] = weight_logits[t];
+    pt.hidden[t] = hidden[t];
+    pt.attn[t] = attn[t];
+  }
+  pool_fwd_multi_kernel<<<waves_grid(ceil_div(batch, 2)), kWave * kWavesPerBlock, 0,
+                          as_stream(stream)>>>(side, side_bstride, side_sstride, batch, n_side,
+                                               dim, pt);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_side_pool_bwd_multi(const float* side, int64_t side_bstride,
+                                          int64_t side_sstride, int64_t batch, int32_t n_side,
+                                          int32_t dim, int32_t n_tasks, const float* const* attn,
+                                          const float* const* grad_hidden, float* grad_side,
+                                          float* const* grad_logits, int64_t grad_logits_ld,
+                                          void* stream) {
+  if (int32_t e = check_pool_multi(side, side_bstride, side_sstride, batch, n_side, dim, n_tasks))
+    return e;
+  RS_CHECK_ARG(attn && grad_hidden && grad_side && grad_logits && grad_logits_ld >= n_side &&
+                   (reinterpret_cast<uintptr_t>(grad_side) & 15) == 0,
+               "bad task arrays");
+  if (batch == 0) return RS_OK;
+  PoolTasks pt{};
+  pt.T = n_tasks;
+  pt.gw_ld = grad_logits_ld;
+  for (int t = 0; t < n_tasks; ++t) {
+    RS_CHECK_ARG(attn[t] && grad_hidden[t] && grad_logits[t] &&
+                     (reinterpret_cast<uintptr_t>(grad_hidden[t]) & 15) == 0,
+                 "task %d: null or unaligned pointer", t);
+    pt.attn[t] = const_cast<float*>(attn[t]);
+    pt.g[t] = grad_hidden[t];
+    pt.gw[t] = grad_logits[t];
+  }
+  pool_bwd_multi_kernel<<<waves_grid(ceil_div(batch, 2)), kWave * kWavesPerBlock, 0,
+                          as_stream(stream)>>>(side, side_bstride, side_sstride, batch, n_side,
+                                               dim, grad_side, pt);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -191,7 +191,32 @@ struct ApplyArgs {
   // OPT_EMIT: segment s's sum goes to uniq_grad row seg_map[s] (skipped when < 0) instead of
   // row s (the row-sharded exchange's padded per-owner send buffer, rs_exchange_pack)
   const int32_t* seg_map;
+  // OPT_DENSE: the gradient rows in up to 4 segments — position p in [gstart[i], gstart[i+1])
+  // reads gseg[i] + (p - gstart[i]) * gld[i] (a table looked up several times hands each
+  // lookup's upstream rows, strided column blocks included, without concatenating them);
+  // n_gseg 0: grad + p * dim
+  const float* gseg[4];
+  int64_t gstart[4];
+  int64_t gld[4];
+  int32_t n_gseg;
 };
+
+__device__ __forceinline__ const float* dense_grad_row(const ApplyArgs& a,
+                                                       const float* __restrict__ grad, int64_t p,
+                                                       int dim) {
+  if (a.n_gseg == 0) return grad + p * dim;
+  const float* b = a.gseg[0];
+  int64_t s0 = 0, ld = a.gld[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    if (i < a.n_gseg && p >= a.gstart[i]) {
+      b = a.gseg[i];
+      s0 = a.gstart[i];
+      ld = a.gld[i];
+    }
+  }
+  return b + (p - s0) * ld;
+}
 
 template <int OPT, int VEC>
 __device__ __forceinline__ void finalize_chunk(const ApplyArgs& a, uint32_t row, int col,
@@ -330,7 +355,10 @@ __device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
       for (int c = 0; c < CPL; ++c) {
         int col = (gl + c * lpr) * VEC;
         if (live && col < dim) {
-          load_stream<VEC>(grad + p * dim + col, r[u][c]);
+          if constexpr (OPT == OPT_DENSE)
+            load_stream<VEC>(dense_grad_row(a, grad, p, dim) + col, r[u][c]);
+          else
+            load_stream<VEC>(grad + p * dim + col, r[u][c]);
         } else {
 #pragma unroll
           for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
@@ -1242,6 +1270,53 @@ extern "C" int32_t rs_embedding_grad_dense(const uint32_t* sorted_rows, const in
   const void* ptrs[2] = {grad_out, dense};
   RowGeom geom = row_geom(dim, ptrs, 2);
   return launch_segments(OPT_DENSE, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);
+}
+
+extern "C" int32_t rs_embedding_grad_dense_segs(const uint32_t* sorted_rows,
+                                                const int32_t* sorted_pos, int64_t n_ids,
+                                                int32_t n_segs, const float* const* seg_ptrs,
+                                                const int64_t* seg_n, const int64_t* seg_ld,
+                                                int32_t dim, int64_t n_rows, float* dense,
+                                                void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(n_segs >= 1 && n_segs <= 4, "1..4 gradient segments");
+  RS_CHECK_ARG(dense && seg_ptrs && seg_n && seg_ld, "null pointer");
+  ApplyArgs a{};
+  int64_t total = 0;
+  // the vector width must suit every segment's base and row stride: a stride is checked as a
+  // byte offset (ld * 4 aligned to VEC * 4 <=> ld % VEC == 0)
+  const void* ptrs[9];
+  int np = 0;
+  for (int i = 0; i < n_segs; ++i) {
+    RS_CHECK_ARG(seg_n[i] >= 0 && seg_ld[i] >= dim, "segment rows >= 0, row stride >= dim");
+    RS_CHECK_ARG(seg_n[i] == 0 || seg_ptrs[i], "null segment pointer");
+    a.gseg[i] = seg_ptrs[i];
+    a.gstart[i] = total;
+    a.gld[i] = seg_ld[i];
+    total += seg_n[i];
+    ptrs[np++] = seg_ptrs[i];
+    ptrs[np++] = reinterpret_cast<const void*>((uintptr_t)seg_ld[i] * 4);
+  }
+  RS_CHECK_ARG(total == n_ids, "segment rows must sum to n_ids");
+  a.n_gseg = n_segs;
+  hipStream_t st = as_stream(stream);
+  RS_CHECK_HIP(hipMemsetAsync(dense, 0, (size_t)n_rows * dim * sizeof(float), st));
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(sorted_rows && sorted_pos, "null pointer");
+  if (ws_bytes < partial_bytes(n_ids, dim)) {
+    set_error("dense-gradient workspace too small");
+    return RS_E_WORKSPACE;
+  }
+  a.table = dense;
+  a.dim = dim;
+  a.partial = static_cast<float*>(workspace);
+  a.chunk = chunk_of(a.partial, n_ids, dim);
+  a.tile_flags = flags_of(a.partial, n_ids, dim);
+  ptrs[np++] = dense;
+  RowGeom geom = row_geom(dim, ptrs, np);
+  // the 128-wide group / tile32 walks address rows as grad + p * dim: keep them off this path
+  if (geom.vec == 4 && geom.cpl == 1 && geom.lpr_log2 == 5) geom.vec = 2, geom.lpr_log2 = 6;
+  return launch_segments(OPT_DENSE, sorted_rows, sorted_pos, n_ids, n_rows, a.gseg[0], a, geom, st);
 }
 
 extern "C" size_t rs_apply_workspace_size(int64_t n_ids, int32_t dim) {

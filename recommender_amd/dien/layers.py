@@ -52,7 +52,18 @@ def _rows_ready(X, H):
 
 
 def _valid_rows(mask_u8):
-    """(idx [R] int32, count [1] int32) of the rows with mask != 0, in order (on the device)."""
+    """(idx [R] int32, count [1] int32) of the rows with mask != 0, in order (on the device).
+    Kept on the mask tensor object, so the layers of one forward that share it (the GRU and the
+    AUGRU of DIEN) list the rows once."""
+    got = getattr(mask_u8, "_rs_valid_rows", None)
+    if got is not None:
+        return got
+    got = _valid_rows_list(mask_u8)
+    mask_u8._rs_valid_rows = got
+    return got
+
+
+def _valid_rows_list(mask_u8):
     dev, R = mask_u8.device, mask_u8.numel()
     idx = torch.empty(R, dtype=torch.int32, device=dev)
     cnt = torch.empty(1, dtype=torch.int32, device=dev)
@@ -321,6 +332,95 @@ class _AttentionFn(torch.autograd.Function):
         return dt, dhs, dk, None
 
 
+class _AttentionEvolveFn(torch.autograd.Function):
+    """DIENAttention then InterestEvolve (dien/model.py:71-73) as one node: the same kernels as
+    _AttentionFn + _AUGRUFn; the backward runs the AUGRU recurrence, then the attention
+    backward on its score gradient, and the attention's part of dL/dhidden is the addend of the
+    AUGRU's input-gradient kernel (rs_masked_dx_acc) — the sum autograd would form, no add pass."""
+
+    @staticmethod
+    def forward(ctx, target, hidden, att_kernel, mask_u8, ku, bu, kr, br, kh, bh):
+        B, T, H = hidden.shape
+        X = H
+        dev = hidden.device
+        st = L.stream_ptr(dev)
+        hs = hidden.contiguous()
+        t2 = target.reshape(B, -1)
+        q = (t2 @ att_kernel.t()).contiguous()
+        a = torch.empty(B, T, device=dev)
+        L.call("rs_dien_attention_fwd", L.ptr(hs), L.ptr(q), L.ptr(mask_u8), B, T, H, L.ptr(a), st)
+        Hh = ku.shape[1]
+        wx = torch.cat([ku[Hh:], kr[Hh:], kh[:X]], dim=1)
+        bx = torch.cat([bu, br, bh])
+        vr = _valid_rows(mask_u8)
+        xw = _masked_proj(hs.reshape(-1, X), wx, bx, vr).view(B, T, 3 * Hh)
+        kuh, krh, khr = ku[:Hh].contiguous(), kr[:Hh].contiguous(), kh[X:].contiguous()
+        final = torch.empty(B, Hh, device=dev)
+        states = torch.empty(B, T, Hh, device=dev)
+        saved = torch.empty(B, T, 4 * Hh, device=dev)
+        L.call("rs_augru_fwd", L.ptr(xw), L.ptr(a), L.ptr(kuh), L.ptr(krh), L.ptr(khr),
+               L.ptr(mask_u8), B, T, Hh, L.ptr(final), L.ptr(states), L.ptr(saved),
+               L.RS_DIEN_SKIP_MASKED_ROWS, st)
+        ctx.save_for_backward(t2, hs, att_kernel, q, a, wx, kuh, krh, khr, states, saved, mask_u8,
+                              *vr)
+        ctx.tshape = target.shape
+        return final
+
+    @staticmethod
+    def backward(ctx, dfinal):
+        (t2, hs, att_kernel, q, a, wx, kuh, krh, khr, states, saved, mask_u8, idx,
+         cnt) = ctx.saved_tensors
+        B, T, X = hs.shape
+        Hh = kuh.shape[0]
+        dev = hs.device
+        st = L.stream_ptr(dev)
+        dxw = torch.empty(B, T, 3 * Hh, device=dev)
+        datt = torch.empty(B, T, device=dev)
+        L.call("rs_augru_bwd", L.ptr(dfinal.contiguous()), L.ptr(a), L.ptr(states), L.ptr(saved),
+               L.ptr(kuh), L.ptr(krh), L.ptr(khr), L.ptr(mask_u8), B, T, Hh, L.ptr(dxw),
+               L.ptr(datt), L.RS_DIEN_SKIP_MASKED_ROWS, st)
+        # attention backward on the score gradient
+        dhs = torch.empty_like(hs)
+        dq = torch.empty(B, X, device=dev)
+        L.call("rs_dien_attention_bwd", L.ptr(hs), L.ptr(q), L.ptr(a), L.ptr(datt), B, T, X,
+               L.ptr(dhs), L.ptr(dq), st)
+        datt_k = dq.t() @ t2
+        dt = (dq @ att_kernel).view(ctx.tshape)
+        d2 = dxw.view(-1, 3 * Hh)
+        vr = (idx, cnt)
+        x2 = hs.reshape(-1, X)
+        dwx, sb = _masked_wgrad(x2, 0, d2, vr)
+        dhur, _ = _masked_wgrad(states.view(-1, Hh), T, d2[:, :2 * Hh], vr, sums=False)
+        dkhr, _ = _masked_wgrad(saved.view(-1, 4 * Hh)[:, 3 * Hh:], 0, d2[:, 2 * Hh:], vr,
+                                sums=False)
+        dku = torch.cat([dhur[:, :Hh], dwx[:, :Hh]], 0)
+        dkr = torch.cat([dhur[:, Hh:], dwx[:, Hh:2 * Hh]], 0)
+        dkh = torch.cat([dwx[:, 2 * Hh:], dkhr], 0)
+        # dL/dhidden = the AUGRU's input gradient + the attention's (the addend)
+        dx = torch.empty_like(hs)
+        L.call("rs_masked_dx_acc", L.ptr(d2), _ld(d2), L.ptr(wx), L.ptr(mask_u8.reshape(-1)),
+               L.ptr(idx), L.ptr(cnt), B * T, X, 3 * Hh, L.ptr(dhs), X, L.ptr(dx), X, st)
+        return (dt, dx, datt_k, None, dku, sb[:Hh], dkr, sb[Hh:2 * Hh], dkh, sb[2 * Hh:])
+
+
+def attention_evolve(attention, evolve, target, hidden, mask):
+    """evolve((hidden, attention((target, hidden), mask=mask)), mask=mask) as one node when the
+    kernels take the shapes (_AttentionEvolveFn), else the two layers."""
+    c = evolve.augru
+    H = hidden.shape[-1]
+    if attention.kernel is None:
+        attention.build(H, target.shape[-1], hidden.device)
+    if (hidden.is_cuda and torch.is_grad_enabled() and c.units == H and _rows_ready(H, H)
+            and attention.kernel.shape == (H, target.shape[-1])):
+        m = _mask_u8(mask, hidden.shape[:2], hidden.device)
+        return _AttentionEvolveFn.apply(target, hidden, attention.kernel, m,
+                                        c.update_gate.kernel, c.update_gate.bias,
+                                        c.reset_gate.kernel, c.reset_gate.bias,
+                                        c.hidden_layer.kernel, c.hidden_layer.bias)
+    score = attention((target, hidden), mask=mask)
+    return evolve((hidden, score), mask=mask)
+
+
 class DIENAttention(nn.Module):
     """dien/layers.py:136-158: score = softmax_L((H·K)·tᵀ + (1-mask)·(-1e9)) → [B, L, 1]."""
 
@@ -343,6 +443,43 @@ class DIENAttention(nn.Module):
 
 
 # ---------------------------------------------------------------------------------------------
+class _BatchNormFn(torch.autograd.Function):
+    """BatchNormalization on [B, C] rows in two launches per direction (csrc/batchnorm.hip:
+    batch statistics, normalisation and the moving-average update in the forward; Σ dy,
+    Σ dy·x̂ and dx in the backward) instead of a dozen elementwise / reduction passes each."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, training):
+        x = x.contiguous()
+        B, C = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        mean = torch.empty(C, device=dev)
+        invstd = torch.empty(C, device=dev)
+        ws = _ws("batch_norm", L.lib().rs_batch_norm_workspace_size(B, C), dev)
+        L.call("rs_batch_norm_fwd", L.ptr(x), B, C, L.ptr(gamma), L.ptr(beta), bn.epsilon,
+               bn.momentum, int(training), L.ptr(bn.moving_mean), L.ptr(bn.moving_variance),
+               L.ptr(y), L.ptr(mean), L.ptr(invstd), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        ctx.save_for_backward(x, gamma, mean, invstd)
+        ctx.training = training
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, invstd = ctx.saved_tensors
+        B, C = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dgamma = torch.empty(C, device=dev)
+        dbeta = torch.empty(C, device=dev)
+        ws = _ws("batch_norm_bwd", L.lib().rs_batch_norm_workspace_size(B, C), dev)
+        L.call("rs_batch_norm_bwd", L.ptr(dy), L.ptr(x), B, C, L.ptr(mean), L.ptr(invstd),
+               L.ptr(gamma), int(ctx.training), L.ptr(dx), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws),
+               ws.numel(), L.stream_ptr(dev))
+        return dx, dgamma, dbeta, None, None
+
+
 class BatchNormalization(nn.Module):
     """keras.layers.BatchNormalization [3p]: momentum 0.99, epsilon 1e-3; training → batch
     statistics + moving-average update; inference → moving statistics."""
@@ -356,6 +493,8 @@ class BatchNormalization(nn.Module):
         self.register_buffer("moving_variance", torch.ones(dim, device=device))
 
     def forward(self, x, training=False):
+        if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.shape[0] > 0:
+            return _BatchNormFn.apply(x, self.gamma, self.beta, self, bool(training))
         if training:
             mean = x.mean(0)
             var = x.var(0, unbiased=False)  # tf.nn.moments: the population variance
@@ -497,7 +636,8 @@ class _InterestExtractFn(torch.autograd.Function):
     (rs_masked_dx_acc: no add)."""
 
     @staticmethod
-    def forward(ctx, pos, neg, mask_u8, kernel, recurrent_kernel, bias, W1, b1, W2, b2, W3, b3):
+    def forward(ctx, pos, neg, mask_u8, kernel, recurrent_kernel, bias, W1, b1, W2, b2, W3, b3,
+                sparse_inputs=False):
         B, T, X = pos.shape
         H = recurrent_kernel.shape[0]
         E = neg.shape[-1]
@@ -514,6 +654,7 @@ class _InterestExtractFn(torch.autograd.Function):
         L.call("rs_dien_aux_fwd", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H, E,
                L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(aux), st)
         ctx.save_for_backward(pos, neg, kernel, rk, out, saved, mask_u8, *vr, W1, b1, W2, b2, W3, b3)
+        ctx.sparse_inputs = sparse_inputs
         return out, aux
 
     @staticmethod
@@ -541,7 +682,8 @@ class _InterestExtractFn(torch.autograd.Function):
         ws = _aux_workspace(B, T, H, E, dev)
         L.call("rs_dien_aux_bwd_acc", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H,
                E, L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(da),
-               L.ptr(dh), 1, L.ptr(dp_aux), L.ptr(dneg), L.ptr(dparams), L.ptr(ws), ws.numel(), st)
+               L.ptr(dh), 1 | (2 if ctx.sparse_inputs else 0), L.ptr(dp_aux), L.ptr(dneg),
+               L.ptr(dparams), L.ptr(ws), ws.numel(), st)
         dxw = torch.empty(B, T, 3 * H, device=dev)
         dinner = torch.empty(B, T, 3 * H, device=dev)
         L.call("rs_gru_bwd", L.ptr(dh), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
@@ -560,7 +702,7 @@ class _InterestExtractFn(torch.autograd.Function):
             n = int(torch.Size(shape).numel())
             outs.append(dparams[o:o + n].view(shape))
             o += n
-        return (dpos, dneg, None, dk, drk, torch.stack([db0, db1]), *outs)
+        return (dpos, dneg, None, dk, drk, torch.stack([db0, db1]), *outs, None)
 
 
 def _sigmoid_ce(labels, logits):
@@ -576,6 +718,10 @@ class InterestExtract(nn.Module):
         super().__init__()
         self.gru = GRU(gru_units, input_dim, device, generator)
         self.auxiliary_net = AuxiliaryNet([80, 40, 1], gru_units + input_dim, device, generator)
+        # True when the caller's pos / neg histories come from lookups that drop the masked
+        # steps' gradients (their grad_mask is this layer's mask, as DIEN's): the gradients of
+        # those steps may then be left unwritten (no zero fill of the [B, L, E] arrays)
+        self.masked_input_grads_dropped = False
 
     def _fused_aux_ready(self, hidden_state, pos_his):
         layers = list(self.auxiliary_net.layers)
@@ -620,7 +766,8 @@ class InterestExtract(nn.Module):
             m = _mask_u8(mask, pos_history.shape[:2], pos_history.device)
             return _InterestExtractFn.apply(pos_history.contiguous(), neg_history.contiguous(), m,
                                             g.kernel, g.recurrent_kernel, g.bias, l1.kernel,
-                                            l1.bias, l2.kernel, l2.bias, l3.kernel, l3.bias)
+                                            l1.bias, l2.kernel, l2.bias, l3.kernel, l3.bias,
+                                            self.masked_input_grads_dropped)
         hidden_state = self.gru(pos_history, mask=mask)
         aux = self.compute_auxiliary_loss((hidden_state, pos_history, neg_history), training, mask)
         return hidden_state, aux

@@ -18,7 +18,7 @@ from torch import nn
 from ..embedding import Embedding
 from ..functional import embedding_lookup_concat
 from .layers import (MLP, DIENAttention, InterestEvolve, InterestExtract, LocalActivationUnit,
-                     compute_his_average)
+                     attention_evolve, compute_his_average)
 
 
 class BaseModel(nn.Module):
@@ -79,6 +79,8 @@ class DIEN(BaseModel):
         dev, gen = kwargs.get("device"), kwargs.get("generator")
         D = self.embedding_dim
         self.interest_extract_layer = InterestExtract(interest_extract_gru_units, D, dev, gen)
+        # forward() looks pos / neg up with the history mask as their gradient mask
+        self.interest_extract_layer.masked_input_grads_dropped = True
         self.attention = DIENAttention(interest_extract_gru_units, D, dev, gen)
         self.interest_evolve = InterestEvolve(interest_evolve_gru_units, interest_extract_gru_units, dev, gen)
         if interest_evolve_gru_units != D:
@@ -91,6 +93,8 @@ class DIEN(BaseModel):
 
     def forward(self, inputs, training=False, mask=None):
         mask = self.item_embedding.compute_mask(inputs["pos_his_item"])
+        # as uint8 once: the lookups' gradient flags and every layer's kernels read this form
+        mask = mask.to(torch.uint8)
         target = self.compute_flat_embedding((inputs["target_item"], inputs["target_cat"]))
         # masked history steps carry no gradient: the GRU / AUGRU skip them (their input rows'
         # gradient is written 0), the attention gives them weight exactly 0 and the aux loss
@@ -98,8 +102,8 @@ class DIEN(BaseModel):
         pos = self.compute_flat_embedding((inputs["pos_his_item"], inputs["pos_his_cat"]), mask)
         neg = self.compute_flat_embedding((inputs["neg_his_item"], inputs["neg_his_cat"]), mask)
         hidden, aux = self.interest_extract_layer((pos, neg), training, mask)
-        score = self.attention((target, hidden), training, mask)
-        rep = self.interest_evolve((hidden, score), training, mask)
+        # attention then AUGRU as one node (the attention's hidden gradient summed in-kernel)
+        rep = attention_evolve(self.attention, self.interest_evolve, target, hidden, mask)
         # dien/model.py:79 passes no `training`: TF 2.2 propagates the call's (head_bn_mode)
         bn_training = bool(training) and self.head_bn_mode == "propagate"
         prob = self.mlp(torch.cat([target.squeeze(1), rep], -1), training=bn_training)

@@ -98,7 +98,7 @@ class DIENStep:
         grads = [p.grad for p in self._gdense]  # None: Keras skips the variable
         nd = len(self._gdense)
         for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
-            got = t.take_grad(with_valid=True)
+            got = t.take_grad(with_valid=True, segments=True)
             grads.append(densify_grad(t, got[0], got[1], self._ws, valid=got[2],
                                       out=self.opt_graph.grad_view(nd + i))
                          if got is not None else None)

@@ -86,7 +86,7 @@ class EGESStep:
         loss.backward()
         grads = []
         for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
-            got = t.take_grad()
+            got = t.take_grad(segments=True)
             grads.append(densify_grad(t, got[0], got[1], self._ws,
                                       out=self.opt_graph.grad_view(i)) if got is not None
                          else None)

@@ -170,11 +170,12 @@ class Embedding(nn.Module):
     def has_grad(self) -> bool:
         return bool(self._pending)
 
-    def take_grad(self, with_valid: bool = False):
+    def take_grad(self, with_valid: bool = False, segments: bool = False):
         """(ids [N] flattened in position order, grad rows [N, dim]) of every lookup since the
         last call, concatenated in call order; clears the pending list. with_valid: a third
         entry, the uint8 [N] flags of positions that carry gradient (None when every lookup
-        registered all its positions)."""
+        registered all its positions). segments: the grad rows of 2-4 lookups stay a list of the
+        lookups' own [N_i, dim] row views (densify_grad reads them in place, no concatenation)."""
         p, self._pending = self._pending, []
         if not p:
             return None
@@ -182,8 +183,12 @@ class Embedding(nn.Module):
             ids, g, v = p[0]
         else:
             # every lookup holds a multiple of n_slots ids, so position % n_slots stays the slot
-            ids = torch.cat([i.to(torch.int64) for i, _, _ in p])
-            g = torch.cat([g for _, g, _ in p])
+            same = all(i.dtype == p[0][0].dtype for i, _, _ in p)
+            ids = torch.cat([i if same else i.to(torch.int64) for i, _, _ in p])
+            if segments and len(p) <= 4 and all(g.stride(-1) == 1 for _, g, _ in p):
+                g = [g for _, g, _ in p]
+            else:
+                g = torch.cat([g for _, g, _ in p])
             v = None
             if any(x is not None for _, _, x in p):
                 v = torch.cat([x if x is not None else torch.ones(i.numel(), dtype=torch.uint8,

@@ -5,6 +5,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..nn import shared_input_dense
 from .layers import MLP
 from .tables import FeatureTables
 
@@ -21,10 +22,14 @@ class ESMM(nn.Module):
     def compute_embedding(self, inputs):
         return self.embedding_layer(inputs)
 
+    def _towers(self, e):
+        # both towers' first layers read e: one GEMM over their concatenated kernels
+        # (shared_input_dense), the rest of each tower on its column block in place
+        h_ctr, h_cvr = shared_input_dense(e, [self.ctr.mlp[0], self.cvr.mlp[0]])
+        return self.ctr(h_ctr, start=1), self.cvr(h_cvr, start=1)
+
     def forward(self, inputs, training=None, mask=None):
-        e = self.compute_embedding(inputs)
-        p_ctr = self.ctr(e)
-        p_cvr = self.cvr(e)
+        p_ctr, p_cvr = self._towers(self.compute_embedding(inputs))
         return torch.cat([p_ctr, p_cvr * p_ctr], dim=-1)
 
     call = forward
@@ -36,5 +41,5 @@ class ESMM(nn.Module):
         return self.ctr(self.compute_embedding(inputs))
 
     def compute_ctcvr(self, inputs):
-        e = self.compute_embedding(inputs)
-        return self.cvr(e) * self.ctr(e)
+        p_ctr, p_cvr = self._towers(self.compute_embedding(inputs))
+        return p_cvr * p_ctr

@@ -18,7 +18,9 @@ class MLP(nn.Module):
                             generator=generator))
         self.mlp = nn.ModuleList(layers)
 
-    def forward(self, inputs, **kwargs):
-        for fc in self.mlp:
+    def forward(self, inputs, start=0, **kwargs):
+        """start: the index of the first layer to run (the layers before it evaluated by the
+        caller, e.g. ESMM's shared first-layer GEMM)."""
+        for fc in list(self.mlp)[start:]:
             inputs = fc(inputs)
         return inputs

@@ -8,13 +8,92 @@ deeper layer instead of num_experts small GEMMs; their weight gradients are spli
 (recommender_amd.nn.wgrad / bwgrad) — hipBLASLt's K = batch kernels are 10x slower."""
 from __future__ import annotations
 
+import ctypes as C
+import os
+
 import torch
 from torch import nn
 
+from .. import _lib as L
 from ..eges.model import side_pool
-from ..nn import Dense, batched_linear, linear
+from ..nn import Dense, _act_bwd, _affine, batched_linear, linear, wgrad
 from .layers import MLP
 from .tables import FeatureTables
+
+# RS_MMOE_FUSED=0: the experts / gates / poolings as separate autograd nodes (A/B switch)
+_FUSED = os.environ.get("RS_MMOE_FUSED", "1") != "0"
+
+
+def _ptrs(ts):
+    return C.cast((C.c_void_p * len(ts))(*[t.data_ptr() for t in ts]), C.c_void_p)
+
+
+class _ExpertsGatesFn(torch.autograd.Function):
+    """MMOE's shared-input block (esmm/mmoe.py:36-46) as one node: the E experts' first layers
+    as one GEMM over their concatenated kernels (relu in its epilogue), the T gates' logits as
+    one GEMM, the experts' second layers as one batched GEMM reading the first layer's output
+    in place ([E, B, H0] seen with rows E·H0 apart: no transpose copy), and the T softmax
+    poolings of the [E, B, H1] expert outputs in one pass (rs_side_pool_fwd_multi).
+    Backward: one pooling pass for all tasks (their expert-output gradients summed inside it),
+    the second layers' relu masks and bias sums per expert, their input gradient by one batched
+    GEMM, then every expert's first-layer mask written from that [E, B, H0] gradient straight
+    into one [B, E·H0 + T·E] buffer beside the gates' logit gradients (rs_act_bwd_colsum_ld),
+    so the input gradient of x is ONE GEMM over K = E·H0 + T·E (no per-consumer GEMMs and adds)
+    and the first-layer + gate kernel gradients one split-K GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, k0, b0, k1, b1, kg, bg, E, T):
+        B = x.shape[0]
+        H0, H1 = k0.shape[1] // E, k1.shape[2]
+        x = x.contiguous()
+        dev = x.device
+        st = L.stream_ptr(dev)
+        y1 = _affine(x, k0, b0, 1)                                  # [B, E*H0]
+        zg = torch.addmm(bg, x, kg)                                 # [B, T*E]
+        y1v = y1.view(B, E, H0).transpose(0, 1)                     # [E, B, H0], in place
+        y2 = torch.relu_(torch.baddbmm(b1, y1v, k1))                # [E, B, H1]
+        hid = [torch.empty(B, H1, device=dev) for _ in range(T)]
+        att = [torch.empty(B, E, device=dev) for _ in range(T)]
+        L.call("rs_side_pool_fwd_multi", L.ptr(y2), H1, B * H1, B, E, H1, T,
+               _ptrs([zg[:, t * E:] for t in range(T)]), T * E, _ptrs(hid), _ptrs(att), st)
+        ctx.save_for_backward(x, k0, k1, kg, y1, y2, *att)
+        ctx.E, ctx.T = E, T
+        return tuple(hid)
+
+    @staticmethod
+    def backward(ctx, *gh):
+        x, k0, k1, kg, y1, y2, *att = ctx.saved_tensors
+        E, T = ctx.E, ctx.T
+        B = x.shape[0]
+        H0, H1 = k0.shape[1] // E, k1.shape[2]
+        N0 = E * H0
+        Nt = N0 + T * E
+        dev = x.device
+        st = L.stream_ptr(dev)
+        gh = [torch.zeros(B, H1, device=dev) if g is None else g.contiguous() for g in gh]
+        dy2 = torch.empty_like(y2)
+        dzc = torch.empty(B, Nt, device=dev)                        # [experts' dz1 | gates' dz]
+        L.call("rs_side_pool_bwd_multi", L.ptr(y2), H1, B * H1, B, E, H1, T, _ptrs(att),
+               _ptrs(gh), L.ptr(dy2), _ptrs([dzc[:, N0 + t * E:] for t in range(T)]), Nt, st)
+        # second layers: relu mask + bias sums per expert, input gradient, kernel gradients
+        dz2 = torch.empty_like(y2)
+        db1 = torch.empty(E, 1, H1, device=dev)
+        for e in range(E):
+            _act_bwd(dy2[e], y2[e], 1, True, dz=dz2[e], db=db1[e, 0])
+        dy1 = torch.bmm(dz2, k1.transpose(1, 2))                   # [E, B, H0]
+        dk1 = torch.stack([wgrad(y1[:, e * H0:(e + 1) * H0], dz2[e]) for e in range(E)])
+        # first layers: each expert's mask from its [B, H0] block of dy1 into dzc
+        db0 = torch.empty(N0, device=dev)
+        nws = L.lib().rs_act_bwd_colsum_workspace_size(B, H0)
+        ws = torch.empty(max(1, nws // 4), device=dev)
+        for e in range(E):
+            L.call("rs_act_bwd_colsum_ld", L.ptr(dy1[e]), H0, L.ptr(y1[:, e * H0:]), N0, B, H0, 1,
+                   L.ptr(dzc[:, e * H0:]), Nt, L.ptr(db0[e * H0:]), L.ptr(ws), ws.numel() * 4, st)
+        dbg = dzc[:, N0:].sum(0)
+        kc = torch.cat([k0, kg], 1)
+        dx = dzc @ kc.t() if ctx.needs_input_grad[0] else None
+        dkc = wgrad(x, dzc)
+        return dx, dkc[:, :N0], db0, dk1, db1, dkc[:, N0:], dbg, None, None
 
 
 class MMOE(nn.Module):
@@ -53,7 +132,29 @@ class MMOE(nn.Module):
             h = batched_linear(h, k, b, act=1)
         return h.transpose(0, 1)                                     # [B, E, H]
 
+    def _fused_ready(self, x):
+        E = len(self.experts)
+        mlps = [e.mlp for e in self.experts]
+        return (_FUSED and x.dim() == 2 and x.is_cuda and torch.is_grad_enabled()
+                and 1 <= self.num_tasks <= 4 and 2 <= E <= 16
+                and all(len(m) == 2 and all(l.act_code == 1 and l.kernel is not None
+                                            and l.bias is not None for l in m) for m in mlps)
+                and len({(m[0].units, m[1].units) for m in mlps}) == 1
+                and mlps[0][1].units % 4 == 0 and mlps[0][1].units <= 128
+                and all(g.kernel is not None and g.bias is not None and g.units == E
+                        for g in self.gates))
+
     def _towers(self, x):
+        if self._fused_ready(x):
+            E, T = len(self.experts), self.num_tasks
+            l0 = [e.mlp[0] for e in self.experts]
+            l1 = [e.mlp[1] for e in self.experts]
+            pooled = _ExpertsGatesFn.apply(
+                x, torch.cat([l.kernel for l in l0], 1), torch.cat([l.bias for l in l0]),
+                torch.stack([l.kernel for l in l1]), torch.stack([l.bias for l in l1])[:, None, :],
+                torch.cat([g.kernel for g in self.gates], 1), torch.cat([g.bias for g in self.gates]),
+                E, T)
+            return [self.task_towers[i](pooled[i]) for i in range(T)]
         # [B, E, H] seen over the [E, B, H] expert outputs: rs_side_pool reads (and writes the
         # gradient of) that layout in place, no transpose pass either way
         ex = self.experts_outputs(x)

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 import weakref
 
 import torch
@@ -41,11 +42,11 @@ def get_activation(act):
 # and the cfg4 full-size oracle check of the dense gradients (65 536-example sums, bound 1e-4 of
 # the 512-chunk magnitude) fails with it by up to 6.7x (tests/test_fullsize_gpu.py), so parity
 # keeps the library default.
-_GEMM_X3 = __import__("os").environ.get("RS_GEMM_X3", "0") == "1"
+_GEMM_X3 = os.environ.get("RS_GEMM_X3", "0") == "1"
 _X3_MIN_N, _X3_MIN_K = 128, 160
 # relu layers: hipBLASLt's bias + relu epilogue (torch._addmm_activation) instead of a separate
 # in-place relu pass; RS_RELU_EPILOGUE=0 restores the pass
-_RELU_EPILOGUE = __import__("os").environ.get("RS_RELU_EPILOGUE", "1") == "1"
+_RELU_EPILOGUE = os.environ.get("RS_RELU_EPILOGUE", "1") == "1"
 
 
 def _x3_ready(*ts, n=0, k=0, batched=False):
@@ -224,6 +225,8 @@ def batched_linear(x, k, b, act: int = 0):
 
 
 _ACT_CODE = {"relu": 1, "sigmoid": 2}
+# RS_SHARED_INPUT_DENSE=0: shared_input_dense runs the layers one by one (A/B switch)
+_SHARED_INPUT = os.environ.get("RS_SHARED_INPUT_DENSE", "1") != "0"
 _wgrad_stream: torch.cuda.Stream | None = None
 
 
@@ -269,7 +272,9 @@ class _DenseFn(torch.autograd.Function):
         k = layer.kernel if rows is None else layer.kernel.index_select(0, rows)
         b = layer.bias
         act = layer.act_code if act is None else act
-        y = _affine(x.contiguous(), k, b, act)
+        # a row-strided x (a column block of a wider activation) goes to the GEMM in place
+        xa = x if (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) >= x.shape[1]) else x.contiguous()
+        y = _affine(xa, k, b, act)
         ctx.layer, ctx.rows, ctx.act = layer, rows, act
         ctx.save_for_backward(x, k, y if act else None)
         return y
@@ -315,6 +320,82 @@ class _DenseFn(torch.autograd.Function):
                 if t is not None:
                     t.record_stream(side)
         return dx, None, None, None, None
+
+
+class _SharedInputDenseFn(torch.autograd.Function):
+    """act(x·k_i + b_i) for several Dense layers reading the same x — ESMM's CTR and CVR towers'
+    first layers (esmm/esmm.py:27-28) — as ONE GEMM over the concatenated kernels: x is read
+    once and the outputs are the column blocks of one [B, ΣN] activation (row stride ΣN, read in
+    place by the next layers). Backward: each block masked from its own gradient into one dz
+    with its bias gradient (rs_act_bwd_colsum_ld), one input-gradient GEMM over K = ΣN (the
+    towers' contributions summed inside it: no add pass) and one split-K weight-gradient GEMM
+    whose column blocks are the layers' kernel gradients (written into .grad as _DenseFn)."""
+
+    @staticmethod
+    def forward(ctx, x, act, layers, *handles):
+        k = torch.cat([l.kernel for l in layers], dim=1)
+        b = torch.cat([l.bias for l in layers])
+        y = _affine(x.contiguous(), k, b, act)
+        ctx.layers, ctx.act = layers, act
+        ctx.save_for_backward(x, k, y)
+        outs, o = [], 0
+        for l in layers:
+            outs.append(y[:, o:o + l.units])
+            o += l.units
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        from . import _lib as L
+
+        x, k, y = ctx.saved_tensors
+        B, Nt = y.shape
+        dz = torch.empty_like(y)
+        db = torch.empty(Nt, device=y.device, dtype=torch.float32)
+        o = 0
+        for l, g in zip(ctx.layers, gs):
+            n = l.units
+            g = torch.zeros(B, n, device=y.device) if g is None else g
+            if g.stride(-1) != 1:
+                g = g.contiguous()
+            ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(B, n) // 4),
+                             device=y.device)
+            L.call("rs_act_bwd_colsum_ld", L.ptr(g), g.stride(0), L.ptr(y[:, o:]), Nt, B, n,
+                   ctx.act, L.ptr(dz[:, o:]), Nt, L.ptr(db[o:]), L.ptr(ws), ws.numel() * 4,
+                   L.stream_ptr(y.device))
+            o += n
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (gemm_x3(dz, k, tb=True) if _x3_ready(dz, k, n=k.shape[0], k=k.shape[1])
+                  else dz @ k.t())
+        main = torch.cuda.current_stream(y.device)
+        side = _wgrad_stream
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side if side is not None else main):
+            dk = wgrad(x, dz)
+            o = 0
+            for l in ctx.layers:
+                _accum_grad(l.kernel, dk[:, o:o + l.units].contiguous())
+                _accum_grad(l.bias, db[o:o + l.units])
+                o += l.units
+        if side is not None:
+            for t in (x, dz, db, dk):
+                t.record_stream(side)
+        return (dx, None, None) + (None,) * len(ctx.layers)
+
+
+def shared_input_dense(x, layers):
+    """[layer(x) for layer in layers] for built relu / sigmoid Dense layers with biases and one
+    activation, as one GEMM (_SharedInputDenseFn); other cases run the layers one by one."""
+    ok = (x.dim() == 2 and x.is_cuda and torch.is_grad_enabled() and len(layers) > 1
+          and all(l.kernel is not None and l.bias is not None for l in layers)
+          and len({l.act_code for l in layers}) == 1 and layers[0].act_code in (1, 2)
+          and len({l.kernel.shape[0] for l in layers}) == 1 and _SHARED_INPUT)
+    if not ok:
+        return tuple(l(x) for l in layers)
+    return _SharedInputDenseFn.apply(x, layers[0].act_code, tuple(layers),
+                                     *[l._handle() for l in layers])
 
 
 class _LinearChainFn(torch.autograd.Function):

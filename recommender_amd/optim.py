@@ -12,9 +12,9 @@ Dense:
 """
 from __future__ import annotations
 
-import os
-
+import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -529,13 +529,33 @@ def densify_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,
     per row, each row's sum stored in place, untouched rows 0). valid (uint8 per id, optional):
     positions flagged 0 are left out — for lookups whose masked positions carry no gradient
     (Embedding.accumulate_grad's valid). out (optional, contiguous fp32 [input_dim, dim]): the
-    gradient is written there (every element) instead of into a new tensor."""
+    gradient is written there (every element) instead of into a new tensor. grad_rows may be a
+    list of 1-4 [N_i, dim] row views (Embedding.take_grad(segments=True): one per lookup, row
+    stride free, unit column stride), read in place as if concatenated."""
     ws = ws or _Workspace()
     dev = table.weight.device
     dim, V = table.output_dim, table.input_dim
     if out is not None and (tuple(out.shape) != (V, dim) or out.dtype != torch.float32
                             or not out.is_contiguous()):
         raise ValueError("out must be a contiguous fp32 [input_dim, dim] tensor")
+    if isinstance(grad_rows, (list, tuple)):
+        segs = list(grad_rows)
+        if (len(segs) > 4 or (valid is None and V * dim <= 16384)
+                or any(g.dim() != 2 or g.shape[1] != dim or g.stride(1) != 1
+                       or (g.shape[0] > 1 and g.stride(0) < dim) for g in segs)):
+            grad_rows = torch.cat([g.reshape(-1, dim) for g in segs])  # the one-array paths
+        else:
+            s = SortedIds.for_table(table, ids, ws, count_unique=False, valid=valid)
+            dense = out if out is not None else torch.empty(V, dim, dtype=torch.float32, device=dev)
+            w = ws.get("dense", L.lib().rs_apply_workspace_size(s.n, dim), dev)
+            k = len(segs)
+            ptrs = (C.c_void_p * 4)(*[g.data_ptr() for g in segs])
+            ns = (C.c_int64 * 4)(*[g.shape[0] for g in segs])
+            lds = (C.c_int64 * 4)(*[g.stride(0) if g.shape[0] > 1 else dim for g in segs])
+            L.call("rs_embedding_grad_dense_segs", L.ptr(s.rows), L.ptr(s.pos), s.n, k,
+                   C.cast(ptrs, C.c_void_p), C.cast(ns, C.c_void_p), C.cast(lds, C.c_void_p), dim,
+                   V, L.ptr(dense), L.ptr(w), w.numel(), L.stream_ptr(dev))
+            return dense
     if valid is None and V * dim <= 16384 and dim <= 256 and dim & (dim - 1) == 0:
         # small table (PinSage year / genre): one pass, per-block LDS copies, no sort
         ids = ids.reshape(-1).contiguous()

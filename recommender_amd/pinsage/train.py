@@ -110,7 +110,7 @@ class PinSageStep:
         grads = [p.grad for p in self.dense]  # None: Keras skips the variable
         nd = len(self.dense)
         for i, t in enumerate(tables):  # densified straight into the flat gradient buffer
-            got = t.take_grad()
+            got = t.take_grad(segments=True)
             grads.append(densify_grad(t, got[0], got[1], self._ws,
                                       out=self.opt_graph.grad_view(nd + i)) if got is not None
                          else None)

@@ -290,3 +290,45 @@ def test_fused_aux_loss_fwd_bwd_vs_oracle(H, B, L, kind, rng):
     assert torch.isnan(aux1[5]) and torch.isfinite(aux1[torch.arange(B, device=DEV) != 5]).all()
     aux1.backward(daux)
     assert torch.isnan(an[0].kernel.grad).all() and torch.isnan(an[2].bias.grad).all()
+
+
+@pytest.mark.parametrize("B", [4096, 1000, 1])
+@pytest.mark.parametrize("training", [True, False])
+def test_batch_norm_kernels_vs_float64(B, training):
+    """BatchNormalization on the fused kernels (csrc/batchnorm.hip) against a float64 evaluation
+    of the Keras formulas: output, moving mean / variance after the update (training) or
+    untouched (inference), and dx / dgamma / dbeta; ragged last chunk (B = 1000) and B = 1."""
+    from recommender_amd.dien.layers import BatchNormalization
+
+    g = torch.Generator(device=DEV).manual_seed(B + int(training))
+    C = 72
+    bn = BatchNormalization(C, device=DEV)
+    bn.gamma.data = torch.rand(C, device=DEV, generator=g) + 0.5
+    bn.beta.data = torch.randn(C, device=DEV, generator=g)
+    bn.moving_mean.copy_(torch.randn(C, device=DEV, generator=g))
+    bn.moving_variance.copy_(torch.rand(C, device=DEV, generator=g) + 0.5)
+    mm0, mv0 = bn.moving_mean.clone().double(), bn.moving_variance.clone().double()
+    x = (torch.randn(B, C, device=DEV, generator=g) * 3 + 1).requires_grad_()
+    up = torch.randn(B, C, device=DEV, generator=g)
+    y = bn(x, training=training)
+    (y * up).sum().backward()
+    x64 = x.detach().double().requires_grad_()
+    ga64 = bn.gamma.detach().double().requires_grad_()
+    be64 = bn.beta.detach().double().requires_grad_()
+    if training:
+        mean, var = x64.mean(0), x64.var(0, unbiased=False)
+    else:
+        mean, var = mm0, mv0
+    y64 = (x64 - mean) * torch.rsqrt(var + 1e-3) * ga64 + be64
+    (y64 * up.double()).sum().backward()
+    _close(y, y64, "bn output")
+    _close(x.grad, x64.grad, "bn dx")
+    _close(bn.gamma.grad, ga64.grad, "bn dgamma")
+    _close(bn.beta.grad, be64.grad, "bn dbeta")
+    if training:
+        d = 1.0 - 0.99
+        _close(bn.moving_mean, mm0 - (mm0 - mean.detach()) * d, "moving mean")
+        _close(bn.moving_variance, mv0 - (mv0 - var.detach()) * d, "moving variance")
+    else:
+        assert torch.equal(bn.moving_mean.double(), mm0)
+        assert torch.equal(bn.moving_variance.double(), mv0)

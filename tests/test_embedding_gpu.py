@@ -72,6 +72,40 @@ def test_concat_lookup_matches_cat_of_lookups(da, db, rng):
     assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
 
 
+@pytest.mark.parametrize("dim", [18, 16, 64, 128, 7])
+@pytest.mark.parametrize("n_lookups", [2, 3, 4])
+def test_densify_segments_equal_concatenation(dim, n_lookups, rng):
+    """densify_grad over a table's lookups handed as separate (strided) row views
+    (take_grad(segments=True): rs_embedding_grad_dense_segs) equals the densified concatenation
+    bit for bit — with and without valid flags, with column-block views (row stride > dim), a
+    one-row lookup, and an out-of-range id (dropped on both sides)."""
+    from recommender_amd.optim import _Workspace, densify_grad
+
+    V = 3001 if dim != 7 else 500
+    sizes = [1, 4096 * 3 + 5, 700, 9000][:n_lookups]
+    for with_valid in (False, True):
+        ws = _Workspace()
+        ids = [torch.from_numpy(rng.integers(0, V, n).astype(np.int32)).to(DEV) for n in sizes]
+        ids[-1][3] = V + 1
+        wide = [torch.from_numpy(rng.standard_normal((n, 2 * dim + 2)).astype(np.float32)).to(DEV)
+                for n in sizes]
+        views = [w[:, :dim] if i % 2 == 0 else w[:, dim + 2:] for i, w in enumerate(wide)]
+        valid = None
+        if with_valid:
+            valid = [torch.from_numpy((rng.random(n) < 0.7).astype(np.uint8)).to(DEV)
+                     for n in sizes]
+        res = []
+        for segmented in (True, False):
+            t = Embedding(V, dim, device=DEV)
+            for k in range(n_lookups):
+                t.accumulate_grad(ids[k], views[k], None if valid is None else valid[k])
+            got = t.take_grad(with_valid=True, segments=segmented)
+            assert isinstance(got[1], list) == segmented
+            res.append(densify_grad(t, got[0], got[1], ws, valid=got[2]).cpu())
+        assert torch.equal(res[0], res[1])
+        assert res[0].abs().sum() > 0
+
+
 def test_gather_slab_and_oob(rng):
     card = [7, 1, 300, 50]
     dim = 64

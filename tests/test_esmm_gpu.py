@@ -266,3 +266,111 @@ def test_world2_sharded_esmm_matches_oracle(opt):
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def test_shared_input_dense_matches_float64():
+    """shared_input_dense (ESMM's two first tower layers as one GEMM over concatenated kernels,
+    each output a column block of one activation): outputs equal the layers run one by one
+    within fp32 GEMM rounding, and the input / kernel / bias gradients equal a float64
+    evaluation under the same relu mask (the mask taken from the outputs, so a pre-activation
+    within rounding of 0 cannot flip between the two sides)."""
+    from recommender_amd.nn import Dense, shared_input_dense
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    B, fi = 3000, 324
+    layers = [Dense(360, "relu", in_features=fi, device=DEV, generator=g),
+              Dense(200, "relu", in_features=fi, device=DEV, generator=g)]
+    for l in layers:
+        l.bias.data.uniform_(-0.1, 0.1, generator=g)
+    x = torch.randn(B, fi, device=DEV, generator=g, requires_grad=True)
+    ups = [torch.randn(B, l.units, device=DEV, generator=g) for l in layers]
+    outs = shared_input_dense(x, layers)
+    assert [tuple(o.shape) for o in outs] == [(B, 360), (B, 200)]
+    assert outs[0].grad_fn is not None
+    with torch.no_grad():
+        for o, l in zip(outs, layers):
+            sep = torch.relu(x @ l.kernel + l.bias)
+            assert_close_rel(o.cpu(), sep.cpu(), rtol=1e-5,
+                             scale=float((x.abs() @ l.kernel.abs()).max()) * 1e-2)
+    sum((o * u).sum() for o, u in zip(outs, ups)).backward()
+    x64 = x.detach().double()
+    dx64 = torch.zeros_like(x64)
+    mag_dx = torch.zeros_like(x64)
+    for o, u, l in zip(outs, ups, layers):
+        dz = (o.detach() > 0).double() * u.double()
+        k64 = l.kernel.detach().double()
+        dx64 += dz @ k64.t()
+        mag_dx += dz.abs() @ k64.abs().t()
+        assert_close_rel(l.kernel.grad.cpu(), (x64.t() @ dz).cpu(), rtol=1e-5,
+                         scale=float((x64.abs().t() @ dz.abs()).max()) * 1e-2, msg="kernel grad")
+        assert_close_rel(l.bias.grad.cpu(), dz.sum(0).cpu(), rtol=1e-5,
+                         scale=float(dz.abs().sum(0).max()) * 1e-2, msg="bias grad")
+    assert_close_rel(x.grad.cpu(), dx64.cpu(), rtol=1e-5, scale=float(mag_dx.max()) * 1e-2,
+                     msg="input grad")
+
+
+def test_side_pool_multi_equals_single_task_poolings():
+    """rs_side_pool_fwd_multi / rs_side_pool_bwd_multi (MMOE's T gate poolings over the same
+    [E, B, H] expert outputs in one pass) equal T rs_side_pool calls bit for bit: pooled rows,
+    softmax weights, logit gradients, and the side gradient as the sum of the T side gradients
+    (task order)."""
+    from recommender_amd import _lib as L
+    from recommender_amd.eges.model import side_pool
+    from recommender_amd.esmm.mmoe import _ptrs
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    E, B, H, T = 8, 1000, 80, 3
+    y = torch.randn(E, B, H, device=DEV, generator=g)
+    z = torch.randn(B, T * E + 3, device=DEV, generator=g)  # logit rows wider than T·E
+    ups = [torch.randn(B, H, device=DEV, generator=g) for _ in range(T)]
+    st = L.stream_ptr(torch.device(DEV))
+    hid = [torch.empty(B, H, device=DEV) for _ in range(T)]
+    att = [torch.empty(B, E, device=DEV) for _ in range(T)]
+    L.call("rs_side_pool_fwd_multi", L.ptr(y), H, B * H, B, E, H, T,
+           _ptrs([z[:, t * E:] for t in range(T)]), z.shape[1], _ptrs(hid), _ptrs(att), st)
+    dy = torch.empty_like(y)
+    dz = torch.full_like(z, 7.0)
+    L.call("rs_side_pool_bwd_multi", L.ptr(y), H, B * H, B, E, H, T, _ptrs(att), _ptrs(ups),
+           L.ptr(dy), _ptrs([dz[:, t * E:] for t in range(T)]), z.shape[1], st)
+    side = y.transpose(0, 1)
+    gsum = None
+    for t in range(T):
+        logit = z[:, t * E:(t + 1) * E].clone().requires_grad_()
+        s = side.detach().requires_grad_()
+        out = side_pool(s, logit.unsqueeze(1)).squeeze(1)
+        assert torch.equal(out.detach(), hid[t])
+        out.backward(ups[t])
+        assert torch.equal(logit.grad, dz[:, t * E:(t + 1) * E])
+        gsum = s.grad.clone() if gsum is None else gsum + s.grad
+    assert torch.equal(gsum.transpose(0, 1).contiguous(), dy)
+    assert bool((dz[:, T * E:] == 7.0).all())  # columns past the tasks' blocks untouched
+
+
+def test_mmoe_fused_block_matches_separate_nodes(monkeypatch):
+    """MMOE's experts / gates / poolings as one node (_ExpertsGatesFn) against the same model run
+    through the separate nodes: outputs and every parameter and input gradient equal within
+    fp32 GEMM rounding (the two paths reach the library GEMMs with different shapes)."""
+    from recommender_amd.esmm import mmoe as M
+
+    vocab = {k: 500 for k in FEAT_VOCAB}
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(M, "_FUSED", fused)
+        gen = torch.Generator(device=DEV).manual_seed(4)
+        model = build("MMOE", vocab, 18, DEV, gen)
+        x = torch.randn(4096, len(vocab) * 18, device=DEV,
+                        generator=torch.Generator(device=DEV).manual_seed(5)).requires_grad_()
+        outs = model._towers(x)
+        up = torch.Generator(device=DEV).manual_seed(6)
+        loss = sum((o * torch.randn(o.shape, device=DEV, generator=up)).sum() for o in outs)
+        loss.backward()
+        grads = [x.grad] + [p.grad for n, p in model.named_parameters()
+                            if p.grad is not None and "embedding" not in n]
+        res.append(([o.detach() for o in outs], grads))
+    (o1, g1), (o2, g2) = res
+    assert len(g1) == len(g2)
+    for a, b in zip(o1, o2):
+        assert_close_rel(a.cpu(), b.cpu(), rtol=1e-5)
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        assert_close_rel(a.cpu(), b.cpu(), rtol=1e-4, scale=float(b.abs().max()) * 1e-3,
+                         msg=f"grad {i}")

@@ -1,5 +1,5 @@
 """Which torch ops a model's graph-captured step records besides the engine's kernels: runs one
-eager static_step of the cfg3 DIEN (or --model pinsage / deepfm) under torch.profiler (CPU
+eager static_step of the cfg3 DIEN (or one step of --model esmm / mmoe at cfg4 size, or a PinSage static step with its sampling) under torch.profiler (CPU
 activity only: the aten calls, with input shapes) and prints the count and shapes of the
 memory-moving glue (add, copy_, cat, stack, fill_, zero_, clone, contiguous, mul, sum). Every
 such call is one kernel / memcpy node in the replayed graph. GPU box: python tools/op_census.py"""
@@ -38,12 +38,46 @@ def dien_step():
     return lambda: step.static_step(feats, label)
 
 
+def multitask_step(name):
+    from recommender_amd.esmm import FEAT_VOCAB
+    from recommender_amd.esmm.train import MultiTaskStep, build
+    from recommender_amd.gemm_tuning import use_tuned_gemms
+    from recommender_amd.synthetic import aliccp_batch, scaled_vocab
+
+    use_tuned_gemms()
+    rng = np.random.default_rng(4)
+    vocab = scaled_vocab(FEAT_VOCAB, 40_000_000)
+    m = build(name.upper(), vocab, 18, "cuda")
+    step = MultiTaskStep(m, "lazy_adam")
+    f, lab = aliccp_batch(rng, 65536, vocab)
+    feats = {k: torch.from_numpy(v).cuda() for k, v in f.items()}
+    label = torch.from_numpy(lab).cuda()
+    return lambda: step(feats, label)
+
+
+def pinsage_step():
+    from recommender_amd.pinsage import PinSageModel, PinSageSampler
+    from recommender_amd.pinsage.train import ML20M, PinSageStep, build_graph
+
+    g = build_graph(ML20M, 4)
+    m = PinSageModel(g, g.itype, 2, 8, 32, 16)
+    train = PinSageStep(m)
+    smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
+    ctr = {"it": 0}
+
+    def fn():
+        ctr["it"] += 1
+        return train.static_step(*smp.sample_static(*smp.sample_pairs_static(4096, 4, ctr["it"])))
+    return fn
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien"])
+    ap.add_argument("--model", default="dien", choices=["dien", "esmm", "mmoe", "pinsage"])
     args = ap.parse_args()
     L.load()
-    fn = {"dien": dien_step}[args.model]()
+    fn = (dien_step() if args.model == "dien" else pinsage_step() if args.model == "pinsage"
+          else multitask_step(args.model))
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
