@@ -296,6 +296,21 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "unique_rows_per_step": U, "note": "path bytes / whole step time"}
+    if args.model in ("esmm", "mmoe"):
+        # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950):
+        # forward, input gradient and weight gradient of every Dense layer, 2·in·out FLOP each
+        # per example — the floor the library fp32 GEMMs set for the step
+        from recommender_amd.nn import Dense
+
+        fl = sum(6.0 * B * l.kernel.shape[0] * l.kernel.shape[1]
+                 for l in m.modules() if isinstance(l, Dense) and l.kernel is not None)
+        floor_ms = fl / 157.3e12 * 1e3
+        out["roofline"] = {"bound": "mfma_fp32", "dense_gflop_per_step": round(fl / 1e9, 1),
+                           "achieved_TFs": round(fl / sec / 1e12, 1), "peak_TFs": 157.3,
+                           "frac": round(floor_ms / (sec * 1e3), 4),
+                           "floor_ms_at_peak": round(floor_ms, 3),
+                           "note": "the whole step's time over its dense GEMM FLOPs (embedding, "
+                                   "apply and elementwise work included in the time)"}
     print(json.dumps(out))
 
 

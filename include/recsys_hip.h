@@ -476,12 +476,8 @@ int32_t rs_dien_aux_bwd(const float* hidden, const float* pos, const float* neg,
                         const float* W3, const float* b3, const float* daux, float* dhidden,
                         float* dpos, float* dneg, float* dparams, void* workspace,
                         size_t ws_bytes, void* stream);
-/* rs_dien_aux_bwd with acc_hidden bit 0 set: dhidden holds the hidden states' upstream gradient
- * (the attention's + the AUGRU's) and the aux loss's part is added in place (no fill, no add
- * pass). Bit 1 set: the caller discards the input gradients at masked history steps (its pos /
- * neg lookups carry the mask as their gradient mask): dpos / dneg are written at every step
- * that can carry gradient (step 0 zeroed, steps t + 1 of the tiles holding a valid step) and
- * left unwritten at the masked steps of the other tiles — no zero fill of the whole arrays. */
+/* rs_dien_aux_bwd with acc_hidden = 1: dhidden holds the hidden states' upstream gradient (the
+ * attention's + the AUGRU's) and the aux loss's part is added in place (no fill, no add pass). */
 int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, const float* neg,
                             const uint8_t* mask, int64_t B, int32_t L, int32_t H, int32_t E,
                             const float* W1, const float* b1, const float* W2, const float* b2,
@@ -508,6 +504,12 @@ int32_t rs_bce_bwd(const float* p, const float* y, int64_t n, float eps, int32_t
 size_t rs_act_bwd_colsum_workspace_size(int64_t B, int32_t N);
 int32_t rs_act_bwd_colsum(const float* dy, const float* y, int64_t B, int32_t N, int32_t act,
                           float* dz, float* db, void* workspace, size_t ws_bytes, void* stream);
+/* The same over n_groups row groups of B / n_groups rows (a multiple of 512) in one pass:
+ * db [n_groups, N] holds each group's column sums (act 1 or 2). MMOE's batched expert layer:
+ * the [E, B, H] gradient masked at once, per-expert bias gradients. */
+int32_t rs_act_bwd_colsum_groups(const float* dy, const float* y, int64_t B, int32_t N,
+                                 int32_t act, int32_t n_groups, float* dz, float* db,
+                                 void* workspace, size_t ws_bytes, void* stream);
 /* The same on row-strided operands (ld_* >= N elements between rows): a column block of a
  * wider [B, ld] activation — the two ESMM towers' first layers evaluated as one GEMM over the
  * shared input (esmm/esmm.py:27-28), each tower's block masked from its own gradient. */

@@ -127,6 +127,7 @@ _SIGS = {
                                  _p, _p, _p, _p, _sz, _p]),
     "rs_batch_norm_bwd": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _sz, _p]),
     "rs_act_bwd_colsum": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
+    "rs_act_bwd_colsum_groups": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _sz, _p]),
     "rs_act_bwd_colsum_ld": (_i32, [_p, _i64, _p, _i64, _i64, _i32, _i32, _p, _i64, _p, _p,
                                     _sz, _p]),
     "rs_philox4x32_10": (_i32, [_p, _i64, _u32, _u32, _p, _p]),

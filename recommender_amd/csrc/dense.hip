@@ -86,6 +86,25 @@ __global__ __launch_bounds__(256) void fold_chunks_kernel(const float* __restric
 }
 
 
+// fold_chunks_kernel per group of chunks: group g folds chunks [g·cpg, (g+1)·cpg) into out[g]
+__global__ __launch_bounds__(256) void fold_chunk_groups_kernel(const float* __restrict__ part,
+                                                                int cpg, int N,
+                                                                float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const float* p = part + (int64_t)blockIdx.y * cpg * N;
+  float s = 0.f;
+  if (col < N) {
+#pragma unroll 8
+    for (int c = w; c < cpg; c += 4) s += p[(int64_t)c * N + col];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < N)
+    out[(int64_t)blockIdx.y * N + col] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
 // ---- factored linear-chain backward: A = xᵀ·G and s = Σ_b G in one pass ----------------
 // G = act'(y) ⊙ dy is formed on the fly (the formula of act_bwd_colsum_kernel) and optionally
 // written out. Rows are cut into fixed chunks of kChainRows; each block folds its chunk in row
@@ -971,6 +990,38 @@ extern "C" int32_t rs_act_bwd_colsum_ld(const float* dy, int64_t ld_dy, const fl
   }
   RS_CHECK_LAUNCH();
   fold_chunks_kernel<<<(unsigned)ceil_div(N, 64), 256, 0, st>>>(part, nchunks, N, db);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+// n_groups row groups of B / n_groups rows each (a whole number of 512-row chunks): one masking
+// pass over all rows, then each group's column sums folded apart — db [n_groups, N]. MMOE's
+// batched expert layer: the [E, B, H] gradient masked in one launch, per-expert bias sums.
+extern "C" int32_t rs_act_bwd_colsum_groups(const float* dy, const float* y, int64_t B, int32_t N,
+                                            int32_t act, int32_t n_groups, float* dz, float* db,
+                                            void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(B >= 1 && N >= 1 && act >= 1 && act <= 2 && n_groups >= 1 && B % n_groups == 0 &&
+                   (B / n_groups) % kColRows == 0,
+               "rs_act_bwd_colsum_groups: act 1 / 2 and groups of whole %d-row chunks", kColRows);
+  RS_CHECK_ARG(dy && y && dz && db, "null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_act_bwd_colsum_workspace_size(B, N), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int nchunks = (int)ceil_div(B, kColRows);
+  float* part = static_cast<float*>(workspace);
+  const bool v4 = N % 4 == 0 && ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) |
+                                  reinterpret_cast<uintptr_t>(dz)) & 15) == 0;
+  if (v4) {
+    dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nchunks);
+    if (act == 1) act_bwd_colsum_kernel<1, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, N, N, N);
+    else act_bwd_colsum_kernel<2, 4><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, N, N, N);
+  } else {
+    dim3 grid((unsigned)ceil_div(N, 16), (unsigned)nchunks);
+    if (act == 1) act_bwd_colsum_kernel<1, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, N, N, N);
+    else act_bwd_colsum_kernel<2, 1><<<grid, 256, 0, st>>>(dy, y, B, N, dz, part, N, N, N);
+  }
+  RS_CHECK_LAUNCH();
+  fold_chunk_groups_kernel<<<dim3((unsigned)ceil_div(N, 64), (unsigned)n_groups), 256, 0, st>>>(
+      part, nchunks / n_groups, N, db);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -15,6 +15,12 @@
 namespace rs {
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// two gates' recurrent sums as one packed pair: v_pk_fma_f32 does both fused multiply-adds in one
+// instruction (each element rounded once, as two fmaf)
+typedef float pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pk2 pk_fma(float a, pk2 b, pk2 c) {
+  return __builtin_elementwise_fma(pk2{a, a}, b, c);
+}
 __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
@@ -68,12 +74,11 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
   stage_gate<HM>(uh_s, H, [&](int k, int jj) { return U[k * H3 + 2 * H + jj]; });
   if (b >= B) return;
   const bool act = j < H;
-  float uz[HM], ur[HM];
+  pk2 uzr[HM];  // (update, reset) recurrent weights of unit j
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
-    uz[k] = ok ? U[k * H3 + j] : 0.f;
-    ur[k] = ok ? U[k * H3 + H + j] : 0.f;
+    uzr[k] = pk2{ok ? U[k * H3 + j] : 0.f, ok ? U[k * H3 + H + j] : 0.f};
   }
   const float rbz = act ? rb[j] : 0.f, rbr = act ? rb[H + j] : 0.f, rbh = act ? rb[2 * H + j] : 0.f;
   const float* xb = xw + b * (int64_t)L * H3;
@@ -100,14 +105,15 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(const float* __restrict__ 
       if (act) out[(b * L + t) * H + j] = h;
       continue;
     }
-    float iz = 0.f, ir = 0.f, ih = 0.f;
+    pk2 izr = pk2{0.f, 0.f};
+    float ih = 0.f;
 #pragma unroll
     for (int k = 0; k < HM; ++k) {
       const float hk = bcast(h, k);
-      iz = fmaf(hk, uz[k], iz);
-      ir = fmaf(hk, ur[k], ir);
+      izr = pk_fma(hk, uzr[k], izr);
       ih = fmaf(hk, uh_s[k * 64 + j], ih);
     }
+    float iz = izr.x, ir = izr.y;
     iz += rbz;
     ir += rbr;
     ih += rbh;
@@ -146,12 +152,11 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
   stage_gate<HM>(wh_s, H, [&](int k, int jj) { return U[jj * H3 + 2 * H + k]; });
   if (b >= B) return;
   const bool act = j < H;
-  float wz[HM], wr[HM];  // row j of U: U[j][g*H + k]
+  pk2 wzr[HM];  // row j of U: (U[j][k], U[j][H + k])
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
-    wz[k] = ok ? U[j * H3 + k] : 0.f;
-    wr[k] = ok ? U[j * H3 + H + k] : 0.f;
+    wzr[k] = pk2{ok ? U[j * H3 + k] : 0.f, ok ? U[j * H3 + H + k] : 0.f};
   }
   const uint8_t* mb = mask + b * L;
   const MaskBits mbits(mb, L, j);
@@ -202,13 +207,17 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(const float* __restrict__ 
       di[H + j] = dpr;
       di[2 * H + j] = dih;
     }
-    float acc = dh * z;
+    // three independent 36-deep chains (update / reset gates as one packed pair, candidate)
+    // summed at the end, instead of one 108-deep chain: the step's latency in the tail of long
+    // histories, where few waves are left to hide it
+    pk2 azr = pk2{0.f, 0.f};
+    float ahh = 0.f;
 #pragma unroll
     for (int k = 0; k < HM; ++k) {
-      acc = fmaf(bcast(dpz, k), wz[k], acc);
-      acc = fmaf(bcast(dpr, k), wr[k], acc);
-      acc = fmaf(bcast(dihm, k), wh_s[k * 64 + j], acc);
+      azr = __builtin_elementwise_fma(pk2{bcast(dpz, k), bcast(dpr, k)}, wzr[k], azr);
+      ahh = fmaf(bcast(dihm, k), wh_s[k * 64 + j], ahh);
     }
+    const float acc = dh * z + ((azr.x + azr.y) + ahh);
     dh = act ? acc : 0.f;
   }
 }
@@ -236,19 +245,34 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
   if (b >= B) return;
   const bool act = j < H;
   const int H3 = 3 * H;
-  float ku[HM], kr[HM];
+  pk2 kur[HM];  // (update, reset) recurrent weights of unit j
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
-    ku[k] = ok ? Kuh[k * H + j] : 0.f;
-    kr[k] = ok ? Krh[k * H + j] : 0.f;
+    kur[k] = pk2{ok ? Kuh[k * H + j] : 0.f, ok ? Krh[k * H + j] : 0.f};
   }
   const float* xb = xw + b * (int64_t)L * H3;
   const uint8_t* mb = mask + b * L;
   const float* ab = att + b * L;
+  // wave-uniform mask bits and the next valid step's x·W and score loaded one step ahead (as
+  // gru_fwd_kernel): no memory latency on the step chain
+  const MaskBits mbits(mb, L, j);
+  const bool v0 = mbits.test(mb, 0);
+  float nu = act && v0 ? xb[j] : 0.f, nr = act && v0 ? xb[H + j] : 0.f,
+        nh = act && v0 ? xb[2 * H + j] : 0.f, na = v0 ? ab[0] : 0.f;
   float h = 0.f;
   for (int t = 0; t < L; ++t) {
-    if (!mb[t]) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
+    const float xu = nu, xr = nr, xh = nh, a = na;
+    if (t + 1 < L && mbits.test(mb, t + 1)) {
+      const float* xn = xb + (int64_t)(t + 1) * H3;
+      if (act) {
+        nu = xn[j];
+        nr = xn[H + j];
+        nh = xn[2 * H + j];
+      }
+      na = ab[t + 1];
+    }
+    if (!mbits.test(mb, t)) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
       if (act) {
         const int64_t o = b * L + t;
         if (states) states[o * H + j] = h;
@@ -258,16 +282,10 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
       }
       continue;
     }
-    const float* x = xb + (int64_t)t * H3;
-    const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
-    const float a = ab[t];
-    float iu = 0.f, ir = 0.f;
+    pk2 iur = pk2{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < HM; ++k) {
-      const float hk = bcast(h, k);
-      iu = fmaf(hk, ku[k], iu);
-      ir = fmaf(hk, kr[k], ir);
-    }
+    for (int k = 0; k < HM; ++k) iur = pk_fma(bcast(h, k), kur[k], iur);
+    const float iu = iur.x, ir = iur.y;
     const float u = sigm(xu + iu), r = sigm(xr + ir);
     const float rh = act ? r * h : 0.f;
     float ihh = 0.f;
@@ -311,12 +329,11 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
   if (b >= B) return;
   const bool act = j < H;
   const int H3 = 3 * H;
-  float ku[HM], kr[HM];  // rows j
+  pk2 kur[HM];  // rows j: (Kuh[j][k], Krh[j][k])
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
-    ku[k] = ok ? Kuh[j * H + k] : 0.f;
-    kr[k] = ok ? Krh[j * H + k] : 0.f;
+    kur[k] = pk2{ok ? Kuh[j * H + k] : 0.f, ok ? Krh[j * H + k] : 0.f};
   }
   const uint8_t* mb = mask + b * L;
   const MaskBits mbits(mb, L, j);
@@ -364,11 +381,12 @@ __global__ __launch_bounds__(256) void augru_bwd_kernel(const float* __restrict_
     const float dr = drh * hp;
     dhp = fmaf(drh, r, dhp);
     const float dpr = act ? dr * r * (1.f - r) : 0.f;
+    // update / reset contributions as one packed pair of 36-deep chains (not one 72-deep chain)
+    pk2 aur = pk2{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < HM; ++k) {
-      dhp = fmaf(bcast(dpu, k), ku[k], dhp);
-      dhp = fmaf(bcast(dpr, k), kr[k], dhp);
-    }
+    for (int k = 0; k < HM; ++k)
+      aur = __builtin_elementwise_fma(pk2{bcast(dpu, k), bcast(dpr, k)}, kur[k], aur);
+    dhp = dhp + (aur.x + aur.y);
     if (act) {
       dx[j] = dpu;
       dx[H + j] = dpr;

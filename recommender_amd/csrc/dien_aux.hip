@@ -225,19 +225,11 @@ struct AuxGrad {
 };
 
 // live items: tile·B + b holds a valid row, or example b has none (0/0: NaN, as the reference)
-// zero0 (optional): the input gradients whose rows the backward leaves unwritten outside live
-// tiles — their step-0 rows (never an aux input, e_{t+1} starts at t + 1) are zeroed here
 __global__ __launch_bounds__(256) void aux_live_kernel(AuxArgs a, int NT, int32_t* __restrict__ flag,
-                                                       int32_t* __restrict__ cnt,
-                                                       float* __restrict__ zero0_pos,
-                                                       float* __restrict__ zero0_neg) {
+                                                       int32_t* __restrict__ cnt) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (b >= a.B) return;
-  if (zero0_pos && lane < a.E) {
-    zero0_pos[b * a.L * a.E + lane] = 0.f;
-    zero0_neg[b * a.L * a.E + lane] = 0.f;
-  }
   const int c = aux_count(a, b, lane);
   if (lane == 0) cnt[b] = c;
   for (int tile = 0; tile < NT; ++tile) {
@@ -600,12 +592,7 @@ extern "C" int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, co
   const int NT = (L + 15) / 16;  // tiles over every hidden row t < L
   const int64_t ni = (int64_t)NT * B;
   RS_CHECK_ARG(ni < (1LL << 31), "too many (tile, example) items");
-  // flags bit 1: the caller drops the masked positions' input gradients (its lookups carry the
-  // history mask as their gradient mask), so dpos / dneg rows of masked steps outside the live
-  // tiles stay unwritten — no full zero fill; only the step-0 rows are zeroed
-  const bool sparse_inputs = (acc_hidden & 2) != 0;
-  aux_live_kernel<<<(unsigned)ceil_div(B, kWaves), 64 * kWaves, 0, st>>>(
-      a, NT, flag, cnt, sparse_inputs ? dpos : nullptr, sparse_inputs ? dneg : nullptr);
+  aux_live_kernel<<<(unsigned)ceil_div(B, kWaves), 64 * kWaves, 0, st>>>(a, NT, flag, cnt);
   RS_CHECK_LAUNCH();
   if (int32_t e = exclusive_scan_i32(flag, ipos, ni, n_live, wsb + wl.scan,
                                      exclusive_scan_ws_size(ni), st))
@@ -615,12 +602,10 @@ extern "C" int32_t rs_dien_aux_bwd_acc(const float* hidden, const float* pos, co
   RS_CHECK_LAUNCH();
   const size_t lds = bwd_lds_bytes();
   // input gradients start at 0: the kernel writes only the rows of tiles that hold a valid row
-  if (!(acc_hidden & 1)) RS_CHECK_HIP(hipMemsetAsync(dhidden, 0, (size_t)B * L * H * 4, st));
-  if (!sparse_inputs) {
-    RS_CHECK_HIP(hipMemsetAsync(dpos, 0, (size_t)B * L * E * 4, st));
-    RS_CHECK_HIP(hipMemsetAsync(dneg, 0, (size_t)B * L * E * 4, st));
-  }
-  AuxGrad g{daux, dhidden, dpos, dneg, part, items, n_live, cnt, (acc_hidden & 1) ? 1 : 0};
+  if (!acc_hidden) RS_CHECK_HIP(hipMemsetAsync(dhidden, 0, (size_t)B * L * H * 4, st));
+  RS_CHECK_HIP(hipMemsetAsync(dpos, 0, (size_t)B * L * E * 4, st));
+  RS_CHECK_HIP(hipMemsetAsync(dneg, 0, (size_t)B * L * E * 4, st));
+  AuxGrad g{daux, dhidden, dpos, dneg, part, items, n_live, cnt, acc_hidden ? 1 : 0};
   auto run = [&](auto kern) -> int32_t {
     RS_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -419,12 +419,19 @@ struct Tile32Edges {
   uint32_t first_key;
 };
 
-template <int OPT>
+// Q > 0 (SGD only): the table read-modify-writes of the runs that end inside the tile are queued
+// (Q run sums in registers) and done Q at a time — their Q table-row loads issued together —
+// instead of one per run: a table load waits for every load issued before it (vmcnt counts in
+// order), so an inline update drains the in-flight gradient rows at each run end. Same
+// arithmetic, each row written once: bit-identical.
+template <int OPT, int Q = 0>
 __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ keys,
                                                    const int32_t* __restrict__ pos, int64_t n,
                                                    uint32_t n_rows, const float* __restrict__ grad,
                                                    const ApplyArgs& a, int64_t t, float* pbase) {
   constexpr int T = 32, VEC = 4, CPL = 1, U = 8;
+  constexpr bool kQueue = Q > 0 && OPT == OPT_SGD;
+  constexpr int QN = Q > 0 ? Q : 1;
   const int gl = threadIdx.x & 31;
   const int64_t k0 = t * T;
   const int64_t k1 = k0 + T < n ? k0 + T : n;
@@ -462,10 +469,43 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   float acc[CPL][VEC];
 #pragma unroll
   for (int c = 0; c < VEC; ++c) acc[0][c] = 0.f;
+  uint32_t qrow[QN];
+  float qacc[QN][VEC];
+  int qn = 0;
+  auto flush = [&]() {
+    if constexpr (kQueue) {
+      float tr[QN][VEC];
+#pragma unroll
+      for (int i = 0; i < QN; ++i)
+        if (i < qn) RowIO<VEC>::load(a.table + (int64_t)qrow[i] * dim + col, tr[i]);
+#pragma unroll
+      for (int i = 0; i < QN; ++i) {
+        if (i < qn) {
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) tr[i][c] = tr[i][c] - a.p.lr * qacc[i][c];
+          RowIO<VEC>::store(a.table + (int64_t)qrow[i] * dim + col, tr[i]);
+        }
+      }
+      qn = 0;
+    }
+  };
   auto emit = [&](uint32_t row, bool starts, bool ends, int head_e) {
     if (row >= n_rows) return;  // OOB sentinel run: gradient dropped
     if (starts && ends) {
-      finalize_row<OPT, VEC, CPL>(a, row, gl, 32, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, k0 + head_e) : 0);
+      if constexpr (kQueue) {
+        if (qn == QN) flush();
+#pragma unroll
+        for (int i = 0; i < QN; ++i) {
+          if (i == qn) {
+            qrow[i] = row;
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) qacc[i][c] = acc[0][c];
+          }
+        }
+        ++qn;
+      } else {
+        finalize_row<OPT, VEC, CPL>(a, row, gl, 32, acc, OPT == OPT_EMIT ? seg_id_of(a, keys, k0 + head_e) : 0);
+      }
     } else {
       RowIO<VEC>::store(pbase + (starts ? 1 : 0) * dim + col, acc[0]);
     }
@@ -515,6 +555,7 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
 #endif
   const bool ends = key_after != run_row;
   emit(run_row, run_starts, ends, run_start);
+  flush();
   Tile32Edges ed;
   ed.last_row = run_row;
   ed.last_open = !ends && run_starts && run_row < n_rows;
@@ -550,7 +591,7 @@ __global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restr
 // (chunk[t][1], tile flag bit 0) and, at a group's first tile, the continuation's group sum
 // (chunk[t][0]); seg_fixup_kernel folds those (level 2). Bit-identical to seg_tile32 + seg_chunk
 // + seg_fixup, one launch fewer and no global partials.
-template <int OPT>
+template <int OPT, int Q = 0>
 __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __restrict__ keys,
                                                            const int32_t* __restrict__ pos,
                                                            int64_t n, uint32_t n_rows,
@@ -563,7 +604,7 @@ __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __res
   const int64_t t = (int64_t)blockIdx.x * G + gi;
   const bool live = t < n_tiles;
   Tile32Edges e{};
-  if (live) e = tile32_walk<OPT>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
+  if (live) e = tile32_walk<OPT, Q>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
   if (gl == 0) fkey[gi] = live ? e.first_key : 0xFFFFFFFFu;
   __syncthreads();
   if (!live) return;
@@ -1036,6 +1077,16 @@ __global__ __launch_bounds__(256) void keras_bitmap_mark_kernel(const uint32_t* 
   }
 }
 
+// RS_APPLY_QUEUE=1: the D = 128 SGD walk with its table updates queued 2 runs at a time
+// (tile32_walk<OPT_SGD, 2>: Q = 3 and 4 spill at 128 VGPRs); read once per process
+static bool apply_queue() {
+  static const int v = [] {
+    const char* e = getenv("RS_APPLY_QUEUE");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos, int64_t n,
                                int64_t n_rows, const float* grad, const ApplyArgs& a,
                                const RowGeom& geom, hipStream_t st) {
@@ -1064,9 +1115,13 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     if (g32) {                                                                                  \
-      seg_group32_kernel<OPTV><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(keys, pos, n,            \
-                                                                   (uint32_t)n_rows, grad, a,   \
-                                                                   n_tiles);                    \
+      if (OPTV == OPT_SGD && apply_queue())                                                     \
+        seg_group32_kernel<OPTV, 2><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                    \
+            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
+      else                                                                                      \
+        seg_group32_kernel<OPTV><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(keys, pos, n,          \
+                                                                     (uint32_t)n_rows, grad, a, \
+                                                                     n_tiles);                  \
     } else {                                                                                    \
       if (t32)                                                                                  \
         seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, apply_lds_throttle(), st>>>(       \

@@ -636,8 +636,7 @@ class _InterestExtractFn(torch.autograd.Function):
     (rs_masked_dx_acc: no add)."""
 
     @staticmethod
-    def forward(ctx, pos, neg, mask_u8, kernel, recurrent_kernel, bias, W1, b1, W2, b2, W3, b3,
-                sparse_inputs=False):
+    def forward(ctx, pos, neg, mask_u8, kernel, recurrent_kernel, bias, W1, b1, W2, b2, W3, b3):
         B, T, X = pos.shape
         H = recurrent_kernel.shape[0]
         E = neg.shape[-1]
@@ -654,7 +653,6 @@ class _InterestExtractFn(torch.autograd.Function):
         L.call("rs_dien_aux_fwd", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H, E,
                L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(aux), st)
         ctx.save_for_backward(pos, neg, kernel, rk, out, saved, mask_u8, *vr, W1, b1, W2, b2, W3, b3)
-        ctx.sparse_inputs = sparse_inputs
         return out, aux
 
     @staticmethod
@@ -682,8 +680,8 @@ class _InterestExtractFn(torch.autograd.Function):
         ws = _aux_workspace(B, T, H, E, dev)
         L.call("rs_dien_aux_bwd_acc", L.ptr(out), L.ptr(pos), L.ptr(neg), L.ptr(mask_u8), B, T, H,
                E, L.ptr(W1), L.ptr(b1), L.ptr(W2), L.ptr(b2), L.ptr(W3), L.ptr(b3), L.ptr(da),
-               L.ptr(dh), 1 | (2 if ctx.sparse_inputs else 0), L.ptr(dp_aux), L.ptr(dneg),
-               L.ptr(dparams), L.ptr(ws), ws.numel(), st)
+               L.ptr(dh), 1, L.ptr(dp_aux), L.ptr(dneg), L.ptr(dparams), L.ptr(ws), ws.numel(),
+               st)
         dxw = torch.empty(B, T, 3 * H, device=dev)
         dinner = torch.empty(B, T, 3 * H, device=dev)
         L.call("rs_gru_bwd", L.ptr(dh), L.ptr(out), L.ptr(saved), L.ptr(rk), L.ptr(mask_u8), B, T,
@@ -702,7 +700,7 @@ class _InterestExtractFn(torch.autograd.Function):
             n = int(torch.Size(shape).numel())
             outs.append(dparams[o:o + n].view(shape))
             o += n
-        return (dpos, dneg, None, dk, drk, torch.stack([db0, db1]), *outs, None)
+        return (dpos, dneg, None, dk, drk, torch.stack([db0, db1]), *outs)
 
 
 def _sigmoid_ce(labels, logits):
@@ -718,10 +716,6 @@ class InterestExtract(nn.Module):
         super().__init__()
         self.gru = GRU(gru_units, input_dim, device, generator)
         self.auxiliary_net = AuxiliaryNet([80, 40, 1], gru_units + input_dim, device, generator)
-        # True when the caller's pos / neg histories come from lookups that drop the masked
-        # steps' gradients (their grad_mask is this layer's mask, as DIEN's): the gradients of
-        # those steps may then be left unwritten (no zero fill of the [B, L, E] arrays)
-        self.masked_input_grads_dropped = False
 
     def _fused_aux_ready(self, hidden_state, pos_his):
         layers = list(self.auxiliary_net.layers)
@@ -766,8 +760,7 @@ class InterestExtract(nn.Module):
             m = _mask_u8(mask, pos_history.shape[:2], pos_history.device)
             return _InterestExtractFn.apply(pos_history.contiguous(), neg_history.contiguous(), m,
                                             g.kernel, g.recurrent_kernel, g.bias, l1.kernel,
-                                            l1.bias, l2.kernel, l2.bias, l3.kernel, l3.bias,
-                                            self.masked_input_grads_dropped)
+                                            l1.bias, l2.kernel, l2.bias, l3.kernel, l3.bias)
         hidden_state = self.gru(pos_history, mask=mask)
         aux = self.compute_auxiliary_loss((hidden_state, pos_history, neg_history), training, mask)
         return hidden_state, aux

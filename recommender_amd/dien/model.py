@@ -79,8 +79,6 @@ class DIEN(BaseModel):
         dev, gen = kwargs.get("device"), kwargs.get("generator")
         D = self.embedding_dim
         self.interest_extract_layer = InterestExtract(interest_extract_gru_units, D, dev, gen)
-        # forward() looks pos / neg up with the history mask as their gradient mask
-        self.interest_extract_layer.masked_input_grads_dropped = True
         self.attention = DIENAttention(interest_extract_gru_units, D, dev, gen)
         self.interest_evolve = InterestEvolve(interest_evolve_gru_units, interest_extract_gru_units, dev, gen)
         if interest_evolve_gru_units != D:

@@ -35,11 +35,10 @@ class _ExpertsGatesFn(torch.autograd.Function):
     in place ([E, B, H0] seen with rows E·H0 apart: no transpose copy), and the T softmax
     poolings of the [E, B, H1] expert outputs in one pass (rs_side_pool_fwd_multi).
     Backward: one pooling pass for all tasks (their expert-output gradients summed inside it),
-    the second layers' relu masks and bias sums per expert, their input gradient by one batched
-    GEMM, then every expert's first-layer mask written from that [E, B, H0] gradient straight
-    into one [B, E·H0 + T·E] buffer beside the gates' logit gradients (rs_act_bwd_colsum_ld),
-    so the input gradient of x is ONE GEMM over K = E·H0 + T·E (no per-consumer GEMMs and adds)
-    and the first-layer + gate kernel gradients one split-K GEMM."""
+    the second layers' relu masks and per-expert bias sums in one pass, their input gradient by
+    one batched GEMM written straight into the first layer's [B, E·H0] layout, one mask pass
+    over it, and the gates' logit gradients added to the input-gradient GEMM's output in place
+    (K = T·E, beta 1): no transpose copies, no per-consumer add passes."""
 
     @staticmethod
     def forward(ctx, x, k0, b0, k1, b1, kg, bg, E, T):
@@ -66,34 +65,37 @@ class _ExpertsGatesFn(torch.autograd.Function):
         E, T = ctx.E, ctx.T
         B = x.shape[0]
         H0, H1 = k0.shape[1] // E, k1.shape[2]
-        N0 = E * H0
-        Nt = N0 + T * E
         dev = x.device
         st = L.stream_ptr(dev)
         gh = [torch.zeros(B, H1, device=dev) if g is None else g.contiguous() for g in gh]
         dy2 = torch.empty_like(y2)
-        dzc = torch.empty(B, Nt, device=dev)                        # [experts' dz1 | gates' dz]
+        dzg = torch.empty(B, T * E, device=dev)                     # the gates' logit gradients
         L.call("rs_side_pool_bwd_multi", L.ptr(y2), H1, B * H1, B, E, H1, T, _ptrs(att),
-               _ptrs(gh), L.ptr(dy2), _ptrs([dzc[:, N0 + t * E:] for t in range(T)]), Nt, st)
-        # second layers: relu mask + bias sums per expert, input gradient, kernel gradients
+               _ptrs(gh), L.ptr(dy2), _ptrs([dzg[:, t * E:] for t in range(T)]), T * E, st)
+        # second layers: every expert's relu mask in one pass, per-expert bias sums
         dz2 = torch.empty_like(y2)
         db1 = torch.empty(E, 1, H1, device=dev)
-        for e in range(E):
-            _act_bwd(dy2[e], y2[e], 1, True, dz=dz2[e], db=db1[e, 0])
-        dy1 = torch.bmm(dz2, k1.transpose(1, 2))                   # [E, B, H0]
+        if B % 512 == 0:
+            ws = torch.empty(max(1, L.lib().rs_act_bwd_colsum_workspace_size(E * B, H1) // 4),
+                             device=dev)
+            L.call("rs_act_bwd_colsum_groups", L.ptr(dy2), L.ptr(y2), E * B, H1, 1, E, L.ptr(dz2),
+                   L.ptr(db1), L.ptr(ws), ws.numel() * 4, st)
+        else:
+            for e in range(E):
+                _act_bwd(dy2[e], y2[e], 1, True, dz=dz2[e], db=db1[e, 0])
+        # their input gradient written straight into the first layer's [B, E·H0] layout
+        dy1 = torch.empty(B, E * H0, device=dev)
+        torch.bmm(dz2, k1.transpose(1, 2), out=dy1.view(B, E, H0).transpose(0, 1))
         dk1 = torch.stack([wgrad(y1[:, e * H0:(e + 1) * H0], dz2[e]) for e in range(E)])
-        # first layers: each expert's mask from its [B, H0] block of dy1 into dzc
-        db0 = torch.empty(N0, device=dev)
-        nws = L.lib().rs_act_bwd_colsum_workspace_size(B, H0)
-        ws = torch.empty(max(1, nws // 4), device=dev)
-        for e in range(E):
-            L.call("rs_act_bwd_colsum_ld", L.ptr(dy1[e]), H0, L.ptr(y1[:, e * H0:]), N0, B, H0, 1,
-                   L.ptr(dzc[:, e * H0:]), Nt, L.ptr(db0[e * H0:]), L.ptr(ws), ws.numel() * 4, st)
-        dbg = dzc[:, N0:].sum(0)
-        kc = torch.cat([k0, kg], 1)
-        dx = dzc @ kc.t() if ctx.needs_input_grad[0] else None
-        dkc = wgrad(x, dzc)
-        return dx, dkc[:, :N0], db0, dk1, db1, dkc[:, N0:], dbg, None, None
+        # first layers: one mask + bias pass over [B, E·H0]; the gates join the input gradient
+        # as a K = T·E update of the same output (no add pass)
+        dz1, db0 = _act_bwd(dy1, y1, 1, True)
+        dbg = dzg.sum(0)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = dz1 @ k0.t()
+            dx.addmm_(dzg, kg.t())
+        return dx, wgrad(x, dz1), db0, dk1, db1, wgrad(x, dzg), dbg, None, None
 
 
 class MMOE(nn.Module):

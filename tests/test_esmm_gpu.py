@@ -372,5 +372,8 @@ def test_mmoe_fused_block_matches_separate_nodes(monkeypatch):
     for a, b in zip(o1, o2):
         assert_close_rel(a.cpu(), b.cpu(), rtol=1e-5)
     for i, (a, b) in enumerate(zip(g1, g2)):
-        assert_close_rel(a.cpu(), b.cpu(), rtol=1e-4, scale=float(b.abs().max()) * 1e-3,
+        # each element within 1e-5 of the tensor's largest: the input gradient is a sum over
+        # K = E·H0 + T·E = 1616 terms (one GEMM) against the same sum split over three GEMMs and
+        # two adds — near-cancelling elements differ by fp32 rounding of the largest terms
+        assert_close_rel(a.cpu(), b.cpu(), rtol=1e-4, scale=float(b.abs().max()) * 1e-1,
                          msg=f"grad {i}")
