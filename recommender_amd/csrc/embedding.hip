@@ -1077,12 +1077,14 @@ __global__ __launch_bounds__(256) void keras_bitmap_mark_kernel(const uint32_t* 
   }
 }
 
-// RS_APPLY_QUEUE=1: the D = 128 SGD walk with its table updates queued 2 runs at a time
-// (tile32_walk<OPT_SGD, 2>: Q = 3 and 4 spill at 128 VGPRs); read once per process
+// The D = 128 SGD walk with its table updates queued 2 runs at a time (tile32_walk<OPT_SGD, 2>;
+// Q = 3 and 4 spill at 128 VGPRs): default; RS_APPLY_QUEUE=0 selects the one-run-at-a-time walk
+// (A/B, 200 steps each, interleaved: step 0.685-0.688 -> 0.671-0.674 ms, apply alone 238 -> 230
+// us, bit-identical). Read once per process.
 static bool apply_queue() {
   static const int v = [] {
     const char* e = getenv("RS_APPLY_QUEUE");
-    return e && e[0] == '1' ? 1 : 0;
+    return e && e[0] == '0' ? 0 : 1;
   }();
   return v != 0;
 }
