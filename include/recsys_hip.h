@@ -537,6 +537,38 @@ int32_t rs_batch_norm_bwd(const float* dy, const float* x, int64_t B, int32_t C,
                           void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Multi-hot mean lookup (PinSage FeatureProjector's genre, pinsage/train/layers.py:68-81):
+ * out[n, :] = (Σ_g table[mh[items[n], g], :]) / G for the items' G-slot id rows of mh
+ * [n_items, G] int32 (ids outside [0, V) read 0 and set RS_ERRBIT_OOB). Backward: the dense
+ * [V, D] table gradient Σ_n Σ_{g: id = r} dout[n] / G (deterministic; V·D <= 256, G <= 32). */
+int32_t rs_multihot_mean_fwd(const float* table, int32_t V, int32_t D, const int32_t* mh, int32_t G,
+                             const int64_t* items, int64_t N, float* out, int32_t* err_flag,
+                             void* stream);
+size_t rs_multihot_mean_bwd_workspace_size(int64_t N, int32_t V, int32_t D);
+int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int64_t* items, int64_t N,
+                             const float* dout, int32_t V, int32_t D, float* dtable,
+                             void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * PinSage's item2item scores and margin loss in one pass (pinsage/train/model.py:14-19,
+ * pinsage/train/train.py:17-20): pos_score[i] = h[pos_src[i]]·h[pos_dst[i]], neg_score likewise,
+ * loss[0] = Σ_{live i} max((neg + delta) - pos, 0) / n_live (valid: uint8 per pair or null =
+ * all live; n_live: device int32 [1] or null = n_pairs; -1 node ids score node 0, as padding).
+ * Backward: dh += the loss's gradient (dloss: device float [1]) scattered with float atomics
+ * (dh zeroed by the caller; the index_add of the gathers it replaces is atomic too). D <= 64. */
+size_t rs_pair_margin_workspace_size(int64_t n_pairs);
+int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
+                           const int32_t* pos_dst, const int32_t* neg_src, const int32_t* neg_dst,
+                           int64_t n_pairs, float delta, const uint8_t* valid,
+                           const int32_t* n_live, float* pos_score, float* neg_score, float* loss,
+                           void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
+                           const int32_t* pos_dst, const int32_t* neg_src, const int32_t* neg_dst,
+                           int64_t n_pairs, float delta, const uint8_t* valid,
+                           const int32_t* n_live, const float* pos_score, const float* neg_score,
+                           const float* dloss, float* dh, int64_t ldd, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * PinSage sampling + aggregation. The graph is the bipartite
  * item/user CSR in both directions: i2u_indptr [n_items+1] int64, i2u_idx int32 user ids,
  * u2i_indptr [n_users+1], u2i_idx item ids. Randomness is Philox4x32-10 keyed by `seed`

@@ -159,6 +159,14 @@ _SIGS = {
     "rs_match_logits_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _i64, _p, _p, _p]),
     "rs_side_pool_fwd_strided": (_i32, [_p, _i64, _i64, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd_strided": (_i32, [_p, _i64, _i64, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "rs_pair_margin_workspace_size": (_sz, [_i64]),
+    "rs_multihot_mean_fwd": (_i32, [_p, _i32, _i32, _p, _i32, _p, _i64, _p, _p, _p]),
+    "rs_multihot_mean_bwd_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "rs_multihot_mean_bwd": (_i32, [_p, _i32, _p, _i64, _p, _i32, _i32, _p, _p, _sz, _p]),
+    "rs_pair_margin_fwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64, C.c_float, _p, _p, _p, _p,
+                                  _p, _p, _sz, _p]),
+    "rs_pair_margin_bwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64, C.c_float, _p, _p, _p, _p,
+                                  _p, _p, _i64, _p]),
     "rs_side_pool_fwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _i64, _p, _p,
                                       _p]),
     "rs_side_pool_bwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p,

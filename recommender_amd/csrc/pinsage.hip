@@ -526,9 +526,226 @@ inline uint32_t stop_threshold(float p) {
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
+// ---- item2item scores + margin loss (pinsage/train/model.py:14-19, train.py:17-20) -------
+// score(u, v) = h[u]·h[v] for the positive and the negative pair of each example, hinge =
+// max((neg + delta) - pos, 0) over the live pairs, loss = Σ hinge / n_live. One thread per pair
+// (D <= 64 row elements, products rounded then summed in order, as the mul + sum it replaces);
+// the block sums folded in block order (deterministic). Padding pairs (src or dst -1) score
+// node 0 and carry no weight, as the capacity-shaped batch's clamp + mask did.
+constexpr int kPairThreads = 256;
+
+__device__ __forceinline__ float row_dot(const float* __restrict__ h, int64_t ld, int D, int u,
+                                         int v) {
+  const float* a = h + (int64_t)u * ld;
+  const float* b = h + (int64_t)v * ld;
+  float s = 0.f;
+  for (int d = 0; d < D; ++d) s += a[d] * b[d];
+  return s;
+}
+
+__global__ __launch_bounds__(kPairThreads) void pair_margin_fwd_kernel(
+    const float* __restrict__ h, int64_t ld, int D, const int32_t* __restrict__ ps,
+    const int32_t* __restrict__ pd, const int32_t* __restrict__ ns, const int32_t* __restrict__ nd,
+    int64_t P, float delta, const uint8_t* __restrict__ valid, float* __restrict__ pos,
+    float* __restrict__ neg, float* __restrict__ part) {
+  __shared__ float red[kPairThreads];
+  const int64_t i = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
+  float w = 0.f;
+  if (i < P) {
+    const float p = row_dot(h, ld, D, max(ps[i], 0), max(pd[i], 0));
+    const float q = row_dot(h, ld, D, max(ns[i], 0), max(nd[i], 0));
+    pos[i] = p;
+    neg[i] = q;
+    const float hinge = fmaxf((q + delta) - p, 0.f);
+    w = (valid == nullptr || valid[i]) ? hinge : 0.f;
+  }
+  red[threadIdx.x] = w;
+  __syncthreads();
+  for (int o = kPairThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(64) void pair_margin_fold_kernel(const float* __restrict__ part,
+                                                             int nb, const int32_t* __restrict__ n_live,
+                                                             int64_t P, float* __restrict__ loss) {
+  if (threadIdx.x != 0) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[b];
+  loss[0] = s / (float)(n_live ? n_live[0] : P);
+}
+
+// dh += ∂loss/∂h: the hinge's gradient dloss / n_live on live pairs with (neg + delta) - pos >= 0
+// (clamp's backward passes at the boundary), -g to the positive score, +g to the negative one,
+// each score's two rows taking the other row times it — scattered with float atomics, as the
+// index_add of the row gathers it replaces (dh zeroed by the caller).
+__global__ __launch_bounds__(kPairThreads) void pair_margin_bwd_kernel(
+    const float* __restrict__ h, int64_t ld, int D, const int32_t* __restrict__ ps,
+    const int32_t* __restrict__ pd, const int32_t* __restrict__ ns, const int32_t* __restrict__ nd,
+    int64_t P, float delta, const uint8_t* __restrict__ valid, const float* __restrict__ pos,
+    const float* __restrict__ neg, const float* __restrict__ dloss,
+    const int32_t* __restrict__ n_live, float* __restrict__ dh, int64_t ldd) {
+  const int64_t i = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
+  if (i >= P) return;
+  if (valid != nullptr && !valid[i]) return;
+  if (!((neg[i] + delta) - pos[i] >= 0.f)) return;
+  const float g = dloss[0] / (float)(n_live ? n_live[0] : P);
+  const int a = max(ps[i], 0), b = max(pd[i], 0), c = max(ns[i], 0), e = max(nd[i], 0);
+  for (int d = 0; d < D; ++d) {
+    const float ha = h[(int64_t)a * ld + d], hb = h[(int64_t)b * ld + d];
+    const float hc = h[(int64_t)c * ld + d], he = h[(int64_t)e * ld + d];
+    atomicAdd(dh + (int64_t)a * ldd + d, -g * hb);
+    atomicAdd(dh + (int64_t)b * ldd + d, -g * ha);
+    atomicAdd(dh + (int64_t)c * ldd + d, g * he);
+    atomicAdd(dh + (int64_t)e * ldd + d, g * hc);
+  }
+}
+
+// ---- multi-hot mean lookup (FeatureProjector's genre, pinsage/train/layers.py:68-81) --------
+// out[n] = mean_g table[mh[item[n], g]] over the item's G multi-hot slots: the item's id row is
+// read in place (no gathered [N, G] id tensor, no [N, G, D] rows) — a sequential sum over g,
+// then / G. Ids outside [0, V) read 0 and flag RS_ERRBIT_OOB.
+__global__ __launch_bounds__(256) void multihot_mean_fwd_kernel(
+    const float* __restrict__ table, int V, int D, const int32_t* __restrict__ mh, int G,
+    const int64_t* __restrict__ items, int64_t N, float* __restrict__ out, int32_t* err_flag) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * D) return;
+  const int64_t n = e / D;
+  const int d = (int)(e - n * D);
+  const int32_t* row = mh + items[n] * G;
+  float s = 0.f;
+  bool oob = false;
+  for (int g = 0; g < G; ++g) {
+    const int r = row[g];
+    if (r >= 0 && r < V) s += table[(int64_t)r * D + d];
+    else oob = true;
+  }
+  out[e] = s / (float)G;
+  if (oob && err_flag) atomicOr(err_flag, RS_ERRBIT_OOB);
+}
+
+// dtable[r][d] = Σ_n Σ_{g: mh[item[n], g] = r} dout[n][d] / G: a block per 256 items stages their
+// id rows in LDS, thread (r, d) sums its entries in (n, g) order into a block partial; partials
+// folded in block order (deterministic). V·D <= 256, G <= 32.
+constexpr int kMhRows = 256;
+__global__ __launch_bounds__(256) void multihot_mean_bwd_part_kernel(
+    const int32_t* __restrict__ mh, int G, const int64_t* __restrict__ items, int64_t N,
+    const float* __restrict__ dout, int V, int D, float* __restrict__ part) {
+  __shared__ int32_t ids[kMhRows * 32];
+  const int64_t n0 = (int64_t)blockIdx.x * kMhRows;
+  const int rows = (int)(N - n0 < kMhRows ? N - n0 : kMhRows);
+  for (int e = threadIdx.x; e < rows * G; e += blockDim.x) {
+    const int i = e / G, g = e - i * G;
+    ids[i * G + g] = mh[items[n0 + i] * G + g];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= V * D) return;
+  const int r = t / D, d = t - r * D;
+  float acc = 0.f;
+  for (int i = 0; i < rows; ++i) {
+    const float x = dout[(n0 + i) * D + d] / (float)G;
+    for (int g = 0; g < G; ++g)
+      if (ids[i * G + g] == r) acc += x;
+  }
+  part[(int64_t)blockIdx.x * V * D + t] = acc;
+}
+
+__global__ __launch_bounds__(256) void multihot_mean_bwd_fold_kernel(const float* __restrict__ part,
+                                                                    int nb, int VD,
+                                                                    float* __restrict__ dtable) {
+  const int t = threadIdx.x;
+  if (t >= VD) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * VD + t];
+  dtable[t] = s;
+}
+
 }  // namespace rs
 
 using namespace rs;
+
+extern "C" int32_t rs_multihot_mean_fwd(const float* table, int32_t V, int32_t D, const int32_t* mh,
+                                        int32_t G, const int64_t* items, int64_t N, float* out,
+                                        int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(V >= 1 && D >= 1 && G >= 1 && N >= 0, "rs_multihot_mean_fwd: bad sizes");
+  if (N == 0) return RS_OK;
+  RS_CHECK_ARG(table && mh && items && out, "rs_multihot_mean_fwd: null pointer");
+  multihot_mean_fwd_kernel<<<(unsigned)ceil_div(N * D, 256), 256, 0, as_stream(stream)>>>(
+      table, V, D, mh, G, items, N, out, err_flag);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" size_t rs_multihot_mean_bwd_workspace_size(int64_t N, int32_t V, int32_t D) {
+  return (size_t)ceil_div(N < 1 ? 1 : N, kMhRows) * V * D * sizeof(float) + 256;
+}
+
+extern "C" int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int64_t* items,
+                                        int64_t N, const float* dout, int32_t V, int32_t D,
+                                        float* dtable, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  RS_CHECK_ARG(V >= 1 && D >= 1 && V * D <= 256 && G >= 1 && G <= 32 && N >= 1,
+               "rs_multihot_mean_bwd: V·D <= 256, 1 <= G <= 32, N >= 1");
+  RS_CHECK_ARG(mh && items && dout && dtable && workspace, "rs_multihot_mean_bwd: null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_multihot_mean_bwd_workspace_size(N, V, D), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)ceil_div(N, kMhRows);
+  float* part = static_cast<float*>(workspace);
+  multihot_mean_bwd_part_kernel<<<nb, 256, 0, st>>>(mh, G, items, N, dout, V, D, part);
+  RS_CHECK_LAUNCH();
+  multihot_mean_bwd_fold_kernel<<<1, 256, 0, st>>>(part, nb, V * D, dtable);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" size_t rs_pair_margin_workspace_size(int64_t n_pairs) {
+  return (size_t)(ceil_div(n_pairs < 1 ? 1 : n_pairs, kPairThreads)) * sizeof(float) + 256;
+}
+
+extern "C" int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
+                                      const int32_t* pos_dst, const int32_t* neg_src,
+                                      const int32_t* neg_dst, int64_t n_pairs, float delta,
+                                      const uint8_t* valid, const int32_t* n_live, float* pos_score,
+                                      float* neg_score, float* loss, void* workspace,
+                                      size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D, "rs_pair_margin_fwd: bad sizes");
+  RS_CHECK_ARG(h && pos_src && pos_dst && neg_src && neg_dst && pos_score && neg_score && loss &&
+                   workspace,
+               "rs_pair_margin_fwd: null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_pair_margin_workspace_size(n_pairs), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)ceil_div(n_pairs, kPairThreads);
+  float* part = static_cast<float*>(workspace);
+  pair_margin_fwd_kernel<<<nb, kPairThreads, 0, st>>>(h, ld, D, pos_src, pos_dst, neg_src, neg_dst,
+                                                      n_pairs, delta, valid, pos_score, neg_score,
+                                                      part);
+  RS_CHECK_LAUNCH();
+  pair_margin_fold_kernel<<<1, 64, 0, st>>>(part, nb, n_live, n_pairs, loss);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
+                                      const int32_t* pos_dst, const int32_t* neg_src,
+                                      const int32_t* neg_dst, int64_t n_pairs, float delta,
+                                      const uint8_t* valid, const int32_t* n_live,
+                                      const float* pos_score, const float* neg_score,
+                                      const float* dloss, float* dh, int64_t ldd, void* stream) {
+  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D && ldd >= D,
+               "rs_pair_margin_bwd: bad sizes");
+  RS_CHECK_ARG(h && pos_src && pos_dst && neg_src && neg_dst && pos_score && neg_score && dloss &&
+                   dh,
+               "rs_pair_margin_bwd: null pointer");
+  pair_margin_bwd_kernel<<<(unsigned)ceil_div(n_pairs, kPairThreads), kPairThreads, 0,
+                           as_stream(stream)>>>(h, ld, D, pos_src, pos_dst, neg_src, neg_dst,
+                                                n_pairs, delta, valid, pos_score, neg_score, dloss,
+                                                n_live, dh, ldd);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
 
 static Graph make_graph(const int64_t* a, const int32_t* b, const int64_t* c, const int32_t* d) {
   return Graph{a, b, c, d};

@@ -132,6 +132,75 @@ class SageNet(nn.Module):
         return self.fc_2(self.fc_1(h_src))
 
 
+class _MultiHotMeanFn(torch.autograd.Function):
+    """table(mh[items]).mean(dim=1) for a multi-hot id matrix mh [n_items, G] (the genre
+    feature): rs_multihot_mean_fwd reads each item's id row in place — no gathered [N, G] ids,
+    no [N, G, D] rows, no mean pass — and the backward forms the table's dense [V, D] gradient
+    in one pass (rs_multihot_mean_bwd), handed to the table as V rows (their densified sum is
+    that gradient) instead of N·G gradient rows."""
+
+    @staticmethod
+    def forward(ctx, handle, table_module, mh, items):
+        w = table_module.weight
+        V, D = w.shape
+        N, G = items.numel(), mh.shape[1]
+        out = torch.empty(N, D, device=w.device)
+        L.call("rs_multihot_mean_fwd", L.ptr(w), V, D, L.ptr(mh), G, L.ptr(items), N, L.ptr(out),
+               L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+        ctx.table_module, ctx.mh, ctx.items = table_module, mh, items
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..functional import _lookup_backward
+
+        tm = ctx.table_module
+        V, D = tm.weight.shape
+        N, G = ctx.items.numel(), ctx.mh.shape[1]
+        dev = g.device
+        dtable = torch.empty(V, D, device=dev)
+        ws = _ws("multihot_bwd", L.lib().rs_multihot_mean_bwd_workspace_size(N, V, D), dev)
+        L.call("rs_multihot_mean_bwd", L.ptr(ctx.mh), G, L.ptr(ctx.items), N,
+               L.ptr(g.contiguous()), V, D, L.ptr(dtable), L.ptr(ws), ws.numel(),
+               L.stream_ptr(dev))
+        _lookup_backward(tm, _arange_i32(V, dev), dtable, None)
+        return None, None, None, None
+
+
+_ws_bufs: dict = {}
+_aranges: dict = {}
+
+
+def _ws(name, nbytes, dev):
+    b = _ws_bufs.get((name, dev))
+    if b is None or b.numel() < nbytes:
+        b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        _ws_bufs[(name, dev)] = b
+    return b
+
+
+def _arange_i32(n, dev):
+    t = _aranges.get((n, dev))
+    if t is None:
+        t = torch.arange(n, dtype=torch.int32, device=dev)
+        _aranges[(n, dev)] = t
+    return t
+
+
+def multihot_mean_lookup(table_module, mh: torch.Tensor, items: torch.Tensor) -> torch.Tensor:
+    """table_module(mh.index_select(0, items)).mean(dim=1), fused (_MultiHotMeanFn) when the
+    shapes take it (V·D <= 256, G <= 32, no fused optimizer on the table). The table's gradient
+    arrives as all V rows (0 for ids the batch never used): the same update under Keras Adam,
+    whose sparse apply decays every row anyway (PinSage's optimizer, train.py:45-46)."""
+    V, D = table_module.weight.shape
+    if (mh.is_cuda and mh.dtype == torch.int32 and mh.is_contiguous() and mh.shape[1] <= 32
+            and V * D <= 256 and table_module.fused_optimizer is None
+            and table_module.slot_offsets is None and items.numel() > 0):
+        return _MultiHotMeanFn.apply(table_module.grad_handle, table_module, mh,
+                                     items.to(torch.int64).contiguous())
+    return table_module(mh.index_select(0, items)).mean(dim=1)
+
+
 class FeatureProjector(nn.Module):
     def __init__(self, full_graph: HeteroGraph, itype: str, embedding_size: int, device=None,
                  generator: torch.Generator | None = None):
@@ -161,6 +230,6 @@ class FeatureProjector(nn.Module):
         if padded:  # capacity-shaped block: padding src nodes (-1) read item 0, grad 0
             ids = ids.clamp_min(0)
         year_embedding = self.year_embedding(self.year.index_select(0, ids))
-        genre_embedding = self.genre_embedding(self.genre.index_select(0, ids)).mean(dim=1)
+        genre_embedding = multihot_mean_lookup(self.genre_embedding, self.genre, ids)
         id_embedding = self.id_embedding(self.item_id.index_select(0, ids))
         return torch.cat([year_embedding, genre_embedding, id_embedding], dim=-1)

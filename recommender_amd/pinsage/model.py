@@ -4,6 +4,8 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from .. import _lib as L
+
 from .graph import NID, HeteroGraph, PairGraph
 from .layers import FeatureProjector, SageNet
 
@@ -27,6 +29,62 @@ def margin_loss(pos_score, neg_score, delta: float = 1.0, valid=None, n_valid=No
     return (hinge.reshape(-1) * valid).sum() / n_valid.to(hinge.dtype).reshape(())
 
 
+class _PairMarginFn(torch.autograd.Function):
+    """item2item_scorer on both pair graphs + margin_loss in one kernel each way
+    (rs_pair_margin_fwd / _bwd): the row gathers, products, sums, clamp, mask and mean were a
+    dozen recorded ops forward and as many backward (a capacity-shaped static step replays every
+    one of them as a graph node)."""
+
+    @staticmethod
+    def forward(ctx, h, ps, pd, ns, nd, valid, n_valid, delta):
+        h = h.contiguous()
+        P, D = ps.numel(), h.shape[1]
+        dev = h.device
+        pos = torch.empty(P, device=dev)
+        neg = torch.empty(P, device=dev)
+        loss = torch.empty((), device=dev)
+        ws = torch.empty(L.lib().rs_pair_margin_workspace_size(P), dtype=torch.uint8, device=dev)
+        # a bool mask's bytes are the 0 / 1 flags the kernel reads
+        L.call("rs_pair_margin_fwd", L.ptr(h), D, D, L.ptr(ps), L.ptr(pd), L.ptr(ns), L.ptr(nd), P,
+               float(delta), L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg), L.ptr(loss),
+               L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        ctx.save_for_backward(h, ps, pd, ns, nd, valid, n_valid, pos, neg)
+        ctx.delta = float(delta)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        h, ps, pd, ns, nd, valid, n_valid, pos, neg = ctx.saved_tensors
+        P, D = ps.numel(), h.shape[1]
+        dh = torch.zeros_like(h)
+        L.call("rs_pair_margin_bwd", L.ptr(h), D, D, L.ptr(ps), L.ptr(pd), L.ptr(ns), L.ptr(nd), P,
+               ctx.delta, L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg),
+               L.ptr(g.reshape(1).contiguous()), L.ptr(dh), D, L.stream_ptr(h.device))
+        return dh, None, None, None, None, None, None, None
+
+
+def _i32(t):
+    return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
+
+
+def pair_margin_loss(pos_graph: PairGraph, neg_graph: PairGraph, h: torch.Tensor,
+                     delta: float = 1.0) -> torch.Tensor:
+    """margin_loss(item2item_scorer(pos_graph, h), item2item_scorer(neg_graph, h), delta, valid,
+    n_valid) — fused (_PairMarginFn) on the GPU for one negative per positive pair."""
+    P = pos_graph.src.numel()
+    if (h.is_cuda and h.dim() == 2 and h.shape[1] <= 64 and h.dtype == torch.float32
+            and neg_graph.src.numel() == P and P > 0):
+        valid = pos_graph.valid
+        if valid is not None and valid.dtype not in (torch.bool, torch.uint8):
+            valid = valid.to(torch.uint8)
+        n_valid = None if pos_graph.n_valid is None else _i32(pos_graph.n_valid)
+        return _PairMarginFn.apply(h, _i32(pos_graph.src), _i32(pos_graph.dst),
+                                   _i32(neg_graph.src), _i32(neg_graph.dst),
+                                   None if valid is None else valid.contiguous(), n_valid, delta)
+    return margin_loss(item2item_scorer(pos_graph, h), item2item_scorer(neg_graph, h), delta,
+                       pos_graph.valid, pos_graph.n_valid)
+
+
 class PinSageModel(nn.Module):
     def __init__(self, full_graph: HeteroGraph, itype: str, num_layers: int, embedding_size: int,
                  conv_hidden_size: int, conv_output_size: int, device=None,
@@ -47,6 +105,10 @@ class PinSageModel(nn.Module):
                                                                                     hidden_repr)
 
     call = forward
+
+    def margin_loss(self, pos_graph, neg_graph, blocks, delta: float = 1.0):
+        """the training loss of train.py:17-20 on this batch (pair_margin_loss)."""
+        return pair_margin_loss(pos_graph, neg_graph, self.get_repr(blocks), delta)
 
     def get_repr(self, blocks):
         hidden_src = self.feature_projector(blocks[0].srcdata[NID],

@@ -26,7 +26,7 @@ from ..synthetic import ML20M, movielens_graph
 from .evaluation import (build_val_test_matrix, get_item_reprs, hit_rate_eval, recommend,
                          train_test_split_by_time)
 from .graph import HeteroGraph
-from .model import PinSageModel, margin_loss
+from .model import PinSageModel
 from .sampler import PinSageSampler, item_pairs
 
 ML1M = dict(n_users=6_040, n_items=3_706, n_edges=1_000_209)
@@ -64,8 +64,7 @@ class PinSageStep:
 
     def __call__(self, pos_graph, neg_graph, blocks):
         self.opt_dense.zero_grad(set_to_none=True)
-        pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
-        loss = margin_loss(pos_score, neg_score, delta=1.0)
+        loss = self.model.margin_loss(pos_graph, neg_graph, blocks, 1.0)
         loss.backward()
         if self.world > 1:
             self._allreduce_and_apply_tables()
@@ -104,8 +103,7 @@ class PinSageStep:
             self.opt_sparse.release_state()  # the graph path's Adam state is opt_graph's
         for p in self.dense:
             p.grad = None
-        pos_score, neg_score = self.model(pos_graph, neg_graph, blocks)
-        loss = margin_loss(pos_score, neg_score, 1.0, pos_graph.valid, pos_graph.n_valid)
+        loss = self.model.margin_loss(pos_graph, neg_graph, blocks, 1.0)
         loss.backward()
         grads = [p.grad for p in self.dense]  # None: Keras skips the variable
         nd = len(self.dense)

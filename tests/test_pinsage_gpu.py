@@ -795,3 +795,71 @@ def test_world2_pinsage_static_step_and_missing_gradients():
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_pair_margin_loss_fused_matches_scorer_and_margin(padded):
+    """pair_margin_loss (rs_pair_margin_fwd / _bwd: both pair graphs' dot scores, the hinge, the
+    live-pair mean and its gradient in one kernel each way) against item2item_scorer +
+    margin_loss by autograd: loss and dL/dh within fp32 rounding; shared nodes across pairs (the
+    backward scatter collides), padding pairs (-1 ids, valid 0) scoring node 0 with no weight,
+    a hinge exactly at 0."""
+    from recommender_amd.pinsage.graph import PairGraph
+    from recommender_amd.pinsage.model import item2item_scorer, margin_loss, pair_margin_loss
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    N, D, P = 300, 16, 1000
+    h = torch.randn(N, D, device=DEV, generator=g) * 0.3
+    src = torch.randint(0, N, (P,), device=DEV, generator=g, dtype=torch.int32)
+    pdst = torch.randint(0, 40, (P,), device=DEV, generator=g, dtype=torch.int32)  # collisions
+    ndst = torch.randint(0, N, (P,), device=DEV, generator=g, dtype=torch.int32)
+    ndst[5], pdst[5], src[5] = 3, 3, 4  # neg == pos row: hinge exactly delta, not at 0
+    valid, n_valid = None, None
+    if padded:
+        valid = torch.ones(P, dtype=torch.bool, device=DEV)
+        valid[P - 37:] = False
+        src[P - 37:], pdst[P - 37:], ndst[P - 37:] = -1, -1, -1
+        n_valid = torch.tensor([P - 37], dtype=torch.int32, device=DEV)
+    pos_g = PairGraph(src, pdst, torch.arange(N, device=DEV), valid, n_valid)
+    neg_g = PairGraph(src, ndst, torch.arange(N, device=DEV), valid, n_valid)
+    h1 = h.clone().requires_grad_()
+    loss = pair_margin_loss(pos_g, neg_g, h1, 1.0)
+    loss.backward()
+    h2 = h.clone().requires_grad_()
+    ref = margin_loss(item2item_scorer(pos_g, h2), item2item_scorer(neg_g, h2), 1.0, valid, n_valid)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
+    # a row's gradient sums its pairs' terms in atomic (arrival) order, as the index_add of the
+    # gathers it replaces: near-cancelling elements judged against the largest
+    assert_close_rel(h1.grad.cpu(), h2.grad.cpu(), rtol=1e-5, scale=float(h2.grad.abs().max()) * 1e-1)
+
+
+def test_multihot_mean_lookup_matches_gather_mean():
+    """multihot_mean_lookup (the genre feature: rs_multihot_mean_fwd / _bwd) against the gathered
+    ids → table lookup → mean(dim=1) path: outputs, and the table's densified gradient, within
+    fp32 rounding; ids spread over the whole table, repeated items, G = 20."""
+    from recommender_amd.embedding import Embedding
+    from recommender_amd.optim import densify_grad
+    from recommender_amd.pinsage.layers import multihot_mean_lookup
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    n_items, G, V, D, N = 500, 20, 20, 8, 3000
+    mh = torch.randint(0, V, (n_items, G), device=DEV, generator=g, dtype=torch.int32)
+    mh[::3] = (mh[::3] < 2).to(torch.int32)  # genre-like {0, 1} rows
+    items = torch.randint(0, n_items, (N,), device=DEV, generator=g)
+    w = torch.randn(V, D, device=DEV, generator=g)
+    up = torch.randn(N, D, device=DEV, generator=g)
+    res = []
+    for fused in (True, False):
+        t = Embedding(V, D, device=DEV, weight=w.cpu())
+        if fused:
+            out = multihot_mean_lookup(t, mh, items)
+        else:
+            out = t(mh.index_select(0, items)).mean(dim=1)
+        (out * up).sum().backward()
+        ids, rows = t.take_grad()
+        res.append((out.detach(), densify_grad(t, ids, rows)))
+    (o1, d1), (o2, d2) = res
+    # 20-term sums in another order: near-cancelling elements judged against the largest
+    assert_close_rel(o1.cpu(), o2.cpu(), rtol=1e-5, scale=float(o2.abs().max()) * 1e-1)
+    assert_close_rel(d1.cpu(), d2.cpu(), rtol=1e-5, scale=float(d2.abs().max()) * 1e-1)
