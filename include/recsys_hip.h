@@ -540,7 +540,8 @@ int32_t rs_batch_norm_bwd(const float* dy, const float* x, int64_t B, int32_t C,
  * Multi-hot mean lookup (PinSage FeatureProjector's genre, pinsage/train/layers.py:68-81):
  * out[n, :] = (Σ_g table[mh[items[n], g], :]) / G for the items' G-slot id rows of mh
  * [n_items, G] int32 (ids outside [0, V) read 0 and set RS_ERRBIT_OOB). Backward: the dense
- * [V, D] table gradient Σ_n Σ_{g: id = r} dout[n] / G (deterministic; V·D <= 256, G <= 32). */
+ * [V, D] table gradient Σ_n Σ_{g: id = r} dout[n] / G (deterministic; V·D <= 256, D <= 64,
+ * G <= 32). */
 int32_t rs_multihot_mean_fwd(const float* table, int32_t V, int32_t D, const int32_t* mh, int32_t G,
                              const int64_t* items, int64_t N, float* out, int32_t* err_flag,
                              void* stream);

@@ -579,7 +579,8 @@ __global__ __launch_bounds__(64) void pair_margin_fold_kernel(const float* __res
 
 // dh += ∂loss/∂h: the hinge's gradient dloss / n_live on live pairs with (neg + delta) - pos >= 0
 // (clamp's backward passes at the boundary), -g to the positive score, +g to the negative one,
-// each score's two rows taking the other row times it — scattered with float atomics, as the
+// each score's two rows taking the other row times it — scattered with hardware float atomics
+// (global_atomic_add_f32: no compare-and-swap loop), as the
 // index_add of the row gathers it replaces (dh zeroed by the caller).
 __global__ __launch_bounds__(kPairThreads) void pair_margin_bwd_kernel(
     const float* __restrict__ h, int64_t ld, int D, const int32_t* __restrict__ ps,
@@ -587,20 +588,21 @@ __global__ __launch_bounds__(kPairThreads) void pair_margin_bwd_kernel(
     int64_t P, float delta, const uint8_t* __restrict__ valid, const float* __restrict__ pos,
     const float* __restrict__ neg, const float* __restrict__ dloss,
     const int32_t* __restrict__ n_live, float* __restrict__ dh, int64_t ldd) {
-  const int64_t i = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
-  if (i >= P) return;
+  // one thread per (pair, element): the pair's four row elements and their four atomics
+  const int64_t k = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
+  if (k >= P * D) return;
+  const int64_t i = k / D;
+  const int d = (int)(k - i * D);
   if (valid != nullptr && !valid[i]) return;
   if (!((neg[i] + delta) - pos[i] >= 0.f)) return;
   const float g = dloss[0] / (float)(n_live ? n_live[0] : P);
   const int a = max(ps[i], 0), b = max(pd[i], 0), c = max(ns[i], 0), e = max(nd[i], 0);
-  for (int d = 0; d < D; ++d) {
-    const float ha = h[(int64_t)a * ld + d], hb = h[(int64_t)b * ld + d];
-    const float hc = h[(int64_t)c * ld + d], he = h[(int64_t)e * ld + d];
-    atomicAdd(dh + (int64_t)a * ldd + d, -g * hb);
-    atomicAdd(dh + (int64_t)b * ldd + d, -g * ha);
-    atomicAdd(dh + (int64_t)c * ldd + d, g * he);
-    atomicAdd(dh + (int64_t)e * ldd + d, g * hc);
-  }
+  const float ha = h[(int64_t)a * ld + d], hb = h[(int64_t)b * ld + d];
+  const float hc = h[(int64_t)c * ld + d], he = h[(int64_t)e * ld + d];
+  unsafeAtomicAdd(dh + (int64_t)a * ldd + d, -g * hb);
+  unsafeAtomicAdd(dh + (int64_t)b * ldd + d, -g * ha);
+  unsafeAtomicAdd(dh + (int64_t)c * ldd + d, g * he);
+  unsafeAtomicAdd(dh + (int64_t)e * ldd + d, g * hc);
 }
 
 // ---- multi-hot mean lookup (FeatureProjector's genre, pinsage/train/layers.py:68-81) --------
@@ -626,27 +628,30 @@ __global__ __launch_bounds__(256) void multihot_mean_fwd_kernel(
   if (oob && err_flag) atomicOr(err_flag, RS_ERRBIT_OOB);
 }
 
-// dtable[r][d] = Σ_n Σ_{g: mh[item[n], g] = r} dout[n][d] / G: a block per 256 items stages their
-// id rows in LDS, thread (r, d) sums its entries in (n, g) order into a block partial; partials
-// folded in block order (deterministic). V·D <= 256, G <= 32.
-constexpr int kMhRows = 256;
+// dtable[r][d] = Σ_n Σ_{g: mh[item[n], g] = r} dout[n][d] / G: a block per 32 items stages their
+// id rows and dout rows in LDS (coalesced), thread (r, d) sums its entries in (n, g) order into
+// the block's partial; the partials are folded per (r, d) by a block of 256 lanes (lane j the
+// blocks j, j + 256, ... in order, then a fixed tree): deterministic. V·D <= 256, G <= 32, D <= 64.
+constexpr int kMhRows = 32;
 __global__ __launch_bounds__(256) void multihot_mean_bwd_part_kernel(
     const int32_t* __restrict__ mh, int G, const int64_t* __restrict__ items, int64_t N,
     const float* __restrict__ dout, int V, int D, float* __restrict__ part) {
   __shared__ int32_t ids[kMhRows * 32];
+  __shared__ float gs[kMhRows * 64];
   const int64_t n0 = (int64_t)blockIdx.x * kMhRows;
   const int rows = (int)(N - n0 < kMhRows ? N - n0 : kMhRows);
   for (int e = threadIdx.x; e < rows * G; e += blockDim.x) {
     const int i = e / G, g = e - i * G;
     ids[i * G + g] = mh[items[n0 + i] * G + g];
   }
+  for (int e = threadIdx.x; e < rows * D; e += blockDim.x) gs[e] = dout[n0 * D + e] / (float)G;
   __syncthreads();
   const int t = threadIdx.x;
   if (t >= V * D) return;
   const int r = t / D, d = t - r * D;
   float acc = 0.f;
   for (int i = 0; i < rows; ++i) {
-    const float x = dout[(n0 + i) * D + d] / (float)G;
+    const float x = gs[i * D + d];
     for (int g = 0; g < G; ++g)
       if (ids[i * G + g] == r) acc += x;
   }
@@ -656,11 +661,17 @@ __global__ __launch_bounds__(256) void multihot_mean_bwd_part_kernel(
 __global__ __launch_bounds__(256) void multihot_mean_bwd_fold_kernel(const float* __restrict__ part,
                                                                     int nb, int VD,
                                                                     float* __restrict__ dtable) {
-  const int t = threadIdx.x;
-  if (t >= VD) return;
+  __shared__ float red[256];
+  const int t = blockIdx.x, j = threadIdx.x;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * VD + t];
-  dtable[t] = s;
+  for (int b = j; b < nb; b += 256) s += part[(int64_t)b * VD + t];
+  red[j] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (j < o) red[j] += red[j + o];
+    __syncthreads();
+  }
+  if (j == 0) dtable[t] = red[0];
 }
 
 }  // namespace rs
@@ -687,8 +698,8 @@ extern "C" int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int6
                                         int64_t N, const float* dout, int32_t V, int32_t D,
                                         float* dtable, void* workspace, size_t ws_bytes,
                                         void* stream) {
-  RS_CHECK_ARG(V >= 1 && D >= 1 && V * D <= 256 && G >= 1 && G <= 32 && N >= 1,
-               "rs_multihot_mean_bwd: V·D <= 256, 1 <= G <= 32, N >= 1");
+  RS_CHECK_ARG(V >= 1 && D >= 1 && D <= 64 && V * D <= 256 && G >= 1 && G <= 32 && N >= 1,
+               "rs_multihot_mean_bwd: V·D <= 256, D <= 64, 1 <= G <= 32, N >= 1");
   RS_CHECK_ARG(mh && items && dout && dtable && workspace, "rs_multihot_mean_bwd: null pointer");
   RS_CHECK_ARG(ws_bytes >= rs_multihot_mean_bwd_workspace_size(N, V, D), "workspace too small");
   hipStream_t st = as_stream(stream);
@@ -696,7 +707,7 @@ extern "C" int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int6
   float* part = static_cast<float*>(workspace);
   multihot_mean_bwd_part_kernel<<<nb, 256, 0, st>>>(mh, G, items, N, dout, V, D, part);
   RS_CHECK_LAUNCH();
-  multihot_mean_bwd_fold_kernel<<<1, 256, 0, st>>>(part, nb, V * D, dtable);
+  multihot_mean_bwd_fold_kernel<<<V * D, 256, 0, st>>>(part, nb, V * D, dtable);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -739,7 +750,7 @@ extern "C" int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, con
   RS_CHECK_ARG(h && pos_src && pos_dst && neg_src && neg_dst && pos_score && neg_score && dloss &&
                    dh,
                "rs_pair_margin_bwd: null pointer");
-  pair_margin_bwd_kernel<<<(unsigned)ceil_div(n_pairs, kPairThreads), kPairThreads, 0,
+  pair_margin_bwd_kernel<<<(unsigned)ceil_div(n_pairs * D, kPairThreads), kPairThreads, 0,
                            as_stream(stream)>>>(h, ld, D, pos_src, pos_dst, neg_src, neg_dst,
                                                 n_pairs, delta, valid, pos_score, neg_score, dloss,
                                                 n_live, dh, ldd);

@@ -194,7 +194,7 @@ def multihot_mean_lookup(table_module, mh: torch.Tensor, items: torch.Tensor) ->
     whose sparse apply decays every row anyway (PinSage's optimizer, train.py:45-46)."""
     V, D = table_module.weight.shape
     if (mh.is_cuda and mh.dtype == torch.int32 and mh.is_contiguous() and mh.shape[1] <= 32
-            and V * D <= 256 and table_module.fused_optimizer is None
+            and V * D <= 256 and D <= 64 and table_module.fused_optimizer is None
             and table_module.slot_offsets is None and items.numel() > 0):
         return _MultiHotMeanFn.apply(table_module.grad_handle, table_module, mh,
                                      items.to(torch.int64).contiguous())
