@@ -71,13 +71,25 @@ def pinsage_step():
     return fn
 
 
+def deepfm_step():
+    from recommender_amd.ctr.train import TrainStep, build_model
+    from recommender_amd.synthetic import criteo_batch
+
+    rng = np.random.default_rng(4)
+    m = build_model("DeepFM", 16, 1_000_000, 26, 13, "cuda")
+    step = TrainStep(m, "keras_adam", fused=False)
+    cat, dn, lb = criteo_batch(rng, 1024, [1_000_000] * 26)
+    batch = (torch.from_numpy(cat).cuda(), torch.from_numpy(dn).cuda(), torch.from_numpy(lb).cuda())
+    return lambda: step.static_step(batch)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien", "esmm", "mmoe", "pinsage"])
+    ap.add_argument("--model", default="dien", choices=["dien", "esmm", "mmoe", "pinsage", "deepfm"])
     args = ap.parse_args()
     L.load()
-    fn = (dien_step() if args.model == "dien" else pinsage_step() if args.model == "pinsage"
-          else multitask_step(args.model))
+    fn = {"dien": dien_step, "pinsage": pinsage_step, "deepfm": deepfm_step}.get(
+        args.model, lambda: multitask_step(args.model))()
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
