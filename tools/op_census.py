@@ -83,12 +83,25 @@ def deepfm_step():
     return lambda: step.static_step(batch)
 
 
+def eges_step():
+    from recommender_amd.eges.train import EGESStep, build, synthetic_batch
+
+    rng = np.random.default_rng(4)
+    m = build("EGES", 63001, 801, 3000, 160)
+    step = EGESStep(m)
+    *inp, lab = synthetic_batch(rng, 1024, 63001, 801, 3000)
+    inp = tuple(torch.from_numpy(a).cuda() for a in inp)
+    lab = torch.from_numpy(lab).cuda()
+    return lambda: step.static_step(inp, lab)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dien", choices=["dien", "esmm", "mmoe", "pinsage", "deepfm"])
+    ap.add_argument("--model", default="dien", choices=["dien", "esmm", "mmoe", "pinsage", "deepfm", "eges"])
     args = ap.parse_args()
     L.load()
-    fn = {"dien": dien_step, "pinsage": pinsage_step, "deepfm": deepfm_step}.get(
+    fn = {"dien": dien_step, "pinsage": pinsage_step, "deepfm": deepfm_step,
+          "eges": eges_step}.get(
         args.model, lambda: multitask_step(args.model))()
     for _ in range(2):
         fn()
