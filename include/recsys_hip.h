@@ -736,11 +736,14 @@ int32_t rs_side_pool_bwd_strided(const float* side, int64_t side_bstride, int64_
  * Σ_s softmax(weight_logits[t][b, :])[s] · side[b, s, :], attn[t] [batch, n_side] the weights
  * (logits rows logits_ld apart). Per task the same arithmetic as rs_side_pool_fwd. Side rows as
  * rs_side_pool_fwd_strided (16-byte aligned, dim % 4 == 0, dim <= 128). The task arrays are host
- * arrays read during the call. */
-int32_t rs_side_pool_fwd_multi(const float* side, int64_t side_bstride, int64_t side_sstride,
+ * arrays read during the call. side_bias (optional, [n_side, dim], 16-byte aligned): the side rows
+ * hold pre-activations z and are first replaced in place by relu(z + side_bias[s]) (MMOE's
+ * batched expert layer's bias and relu), then pooled. */
+int32_t rs_side_pool_fwd_multi(float* side, int64_t side_bstride, int64_t side_sstride,
                                int64_t batch, int32_t n_side, int32_t dim, int32_t n_tasks,
                                const float* const* weight_logits, int64_t logits_ld,
-                               float* const* hidden, float* const* attn, void* stream);
+                               float* const* hidden, float* const* attn, const float* side_bias,
+                               void* stream);
 /* Backward of rs_side_pool_fwd_multi: grad_side = Σ_t attn[t][s] · grad_hidden[t] (task order,
  * each product rounded: the sum of n_tasks rs_side_pool_bwd results), grad_logits[t] as
  * rs_side_pool_bwd's (rows grad_logits_ld apart). One pass over the side rows. */

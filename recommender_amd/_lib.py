@@ -168,7 +168,7 @@ _SIGS = {
     "rs_pair_margin_bwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64, C.c_float, _p, _p, _p, _p,
                                   _p, _p, _i64, _p]),
     "rs_side_pool_fwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _i64, _p, _p,
-                                      _p]),
+                                      _p, _p]),
     "rs_side_pool_bwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p,
                                       _i64, _p]),
     "rs_side_pool_fwd": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p, _p]),

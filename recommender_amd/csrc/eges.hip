@@ -246,9 +246,13 @@ struct PoolTasks {
   int T;
 };
 
+// sbias (optional, [S, D]): the side rows arrive as pre-activations z and become
+// relu(z + sbias[s]) — written back in place (the rows the backward reads) before pooling:
+// MMOE's batched expert layer's bias and relu taken here instead of a bias broadcast into the
+// GEMM output and a relu pass over it.
 __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_multi_kernel(
-    const float* __restrict__ side, int64_t sb, int64_t ss, int64_t B, int32_t S, int32_t D,
-    PoolTasks pt) {
+    float* __restrict__ side, int64_t sb, int64_t ss, int64_t B, int32_t S, int32_t D,
+    const float* __restrict__ sbias, PoolTasks pt) {
   const int lane = threadIdx.x & 63, c = lane & 31;
   const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if (b >= B) return;
@@ -258,6 +262,17 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_multi_kernel(
   for (int s = 0; s < kMaxSide; ++s)
     if (s < S) v[s] = on ? *reinterpret_cast<const pf4*>(side + b * sb + s * ss + 4 * c)
                          : pf4{0.f, 0.f, 0.f, 0.f};
+  if (sbias && on) {
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s) {
+      if (s < S) {
+        const pf4 bb = *reinterpret_cast<const pf4*>(sbias + s * D + 4 * c);
+        const pf4 z = v[s] + bb;
+        v[s] = pf4{fmaxf(z[0], 0.f), fmaxf(z[1], 0.f), fmaxf(z[2], 0.f), fmaxf(z[3], 0.f)};
+        *reinterpret_cast<pf4*>(side + b * sb + s * ss + 4 * c) = v[s];
+      }
+    }
+  }
   for (int t = 0; t < pt.T; ++t) {
     const float* wl = pt.wl[t] + b * pt.wl_ld;
     float a[kMaxSide];
@@ -563,11 +578,12 @@ static int32_t check_pool_multi(const float* side, int64_t sb, int64_t ss, int64
   return RS_OK;
 }
 
-extern "C" int32_t rs_side_pool_fwd_multi(const float* side, int64_t side_bstride,
+extern "C" int32_t rs_side_pool_fwd_multi(float* side, int64_t side_bstride,
                                           int64_t side_sstride, int64_t batch, int32_t n_side,
                                           int32_t dim, int32_t n_tasks,
                                           const float* const* weight_logits, int64_t logits_ld,
-                                          float* const* hidden, float* const* attn, void* stream) {
+                                          float* const* hidden, float* const* attn,
+                                          const float* side_bias, void* stream) {
   if (int32_t e = check_pool_multi(side, side_bstride, side_sstride, batch, n_side, dim, n_tasks))
     return e;
   RS_CHECK_ARG(weight_logits && hidden && attn && logits_ld >= n_side, "bad task arrays");
@@ -583,9 +599,11 @@ extern "C" int32_t rs_side_pool_fwd_multi(const float* side, int64_t side_bstrid
     pt.hidden[t] = hidden[t];
     pt.attn[t] = attn[t];
   }
+  RS_CHECK_ARG(!side_bias || (reinterpret_cast<uintptr_t>(side_bias) & 15) == 0,
+               "rs_side_pool_fwd_multi: side_bias must be 16-byte aligned");
   pool_fwd_multi_kernel<<<waves_grid(ceil_div(batch, 2)), kWave * kWavesPerBlock, 0,
                           as_stream(stream)>>>(side, side_bstride, side_sstride, batch, n_side,
-                                               dim, pt);
+                                               dim, side_bias, pt);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -33,7 +33,9 @@ class _ExpertsGatesFn(torch.autograd.Function):
     as one GEMM over their concatenated kernels (relu in its epilogue), the T gates' logits as
     one GEMM, the experts' second layers as one batched GEMM reading the first layer's output
     in place ([E, B, H0] seen with rows E·H0 apart: no transpose copy), and the T softmax
-    poolings of the [E, B, H1] expert outputs in one pass (rs_side_pool_fwd_multi).
+    poolings of the [E, B, H1] expert outputs in one pass (rs_side_pool_fwd_multi, which also
+    adds the second layers' bias and applies their relu in place: no bias broadcast into the
+    GEMM output, no relu pass).
     Backward: one pooling pass for all tasks (their expert-output gradients summed inside it),
     the second layers' relu masks and per-expert bias sums in one pass, their input gradient by
     one batched GEMM written straight into the first layer's [B, E·H0] layout, one mask pass
@@ -50,11 +52,13 @@ class _ExpertsGatesFn(torch.autograd.Function):
         y1 = _affine(x, k0, b0, 1)                                  # [B, E*H0]
         zg = torch.addmm(bg, x, kg)                                 # [B, T*E]
         y1v = y1.view(B, E, H0).transpose(0, 1)                     # [E, B, H0], in place
-        y2 = torch.relu_(torch.baddbmm(b1, y1v, k1))                # [E, B, H1]
+        y2 = torch.bmm(y1v, k1)                                     # [E, B, H1] pre-activation
         hid = [torch.empty(B, H1, device=dev) for _ in range(T)]
         att = [torch.empty(B, E, device=dev) for _ in range(T)]
+        # the pooling pass adds the bias and applies the relu to y2 in place, then pools
         L.call("rs_side_pool_fwd_multi", L.ptr(y2), H1, B * H1, B, E, H1, T,
-               _ptrs([zg[:, t * E:] for t in range(T)]), T * E, _ptrs(hid), _ptrs(att), st)
+               _ptrs([zg[:, t * E:] for t in range(T)]), T * E, _ptrs(hid), _ptrs(att),
+               L.ptr(b1.reshape(E, H1).contiguous()), st)
         ctx.save_for_backward(x, k0, k1, kg, y1, y2, *att)
         ctx.E, ctx.T = E, T
         return tuple(hid)

@@ -327,7 +327,7 @@ def test_side_pool_multi_equals_single_task_poolings():
     hid = [torch.empty(B, H, device=DEV) for _ in range(T)]
     att = [torch.empty(B, E, device=DEV) for _ in range(T)]
     L.call("rs_side_pool_fwd_multi", L.ptr(y), H, B * H, B, E, H, T,
-           _ptrs([z[:, t * E:] for t in range(T)]), z.shape[1], _ptrs(hid), _ptrs(att), st)
+           _ptrs([z[:, t * E:] for t in range(T)]), z.shape[1], _ptrs(hid), _ptrs(att), None, st)
     dy = torch.empty_like(y)
     dz = torch.full_like(z, 7.0)
     L.call("rs_side_pool_bwd_multi", L.ptr(y), H, B * H, B, E, H, T, _ptrs(att), _ptrs(ups),
@@ -344,6 +344,19 @@ def test_side_pool_multi_equals_single_task_poolings():
         gsum = s.grad.clone() if gsum is None else gsum + s.grad
     assert torch.equal(gsum.transpose(0, 1).contiguous(), dy)
     assert bool((dz[:, T * E:] == 7.0).all())  # columns past the tasks' blocks untouched
+    # with side_bias: the rows become relu(z + bias) in place, then pool as before
+    bias = torch.randn(E, H, device=DEV, generator=g)
+    zz = torch.randn(E, B, H, device=DEV, generator=g)
+    want = torch.relu(zz + bias[:, None, :])
+    hid2 = [torch.empty(B, H, device=DEV) for _ in range(T)]
+    att2 = [torch.empty(B, E, device=DEV) for _ in range(T)]
+    L.call("rs_side_pool_fwd_multi", L.ptr(zz), H, B * H, B, E, H, T,
+           _ptrs([z[:, t * E:] for t in range(T)]), z.shape[1], _ptrs(hid2), _ptrs(att2),
+           L.ptr(bias), st)
+    assert torch.equal(zz, want)
+    for t in range(T):
+        ref = side_pool(want.transpose(0, 1), z[:, t * E:(t + 1) * E].unsqueeze(1)).squeeze(1)
+        assert torch.equal(hid2[t], ref)
 
 
 def test_mmoe_fused_block_matches_separate_nodes(monkeypatch):
