@@ -294,7 +294,10 @@ def test_pinsage_model_forward_backward():
     (p64, n64, l64, P64), (p32, n32, _, P32) = ref[torch.float64], ref[torch.float32]
 
     def close(got, name, r64, r32):
-        assert_close_f64(got, r64, r32, name, floor=1e-6)
+        # one fp32 sample of the restatement's rounding; the model sums some rows in other
+        # orders (the genre multi-hot mean sequentially, the row gathers' backward by atomics in
+        # arrival order, so the fp32 path is not even run-to-run identical): 8x its error
+        assert_close_f64(got, r64, r32, name, floor=1e-6, noise=8.0)
 
     close(pos, "pos score", p64, p32)
     close(neg, "neg score", n64, n32)
