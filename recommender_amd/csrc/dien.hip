@@ -245,34 +245,19 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
   if (b >= B) return;
   const bool act = j < H;
   const int H3 = 3 * H;
-  pk2 kur[HM];  // (update, reset) recurrent weights of unit j
+  float ku[HM], kr[HM];
 #pragma unroll
   for (int k = 0; k < HM; ++k) {
     const bool ok = act && k < H;
-    kur[k] = pk2{ok ? Kuh[k * H + j] : 0.f, ok ? Krh[k * H + j] : 0.f};
+    ku[k] = ok ? Kuh[k * H + j] : 0.f;
+    kr[k] = ok ? Krh[k * H + j] : 0.f;
   }
   const float* xb = xw + b * (int64_t)L * H3;
   const uint8_t* mb = mask + b * L;
   const float* ab = att + b * L;
-  // wave-uniform mask bits and the next valid step's x·W and score loaded one step ahead (as
-  // gru_fwd_kernel): no memory latency on the step chain
-  const MaskBits mbits(mb, L, j);
-  const bool v0 = mbits.test(mb, 0);
-  float nu = act && v0 ? xb[j] : 0.f, nr = act && v0 ? xb[H + j] : 0.f,
-        nh = act && v0 ? xb[2 * H + j] : 0.f, na = v0 ? ab[0] : 0.f;
   float h = 0.f;
   for (int t = 0; t < L; ++t) {
-    const float xu = nu, xr = nr, xh = nh, a = na;
-    if (t + 1 < L && mbits.test(mb, t + 1)) {
-      const float* xn = xb + (int64_t)(t + 1) * H3;
-      if (act) {
-        nu = xn[j];
-        nr = xn[H + j];
-        nh = xn[2 * H + j];
-      }
-      na = ab[t + 1];
-    }
-    if (!mbits.test(mb, t)) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
+    if (!mb[t]) {  // masked step: state carried, arithmetic skipped (as in gru_fwd_kernel)
       if (act) {
         const int64_t o = b * L + t;
         if (states) states[o * H + j] = h;
@@ -282,10 +267,16 @@ __global__ __launch_bounds__(256) void augru_fwd_kernel(const float* __restrict_
       }
       continue;
     }
-    pk2 iur = pk2{0.f, 0.f};
+    const float* x = xb + (int64_t)t * H3;
+    const float xu = act ? x[j] : 0.f, xr = act ? x[H + j] : 0.f, xh = act ? x[2 * H + j] : 0.f;
+    const float a = ab[t];
+    float iu = 0.f, ir = 0.f;
 #pragma unroll
-    for (int k = 0; k < HM; ++k) iur = pk_fma(bcast(h, k), kur[k], iur);
-    const float iu = iur.x, ir = iur.y;
+    for (int k = 0; k < HM; ++k) {
+      const float hk = bcast(h, k);
+      iu = fmaf(hk, ku[k], iu);
+      ir = fmaf(hk, kr[k], ir);
+    }
     const float u = sigm(xu + iu), r = sigm(xr + ir);
     const float rh = act ? r * h : 0.f;
     float ihh = 0.f;
