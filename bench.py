@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 WATCH = ["rs_dlrm_train_step_fwd_unit",
          "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
          "rs_dlrm_interaction_fwd_head_dx",
-         "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids",
+         "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots",
          "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
          "rs_embedding_dedup_grad"]
 # the embedding path of SURVEY §8(d) (lookup fwd + bwd + dedup + apply) as the production step
@@ -46,9 +46,9 @@ WATCH = ["rs_dlrm_train_step_fwd_unit",
 PATH_KERNELS = ("rs_dlrm_train_step_fwd_unit",
                 "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
                 "rs_dlrm_interaction_fwd_head_dx", "rs_dlrm_interaction_bwd",
-                "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids", "rs_sort_ids_sharded",
+                "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots", "rs_sort_ids_sharded",
                 "rs_embedding_apply", "rs_embedding_apply_scaled")
-SIDE_STREAM = {"rs_sort_ids", "rs_embedding_apply", "rs_embedding_apply_scaled",
+SIDE_STREAM = {"rs_sort_ids_slots", "rs_embedding_apply", "rs_embedding_apply_scaled",
                "rs_sort_ids_sharded", "rs_embedding_dedup_grad"}
 # device symbols behind each C-ABI entry (for the PMC passes)
 # (entry, device-symbol regex of its kernels, the one kernel every call launches once)
@@ -58,9 +58,10 @@ PMC_SYMBOLS = [
     ("rs_dlrm_interaction_fwd_head", r"inter_fwd_mfma<128, rs::GatherSrc, true, true, false>",
      "inter_fwd_mfma"),
     ("rs_dlrm_interaction_bwd_rank1", r"dlrm_bwd_pipe", "dlrm_bwd_pipe"),
-    # pass 0's histogram (keys built from the ids in the same launch) runs once per sort; the
-    # template carries further parameters (digit bits, keys per lane), so match the prefix only
-    ("rs_sort_ids", r"radix_|scan_|count_unique", r"radix_hist_kernel<\d+, true"),
+    # the slot-segmented sort's pass-0 histogram runs once per sort (the LSD form's pass-0
+    # histogram, keys built from the ids, when a slab takes that form)
+    ("rs_sort_ids_slots", r"slot_sort_|radix_|scan_|count_unique",
+     r"slot_sort_hist0_kernel|radix_hist_kernel<\d+, true"),
     ("rs_embedding_apply", r"seg_tile|seg_group|seg_chunk|seg_fixup", "seg_tile|seg_group"),
 ]
 
@@ -265,7 +266,7 @@ def kernel_bytes(name, B, S, D, id_bytes, U):
         return N * 8 + N * 4 * D + U * 2 * 4 * D
     if name == "rs_embedding_apply_scaled":  # + G[b] when the step hands unit rows (4 B/example)
         return N * 8 + N * 4 * D + U * 2 * 4 * D
-    if name == "rs_sort_ids":
+    if name in ("rs_sort_ids_slots", "rs_sort_ids"):
         return N * id_bytes + N * 8
     return 0
 
@@ -312,9 +313,10 @@ def isolated_path(model, ids, iters=10):
         L.ptr(err), st))
     calls = {
         train[0]: train[1],
-        "rs_sort_ids": lambda: L.call(
-            "rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(so), S, V, L.ptr(rows),
-            L.ptr(pos), None, L.ptr(err), L.ptr(sws), sws.numel(), st),
+        "rs_sort_ids_slots": lambda: L.call(
+            "rs_sort_ids_slots", L.ptr(ids), L.id_dtype_code(ids), n, None, L.ptr(so), S, V,
+            emb.max_slot_rows, L.ptr(rows), L.ptr(pos), None, L.ptr(err), L.ptr(sws), sws.numel(),
+            st),
         "rs_embedding_apply_scaled": lambda: L.call(
             "rs_embedding_apply_scaled", L.RS_OPT_SGD, L.ptr(w), None, None, V, D, L.ptr(rows),
             L.ptr(pos), n, L.ptr(dxu), L.ptr(gb), S, prm, None,

@@ -60,6 +60,9 @@ typedef struct rs_adam_params {
 
 const char* rs_last_error(void);
 int32_t rs_version(void);
+/* sha256 prefix of the kernel sources + this header the library was built from (the host-side
+ * loader compares it with the sources it ships beside: a stale build is refused) */
+const char* rs_build_id(void);
 /* number of gfx950 devices visible; 0 when no GPU (used by loaders to fail loudly) */
 int32_t rs_device_count(void);
 /* STREAM-style device copy (16-byte accesses): the measured HBM-bandwidth reference of the
@@ -110,6 +113,19 @@ int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t n_ids, con
                            const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                            uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
                            int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
+
+/* rs_sort_ids_masked (valid may be NULL) with the largest slot's row count given: when the ids
+ * are [B, n_slots] (B <= 131072, n_slots <= 64), one GPU, and every slot has < 2^24 rows, the
+ * sort runs slot by slot (the slot of position p is p % n_slots: the order over slots is free) in
+ * <= 2 passes of <= 12-bit digits, 4 launches; otherwise the LSD sort. The output is the same.
+ * rs_sort_ids / rs_sort_ids_masked take that path when n_rows <= 2^24.
+ * Sentinel order (every sort here): excluded / OOB positions follow all valid rows, grouped by
+ * slot, each group in position order; their sorted_rows value is n_rows (key space). */
+int32_t rs_sort_ids_slots(const void* ids, int32_t id_dtype, int64_t n_ids, const uint8_t* valid,
+                          const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
+                          int64_t max_slot_rows, uint32_t* sorted_rows, int32_t* sorted_pos,
+                          int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
+                          void* stream);
 
 /* Row-sharded variant: rows dealt cyclically over `world` ranks
  * (owner = row % world, local row = row / world). Keys are owner-major:
@@ -539,35 +555,53 @@ int32_t rs_batch_norm_bwd(const float* dy, const float* x, int64_t B, int32_t C,
 /* ------------------------------------------------------------------------------------
  * Multi-hot mean lookup (PinSage FeatureProjector's genre, pinsage/train/layers.py:68-81):
  * out[n, :] = (Σ_g table[mh[items[n], g], :]) / G for the items' G-slot id rows of mh
- * [n_items, G] int32 (ids outside [0, V) read 0 and set RS_ERRBIT_OOB). Backward: the dense
- * [V, D] table gradient Σ_n Σ_{g: id = r} dout[n] / G (deterministic; V·D <= 256, D <= 64,
- * G <= 32). */
+ * [n_items, G] int32 (ids outside [0, V) read 0 and set RS_ERRBIT_OOB; items outside
+ * [0, n_items) give a zero row forward, no gradient backward, and set RS_ERRBIT_OOB). Backward:
+ * the dense [V, D] table gradient Σ_n Σ_{g: id = r} dout[n] / G (deterministic; V·D <= 256,
+ * D <= 64, G <= 32). */
 int32_t rs_multihot_mean_fwd(const float* table, int32_t V, int32_t D, const int32_t* mh, int32_t G,
-                             const int64_t* items, int64_t N, float* out, int32_t* err_flag,
-                             void* stream);
+                             int64_t n_items, const int64_t* items, int64_t N, float* out,
+                             int32_t* err_flag, void* stream);
 size_t rs_multihot_mean_bwd_workspace_size(int64_t N, int32_t V, int32_t D);
-int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int64_t* items, int64_t N,
-                             const float* dout, int32_t V, int32_t D, float* dtable,
-                             void* workspace, size_t ws_bytes, void* stream);
+int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, int64_t n_items, const int64_t* items,
+                             int64_t N, const float* dout, int32_t V, int32_t D, float* dtable,
+                             int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Deterministic index_add of rows (the backward of a row gather h.index_select(0, ids), e.g.
+ * PinSage's item2item scorer, pinsage/train/model.py:14-19): out [n_rows, dim] (contiguous) =
+ * 0, then out[ids[p]] += rows[p] for every p with valid[p] != 0 (valid may be NULL = all). Each
+ * row's terms are summed in position order inside tiles of RS_DEDUP_TILE sorted entries, tile
+ * partials in tile order (rs_sort_ids + rs_embedding_grad_dense): run-to-run identical, unlike
+ * float atomics. Ids outside [0, n_rows) are skipped and set RS_ERRBIT_OOB. */
+size_t rs_index_add_rows_workspace_size(int64_t n, int32_t dim);
+int32_t rs_index_add_rows(const void* ids, int32_t id_dtype, int64_t n, const uint8_t* valid,
+                          const float* rows, int32_t dim, int64_t n_rows, float* out,
+                          int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * PinSage's item2item scores and margin loss in one pass (pinsage/train/model.py:14-19,
  * pinsage/train/train.py:17-20): pos_score[i] = h[pos_src[i]]·h[pos_dst[i]], neg_score likewise,
  * loss[0] = Σ_{live i} max((neg + delta) - pos, 0) / n_live (valid: uint8 per pair or null =
- * all live; n_live: device int32 [1] or null = n_pairs; -1 node ids score node 0, as padding).
- * Backward: dh += the loss's gradient (dloss: device float [1]) scattered with float atomics
- * (dh zeroed by the caller; the index_add of the gathers it replaces is atomic too). D <= 64. */
+ * all live; n_live: device int32 [1] or null = n_pairs; -1 node ids score node 0, as padding;
+ * ids >= n_rows read a zero row and set RS_ERRBIT_OOB in err_flag, which may be NULL).
+ * Backward: dh [n_rows, D] contiguous = the loss's gradient (dloss: device float [1]); every
+ * pair's four row terms are written as rows and folded per node by rs_index_add_rows (fixed
+ * order: deterministic, no float atomics). D <= 64. */
 size_t rs_pair_margin_workspace_size(int64_t n_pairs);
-int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
-                           const int32_t* pos_dst, const int32_t* neg_src, const int32_t* neg_dst,
-                           int64_t n_pairs, float delta, const uint8_t* valid,
-                           const int32_t* n_live, float* pos_score, float* neg_score, float* loss,
-                           void* workspace, size_t ws_bytes, void* stream);
-int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
-                           const int32_t* pos_dst, const int32_t* neg_src, const int32_t* neg_dst,
-                           int64_t n_pairs, float delta, const uint8_t* valid,
-                           const int32_t* n_live, const float* pos_score, const float* neg_score,
-                           const float* dloss, float* dh, int64_t ldd, void* stream);
+int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, int64_t n_rows,
+                           const int32_t* pos_src, const int32_t* pos_dst, const int32_t* neg_src,
+                           const int32_t* neg_dst, int64_t n_pairs, float delta,
+                           const uint8_t* valid, const int32_t* n_live, float* pos_score,
+                           float* neg_score, float* loss, int32_t* err_flag, void* workspace,
+                           size_t ws_bytes, void* stream);
+size_t rs_pair_margin_bwd_workspace_size(int64_t n_pairs, int32_t D);
+int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, int64_t n_rows,
+                           const int32_t* pos_src, const int32_t* pos_dst, const int32_t* neg_src,
+                           const int32_t* neg_dst, int64_t n_pairs, float delta,
+                           const uint8_t* valid, const int32_t* n_live, const float* pos_score,
+                           const float* neg_score, const float* dloss, float* dh,
+                           int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * PinSage sampling + aggregation. The graph is the bipartite

@@ -49,12 +49,18 @@ def embedding_lookup(table: np.ndarray, ids: np.ndarray, slot_offsets=None, rais
 
 
 def sort_ids(ids, n_rows, slot_offsets=None):
-    """Stable sort of rows (OOB rows get the sentinel n_rows and sort last); returns
-    (sorted_rows uint32, sorted_pos int32, n_unique)."""
+    """Stable sort of rows; returns (sorted_rows uint32, sorted_pos int32, n_unique). OOB rows
+    (and positions a caller excludes: pass them as -1) sort after every valid row, grouped by
+    slot (sentinel key n_rows + slot, slot = position % n_slots; one group without slot
+    offsets), each group in position order; their sorted_rows value is n_rows
+    (csrc/sort.hip: the LSD sort's sentinel keys and the slot-segmented sort's order)."""
     rows = global_rows(ids, n_rows, slot_offsets)
-    keys = np.where(rows < 0, n_rows, rows).astype(np.int64)
+    flat = np.asarray(ids).reshape(-1)
+    n_slots = 1 if slot_offsets is None else np.asarray(slot_offsets).size - 1
+    slot = np.arange(flat.size) % n_slots
+    keys = np.where(rows < 0, n_rows + slot, rows).astype(np.int64)
     pos = np.argsort(keys, kind="stable")
-    sk = keys[pos]
+    sk = np.minimum(keys[pos], n_rows)
     valid = sk < n_rows
     n_unique = int(np.unique(sk[valid]).size)
     return sk.astype(np.uint32), pos.astype(np.int32), n_unique

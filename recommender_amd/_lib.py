@@ -51,6 +51,7 @@ _p, _i32, _i64, _sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
 _u32, _u64 = C.c_uint32, C.c_uint64
 _SIGS = {
     "rs_last_error": (C.c_char_p, []),
+    "rs_build_id": (C.c_char_p, []),
     "rs_version": (_i32, []),
     "rs_device_count": (_i32, []),
     "rs_stream_copy": (_i32, [_p, _p, _sz, _p]),
@@ -59,6 +60,8 @@ _SIGS = {
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_sort_ids_masked": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_sort_ids_slots": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _sz,
+                                 _p]),
     "rs_sort_ids_sharded": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _sz,
                                    _p]),
     "rs_unique_inverse": (_i32, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
@@ -160,13 +163,17 @@ _SIGS = {
     "rs_side_pool_fwd_strided": (_i32, [_p, _i64, _i64, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_side_pool_bwd_strided": (_i32, [_p, _i64, _i64, _p, _p, _i64, _i32, _i32, _p, _p, _p]),
     "rs_pair_margin_workspace_size": (_sz, [_i64]),
-    "rs_multihot_mean_fwd": (_i32, [_p, _i32, _i32, _p, _i32, _p, _i64, _p, _p, _p]),
+    "rs_multihot_mean_fwd": (_i32, [_p, _i32, _i32, _p, _i32, _i64, _p, _i64, _p, _p, _p]),
     "rs_multihot_mean_bwd_workspace_size": (_sz, [_i64, _i32, _i32]),
-    "rs_multihot_mean_bwd": (_i32, [_p, _i32, _p, _i64, _p, _i32, _i32, _p, _p, _sz, _p]),
-    "rs_pair_margin_fwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64, C.c_float, _p, _p, _p, _p,
-                                  _p, _p, _sz, _p]),
-    "rs_pair_margin_bwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64, C.c_float, _p, _p, _p, _p,
-                                  _p, _p, _i64, _p]),
+    "rs_multihot_mean_bwd": (_i32, [_p, _i32, _i64, _p, _i64, _p, _i32, _i32, _p, _p, _p, _sz,
+                                    _p]),
+    "rs_index_add_rows_workspace_size": (_sz, [_i64, _i32]),
+    "rs_index_add_rows": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _p, _p, _p, _sz, _p]),
+    "rs_pair_margin_fwd": (_i32, [_p, _i64, _i32, _i64, _p, _p, _p, _p, _i64, C.c_float, _p, _p,
+                                  _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_pair_margin_bwd_workspace_size": (_sz, [_i64, _i32]),
+    "rs_pair_margin_bwd": (_i32, [_p, _i64, _i32, _i64, _p, _p, _p, _p, _i64, C.c_float, _p, _p,
+                                  _p, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_side_pool_fwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _i64, _p, _p,
                                       _p, _p]),
     "rs_side_pool_bwd_multi": (_i32, [_p, _i64, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p,
@@ -272,8 +279,23 @@ def load(path: str | os.PathLike | None = None):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    check_build_id(lib, p)
     _lib = lib
     return lib
+
+
+def check_build_id(lib, path) -> None:
+    """Refuse a library built from other sources than the csrc/ + include/ next to it (the .so
+    travels prebuilt, untracked: without this a GPU box could test a stale build of a changed
+    kernel with no signal). Skipped when the sources are absent (a library shipped alone)."""
+    from .build import CSRC, source_hash
+
+    if not CSRC.is_dir() or os.environ.get("RS_SKIP_BUILD_ID") == "1":
+        return
+    built, want = lib.rs_build_id().decode(), source_hash()
+    if built != want:
+        raise RecsysError(f"{path} was built from other sources (build id {built}, sources "
+                          f"{want}): rebuild with `python -m recommender_amd.build`")
 
 
 def lib():

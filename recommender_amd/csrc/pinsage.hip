@@ -531,11 +531,23 @@ inline uint32_t stop_threshold(float p) {
 // max((neg + delta) - pos, 0) over the live pairs, loss = Σ hinge / n_live. One thread per pair
 // (D <= 64 row elements, products rounded then summed in order, as the mul + sum it replaces);
 // the block sums folded in block order (deterministic). Padding pairs (src or dst -1) score
-// node 0 and carry no weight, as the capacity-shaped batch's clamp + mask did.
+// node 0 and carry no weight, as the capacity-shaped batch's clamp + mask did; a node id >= n_rows
+// reads a zero row and flags RS_ERRBIT_OOB.
 constexpr int kPairThreads = 256;
+
+// the row a pair endpoint reads: -1 (padding) -> node 0, >= n_rows -> none (oob)
+__device__ __forceinline__ int pair_row(int32_t r, int64_t n_rows, bool& oob) {
+  if (r < 0) return 0;
+  if (r >= n_rows) {
+    oob = true;
+    return -1;
+  }
+  return r;
+}
 
 __device__ __forceinline__ float row_dot(const float* __restrict__ h, int64_t ld, int D, int u,
                                          int v) {
+  if (u < 0 || v < 0) return 0.f;
   const float* a = h + (int64_t)u * ld;
   const float* b = h + (int64_t)v * ld;
   float s = 0.f;
@@ -544,21 +556,25 @@ __device__ __forceinline__ float row_dot(const float* __restrict__ h, int64_t ld
 }
 
 __global__ __launch_bounds__(kPairThreads) void pair_margin_fwd_kernel(
-    const float* __restrict__ h, int64_t ld, int D, const int32_t* __restrict__ ps,
+    const float* __restrict__ h, int64_t ld, int D, int64_t n_rows, const int32_t* __restrict__ ps,
     const int32_t* __restrict__ pd, const int32_t* __restrict__ ns, const int32_t* __restrict__ nd,
     int64_t P, float delta, const uint8_t* __restrict__ valid, float* __restrict__ pos,
-    float* __restrict__ neg, float* __restrict__ part) {
+    float* __restrict__ neg, float* __restrict__ part, int32_t* err_flag) {
   __shared__ float red[kPairThreads];
   const int64_t i = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
   float w = 0.f;
+  bool oob = false;
   if (i < P) {
-    const float p = row_dot(h, ld, D, max(ps[i], 0), max(pd[i], 0));
-    const float q = row_dot(h, ld, D, max(ns[i], 0), max(nd[i], 0));
+    const int a = pair_row(ps[i], n_rows, oob), b = pair_row(pd[i], n_rows, oob);
+    const int c = pair_row(ns[i], n_rows, oob), e = pair_row(nd[i], n_rows, oob);
+    const float p = row_dot(h, ld, D, a, b);
+    const float q = row_dot(h, ld, D, c, e);
     pos[i] = p;
     neg[i] = q;
     const float hinge = fmaxf((q + delta) - p, 0.f);
     w = (valid == nullptr || valid[i]) ? hinge : 0.f;
   }
+  if (oob) flag_oob(err_flag);
   red[threadIdx.x] = w;
   __syncthreads();
   for (int o = kPairThreads / 2; o > 0; o >>= 1) {
@@ -577,32 +593,43 @@ __global__ __launch_bounds__(64) void pair_margin_fold_kernel(const float* __res
   loss[0] = s / (float)(n_live ? n_live[0] : P);
 }
 
-// dh += ∂loss/∂h: the hinge's gradient dloss / n_live on live pairs with (neg + delta) - pos >= 0
-// (clamp's backward passes at the boundary), -g to the positive score, +g to the negative one,
-// each score's two rows taking the other row times it — scattered with hardware float atomics
-// (global_atomic_add_f32: no compare-and-swap loop), as the
-// index_add of the row gathers it replaces (dh zeroed by the caller).
-__global__ __launch_bounds__(kPairThreads) void pair_margin_bwd_kernel(
-    const float* __restrict__ h, int64_t ld, int D, const int32_t* __restrict__ ps,
+// The backward's row terms: the hinge's gradient g = dloss / n_live on live pairs with
+// (neg + delta) - pos >= 0 (clamp's backward passes at the boundary), -g to the positive score,
+// +g to the negative one; each score's two rows take the other row times it. Endpoint
+// e = role·P + i (roles: pos src, pos dst, neg src, neg dst) gets the row terms[e] = coef · h[other]
+// (one fmul_rn, the product the gathers' backward formed), key[e] = its node and live[e] = 1 when
+// it carries a gradient; rs_index_add_rows then folds them per node in a fixed order. One thread
+// per (pair, element).
+__global__ __launch_bounds__(kPairThreads) void pair_margin_terms_kernel(
+    const float* __restrict__ h, int64_t ld, int D, int64_t n_rows, const int32_t* __restrict__ ps,
     const int32_t* __restrict__ pd, const int32_t* __restrict__ ns, const int32_t* __restrict__ nd,
     int64_t P, float delta, const uint8_t* __restrict__ valid, const float* __restrict__ pos,
     const float* __restrict__ neg, const float* __restrict__ dloss,
-    const int32_t* __restrict__ n_live, float* __restrict__ dh, int64_t ldd) {
-  // one thread per (pair, element): the pair's four row elements and their four atomics
+    const int32_t* __restrict__ n_live, float* __restrict__ terms, int32_t* __restrict__ key,
+    uint8_t* __restrict__ live) {
   const int64_t k = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
   if (k >= P * D) return;
   const int64_t i = k / D;
   const int d = (int)(k - i * D);
-  if (valid != nullptr && !valid[i]) return;
-  if (!((neg[i] + delta) - pos[i] >= 0.f)) return;
-  const float g = dloss[0] / (float)(n_live ? n_live[0] : P);
-  const int a = max(ps[i], 0), b = max(pd[i], 0), c = max(ns[i], 0), e = max(nd[i], 0);
-  const float ha = h[(int64_t)a * ld + d], hb = h[(int64_t)b * ld + d];
-  const float hc = h[(int64_t)c * ld + d], he = h[(int64_t)e * ld + d];
-  unsafeAtomicAdd(dh + (int64_t)a * ldd + d, -g * hb);
-  unsafeAtomicAdd(dh + (int64_t)b * ldd + d, -g * ha);
-  unsafeAtomicAdd(dh + (int64_t)c * ldd + d, g * he);
-  unsafeAtomicAdd(dh + (int64_t)e * ldd + d, g * hc);
+  bool oob = false;
+  const int a = pair_row(ps[i], n_rows, oob), b = pair_row(pd[i], n_rows, oob);
+  const int c = pair_row(ns[i], n_rows, oob), e = pair_row(nd[i], n_rows, oob);
+  const bool on = (valid == nullptr || valid[i]) && ((neg[i] + delta) - pos[i] >= 0.f);
+  const float g = on ? dloss[0] / (float)(n_live ? n_live[0] : P) : 0.f;
+  const float ha = a >= 0 ? h[(int64_t)a * ld + d] : 0.f, hb = b >= 0 ? h[(int64_t)b * ld + d] : 0.f;
+  const float hc = c >= 0 ? h[(int64_t)c * ld + d] : 0.f, he = e >= 0 ? h[(int64_t)e * ld + d] : 0.f;
+  terms[(0 * P + i) * D + d] = -g * hb;
+  terms[(1 * P + i) * D + d] = -g * ha;
+  terms[(2 * P + i) * D + d] = g * he;
+  terms[(3 * P + i) * D + d] = g * hc;
+  if (d == 0) {
+    const int rows[4] = {a, b, c, e};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      key[r * P + i] = rows[r] < 0 ? 0 : rows[r];
+      live[r * P + i] = (on && rows[r] >= 0) ? 1 : 0;
+    }
+  }
 }
 
 // ---- multi-hot mean lookup (FeatureProjector's genre, pinsage/train/layers.py:68-81) --------
@@ -611,12 +638,19 @@ __global__ __launch_bounds__(kPairThreads) void pair_margin_bwd_kernel(
 // then / G. Ids outside [0, V) read 0 and flag RS_ERRBIT_OOB.
 __global__ __launch_bounds__(256) void multihot_mean_fwd_kernel(
     const float* __restrict__ table, int V, int D, const int32_t* __restrict__ mh, int G,
-    const int64_t* __restrict__ items, int64_t N, float* __restrict__ out, int32_t* err_flag) {
+    int64_t n_items, const int64_t* __restrict__ items, int64_t N, float* __restrict__ out,
+    int32_t* err_flag) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N * D) return;
   const int64_t n = e / D;
   const int d = (int)(e - n * D);
-  const int32_t* row = mh + items[n] * G;
+  const int64_t item = items[n];
+  if (item < 0 || item >= n_items) {  // no id row to read: a zero row
+    out[e] = 0.f;
+    if (d == 0) flag_oob(err_flag);
+    return;
+  }
+  const int32_t* row = mh + item * G;
   float s = 0.f;
   bool oob = false;
   for (int g = 0; g < G; ++g) {
@@ -634,15 +668,19 @@ __global__ __launch_bounds__(256) void multihot_mean_fwd_kernel(
 // blocks j, j + 256, ... in order, then a fixed tree): deterministic. V·D <= 256, G <= 32, D <= 64.
 constexpr int kMhRows = 32;
 __global__ __launch_bounds__(256) void multihot_mean_bwd_part_kernel(
-    const int32_t* __restrict__ mh, int G, const int64_t* __restrict__ items, int64_t N,
-    const float* __restrict__ dout, int V, int D, float* __restrict__ part) {
+    const int32_t* __restrict__ mh, int G, int64_t n_items, const int64_t* __restrict__ items,
+    int64_t N, const float* __restrict__ dout, int V, int D, float* __restrict__ part,
+    int32_t* err_flag) {
   __shared__ int32_t ids[kMhRows * 32];
   __shared__ float gs[kMhRows * 64];
   const int64_t n0 = (int64_t)blockIdx.x * kMhRows;
   const int rows = (int)(N - n0 < kMhRows ? N - n0 : kMhRows);
   for (int e = threadIdx.x; e < rows * G; e += blockDim.x) {
     const int i = e / G, g = e - i * G;
-    ids[i * G + g] = mh[items[n0 + i] * G + g];
+    const int64_t item = items[n0 + i];
+    const bool ok = item >= 0 && item < n_items;  // an out-of-range item adds nothing
+    ids[i * G + g] = ok ? mh[item * G + g] : -1;
+    if (!ok && g == 0) flag_oob(err_flag);
   }
   for (int e = threadIdx.x; e < rows * D; e += blockDim.x) gs[e] = dout[n0 * D + e] / (float)G;
   __syncthreads();
@@ -679,13 +717,13 @@ __global__ __launch_bounds__(256) void multihot_mean_bwd_fold_kernel(const float
 using namespace rs;
 
 extern "C" int32_t rs_multihot_mean_fwd(const float* table, int32_t V, int32_t D, const int32_t* mh,
-                                        int32_t G, const int64_t* items, int64_t N, float* out,
-                                        int32_t* err_flag, void* stream) {
-  RS_CHECK_ARG(V >= 1 && D >= 1 && G >= 1 && N >= 0, "rs_multihot_mean_fwd: bad sizes");
+                                        int32_t G, int64_t n_items, const int64_t* items, int64_t N,
+                                        float* out, int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(V >= 1 && D >= 1 && G >= 1 && N >= 0 && n_items >= 0, "rs_multihot_mean_fwd: bad sizes");
   if (N == 0) return RS_OK;
   RS_CHECK_ARG(table && mh && items && out, "rs_multihot_mean_fwd: null pointer");
   multihot_mean_fwd_kernel<<<(unsigned)ceil_div(N * D, 256), 256, 0, as_stream(stream)>>>(
-      table, V, D, mh, G, items, N, out, err_flag);
+      table, V, D, mh, G, n_items, items, N, out, err_flag);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -694,18 +732,20 @@ extern "C" size_t rs_multihot_mean_bwd_workspace_size(int64_t N, int32_t V, int3
   return (size_t)ceil_div(N < 1 ? 1 : N, kMhRows) * V * D * sizeof(float) + 256;
 }
 
-extern "C" int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, const int64_t* items,
-                                        int64_t N, const float* dout, int32_t V, int32_t D,
-                                        float* dtable, void* workspace, size_t ws_bytes,
-                                        void* stream) {
-  RS_CHECK_ARG(V >= 1 && D >= 1 && D <= 64 && V * D <= 256 && G >= 1 && G <= 32 && N >= 1,
+extern "C" int32_t rs_multihot_mean_bwd(const int32_t* mh, int32_t G, int64_t n_items,
+                                        const int64_t* items, int64_t N, const float* dout,
+                                        int32_t V, int32_t D, float* dtable, int32_t* err_flag,
+                                        void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(V >= 1 && D >= 1 && D <= 64 && V * D <= 256 && G >= 1 && G <= 32 && N >= 1 &&
+                   n_items >= 0,
                "rs_multihot_mean_bwd: V·D <= 256, D <= 64, 1 <= G <= 32, N >= 1");
   RS_CHECK_ARG(mh && items && dout && dtable && workspace, "rs_multihot_mean_bwd: null pointer");
   RS_CHECK_ARG(ws_bytes >= rs_multihot_mean_bwd_workspace_size(N, V, D), "workspace too small");
   hipStream_t st = as_stream(stream);
   const int nb = (int)ceil_div(N, kMhRows);
   float* part = static_cast<float*>(workspace);
-  multihot_mean_bwd_part_kernel<<<nb, 256, 0, st>>>(mh, G, items, N, dout, V, D, part);
+  multihot_mean_bwd_part_kernel<<<nb, 256, 0, st>>>(mh, G, n_items, items, N, dout, V, D, part,
+                                                    err_flag);
   RS_CHECK_LAUNCH();
   multihot_mean_bwd_fold_kernel<<<V * D, 256, 0, st>>>(part, nb, V * D, dtable);
   RS_CHECK_LAUNCH();
@@ -716,13 +756,15 @@ extern "C" size_t rs_pair_margin_workspace_size(int64_t n_pairs) {
   return (size_t)(ceil_div(n_pairs < 1 ? 1 : n_pairs, kPairThreads)) * sizeof(float) + 256;
 }
 
-extern "C" int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
-                                      const int32_t* pos_dst, const int32_t* neg_src,
-                                      const int32_t* neg_dst, int64_t n_pairs, float delta,
-                                      const uint8_t* valid, const int32_t* n_live, float* pos_score,
-                                      float* neg_score, float* loss, void* workspace,
+extern "C" int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, int64_t n_rows,
+                                      const int32_t* pos_src, const int32_t* pos_dst,
+                                      const int32_t* neg_src, const int32_t* neg_dst,
+                                      int64_t n_pairs, float delta, const uint8_t* valid,
+                                      const int32_t* n_live, float* pos_score, float* neg_score,
+                                      float* loss, int32_t* err_flag, void* workspace,
                                       size_t ws_bytes, void* stream) {
-  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D, "rs_pair_margin_fwd: bad sizes");
+  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D && n_rows >= 1,
+               "rs_pair_margin_fwd: bad sizes");
   RS_CHECK_ARG(h && pos_src && pos_dst && neg_src && neg_dst && pos_score && neg_score && loss &&
                    workspace,
                "rs_pair_margin_fwd: null pointer");
@@ -730,32 +772,58 @@ extern "C" int32_t rs_pair_margin_fwd(const float* h, int64_t ld, int32_t D, con
   hipStream_t st = as_stream(stream);
   const int nb = (int)ceil_div(n_pairs, kPairThreads);
   float* part = static_cast<float*>(workspace);
-  pair_margin_fwd_kernel<<<nb, kPairThreads, 0, st>>>(h, ld, D, pos_src, pos_dst, neg_src, neg_dst,
-                                                      n_pairs, delta, valid, pos_score, neg_score,
-                                                      part);
+  pair_margin_fwd_kernel<<<nb, kPairThreads, 0, st>>>(h, ld, D, n_rows, pos_src, pos_dst, neg_src,
+                                                      neg_dst, n_pairs, delta, valid, pos_score,
+                                                      neg_score, part, err_flag);
   RS_CHECK_LAUNCH();
   pair_margin_fold_kernel<<<1, 64, 0, st>>>(part, nb, n_live, n_pairs, loss);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
 
-extern "C" int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, const int32_t* pos_src,
-                                      const int32_t* pos_dst, const int32_t* neg_src,
-                                      const int32_t* neg_dst, int64_t n_pairs, float delta,
-                                      const uint8_t* valid, const int32_t* n_live,
-                                      const float* pos_score, const float* neg_score,
-                                      const float* dloss, float* dh, int64_t ldd, void* stream) {
-  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D && ldd >= D,
+// workspace: terms [4P, D] fp32, keys [4P] int32, live [4P] uint8, then rs_index_add_rows' own
+static size_t pair_terms_bytes(int64_t P, int32_t D, float** terms, int32_t** key, uint8_t** live,
+                               void* ws) {
+  Carver c(ws, ~(size_t)0);
+  *terms = c.take<float>((size_t)4 * P * D);
+  *key = c.take<int32_t>((size_t)4 * P);
+  *live = c.take<uint8_t>((size_t)4 * P);
+  return align_up(c.off, 256);
+}
+
+extern "C" size_t rs_pair_margin_bwd_workspace_size(int64_t n_pairs, int32_t D) {
+  float* t;
+  int32_t* k;
+  uint8_t* l;
+  const int64_t P = n_pairs < 1 ? 1 : n_pairs;
+  return pair_terms_bytes(P, D, &t, &k, &l, nullptr) + rs_index_add_rows_workspace_size(4 * P, D);
+}
+
+extern "C" int32_t rs_pair_margin_bwd(const float* h, int64_t ld, int32_t D, int64_t n_rows,
+                                      const int32_t* pos_src, const int32_t* pos_dst,
+                                      const int32_t* neg_src, const int32_t* neg_dst,
+                                      int64_t n_pairs, float delta, const uint8_t* valid,
+                                      const int32_t* n_live, const float* pos_score,
+                                      const float* neg_score, const float* dloss, float* dh,
+                                      int32_t* err_flag, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  RS_CHECK_ARG(n_pairs >= 1 && D >= 1 && D <= 64 && ld >= D && n_rows >= 1,
                "rs_pair_margin_bwd: bad sizes");
   RS_CHECK_ARG(h && pos_src && pos_dst && neg_src && neg_dst && pos_score && neg_score && dloss &&
-                   dh,
+                   dh && workspace,
                "rs_pair_margin_bwd: null pointer");
-  pair_margin_bwd_kernel<<<(unsigned)ceil_div(n_pairs * D, kPairThreads), kPairThreads, 0,
-                           as_stream(stream)>>>(h, ld, D, pos_src, pos_dst, neg_src, neg_dst,
-                                                n_pairs, delta, valid, pos_score, neg_score, dloss,
-                                                n_live, dh, ldd);
+  RS_CHECK_ARG(ws_bytes >= rs_pair_margin_bwd_workspace_size(n_pairs, D), "workspace too small");
+  float* terms;
+  int32_t* key;
+  uint8_t* live;
+  const size_t head = pair_terms_bytes(n_pairs, D, &terms, &key, &live, workspace);
+  hipStream_t st = as_stream(stream);
+  pair_margin_terms_kernel<<<(unsigned)ceil_div(n_pairs * D, kPairThreads), kPairThreads, 0, st>>>(
+      h, ld, D, n_rows, pos_src, pos_dst, neg_src, neg_dst, n_pairs, delta, valid, pos_score,
+      neg_score, dloss, n_live, terms, key, live);
   RS_CHECK_LAUNCH();
-  return RS_OK;
+  return rs_index_add_rows(key, RS_ID_I32, 4 * n_pairs, live, terms, D, n_rows, dh, err_flag,
+                           static_cast<char*>(workspace) + head, ws_bytes - head, stream);
 }
 
 static Graph make_graph(const int64_t* a, const int32_t* b, const int64_t* c, const int32_t* d) {

@@ -59,12 +59,21 @@ struct KeyGen {
   const uint8_t* valid;  // optional: positions with valid[i] == 0 take the sentinel key, unflagged
 };
 
+// Sentinel of position i: key_space + its slot, so excluded / OOB positions sort after every
+// valid row grouped by slot, each group in position order (the last pass writes them all as
+// key_space: the outputs' sentinel value is unchanged). The slot-segmented sort (below) gives the
+// same order.
+__device__ __forceinline__ uint32_t sentinel_key(const KeyGen& g, int64_t i) {
+  const int64_t sl = g.slot_offsets ? i % g.n_slots : 0;
+  return static_cast<uint32_t>(g.key_space + sl);
+}
+
 __device__ __forceinline__ uint32_t make_key(const KeyGen& g, int64_t i, bool& oob) {
-  if (g.valid && !g.valid[i]) return static_cast<uint32_t>(g.key_space);  // excluded position
+  if (g.valid && !g.valid[i]) return sentinel_key(g, i);  // excluded position
   const int64_t r = global_row(g.ids, g.dtype, i, g.slot_offsets, g.n_slots, g.n_rows);
   if (r < 0) {
     oob = true;
-    return static_cast<uint32_t>(g.key_space);  // sentinel: sorts after every valid row
+    return sentinel_key(g, i);  // sentinel: sorts after every valid row
   }
   return static_cast<uint32_t>(g.world == 1 ? r : (r % g.world) * g.shard_stride + r / g.world);
 }
@@ -97,16 +106,16 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     if (FROM_IDS) {
       if (lds_slots) {
         uint32_t key = 0u;
+        const int sl = (int)((uint32_t)i % (uint32_t)kg.n_slots);
         if (i < n && kg.valid && !kg.valid[i]) {
-          key = static_cast<uint32_t>(kg.key_space);  // excluded position: sentinel, unflagged
+          key = static_cast<uint32_t>(kg.key_space + sl);  // excluded position: sentinel, unflagged
           keys[i] = key;
         } else if (i < n) {
           const int64_t id = load_id(kg.ids, kg.dtype, i);
-          const int sl = (int)((uint32_t)i % (uint32_t)kg.n_slots);
           const int64_t lo = offs[sl], hi = offs[sl + 1];
           if (id < 0 || id >= hi - lo) {
             oob = true;
-            key = static_cast<uint32_t>(kg.key_space);  // sentinel: sorts after every valid row
+            key = static_cast<uint32_t>(kg.key_space + sl);  // sentinel: sorts after every valid row
           } else {
             const int64_t r = lo + id;
             key = static_cast<uint32_t>(kg.world == 1 ? r
@@ -187,7 +196,7 @@ template <int BITS, bool IOTA_VALS, int KPL = kSortKeysPerLane>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, int64_t n, int shift,
     const int32_t* __restrict__ hist_scanned, const int32_t* __restrict__ totals, int n_tiles,
-    uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out) {
+    uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, uint32_t clamp_key) {
   constexpr int BINS = 1 << BITS;
   constexpr int WAVES = kSortThreads / 64;
   constexpr int PER = (BINS + kSortThreads - 1) / kSortThreads;  // digits per thread
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
   for (int j = threadIdx.x; j < tile_n; j += kSortThreads) {
     const uint32_t k = sk[j];
     const int32_t dst = doff[(k >> shift) & (BINS - 1)] + j;
-    keys_out[dst] = k;
+    keys_out[dst] = k < clamp_key ? k : clamp_key;  // the last pass folds the slot sentinels
     vals_out[dst] = sv[j];
   }
 }
@@ -426,7 +435,7 @@ static size_t sort_ws_layout(int64_t n_ids, Carver& c, uint32_t** keys_alt, int3
 template <int BITS, bool FIRST_FROM_IDS, int KPL>
 static int32_t launch_pass_k(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
                              int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
-                             const KeyGen& kg, hipStream_t st) {
+                             const KeyGen& kg, hipStream_t st, uint32_t clamp_key) {
   radix_hist_kernel<BITS, FIRST_FROM_IDS, KPL><<<n_tiles, kSortThreads, 0, st>>>(kin, kg, n, shift,
                                                                                  hist, n_tiles);
   RS_CHECK_LAUNCH();
@@ -434,7 +443,7 @@ static int32_t launch_pass_k(uint32_t* kin, const int32_t* vin, uint32_t* kout, 
   radix_colscan_kernel<<<(BINS + 3) / 4, 256, 0, st>>>(hist, n_tiles, BINS, totals);
   RS_CHECK_LAUNCH();
   radix_scatter_kernel<BITS, FIRST_FROM_IDS, KPL><<<n_tiles, kSortThreads, 0, st>>>(
-      kin, vin, n, shift, hist, totals, n_tiles, kout, vout);
+      kin, vin, n, shift, hist, totals, n_tiles, kout, vout, clamp_key);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
@@ -442,23 +451,25 @@ static int32_t launch_pass_k(uint32_t* kin, const int32_t* vin, uint32_t* kout, 
 template <int BITS, bool FIRST_FROM_IDS>
 static int32_t launch_pass(uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
                            int64_t n, int shift, int32_t* hist, int32_t* totals, int n_tiles,
-                           const KeyGen& kg, hipStream_t st) {
+                           const KeyGen& kg, hipStream_t st, uint32_t clamp_key) {
   if (sort_kpl(n) == kSortKeysPerLaneTiny)
     return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLaneTiny>(kin, vin, kout, vout, n, shift,
-                                                                     hist, totals, n_tiles, kg, st);
+                                                                     hist, totals, n_tiles, kg, st,
+                                                                     clamp_key);
   if (sort_kpl(n) == kSortKeysPerLaneSmall)
     return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLaneSmall>(kin, vin, kout, vout, n, shift,
-                                                                      hist, totals, n_tiles, kg, st);
+                                                                      hist, totals, n_tiles, kg, st,
+                                                                      clamp_key);
   return launch_pass_k<BITS, FIRST_FROM_IDS, kSortKeysPerLane>(kin, vin, kout, vout, n, shift, hist,
-                                                               totals, n_tiles, kg, st);
+                                                               totals, n_tiles, kg, st, clamp_key);
 }
 
 template <bool FIRST_FROM_IDS>
 static int32_t dispatch_pass(int bits, uint32_t* kin, const int32_t* vin, uint32_t* kout,
                              int32_t* vout, int64_t n, int shift, int32_t* hist, int32_t* totals,
-                             int n_tiles, const KeyGen& kg, hipStream_t st) {
+                             int n_tiles, const KeyGen& kg, hipStream_t st, uint32_t clamp_key) {
 #define RS_PASS(B) \
-  case B: return launch_pass<B, FIRST_FROM_IDS>(kin, vin, kout, vout, n, shift, hist, totals, n_tiles, kg, st);
+  case B: return launch_pass<B, FIRST_FROM_IDS>(kin, vin, kout, vout, n, shift, hist, totals, n_tiles, kg, st, clamp_key);
   switch (bits) {
     RS_PASS(1) RS_PASS(2) RS_PASS(3) RS_PASS(4) RS_PASS(5) RS_PASS(6) RS_PASS(7) RS_PASS(8) RS_PASS(9)
   }
@@ -469,11 +480,12 @@ static int32_t dispatch_pass(int bits, uint32_t* kin, const int32_t* vin, uint32
 
 // Sort (keys, vals) ascending by key (stable); result ends in keys_out/vals_out.
 // keys_in/vals_in are clobbered. kg != null: the keys are made from ids in pass 0 (keys_in is
-// then only scratch and vals are the positions 0..n-1; vals_in is not read).
+// then only scratch and vals are the positions 0..n-1; vals_in is not read), sentinels are
+// kg->key_space + slot and the output keys are clamped to kg->key_space. Keys are <= max_key.
 static int32_t radix_sort_impl(uint32_t* keys_in, int32_t* vals_in, uint32_t* keys_out,
-                               int32_t* vals_out, int64_t n, int64_t n_rows, void* ws,
+                               int32_t* vals_out, int64_t n, int64_t max_key, void* ws,
                                size_t ws_bytes, const KeyGen* kg, hipStream_t st) {
-  SortPlan p = plan_sort(n, n_rows);
+  SortPlan p = plan_sort(n, max_key);
   Carver c(ws, ws_bytes);
   uint32_t* kalt;
   int32_t* valt;
@@ -492,10 +504,12 @@ static int32_t radix_sort_impl(uint32_t* keys_in, int32_t* vals_in, uint32_t* ke
     bool last = pass == p.passes - 1;
     uint32_t* kb = last ? keys_out : (ka == keys_in ? kalt : keys_in);
     int32_t* vb = last ? vals_out : (va == vals_in ? valt : vals_in);
+    const uint32_t clamp = (last && kg) ? static_cast<uint32_t>(kg->key_space) : 0xFFFFFFFFu;
     int32_t s = (pass == 0 && kg)
-                    ? dispatch_pass<true>(p.bits, ka, va, kb, vb, n, 0, hist, totals, p.n_tiles, *kg, st)
+                    ? dispatch_pass<true>(p.bits, ka, va, kb, vb, n, 0, hist, totals, p.n_tiles, *kg, st,
+                                          clamp)
                     : dispatch_pass<false>(p.bits, ka, va, kb, vb, n, pass * p.bits, hist, totals,
-                                           p.n_tiles, none, st);
+                                           p.n_tiles, none, st, clamp);
     if (s) return s;
     ka = kb;
     va = vb;
@@ -648,6 +662,501 @@ int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
   return RS_OK;
 }
 
+// ---- slot-segmented sort (one GPU; BASELINE north star: 26 slots x 65 536 examples) ---------
+// The sorted order is (slot, id) for valid positions, then the sentinels grouped by slot (each
+// in position order): the slot of position p = b·S + s is known from p, so the order over slots
+// needs no sorting pass. Inside a slot, its B ids (rows_s < 2^24) are sorted stably in at most
+// two LSD passes of <= 12-bit digits (w0 = min(bits_s, 12) low bits, then the rest), per
+// (slot, tile of 4096 examples) block:
+//   hist    the tile's digit counts (uint16 [4096], ballot-aggregated in LDS), its valid and
+//           sentinel counts;
+//   scatter the block re-reads its slot's tile histograms (<= 32 x 8 KB, L2), forms the digit
+//           bases and its own tile prefix in place (no column-scan launch), ranks its keys with
+//           per-wave running counts (stable), and writes each key to its final (single-pass
+//           slot) or temporary (two-pass slot) place; sentinels go to the end.
+// Four launches for the north star's 1.7 M ids (hist, scatter per pass; the second pass only
+// over the slots wider than 12 bits), against nine for the three-pass LSD sort. Blocks are
+// placed XCD-aware: pass 0 puts the 26 slots' tiles of one example range on one XCD (their ids
+// share cache lines), pass 1 puts one slot's tiles on one XCD (its histograms and output stay in
+// that XCD's L2).
+constexpr int kSegThreads = 256;
+constexpr int kSegKPL = 16;
+constexpr int kSegTile = kSegThreads * kSegKPL;  // 4096 examples of one slot
+constexpr int kSegBits = 12;
+constexpr int kSegBins = 1 << kSegBits;
+constexpr int kSegMaxTiles = 32;   // tiles per slot: B <= 131 072
+constexpr int kSegMaxSlots = 64;
+constexpr int kSegMaxBits = 2 * kSegBits;  // slot ids < 2^24
+constexpr int kNumXcd = 8;
+
+struct SegArgs {
+  const void* ids;
+  int32_t dtype;
+  const uint8_t* valid;         // optional: 0 = excluded (sentinel, unflagged)
+  const int64_t* slot_offsets;  // null: one slot of n_rows rows
+  int n_slots;
+  int64_t B;                    // examples (ids per slot)
+  int tiles;                    // tiles per slot
+  int64_t n_rows;
+  uint16_t* hist0;              // [n_slots][tiles][4096]
+  uint16_t* hist1;
+  int32_t* vcnt;                // [n_slots][tiles] valid ids per tile (pass-0 tiles)
+  int32_t* scnt;                // [n_slots][tiles] sentinels per tile
+  uint2* tmp;                   // [n] (id, position) after pass 0 of a two-pass slot
+  uint32_t* rows_out;
+  int32_t* pos_out;
+  int32_t* err_flag;
+};
+
+__device__ __forceinline__ int seg_bits(int64_t rows) {  // ids in [0, rows) fit in this many bits
+  int b = 0;
+  while (b < 31 && ((int64_t)1 << b) < rows) ++b;
+  return b;
+}
+
+struct SegSlot {
+  int64_t lo, rows;
+  int w0, w1;
+};
+
+__device__ __forceinline__ SegSlot seg_slot(const SegArgs& a, int s) {
+  SegSlot r;
+  r.lo = a.slot_offsets ? a.slot_offsets[s] : 0;
+  r.rows = a.slot_offsets ? a.slot_offsets[s + 1] - r.lo : a.n_rows;
+  const int bits = seg_bits(r.rows);
+  r.w0 = bits < kSegBits ? bits : kSegBits;
+  r.w1 = bits - r.w0;
+  return r;
+}
+
+// pass 0 block → (slot, tile): the slots' tiles of one example range share an XCD
+__device__ __forceinline__ void seg_tile0(const SegArgs& a, int& s, int& t) {
+  const int x = blockIdx.x % kNumXcd, rest = blockIdx.x / kNumXcd;
+  s = rest % a.n_slots;
+  t = (rest / a.n_slots) * kNumXcd + x;
+}
+// pass 1 block → (slot, tile): one slot's tiles share an XCD
+__device__ __forceinline__ void seg_tile1(const SegArgs& a, int& s, int& t) {
+  const int x = blockIdx.x % kNumXcd, rest = blockIdx.x / kNumXcd;
+  const int spx = (a.n_slots + kNumXcd - 1) / kNumXcd;
+  s = x + kNumXcd * (rest % spx);
+  t = rest / spx;
+}
+
+// the tile's keys of pass 0: id (local to the slot) per lane and k; live = a valid id, sent = a
+// sentinel (excluded or out of range); wave w owns tile entries [w·64·KPL, (w+1)·64·KPL)
+template <bool ID64>
+__device__ __forceinline__ void seg_load0(const SegArgs& a, const SegSlot& sl, int s, int t,
+                                          uint32_t (&id)[kSegKPL], uint32_t& live,
+                                          uint32_t& sent, bool& oob) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  live = 0u;
+  sent = 0u;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const int64_t b = (int64_t)t * kSegTile + wave * 64 * kSegKPL + k * 64 + lane;
+    id[k] = 0u;
+    if (b < a.B) {
+      const int64_t p = b * a.n_slots + s;
+      const int64_t v = ID64 ? static_cast<const int64_t*>(a.ids)[p]
+                             : static_cast<int64_t>(static_cast<const int32_t*>(a.ids)[p]);
+      if (a.valid && !a.valid[p]) {
+        sent |= 1u << k;
+      } else if (v < 0 || v >= sl.rows) {
+        sent |= 1u << k;
+        oob = true;
+      } else {
+        id[k] = static_cast<uint32_t>(v);
+        live |= 1u << k;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void seg_store_hist(uint16_t* __restrict__ h, const int32_t* cnt,
+                                               int bins) {
+  for (int d = threadIdx.x; d < bins; d += blockDim.x) h[d] = static_cast<uint16_t>(cnt[d]);
+}
+
+template <bool ID64>
+__global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a) {
+  __shared__ int32_t cnt[kSegBins];
+  __shared__ int32_t nsent;
+  int s, t;
+  seg_tile0(a, s, t);
+  if (s >= a.n_slots || t >= a.tiles) return;
+  const SegSlot sl = seg_slot(a, s);
+  const int bins = 1 << sl.w0;
+  for (int d = threadIdx.x; d < bins; d += blockDim.x) cnt[d] = 0;
+  if (threadIdx.x == 0) nsent = 0;
+  __syncthreads();
+  uint32_t id[kSegKPL], live, sent;
+  bool oob = false;
+  seg_load0<ID64>(a, sl, s, t, id, live, sent, oob);
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt64();
+  const uint32_t mask = (uint32_t)bins - 1u;
+  int ns = 0;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const bool lv = (live >> k) & 1u;
+    const uint32_t d = id[k] & mask;
+    const uint64_t m = match_digit<kSegBits>(d, lv);
+    if (lv && (m & lt) == 0) atomicAdd(&cnt[d], __popcll(m));
+    ns += __popcll(__ballot((sent >> k) & 1u));
+  }
+  if (lane == 0 && ns) atomicAdd(&nsent, ns);
+  if (__any(oob) && lane == 0) flag_oob(a.err_flag);
+  __syncthreads();
+  const int64_t tile = (int64_t)s * a.tiles + t;
+  seg_store_hist(a.hist0 + tile * kSegBins, cnt, bins);
+  if (threadIdx.x == 0) {
+    const int64_t b0 = (int64_t)t * kSegTile;
+    const int64_t tn = a.B - b0 < kSegTile ? a.B - b0 : kSegTile;
+    a.vcnt[tile] = (int32_t)tn - nsent;
+    a.scnt[tile] = nsent;
+  }
+}
+
+// slot starts: vstart[s] = valid ids of slots < s, sstart[s] = sentinels of slots < s, plus the
+// totals; from the pass-0 tile counts (n_slots x tiles ints, L2)
+__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstart, int32_t* sstart) {
+  if (threadIdx.x < a.n_slots) {
+    int32_t v = 0, z = 0;
+    for (int t = 0; t < a.tiles; ++t) {
+      v += a.vcnt[threadIdx.x * a.tiles + t];
+      z += a.scnt[threadIdx.x * a.tiles + t];
+    }
+    vstart[threadIdx.x] = v;
+    sstart[threadIdx.x] = z;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t rv = 0, rz = 0;
+    for (int q = 0; q <= a.n_slots; ++q) {
+      const int32_t v = q < a.n_slots ? vstart[q] : 0, z = q < a.n_slots ? sstart[q] : 0;
+      vstart[q] = rv;
+      sstart[q] = rz;
+      rv += v;
+      rz += z;
+    }
+  }
+  __syncthreads();
+}
+
+// doff[d] = base + (ids of digits < d in the slot) + (ids of digit d in the slot's tiles < t), from
+// the slot's tile histograms: thread j owns digits [16 j, 16 j + 16)
+__device__ __forceinline__ void seg_digit_offsets(const uint16_t* __restrict__ hist, int n_tiles,
+                                                  int t, int bins, int32_t base,
+                                                  int32_t* __restrict__ doff, int32_t* wsum) {
+  constexpr int PER = kSegBins / kSegThreads;  // 16
+  const int d0 = threadIdx.x * PER;
+  int32_t tot[PER], pre[PER];
+#pragma unroll
+  for (int c = 0; c < PER; ++c) tot[c] = pre[c] = 0;
+  if (d0 < bins) {
+    for (int tt = 0; tt < n_tiles; ++tt) {
+      const uint16_t* h = hist + (int64_t)tt * kSegBins + d0;
+      uint16_t v[PER];
+      if (bins >= PER) {
+        const uint4 x0 = reinterpret_cast<const uint4*>(h)[0], x1 = reinterpret_cast<const uint4*>(h)[1];
+        const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          v[2 * c] = (uint16_t)(w[c] & 0xFFFFu);
+          v[2 * c + 1] = (uint16_t)(w[c] >> 16);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < PER; ++c) v[c] = d0 + c < bins ? h[c] : 0;
+      }
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        tot[c] += v[c];
+        if (tt < t) pre[c] += v[c];
+      }
+    }
+  }
+  int32_t sum = 0;
+#pragma unroll
+  for (int c = 0; c < PER; ++c) sum += tot[c];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t x = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int32_t run = base + x - sum;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {
+    if (d0 + c < bins) doff[d0 + c] = run + pre[c];
+    run += tot[c];
+  }
+}
+
+// stable in-tile ranks: rank[k] = position of key k among the tile's keys of its digit that
+// precede it (waves own consecutive stretches; per-wave running counts, then each digit's
+// counts turned into wave offsets). wcnt: [4][kSegBins] uint16 in LDS.
+__device__ __forceinline__ void seg_rank(const uint32_t (&dig)[kSegKPL], uint32_t live,
+                                         uint16_t (*wcnt)[kSegBins], int bins,
+                                         int32_t (&rank)[kSegKPL]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt64();
+  for (int e = threadIdx.x; e < 4 * bins; e += blockDim.x) wcnt[e / bins][e % bins] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const bool lv = (live >> k) & 1u;
+    const uint32_t d = dig[k];
+    const uint64_t m = match_digit<kSegBits>(d, lv);
+    const int32_t before = __popcll(m & lt);
+    const int32_t prev = lv ? wcnt[wave][d] : 0;
+    rank[k] = prev + before;
+    __builtin_amdgcn_wave_barrier();
+    if (lv && (m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + before + 1);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < bins; d += blockDim.x) {
+    int32_t run = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int32_t c = wcnt[w][d];
+      wcnt[w][d] = (uint16_t)run;
+      run += c;
+    }
+  }
+  __syncthreads();
+}
+
+template <bool ID64>
+__global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs a) {
+  __shared__ uint16_t wcnt[4][kSegBins];
+  __shared__ int32_t doff[kSegBins];
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
+  __shared__ int32_t wsum[4], wsent[4];
+  int s, t;
+  seg_tile0(a, s, t);
+  if (s >= a.n_slots || t >= a.tiles) return;
+  const SegSlot sl = seg_slot(a, s);
+  const int bins = 1 << sl.w0;
+  seg_slot_starts(a, vstart, sstart);
+  const int32_t n_valid = vstart[a.n_slots];
+  int32_t sent_pre = 0;  // sentinels of this slot's earlier tiles
+  for (int tt = 0; tt < t; ++tt) sent_pre += a.scnt[s * a.tiles + tt];
+  seg_digit_offsets(a.hist0 + (int64_t)s * a.tiles * kSegBins, a.tiles, t, bins, vstart[s], doff,
+                    wsum);
+  uint32_t id[kSegKPL], live, sent;
+  bool oob = false;  // flagged by the histogram pass
+  seg_load0<ID64>(a, sl, s, t, id, live, sent, oob);
+  uint32_t dig[kSegKPL];
+  const uint32_t mask = (uint32_t)bins - 1u;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) dig[k] = id[k] & mask;
+  int32_t rank[kSegKPL];
+  seg_rank(dig, live, wcnt, bins, rank);
+  // sentinel ranks: waves in order, lanes in order
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt64();
+  int32_t srank[kSegKPL];
+  int32_t srun = 0;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const uint64_t m = __ballot((sent >> k) & 1u);
+    srank[k] = srun + __popcll(m & lt);
+    srun += __popcll(m);
+  }
+  if (lane == 0) wsent[wave] = srun;
+  __syncthreads();
+  int32_t sbase = n_valid + sstart[s] + sent_pre;
+  for (int w = 0; w < wave; ++w) sbase += wsent[w];
+  const bool final_pass = sl.w1 == 0;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const int64_t b = (int64_t)t * kSegTile + wave * 64 * kSegKPL + k * 64 + lane;
+    const int32_t p = (int32_t)(b * a.n_slots + s);
+    if ((live >> k) & 1u) {
+      const int32_t dst = doff[dig[k]] + wcnt[wave][dig[k]] + rank[k];
+      if (final_pass) {
+        a.rows_out[dst] = static_cast<uint32_t>(sl.lo + id[k]);
+        a.pos_out[dst] = p;
+      } else {
+        a.tmp[dst] = make_uint2(id[k], static_cast<uint32_t>(p));
+      }
+    } else if ((sent >> k) & 1u) {
+      const int32_t dst = sbase + srank[k];
+      a.rows_out[dst] = static_cast<uint32_t>(a.n_rows);
+      a.pos_out[dst] = p;
+    }
+  }
+}
+
+// pass 1 (slots wider than 12 bits): tile t of slot s = tmp[vstart[s] + 4096 t ..) (its valid ids
+// in pass-0 order), digit = id >> w0
+__device__ __forceinline__ void seg_load1(const SegArgs& a, const SegSlot& sl, int32_t start,
+                                          int32_t n_s, int t, uint32_t (&id)[kSegKPL],
+                                          int32_t (&pos)[kSegKPL], uint32_t& live) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  live = 0u;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const int32_t j = t * kSegTile + wave * 64 * kSegKPL + k * 64 + lane;
+    id[k] = 0u;
+    pos[k] = 0;
+    if (j < n_s) {
+      const uint2 e = a.tmp[start + j];
+      id[k] = e.x;
+      pos[k] = static_cast<int32_t>(e.y);
+      live |= 1u << k;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a) {
+  __shared__ int32_t cnt[kSegBins];
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
+  int s, t;
+  seg_tile1(a, s, t);
+  if (s >= a.n_slots || t >= a.tiles) return;
+  const SegSlot sl = seg_slot(a, s);
+  if (sl.w1 == 0) return;
+  seg_slot_starts(a, vstart, sstart);
+  const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
+  const int bins = 1 << sl.w1;
+  for (int d = threadIdx.x; d < bins; d += blockDim.x) cnt[d] = 0;
+  __syncthreads();
+  uint32_t id[kSegKPL], live;
+  int32_t pos[kSegKPL];
+  seg_load1(a, sl, start, n_s, t, id, pos, live);
+  const uint64_t lt = lanemask_lt64();
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const bool lv = (live >> k) & 1u;
+    const uint32_t d = id[k] >> sl.w0;
+    const uint64_t m = match_digit<kSegBits>(d, lv);
+    if (lv && (m & lt) == 0) atomicAdd(&cnt[d], __popcll(m));
+  }
+  __syncthreads();
+  seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins, cnt, bins);
+}
+
+__global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs a) {
+  __shared__ uint16_t wcnt[4][kSegBins];
+  __shared__ int32_t doff[kSegBins];
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
+  __shared__ int32_t wsum[4];
+  int s, t;
+  seg_tile1(a, s, t);
+  if (s >= a.n_slots || t >= a.tiles) return;
+  const SegSlot sl = seg_slot(a, s);
+  if (sl.w1 == 0) return;
+  seg_slot_starts(a, vstart, sstart);
+  const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
+  const int n_tiles_s = (n_s + kSegTile - 1) / kSegTile;
+  if (t >= n_tiles_s) return;  // uniform per block: after the block-wide syncs above
+  const int bins = 1 << sl.w1;
+  seg_digit_offsets(a.hist1 + (int64_t)s * a.tiles * kSegBins, n_tiles_s, t, bins, start, doff,
+                    wsum);
+  uint32_t id[kSegKPL], live;
+  int32_t pos[kSegKPL];
+  seg_load1(a, sl, start, n_s, t, id, pos, live);
+  uint32_t dig[kSegKPL];
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) dig[k] = id[k] >> sl.w0;
+  int32_t rank[kSegKPL];
+  seg_rank(dig, live, wcnt, bins, rank);
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    if ((live >> k) & 1u) {
+      const int32_t dst = doff[dig[k]] + wcnt[wave][dig[k]] + rank[k];
+      a.rows_out[dst] = static_cast<uint32_t>(sl.lo + id[k]);
+      a.pos_out[dst] = pos[k];
+    }
+  }
+}
+
+static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArgs* a) {
+  uint16_t* h0 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
+  uint16_t* h1 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
+  int32_t* v = c.take<int32_t>((size_t)n_slots * tiles);
+  int32_t* z = c.take<int32_t>((size_t)n_slots * tiles);
+  uint2* tmp = c.take<uint2>(n);
+  if (a) {
+    a->hist0 = h0;
+    a->hist1 = h1;
+    a->vcnt = v;
+    a->scnt = z;
+    a->tmp = tmp;
+  }
+  return c.off;
+}
+
+// the slot-segmented sort fits: one GPU, ids [B, n_slots], B <= 32 tiles, every slot < 2^24 rows
+static bool seg_eligible(int64_t n_ids, int n_slots, int world, int64_t max_slot_rows) {
+  if (world != 1 || n_slots < 1 || n_slots > kSegMaxSlots || n_ids < 1) return false;
+  if (n_ids % n_slots) return false;
+  const int64_t B = n_ids / n_slots;
+  return B <= (int64_t)kSegMaxTiles * kSegTile && max_slot_rows >= 1 &&
+         max_slot_rows <= ((int64_t)1 << kSegMaxBits);
+}
+
+size_t seg_ws_size(int64_t n_ids) {
+  // tiles over all slots <= n/4096 + n_slots (each slot rounds up once)
+  const int64_t tiles_total = n_ids / kSegTile + kSegMaxSlots;
+  Carver c(nullptr, 0);
+  c.take<uint16_t>((size_t)tiles_total * kSegBins);
+  c.take<uint16_t>((size_t)tiles_total * kSegBins);
+  c.take<int32_t>((size_t)tiles_total);
+  c.take<int32_t>((size_t)tiles_total);
+  c.take<uint2>(n_ids);
+  return c.off + 1024;
+}
+
+static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const uint8_t* valid,
+                        const int64_t* slot_offsets, int n_slots, int64_t n_rows,
+                        uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* err_flag,
+                        void* workspace, size_t ws_bytes, hipStream_t st) {
+  SegArgs a{};
+  a.ids = ids;
+  a.dtype = id_dtype;
+  a.valid = valid;
+  a.slot_offsets = slot_offsets;
+  a.n_slots = n_slots;
+  a.B = n_ids / n_slots;
+  a.tiles = (int)ceil_div(a.B, kSegTile);
+  a.n_rows = n_rows;
+  a.rows_out = sorted_rows;
+  a.pos_out = sorted_pos;
+  a.err_flag = err_flag;
+  Carver c(workspace, ws_bytes);
+  seg_ws_layout(n_ids, n_slots, a.tiles, c, &a);
+  if (!c.ok()) {
+    set_error("sort workspace too small: need %zu have %zu", c.off, ws_bytes);
+    return RS_E_WORKSPACE;
+  }
+  const int tiles_pad = (int)ceil_div(a.tiles, kNumXcd) * kNumXcd;
+  const int grid0 = tiles_pad * n_slots;
+  const int spx = (int)ceil_div(n_slots, kNumXcd);
+  const int grid1 = kNumXcd * spx * a.tiles;
+  if (id_dtype == RS_ID_I64) slot_sort_hist0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
+  else slot_sort_hist0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  if (id_dtype == RS_ID_I64) slot_sort_scatter0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
+  else slot_sort_scatter0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  // pass 1 only matters for slots wider than 12 bits; its blocks of narrower slots exit at once
+  slot_sort_hist1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  slot_sort_scatter1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -656,13 +1165,25 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                              const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                              int32_t world, uint32_t* sorted_keys, int32_t* sorted_pos,
                              int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
-                             hipStream_t st, const uint8_t* valid);
+                             hipStream_t st, const uint8_t* valid, int64_t max_slot_rows);
+
+// RS_SORT_LSD=1: every id sort takes the three-pass LSD form (A/B against the slot-segmented
+// sort; the two give the same output). Read once per process.
+static bool sort_lsd_forced() {
+  static const int v = [] {
+    const char* e = getenv("RS_SORT_LSD");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
+}
 
 extern "C" size_t rs_sort_ids_workspace_size(int64_t n_ids) {
   Carver c(nullptr, 0);
   c.take<uint32_t>(n_ids);
   c.take<int32_t>(n_ids);
-  return c.off + radix_sort_ws_size(n_ids) + exclusive_scan_ws_size(n_ids) + 1024;
+  const size_t lsd = c.off + radix_sort_ws_size(n_ids) + exclusive_scan_ws_size(n_ids) + 1024;
+  const size_t seg = seg_ws_size(n_ids);
+  return lsd > seg ? lsd : seg;
 }
 
 extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
@@ -670,7 +1191,8 @@ extern "C" int32_t rs_sort_ids(const void* ids, int32_t id_dtype, int64_t n_ids,
                                uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
                                int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream) {
   return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
-                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr);
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr,
+                       n_rows);
 }
 
 extern "C" int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t n_ids,
@@ -680,7 +1202,20 @@ extern "C" int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t
                                       void* workspace, size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(valid || n_ids == 0, "valid is null");
   return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
-                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), valid);
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), valid,
+                       n_rows);
+}
+
+extern "C" int32_t rs_sort_ids_slots(const void* ids, int32_t id_dtype, int64_t n_ids,
+                                     const uint8_t* valid, const int64_t* slot_offsets,
+                                     int32_t n_slots, int64_t n_rows, int64_t max_slot_rows,
+                                     uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
+                                     int32_t* err_flag, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  RS_CHECK_ARG(max_slot_rows >= 1 && max_slot_rows <= n_rows, "max_slot_rows out of range");
+  return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, 1, sorted_rows,
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), valid,
+                       max_slot_rows);
 }
 
 extern "C" int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_t n_ids,
@@ -689,7 +1224,8 @@ extern "C" int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_
                                        int32_t* n_unique, int32_t* err_flag, void* workspace,
                                        size_t ws_bytes, void* stream) {
   return sort_ids_impl(ids, id_dtype, n_ids, slot_offsets, n_slots, n_rows, world, sorted_keys,
-                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr);
+                       sorted_pos, n_unique, err_flag, workspace, ws_bytes, as_stream(stream), nullptr,
+                       n_rows);
 }
 
 extern "C" int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos,
@@ -735,7 +1271,7 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                              const int64_t* slot_offsets, int32_t n_slots, int64_t n_rows,
                              int32_t world, uint32_t* sorted_rows, int32_t* sorted_pos,
                              int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
-                             hipStream_t st, const uint8_t* valid) {
+                             hipStream_t st, const uint8_t* valid, int64_t max_slot_rows) {
   RS_CHECK_ARG(n_ids >= 0 && n_ids < (int64_t(1) << 31), "n_ids out of range");
   RS_CHECK_ARG(n_rows > 0 && n_rows < (int64_t(1) << 31) - 1, "n_rows out of range");
   RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
@@ -747,6 +1283,19 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
   RS_CHECK_ARG(key_space < (int64_t(1) << 31) - 1, "key space out of range");
   if (n_unique) RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, sizeof(int32_t), st));
   if (n_ids == 0) return RS_OK;
+  if ((slot_offsets || n_slots == 1) && seg_eligible(n_ids, n_slots, world, max_slot_rows) &&
+      !sort_lsd_forced()) {
+    // the slot-segmented sort: same output, four launches (RS_SORT_LSD=1: the LSD sort, A/B)
+    int32_t s = seg_sort(ids, id_dtype, n_ids, valid, slot_offsets, n_slots, n_rows, sorted_rows,
+                         sorted_pos, err_flag, workspace, ws_bytes, st);
+    if (s) return s;
+    if (n_unique) {
+      const int cblocks = (int)std::min<int64_t>(ceil_div(ceil_div(n_ids, 4), 256), 2048);
+      count_unique_kernel<<<cblocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);
+      RS_CHECK_LAUNCH();
+    }
+    return RS_OK;
+  }
   Carver c(workspace, ws_bytes);
   uint32_t* keys = c.take<uint32_t>(n_ids);
   int32_t* vals = c.take<int32_t>(n_ids);
@@ -759,7 +1308,9 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
   // pass 0 makes the keys from the ids (slot offset + id; owner-major when world > 1)
   const KeyGen kg{ids, id_dtype, slot_offsets, n_slots, n_rows, world, shard_stride, key_space, err_flag,
                   valid};
-  int32_t s = radix_sort_impl(keys, vals, sorted_rows, sorted_pos, n_ids, key_space,
+  const int64_t max_key = key_space + (slot_offsets ? n_slots - 1 : 0);  // slot sentinels
+  RS_CHECK_ARG(max_key < (int64_t(1) << 31) - 1, "key space out of range");
+  int32_t s = radix_sort_impl(keys, vals, sorted_rows, sorted_pos, n_ids, max_key,
                               static_cast<char*>(workspace) + rest_off, ws_bytes - rest_off, &kg, st);
   if (s) return s;
   if (n_unique) {

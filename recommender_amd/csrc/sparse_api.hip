@@ -123,3 +123,34 @@ extern "C" int32_t rs_apply_keras_dense_adam(float* table, float* m, float* v, i
   if (st) return st;
   return rs_keras_adam_dense_sweep(table, m, v, n_rows, dim, params, touched_bitmap, stream);
 }
+
+// Deterministic index_add (the backward of a row gather): rs_sort_ids_masked over the ids (one
+// shared table of n_rows rows), then rs_embedding_grad_dense — out zeroed, each touched row the
+// tiled fixed-order sum of its rows.
+extern "C" size_t rs_index_add_rows_workspace_size(int64_t n, int32_t dim) {
+  const int64_t m = n < 1 ? 1 : n;
+  size_t a = rs_sort_ids_workspace_size(m), c = rs_apply_workspace_size(m, dim);
+  return sorted_head(m) + (a > c ? a : c);
+}
+
+extern "C" int32_t rs_index_add_rows(const void* ids, int32_t id_dtype, int64_t n,
+                                     const uint8_t* valid, const float* rows, int32_t dim,
+                                     int64_t n_rows, float* out, int32_t* err_flag,
+                                     void* workspace, size_t ws_bytes, void* stream) {
+  RS_CHECK_ARG(n >= 0 && dim >= 1 && n_rows >= 1, "rs_index_add_rows: bad sizes");
+  RS_CHECK_ARG(out && (n == 0 || (ids && rows)), "rs_index_add_rows: null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_index_add_rows_workspace_size(n, dim),
+               "rs_index_add_rows: workspace too small");
+  SortedScratch s;
+  RS_CHECK_ARG(carve(workspace, ws_bytes, n < 1 ? 1 : n, s), "rs_index_add_rows: workspace too small");
+  if (n > 0) {
+    const int32_t st = valid ? rs_sort_ids_masked(ids, id_dtype, n, valid, nullptr, 1, n_rows,
+                                                  s.rows, s.pos, nullptr, err_flag, s.rest,
+                                                  s.rest_bytes, stream)
+                             : rs_sort_ids(ids, id_dtype, n, nullptr, 1, n_rows, s.rows, s.pos,
+                                           nullptr, err_flag, s.rest, s.rest_bytes, stream);
+    if (st) return st;
+  }
+  return rs_embedding_grad_dense(s.rows, s.pos, n, rows, dim, n_rows, out, s.rest, s.rest_bytes,
+                                 stream);
+}

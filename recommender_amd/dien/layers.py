@@ -53,14 +53,15 @@ def _rows_ready(X, H):
 
 def _valid_rows(mask_u8):
     """(idx [R] int32, count [1] int32) of the rows with mask != 0, in order (on the device).
-    Kept on the mask tensor object, so the layers of one forward that share it (the GRU and the
-    AUGRU of DIEN) list the rows once."""
+    Kept on the mask tensor object with its version counter, so the layers of one forward that
+    share it (the GRU and the AUGRU of DIEN) list the rows once, and a mask buffer refilled in
+    place (a static step's inputs, an eval loop) is listed again."""
     got = getattr(mask_u8, "_rs_valid_rows", None)
-    if got is not None:
-        return got
-    got = _valid_rows_list(mask_u8)
-    mask_u8._rs_valid_rows = got
-    return got
+    if got is not None and got[0] == mask_u8._version:
+        return got[1]
+    rows = _valid_rows_list(mask_u8)
+    mask_u8._rs_valid_rows = (mask_u8._version, rows)
+    return rows
 
 
 def _valid_rows_list(mask_u8):

@@ -39,6 +39,12 @@ class Embedding(nn.Module):
         self.register_buffer("weight", w)
         self.register_buffer("slot_offsets",
                              None if slot_offsets is None else slot_offsets.to(device, torch.int64))
+        # the largest slot's row count, host-side (the sort picks its form from it)
+        if slot_offsets is None:
+            self.max_slot_rows = self.input_dim
+        else:
+            so = torch.as_tensor(slot_offsets).to("cpu", torch.int64)
+            self.max_slot_rows = max(1, int((so[1:] - so[:-1]).max())) if so.numel() > 1 else 1
         self.register_buffer("err_flag", torch.zeros(1, dtype=torch.int32, device=device))
         # zero-size leaf that keeps the lookup inside the autograd graph
         self.grad_handle = nn.Parameter(torch.zeros(0, device=device), requires_grad=True)

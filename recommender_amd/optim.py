@@ -49,13 +49,16 @@ class _Workspace:
 
 
 class SortedIds:
-    """Radix-sorted ids of one step (rs_sort_ids): sorted rows (uint32 bits in int32),
-    original positions, device count of distinct valid rows."""
+    """Radix-sorted ids of one step (rs_sort_ids_slots / rs_sort_ids_sharded): sorted rows
+    (uint32 bits in int32), original positions, device count of distinct valid rows."""
 
     def __init__(self, ids: torch.Tensor, n_rows: int, slot_offsets: torch.Tensor | None = None,
                  err_flag: torch.Tensor | None = None, ws: _Workspace | None = None,
-                 count_unique: bool = True, world: int = 1, valid: torch.Tensor | None = None):
-        """valid (uint8 [n], optional): positions with 0 are left out (sentinel key, no flag)."""
+                 count_unique: bool = True, world: int = 1, valid: torch.Tensor | None = None,
+                 max_slot_rows: int | None = None):
+        """valid (uint8 [n], optional): positions with 0 are left out (sentinel key, no flag).
+        max_slot_rows: the largest slot's row count (host-known; Embedding.max_slot_rows) — it
+        lets a slab whose slots are all < 2^24 rows take the slot-segmented sort."""
         ws = ws or _Workspace()
         ids = ids.contiguous()
         L.require_device(ids, "ids")
@@ -68,17 +71,14 @@ class SortedIds:
         n_slots = 1 if slot_offsets is None else slot_offsets.numel() - 1
         nbytes = L.lib().rs_sort_ids_workspace_size(n)
         w = ws.get("sort", nbytes, dev)
-        if valid is not None:
-            if world != 1 or valid.numel() != n or valid.dtype != torch.uint8:
-                raise ValueError("valid: a uint8 flag per id, one GPU")
-            L.call("rs_sort_ids_masked", L.ptr(ids), L.id_dtype_code(ids), n,
-                   L.ptr(valid.contiguous()), L.ptr(slot_offsets), n_slots, int(n_rows),
-                   L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique), L.ptr(err_flag),
-                   L.ptr(w), w.numel(), L.stream_ptr(dev))
-        elif world == 1:
-            L.call("rs_sort_ids", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets), n_slots,
-                   int(n_rows), L.ptr(self.rows), L.ptr(self.pos), L.ptr(self.n_unique),
-                   L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
+        if valid is not None and (world != 1 or valid.numel() != n or valid.dtype != torch.uint8):
+            raise ValueError("valid: a uint8 flag per id, one GPU")
+        if world == 1:
+            msr = int(n_rows) if max_slot_rows is None else int(max_slot_rows)
+            L.call("rs_sort_ids_slots", L.ptr(ids), L.id_dtype_code(ids), n,
+                   L.ptr(None if valid is None else valid.contiguous()), L.ptr(slot_offsets),
+                   n_slots, int(n_rows), msr, L.ptr(self.rows), L.ptr(self.pos),
+                   L.ptr(self.n_unique), L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
         else:
             L.call("rs_sort_ids_sharded", L.ptr(ids), L.id_dtype_code(ids), n, L.ptr(slot_offsets),
                    n_slots, int(n_rows), int(world), L.ptr(self.rows), L.ptr(self.pos),
@@ -88,7 +88,7 @@ class SortedIds:
     def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None,
                   count_unique: bool = True, valid: torch.Tensor | None = None):
         return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws, count_unique,
-                   valid=valid)
+                   valid=valid, max_slot_rows=getattr(table, "max_slot_rows", None))
 
 
 def dedup_grad(table: Embedding, ids: torch.Tensor, grad_rows: torch.Tensor,

@@ -145,8 +145,8 @@ class _MultiHotMeanFn(torch.autograd.Function):
         V, D = w.shape
         N, G = items.numel(), mh.shape[1]
         out = torch.empty(N, D, device=w.device)
-        L.call("rs_multihot_mean_fwd", L.ptr(w), V, D, L.ptr(mh), G, L.ptr(items), N, L.ptr(out),
-               L.ptr(table_module.err_flag), L.stream_ptr(w.device))
+        L.call("rs_multihot_mean_fwd", L.ptr(w), V, D, L.ptr(mh), G, mh.shape[0], L.ptr(items), N,
+               L.ptr(out), L.ptr(table_module.err_flag), L.stream_ptr(w.device))
         ctx.table_module, ctx.mh, ctx.items = table_module, mh, items
         return out
 
@@ -160,9 +160,9 @@ class _MultiHotMeanFn(torch.autograd.Function):
         dev = g.device
         dtable = torch.empty(V, D, device=dev)
         ws = _ws("multihot_bwd", L.lib().rs_multihot_mean_bwd_workspace_size(N, V, D), dev)
-        L.call("rs_multihot_mean_bwd", L.ptr(ctx.mh), G, L.ptr(ctx.items), N,
-               L.ptr(g.contiguous()), V, D, L.ptr(dtable), L.ptr(ws), ws.numel(),
-               L.stream_ptr(dev))
+        L.call("rs_multihot_mean_bwd", L.ptr(ctx.mh), G, ctx.mh.shape[0], L.ptr(ctx.items), N,
+               L.ptr(g.contiguous()), V, D, L.ptr(dtable), L.ptr(tm.err_flag), L.ptr(ws),
+               ws.numel(), L.stream_ptr(dev))
         _lookup_backward(tm, _arange_i32(V, dev), dtable, None)
         return None, None, None, None
 

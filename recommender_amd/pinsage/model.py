@@ -10,13 +10,69 @@ from .graph import NID, HeteroGraph, PairGraph
 from .layers import FeatureProjector, SageNet
 
 
+_err_flags: dict = {}
+
+
+def oob_flag(dev) -> torch.Tensor:
+    """The device int32 flag the fused pair kernels set (RS_ERRBIT_OOB) for a node id past h's
+    rows (the index_select they replace raised on one)."""
+    f = _err_flags.get(dev)
+    if f is None:
+        f = torch.zeros(1, dtype=torch.int32, device=dev)
+        _err_flags[dev] = f
+    return f
+
+
+_ws_bufs: dict = {}
+
+
+def _ws(name, nbytes, dev):
+    b = _ws_bufs.get((name, dev))
+    if b is None or b.numel() < nbytes:
+        b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        _ws_bufs[(name, dev)] = b
+    return b
+
+
+class _GatherRowsFn(torch.autograd.Function):
+    """h.index_select(0, idx) whose backward is a fixed-order index_add (rs_index_add_rows:
+    sort + tiled segmented sum) — run-to-run identical, where index_select's backward adds
+    colliding rows with float atomics in arrival order."""
+
+    @staticmethod
+    def forward(ctx, h, idx):
+        ctx.save_for_backward(idx)
+        ctx.n_rows = h.shape[0]
+        return h.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        g = g.contiguous()
+        n, D = idx.numel(), g.shape[1]
+        dev = g.device
+        dh = torch.empty(ctx.n_rows, D, device=dev, dtype=g.dtype)
+        ws = _ws("index_add", L.lib().rs_index_add_rows_workspace_size(n, D), dev)
+        L.call("rs_index_add_rows", L.ptr(idx), L.id_dtype_code(idx), n, None, L.ptr(g), D,
+               ctx.n_rows, L.ptr(dh), L.ptr(oob_flag(dev)), L.ptr(ws), ws.numel(),
+               L.stream_ptr(dev))
+        return dh, None
+
+
+def gather_rows(h: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """h[idx] with a deterministic backward on the GPU (fp32 2-D h), index_select elsewhere."""
+    if h.is_cuda and h.dim() == 2 and h.dtype == torch.float32 and h.requires_grad:
+        return _GatherRowsFn.apply(h, idx.contiguous())
+    return h.index_select(0, idx)
+
+
 def item2item_scorer(graph: PairGraph, h: torch.Tensor) -> torch.Tensor:
     """apply_edges(u_dot_v) (model.py:14-19): score [E, 1] = h[src] · h[dst]."""
     src, dst = graph.src.to(torch.int64), graph.dst.to(torch.int64)
     if graph.valid is not None:  # capacity-shaped: padding pairs (-1) score node 0, masked later
         src, dst = src.clamp_min(0), dst.clamp_min(0)
-    s = h.index_select(0, src)
-    d = h.index_select(0, dst)
+    s = gather_rows(h, src)
+    d = gather_rows(h, dst)
     return (s * d).sum(dim=-1, keepdim=True)
 
 
@@ -33,7 +89,8 @@ class _PairMarginFn(torch.autograd.Function):
     """item2item_scorer on both pair graphs + margin_loss in one kernel each way
     (rs_pair_margin_fwd / _bwd): the row gathers, products, sums, clamp, mask and mean were a
     dozen recorded ops forward and as many backward (a capacity-shaped static step replays every
-    one of them as a graph node)."""
+    one of them as a graph node). The backward folds each node's pair terms in a fixed order
+    (rs_index_add_rows inside rs_pair_margin_bwd): deterministic."""
 
     @staticmethod
     def forward(ctx, h, ps, pd, ns, nd, valid, n_valid, delta):
@@ -43,11 +100,11 @@ class _PairMarginFn(torch.autograd.Function):
         pos = torch.empty(P, device=dev)
         neg = torch.empty(P, device=dev)
         loss = torch.empty((), device=dev)
-        ws = torch.empty(L.lib().rs_pair_margin_workspace_size(P), dtype=torch.uint8, device=dev)
+        ws = _ws("pair_fwd", L.lib().rs_pair_margin_workspace_size(P), dev)
         # a bool mask's bytes are the 0 / 1 flags the kernel reads
-        L.call("rs_pair_margin_fwd", L.ptr(h), D, D, L.ptr(ps), L.ptr(pd), L.ptr(ns), L.ptr(nd), P,
-               float(delta), L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg), L.ptr(loss),
-               L.ptr(ws), ws.numel(), L.stream_ptr(dev))
+        L.call("rs_pair_margin_fwd", L.ptr(h), D, D, h.shape[0], L.ptr(ps), L.ptr(pd), L.ptr(ns),
+               L.ptr(nd), P, float(delta), L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg),
+               L.ptr(loss), L.ptr(oob_flag(dev)), L.ptr(ws), ws.numel(), L.stream_ptr(dev))
         ctx.save_for_backward(h, ps, pd, ns, nd, valid, n_valid, pos, neg)
         ctx.delta = float(delta)
         return loss
@@ -56,10 +113,13 @@ class _PairMarginFn(torch.autograd.Function):
     def backward(ctx, g):
         h, ps, pd, ns, nd, valid, n_valid, pos, neg = ctx.saved_tensors
         P, D = ps.numel(), h.shape[1]
-        dh = torch.zeros_like(h)
-        L.call("rs_pair_margin_bwd", L.ptr(h), D, D, L.ptr(ps), L.ptr(pd), L.ptr(ns), L.ptr(nd), P,
-               ctx.delta, L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg),
-               L.ptr(g.reshape(1).contiguous()), L.ptr(dh), D, L.stream_ptr(h.device))
+        dev = h.device
+        dh = torch.empty_like(h)
+        ws = _ws("pair_bwd", L.lib().rs_pair_margin_bwd_workspace_size(P, D), dev)
+        L.call("rs_pair_margin_bwd", L.ptr(h), D, D, h.shape[0], L.ptr(ps), L.ptr(pd), L.ptr(ns),
+               L.ptr(nd), P, ctx.delta, L.ptr(valid), L.ptr(n_valid), L.ptr(pos), L.ptr(neg),
+               L.ptr(g.reshape(1).contiguous()), L.ptr(dh), L.ptr(oob_flag(dev)), L.ptr(ws),
+               ws.numel(), L.stream_ptr(dev))
         return dh, None, None, None, None, None, None, None
 
 

@@ -332,3 +332,19 @@ def test_batch_norm_kernels_vs_float64(B, training):
     else:
         assert torch.equal(bn.moving_mean.double(), mm0)
         assert torch.equal(bn.moving_variance.double(), mv0)
+
+
+def test_valid_rows_cache_follows_in_place_refill():
+    """The valid-row list kept on a uint8 mask is rebuilt when the same buffer is refilled in
+    place (a static step's inputs, an eval loop): never the previous batch's rows."""
+    from recommender_amd.dien.layers import _valid_rows
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    m = (torch.rand(64, 20, device=DEV, generator=g) < 0.3).to(torch.uint8)
+    idx, cnt = _valid_rows(m)
+    ref = torch.nonzero(m.reshape(-1)).reshape(-1).to(torch.int32)
+    assert int(cnt) == ref.numel() and torch.equal(idx[: ref.numel()], ref)
+    m.copy_((torch.rand(64, 20, device=DEV, generator=g) < 0.6).to(torch.uint8))
+    idx2, cnt2 = _valid_rows(m)
+    ref2 = torch.nonzero(m.reshape(-1)).reshape(-1).to(torch.int32)
+    assert int(cnt2) == ref2.numel() and torch.equal(idx2[: ref2.numel()], ref2)

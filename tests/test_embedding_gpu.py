@@ -177,6 +177,67 @@ def test_sort_ids_large_slab_four_passes(per_slot, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("B", [1, 4095, 4096, 4097, 65536, 131072])
+@pytest.mark.parametrize("layout", ["slab26", "shared"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_sort_ids_slot_segmented(B, layout, masked, rng):
+    """The slot-segmented sort (rs_sort_ids_slots: per-slot two-pass 12-bit LSD, 4 launches)
+    against the oracle's stable sort, bit-exact: tile edges (4096-example tiles, up to the
+    32-tile limit), one-row / 12-bit / 13-bit / 2^24-row / Criteo-scale slots (one and two
+    passes), int32 and int64 ids, out-of-range ids in several slots and masked positions (the
+    sentinels grouped by slot after all valid rows), the unique count."""
+    if layout == "slab26":
+        cards = [1, 4096, 4097, 1 << 24, 12_010_734, 3, 100_000] + [1000 + 37 * i for i in range(19)]
+        S = len(cards)
+        so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+        V = int(so[-1])
+        ids = np.stack([zipf_ids(rng, B, c) for c in cards], 1).astype(np.int64)
+        for j, c in enumerate(cards):  # every third id uniform: all digits of wide slots
+            ids[1::3, j] = rng.integers(0, c, ids[1::3, j].shape)
+        ids[::53, 4] = cards[4] + 11  # OOB in two slots
+        ids[::71, 9] = -2
+        dev_so = torch.from_numpy(so).to(DEV)
+        msr = max(cards)
+    else:
+        S, V = 1, 5_000_000
+        so, dev_so, msr = None, None, None
+        ids = zipf_ids(rng, B, V).astype(np.int64)
+        ids[::61] = V + 1
+    dt = np.int32 if masked else np.int64  # both id widths
+    ids_t = torch.from_numpy(ids.astype(dt)).to(DEV)
+    flat = ids.reshape(-1)
+    if masked:
+        keep = rng.random(flat.size) < 0.7
+        s = SortedIds(ids_t, V, dev_so, valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV),
+                      max_slot_rows=msr)
+        rows_ref, pos_ref, nu_ref = O.sort_ids(np.where(keep, flat, -1).reshape(ids.shape), V, so)
+    else:
+        s = SortedIds(ids_t, V, dev_so, max_slot_rows=msr)
+        rows_ref, pos_ref, nu_ref = O.sort_ids(ids, V, so)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
+def test_sort_ids_lsd_slot_sentinels(rng):
+    """A slab with a slot past 2^24 rows takes the LSD sort: its sentinels (OOB ids in several
+    slots, masked positions) come out grouped by slot like the slot-segmented sort's."""
+    cards = [40_000_000, 17, 300_000, 5]
+    S, B = len(cards), 20_000
+    so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+    V = int(so[-1])
+    ids = np.stack([zipf_ids(rng, B, c) for c in cards], 1).astype(np.int64)
+    ids[::29, 1] = 99
+    ids[::31, 3] = -1
+    keep = rng.random(ids.size) < 0.8
+    s = SortedIds(torch.from_numpy(ids).to(DEV), V, torch.from_numpy(so).to(DEV),
+                  valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV), max_slot_rows=max(cards))
+    rows_ref, pos_ref, nu_ref = O.sort_ids(np.where(keep, ids.reshape(-1), -1).reshape(ids.shape), V, so)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
 def test_sort_ids_empty():
     s = SortedIds(torch.zeros(0, dtype=torch.int64, device=DEV), 10)
     assert s.n == 0 and int(s.n_unique.item()) == 0

@@ -20,6 +20,20 @@ def test_every_header_symbol_has_a_python_signature():
     assert set(L.header_symbols()) <= set(L._SIGS)
 
 
+def test_build_id_matches_sources_and_stale_library_is_refused(lib):
+    from recommender_amd.build import source_hash
+
+    assert lib.rs_build_id().decode() == source_hash()
+
+    class Stale:
+        @staticmethod
+        def rs_build_id():
+            return b"0000000000000000"
+
+    with pytest.raises(L.RecsysError, match="other sources"):
+        L.check_build_id(Stale(), "stale.so")
+
+
 def test_argument_validation_without_gpu(lib):
     # null table with n_ids > 0 → RS_E_INVALID and a message, no device access
     st = lib.rs_embedding_fwd(None, 10, 4, None, 1, 5, None, 1, None, None, None)

@@ -15,6 +15,7 @@ from recommender_amd import _lib as L
 from recommender_amd.pinsage import PinSageModel, PinSageSampler
 from recommender_amd.pinsage.graph import HeteroGraph
 from recommender_amd.pinsage.layers import frobenius_normalize, weighted_mean_agg
+from recommender_amd.pinsage.model import oob_flag as model_oob_flag
 from recommender_amd.pinsage.sampler import item_pairs
 from recommender_amd.pinsage.train import PinSageStep
 from tests.conftest import assert_close_rel, assert_close_f64
@@ -277,11 +278,28 @@ def test_pinsage_model_forward_backward():
     smp = PinSageSampler(g, g.itype, g.utype, 2, 2, 4, 0.0, 3, seed=4)
     h, p, n = item_pairs(g, 128, 4, 0)
     pos_g, neg_g, blocks = smp.sample_from_item_pairs(h, p, n)
-    pos, neg = model(pos_g, neg_g, blocks)
+    from recommender_amd.optim import densify_grad
     from recommender_amd.pinsage.model import margin_loss, item2item_scorer
 
-    loss = margin_loss(pos, neg)
-    loss.backward()
+    def run():
+        for prm in model.parameters():
+            prm.grad = None
+        pos, neg = model(pos_g, neg_g, blocks)
+        loss = margin_loss(pos, neg)
+        loss.backward()
+        grads = {n: prm.grad.clone() for n, prm in model.named_parameters() if prm.grad is not None}
+        for t, name in zip(model.tables(), ("year", "genre", "id")):
+            ids, rows = t.take_grad()
+            grads[f"table {name}"] = densify_grad(t, ids, rows)
+        return pos.detach(), neg.detach(), loss, grads
+
+    pos, neg, loss, grads = run()
+    # deterministic: the same step again gives the same bits (no float atomics on the path)
+    pos2, neg2, loss2, grads2 = run()
+    assert torch.equal(pos, pos2) and torch.equal(neg, neg2) and torch.equal(loss, loss2)
+    assert grads.keys() == grads2.keys()
+    for k in grads:
+        assert torch.equal(grads[k], grads2[k]), f"{k} differs between two identical steps"
     # the restatement in float64 (the reference) and in fp32 (its rounding: the noise sample of
     # tests/conftest.py assert_close_f64: 1e-5 relative + 4x the fp32 error + 1e-6 of the largest)
     ref = {}
@@ -294,10 +312,10 @@ def test_pinsage_model_forward_backward():
     (p64, n64, l64, P64), (p32, n32, _, P32) = ref[torch.float64], ref[torch.float32]
 
     def close(got, name, r64, r32):
-        # one fp32 sample of the restatement's rounding; the model sums some rows in other
-        # orders (the genre multi-hot mean sequentially, the row gathers' backward by atomics in
-        # arrival order, so the fp32 path is not even run-to-run identical): 8x its error
-        assert_close_f64(got, r64, r32, name, floor=1e-6, noise=8.0)
+        # one fp32 sample of the restatement's rounding (the model sums some rows in other,
+        # fixed orders: the genre multi-hot mean sequentially, the row gathers' backward by
+        # sorted tiles): 4x its error, tests/conftest.py's default
+        assert_close_f64(got, r64, r32, name, floor=1e-6, noise=4.0)
 
     close(pos, "pos score", p64, p32)
     close(neg, "neg score", n64, n32)
@@ -309,11 +327,9 @@ def test_pinsage_model_forward_backward():
                   (c.fc_2.kernel, f"c{li}k2"), (c.fc_2.bias, f"c{li}b2")]
     for prm, name in pairs:
         close(prm.grad, name, P64[name].grad, P32[name].grad)
-    for t, name in zip(model.tables(), ("year", "genre", "id")):
-        ids, rows = t.take_grad()
-        dense = torch.zeros_like(t.weight).index_add(0, ids.reshape(-1).long(),
-                                                     rows.reshape(-1, t.output_dim))
-        close(dense, f"table {name}", P64[name].grad, P32[name].grad)
+    assert int(model_oob_flag(pos.device)) == 0
+    for name in ("year", "genre", "id"):
+        close(grads[f"table {name}"], f"table {name}", P64[name].grad, P32[name].grad)
 
 
 def test_pinsage_train_steps_reduce_loss():
@@ -832,9 +848,47 @@ def test_pair_margin_loss_fused_matches_scorer_and_margin(padded):
     ref = margin_loss(item2item_scorer(pos_g, h2), item2item_scorer(neg_g, h2), 1.0, valid, n_valid)
     ref.backward()
     assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
-    # a row's gradient sums its pairs' terms in atomic (arrival) order, as the index_add of the
-    # gathers it replaces: near-cancelling elements judged against the largest
+    # a row's gradient sums its pairs' terms in sorted-tile order (the reference's index_add in
+    # atomic arrival order): near-cancelling elements judged against the largest
     assert_close_rel(h1.grad.cpu(), h2.grad.cpu(), rtol=1e-5, scale=float(h2.grad.abs().max()) * 1e-1)
+    # deterministic: the same call again gives the same bits
+    h3 = h.clone().requires_grad_()
+    loss3 = pair_margin_loss(pos_g, neg_g, h3, 1.0)
+    loss3.backward()
+    assert torch.equal(loss3, loss) and torch.equal(h3.grad, h1.grad)
+    assert int(model_oob_flag(h.device)) == 0
+
+
+def test_pair_margin_out_of_range_node_flags_and_reads_zero():
+    """A pair endpoint past h's rows (the index_select it replaces raised) reads a zero row,
+    receives no gradient and sets RS_ERRBIT_OOB; the other pairs are unaffected."""
+    from recommender_amd.pinsage.graph import PairGraph
+    from recommender_amd.pinsage.model import pair_margin_loss
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    N, D, P = 50, 8, 64
+    h = torch.randn(N, D, device=DEV, generator=g)
+    src = torch.randint(0, N, (P,), device=DEV, generator=g, dtype=torch.int32)
+    pdst = torch.randint(0, N, (P,), device=DEV, generator=g, dtype=torch.int32)
+    ndst = torch.randint(0, N, (P,), device=DEV, generator=g, dtype=torch.int32)
+    flag = model_oob_flag(h.device)
+    flag.zero_()
+    ndst[3] = N + 5
+    pos_g = PairGraph(src, pdst, torch.arange(N, device=DEV))
+    neg_g = PairGraph(src, ndst, torch.arange(N, device=DEV))
+    h1 = h.clone().requires_grad_()
+    loss = pair_margin_loss(pos_g, neg_g, h1, 1.0)
+    loss.backward()
+    assert int(flag) & L.RS_ERRBIT_OOB
+    # restated: the bad endpoint's score reads a zero row (score 0)
+    pos = (h[src.long()] * h[pdst.long()]).sum(1)
+    nd = ndst.long().clamp_max(N - 1)
+    neg = (h[src.long()] * h[nd]).sum(1)
+    neg[3] = 0.0
+    ref = torch.clamp(neg + 1.0 - pos, min=0).mean()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref))
+    assert torch.isfinite(h1.grad).all()
+    flag.zero_()
 
 
 def test_multihot_mean_lookup_matches_gather_mean():
