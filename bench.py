@@ -38,7 +38,7 @@ WATCH = ["rs_dlrm_train_step_fwd_unit",
          "rs_dlrm_interaction_fwd_head_dx",
          "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots",
          "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
-         "rs_embedding_dedup_grad"]
+         "rs_embedding_dedup_grad", "rs_embedding_dedup_grad_mapped", "rs_gather_rows_padded"]
 # the embedding path of SURVEY §8(d) (lookup fwd + bwd + dedup + apply) as the production step
 # launches it: the fused gather + interaction + unit-backward kernel (main stream), the radix
 # sort and the segmented-sum apply (fused optimizer's side stream, co-running with dense GEMMs:
@@ -49,7 +49,8 @@ PATH_KERNELS = ("rs_dlrm_train_step_fwd_unit",
                 "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots", "rs_sort_ids_sharded",
                 "rs_embedding_apply", "rs_embedding_apply_scaled")
 SIDE_STREAM = {"rs_sort_ids_slots", "rs_embedding_apply", "rs_embedding_apply_scaled",
-               "rs_sort_ids_sharded", "rs_embedding_dedup_grad"}
+               "rs_sort_ids_sharded", "rs_embedding_dedup_grad", "rs_embedding_dedup_grad_mapped",
+               "rs_gather_rows_padded"}
 # device symbols behind each C-ABI entry (for the PMC passes)
 # (entry, device-symbol regex of its kernels, the one kernel every call launches once)
 PMC_SYMBOLS = [
@@ -243,12 +244,28 @@ def measured_unique(pool, model):
     return float(np.mean(us))
 
 
-def kernel_bytes(name, B, S, D, id_bytes, U):
+def kernel_bytes(name, B, S, D, id_bytes, U, world=1, cap=0):
     """Algorithmic HBM bytes of one launch. The interaction row is the
-    compact one: F(F-1)/2 pair values + D bottom values (the zero padding is not counted)."""
+    compact one: F(F-1)/2 pair values + D bottom values (the zero padding is not counted).
+    world > 1 (row-sharded slab; B = the per-rank batch, U = its unique rows,
+    cap = the exchange capacity): the owner's sort and apply run over the E = world·cap received
+    slots, of which ≈U hold rows (each rank sends every owner ≈U/world rows); the owner's
+    distinct rows are taken as ≈U too (an upper bound: ranks that share a row send it twice)."""
     F = S + 1
     N = B * S
     Z = F * (F - 1) // 2 + D
+    if world > 1:
+        E = world * cap
+        if name == "rs_sort_ids_sharded":
+            return N * id_bytes + N * 8
+        if name == "rs_embedding_dedup_grad_mapped":  # rank-local sum per unique row into its slot
+            return N * 8 + N * 4 * D + U * 4 * D
+        if name == "rs_sort_ids_slots":  # the owner's masked sort of the received slots
+            return E * (4 + 1) + E * 8
+        if name == "rs_embedding_apply":  # E sorted entries, ≈U rows read, their rows updated
+            return E * 8 + U * 4 * D + U * 2 * 4 * D
+        if name == "rs_gather_rows_padded":  # the owner serves the requested rows
+            return E * 4 + E * 2 * 4 * D
     if name == "rs_dlrm_interaction_fwd":
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z)
     if name == "rs_dlrm_interaction_fwd_head":  # + the fused top-MLP output y[b]
@@ -591,7 +608,8 @@ def main():
     for name, (ms, cnt) in tot.items():
         if cnt:
             avg = ms / cnt
-            by = kernel_bytes(name, args.batch, S, D, 8, U)
+            by = kernel_bytes(name, args.batch, S, D, 8, U, world,
+                              getattr(model.embedding_layer, "capacity", 0) or 0)
             kern[name] = {"avg_us": round(avg * 1e3, 2), "calls": cnt,
                           "algorithmic_bytes": int(by),
                           "achieved_GBs": round(by / (avg * 1e-3) / 1e9, 1),

@@ -50,6 +50,16 @@ def main():
                     help="deepfm_file: rows of the Criteo-shaped TFRecord file written and trained on")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lazy_adam", "keras_adam"],
                     help="dlrm_cfg2 only (the reference DLRM SGD path or Keras / lazy Adam)")
+    ap.add_argument("--cfg4-optimizer", default="keras_adam_deferred",
+                    choices=["keras_adam_deferred", "keras_adam", "lazy_adam"],
+                    help="esmm / mmoe: the reference's Keras Adam (esmm/train.py:125) with each "
+                         "row's dense decay replayed when next read (default; its materialize() "
+                         "is timed and amortised into the value), the same with the per-step "
+                         "dense sweep, or lazy Adam (touched rows only; also reported as the "
+                         "secondary key of the default run)")
+    ap.add_argument("--cpu-baseline", type=int, default=1,
+                    help="1: time the oracle's host step (the reference's CPU path restated) "
+                         "beside the GPU step and report it under cpu_baseline")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0)
@@ -127,13 +137,15 @@ def main():
         B = args.batch or 65536
         vocab = scaled_vocab(FEAT_VOCAB, args.rows)
         m = build(args.model.upper(), vocab, 18, dev)
-        step = MultiTaskStep(m, "lazy_adam")
+        cfg4_train = step = MultiTaskStep(m, args.cfg4_optimizer)
         batches = []
         for _ in range(4):
             f, lab = aliccp_batch(rng, B, vocab)
             batches.append(({k: torch.from_numpy(v).to(dev) for k, v in f.items()}, torch.from_numpy(lab).to(dev)))
-        watch = ["rs_embedding_fwd", "rs_sort_ids", "rs_embedding_apply"]
-        cfg = {"workload": f"{args.model}_aliccp_18x{args.rows}x18", "batch": B, "optimizer": "lazy_adam"}
+        watch = ["rs_embedding_fwd", "rs_sort_ids_slots", "rs_embedding_apply",
+                 "rs_embedding_apply_scaled", "rs_keras_adam_catchup", "rs_keras_adam_dense_sweep"]
+        cfg = {"workload": f"{args.model}_aliccp_18x{args.rows}x18", "batch": B,
+               "optimizer": args.cfg4_optimizer}
     elif args.model == "pinsage":
         from recommender_amd.pinsage import PinSageModel, PinSageSampler
         from recommender_amd.pinsage.sampler import item_pairs
@@ -278,10 +290,46 @@ def main():
     sec, k = run(step, batches, args.steps, args.warmup, watch)
     if args.model == "dlrm_cfg2" and args.cfg2_graph == 2 and args.optimizer == "sgd":
         sec /= B_pool  # one replay = the whole pool of steps
+    extra = {}
+    if args.model in ("esmm", "mmoe") and args.cfg4_optimizer == "keras_adam_deferred":
+        # the replayed decay of every row not touched since the start: materialize() brings the
+        # slab to the dense sweep's state; its time is amortised over every step run so far
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cfg4_train.materialize()
+        torch.cuda.synchronize()
+        mat = time.perf_counter() - t0
+        extra["steps_only_ms_per_step"] = round(sec * 1e3, 3)
+        extra["materialize_ms"] = round(mat * 1e3, 2)
+        extra["materialize_amortised_over_steps"] = args.steps + args.warmup
+        sec = sec + mat / (args.steps + args.warmup)
+        # lazy Adam (touched rows only, not the reference's update rule) as the secondary key
+        del cfg4_train, step
+        m = None
+        torch.cuda.empty_cache()
+        from recommender_amd.esmm.train import MultiTaskStep, build
+
+        m2 = build(args.model.upper(), vocab, 18, dev)
+        lz = MultiTaskStep(m2, "lazy_adam")
+        sec_l, _ = run(lz, batches, args.steps, args.warmup, [])
+        extra["lazy_adam"] = {"examples_per_sec": round(B / sec_l, 1),
+                              "ms_per_step": round(sec_l * 1e3, 3),
+                              "note": "touched rows only: not the reference's Keras Adam"}
+        del lz, m2
     out = {"model": args.model, "examples_per_sec": round(B / sec, 1),
-           "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k}
-    if args.model == "deepfm":
-        out["cpu_baseline"] = deepfm_cpu_baseline(B)
+           "ms_per_step": round(sec * 1e3, 3), "config": cfg, "kernels_us": k, **extra}
+    if args.cpu_baseline:
+        fns = {"deepfm": lambda: deepfm_cpu_baseline(B),
+               "dlrm_cfg2": cfg2_cpu_baseline,
+               "dien": dien_cpu_baseline,
+               "esmm": lambda: esmm_cpu_baseline("esmm", args.rows),
+               "mmoe": lambda: esmm_cpu_baseline("mmoe", args.rows),
+               "pinsage": pinsage_cpu_baseline,
+               "eges": eges_cpu_baseline}
+        try:
+            out["cpu_baseline"] = fns[args.model]()
+        except Exception as e:  # reported, not fatal: the GPU line stands on its own
+            out["cpu_baseline"] = {"error": repr(e)[:300]}
     if args.model == "dlrm_cfg2":
         # SURVEY 8(d)'s path bytes per step at the measured unique-row count (fwd S(id + 8D) +
         # bwd S(id + 4D) + (U/B)·8D per example) over the WHOLE step time (dense half included:
@@ -390,6 +438,228 @@ def deepfm_from_file(args):
            "cpu_baseline": deepfm_cpu_baseline(B)}
     os.remove(path)
     print(json.dumps(out))
+
+
+def _host_threads():
+    cores = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(cores, omp) if omp > 0 else cores
+
+
+def _time_host(fn, n_warm, n_meas):
+    """Median seconds of fn() over n_meas calls after n_warm, with the host's thread share (the
+    box's OMP_NUM_THREADS for one GPU) given to torch and the BLAS pools; returns (s, threads)."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    threads = _host_threads()
+    old = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    times = []
+    try:
+        with threadpool_limits(threads):
+            used = max([i.get("num_threads", 1) for i in threadpool_info()] + [threads])
+            for i in range(n_warm + n_meas):
+                t0 = time.perf_counter()
+                fn(i)
+                if i >= n_warm:
+                    times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(old)
+    return float(np.median(times)), int(used)
+
+
+def _baseline(B, sec, used, sample):
+    return {"value": round(B / sec, 1), "unit": "examples/sec", "cores": used, "kind": "port",
+            "sample": f"{sample}; median {sec * 1e3:.1f} ms/step"}
+
+
+def cfg2_cpu_baseline(B=1024, rows_per_slot=100_000, n_warm=2, n_meas=5):
+    """cfg2 on the host: oracle/ctr.py dlrm_sgd_step (NumPy fp32: gather, interaction, the
+    [512, 256, 64] / [512, 256, 1] MLPs, BCE, backward, tiled dedup + SGD) at D 64, batch B,
+    26 slots of rows_per_slot rows (a row's work does not depend on the table size)."""
+    from oracle.ctr import DLRMState, dlrm_sgd_step
+    from recommender_amd.synthetic import criteo_batch
+
+    S, D = 26, 64
+    rng = np.random.default_rng(4)
+    cards = [rows_per_slot] * S
+    so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+    table = rng.uniform(-0.05, 0.05, (int(so[-1]), D)).astype(np.float32)
+
+    def mlp(fin, units):
+        out = []
+        for u in units:
+            lim = np.sqrt(6.0 / (fin + u))
+            out.append((rng.uniform(-lim, lim, (fin, u)).astype(np.float32), np.zeros(u, np.float32)))
+            fin = u
+        return out
+
+    F = S + 1
+    st = DLRMState(table, so, mlp(13, [512, 256, D]), mlp(F * F + D, [512, 256, 1]))
+    pool = [criteo_batch(rng, B, cards) for _ in range(3)]
+
+    def one(i):
+        cat, dn, lb = pool[i % 3]
+        dlrm_sgd_step(st, cat, dn, lb, 0.01)
+
+    sec, used = _time_host(one, n_warm, n_meas)
+    return _baseline(B, sec, used, f"oracle/ctr.py dlrm_sgd_step, D 64, batch {B}, 26 x "
+                                   f"{rows_per_slot} rows, {n_warm} warm-up + {n_meas}")
+
+
+def dien_cpu_baseline(B=64, n_warm=1, n_meas=3):
+    """cfg3 on the host: oracle/dien.py dien_step (torch fp32 autograd on the CPU: GRU, aux
+    loss, attention, AUGRU, head MLP — the reference's dien/train.py:14-22 forward + tape) plus
+    the Keras Adam update of every dense parameter and of both tables (dense, as Keras does),
+    on a CPU-built DIEN of the cfg3 shape, L 100."""
+    from oracle.dien import dien_step
+    from oracle.models import keras_adam_torch
+    from oracle.embedding import keras_adam_coefficients
+    from recommender_amd.dien import DIEN
+    from recommender_amd.dien.train import synthetic_batch
+
+    m = DIEN(36, 36, item_vocab_size=63001, item_embedding_size=18, cat_vocab_size=801,
+             cat_embedding_size=18, mlp_units=[200, 80, 1], device="cpu")
+    rng = np.random.default_rng(4)
+    pool = []
+    for _ in range(2):
+        f, lab = synthetic_batch(rng, B, 100, 63001, 801)
+        pool.append(({k: torch.from_numpy(v) for k, v in f.items()}, torch.from_numpy(lab)))
+    state = {}
+
+    def one(i):
+        feats, lab = pool[i % 2]
+        r = dien_step(m, feats, lab, dtype=torch.float32)
+        c = {k: float(v) for k, v in keras_adam_coefficients(i + 1).items()}
+        named = dict(m.named_parameters())
+        with torch.no_grad():
+            for n, g in r["grads"].items():
+                p = named[n]
+                mm, vv = state.get(n, (torch.zeros_like(p), torch.zeros_like(p)))
+                w2, mm, vv = keras_adam_torch(p, mm, vv, g, c)
+                p.copy_(w2)
+                state[n] = (mm, vv)
+            for t in (m.item_embedding, m.cat_embedding):  # Keras Adam on the whole table
+                w = t.weight
+                mm, vv = state.get(id(t), (torch.zeros_like(w), torch.zeros_like(w)))
+                w2, mm, vv = keras_adam_torch(w, mm, vv, torch.zeros_like(w), c)
+                w.copy_(w2)
+                state[id(t)] = (mm, vv)
+
+    sec, used = _time_host(one, n_warm, n_meas)
+    return _baseline(B, sec, used, f"oracle/dien.py dien_step (torch fp32 autograd, CPU) + Keras "
+                                   f"Adam of the dense parameters and both tables, batch {B}, "
+                                   f"L 100, {n_warm} warm-up + {n_meas}")
+
+
+def esmm_cpu_baseline(kind, rows, B=2048, n_warm=1, n_meas=3):
+    """cfg4 on the host: oracle/models.py esmm_family_step (torch fp32 autograd on the CPU) of a
+    CPU-built ESMM / MMOE over the same 18-table slab (`rows` rows, D 18), then the reference
+    optimizer (esmm/train.py:125, Keras Adam): the dense parameters, and the slab's tiled dedup
+    (oracle segment_sum_tiled) + Keras Adam over every row (m, v decayed densely)."""
+    from oracle import embedding as OE
+    from oracle.models import esmm_family_step, keras_adam_torch
+    from recommender_amd.esmm import FEAT_VOCAB
+    from recommender_amd.esmm.train import build
+    from recommender_amd.synthetic import aliccp_batch, scaled_vocab
+
+    vocab = scaled_vocab(FEAT_VOCAB, rows)
+    m = build(kind.upper(), vocab, 18, "cpu")
+    slab = m.embedding_layer.slab
+    rng = np.random.default_rng(4)
+    pool = []
+    for _ in range(2):
+        f, lab = aliccp_batch(rng, B, vocab)
+        pool.append(({k: torch.from_numpy(v) for k, v in f.items()}, torch.from_numpy(lab)))
+    so = slab.slot_offsets.numpy()
+    table = slab.weight.numpy()
+    mt, vt = np.zeros_like(table), np.zeros_like(table)
+    dense = [p for n, p in m.named_parameters() if not n.endswith("grad_handle")]
+    dstate = [(torch.zeros_like(p), torch.zeros_like(p)) for p in dense]
+
+    def one(i):
+        nonlocal table, mt, vt
+        feats, lab = pool[i % 2]
+        loss, y, dg, rows_g = esmm_family_step(m, slab.weight, slab.slot_offsets, feats, lab)
+        co = OE.keras_adam_coefficients(i + 1)
+        c = {k: float(v) for k, v in co.items()}
+        with torch.no_grad():
+            for j, (p, g) in enumerate(zip(dense, dg)):
+                w2, mm, vv = keras_adam_torch(p, dstate[j][0], dstate[j][1], g, c)
+                p.copy_(w2)
+                dstate[j] = (mm, vv)
+        ids = np.stack([feats[k].reshape(-1).numpy() for k in feats], 1)
+        sr, sp, _ = OE.sort_ids(ids, table.shape[0], so)
+        ur, ug = OE.segment_sum_tiled(sr, sp, rows_g.numpy(), table.shape[0])
+        t2, mt, vt = OE.apply_keras_adam(table, mt, vt, ur.astype(np.int64), ug, co)
+        table[...] = t2
+
+    sec, used = _time_host(one, n_warm, n_meas)
+    return _baseline(B, sec, used, f"oracle/models.py esmm_family_step (torch fp32 autograd, "
+                                   f"CPU) + Keras Adam (dense parameters; slab: tiled dedup + "
+                                   f"dense m / v sweep over all {table.shape[0]} rows), "
+                                   f"{kind.upper()}, batch {B}, {n_warm} warm-up + {n_meas}")
+
+
+def pinsage_cpu_baseline(B=256, n_warm=1, n_meas=3):
+    """cfg5 on the host: the sampling of oracle/pinsage.py (item pairs, metapath walks, visit
+    counts, top-k, to_block; NumPy) and oracle/pinsage.py torch_train_step (torch fp32 autograd,
+    CPU) on a CPU-built PinSageModel over the same ML-20M-shaped graph, batch B pairs."""
+    from oracle import pinsage as OP
+    from recommender_amd.pinsage import PinSageModel
+    from recommender_amd.pinsage.train import ML20M, build_graph
+
+    g = build_graph(ML20M, 4, device="cpu")
+    m = PinSageModel(g, g.itype, 2, 8, 32, 16, device="cpu")
+    og = OP.BipartiteGraph(g.i2u_indptr.numpy(), g.i2u.numpy(), g.u2i_indptr.numpy(),
+                           g.u2i.numpy())
+    year = m.feature_projector.year.numpy()
+    genre = m.feature_projector.genre.numpy()
+
+    def one(i):
+        heads, pos, neg = OP.item_pairs(og, i * B, B, 4, i)
+        seeds, pe, ne, blocks = OP.sample_from_item_pairs(og, heads, pos, neg, 2, 4, 2, 0.0, 3, 4, i)
+        OP.torch_train_step(m, blocks, pe, ne, year, genre)
+
+    sec, used = _time_host(one, n_warm, n_meas)
+    return {"value": round(B / sec, 1), "unit": "pairs/sec", "cores": used, "kind": "port",
+            "sample": f"oracle/pinsage.py sampling (NumPy) + torch_train_step (torch fp32 autograd, "
+                      f"CPU), batch {B} pairs, {n_warm} warm-up + {n_meas}; median "
+                      f"{sec * 1e3:.1f} ms/step"}
+
+
+def eges_cpu_baseline(B=1024, n_warm=2, n_meas=5):
+    """EGES on the host: oracle/models.py eges_step (torch fp32 autograd, CPU) of a CPU-built
+    EGES (63 001 items, D 160, 5 negatives) plus Keras Adam of its tables (dense, as Keras)."""
+    from oracle.models import eges_step, keras_adam_torch
+    from oracle.embedding import keras_adam_coefficients
+    from recommender_amd.eges.train import build, synthetic_batch
+
+    m = build("EGES", 63001, 801, 3000, 160, device="cpu")
+    rng = np.random.default_rng(4)
+    pool = []
+    for _ in range(2):
+        *inp, lab = synthetic_batch(rng, B, 63001, 801, 3000)
+        pool.append((tuple(torch.from_numpy(a) for a in inp), torch.from_numpy(lab)))
+    state = {}
+
+    def one(i):
+        inp, lab = pool[i % 2]
+        loss, logits, out = eges_step(m, inp, lab)
+        c = {k: float(v) for k, v in keras_adam_coefficients(i + 1).items()}
+        with torch.no_grad():
+            for name, (ids, rows) in out.items():
+                w = getattr(m, name).weight
+                g = torch.zeros_like(w).index_add_(0, ids, rows)
+                mm, vv = state.get(name, (torch.zeros_like(w), torch.zeros_like(w)))
+                w2, mm, vv = keras_adam_torch(w, mm, vv, g, c)
+                w.copy_(w2)
+                state[name] = (mm, vv)
+
+    sec, used = _time_host(one, n_warm, n_meas)
+    return _baseline(B, sec, used, f"oracle/models.py eges_step (torch fp32 autograd, CPU) + "
+                                   f"Keras Adam of every table, batch {B}, {n_warm} warm-up + "
+                                   f"{n_meas}")
 
 
 def deepfm_cpu_baseline(B, n_warm=5, n_meas=20):

@@ -159,6 +159,20 @@ int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_unique,
                          int32_t* overflow, void* stream);
 /* The owner's side of the exchange: out[i] = shard[ids[i]], a zero row where ids[i] < 0
  * (padding) or out of range; no error flag (padding is expected). */
+/* The spill round of the capacity-bounded exchange (a batch with more unique rows for some owner
+ * than the capacity): rs_exchange_excess writes max_o max(0, owner_counts[o] - capacity) (int64,
+ * device) — all-reduced (MAX) over the ranks it is the spill capacity C2; rs_exchange_pack_spill
+ * then gives unique u of owner o with j = u - (first unique of o) >= capacity the slot
+ * world·capacity + o·C2 + (j - capacity), its owner-local row to spill_ids[o·C2 + j - capacity]
+ * (−1 = padding), and rewrites inverse_slot from slot_of_unique (rows within the capacity keep
+ * the slots rs_exchange_pack gave them). *overflow is set only if C2 is below this rank's excess. */
+int32_t rs_exchange_excess(const int32_t* owner_counts, int32_t world, int64_t capacity,
+                           int64_t* excess, void* stream);
+int32_t rs_exchange_pack_spill(const uint32_t* uniq_keys, const int32_t* n_unique,
+                               const int32_t* owner_counts, int32_t world, int64_t shard_stride,
+                               int64_t capacity, int64_t spill_capacity, const int32_t* inverse,
+                               int64_t n_ids, int32_t* spill_ids, int32_t* slot_of_unique,
+                               int32_t* inverse_slot, int32_t* overflow, void* stream);
 int32_t rs_gather_rows_padded(const float* shard, int64_t n_rows, int32_t dim, const int32_t* ids,
                               int64_t n, float* out, void* stream);
 

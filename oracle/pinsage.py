@@ -359,3 +359,50 @@ def split_by_time(users, ts):
         tr.extend(e[: e.size - min(e.size - 1, 2)] if e.size > 1 else e)
     return np.sort(np.asarray(tr, np.int64)), np.sort(np.asarray(va, np.int64)), \
         np.sort(np.asarray(te, np.int64))
+
+
+# ---- one train step on the host (torch fp32 autograd; the CPU baseline of cfg5) ------------
+def torch_train_step(model_cpu, blocks, pos_edges, neg_edges, year, genre, delta=1.0):
+    """pinsage/train/train.py:17-20,40-48 on the CPU: get_repr (FeatureProjector → Convolve x L →
+    fc_1 / fc_2, layers.py / model.py) from a CPU-built PinSageModel's parameters and the numpy
+    blocks of sample_from_item_pairs, u_dot_v scores, margin loss, and the gradients of every
+    dense parameter and table (torch autograd; index_add aggregation). Used only to time the
+    reference's CPU path beside the GPU step (benchmarks/bench_models.py). Returns (loss, grads)."""
+    import torch
+
+    fp = model_cpu.feature_projector
+    leaves = []
+
+    def leaf(t):
+        x = t.detach().clone().requires_grad_(True)
+        leaves.append(x)
+        return x
+
+    ids = torch.from_numpy(np.asarray(blocks[0].src_nodes, np.int64))
+    ye = leaf(fp.year_embedding.weight)[torch.from_numpy(np.asarray(year, np.int64))[ids]]
+    ge = leaf(fp.genre_embedding.weight)[torch.from_numpy(np.asarray(genre, np.int64))[ids]].mean(1)
+    ie = leaf(fp.id_embedding.weight)[ids]
+    h = torch.cat([ye, ge, ie], -1)
+    for conv, b in zip(model_cpu.sagenet.convolves, blocks):
+        h_dst = h[: b.n_dst]
+        u = torch.relu(h @ leaf(conv.fc_1.kernel) + leaf(conv.fc_1.bias))
+        src = torch.from_numpy(np.asarray(b.edge_src, np.int64))
+        dst = torch.from_numpy(np.asarray(b.edge_dst, np.int64))
+        w = torch.from_numpy(np.asarray(b.edge_w, np.float32))
+        vs = torch.zeros(b.n_dst, u.shape[1]).index_add(0, dst, u[src] * w[:, None])
+        ws = torch.zeros(b.n_dst).index_add(0, dst, w)
+        nv = vs / torch.clamp(ws, min=1)[:, None]
+        new = torch.relu(torch.cat([nv, h_dst], -1) @ leaf(conv.fc_2.kernel) + leaf(conv.fc_2.bias))
+        h = new / torch.norm(new)
+    s = model_cpu.sagenet
+    h = torch.relu(h @ leaf(s.fc_1.kernel) + leaf(s.fc_1.bias))
+    h = h @ leaf(s.fc_2.kernel) + leaf(s.fc_2.bias)
+
+    def score(edges):
+        a = torch.from_numpy(np.asarray(edges[0], np.int64))
+        c = torch.from_numpy(np.asarray(edges[1], np.int64))
+        return (h[a] * h[c]).sum(-1)
+
+    loss = torch.clamp(score(neg_edges) + delta - score(pos_edges), min=0).mean()
+    grads = torch.autograd.grad(loss, leaves)
+    return float(loss.detach()), grads

@@ -6,9 +6,11 @@
 // sizes: no host sync on the counts, and the whole step can be stream-ordered and graph-captured.
 // A rank's unique rows (owner-major sorted keys, rs_unique_inverse) are dealt to the slots in
 // key order: unique u of owner o goes to slot o·C + (u − first unique of o). Slots left over are
-// padding (id −1: the owner gathers a zero row and its apply leaves the slot out). A rank with
-// more than C unique rows for one owner sets `overflow` (the rows past C are not exchanged; the
-// host raises before trusting the step: recommender_amd/sharded.py).
+// padding (id −1: the owner gathers a zero row and its apply leaves the slot out). Rows past C
+// (a batch with more unique rows for one owner than the capacity) take a spill round: every rank
+// learns the all-reduced largest excess C2 (rs_exchange_excess), and the excess rows go in a
+// second pair of equal-split all-to-alls of [world, C2] blocks (rs_exchange_pack_spill) — slots
+// world·C + o·C2 + j, after the capacity block (recommender_amd/sharded.py).
 #include "common.hpp"
 
 namespace rs {
@@ -66,6 +68,47 @@ __global__ __launch_bounds__(256) void exchange_inverse_kernel(const int32_t* __
   }
 }
 
+// the rows past the capacity: unique u of owner o with j = u - ostart[o] >= cap goes to spill
+// slot world·cap + o·cap2 + (j - cap) (cap2 >= every rank's largest excess: the all-reduced
+// maximum), its local row to spill_ids[o·cap2 + j - cap]
+__global__ __launch_bounds__(256) void exchange_spill_slots_kernel(
+    const uint32_t* __restrict__ uniq, const int32_t* __restrict__ n_unique,
+    const int32_t* __restrict__ counts, int world, int64_t stride, int64_t cap, int64_t cap2,
+    int64_t n_max, int32_t* __restrict__ spill_ids, int32_t* __restrict__ slot_of,
+    int32_t* __restrict__ overflow) {
+  __shared__ int32_t ostart[kMaxWorld];
+  owner_starts(counts, world, ostart);
+  const int64_t U = *n_unique;
+  bool over = false;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_max;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    if (u >= U) break;
+    const int64_t key = uniq[u];
+    const int o = (int)(key / stride);
+    const int64_t j = u - ostart[o] - cap;
+    if (j < 0) continue;
+    if (j < cap2) {
+      spill_ids[(int64_t)o * cap2 + j] = (int32_t)(key - (int64_t)o * stride);
+      slot_of[u] = (int32_t)((int64_t)world * cap + (int64_t)o * cap2 + j);
+    } else {
+      over = true;  // cap2 smaller than the excess: the caller passed a wrong cap2
+    }
+  }
+  if (__any(over) && (threadIdx.x & 63) == 0 && overflow) atomicOr(overflow, 1);
+}
+
+// the largest excess over the capacity among this rank's owners: max(0, counts[o] - cap)
+__global__ void exchange_excess_kernel(const int32_t* __restrict__ counts, int world, int64_t cap,
+                                       int64_t* __restrict__ excess) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t m = 0;
+  for (int o = 0; o < world; ++o) {
+    const int64_t e = (int64_t)counts[o] - cap;
+    m = e > m ? e : m;
+  }
+  *excess = m;
+}
+
 // the owner's side: out[i] = shard[ids[i]] for ids in range, a zero row for padding (ids < 0).
 // A half-wave (32 lanes x float4) per row at D = 128; rows of other widths by float lanes.
 __global__ __launch_bounds__(256) void gather_padded_kernel(const float* __restrict__ shard,
@@ -113,6 +156,41 @@ extern "C" int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_
   exchange_slots_kernel<<<blocks, 256, 0, st>>>(uniq_keys, n_unique, owner_counts, world,
                                                 shard_stride, capacity, n_ids, send_ids,
                                                 slot_of_unique, overflow);
+  RS_CHECK_LAUNCH();
+  exchange_inverse_kernel<<<blocks, 256, 0, st>>>(inverse, slot_of_unique, n_ids, inverse_slot);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_exchange_excess(const int32_t* owner_counts, int32_t world, int64_t capacity,
+                                      int64_t* excess, void* stream) {
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity > 0, "bad sizes");
+  RS_CHECK_ARG(owner_counts && excess, "null pointer");
+  exchange_excess_kernel<<<1, 64, 0, as_stream(stream)>>>(owner_counts, world, capacity, excess);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_exchange_pack_spill(const uint32_t* uniq_keys, const int32_t* n_unique,
+                                          const int32_t* owner_counts, int32_t world,
+                                          int64_t shard_stride, int64_t capacity,
+                                          int64_t spill_capacity, const int32_t* inverse,
+                                          int64_t n_ids, int32_t* spill_ids,
+                                          int32_t* slot_of_unique, int32_t* inverse_slot,
+                                          int32_t* overflow, void* stream) {
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld, "world out of range");
+  RS_CHECK_ARG(shard_stride > 0 && capacity > 0 && spill_capacity > 0 && n_ids >= 0, "bad sizes");
+  RS_CHECK_ARG((int64_t)world * (capacity + spill_capacity) < (int64_t(1) << 31),
+               "world x capacity out of range");
+  RS_CHECK_ARG(spill_ids && n_unique && owner_counts, "null pointer");
+  hipStream_t st = as_stream(stream);
+  RS_CHECK_HIP(hipMemsetAsync(spill_ids, 0xFF, (size_t)world * spill_capacity * sizeof(int32_t), st));
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(uniq_keys && inverse && slot_of_unique && inverse_slot, "null pointer");
+  const int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 2048);
+  exchange_spill_slots_kernel<<<blocks, 256, 0, st>>>(uniq_keys, n_unique, owner_counts, world,
+                                                      shard_stride, capacity, spill_capacity, n_ids,
+                                                      spill_ids, slot_of_unique, overflow);
   RS_CHECK_LAUNCH();
   exchange_inverse_kernel<<<blocks, 256, 0, st>>>(inverse, slot_of_unique, n_ids, inverse_slot);
   RS_CHECK_LAUNCH();

@@ -703,6 +703,7 @@ struct SegArgs {
   int32_t* vcnt;                // [n_slots][tiles] valid ids per tile (pass-0 tiles)
   int32_t* scnt;                // [n_slots][tiles] sentinels per tile
   uint2* tmp;                   // [n] (id, position) after pass 0 of a two-pass slot
+  uint32_t* keys0;              // [n_slots][tiles][4096] pass-0 keys in tile order (bit 31: sentinel)
   uint32_t* rows_out;
   int32_t* pos_out;
   int32_t* err_flag;
@@ -807,8 +808,14 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
   }
   if (lane == 0 && ns) atomicAdd(&nsent, ns);
   if (__any(oob) && lane == 0) flag_oob(a.err_flag);
-  __syncthreads();
   const int64_t tile = (int64_t)s * a.tiles + t;
+  {  // the keys in tile order for the scatter (contiguous; the ids were strided by n_slots)
+    const int wave = threadIdx.x >> 6;
+    uint32_t* kt = a.keys0 + tile * kSegTile + wave * 64 * kSegKPL + lane;
+#pragma unroll
+    for (int k = 0; k < kSegKPL; ++k) kt[k * 64] = ((sent >> k) & 1u) ? 0x80000000u : id[k];
+  }
+  __syncthreads();
   seg_store_hist(a.hist0 + tile * kSegBins, cnt, bins);
   if (threadIdx.x == 0) {
     const int64_t b0 = (int64_t)t * kSegTile;
@@ -818,27 +825,46 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
   }
 }
 
-// slot starts: vstart[s] = valid ids of slots < s, sstart[s] = sentinels of slots < s, plus the
-// totals; from the pass-0 tile counts (n_slots x tiles ints, L2)
-__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstart, int32_t* sstart) {
-  if (threadIdx.x < a.n_slots) {
-    int32_t v = 0, z = 0;
-    for (int t = 0; t < a.tiles; ++t) {
-      v += a.vcnt[threadIdx.x * a.tiles + t];
-      z += a.scnt[threadIdx.x * a.tiles + t];
-    }
-    vstart[threadIdx.x] = v;
-    sstart[threadIdx.x] = z;
+// slot starts: vstart[s] = valid ids of slots < s, sstart[s] = sentinels of slots < s (index
+// n_slots: the totals), and *spre = sentinels of slot s0's tiles before t0; from the pass-0 tile
+// counts (n_slots x tiles ints in L2 / MALL), every count loaded by its own lane in one round
+// trip, summed per slot in LDS, the slot prefix by one wave's scan
+__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int s0, int t0, int32_t* vstart,
+                                                int32_t* sstart, int32_t* spre) {
+  if (threadIdx.x <= a.n_slots) {
+    vstart[threadIdx.x] = 0;
+    sstart[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) *spre = 0;
+  __syncthreads();
+  const int total = a.n_slots * a.tiles;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int sl = e / a.tiles, tt = e - sl * a.tiles;
+    const int32_t v = a.vcnt[e], z = a.scnt[e];
+    if (v) atomicAdd(&vstart[sl], v);
+    if (z) atomicAdd(&sstart[sl], z);
+    if (z && sl == s0 && tt < t0) atomicAdd(spre, z);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t rv = 0, rz = 0;
-    for (int q = 0; q <= a.n_slots; ++q) {
-      const int32_t v = q < a.n_slots ? vstart[q] : 0, z = q < a.n_slots ? sstart[q] : 0;
-      vstart[q] = rv;
-      sstart[q] = rz;
-      rv += v;
-      rz += z;
+  if (threadIdx.x < 64) {  // exclusive scan over the slots (n_slots <= 64), totals at n_slots
+    const int lane = threadIdx.x;
+    const int32_t v = lane < a.n_slots ? vstart[lane] : 0, z = lane < a.n_slots ? sstart[lane] : 0;
+    int32_t xv = v, xz = z;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t yv = __shfl_up(xv, off), yz = __shfl_up(xz, off);
+      if (lane >= off) {
+        xv += yv;
+        xz += yz;
+      }
+    }
+    if (lane < a.n_slots) {
+      vstart[lane] = xv - v;
+      sstart[lane] = xz - z;
+    }
+    if (lane == 63) {
+      vstart[a.n_slots] = xv;
+      sstart[a.n_slots] = xz;
     }
   }
   __syncthreads();
@@ -854,26 +880,44 @@ __device__ __forceinline__ void seg_digit_offsets(const uint16_t* __restrict__ h
   int32_t tot[PER], pre[PER];
 #pragma unroll
   for (int c = 0; c < PER; ++c) tot[c] = pre[c] = 0;
-  if (d0 < bins) {
-    for (int tt = 0; tt < n_tiles; ++tt) {
-      const uint16_t* h = hist + (int64_t)tt * kSegBins + d0;
-      uint16_t v[PER];
-      if (bins >= PER) {
-        const uint4 x0 = reinterpret_cast<const uint4*>(h)[0], x1 = reinterpret_cast<const uint4*>(h)[1];
-        const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  if (d0 < bins && bins >= PER) {
+    // eight tiles' 32-byte slices in flight at a time (one round trip per eight tiles, not one
+    // per tile: the slot's histograms come from L2 / MALL)
+    constexpr int TB = 8;
+    for (int tt0 = 0; tt0 < n_tiles; tt0 += TB) {
+      uint4 x[TB][2];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          v[2 * c] = (uint16_t)(w[c] & 0xFFFFu);
-          v[2 * c + 1] = (uint16_t)(w[c] >> 16);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < PER; ++c) v[c] = d0 + c < bins ? h[c] : 0;
+      for (int j = 0; j < TB; ++j) {
+        const uint4* h = reinterpret_cast<const uint4*>(hist + (int64_t)(tt0 + j) * kSegBins + d0);
+        const bool in = tt0 + j < n_tiles;
+        x[j][0] = in ? h[0] : make_uint4(0u, 0u, 0u, 0u);
+        x[j][1] = in ? h[1] : make_uint4(0u, 0u, 0u, 0u);
       }
 #pragma unroll
+      for (int j = 0; j < TB; ++j) {
+        const uint32_t w[8] = {x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w,
+                               x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w};
+        const bool before = tt0 + j < t;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int32_t lo = (int32_t)(w[c] & 0xFFFFu), hi = (int32_t)(w[c] >> 16);
+          tot[2 * c] += lo;
+          tot[2 * c + 1] += hi;
+          if (before) {
+            pre[2 * c] += lo;
+            pre[2 * c + 1] += hi;
+          }
+        }
+      }
+    }
+  } else if (d0 < bins) {  // fewer than 16 bins (a slot of <= 8 rows): thread 0 alone
+    for (int tt = 0; tt < n_tiles; ++tt) {
+      const uint16_t* h = hist + (int64_t)tt * kSegBins + d0;
+#pragma unroll
       for (int c = 0; c < PER; ++c) {
-        tot[c] += v[c];
-        if (tt < t) pre[c] += v[c];
+        const int32_t v = d0 + c < bins ? h[c] : 0;
+        tot[c] += v;
+        if (tt < t) pre[c] += v;
       }
     }
   }
@@ -944,15 +988,28 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   const int bins = 1 << sl.w0;
-  seg_slot_starts(a, vstart, sstart);
+  uint32_t id[kSegKPL], live = 0u, sent = 0u;
+  {  // the histogram pass's keys (bit 31: sentinel), past the tile's end neither — issued first,
+     // so they arrive while the slot starts and digit offsets are formed
+    const int64_t b0 = (int64_t)t * kSegTile;
+    const int tn = (int)(a.B - b0 < kSegTile ? a.B - b0 : kSegTile);
+    const int w0 = (threadIdx.x >> 6) * 64 * kSegKPL + (threadIdx.x & 63);
+    const uint32_t* kt = a.keys0 + ((int64_t)s * a.tiles + t) * kSegTile + w0;
+#pragma unroll
+    for (int k = 0; k < kSegKPL; ++k) {
+      const bool in = w0 + k * 64 < tn;
+      const uint32_t v = in ? kt[k * 64] : 0u;
+      id[k] = v & 0x7FFFFFFFu;
+      if (in && (v >> 31)) sent |= 1u << k;
+      else if (in) live |= 1u << k;
+    }
+  }
+  __shared__ int32_t spre;
+  seg_slot_starts(a, s, t, vstart, sstart, &spre);
   const int32_t n_valid = vstart[a.n_slots];
-  int32_t sent_pre = 0;  // sentinels of this slot's earlier tiles
-  for (int tt = 0; tt < t; ++tt) sent_pre += a.scnt[s * a.tiles + tt];
+  const int32_t sent_pre = spre;  // sentinels of this slot's earlier tiles
   seg_digit_offsets(a.hist0 + (int64_t)s * a.tiles * kSegBins, a.tiles, t, bins, vstart[s], doff,
                     wsum);
-  uint32_t id[kSegKPL], live, sent;
-  bool oob = false;  // flagged by the histogram pass
-  seg_load0<ID64>(a, sl, s, t, id, live, sent, oob);
   uint32_t dig[kSegKPL];
   const uint32_t mask = (uint32_t)bins - 1u;
 #pragma unroll
@@ -1024,7 +1081,8 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a)
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   if (sl.w1 == 0) return;
-  seg_slot_starts(a, vstart, sstart);
+  __shared__ int32_t spre;
+  seg_slot_starts(a, s, t, vstart, sstart, &spre);
   const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
   const int bins = 1 << sl.w1;
   for (int d = threadIdx.x; d < bins; d += blockDim.x) cnt[d] = 0;
@@ -1054,7 +1112,8 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   if (sl.w1 == 0) return;
-  seg_slot_starts(a, vstart, sstart);
+  __shared__ int32_t spre;
+  seg_slot_starts(a, s, t, vstart, sstart, &spre);
   const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
   const int n_tiles_s = (n_s + kSegTile - 1) / kSegTile;
   if (t >= n_tiles_s) return;  // uniform per block: after the block-wide syncs above
@@ -1081,12 +1140,14 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
 }
 
 static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArgs* a) {
+  uint32_t* k0 = c.take<uint32_t>((size_t)n_slots * tiles * kSegTile);
   uint16_t* h0 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
   uint16_t* h1 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
   int32_t* v = c.take<int32_t>((size_t)n_slots * tiles);
   int32_t* z = c.take<int32_t>((size_t)n_slots * tiles);
   uint2* tmp = c.take<uint2>(n);
   if (a) {
+    a->keys0 = k0;
     a->hist0 = h0;
     a->hist1 = h1;
     a->vcnt = v;
@@ -1109,6 +1170,7 @@ size_t seg_ws_size(int64_t n_ids) {
   // tiles over all slots <= n/4096 + n_slots (each slot rounds up once)
   const int64_t tiles_total = n_ids / kSegTile + kSegMaxSlots;
   Carver c(nullptr, 0);
+  c.take<uint32_t>((size_t)tiles_total * kSegTile);
   c.take<uint16_t>((size_t)tiles_total * kSegBins);
   c.take<uint16_t>((size_t)tiles_total * kSegBins);
   c.take<int32_t>((size_t)tiles_total);

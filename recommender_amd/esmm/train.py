@@ -40,6 +40,11 @@ class MultiTaskStep:
     so both halves follow the mean loss over the global batch."""
 
     def __init__(self, model, optimizer="keras_adam", lr=1e-3, comm=None):
+        """optimizer: "keras_adam" (the reference's tf.keras Adam, esmm/train.py:125: every
+        slab row decays each step — a dense m / v sweep), "keras_adam_deferred" (the same update
+        with each row's decay replayed when the row is next read, SparseAdam(defer_decay=True),
+        fused into the step: bit-identical to "keras_adam" after materialize()), "lazy_adam"
+        (touched rows only) or "sgd"."""
         self.model = model
         self.comm = comm
         dense = [p for n, p in model.named_parameters() if not n.endswith("grad_handle")]
@@ -49,6 +54,13 @@ class MultiTaskStep:
         if optimizer == "sgd":
             self.opt_dense = torch.optim.SGD(dense, lr=lr)
             self.opt_sparse = SparseSGD([table], lr=lr)
+        elif optimizer == "keras_adam_deferred":
+            if slab is not table:
+                raise ValueError("keras_adam_deferred: one GPU (the row-sharded slab applies "
+                                 "inside its exchange)")
+            self.opt_dense = KerasAdam(dense, lr=lr)
+            self.opt_sparse = SparseAdam([table], lr=lr, mode="keras", fused=True,
+                                         defer_join=True, defer_decay=True)
         else:
             self.opt_dense = KerasAdam(dense, lr=lr)
             self.opt_sparse = SparseAdam([table], lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy")
@@ -71,6 +83,12 @@ class MultiTaskStep:
         else:
             self.opt_sparse.step()
         return loss
+
+    def materialize(self):
+        """keras_adam_deferred: bring every slab row up to the last step (the dense sweep's
+        state, bit for bit); a no-op otherwise."""
+        if hasattr(self.opt_sparse, "materialize"):
+            self.opt_sparse.materialize()
 
     def _allreduce_dense(self):
         grads = [p.grad for p in self.dense if p.grad is not None]

@@ -20,9 +20,13 @@ rows of every slot spread over all ranks). Per step, on each rank:
 
 The capacity C (row slots per (rank, owner) pair) is calibrated once, on the first exchanged
 batch (the largest per-owner unique count over all ranks x capacity_factor + 256), so every
-later all-to-all has fixed equal split sizes: no host sync per step, and the whole sharded step
-is stream-ordered (graph-capturable under RCCL). A batch with more than C unique rows for one
-owner sets an overflow flag that the host raises on (check_overflow) — loud, never silent.
+all-to-all has fixed equal split sizes. A batch with more than C unique rows for some owner takes
+a spill round instead of failing: each rank's largest excess over C is all-reduced (MAX) on the
+device beside the row-id all-to-all, and when it is C2 > 0 every rank exchanges the excess rows in
+a second pair of equal-split all-to-alls of [world, C2] blocks (slots after the capacity block),
+so every rank issues the same collectives and no row is dropped. The host reads C2 when the step
+needs its rows (exchange_finish): with the exchange prefetched a step ahead (the production
+path) the value is long on the host; a step without prefetch waits for its own sort there.
 The exchange runs on a side HIP stream (RCCL all-to-alls on their own), overlapping the bottom
 MLP on the main stream; its first half (sort … row-id all-to-all) reads no table state and can
 be queued a step ahead (prefetch).
@@ -62,15 +66,16 @@ class Comm:
         else:
             dist.all_to_all_single(out, inp, osp, isp, group=self.group)
 
-    def all_reduce_(self, t: torch.Tensor):
+    def all_reduce_(self, t: torch.Tensor, op=None):
         if self.world == 1:
             return
+        op = dist.ReduceOp.SUM if op is None else op
         if self.staged:
             c = t.cpu()
-            dist.all_reduce(c, group=self.group)
+            dist.all_reduce(c, op=op, group=self.group)
             t.copy_(c)
         else:
-            dist.all_reduce(t, group=self.group)
+            dist.all_reduce(t, op=op, group=self.group)
 
 
 class _UniqueRows:
@@ -127,7 +132,7 @@ class ShardedSlabEmbedding(nn.Module):
         # batch (_calibrate), then fixed
         self.capacity = capacity
         self.capacity_factor = float(capacity_factor)
-        self._overflow_checks: list = []  # (event, pinned flag) of packed exchanges
+        self.spill_rounds = 0  # steps that exchanged rows past the capacity (a spill round)
 
     @property
     def n_slots(self):
@@ -158,15 +163,16 @@ class ShardedSlabEmbedding(nn.Module):
     def exchange_begin(self, ids: torch.Tensor):
         """Queue the first half of a step's exchange on the side stream: owner-major sort, unique
         / inverse + per-owner counts, the capacity-bounded packing (rs_exchange_pack: every
-        unique row gets a fixed slot in a [world, capacity] send block, each position the slot
-        of its row) and the all-to-all of the row ids. Nothing here reads the table, so it may
-        run a step ahead (prefetch); no host sync once the capacity is known."""
+        unique row within the capacity gets a fixed slot in a [world, capacity] send block, each
+        position the slot of its row), the all-reduced largest excess over the capacity (the
+        spill round's size, rs_exchange_excess) and the all-to-all of the row ids. Nothing here
+        reads the table, so it may run a step ahead (prefetch); no host sync once the capacity
+        is known."""
         L.require_device(ids, "ids")
         dev = ids.device
         ids = ids.contiguous()
         main = torch.cuda.current_stream(dev)
         self.side.wait_stream(main)
-        self.check_overflow(block=False)
         W = self.world
         with torch.cuda.stream(self.side):
             s = SortedIds(ids, self.input_dim, self.slot_offsets, self.err_flag, self.ws,
@@ -190,34 +196,24 @@ class ShardedSlabEmbedding(nn.Module):
             L.call("rs_exchange_pack", L.ptr(uniq), L.ptr(n_unique), L.ptr(counts), W,
                    self.stride, C, L.ptr(inverse), n, L.ptr(send_ids), L.ptr(slot_of),
                    L.ptr(inv_slot), L.ptr(overflow), L.stream_ptr(dev))
-            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            host.copy_(overflow, non_blocking=True)
-            ovf_ready = torch.cuda.Event()
-            ovf_ready.record(self.side)
+            # the spill round's size: every rank's largest excess over C, all-reduced (MAX)
+            excess = torch.empty(1, dtype=torch.int64, device=dev)
+            L.call("rs_exchange_excess", L.ptr(counts), W, C, L.ptr(excess), L.stream_ptr(dev))
+            self.comm.all_reduce_(excess, dist.ReduceOp.MAX)
+            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            host.copy_(excess, non_blocking=True)
+            excess_ready = torch.cuda.Event()
+            excess_ready.record(self.side)
             recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
             self.comm.all_to_all(recv_ids, send_ids)
-        self._overflow_checks.append((ovf_ready, host))
-        return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot[:n], recv_ids=recv_ids,
-                    capacity=C, dev=dev)
+        return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, recv_ids=recv_ids,
+                    capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
+                    inverse=inverse, excess=(excess_ready, host))
 
     def check_overflow(self, block: bool = True):
-        """Raise if a packed exchange had more unique rows for one owner than the capacity (the
-        rows past it were not exchanged, so that step's results are wrong). block=False only
-        looks at packings whose flag has reached the host; exchange_begin calls it so, join()
-        with block=True."""
-        keep = []
-        for ev, host in self._overflow_checks:
-            if not block and not ev.query():
-                keep.append((ev, host))
-                continue
-            ev.synchronize()
-            if int(host.item()):
-                self._overflow_checks = []
-                raise RuntimeError(
-                    f"ShardedSlabEmbedding: a rank had more unique rows for one owner than the "
-                    f"exchange capacity ({self.capacity}); rebuild with a larger capacity_factor "
-                    f"(now {self.capacity_factor}) or an explicit capacity")
-        self._overflow_checks = keep
+        """Kept for callers of the round-4 API: a batch past the capacity now takes a spill
+        round (exchange_finish) instead of raising, so there is nothing to check."""
+        return None
 
     @staticmethod
     def _ids_key(ids):
@@ -250,26 +246,47 @@ class ShardedSlabEmbedding(nn.Module):
         return None
 
     def exchange_finish(self, st):
-        """The second half, on the side stream after the previous step's owner apply: the owners
-        gather the requested rows (rs_gather_rows_padded: padding slots read zero rows) and the
-        rows go back in one all-to-all of equal [capacity, D] blocks. Returns (view: the
-        [world * capacity, D] rows, inverse ids [B, S] int32 = each position's slot)."""
+        """The second half, on the side stream after the previous step's owner apply: the spill
+        round's ids when the all-reduced excess C2 is > 0 (rs_exchange_pack_spill: the rows past
+        the capacity get slots world·C + o·C2 + j and their ids go in a second equal-split
+        all-to-all), the owners gather the requested rows (rs_gather_rows_padded: padding slots
+        read zero rows) and the rows go back in one all-to-all of equal [capacity, D] blocks (two
+        with a spill round). Returns (view: the [world * (C + C2), D] rows, inverse ids [B, S]
+        int32 = each position's slot)."""
         dev, W, C = st["dev"], self.world, st["capacity"]
         main = torch.cuda.current_stream(dev)
         D = self.output_dim
+        ev, host = st["excess"]
+        ev.synchronize()  # prefetched a step ahead: long done
+        C2 = int(host.item())
+        n = st["ids"].numel()
+        recv_spill = None
         with torch.cuda.stream(self.side):
-            served = torch.empty(W * C, D, device=dev)
-            L.call("rs_gather_rows_padded", L.ptr(self.shard.weight), self.shard.input_dim, D,
-                   L.ptr(st["recv_ids"]), W * C, L.ptr(served), L.stream_ptr(dev))
-            rows = torch.empty(W * C, D, device=dev)
-            self.comm.all_to_all(rows, served)
+            if C2 > 0:
+                self.spill_rounds += 1
+                spill_ids = torch.empty(W * C2, dtype=torch.int32, device=dev)
+                L.call("rs_exchange_pack_spill", L.ptr(st["uniq"]), L.ptr(st["n_unique"]),
+                       L.ptr(st["counts"]), W, self.stride, C, C2, L.ptr(st["inverse"]), n,
+                       L.ptr(spill_ids), L.ptr(st["slot_of"]), L.ptr(st["inv_slot"]), None,
+                       L.stream_ptr(dev))
+                recv_spill = torch.empty(W * C2, dtype=torch.int32, device=dev)
+                self.comm.all_to_all(recv_spill, spill_ids)
+            rows = torch.empty(W * (C + C2), D, device=dev)
+            for lo, hi, rid in ((0, W * C, st["recv_ids"]), (W * C, W * (C + C2), recv_spill)):
+                if hi == lo:
+                    continue
+                served = torch.empty(hi - lo, D, device=dev)
+                L.call("rs_gather_rows_padded", L.ptr(self.shard.weight), self.shard.input_dim, D,
+                       L.ptr(rid), hi - lo, L.ptr(served), L.stream_ptr(dev))
+                self.comm.all_to_all(rows[lo:hi], served)
         main.wait_stream(self.side)
-        inverse = st["inv_slot"]
+        inverse = st["inv_slot"][:n]
         for t in (rows, inverse):
             t.record_stream(main)
         self.view.weight = rows
-        self.view.input_dim = W * C
-        self._st = dict(sorted=st["s"], slot_of=st["slot_of"], recv_ids=st["recv_ids"], capacity=C)
+        self.view.input_dim = W * (C + C2)
+        self._st = dict(sorted=st["s"], slot_of=st["slot_of"], recv_ids=st["recv_ids"],
+                        recv_spill=recv_spill, capacity=C, spill=C2)
         return self.view, inverse.view(st["ids"].shape)
 
     def exchange(self, ids: torch.Tensor):
@@ -305,10 +322,10 @@ class ShardedSlabEmbedding(nn.Module):
         main = torch.cuda.current_stream(dev)
         self.side.wait_stream(main)
         s = st["sorted"]
-        W, C, D = self.world, st["capacity"], self.output_dim
+        W, C, C2, D = self.world, st["capacity"], st["spill"], self.output_dim
         with torch.cuda.stream(self.side):
             g = grad_rows.contiguous()
-            send_grad = torch.empty(W * C, D, dtype=torch.float32, device=dev)
+            send_grad = torch.empty(W * (C + C2), D, dtype=torch.float32, device=dev)
             uniq_rows = torch.empty(max(s.n, 1), dtype=torch.int32, device=dev)
             if s.n:
                 w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(s.n, D), dev)
@@ -318,13 +335,21 @@ class ShardedSlabEmbedding(nn.Module):
                        L.ptr(g), L.ptr(row_scale), self.n_slots if row_scale is not None else 1,
                        D, self.key_space, L.ptr(st["slot_of"]), L.ptr(uniq_rows),
                        L.ptr(send_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
-            recv_grad = torch.empty(W * C, D, dtype=torch.float32, device=dev)
-            self.comm.all_to_all(recv_grad, send_grad)
+            recv_grad = torch.empty(W * (C + C2), D, dtype=torch.float32, device=dev)
+            self.comm.all_to_all(recv_grad[: W * C], send_grad[: W * C])
+            recv_ids = st["recv_ids"]
+            if C2 > 0:
+                self.comm.all_to_all(recv_grad[W * C:], send_grad[W * C:])
+                # source-rank-major [world, C + C2]: each row's terms stay in source-rank order,
+                # the order the owner's fold has without a spill round (the oracle's)
+                recv_grad = torch.cat([recv_grad[: W * C].view(W, C, D),
+                                       recv_grad[W * C:].view(W, C2, D)], 1).view(-1, D)
+                recv_ids = torch.cat([recv_ids.view(W, C), st["recv_spill"].view(W, C2)],
+                                     1).view(-1)
             if self.optimizer is None:
                 raise RuntimeError("ShardedSlabEmbedding has no optimizer (set_optimizer)")
             opt = self.optimizer
             params = opt._params()
-            recv_ids = st["recv_ids"]
             valid = (recv_ids >= 0).to(torch.uint8)
             if self.world > 1 and not global_grads:
                 if opt.kind == L.RS_OPT_SGD:
@@ -339,10 +364,8 @@ class ShardedSlabEmbedding(nn.Module):
         self._st = None
 
     def join(self):
-        """Make the current stream wait for the exchange / apply chain (and raise if a finished
-        exchange overflowed its capacity)."""
+        """Make the current stream wait for the exchange / apply chain."""
         torch.cuda.current_stream(self.side.device).wait_stream(self.side)
-        self.check_overflow(block=False)
 
     def full_weight(self) -> torch.Tensor:
         """Gather the whole slab (tests / checkpoints): [V, D] with row g from rank g % W."""

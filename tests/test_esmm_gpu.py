@@ -126,6 +126,40 @@ def test_esmm_family_keras_adam_step_vs_oracle(kind):
     np.testing.assert_array_equal(v_t.cpu().numpy(), v2)
 
 
+@pytest.mark.parametrize("kind", ["ESMM", "MMOE"])
+def test_keras_adam_deferred_decay_equals_dense_sweep(kind):
+    """cfg4's timed optimizer: MultiTaskStep("keras_adam_deferred") — the reference's Keras Adam
+    with each slab row's decay replayed when the row is next read (fused sparse optimizer, no
+    per-step dense sweep) — equals MultiTaskStep("keras_adam") (the dense m / v sweep every
+    step) after materialize(): table, m, v and every dense parameter bit for bit over 4 steps,
+    losses equal."""
+    vocab = {k: min(v, 5000) for k, v in FEAT_VOCAB.items()}
+    rng = np.random.default_rng(8)
+    batches = []
+    for _ in range(4):
+        f, lab = aliccp_batch(rng, 512, vocab)
+        batches.append(({k: torch.from_numpy(v).to(DEV) for k, v in f.items()},
+                        torch.from_numpy(lab).to(DEV)))
+    res = []
+    for opt in ("keras_adam", "keras_adam_deferred"):
+        g = torch.Generator(device=DEV)
+        g.manual_seed(3)
+        model = build(kind, vocab, 18, DEV, g)
+        step = MultiTaskStep(model, opt)
+        losses = [float(step(f, lab)) for f, lab in batches]
+        step.materialize()
+        torch.cuda.synchronize()
+        slab = model.embedding_layer.slab
+        m, v, _ = step.opt_sparse._slots(slab)
+        res.append((losses, slab.weight.detach().clone(), m.clone(), v.clone(),
+                    [p.detach().clone() for p in step.dense]))
+    (la, wa, ma, va, da), (lb, wb, mb, vb, db) = res
+    assert la == lb
+    assert torch.equal(wa, wb) and torch.equal(ma, mb) and torch.equal(va, vb)
+    for x, y in zip(da, db):
+        assert torch.equal(x, y)
+
+
 def _copy_into_sharded(m1, m2, rank=0, world=1):
     sd = {k: v for k, v in m1.state_dict().items() if not k.startswith("embedding_layer")}
     m2.load_state_dict(sd, strict=False)

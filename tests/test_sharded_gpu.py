@@ -137,9 +137,11 @@ def test_world2_sharded_embedding_matches_oracle(opt, even):
     assert all(v == "ok" for v in res.values()), res
 
 
-def _fused_dlrm_world2_worker(rank, world, port, q):
-    """The production fused DLRM step over a row-sharded slab, two ranks on the one GPU (gloo):
-    every check is against the oracle on the GLOBAL batch (both ranks' examples)."""
+def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
+    """The production fused DLRM step over a row-sharded slab, `world` ranks on the one GPU
+    (gloo): every check is against the oracle on the GLOBAL batch (all ranks' examples). Two
+    steps; `spill`: the second batch has uniform ids (many more unique rows than the capacity the
+    first, Zipf, batch calibrated), so its exchange takes the spill round — on the last step."""
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -164,13 +166,17 @@ def _fused_dlrm_world2_worker(rank, world, port, q):
         comm = Comm()
         emb = ShardedSlabEmbedding(cards, D, comm, device=DEV, full_weight=torch.from_numpy(table))
         g = torch.Generator(device=DEV)
-        g.manual_seed(3)  # the same MLP init on both ranks
+        g.manual_seed(3)  # the same MLP init on every rank
         model = DLRM([128, 64, D], [128, 64, 1], D, V, S, 13, device=DEV, generator=g,
                      embedding_layer=emb)
         step = TrainStep(model, "sgd", lr=lr, comm=comm)
-        per = [criteo_batch(np.random.default_rng(40 + r), B, cards) for r in range(world)]
-        cat, dn, lb = per[rank]
-        assert step.fused_step_ready((torch.from_numpy(cat).to(DEV), None, None))
+        steps = [[criteo_batch(np.random.default_rng(40 + 10 * k + r), B, cards) for r in range(world)]
+                 for k in range(2)]
+        if spill:
+            for r in range(world):
+                c2 = steps[1][r][0]
+                for j, c in enumerate(cards):
+                    c2[:, j] = np.random.default_rng(70 + r + 100 * j).integers(0, c, B)
         top0, bot0 = _layers(model.top_mlp), _layers(model.bottom_mlp)
         cap = {}
         bx = emb.backward_exchange
@@ -184,37 +190,46 @@ def _fused_dlrm_world2_worker(rank, world, port, q):
             return bx(grad_rows, global_grads=global_grads, row_scale=row_scale)
 
         emb.backward_exchange = spy
-        batch = tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb))
-        loss = float(step(batch))
-        emb.join()
-        torch.cuda.synchronize()
-        # both ranks' gradient rows, for the sharded-apply oracle
-        gr = [torch.empty_like(cap["g"].cpu()) for _ in range(world)]
-        dist.all_gather(gr, cap["g"].cpu())
-        want = OS.sharded_sgd_step(table, [p[0] for p in per], [x.numpy() for x in gr], lr, world,
-                                   so, global_grads=True)
-        full = emb.full_weight().cpu().numpy()
-        np.testing.assert_array_equal(full, want)
-        assert (full != table).any(1).sum() > 1000
-        # the dense half and the loss against the oracle step on the global batch
-        st = DLRMState(table.copy(), so, [(k.copy(), b.copy()) for k, b in bot0],
-                       [(k.copy(), b.copy()) for k, b in top0])
-        det = {}
-        gcat = np.concatenate([p[0] for p in per])
-        gdn = np.concatenate([p[1] for p in per])
-        glb = np.concatenate([p[2] for p in per])
-        ref_loss = dlrm_sgd_step(st, gcat, gdn, glb, lr, det)
-        assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
-        top_tol, bot_tol = dense_half_tolerances(det, B * world)
-        _check_chain("top MLP", _grads(model.top_mlp), det["top_grads"], top_tol)
-        _check_chain("bottom MLP", _grads(model.bottom_mlp), det["bottom_grads"], bot_tol)
-        _check_sgd("top MLP", top0, _layers(model.top_mlp), _grads(model.top_mlp), lr)
-        _check_sgd("bottom MLP", bot0, _layers(model.bottom_mlp), _grads(model.bottom_mlp), lr)
-        # this rank's gradient rows against the oracle's rows of its examples
-        dx = det["dx"].reshape(world, B * S, D)[rank]
-        dxb = det["dx_bound"].reshape(world, B * S, D)[rank]
-        err = np.abs(cap["g"].cpu().numpy().astype(np.float64) - dx)
-        assert (err <= 1e-5 * dxb + 1e-38).all(), "gradient rows"
+        want = table
+        for k, per in enumerate(steps):
+            cat, dn, lb = per[rank]
+            batch = tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb))
+            assert step.fused_step_ready((batch[0], None, None))
+            loss = float(step(batch))
+            emb.join()
+            torch.cuda.synchronize()
+            # all ranks' gradient rows, for the sharded-apply oracle
+            gr = [torch.empty_like(cap["g"].cpu()) for _ in range(world)]
+            dist.all_gather(gr, cap["g"].cpu())
+            want = OS.sharded_sgd_step(want, [p[0] for p in per], [x.numpy() for x in gr], lr,
+                                       world, so, global_grads=True)
+            full = emb.full_weight().cpu().numpy()
+            np.testing.assert_array_equal(full, want)
+            if k == 0:
+                assert (full != table).any(1).sum() > 1000
+                # the dense half and the loss against the oracle step on the global batch
+                st = DLRMState(table.copy(), so, [(k_.copy(), b_.copy()) for k_, b_ in bot0],
+                               [(k_.copy(), b_.copy()) for k_, b_ in top0])
+                det = {}
+                gcat = np.concatenate([p[0] for p in per])
+                gdn = np.concatenate([p[1] for p in per])
+                glb = np.concatenate([p[2] for p in per])
+                ref_loss = dlrm_sgd_step(st, gcat, gdn, glb, lr, det)
+                assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
+                top_tol, bot_tol = dense_half_tolerances(det, B * world)
+                _check_chain("top MLP", _grads(model.top_mlp), det["top_grads"], top_tol)
+                _check_chain("bottom MLP", _grads(model.bottom_mlp), det["bottom_grads"], bot_tol)
+                _check_sgd("top MLP", top0, _layers(model.top_mlp), _grads(model.top_mlp), lr)
+                _check_sgd("bottom MLP", bot0, _layers(model.bottom_mlp), _grads(model.bottom_mlp),
+                           lr)
+                # this rank's gradient rows against the oracle's rows of its examples
+                dx = det["dx"].reshape(world, B * S, D)[rank]
+                dxb = det["dx_bound"].reshape(world, B * S, D)[rank]
+                err = np.abs(cap["g"].cpu().numpy().astype(np.float64) - dx)
+                assert (err <= 1e-5 * dxb + 1e-38).all(), "gradient rows"
+                assert emb.spill_rounds == 0
+        if spill:
+            assert emb.spill_rounds == 1, emb.spill_rounds
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover
         import traceback
@@ -224,19 +239,22 @@ def _fused_dlrm_world2_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_world2_fused_dlrm_step_matches_oracle():
-    """TrainStep's fused DLRM step on a row-sharded slab at world 2 (gloo, both ranks on the one
-    GPU): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the batch sums
-    are all-reduced (the dense half of the global step); the owners apply the gradient rows.
-    Slab bit-exact vs oracle/sharded.py fed with both ranks' kernel rows; loss, the twelve MLP
-    gradients (per-element bounds) and the SGD apply vs the oracle step on the global batch."""
+@pytest.mark.parametrize("world,spill", [(2, False), (2, True), (3, True), (4, False), (4, True)])
+def test_worldn_fused_dlrm_step_matches_oracle(world, spill):
+    """TrainStep's fused DLRM step on a row-sharded slab at world 2 / 3 / 4 (gloo, all ranks on
+    the one GPU): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the
+    batch sums are all-reduced (the dense half of the global step); the owners apply the gradient
+    rows. Two steps, slab bit-exact vs oracle/sharded.py fed with every rank's kernel rows after
+    each; loss, the twelve MLP gradients (per-element bounds) and the SGD apply vs the oracle step
+    on the global batch. `spill`: the last step's batch overflows the calibrated capacity and is
+    exchanged with the spill round — still bit-exact, on every rank."""
     import torch.multiprocessing as mp
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29300 + (os.getpid() % 500)
-    ps = [ctx.Process(target=_fused_dlrm_world2_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 29300 + (os.getpid() % 400) + 13 * world + (5 if spill else 0)
+    ps = [ctx.Process(target=_fused_dlrm_worldn_worker, args=(r, world, port, q, spill))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -328,30 +346,34 @@ def test_world2_prefetched_exchange_bit_identical():
     assert all(v == "ok" for v in res.values()), res
 
 
-def test_exchange_capacity_overflow_raises():
-    """A batch with more unique rows for one owner than the exchange capacity must not train
-    silently: the packing flags it and the next host check raises. The calibrated capacity of
-    the same slab holds the batch."""
+def test_exchange_capacity_spill_round():
+    """A batch with more unique rows for one owner than the exchange capacity takes the spill
+    round (the excess rows in a second pair of equal-split all-to-alls) instead of failing: the
+    lookup equals the slab's rows, and three SGD steps on a capacity-64 slab equal the same steps
+    on a calibrated one, bit for bit."""
+    from recommender_amd.optim import SparseSGD
     from recommender_amd.sharded import Comm, ShardedSlabEmbedding
     from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
 
     cards = criteo_cardinalities(100_000, 26)
-    cat, _, _ = criteo_batch(np.random.default_rng(3), 256, cards)
-    ids = torch.from_numpy(cat).to(DEV)
-    tiny = ShardedSlabEmbedding(cards, 16, Comm(), device=DEV, capacity=64)
-    with torch.no_grad():
-        tiny(ids)
-    torch.cuda.synchronize()
-    with pytest.raises(RuntimeError, match="capacity"):
-        tiny.check_overflow()
-    ok = ShardedSlabEmbedding(cards, 16, Comm(), device=DEV)
-    with torch.no_grad():
-        out = ok(ids)
-    torch.cuda.synchronize()
-    ok.check_overflow()
-    assert ok.capacity >= 256
-    # the lookup itself: every position's row from the slab
-    full = ok.full_weight()
-    so = ok.slot_offsets
-    rows = ids.long() + so[:-1][None, :]
-    assert torch.equal(out.reshape(-1, 16), full[rows.reshape(-1)])
+    rng = np.random.default_rng(3)
+    batches = [torch.from_numpy(criteo_batch(rng, 256, cards)[0]).to(DEV) for _ in range(3)]
+    w0 = torch.from_numpy(np.random.default_rng(5).uniform(-0.05, 0.05, (sum(cards), 16))
+                          .astype(np.float32))
+    res = []
+    for capacity in (64, None):
+        emb = ShardedSlabEmbedding(cards, 16, Comm(), device=DEV, full_weight=w0, capacity=capacity)
+        emb.set_optimizer(SparseSGD([emb.shard], lr=0.1))
+        for ids in batches:
+            out = emb(ids)
+            torch.cuda.synchronize()
+            full = emb.full_weight()
+            rows = ids.long() + emb.slot_offsets[:-1][None, :]
+            assert torch.equal(out.detach().reshape(-1, 16), full[rows.reshape(-1)])
+            (out * 0.5).sum().backward()
+            emb.join()
+        torch.cuda.synchronize()
+        res.append((emb.full_weight().cpu(), emb.spill_rounds))
+    (wa, spills), (wb, none) = res
+    assert spills == 3 and none == 0
+    assert torch.equal(wa, wb)
