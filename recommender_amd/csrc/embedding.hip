@@ -424,7 +424,11 @@ struct Tile32Edges {
 // instead of one per run: a table load waits for every load issued before it (vmcnt counts in
 // order), so an inline update drains the in-flight gradient rows at each run end. Same
 // arithmetic, each row written once: bit-identical.
-template <int OPT, int Q = 0>
+// P > 0 (SGD only, round 5): the table rows of the tile's first P complete runs (runs that start
+// and end inside the tile: the ones updated on the spot) are loaded at the tile's start, from the
+// lane-parallel keys, ahead of every gradient-row load — so those updates wait for nothing; runs
+// past the P-th take the queue (Q) as before. Same arithmetic, each row written once.
+template <int OPT, int Q = 0, int P = 0>
 __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ keys,
                                                    const int32_t* __restrict__ pos, int64_t n,
                                                    uint32_t n_rows, const float* __restrict__ grad,
@@ -432,6 +436,8 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   constexpr int T = 32, VEC = 4, CPL = 1, U = 8;
   constexpr bool kQueue = Q > 0 && OPT == OPT_SGD;
   constexpr int QN = Q > 0 ? Q : 1;
+  constexpr bool kPre = P > 0 && OPT == OPT_SGD;
+  constexpr int PN = P > 0 ? P : 1;
   const int gl = threadIdx.x & 31;
   const int64_t k0 = t * T;
   const int64_t k1 = k0 + T < n ? k0 + T : n;
@@ -447,6 +453,26 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   const uint32_t key_before = k0 > 0 ? keys[k0 - 1] : 0xFFFFFFFFu;
   const uint32_t key_after = k1 < n ? keys[k1] : 0xFFFFFFFEu;
   auto key_of = [&](int u) { return (uint32_t)__shfl((int)kv, u, 32); };
+  // the first P complete runs' table rows, loaded before any gradient row
+  float pre[PN][VEC];
+  int n_pre = 0, ci = 0;  // preloaded rows, complete runs emitted so far
+  if constexpr (kPre) {
+    const uint32_t knext = gl + 1 < ne ? key_of(gl + 1) : key_after;
+    (void)key_of(gl);  // keep the shuffles of both calls in the same (uniform) control flow
+    const bool cend = lv && knext != kv && kv != key_before;  // a complete run's last entry
+    const uint64_t bm = __ballot(cend) >> (threadIdx.x & 32);
+    uint32_t m = (uint32_t)bm;
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+      const int e = m ? __builtin_ctz(m) : 0;
+      const uint32_t row = key_of(e);
+      if (m) {
+        RowIO<VEC>::load(a.table + (int64_t)row * dim + col, pre[i]);
+        ++n_pre;
+        m &= m - 1;
+      }
+    }
+  }
   // the row scale multiplies at the sum (consume), not here: a multiply right behind each load
   // would wait for it and serialise the batch's loads (measured: apply 215 -> 272 us alone)
   auto load_batch = [&](int b0, float (&r)[U][VEC]) {
@@ -492,6 +518,21 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   auto emit = [&](uint32_t row, bool starts, bool ends, int head_e) {
     if (row >= n_rows) return;  // OOB sentinel run: gradient dropped
     if (starts && ends) {
+      if constexpr (kPre) {
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < PN; ++i) {
+          if (i == ci && i < n_pre) {
+            float tr[VEC];
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) tr[c] = pre[i][c] - a.p.lr * acc[0][c];
+            RowIO<VEC>::store(a.table + (int64_t)row * dim + col, tr);
+            done = true;
+          }
+        }
+        ++ci;
+        if (done) return;
+      }
       if constexpr (kQueue) {
         if (qn == QN) flush();
 #pragma unroll
@@ -591,7 +632,7 @@ __global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restr
 // (chunk[t][1], tile flag bit 0) and, at a group's first tile, the continuation's group sum
 // (chunk[t][0]); seg_fixup_kernel folds those (level 2). Bit-identical to seg_tile32 + seg_chunk
 // + seg_fixup, one launch fewer and no global partials.
-template <int OPT, int Q = 0>
+template <int OPT, int Q = 0, int P = 0>
 __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __restrict__ keys,
                                                            const int32_t* __restrict__ pos,
                                                            int64_t n, uint32_t n_rows,
@@ -604,7 +645,7 @@ __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __res
   const int64_t t = (int64_t)blockIdx.x * G + gi;
   const bool live = t < n_tiles;
   Tile32Edges e{};
-  if (live) e = tile32_walk<OPT, Q>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
+  if (live) e = tile32_walk<OPT, Q, P>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
   if (gl == 0) fkey[gi] = live ? e.first_key : 0xFFFFFFFFu;
   __syncthreads();
   if (!live) return;
@@ -1088,6 +1129,15 @@ static bool apply_queue() {
   }();
   return v != 0;
 }
+// RS_APPLY_PRE=2 / 4: the walk loads the first 2 / 4 complete runs' table rows at each tile's
+// start instead of queueing the updates (A/B; 0 = off)
+static int apply_pre() {
+  static const int v = [] {
+    const char* e = getenv("RS_APPLY_PRE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos, int64_t n,
                                int64_t n_rows, const float* grad, const ApplyArgs& a,
@@ -1117,7 +1167,13 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     if (g32) {                                                                                  \
-      if (OPTV == OPT_SGD && apply_queue())                                                     \
+      if (OPTV == OPT_SGD && apply_pre() == 2)                                                  \
+        seg_group32_kernel<OPTV, 0, 2><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                 \
+            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
+      else if (OPTV == OPT_SGD && apply_pre() == 4)                                             \
+        seg_group32_kernel<OPTV, 0, 4><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                 \
+            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
+      else if (OPTV == OPT_SGD && apply_queue())                                                \
         seg_group32_kernel<OPTV, 2><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                    \
             keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
       else                                                                                      \
