@@ -2107,7 +2107,6 @@ static int32_t train_step_launch(
       const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch, 1);
       blocks = ceil_div(batch, 4 * (int64_t)epw);
       kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw, gbot);
-      RS_CHECK_LAUNCH();
       train_gbot_reduce_kernel<<<blocks, 256, 0, st>>>(gbot, xin, batch, epw, part);
     };
     if (id_dtype == RS_ID_I64) go3(dlrm_train_chunk3<true>);

@@ -704,6 +704,10 @@ struct SegArgs {
   int32_t* scnt;                // [n_slots][tiles] sentinels per tile
   uint2* tmp;                   // [n] (id, position) after pass 0 of a two-pass slot
   uint32_t* keys0;              // [n_slots][tiles][4096] pass-0 keys in tile order (bit 31: sentinel)
+  int32_t* offs0;               // [n_slots][tiles][4096] output index of a tile's first key per digit
+  int32_t* offs1;
+  int32_t* starts;              // [2][kSegMaxSlots + 1] valid / sentinel starts per slot (+ totals)
+  int32_t* spre;                // [n_slots][tiles] sentinels of the slot's earlier tiles
   uint32_t* rows_out;
   int32_t* pos_out;
   int32_t* err_flag;
@@ -795,15 +799,13 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
   bool oob = false;
   seg_load0<ID64>(a, sl, s, t, id, live, sent, oob);
   const int lane = threadIdx.x & 63;
-  const uint64_t lt = lanemask_lt64();
   const uint32_t mask = (uint32_t)bins - 1u;
   int ns = 0;
 #pragma unroll
   for (int k = 0; k < kSegKPL; ++k) {
-    const bool lv = (live >> k) & 1u;
-    const uint32_t d = id[k] & mask;
-    const uint64_t m = match_digit<kSegBits>(d, lv);
-    if (lv && (m & lt) == 0) atomicAdd(&cnt[d], __popcll(m));
+    // one LDS atomic per key: the LDS unit serialises a hot digit's lanes, which costs less
+    // than the 12-ballot match that would aggregate them on the VALU
+    if ((live >> k) & 1u) atomicAdd(&cnt[id[k] & mask], 1);
     ns += __popcll(__ballot((sent >> k) & 1u));
   }
   if (lane == 0 && ns) atomicAdd(&nsent, ns);
@@ -826,24 +828,20 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
 }
 
 // slot starts: vstart[s] = valid ids of slots < s, sstart[s] = sentinels of slots < s (index
-// n_slots: the totals), and *spre = sentinels of slot s0's tiles before t0; from the pass-0 tile
-// counts (n_slots x tiles ints in L2 / MALL), every count loaded by its own lane in one round
-// trip, summed per slot in LDS, the slot prefix by one wave's scan
-__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int s0, int t0, int32_t* vstart,
-                                                int32_t* sstart, int32_t* spre) {
+// n_slots: the totals), from the pass-0 tile counts (n_slots x tiles ints, L2 / MALL): every count
+// loaded by its own lane in one round trip, summed per slot in LDS, the slot prefix by one wave
+__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstart, int32_t* sstart) {
   if (threadIdx.x <= a.n_slots) {
     vstart[threadIdx.x] = 0;
     sstart[threadIdx.x] = 0;
   }
-  if (threadIdx.x == 0) *spre = 0;
   __syncthreads();
   const int total = a.n_slots * a.tiles;
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int sl = e / a.tiles, tt = e - sl * a.tiles;
+    const int sl = e / a.tiles;
     const int32_t v = a.vcnt[e], z = a.scnt[e];
     if (v) atomicAdd(&vstart[sl], v);
     if (z) atomicAdd(&sstart[sl], z);
-    if (z && sl == s0 && tt < t0) atomicAdd(spre, z);
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over the slots (n_slots <= 64), totals at n_slots
@@ -870,57 +868,80 @@ __device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int s0, int t0
   __syncthreads();
 }
 
-// doff[d] = base + (ids of digits < d in the slot) + (ids of digit d in the slot's tiles < t), from
-// the slot's tile histograms: thread j owns digits [16 j, 16 j + 16)
-__device__ __forceinline__ void seg_digit_offsets(const uint16_t* __restrict__ hist, int n_tiles,
-                                                  int t, int bins, int32_t base,
-                                                  int32_t* __restrict__ doff, int32_t* wsum) {
-  constexpr int PER = kSegBins / kSegThreads;  // 16
-  const int d0 = threadIdx.x * PER;
-  int32_t tot[PER], pre[PER];
+// the 16 uint16 counts of digits [d0, d0 + 16) of tiles [t0, t0 + 8) (zeros past n_tiles)
+__device__ __forceinline__ void seg_load8(const uint16_t* __restrict__ hist, int t0, int n_tiles,
+                                          int d0, uint4 (&x)[8][2]) {
 #pragma unroll
-  for (int c = 0; c < PER; ++c) tot[c] = pre[c] = 0;
-  if (d0 < bins && bins >= PER) {
-    // eight tiles' 32-byte slices in flight at a time (one round trip per eight tiles, not one
-    // per tile: the slot's histograms come from L2 / MALL)
-    constexpr int TB = 8;
-    for (int tt0 = 0; tt0 < n_tiles; tt0 += TB) {
-      uint4 x[TB][2];
-#pragma unroll
-      for (int j = 0; j < TB; ++j) {
-        const uint4* h = reinterpret_cast<const uint4*>(hist + (int64_t)(tt0 + j) * kSegBins + d0);
-        const bool in = tt0 + j < n_tiles;
-        x[j][0] = in ? h[0] : make_uint4(0u, 0u, 0u, 0u);
-        x[j][1] = in ? h[1] : make_uint4(0u, 0u, 0u, 0u);
+  for (int j = 0; j < 8; ++j) {
+    const uint4* h = reinterpret_cast<const uint4*>(hist + (int64_t)(t0 + j) * kSegBins + d0);
+    const bool in = t0 + j < n_tiles;
+    x[j][0] = in ? h[0] : make_uint4(0u, 0u, 0u, 0u);
+    x[j][1] = in ? h[1] : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+__device__ __forceinline__ int32_t seg_u16(const uint4 (&x)[2], int c) {
+  const uint32_t w = c < 8 ? (&x[0].x)[c >> 1] : (&x[1].x)[(c - 8) >> 1];
+  return (int32_t)((c & 1) ? (w >> 16) : (w & 0xFFFFu));
+}
+
+// One block per slot, after a pass's histograms: offs[t][d] = base + (keys of digits < d in the
+// slot) + (keys of digit d in the slot's tiles < t) for every tile t — the column scan the scatter
+// blocks then read as one 16 KB row each. Pass 0 also writes the slot starts and each tile's
+// sentinel prefix. Thread j owns digits [16 j, 16 j + 16).
+template <int PASS>
+__global__ __launch_bounds__(kSegThreads) void slot_sort_scan_kernel(SegArgs a) {
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
+  __shared__ int32_t wsum[4];
+  const int s = blockIdx.x;
+  if (s >= a.n_slots) return;
+  const SegSlot sl = seg_slot(a, s);
+  if (PASS == 1 && sl.w1 == 0) return;
+  if (PASS == 0) {
+    seg_slot_starts(a, vstart, sstart);
+    if (s == 0)
+      for (int q = threadIdx.x; q <= a.n_slots; q += blockDim.x) {
+        a.starts[q] = vstart[q];
+        a.starts[kSegMaxSlots + 1 + q] = sstart[q];
       }
-#pragma unroll
-      for (int j = 0; j < TB; ++j) {
-        const uint32_t w[8] = {x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w,
-                               x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w};
-        const bool before = tt0 + j < t;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int32_t lo = (int32_t)(w[c] & 0xFFFFu), hi = (int32_t)(w[c] >> 16);
-          tot[2 * c] += lo;
-          tot[2 * c + 1] += hi;
-          if (before) {
-            pre[2 * c] += lo;
-            pre[2 * c + 1] += hi;
-          }
-        }
+    if (threadIdx.x == 0) {
+      int32_t run = 0;
+      for (int t = 0; t < a.tiles; ++t) {
+        a.spre[s * a.tiles + t] = run;
+        run += a.scnt[s * a.tiles + t];
       }
     }
-  } else if (d0 < bins) {  // fewer than 16 bins (a slot of <= 8 rows): thread 0 alone
-    for (int tt = 0; tt < n_tiles; ++tt) {
-      const uint16_t* h = hist + (int64_t)tt * kSegBins + d0;
+  } else {
+    if (threadIdx.x <= 1) vstart[s + threadIdx.x] = a.starts[s + threadIdx.x];
+    __syncthreads();
+  }
+  const int32_t base = vstart[s];
+  const int bins = 1 << (PASS == 0 ? sl.w0 : sl.w1);
+  const int n_tiles = PASS == 0 ? a.tiles : (vstart[s + 1] - base + kSegTile - 1) / kSegTile;
+  const uint16_t* hist = (PASS == 0 ? a.hist0 : a.hist1) + (int64_t)s * a.tiles * kSegBins;
+  int32_t* offs = (PASS == 0 ? a.offs0 : a.offs1) + (int64_t)s * a.tiles * kSegBins;
+  constexpr int PER = kSegBins / kSegThreads;  // 16
+  const int d0 = threadIdx.x * PER;
+  const bool vec = bins >= PER;
+  int32_t tot[PER];
 #pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const int32_t v = d0 + c < bins ? h[c] : 0;
-        tot[c] += v;
-        if (tt < t) pre[c] += v;
+  for (int c = 0; c < PER; ++c) tot[c] = 0;
+  if (d0 < bins) {
+    for (int t0 = 0; t0 < n_tiles; t0 += 8) {
+      if (vec) {
+        uint4 x[8][2];
+        seg_load8(hist, t0, n_tiles, d0, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int c = 0; c < PER; ++c) tot[c] += seg_u16(x[j], c);
+      } else {
+        for (int t = t0; t < n_tiles && t < t0 + 8; ++t)
+          for (int c = 0; c < PER && d0 + c < bins; ++c) tot[c] += hist[(int64_t)t * kSegBins + d0 + c];
       }
     }
   }
+  // exclusive scan of the digit totals over the block
   int32_t sum = 0;
 #pragma unroll
   for (int c = 0; c < PER; ++c) sum += tot[c];
@@ -935,10 +956,35 @@ __device__ __forceinline__ void seg_digit_offsets(const uint16_t* __restrict__ h
   __syncthreads();
   int32_t run = base + x - sum;
   for (int w = 0; w < wave; ++w) run += wsum[w];
+  int32_t cur[PER];
 #pragma unroll
   for (int c = 0; c < PER; ++c) {
-    if (d0 + c < bins) doff[d0 + c] = run + pre[c];
+    cur[c] = run;
     run += tot[c];
+  }
+  if (d0 >= bins) return;
+  // the tiles in order: each tile's row of offsets, then its counts added
+  for (int t0 = 0; t0 < n_tiles; t0 += 8) {
+    if (vec) {
+      uint4 xx[8][2];
+      seg_load8(hist, t0, n_tiles, d0, xx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (t0 + j < n_tiles) {
+          int4* o = reinterpret_cast<int4*>(offs + (int64_t)(t0 + j) * kSegBins + d0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = make_int4(cur[4 * q], cur[4 * q + 1], cur[4 * q + 2], cur[4 * q + 3]);
+#pragma unroll
+          for (int c = 0; c < PER; ++c) cur[c] += seg_u16(xx[j], c);
+        }
+      }
+    } else {
+      for (int t = t0; t < n_tiles && t < t0 + 8; ++t)
+        for (int c = 0; c < PER && d0 + c < bins; ++c) {
+          offs[(int64_t)t * kSegBins + d0 + c] = cur[c];
+          cur[c] += hist[(int64_t)t * kSegBins + d0 + c];
+        }
+    }
   }
 }
 
@@ -977,20 +1023,31 @@ __device__ __forceinline__ void seg_rank(const uint32_t (&dig)[kSegKPL], uint32_
   __syncthreads();
 }
 
+// the tile's row of digit offsets into LDS (16 KB, one round trip)
+__device__ __forceinline__ void seg_stage_offs(const int32_t* __restrict__ offs, int bins,
+                                               int32_t* __restrict__ doff) {
+  const int d0 = threadIdx.x * 16;
+  if (d0 + 16 <= bins) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      reinterpret_cast<int4*>(doff + d0)[q] = reinterpret_cast<const int4*>(offs + d0)[q];
+  } else {
+    for (int d = d0; d < bins && d < d0 + 16; ++d) doff[d] = offs[d];
+  }
+}
+
 template <bool ID64>
 __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs a) {
   __shared__ uint16_t wcnt[4][kSegBins];
   __shared__ int32_t doff[kSegBins];
-  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
-  __shared__ int32_t wsum[4], wsent[4];
+  __shared__ int32_t wsent[4];
   int s, t;
   seg_tile0(a, s, t);
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   const int bins = 1 << sl.w0;
   uint32_t id[kSegKPL], live = 0u, sent = 0u;
-  {  // the histogram pass's keys (bit 31: sentinel), past the tile's end neither — issued first,
-     // so they arrive while the slot starts and digit offsets are formed
+  {  // the histogram pass's keys (bit 31: sentinel), past the tile's end neither
     const int64_t b0 = (int64_t)t * kSegTile;
     const int tn = (int)(a.B - b0 < kSegTile ? a.B - b0 : kSegTile);
     const int w0 = (threadIdx.x >> 6) * 64 * kSegKPL + (threadIdx.x & 63);
@@ -1004,18 +1061,15 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
       else if (in) live |= 1u << k;
     }
   }
-  __shared__ int32_t spre;
-  seg_slot_starts(a, s, t, vstart, sstart, &spre);
-  const int32_t n_valid = vstart[a.n_slots];
-  const int32_t sent_pre = spre;  // sentinels of this slot's earlier tiles
-  seg_digit_offsets(a.hist0 + (int64_t)s * a.tiles * kSegBins, a.tiles, t, bins, vstart[s], doff,
-                    wsum);
+  seg_stage_offs(a.offs0 + ((int64_t)s * a.tiles + t) * kSegBins, bins, doff);
+  const int32_t n_valid = a.starts[a.n_slots];
+  const int32_t sent_base = n_valid + a.starts[kSegMaxSlots + 1 + s] + a.spre[s * a.tiles + t];
   uint32_t dig[kSegKPL];
   const uint32_t mask = (uint32_t)bins - 1u;
 #pragma unroll
   for (int k = 0; k < kSegKPL; ++k) dig[k] = id[k] & mask;
   int32_t rank[kSegKPL];
-  seg_rank(dig, live, wcnt, bins, rank);
+  seg_rank(dig, live, wcnt, bins, rank);  // its block barriers also publish doff
   // sentinel ranks: waves in order, lanes in order
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt64();
@@ -1029,7 +1083,7 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
   }
   if (lane == 0) wsent[wave] = srun;
   __syncthreads();
-  int32_t sbase = n_valid + sstart[s] + sent_pre;
+  int32_t sbase = sent_base;
   for (int w = 0; w < wave; ++w) sbase += wsent[w];
   const bool final_pass = sl.w1 == 0;
 #pragma unroll
@@ -1052,11 +1106,11 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
   }
 }
 
-// pass 1 (slots wider than 12 bits): tile t of slot s = tmp[vstart[s] + 4096 t ..) (its valid ids
-// in pass-0 order), digit = id >> w0
-__device__ __forceinline__ void seg_load1(const SegArgs& a, const SegSlot& sl, int32_t start,
-                                          int32_t n_s, int t, uint32_t (&id)[kSegKPL],
-                                          int32_t (&pos)[kSegKPL], uint32_t& live) {
+// pass 1 (slots wider than 12 bits): tile t of slot s = tmp[start + 4096 t ..) (its valid ids in
+// pass-0 order), digit = id >> w0
+__device__ __forceinline__ void seg_load1(const SegArgs& a, int32_t start, int32_t n_s, int t,
+                                          uint32_t (&id)[kSegKPL], int32_t (&pos)[kSegKPL],
+                                          uint32_t& live) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   live = 0u;
 #pragma unroll
@@ -1075,29 +1129,22 @@ __device__ __forceinline__ void seg_load1(const SegArgs& a, const SegSlot& sl, i
 
 __global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a) {
   __shared__ int32_t cnt[kSegBins];
-  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
   int s, t;
   seg_tile1(a, s, t);
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   if (sl.w1 == 0) return;
-  __shared__ int32_t spre;
-  seg_slot_starts(a, s, t, vstart, sstart, &spre);
-  const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
+  const int32_t start = a.starts[s], n_s = a.starts[s + 1] - start;
+  if (t * kSegTile >= n_s) return;
   const int bins = 1 << sl.w1;
-  for (int d = threadIdx.x; d < bins; d += blockDim.x) cnt[d] = 0;
-  __syncthreads();
   uint32_t id[kSegKPL], live;
   int32_t pos[kSegKPL];
-  seg_load1(a, sl, start, n_s, t, id, pos, live);
-  const uint64_t lt = lanemask_lt64();
+  seg_load1(a, start, n_s, t, id, pos, live);
+  for (int d = threadIdx.x; d < bins; d += blockDim.x) cnt[d] = 0;
+  __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kSegKPL; ++k) {
-    const bool lv = (live >> k) & 1u;
-    const uint32_t d = id[k] >> sl.w0;
-    const uint64_t m = match_digit<kSegBits>(d, lv);
-    if (lv && (m & lt) == 0) atomicAdd(&cnt[d], __popcll(m));
-  }
+  for (int k = 0; k < kSegKPL; ++k)
+    if ((live >> k) & 1u) atomicAdd(&cnt[id[k] >> sl.w0], 1);
   __syncthreads();
   seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins, cnt, bins);
 }
@@ -1105,24 +1152,18 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a)
 __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs a) {
   __shared__ uint16_t wcnt[4][kSegBins];
   __shared__ int32_t doff[kSegBins];
-  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
-  __shared__ int32_t wsum[4];
   int s, t;
   seg_tile1(a, s, t);
   if (s >= a.n_slots || t >= a.tiles) return;
   const SegSlot sl = seg_slot(a, s);
   if (sl.w1 == 0) return;
-  __shared__ int32_t spre;
-  seg_slot_starts(a, s, t, vstart, sstart, &spre);
-  const int32_t start = vstart[s], n_s = vstart[s + 1] - vstart[s];
-  const int n_tiles_s = (n_s + kSegTile - 1) / kSegTile;
-  if (t >= n_tiles_s) return;  // uniform per block: after the block-wide syncs above
+  const int32_t start = a.starts[s], n_s = a.starts[s + 1] - start;
+  if (t * kSegTile >= n_s) return;
   const int bins = 1 << sl.w1;
-  seg_digit_offsets(a.hist1 + (int64_t)s * a.tiles * kSegBins, n_tiles_s, t, bins, start, doff,
-                    wsum);
   uint32_t id[kSegKPL], live;
   int32_t pos[kSegKPL];
-  seg_load1(a, sl, start, n_s, t, id, pos, live);
+  seg_load1(a, start, n_s, t, id, pos, live);
+  seg_stage_offs(a.offs1 + ((int64_t)s * a.tiles + t) * kSegBins, bins, doff);
   uint32_t dig[kSegKPL];
 #pragma unroll
   for (int k = 0; k < kSegKPL; ++k) dig[k] = id[k] >> sl.w0;
@@ -1140,18 +1181,27 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
 }
 
 static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArgs* a) {
-  uint32_t* k0 = c.take<uint32_t>((size_t)n_slots * tiles * kSegTile);
-  uint16_t* h0 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
-  uint16_t* h1 = c.take<uint16_t>((size_t)n_slots * tiles * kSegBins);
-  int32_t* v = c.take<int32_t>((size_t)n_slots * tiles);
-  int32_t* z = c.take<int32_t>((size_t)n_slots * tiles);
+  const size_t nt = (size_t)n_slots * tiles;
+  uint32_t* k0 = c.take<uint32_t>(nt * kSegTile);
+  uint16_t* h0 = c.take<uint16_t>(nt * kSegBins);
+  uint16_t* h1 = c.take<uint16_t>(nt * kSegBins);
+  int32_t* o0 = c.take<int32_t>(nt * kSegBins);
+  int32_t* o1 = c.take<int32_t>(nt * kSegBins);
+  int32_t* v = c.take<int32_t>(nt);
+  int32_t* z = c.take<int32_t>(nt);
+  int32_t* sp = c.take<int32_t>(nt);
+  int32_t* st = c.take<int32_t>(2 * (kSegMaxSlots + 1));
   uint2* tmp = c.take<uint2>(n);
   if (a) {
     a->keys0 = k0;
     a->hist0 = h0;
     a->hist1 = h1;
+    a->offs0 = o0;
+    a->offs1 = o1;
     a->vcnt = v;
     a->scnt = z;
+    a->spre = sp;
+    a->starts = st;
     a->tmp = tmp;
   }
   return c.off;
@@ -1169,12 +1219,19 @@ static bool seg_eligible(int64_t n_ids, int n_slots, int world, int64_t max_slot
 size_t seg_ws_size(int64_t n_ids) {
   // tiles over all slots <= n/4096 + n_slots (each slot rounds up once)
   const int64_t tiles_total = n_ids / kSegTile + kSegMaxSlots;
+  SegArgs a{};
   Carver c(nullptr, 0);
-  c.take<uint32_t>((size_t)tiles_total * kSegTile);
-  c.take<uint16_t>((size_t)tiles_total * kSegBins);
-  c.take<uint16_t>((size_t)tiles_total * kSegBins);
-  c.take<int32_t>((size_t)tiles_total);
-  c.take<int32_t>((size_t)tiles_total);
+  (void)a;
+  const size_t nt = (size_t)tiles_total;
+  c.take<uint32_t>(nt * kSegTile);
+  c.take<uint16_t>(nt * kSegBins);
+  c.take<uint16_t>(nt * kSegBins);
+  c.take<int32_t>(nt * kSegBins);
+  c.take<int32_t>(nt * kSegBins);
+  c.take<int32_t>(nt);
+  c.take<int32_t>(nt);
+  c.take<int32_t>(nt);
+  c.take<int32_t>(2 * (kSegMaxSlots + 1));
   c.take<uint2>(n_ids);
   return c.off + 1024;
 }
@@ -1208,11 +1265,15 @@ static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const 
   if (id_dtype == RS_ID_I64) slot_sort_hist0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_hist0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
+  slot_sort_scan_kernel<0><<<n_slots, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
   if (id_dtype == RS_ID_I64) slot_sort_scatter0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_scatter0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   // pass 1 only matters for slots wider than 12 bits; its blocks of narrower slots exit at once
   slot_sort_hist1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
+  RS_CHECK_LAUNCH();
+  slot_sort_scan_kernel<1><<<n_slots, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   slot_sort_scatter1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();

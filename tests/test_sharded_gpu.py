@@ -158,7 +158,9 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
         from recommender_amd.synthetic import criteo_batch, criteo_cardinalities
 
         MLP.factored_min_batch = 0
-        S, D, B, lr = 26, 128, 1024, 0.05
+        # global batch 2048 at every world size: the dense-half check's per-element bounds are
+        # stated for sums of that many examples
+        S, D, B, lr = 26, 128, 2048 // world, 0.05
         cards = criteo_cardinalities(200_000, S)
         V = sum(cards)
         so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
@@ -242,7 +244,7 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
 @pytest.mark.parametrize("world,spill", [(2, False), (2, True), (3, True), (4, False), (4, True)])
 def test_worldn_fused_dlrm_step_matches_oracle(world, spill):
     """TrainStep's fused DLRM step on a row-sharded slab at world 2 / 3 / 4 (gloo, all ranks on
-    the one GPU): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the
+    the one GPU; global batch 2048 split over the ranks): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the
     batch sums are all-reduced (the dense half of the global step); the owners apply the gradient
     rows. Two steps, slab bit-exact vs oracle/sharded.py fed with every rank's kernel rows after
     each; loss, the twelve MLP gradients (per-element bounds) and the SGD apply vs the oracle step
