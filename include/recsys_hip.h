@@ -204,6 +204,20 @@ int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows, const int32_
                                        int64_t n_rows, const int32_t* seg_map, uint32_t* uniq_rows,
                                        float* uniq_grad, void* workspace, size_t ws_bytes,
                                        void* stream);
+/* rs_embedding_dedup_grad_mapped over the keys in [key_lo, key_hi) only (segments numbered over
+ * the whole key space n_rows, so two calls over adjoining ranges emit exactly the segments one
+ * call does, with the same sums); seg_ready 1: the workspace already holds the segment ids of a
+ * previous call on the same sorted keys. D = 128 with 16-byte aligned rows (the group walk).
+ * The row-sharded step deduplicates its two owner halves apart, so the first half's gradient
+ * all-to-all runs while the second half is summed. */
+int32_t rs_embedding_dedup_grad_mapped_range(const uint32_t* sorted_rows, const int32_t* sorted_pos,
+                                             int64_t n_ids, const float* grad_out,
+                                             const float* row_scale, int32_t scale_group,
+                                             int32_t dim, int64_t n_rows, uint32_t key_lo,
+                                             uint32_t key_hi, int32_t seg_ready,
+                                             const int32_t* seg_map, uint32_t* uniq_rows,
+                                             float* uniq_grad, void* workspace, size_t ws_bytes,
+                                             void* stream);
 
 /* The deduplicated gradient as a dense [n_rows, dim] tensor: rows without ids 0, every other row
  * its segment sum (same additions, same order as rs_embedding_dedup_grad); dense is fully written.

@@ -191,6 +191,10 @@ struct ApplyArgs {
   // OPT_EMIT: segment s's sum goes to uniq_grad row seg_map[s] (skipped when < 0) instead of
   // row s (the row-sharded exchange's padded per-owner send buffer, rs_exchange_pack)
   const int32_t* seg_map;
+  // the D = 128 walk (tile32_walk) takes only keys in [key_lo, n_rows) as rows; the others are
+  // treated as the OOB sentinel (dropped). 0 = every key below n_rows (the row-sharded exchange
+  // deduplicates its two owner halves in two launches, rs_embedding_dedup_grad_mapped_range)
+  uint32_t key_lo;
   // OPT_DENSE: the gradient rows in up to 4 segments — position p in [gstart[i], gstart[i+1])
   // reads gseg[i] + (p - gstart[i]) * gld[i] (a table looked up several times hands each
   // lookup's upstream rows, strided column blocks included, without concatenating them);
@@ -446,9 +450,12 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   const int col = gl * VEC;
   // lane-parallel tile metadata
   const bool mine = gl < ne;
+  // a row of this walk: below n_rows and at or past a.key_lo (one unsigned compare)
+  const uint32_t klo = a.key_lo, kspan = n_rows - a.key_lo;
+  auto key_ok = [&](uint32_t k) { return k - klo < kspan; };
   const uint32_t kv = mine ? keys[k0 + gl] : 0xFFFFFFFFu;
   const int32_t pv = mine ? pos[k0 + gl] : 0;
-  const bool lv = mine && kv < n_rows;
+  const bool lv = mine && key_ok(kv);
   const float sv = (a.row_scale && lv) ? a.row_scale[pv / a.scale_group] : 1.f;
   const uint32_t key_before = k0 > 0 ? keys[k0 - 1] : 0xFFFFFFFFu;
   const uint32_t key_after = k1 < n ? keys[k1] : 0xFFFFFFFEu;
@@ -480,7 +487,7 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
     for (int u = 0; u < U; ++u) {
       const int e = b0 + u;
       const int32_t p = __shfl(pv, e, 32);
-      const bool live = e < ne && key_of(e) < n_rows;
+      const bool live = e < ne && key_ok(key_of(e));
       if (live) {
         load_stream<VEC>(grad + (int64_t)p * dim + col, r[u]);
       } else {
@@ -516,7 +523,7 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
     }
   };
   auto emit = [&](uint32_t row, bool starts, bool ends, int head_e) {
-    if (row >= n_rows) return;  // OOB sentinel run: gradient dropped
+    if (!key_ok(row)) return;  // OOB sentinel (or out-of-range) run: gradient dropped
     if (starts && ends) {
       if constexpr (kPre) {
         bool done = false;
@@ -599,9 +606,9 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   flush();
   Tile32Edges ed;
   ed.last_row = run_row;
-  ed.last_open = !ends && run_starts && run_row < n_rows;
+  ed.last_open = !ends && run_starts && key_ok(run_row);
   ed.first_key = key_of(0);
-  ed.first_cont = k0 > 0 && ed.first_key < n_rows && key_before == ed.first_key;
+  ed.first_cont = k0 > 0 && key_ok(ed.first_key) && key_before == ed.first_key;
   return ed;
 }
 
@@ -1164,6 +1171,10 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #else
   const bool g32 = false;
 #endif
+  if (a.key_lo && !g32) {
+    set_error("a key range needs the D = 128 group walk (16-byte aligned rows)");
+    return RS_E_UNSUPPORTED;
+  }
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     if (g32) {                                                                                  \
@@ -1319,6 +1330,12 @@ extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
                                         workspace, ws_bytes, stream);
 }
 
+extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
+    const uint32_t* sorted_rows, const int32_t* sorted_pos, int64_t n_ids, const float* grad_out,
+    const float* row_scale, int32_t scale_group, int32_t dim, int64_t n_rows, uint32_t key_lo,
+    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_map, uint32_t* uniq_rows,
+    float* uniq_grad, void* workspace, size_t ws_bytes, void* stream);
+
 extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
                                                   const int32_t* sorted_pos, int64_t n_ids,
                                                   const float* grad_out, const float* row_scale,
@@ -1326,7 +1343,19 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
                                                   const int32_t* seg_map, uint32_t* uniq_rows,
                                                   float* uniq_grad, void* workspace,
                                                   size_t ws_bytes, void* stream) {
+  return rs_embedding_dedup_grad_mapped_range(sorted_rows, sorted_pos, n_ids, grad_out, row_scale,
+                                              scale_group, dim, n_rows, 0u, (uint32_t)n_rows, 0,
+                                              seg_map, uniq_rows, uniq_grad, workspace, ws_bytes,
+                                              stream);
+}
+
+extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
+    const uint32_t* sorted_rows, const int32_t* sorted_pos, int64_t n_ids, const float* grad_out,
+    const float* row_scale, int32_t scale_group, int32_t dim, int64_t n_rows, uint32_t key_lo,
+    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_map, uint32_t* uniq_rows,
+    float* uniq_grad, void* workspace, size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
+  RS_CHECK_ARG(key_lo < key_hi && (int64_t)key_hi <= n_rows, "key range outside [0, n_rows)");
   RS_CHECK_ARG(!row_scale || scale_group >= 1, "scale_group must be >= 1");
   if (n_ids == 0) return RS_OK;
   RS_CHECK_ARG(sorted_rows && sorted_pos && grad_out && uniq_rows && uniq_grad, "null pointer");
@@ -1340,10 +1369,12 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
   int32_t* seg = c.take<int32_t>(n_ids);
   void* scan_ws = c.take<char>(exclusive_scan_ws_size(n_ids));
   int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
-  head_flags_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, seg);
-  RS_CHECK_LAUNCH();
-  int32_t s = exclusive_scan_i32(seg, seg, n_ids, nullptr, scan_ws, exclusive_scan_ws_size(n_ids), st);
-  if (s) return s;
+  if (!seg_ready) {  // segment ids over the whole key space (a second range call reuses them)
+    head_flags_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, seg);
+    RS_CHECK_LAUNCH();
+    int32_t s = exclusive_scan_i32(seg, seg, n_ids, nullptr, scan_ws, exclusive_scan_ws_size(n_ids), st);
+    if (s) return s;
+  }
   ApplyArgs a{};
   a.dim = dim;
   a.partial = partial;
@@ -1355,9 +1386,10 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
   a.row_scale = row_scale;
   a.scale_group = scale_group;
   a.seg_map = seg_map;
+  a.key_lo = key_lo;
   const void* ptrs[2] = {grad_out, uniq_grad};
   RowGeom geom = row_geom(dim, ptrs, 2);
-  return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, n_rows, grad_out, a, geom, st);
+  return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, key_hi, grad_out, a, geom, st);
 }
 
 extern "C" int32_t rs_embedding_grad_dense(const uint32_t* sorted_rows, const int32_t* sorted_pos,

@@ -52,19 +52,22 @@ class Comm:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
-        """Splits None: equal blocks (the sharded slab's capacity-bounded exchange)."""
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None,
+                   async_op: bool = False):
+        """Splits None: equal blocks (the sharded slab's capacity-bounded exchange). async_op
+        (RCCL): returns the work handle instead of ordering the current stream after it (gloo
+        rehearsals stage through the host and return None)."""
         if self.world == 1:
             out.copy_(inp)
-            return
+            return None
         osp = None if out_splits is None else list(out_splits)
         isp = None if in_splits is None else list(in_splits)
         if self.staged:
             o = torch.empty(out.shape, dtype=out.dtype)
             dist.all_to_all_single(o, inp.cpu(), osp, isp, group=self.group)
             out.copy_(o)
-        else:
-            dist.all_to_all_single(out, inp, osp, isp, group=self.group)
+            return None
+        return dist.all_to_all_single(out, inp, osp, isp, group=self.group, async_op=async_op)
 
     def all_reduce_(self, t: torch.Tensor, op=None):
         if self.world == 1:
@@ -133,6 +136,9 @@ class ShardedSlabEmbedding(nn.Module):
         self.capacity = capacity
         self.capacity_factor = float(capacity_factor)
         self.spill_rounds = 0  # steps that exchanged rows past the capacity (a spill round)
+        # the backward's dedup + gradient all-to-all in two owner halves (D = 128): the first
+        # half's all-to-all runs while the second half is summed (RCCL); False: one of each
+        self.split_halves = True
 
     @property
     def n_slots(self):
@@ -327,16 +333,44 @@ class ShardedSlabEmbedding(nn.Module):
             g = grad_rows.contiguous()
             send_grad = torch.empty(W * (C + C2), D, dtype=torch.float32, device=dev)
             uniq_rows = torch.empty(max(s.n, 1), dtype=torch.int32, device=dev)
-            if s.n:
-                w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(s.n, D), dev)
-                if row_scale is not None and row_scale.numel() * self.n_slots != s.n:
-                    raise ValueError("row_scale must hold one value per example")
-                L.call("rs_embedding_dedup_grad_mapped", L.ptr(s.rows), L.ptr(s.pos), s.n,
-                       L.ptr(g), L.ptr(row_scale), self.n_slots if row_scale is not None else 1,
-                       D, self.key_space, L.ptr(st["slot_of"]), L.ptr(uniq_rows),
-                       L.ptr(send_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
             recv_grad = torch.empty(W * (C + C2), D, dtype=torch.float32, device=dev)
-            self.comm.all_to_all(recv_grad[: W * C], send_grad[: W * C])
+            if row_scale is not None and row_scale.numel() * self.n_slots != s.n:
+                raise ValueError("row_scale must hold one value per example")
+            w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(max(s.n, 1), D), dev)
+
+            def dedup(lo, hi, seg_ready):
+                if s.n:
+                    L.call("rs_embedding_dedup_grad_mapped_range", L.ptr(s.rows), L.ptr(s.pos),
+                           s.n, L.ptr(g), L.ptr(row_scale),
+                           self.n_slots if row_scale is not None else 1, D, self.key_space, lo,
+                           hi, seg_ready, L.ptr(st["slot_of"]), L.ptr(uniq_rows),
+                           L.ptr(send_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
+
+            if W >= 2 and D == 128 and self.split_halves:
+                # owner halves [0, W/2) and [W/2, W): keys are owner-major, so half A's rows are
+                # the keys below (W/2)·stride. Each half: its dedup, then an all-to-all in which
+                # only that half's owners receive (every rank sends them C rows); with RCCL the
+                # first all-to-all runs while the second half is summed
+                h = W // 2
+                K = h * self.stride
+                mine_a = self.rank < h
+                none = torch.empty(0, D, dtype=torch.float32, device=dev)
+                dedup(0, K, 0)
+                work_a = self.comm.all_to_all(recv_grad[: W * C] if mine_a else none,
+                                              send_grad[: h * C],
+                                              [C] * W if mine_a else [0] * W,
+                                              [C] * h + [0] * (W - h), async_op=True)
+                dedup(K, self.key_space, 1)
+                work_b = self.comm.all_to_all(none if mine_a else recv_grad[: W * C],
+                                              send_grad[h * C: W * C],
+                                              [0] * W if mine_a else [C] * W,
+                                              [0] * h + [C] * (W - h), async_op=True)
+                for wk in (work_a, work_b):
+                    if wk is not None:
+                        wk.wait()
+            else:
+                dedup(0, self.key_space, 0)
+                self.comm.all_to_all(recv_grad[: W * C], send_grad[: W * C])
             recv_ids = st["recv_ids"]
             if C2 > 0:
                 self.comm.all_to_all(recv_grad[W * C:], send_grad[W * C:])
