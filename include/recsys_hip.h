@@ -157,8 +157,6 @@ int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_unique,
                          int64_t capacity, const int32_t* inverse, int64_t n_ids,
                          int32_t* send_ids, int32_t* slot_of_unique, int32_t* inverse_slot,
                          int32_t* overflow, void* stream);
-/* The owner's side of the exchange: out[i] = shard[ids[i]], a zero row where ids[i] < 0
- * (padding) or out of range; no error flag (padding is expected). */
 /* The spill round of the capacity-bounded exchange (a batch with more unique rows for some owner
  * than the capacity): rs_exchange_excess writes max_o max(0, owner_counts[o] - capacity) (int64,
  * device) — all-reduced (MAX) over the ranks it is the spill capacity C2; rs_exchange_pack_spill
@@ -173,8 +171,28 @@ int32_t rs_exchange_pack_spill(const uint32_t* uniq_keys, const int32_t* n_uniqu
                                int64_t capacity, int64_t spill_capacity, const int32_t* inverse,
                                int64_t n_ids, int32_t* spill_ids, int32_t* slot_of_unique,
                                int32_t* inverse_slot, int32_t* overflow, void* stream);
+/* The owner's side of the exchange: out[i] = shard[ids[i]], a zero row where ids[i] < 0
+ * (padding) or out of range; no error flag (padding is expected). */
 int32_t rs_gather_rows_padded(const float* shard, int64_t n_rows, int32_t dim, const int32_t* ids,
                               int64_t n, float* out, void* stream);
+/* Rows a step ahead (recommender_amd/sharded.py): the next step's rows are gathered and sent
+ * while the current step runs, and only the rows the current step updates are sent again after
+ * its apply. rs_exchange_classify (owner): of the requested slots recv_ids[world*capacity]
+ * (owner-local rows, -1 = padding), those whose row has stamp[row] == pred_seq (requested by
+ * the previous step) are listed per requester r: late_rows[r*capacity + k] = the row,
+ * late_slot[r*capacity + k] = its slot in r's block, late_count[r] = the count (the rest of
+ * late_rows / late_slot is -1; list order is not fixed run to run); then stamp[row] = seq for
+ * every requested row. rs_exchange_scatter_late (requester): for the [world, late_capacity]
+ * block of late rows received from the owners and each owner's late_slot block
+ * recv_slot[world*capacity], rows[o*capacity + recv_slot[o*capacity + k]] =
+ * recv_rows[o*late_capacity + k] (slot -1 skipped). dim % 4 == 0, 16-byte aligned rows. */
+int32_t rs_exchange_classify(const int32_t* recv_ids, int32_t world, int64_t capacity,
+                             int32_t* stamp, int64_t n_rows, int32_t pred_seq, int32_t seq,
+                             int32_t* late_rows, int32_t* late_slot, int32_t* late_count,
+                             void* stream);
+int32_t rs_exchange_scatter_late(const float* recv_rows, const int32_t* recv_slot, int32_t world,
+                                 int64_t capacity, int64_t late_capacity, int32_t dim, float* rows,
+                                 void* stream);
 
 /* a-2 (part 2) deduplicated gradient: uniq_rows[u], uniq_grad[u, dim] for the n_unique
  * distinct valid rows (count from rs_sort_ids), uniq_grad[u] = Σ grad_out[p] over the

@@ -135,9 +135,119 @@ __global__ __launch_bounds__(256) void gather_padded_kernel(const float* __restr
   }
 }
 
+// The owner's side of the rows-ahead exchange: the next step's requested slots (recv_ids, a
+// [world, cap] block per requester) whose row the previous step requested too (stamp[row] ==
+// pred: those rows change in the previous step's apply) are listed per requester —
+// late_rows[r·cap + k] = the local row, late_slot[r·cap + k] = its slot in r's block, late_cnt[r]
+// = k's bound — and re-sent after that apply; every other slot's row is final when gathered a
+// step early. Waves compact with a ballot per requester (a wave may straddle two blocks) and
+// one atomic per (wave, requester), so the list order varies run to run, the rows it carries do
+// not.
+__global__ __launch_bounds__(256) void exchange_classify_kernel(
+    const int32_t* __restrict__ recv_ids, int64_t n, int64_t cap, const int32_t* __restrict__ stamp,
+    int64_t n_rows, int32_t pred, int32_t* __restrict__ late_rows, int32_t* __restrict__ late_slot,
+    int32_t* __restrict__ late_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_pad = (n + 63) & ~int64_t(63);  // whole waves take every ballot
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t r = -1;
+    if (i < n) r = recv_ids[i];
+    const bool hit = r >= 0 && r < n_rows && stamp[r] == pred;
+    const int64_t o = i / cap;
+    uint64_t pending = __ballot(hit);
+    while (pending) {
+      const int leader = __ffsll((unsigned long long)pending) - 1;
+      const int64_t ol = __shfl(o, leader);
+      const bool mine = hit && o == ol;
+      const uint64_t same = __ballot(mine);
+      int32_t base = 0;
+      if (lane == leader) base = atomicAdd(late_cnt + ol, __popcll(same));
+      base = __shfl(base, leader);
+      if (mine) {
+        const int32_t k = base + __popcll(same & ((uint64_t(1) << lane) - 1));
+        late_rows[ol * cap + k] = r;
+        late_slot[ol * cap + k] = (int32_t)(i - ol * cap);
+      }
+      pending &= ~same;
+    }
+  }
+}
+
+// stamp[row] = seq for every requested row (run after the classify of the same step)
+__global__ __launch_bounds__(256) void exchange_mark_kernel(const int32_t* __restrict__ recv_ids,
+                                                            int64_t n, int32_t* __restrict__ stamp,
+                                                            int64_t n_rows, int32_t seq) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = recv_ids[i];
+    if (r >= 0 && r < n_rows) stamp[r] = seq;
+  }
+}
+
+// the requester's side: late row k of owner o (recv[o·cap_late + k]) overwrites its slot
+// o·cap + slot[o·cap + k] of the rows gathered a step early; slot −1 is padding
+__global__ __launch_bounds__(256) void exchange_scatter_late_kernel(
+    const float* __restrict__ recv, const int32_t* __restrict__ slot, int world, int64_t cap,
+    int64_t cap_late, int dim, float* __restrict__ rows) {
+  const int lanes = 32, per_block = 256 / lanes;
+  const int sub = threadIdx.x / lanes, l = threadIdx.x % lanes;
+  const int64_t n = (int64_t)world * cap_late;
+  for (int64_t e = blockIdx.x * (int64_t)per_block + sub; e < n;
+       e += (int64_t)gridDim.x * per_block) {
+    const int64_t o = e / cap_late, k = e - o * cap_late;
+    const int32_t j = slot[o * cap + k];
+    if (j < 0) continue;
+    const float4* src = reinterpret_cast<const float4*>(recv + e * dim);
+    float4* dst = reinterpret_cast<float4*>(rows + (o * cap + j) * dim);
+    for (int c = l; c < dim / 4; c += lanes) dst[c] = src[c];
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
+
+extern "C" int32_t rs_exchange_classify(const int32_t* recv_ids, int32_t world, int64_t capacity,
+                                        int32_t* stamp, int64_t n_rows, int32_t pred_seq,
+                                        int32_t seq, int32_t* late_rows, int32_t* late_slot,
+                                        int32_t* late_count, void* stream) {
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity > 0 && n_rows >= 0, "bad sizes");
+  RS_CHECK_ARG((int64_t)world * capacity < (int64_t(1) << 31), "world x capacity out of range");
+  RS_CHECK_ARG(recv_ids && stamp && late_rows && late_slot && late_count, "null pointer");
+  RS_CHECK_ARG(seq != pred_seq, "seq must differ from pred_seq");
+  hipStream_t st = as_stream(stream);
+  const int64_t n = (int64_t)world * capacity;
+  RS_CHECK_HIP(hipMemsetAsync(late_rows, 0xFF, (size_t)n * sizeof(int32_t), st));
+  RS_CHECK_HIP(hipMemsetAsync(late_slot, 0xFF, (size_t)n * sizeof(int32_t), st));
+  RS_CHECK_HIP(hipMemsetAsync(late_count, 0, (size_t)world * sizeof(int32_t), st));
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+  exchange_classify_kernel<<<blocks, 256, 0, st>>>(recv_ids, n, capacity, stamp, n_rows, pred_seq,
+                                                   late_rows, late_slot, late_count);
+  RS_CHECK_LAUNCH();
+  exchange_mark_kernel<<<blocks, 256, 0, st>>>(recv_ids, n, stamp, n_rows, seq);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
+extern "C" int32_t rs_exchange_scatter_late(const float* recv_rows, const int32_t* recv_slot,
+                                            int32_t world, int64_t capacity, int64_t late_capacity,
+                                            int32_t dim, float* rows, void* stream) {
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity > 0, "bad sizes");
+  RS_CHECK_ARG(late_capacity >= 0 && late_capacity <= capacity, "late capacity out of range");
+  RS_CHECK_ARG(dim > 0 && (dim & 3) == 0, "dim must be a multiple of 4");
+  if (late_capacity == 0) return RS_OK;
+  RS_CHECK_ARG(recv_rows && recv_slot && rows, "null pointer");
+  RS_CHECK_ARG(((reinterpret_cast<uintptr_t>(recv_rows) | reinterpret_cast<uintptr_t>(rows)) & 15) == 0,
+               "rows must be 16-byte aligned");
+  const int64_t n = (int64_t)world * late_capacity;
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 8), 4096);
+  exchange_scatter_late_kernel<<<blocks, 256, 0, as_stream(stream)>>>(recv_rows, recv_slot, world,
+                                                                      capacity, late_capacity, dim,
+                                                                      rows);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
 
 extern "C" int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_unique,
                                     const int32_t* owner_counts, int32_t world, int64_t shard_stride,
@@ -164,7 +274,7 @@ extern "C" int32_t rs_exchange_pack(const uint32_t* uniq_keys, const int32_t* n_
 
 extern "C" int32_t rs_exchange_excess(const int32_t* owner_counts, int32_t world, int64_t capacity,
                                       int64_t* excess, void* stream) {
-  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity > 0, "bad sizes");
+  RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity >= 0, "bad sizes");
   RS_CHECK_ARG(owner_counts && excess, "null pointer");
   exchange_excess_kernel<<<1, 64, 0, as_stream(stream)>>>(owner_counts, world, capacity, excess);
   RS_CHECK_LAUNCH();

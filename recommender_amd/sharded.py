@@ -139,6 +139,16 @@ class ShardedSlabEmbedding(nn.Module):
         # the backward's dedup + gradient all-to-all in two owner halves (D = 128): the first
         # half's all-to-all runs while the second half is summed (RCCL); False: one of each
         self.split_halves = True
+        # rows a step ahead (world > 1, SGD / lazy Adam): a prefetched step's capacity block is
+        # gathered and sent while the step before it runs; after that step's apply only the rows
+        # it updated (the ones both steps request, per owner stamps) are sent again
+        self.rows_ahead = True
+        self.rows_ahead_modes = {"fresh": 0, "late": 0, "full": 0}
+        self._stamp = None  # int32 per local row: the last step (seq) that requested it
+        self._seq = 0  # exchange_begin count
+        self._marked = -1  # the last seq whose requested rows were stamped
+        self._apply_count = 0
+        self._last_applied = (0, 0)  # (seq, spill size) of the last applied step
 
     @property
     def n_slots(self):
@@ -202,19 +212,66 @@ class ShardedSlabEmbedding(nn.Module):
             L.call("rs_exchange_pack", L.ptr(uniq), L.ptr(n_unique), L.ptr(counts), W,
                    self.stride, C, L.ptr(inverse), n, L.ptr(send_ids), L.ptr(slot_of),
                    L.ptr(inv_slot), L.ptr(overflow), L.stream_ptr(dev))
-            # the spill round's size: every rank's largest excess over C, all-reduced (MAX)
-            excess = torch.empty(1, dtype=torch.int64, device=dev)
+            recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
+            self.comm.all_to_all(recv_ids, send_ids)
+            self._seq += 1
+            seq = self._seq
+            ahead = self._rows_ahead_ok()
+            # all-reduced (MAX) over the ranks: [0] the spill round's size (every rank's largest
+            # excess over C), [1] with rows ahead the late round's size (the most rows one owner
+            # re-sends one requester after the previous step's apply)
+            excess = torch.empty(2 if ahead else 1, dtype=torch.int64, device=dev)
             L.call("rs_exchange_excess", L.ptr(counts), W, C, L.ptr(excess), L.stream_ptr(dev))
+            late = None
+            if ahead:
+                if self._stamp is None:
+                    self._stamp = torch.zeros(max(self.shard.input_dim, 1), dtype=torch.int32,
+                                              device=dev)
+                late_rows = torch.empty(W * C, dtype=torch.int32, device=dev)
+                late_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
+                late_cnt = torch.empty(W, dtype=torch.int32, device=dev)
+                L.call("rs_exchange_classify", L.ptr(recv_ids), W, C, L.ptr(self._stamp),
+                       self.shard.input_dim, seq - 1, seq, L.ptr(late_rows), L.ptr(late_slot),
+                       L.ptr(late_cnt), L.stream_ptr(dev))
+                L.call("rs_exchange_excess", L.ptr(late_cnt), W, 0, L.ptr(excess[1:]),
+                       L.stream_ptr(dev))
+                recv_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
+                self.comm.all_to_all(recv_slot, late_slot)
+                # the classify is against the previous step's stamps only if that step marked
+                late = (late_rows, recv_slot, self._marked == seq - 1)
+                self._marked = seq
             self.comm.all_reduce_(excess, dist.ReduceOp.MAX)
-            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            host = torch.empty(excess.numel(), dtype=torch.int64, pin_memory=True)
             host.copy_(excess, non_blocking=True)
             excess_ready = torch.cuda.Event()
             excess_ready.record(self.side)
-            recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
-            self.comm.all_to_all(recv_ids, send_ids)
         return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, recv_ids=recv_ids,
                     capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
-                    inverse=inverse, excess=(excess_ready, host))
+                    inverse=inverse, excess=(excess_ready, host), seq=seq, late=late, early=None)
+
+    def _rows_ahead_ok(self) -> bool:
+        """Rows a step ahead need an update that changes only the rows it receives (SGD, lazy
+        Adam; Keras Adam's dense decay moves every row) and rows of a multiple-of-4 width."""
+        opt = self.optimizer
+        return (self.rows_ahead and self.world > 1 and self.output_dim % 4 == 0
+                and opt is not None and opt.kind in (L.RS_OPT_SGD, L.RS_OPT_LAZY_ADAM))
+
+    def _gather_send(self, ids: torch.Tensor, out: torch.Tensor):
+        """Owners gather the requested rows (padding slots read zero rows) and send them back:
+        out[...] = the rows this rank asked for, in its slot order. On the side stream."""
+        dev = out.device
+        served = torch.empty_like(out)
+        L.call("rs_gather_rows_padded", L.ptr(self.shard.weight), self.shard.input_dim,
+               self.output_dim, L.ptr(ids), ids.numel(), L.ptr(served), L.stream_ptr(dev))
+        self.comm.all_to_all(out, served)
+
+    def _issue_early(self, st):
+        """The capacity block's rows, gathered now: final for every row the steps applied in
+        between leave alone; exchange_finish re-sends the rest (on the side stream)."""
+        W, C = self.world, st["capacity"]
+        rows = torch.empty(W * C, self.output_dim, device=st["dev"])
+        self._gather_send(st["recv_ids"], rows)
+        st["early"] = (rows, self._apply_count)
 
     def check_overflow(self, block: bool = True):
         """Kept for callers of the round-4 API: a batch past the capacity now takes a spill
@@ -264,10 +321,34 @@ class ShardedSlabEmbedding(nn.Module):
         D = self.output_dim
         ev, host = st["excess"]
         ev.synchronize()  # prefetched a step ahead: long done
-        C2 = int(host.item())
+        C2 = int(host[0])
         n = st["ids"].numel()
         recv_spill = None
         with torch.cuda.stream(self.side):
+            if st["early"] is None:  # not issued ahead: gathered now, after every queued apply
+                self._issue_early(st)
+            rows_c, count0 = st["early"]
+            k = self._apply_count - count0
+            late = st["late"]
+            if k == 0:
+                mode = "fresh"  # no apply since the gather
+            elif (k == 1 and late is not None and late[2]
+                  and self._last_applied == (st["seq"] - 1, 0)):
+                mode = "late"  # one apply since, the previous step's, without a spill round
+            else:
+                mode = "full"
+            self.rows_ahead_modes[mode] += 1
+            if mode == "late":
+                C_late = int(host[1])
+                if C_late > 0:
+                    late_rows, recv_slot, _ = late
+                    ids_l = late_rows.view(W, C)[:, :C_late].contiguous()
+                    recv = torch.empty(W * C_late, D, device=dev)
+                    self._gather_send(ids_l, recv)
+                    L.call("rs_exchange_scatter_late", L.ptr(recv), L.ptr(recv_slot), W, C, C_late,
+                           D, L.ptr(rows_c), L.stream_ptr(dev))
+            elif mode == "full":
+                self._gather_send(st["recv_ids"], rows_c)
             if C2 > 0:
                 self.spill_rounds += 1
                 spill_ids = torch.empty(W * C2, dtype=torch.int32, device=dev)
@@ -277,22 +358,26 @@ class ShardedSlabEmbedding(nn.Module):
                        L.stream_ptr(dev))
                 recv_spill = torch.empty(W * C2, dtype=torch.int32, device=dev)
                 self.comm.all_to_all(recv_spill, spill_ids)
-            rows = torch.empty(W * (C + C2), D, device=dev)
-            for lo, hi, rid in ((0, W * C, st["recv_ids"]), (W * C, W * (C + C2), recv_spill)):
-                if hi == lo:
-                    continue
-                served = torch.empty(hi - lo, D, device=dev)
-                L.call("rs_gather_rows_padded", L.ptr(self.shard.weight), self.shard.input_dim, D,
-                       L.ptr(rid), hi - lo, L.ptr(served), L.stream_ptr(dev))
-                self.comm.all_to_all(rows[lo:hi], served)
-        main.wait_stream(self.side)
+                rows = torch.empty(W * (C + C2), D, device=dev)
+                rows[: W * C].copy_(rows_c)
+                self._gather_send(recv_spill, rows[W * C:])
+            else:
+                rows = rows_c
+            ready = torch.cuda.Event()
+            ready.record(self.side)
+            # the next prefetched step's rows, gathered and sent beside this step's train kernel
+            if self._prefetched:
+                nxt = self._prefetched[0][2]
+                if nxt["early"] is None and nxt["late"] is not None:
+                    self._issue_early(nxt)
+        main.wait_event(ready)
         inverse = st["inv_slot"][:n]
         for t in (rows, inverse):
             t.record_stream(main)
         self.view.weight = rows
         self.view.input_dim = W * (C + C2)
         self._st = dict(sorted=st["s"], slot_of=st["slot_of"], recv_ids=st["recv_ids"],
-                        recv_spill=recv_spill, capacity=C, spill=C2)
+                        recv_spill=recv_spill, capacity=C, spill=C2, seq=st["seq"])
         return self.view, inverse.view(st["ids"].shape)
 
     def exchange(self, ids: torch.Tensor):
@@ -392,6 +477,8 @@ class ShardedSlabEmbedding(nn.Module):
                     recv_grad.mul_(1.0 / self.world)
             # every owner applies (an owner no rank sent a row to still runs Keras' dense decay)
             opt.apply(self.shard, recv_ids, recv_grad, params, valid=valid)
+        self._apply_count += 1
+        self._last_applied = (st["seq"], C2)
         g.record_stream(self.side)
         if row_scale is not None:
             row_scale.record_stream(self.side)

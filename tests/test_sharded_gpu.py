@@ -137,11 +137,14 @@ def test_world2_sharded_embedding_matches_oracle(opt, even):
     assert all(v == "ok" for v in res.values()), res
 
 
-def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
+def _fused_dlrm_worldn_worker(rank, world, port, q, spill, prefetch):
     """The production fused DLRM step over a row-sharded slab, `world` ranks on the one GPU
-    (gloo): every check is against the oracle on the GLOBAL batch (all ranks' examples). Two
+    (gloo): every check is against the oracle on the GLOBAL batch (all ranks' examples). Three
     steps; `spill`: the second batch has uniform ids (many more unique rows than the capacity the
-    first, Zipf, batch calibrated), so its exchange takes the spill round — on the last step."""
+    first, Zipf, batch calibrated), so its exchange takes the spill round. `prefetch`: each
+    step's exchange is queued during the step before (TrainStep.prefetch), so its rows are
+    gathered a step early and only the rows the step before updates are sent again (rows ahead):
+    the later steps take that late round, or the full re-send after a spill round."""
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -173,7 +176,7 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
                      embedding_layer=emb)
         step = TrainStep(model, "sgd", lr=lr, comm=comm)
         steps = [[criteo_batch(np.random.default_rng(40 + 10 * k + r), B, cards) for r in range(world)]
-                 for k in range(2)]
+                 for k in range(3)]
         if spill:
             for r in range(world):
                 c2 = steps[1][r][0]
@@ -193,10 +196,12 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
 
         emb.backward_exchange = spy
         want = table
+        dev_batches = [tuple(torch.from_numpy(x).to(DEV) for x in per[rank]) for per in steps]
         for k, per in enumerate(steps):
-            cat, dn, lb = per[rank]
-            batch = tuple(torch.from_numpy(x).to(DEV) for x in (cat, dn, lb))
+            batch = dev_batches[k]
             assert step.fused_step_ready((batch[0], None, None))
+            if prefetch and k + 1 < len(steps):
+                step.prefetch(dev_batches[k + 1])
             loss = float(step(batch))
             emb.join()
             torch.cuda.synchronize()
@@ -232,6 +237,13 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
                 assert emb.spill_rounds == 0
         if spill:
             assert emb.spill_rounds == 1, emb.spill_rounds
+        modes = emb.rows_ahead_modes
+        if prefetch:
+            want_modes = {"fresh": 1, "late": 1, "full": 1} if spill else {"fresh": 1, "late": 2,
+                                                                           "full": 0}
+        else:
+            want_modes = {"fresh": 3, "late": 0, "full": 0}
+        assert modes == want_modes, modes
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover
         import traceback
@@ -241,21 +253,26 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,spill", [(2, False), (2, True), (3, True), (4, False), (4, True)])
-def test_worldn_fused_dlrm_step_matches_oracle(world, spill):
+@pytest.mark.parametrize("world,spill,prefetch", [(2, False, False), (2, True, True),
+                                                  (2, False, True), (3, True, False),
+                                                  (3, False, True), (4, False, False),
+                                                  (4, True, True)])
+def test_worldn_fused_dlrm_step_matches_oracle(world, spill, prefetch):
     """TrainStep's fused DLRM step on a row-sharded slab at world 2 / 3 / 4 (gloo, all ranks on
     the one GPU; global batch 2048 split over the ranks): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the
     batch sums are all-reduced (the dense half of the global step); the owners apply the gradient
     rows. Two steps, slab bit-exact vs oracle/sharded.py fed with every rank's kernel rows after
     each; loss, the twelve MLP gradients (per-element bounds) and the SGD apply vs the oracle step
-    on the global batch. `spill`: the last step's batch overflows the calibrated capacity and is
-    exchanged with the spill round — still bit-exact, on every rank."""
+    on the global batch. `spill`: the second step's batch overflows the calibrated capacity and
+    is exchanged with the spill round — still bit-exact, on every rank. `prefetch`: rows a step
+    ahead (each step's capacity block gathered during the step before, the rows that step
+    updated re-sent after its apply), the same bits."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29300 + (os.getpid() % 400) + 13 * world + (5 if spill else 0)
-    ps = [ctx.Process(target=_fused_dlrm_worldn_worker, args=(r, world, port, q, spill))
+    port = 29300 + (os.getpid() % 400) + 13 * world + (5 if spill else 0) + (7 if prefetch else 0)
+    ps = [ctx.Process(target=_fused_dlrm_worldn_worker, args=(r, world, port, q, spill, prefetch))
           for r in range(world)]
     for p in ps:
         p.start()
