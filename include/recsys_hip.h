@@ -177,17 +177,19 @@ int32_t rs_gather_rows_padded(const float* shard, int64_t n_rows, int32_t dim, c
                               int64_t n, float* out, void* stream);
 /* Rows a step ahead (recommender_amd/sharded.py): the next step's rows are gathered and sent
  * while the current step runs, and only the rows the current step updates are sent again after
- * its apply. rs_exchange_classify (owner): of the requested slots recv_ids[world*capacity]
- * (owner-local rows, -1 = padding), those whose row has stamp[row] == pred_seq (requested by
- * the previous step) are listed per requester r: late_rows[r*capacity + k] = the row,
- * late_slot[r*capacity + k] = its slot in r's block, late_count[r] = the count (the rest of
- * late_rows / late_slot is -1; list order is not fixed run to run); then stamp[row] = seq for
- * every requested row. rs_exchange_scatter_late (requester): for the [world, late_capacity]
- * block of late rows received from the owners and each owner's late_slot block
+ * its apply. rs_exchange_mark (owner): stamp[row] = seq for every requested row ids[i] >= 0
+ * of the step now finishing. rs_exchange_classify (owner): of the next step's requested slots
+ * recv_ids[world*capacity] (owner-local rows, -1 = padding), those with stamp[row] == pred_seq
+ * are listed per requester r: late_rows[r*capacity + k] = the row, late_slot[r*capacity + k] =
+ * its slot in r's block, late_count[r] = the count (the rest of late_rows / late_slot is -1;
+ * list order is not fixed run to run). rs_exchange_scatter_late (requester): for the [world,
+ * late_capacity] block of late rows received from the owners and each owner's late_slot block
  * recv_slot[world*capacity], rows[o*capacity + recv_slot[o*capacity + k]] =
  * recv_rows[o*late_capacity + k] (slot -1 skipped). dim % 4 == 0, 16-byte aligned rows. */
+int32_t rs_exchange_mark(const int32_t* ids, int64_t n, int32_t* stamp, int64_t n_rows,
+                         int32_t seq, void* stream);
 int32_t rs_exchange_classify(const int32_t* recv_ids, int32_t world, int64_t capacity,
-                             int32_t* stamp, int64_t n_rows, int32_t pred_seq, int32_t seq,
+                             const int32_t* stamp, int64_t n_rows, int32_t pred_seq,
                              int32_t* late_rows, int32_t* late_slot, int32_t* late_count,
                              void* stream);
 int32_t rs_exchange_scatter_late(const float* recv_rows, const int32_t* recv_slot, int32_t world,

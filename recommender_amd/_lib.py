@@ -81,7 +81,8 @@ _SIGS = {
     "rs_exchange_pack_spill": (_i32, [_p, _p, _p, _i32, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p,
                                       _p]),
     "rs_gather_rows_padded": (_i32, [_p, _i64, _i32, _p, _i64, _p, _p]),
-    "rs_exchange_classify": (_i32, [_p, _i32, _i64, _p, _i64, _i32, _i32, _p, _p, _p, _p]),
+    "rs_exchange_mark": (_i32, [_p, _i64, _p, _i64, _i32, _p]),
+    "rs_exchange_classify": (_i32, [_p, _i32, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
     "rs_exchange_scatter_late": (_i32, [_p, _p, _i32, _i64, _i64, _i32, _p, _p]),
     "rs_embedding_grad_dense": (_i32, [_p, _p, _i64, _p, _i32, _i64, _p, _p, _sz, _p]),
     "rs_embedding_grad_dense_segs": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _i64, _p, _p,

@@ -135,14 +135,13 @@ __global__ __launch_bounds__(256) void gather_padded_kernel(const float* __restr
   }
 }
 
-// The owner's side of the rows-ahead exchange: the next step's requested slots (recv_ids, a
-// [world, cap] block per requester) whose row the previous step requested too (stamp[row] ==
-// pred: those rows change in the previous step's apply) are listed per requester —
-// late_rows[r·cap + k] = the local row, late_slot[r·cap + k] = its slot in r's block, late_cnt[r]
-// = k's bound — and re-sent after that apply; every other slot's row is final when gathered a
-// step early. Waves compact with a ballot per requester (a wave may straddle two blocks) and
-// one atomic per (wave, requester), so the list order varies run to run, the rows it carries do
-// not.
+// The owner's side of the rows-ahead exchange: of the next step's requested slots (recv_ids, a
+// [world, cap] block per requester), those whose row the step now finishing requested too
+// (stamp[row] == pred: rows its apply changes) are listed per requester — late_rows[r·cap + k]
+// = the local row, late_slot[r·cap + k] = its slot in r's block, late_cnt[r] = k's bound — and
+// re-sent after that apply; every other slot's row is final when gathered a step early. Waves
+// compact with a ballot per requester (a wave may straddle two blocks) and one atomic per
+// (wave, requester), so the list order varies run to run, the rows it carries do not.
 __global__ __launch_bounds__(256) void exchange_classify_kernel(
     const int32_t* __restrict__ recv_ids, int64_t n, int64_t cap, const int32_t* __restrict__ stamp,
     int64_t n_rows, int32_t pred, int32_t* __restrict__ late_rows, int32_t* __restrict__ late_slot,
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(256) void exchange_classify_kernel(
   }
 }
 
-// stamp[row] = seq for every requested row (run after the classify of the same step)
+// stamp[row] = seq for every requested row of a step (before the next step's classify)
 __global__ __launch_bounds__(256) void exchange_mark_kernel(const int32_t* __restrict__ recv_ids,
                                                             int64_t n, int32_t* __restrict__ stamp,
                                                             int64_t n_rows, int32_t seq) {
@@ -208,14 +207,24 @@ __global__ __launch_bounds__(256) void exchange_scatter_late_kernel(
 
 using namespace rs;
 
+extern "C" int32_t rs_exchange_mark(const int32_t* recv_ids, int64_t n, int32_t* stamp,
+                                    int64_t n_rows, int32_t seq, void* stream) {
+  RS_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31) && n_rows >= 0, "bad sizes");
+  if (n == 0) return RS_OK;
+  RS_CHECK_ARG(recv_ids && stamp, "null pointer");
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+  exchange_mark_kernel<<<blocks, 256, 0, as_stream(stream)>>>(recv_ids, n, stamp, n_rows, seq);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
 extern "C" int32_t rs_exchange_classify(const int32_t* recv_ids, int32_t world, int64_t capacity,
-                                        int32_t* stamp, int64_t n_rows, int32_t pred_seq,
-                                        int32_t seq, int32_t* late_rows, int32_t* late_slot,
+                                        const int32_t* stamp, int64_t n_rows, int32_t pred_seq,
+                                        int32_t* late_rows, int32_t* late_slot,
                                         int32_t* late_count, void* stream) {
   RS_CHECK_ARG(world >= 1 && world <= kMaxWorld && capacity > 0 && n_rows >= 0, "bad sizes");
   RS_CHECK_ARG((int64_t)world * capacity < (int64_t(1) << 31), "world x capacity out of range");
   RS_CHECK_ARG(recv_ids && stamp && late_rows && late_slot && late_count, "null pointer");
-  RS_CHECK_ARG(seq != pred_seq, "seq must differ from pred_seq");
   hipStream_t st = as_stream(stream);
   const int64_t n = (int64_t)world * capacity;
   RS_CHECK_HIP(hipMemsetAsync(late_rows, 0xFF, (size_t)n * sizeof(int32_t), st));
@@ -224,8 +233,6 @@ extern "C" int32_t rs_exchange_classify(const int32_t* recv_ids, int32_t world, 
   const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
   exchange_classify_kernel<<<blocks, 256, 0, st>>>(recv_ids, n, capacity, stamp, n_rows, pred_seq,
                                                    late_rows, late_slot, late_count);
-  RS_CHECK_LAUNCH();
-  exchange_mark_kernel<<<blocks, 256, 0, st>>>(recv_ids, n, stamp, n_rows, seq);
   RS_CHECK_LAUNCH();
   return RS_OK;
 }

@@ -680,13 +680,18 @@ int32_t exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
 // share cache lines), pass 1 puts one slot's tiles on one XCD (its histograms and output stay in
 // that XCD's L2).
 constexpr int kSegThreads = 256;
-constexpr int kSegKPL = 16;
+#ifndef RS_SEG_KPL
+#define RS_SEG_KPL 16
+#endif
+constexpr int kSegKPL = RS_SEG_KPL;              // keys per thread (A/B builds: 8)
 constexpr int kSegTile = kSegThreads * kSegKPL;  // 4096 examples of one slot
 constexpr int kSegBits = 12;
 constexpr int kSegBins = 1 << kSegBits;
-constexpr int kSegMaxTiles = 32;   // tiles per slot: B <= 131 072
+constexpr int kSegMaxTiles = 32 * 16 / kSegKPL;  // tiles per slot: B <= 131 072
 constexpr int kSegMaxSlots = 64;
 constexpr int kSegMaxBits = 2 * kSegBits;  // slot ids < 2^24
+constexpr int kSegChunk = 256;                 // digits per scan block
+constexpr int kSegChunks = kSegBins / kSegChunk;
 constexpr int kNumXcd = 8;
 
 struct SegArgs {
@@ -708,6 +713,8 @@ struct SegArgs {
   int32_t* offs1;
   int32_t* starts;              // [2][kSegMaxSlots + 1] valid / sentinel starts per slot (+ totals)
   int32_t* spre;                // [n_slots][tiles] sentinels of the slot's earlier tiles
+  int32_t* csum0;               // [n_slots][tiles][kSegChunks] keys per 256-digit chunk of a tile
+  int32_t* csum1;
   uint32_t* rows_out;
   int32_t* pos_out;
   int32_t* err_flag;
@@ -778,9 +785,19 @@ __device__ __forceinline__ void seg_load0(const SegArgs& a, const SegSlot& sl, i
   }
 }
 
-__device__ __forceinline__ void seg_store_hist(uint16_t* __restrict__ h, const int32_t* cnt,
-                                               int bins) {
+// the tile's counts as uint16, and its keys per 256-digit chunk (csum[q], q < kSegChunks): thread
+// j sums digits [16 j, 16 j + 16), 16 threads a chunk
+__device__ __forceinline__ void seg_store_hist(uint16_t* __restrict__ h, int32_t* __restrict__ csum,
+                                               const int32_t* cnt, int bins) {
   for (int d = threadIdx.x; d < bins; d += blockDim.x) h[d] = static_cast<uint16_t>(cnt[d]);
+  constexpr int PER = kSegBins / kSegThreads;  // 16
+  const int d0 = threadIdx.x * PER;
+  int32_t v = 0;
+#pragma unroll
+  for (int c = 0; c < PER; ++c) v += d0 + c < bins ? cnt[d0 + c] : 0;
+#pragma unroll
+  for (int off = 8; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 15) == 0) csum[threadIdx.x >> 4] = v;
 }
 
 template <bool ID64>
@@ -818,7 +835,7 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
     for (int k = 0; k < kSegKPL; ++k) kt[k * 64] = ((sent >> k) & 1u) ? 0x80000000u : id[k];
   }
   __syncthreads();
-  seg_store_hist(a.hist0 + tile * kSegBins, cnt, bins);
+  seg_store_hist(a.hist0 + tile * kSegBins, a.csum0 + tile * kSegChunks, cnt, bins);
   if (threadIdx.x == 0) {
     const int64_t b0 = (int64_t)t * kSegTile;
     const int64_t tn = a.B - b0 < kSegTile ? a.B - b0 : kSegTile;
@@ -868,43 +885,30 @@ __device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstar
   __syncthreads();
 }
 
-// the 16 uint16 counts of digits [d0, d0 + 16) of tiles [t0, t0 + 8) (zeros past n_tiles)
-__device__ __forceinline__ void seg_load8(const uint16_t* __restrict__ hist, int t0, int n_tiles,
-                                          int d0, uint4 (&x)[8][2]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint4* h = reinterpret_cast<const uint4*>(hist + (int64_t)(t0 + j) * kSegBins + d0);
-    const bool in = t0 + j < n_tiles;
-    x[j][0] = in ? h[0] : make_uint4(0u, 0u, 0u, 0u);
-    x[j][1] = in ? h[1] : make_uint4(0u, 0u, 0u, 0u);
-  }
-}
-
-__device__ __forceinline__ int32_t seg_u16(const uint4 (&x)[2], int c) {
-  const uint32_t w = c < 8 ? (&x[0].x)[c >> 1] : (&x[1].x)[(c - 8) >> 1];
-  return (int32_t)((c & 1) ? (w >> 16) : (w & 0xFFFFu));
-}
-
-// One block per slot, after a pass's histograms: offs[t][d] = base + (keys of digits < d in the
-// slot) + (keys of digit d in the slot's tiles < t) for every tile t — the column scan the scatter
-// blocks then read as one 16 KB row each. Pass 0 also writes the slot starts and each tile's
-// sentinel prefix. Thread j owns digits [16 j, 16 j + 16).
+// One block per (slot, 256-digit chunk), after a pass's histograms: offs[t][d] = base + (keys
+// of digits < d in the slot) + (keys of digit d in the slot's tiles < t) for every tile t — the
+// column scan the scatter blocks then read as one 16 KB row each. The keys of the slot's lower
+// chunks come from the tiles' chunk sums (csum); thread j owns digit 256 c + j and loads its
+// column of counts once (every tile's row of the chunk is one coalesced 512 B load). Pass 0 also
+// writes the slot starts and each tile's sentinel prefix.
 template <int PASS>
 __global__ __launch_bounds__(kSegThreads) void slot_sort_scan_kernel(SegArgs a) {
   __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
-  __shared__ int32_t wsum[4];
-  const int s = blockIdx.x;
+  __shared__ int32_t wsum[4], wlow[4];
+  const int s = blockIdx.x / kSegChunks, c = blockIdx.x % kSegChunks;
   if (s >= a.n_slots) return;
   const SegSlot sl = seg_slot(a, s);
   if (PASS == 1 && sl.w1 == 0) return;
+  const int bins = 1 << (PASS == 0 ? sl.w0 : sl.w1);
+  if (c * kSegChunk >= bins) return;  // block-uniform
   if (PASS == 0) {
     seg_slot_starts(a, vstart, sstart);
-    if (s == 0)
+    if (s == 0 && c == 0)
       for (int q = threadIdx.x; q <= a.n_slots; q += blockDim.x) {
         a.starts[q] = vstart[q];
         a.starts[kSegMaxSlots + 1 + q] = sstart[q];
       }
-    if (threadIdx.x == 0) {
+    if (c == 0 && threadIdx.x == 0) {
       int32_t run = 0;
       for (int t = 0; t < a.tiles; ++t) {
         a.spre[s * a.tiles + t] = run;
@@ -916,74 +920,40 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scan_kernel(SegArgs a) 
     __syncthreads();
   }
   const int32_t base = vstart[s];
-  const int bins = 1 << (PASS == 0 ? sl.w0 : sl.w1);
   const int n_tiles = PASS == 0 ? a.tiles : (vstart[s + 1] - base + kSegTile - 1) / kSegTile;
   const uint16_t* hist = (PASS == 0 ? a.hist0 : a.hist1) + (int64_t)s * a.tiles * kSegBins;
+  const int32_t* cs = (PASS == 0 ? a.csum0 : a.csum1) + (int64_t)s * a.tiles * kSegChunks;
   int32_t* offs = (PASS == 0 ? a.offs0 : a.offs1) + (int64_t)s * a.tiles * kSegBins;
-  constexpr int PER = kSegBins / kSegThreads;  // 16
-  const int d0 = threadIdx.x * PER;
-  const bool vec = bins >= PER;
-  int32_t tot[PER];
+  const int d = c * kSegChunk + threadIdx.x;
+  const bool in = d < bins;
+  int32_t h[kSegMaxTiles];
+  int32_t tot = 0;
 #pragma unroll
-  for (int c = 0; c < PER; ++c) tot[c] = 0;
-  if (d0 < bins) {
-    for (int t0 = 0; t0 < n_tiles; t0 += 8) {
-      if (vec) {
-        uint4 x[8][2];
-        seg_load8(hist, t0, n_tiles, d0, x);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int c = 0; c < PER; ++c) tot[c] += seg_u16(x[j], c);
-      } else {
-        for (int t = t0; t < n_tiles && t < t0 + 8; ++t)
-          for (int c = 0; c < PER && d0 + c < bins; ++c) tot[c] += hist[(int64_t)t * kSegBins + d0 + c];
-      }
-    }
+  for (int t = 0; t < kSegMaxTiles; ++t) {
+    h[t] = (in && t < n_tiles) ? (int32_t)hist[(int64_t)t * kSegBins + d] : 0;
+    tot += h[t];
   }
-  // exclusive scan of the digit totals over the block
-  int32_t sum = 0;
-#pragma unroll
-  for (int c = 0; c < PER; ++c) sum += tot[c];
+  int32_t low = 0;  // keys of the slot's digits below this chunk
+  for (int e = threadIdx.x; e < n_tiles * c; e += blockDim.x) low += cs[(e / c) * kSegChunks + e % c];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t x = sum;
+  int32_t x = tot;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int32_t y = __shfl_up(x, off);
     if (lane >= off) x += y;
+    low += __shfl_xor(low, off);
   }
   if (lane == 63) wsum[wave] = x;
+  if (lane == 0) wlow[wave] = low;
   __syncthreads();
-  int32_t run = base + x - sum;
+  int32_t run = base + x - tot + wlow[0] + wlow[1] + wlow[2] + wlow[3];
   for (int w = 0; w < wave; ++w) run += wsum[w];
-  int32_t cur[PER];
+  if (!in) return;
 #pragma unroll
-  for (int c = 0; c < PER; ++c) {
-    cur[c] = run;
-    run += tot[c];
-  }
-  if (d0 >= bins) return;
-  // the tiles in order: each tile's row of offsets, then its counts added
-  for (int t0 = 0; t0 < n_tiles; t0 += 8) {
-    if (vec) {
-      uint4 xx[8][2];
-      seg_load8(hist, t0, n_tiles, d0, xx);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (t0 + j < n_tiles) {
-          int4* o = reinterpret_cast<int4*>(offs + (int64_t)(t0 + j) * kSegBins + d0);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = make_int4(cur[4 * q], cur[4 * q + 1], cur[4 * q + 2], cur[4 * q + 3]);
-#pragma unroll
-          for (int c = 0; c < PER; ++c) cur[c] += seg_u16(xx[j], c);
-        }
-      }
-    } else {
-      for (int t = t0; t < n_tiles && t < t0 + 8; ++t)
-        for (int c = 0; c < PER && d0 + c < bins; ++c) {
-          offs[(int64_t)t * kSegBins + d0 + c] = cur[c];
-          cur[c] += hist[(int64_t)t * kSegBins + d0 + c];
-        }
+  for (int t = 0; t < kSegMaxTiles; ++t) {
+    if (t < n_tiles) {
+      offs[(int64_t)t * kSegBins + d] = run;
+      run += h[t];
     }
   }
 }
@@ -1146,7 +1116,8 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a)
   for (int k = 0; k < kSegKPL; ++k)
     if ((live >> k) & 1u) atomicAdd(&cnt[id[k] >> sl.w0], 1);
   __syncthreads();
-  seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins, cnt, bins);
+  seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins,
+                 a.csum1 + ((int64_t)s * a.tiles + t) * kSegChunks, cnt, bins);
 }
 
 __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs a) {
@@ -1190,6 +1161,8 @@ static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArg
   int32_t* v = c.take<int32_t>(nt);
   int32_t* z = c.take<int32_t>(nt);
   int32_t* sp = c.take<int32_t>(nt);
+  int32_t* cs0 = c.take<int32_t>(nt * kSegChunks);
+  int32_t* cs1 = c.take<int32_t>(nt * kSegChunks);
   int32_t* st = c.take<int32_t>(2 * (kSegMaxSlots + 1));
   uint2* tmp = c.take<uint2>(n);
   if (a) {
@@ -1201,6 +1174,8 @@ static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArg
     a->vcnt = v;
     a->scnt = z;
     a->spre = sp;
+    a->csum0 = cs0;
+    a->csum1 = cs1;
     a->starts = st;
     a->tmp = tmp;
   }
@@ -1231,6 +1206,8 @@ size_t seg_ws_size(int64_t n_ids) {
   c.take<int32_t>(nt);
   c.take<int32_t>(nt);
   c.take<int32_t>(nt);
+  c.take<int32_t>(nt * kSegChunks);
+  c.take<int32_t>(nt * kSegChunks);
   c.take<int32_t>(2 * (kSegMaxSlots + 1));
   c.take<uint2>(n_ids);
   return c.off + 1024;
@@ -1265,7 +1242,7 @@ static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const 
   if (id_dtype == RS_ID_I64) slot_sort_hist0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_hist0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
-  slot_sort_scan_kernel<0><<<n_slots, kSegThreads, 0, st>>>(a);
+  slot_sort_scan_kernel<0><<<n_slots * kSegChunks, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   if (id_dtype == RS_ID_I64) slot_sort_scatter0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_scatter0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
@@ -1273,7 +1250,7 @@ static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const 
   // pass 1 only matters for slots wider than 12 bits; its blocks of narrower slots exit at once
   slot_sort_hist1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
-  slot_sort_scan_kernel<1><<<n_slots, kSegThreads, 0, st>>>(a);
+  slot_sort_scan_kernel<1><<<n_slots * kSegChunks, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   slot_sort_scatter1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();

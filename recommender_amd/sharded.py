@@ -144,11 +144,10 @@ class ShardedSlabEmbedding(nn.Module):
         # it updated (the ones both steps request, per owner stamps) are sent again
         self.rows_ahead = True
         self.rows_ahead_modes = {"fresh": 0, "late": 0, "full": 0}
-        self._stamp = None  # int32 per local row: the last step (seq) that requested it
-        self._seq = 0  # exchange_begin count
-        self._marked = -1  # the last seq whose requested rows were stamped
+        self._stamp = None  # int32 per local row: the last finished step (seq) that requested it
+        self._seq = 0  # exchange_begin count (each step's seq)
         self._apply_count = 0
-        self._last_applied = (0, 0)  # (seq, spill size) of the last applied step
+        self._last_applied = 0  # seq of the last applied step
 
     @property
     def n_slots(self):
@@ -212,42 +211,21 @@ class ShardedSlabEmbedding(nn.Module):
             L.call("rs_exchange_pack", L.ptr(uniq), L.ptr(n_unique), L.ptr(counts), W,
                    self.stride, C, L.ptr(inverse), n, L.ptr(send_ids), L.ptr(slot_of),
                    L.ptr(inv_slot), L.ptr(overflow), L.stream_ptr(dev))
-            recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
-            self.comm.all_to_all(recv_ids, send_ids)
-            self._seq += 1
-            seq = self._seq
-            ahead = self._rows_ahead_ok()
-            # all-reduced (MAX) over the ranks: [0] the spill round's size (every rank's largest
-            # excess over C), [1] with rows ahead the late round's size (the most rows one owner
-            # re-sends one requester after the previous step's apply)
-            excess = torch.empty(2 if ahead else 1, dtype=torch.int64, device=dev)
+            # the spill round's size: every rank's largest excess over C, all-reduced (MAX)
+            excess = torch.empty(1, dtype=torch.int64, device=dev)
             L.call("rs_exchange_excess", L.ptr(counts), W, C, L.ptr(excess), L.stream_ptr(dev))
-            late = None
-            if ahead:
-                if self._stamp is None:
-                    self._stamp = torch.zeros(max(self.shard.input_dim, 1), dtype=torch.int32,
-                                              device=dev)
-                late_rows = torch.empty(W * C, dtype=torch.int32, device=dev)
-                late_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
-                late_cnt = torch.empty(W, dtype=torch.int32, device=dev)
-                L.call("rs_exchange_classify", L.ptr(recv_ids), W, C, L.ptr(self._stamp),
-                       self.shard.input_dim, seq - 1, seq, L.ptr(late_rows), L.ptr(late_slot),
-                       L.ptr(late_cnt), L.stream_ptr(dev))
-                L.call("rs_exchange_excess", L.ptr(late_cnt), W, 0, L.ptr(excess[1:]),
-                       L.stream_ptr(dev))
-                recv_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
-                self.comm.all_to_all(recv_slot, late_slot)
-                # the classify is against the previous step's stamps only if that step marked
-                late = (late_rows, recv_slot, self._marked == seq - 1)
-                self._marked = seq
             self.comm.all_reduce_(excess, dist.ReduceOp.MAX)
-            host = torch.empty(excess.numel(), dtype=torch.int64, pin_memory=True)
+            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
             host.copy_(excess, non_blocking=True)
             excess_ready = torch.cuda.Event()
             excess_ready.record(self.side)
+            recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
+            self.comm.all_to_all(recv_ids, send_ids)
+        self._seq += 1
         return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, recv_ids=recv_ids,
                     capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
-                    inverse=inverse, excess=(excess_ready, host), seq=seq, late=late, early=None)
+                    inverse=inverse, excess=(excess_ready, host), seq=self._seq, early=None,
+                    late=None)
 
     def _rows_ahead_ok(self) -> bool:
         """Rows a step ahead need an update that changes only the rows it receives (SGD, lazy
@@ -272,6 +250,38 @@ class ShardedSlabEmbedding(nn.Module):
         rows = torch.empty(W * C, self.output_dim, device=st["dev"])
         self._gather_send(st["recv_ids"], rows)
         st["early"] = (rows, self._apply_count)
+
+    def _ahead(self, cur, nxt):
+        """In exchange_finish of step `cur`, on the side stream: stamp cur's requested rows
+        (capacity block and spill: the rows its apply will change), list the next step's slots
+        whose rows are among them (rs_exchange_classify: re-sent after cur's apply), all-reduce the
+        largest such list (the late round's size, read on the host at nxt's finish), send each
+        requester its slot list, and gather + send nxt's capacity block now."""
+        dev, W, C = nxt["dev"], self.world, nxt["capacity"]
+        if self._stamp is None:
+            self._stamp = torch.zeros(max(self.shard.input_dim, 1), dtype=torch.int32, device=dev)
+        seq = cur["seq"]
+        for ids in (cur["recv_ids"], cur.get("recv_spill")):
+            if ids is not None:
+                L.call("rs_exchange_mark", L.ptr(ids), ids.numel(), L.ptr(self._stamp),
+                       self.shard.input_dim, seq, L.stream_ptr(dev))
+        late_rows = torch.empty(W * C, dtype=torch.int32, device=dev)
+        late_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
+        late_cnt = torch.empty(W, dtype=torch.int32, device=dev)
+        L.call("rs_exchange_classify", L.ptr(nxt["recv_ids"]), W, C, L.ptr(self._stamp),
+               self.shard.input_dim, seq, L.ptr(late_rows), L.ptr(late_slot), L.ptr(late_cnt),
+               L.stream_ptr(dev))
+        mx = torch.empty(1, dtype=torch.int64, device=dev)
+        L.call("rs_exchange_excess", L.ptr(late_cnt), W, 0, L.ptr(mx), L.stream_ptr(dev))
+        self.comm.all_reduce_(mx, dist.ReduceOp.MAX)
+        host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        host.copy_(mx, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        recv_slot = torch.empty(W * C, dtype=torch.int32, device=dev)
+        self.comm.all_to_all(recv_slot, late_slot)
+        nxt["late"] = dict(rows=late_rows, recv_slot=recv_slot, count=(ev, host), pred=seq)
+        self._issue_early(nxt)
 
     def check_overflow(self, block: bool = True):
         """Kept for callers of the round-4 API: a batch past the capacity now takes a spill
@@ -321,7 +331,7 @@ class ShardedSlabEmbedding(nn.Module):
         D = self.output_dim
         ev, host = st["excess"]
         ev.synchronize()  # prefetched a step ahead: long done
-        C2 = int(host[0])
+        C2 = int(host.item())
         n = st["ids"].numel()
         recv_spill = None
         with torch.cuda.stream(self.side):
@@ -332,21 +342,21 @@ class ShardedSlabEmbedding(nn.Module):
             late = st["late"]
             if k == 0:
                 mode = "fresh"  # no apply since the gather
-            elif (k == 1 and late is not None and late[2]
-                  and self._last_applied == (st["seq"] - 1, 0)):
-                mode = "late"  # one apply since, the previous step's, without a spill round
+            elif k == 1 and late is not None and self._last_applied == late["pred"]:
+                mode = "late"  # one apply since: the one of the step whose rows were stamped
             else:
                 mode = "full"
             self.rows_ahead_modes[mode] += 1
             if mode == "late":
-                C_late = int(host[1])
+                lev, lhost = late["count"]
+                lev.synchronize()  # recorded a step ago
+                C_late = int(lhost.item())
                 if C_late > 0:
-                    late_rows, recv_slot, _ = late
-                    ids_l = late_rows.view(W, C)[:, :C_late].contiguous()
+                    ids_l = late["rows"].view(W, C)[:, :C_late].contiguous()
                     recv = torch.empty(W * C_late, D, device=dev)
                     self._gather_send(ids_l, recv)
-                    L.call("rs_exchange_scatter_late", L.ptr(recv), L.ptr(recv_slot), W, C, C_late,
-                           D, L.ptr(rows_c), L.stream_ptr(dev))
+                    L.call("rs_exchange_scatter_late", L.ptr(recv), L.ptr(late["recv_slot"]), W,
+                           C, C_late, D, L.ptr(rows_c), L.stream_ptr(dev))
             elif mode == "full":
                 self._gather_send(st["recv_ids"], rows_c)
             if C2 > 0:
@@ -366,10 +376,11 @@ class ShardedSlabEmbedding(nn.Module):
             ready = torch.cuda.Event()
             ready.record(self.side)
             # the next prefetched step's rows, gathered and sent beside this step's train kernel
-            if self._prefetched:
+            st["recv_spill"] = recv_spill
+            if self._prefetched and self._rows_ahead_ok():
                 nxt = self._prefetched[0][2]
-                if nxt["early"] is None and nxt["late"] is not None:
-                    self._issue_early(nxt)
+                if nxt["early"] is None:
+                    self._ahead(st, nxt)
         main.wait_event(ready)
         inverse = st["inv_slot"][:n]
         for t in (rows, inverse):
@@ -478,7 +489,7 @@ class ShardedSlabEmbedding(nn.Module):
             # every owner applies (an owner no rank sent a row to still runs Keras' dense decay)
             opt.apply(self.shard, recv_ids, recv_grad, params, valid=valid)
         self._apply_count += 1
-        self._last_applied = (st["seq"], C2)
+        self._last_applied = st["seq"]
         g.record_stream(self.side)
         if row_scale is not None:
             row_scale.record_stream(self.side)

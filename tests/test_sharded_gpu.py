@@ -139,12 +139,13 @@ def test_world2_sharded_embedding_matches_oracle(opt, even):
 
 def _fused_dlrm_worldn_worker(rank, world, port, q, spill, prefetch):
     """The production fused DLRM step over a row-sharded slab, `world` ranks on the one GPU
-    (gloo): every check is against the oracle on the GLOBAL batch (all ranks' examples). Three
-    steps; `spill`: the second batch has uniform ids (many more unique rows than the capacity the
-    first, Zipf, batch calibrated), so its exchange takes the spill round. `prefetch`: each
-    step's exchange is queued during the step before (TrainStep.prefetch), so its rows are
-    gathered a step early and only the rows the step before updates are sent again (rows ahead):
-    the later steps take that late round, or the full re-send after a spill round."""
+    (gloo): every check is against the oracle on the GLOBAL batch (all ranks' examples). Four
+    steps; `spill`: the third batch has uniform ids (many more unique rows than the capacity the
+    first exchanged, Zipf, batch calibrated), so its exchange takes the spill round. `prefetch`:
+    each step's exchange is queued during the step before (TrainStep.prefetch), so its rows are
+    gathered a step early and only the rows the step before updates (its capacity block and
+    spill rows) are sent again after that step's apply: every step but the first takes that late
+    round."""
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -176,10 +177,10 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill, prefetch):
                      embedding_layer=emb)
         step = TrainStep(model, "sgd", lr=lr, comm=comm)
         steps = [[criteo_batch(np.random.default_rng(40 + 10 * k + r), B, cards) for r in range(world)]
-                 for k in range(3)]
+                 for k in range(4)]
         if spill:
             for r in range(world):
-                c2 = steps[1][r][0]
+                c2 = steps[2][r][0]
                 for j, c in enumerate(cards):
                     c2[:, j] = np.random.default_rng(70 + r + 100 * j).integers(0, c, B)
         top0, bot0 = _layers(model.top_mlp), _layers(model.bottom_mlp)
@@ -238,11 +239,8 @@ def _fused_dlrm_worldn_worker(rank, world, port, q, spill, prefetch):
         if spill:
             assert emb.spill_rounds == 1, emb.spill_rounds
         modes = emb.rows_ahead_modes
-        if prefetch:
-            want_modes = {"fresh": 1, "late": 1, "full": 1} if spill else {"fresh": 1, "late": 2,
-                                                                           "full": 0}
-        else:
-            want_modes = {"fresh": 3, "late": 0, "full": 0}
+        want_modes = ({"fresh": 1, "late": 3, "full": 0} if prefetch else
+                      {"fresh": 4, "late": 0, "full": 0})
         assert modes == want_modes, modes
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover
@@ -261,9 +259,9 @@ def test_worldn_fused_dlrm_step_matches_oracle(world, spill, prefetch):
     """TrainStep's fused DLRM step on a row-sharded slab at world 2 / 3 / 4 (gloo, all ranks on
     the one GPU; global batch 2048 split over the ranks): the train kernel reads the exchanged unique rows with dL/dl_b = 1/(B·W); the
     batch sums are all-reduced (the dense half of the global step); the owners apply the gradient
-    rows. Two steps, slab bit-exact vs oracle/sharded.py fed with every rank's kernel rows after
+    rows. Four steps, slab bit-exact vs oracle/sharded.py fed with every rank's kernel rows after
     each; loss, the twelve MLP gradients (per-element bounds) and the SGD apply vs the oracle step
-    on the global batch. `spill`: the second step's batch overflows the calibrated capacity and
+    on the global batch. `spill`: the third step's batch overflows the calibrated capacity and
     is exchanged with the spill round — still bit-exact, on every rank. `prefetch`: rows a step
     ahead (each step's capacity block gathered during the step before, the rows that step
     updated re-sent after its apply), the same bits."""
