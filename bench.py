@@ -221,6 +221,17 @@ def init_dist(args):
     return world, rank, local
 
 
+def exchange_info(emb):
+    """The row-sharded exchange's counters over the run: capacity, spill rounds, the
+    rows-ahead modes and, on late steps, the share of the capacity block re-sent after the
+    previous step's apply."""
+    late = getattr(emb, "late_slots", [0, 0])
+    return {"capacity": getattr(emb, "capacity", None), "spill_rounds": getattr(emb, "spill_rounds", 0),
+            "rows_ahead_modes": dict(getattr(emb, "rows_ahead_modes", {})),
+            "late_fraction": round(late[0] / late[1], 4) if late[1] else None,
+            "split_halves": bool(getattr(emb, "split_halves", False))}
+
+
 def barrier(world):
     if world > 1:
         dist.barrier()
@@ -745,7 +756,8 @@ def main():
                        "parallelism": (f"row-sharded slab x{world} (RCCL all-to-all of the unique rows and of their "
                                        f"gradient rows) + dp{world} MLPs (all-reduce of the fused kernel's "
                                        f"batch sums)") if world > 1 else "single",
-                       "prefetch": bool(args.prefetch)},
+                       "prefetch": bool(args.prefetch),
+                       **({"exchange": exchange_info(model.embedding_layer)} if world > 1 else {})},
             "mlp": {"backward": args.mlp_bwd, "forward": args.mlp_fwd,
                     "note": "ctr MLP hidden layers are linear (ctr/layers.py:8), so each MLP is one "
                             "affine map: the composed forward evaluates x·K1·K2·K3 + c as x·(K1K2K3) + c "

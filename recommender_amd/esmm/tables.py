@@ -35,5 +35,9 @@ class FeatureTables(nn.Module):
         if order != list(range(len(self.feats))):
             raise ValueError("inputs must hold every feature of feat_vocab, in its order")
         ids = torch.stack([inputs[f].reshape(-1) for f in inputs], dim=1)  # [B, F]
+        if getattr(self.slab, "fused_optimizer", None) is not None and torch.is_grad_enabled():
+            # fused sparse optimizer: the step's sort is queued before the lookup (with the
+            # deferred-decay Keras Adam its rows' skipped decay is replayed before they are read)
+            self.slab.presort(ids)
         emb = self.slab(ids)                                                # [B, F, D]
         return emb.reshape(emb.shape[0], -1)                                # [B, F*D]

@@ -144,6 +144,7 @@ class ShardedSlabEmbedding(nn.Module):
         # it updated (the ones both steps request, per owner stamps) are sent again
         self.rows_ahead = True
         self.rows_ahead_modes = {"fresh": 0, "late": 0, "full": 0}
+        self.late_slots = [0, 0]  # late steps: (slots re-sent W·C_late, capacity slots W·C)
         self._stamp = None  # int32 per local row: the last finished step (seq) that requested it
         self._seq = 0  # exchange_begin count (each step's seq)
         self._apply_count = 0
@@ -351,6 +352,8 @@ class ShardedSlabEmbedding(nn.Module):
                 lev, lhost = late["count"]
                 lev.synchronize()  # recorded a step ago
                 C_late = int(lhost.item())
+                self.late_slots[0] += W * C_late
+                self.late_slots[1] += W * C
                 if C_late > 0:
                     ids_l = late["rows"].view(W, C)[:, :C_late].contiguous()
                     recv = torch.empty(W * C_late, D, device=dev)
