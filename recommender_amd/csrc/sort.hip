@@ -908,12 +908,16 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scan_kernel(SegArgs a) 
         a.starts[q] = vstart[q];
         a.starts[kSegMaxSlots + 1 + q] = sstart[q];
       }
-    if (c == 0 && threadIdx.x == 0) {
-      int32_t run = 0;
-      for (int t = 0; t < a.tiles; ++t) {
-        a.spre[s * a.tiles + t] = run;
-        run += a.scnt[s * a.tiles + t];
+    if (c == 0 && threadIdx.x < 64) {  // the sentinel prefix over the slot's tiles (<= 64)
+      const int lane = threadIdx.x;
+      const int32_t z = lane < a.tiles ? a.scnt[s * a.tiles + lane] : 0;
+      int32_t x = z;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
       }
+      if (lane < a.tiles) a.spre[s * a.tiles + lane] = x - z;
     }
   } else {
     if (threadIdx.x <= 1) vstart[s + threadIdx.x] = a.starts[s + threadIdx.x];
