@@ -38,7 +38,9 @@ WATCH = ["rs_dlrm_train_step_fwd_unit",
          "rs_dlrm_interaction_fwd_head_dx",
          "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots",
          "rs_embedding_apply", "rs_embedding_apply_scaled", "rs_sort_ids_sharded",
-         "rs_embedding_dedup_grad", "rs_embedding_dedup_grad_mapped", "rs_gather_rows_padded"]
+         "rs_embedding_dedup_grad", "rs_embedding_dedup_grad_mapped", "rs_gather_rows_padded",
+         "rs_embedding_dedup_grad_mapped_range", "rs_exchange_classify", "rs_exchange_mark",
+         "rs_exchange_scatter_late"]
 # the embedding path of SURVEY §8(d) (lookup fwd + bwd + dedup + apply) as the production step
 # launches it: the fused gather + interaction + unit-backward kernel (main stream), the radix
 # sort and the segmented-sum apply (fused optimizer's side stream, co-running with dense GEMMs:
@@ -50,7 +52,8 @@ PATH_KERNELS = ("rs_dlrm_train_step_fwd_unit",
                 "rs_embedding_apply", "rs_embedding_apply_scaled")
 SIDE_STREAM = {"rs_sort_ids_slots", "rs_embedding_apply", "rs_embedding_apply_scaled",
                "rs_sort_ids_sharded", "rs_embedding_dedup_grad", "rs_embedding_dedup_grad_mapped",
-               "rs_gather_rows_padded"}
+               "rs_gather_rows_padded", "rs_embedding_dedup_grad_mapped_range",
+               "rs_exchange_classify", "rs_exchange_mark", "rs_exchange_scatter_late"}
 # device symbols behind each C-ABI entry (for the PMC passes)
 # (entry, device-symbol regex of its kernels, the one kernel every call launches once)
 PMC_SYMBOLS = [
@@ -275,8 +278,15 @@ def kernel_bytes(name, B, S, D, id_bytes, U, world=1, cap=0):
             return E * (4 + 1) + E * 8
         if name == "rs_embedding_apply":  # E sorted entries, ≈U rows read, their rows updated
             return E * 8 + U * 4 * D + U * 2 * 4 * D
-        if name == "rs_gather_rows_padded":  # the owner serves the requested rows
+        if name == "rs_gather_rows_padded":  # the owner serves the requested rows (the early
+            # block; a late round's call moves only its C_late slots, so the average overstates)
             return E * 4 + E * 2 * 4 * D
+        if name == "rs_embedding_dedup_grad_mapped_range":  # one owner half of the dedup
+            return (N * 8 + N * 4 * D + U * 4 * D) // 2
+        if name == "rs_exchange_classify":  # slots, stamps read, the late lists written
+            return E * 4 + E * 4 + E * 8
+        if name == "rs_exchange_mark":  # one requested-slot block (or a spill block)
+            return E * 4 + E * 4
     if name == "rs_dlrm_interaction_fwd":
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z)
     if name == "rs_dlrm_interaction_fwd_head":  # + the fused top-MLP output y[b]
@@ -719,13 +729,23 @@ def main():
     weak = None
     if world > 1 and args.scaling == "strong" and args.weak_secondary:
         wpool = make_pool(args, cards, rank, dev, batch=requested_batch)
+        WP = len(wpool)
+        emb = model.embedding_layer
+        if hasattr(emb, "capacity"):
+            emb.capacity = None  # the exchange capacity recalibrated on this batch size
+
+        def wstep(i):
+            if args.prefetch:
+                step.prefetch(wpool[(i + 1) % WP])
+            step(wpool[i % WP])
+
         for i in range(3):
-            step(wpool[i % len(wpool)])
+            wstep(i)
         torch.cuda.synchronize()
         barrier(world)
         tw0 = time.perf_counter()
         for i in range(args.steps):
-            step(wpool[i % len(wpool)])
+            wstep(i)
         torch.cuda.synchronize()
         barrier(world)
         tw = time.perf_counter() - tw0
