@@ -291,6 +291,14 @@ def main():
     if args.model == "dlrm_cfg2" and args.cfg2_graph == 2 and args.optimizer == "sgd":
         sec /= B_pool  # one replay = the whole pool of steps
     extra = {}
+    dense_fl = None
+    if args.model in ("esmm", "mmoe"):
+        # the dense layers' GEMM work (forward, input gradient and weight gradient of every Dense
+        # layer, 2·in·out FLOP each per example), counted before the model is released below
+        from recommender_amd.nn import Dense
+
+        dense_fl = sum(6.0 * B * l.kernel.shape[0] * l.kernel.shape[1]
+                       for l in m.modules() if isinstance(l, Dense) and l.kernel is not None)
     if args.model in ("esmm", "mmoe") and args.cfg4_optimizer == "keras_adam_deferred":
         # the replayed decay of every row not touched since the start: materialize() brings the
         # slab to the dense sweep's state; its time is amortised over every step run so far
@@ -345,13 +353,9 @@ def main():
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "unique_rows_per_step": U, "note": "path bytes / whole step time"}
     if args.model in ("esmm", "mmoe"):
-        # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950):
-        # forward, input gradient and weight gradient of every Dense layer, 2·in·out FLOP each
-        # per example — the floor the library fp32 GEMMs set for the step
-        from recommender_amd.nn import Dense
-
-        fl = sum(6.0 * B * l.kernel.shape[0] * l.kernel.shape[1]
-                 for l in m.modules() if isinstance(l, Dense) and l.kernel is not None)
+        # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950)
+        # — the floor the library fp32 GEMMs set for the step
+        fl = dense_fl
         floor_ms = fl / 157.3e12 * 1e3
         out["roofline"] = {"bound": "mfma_fp32", "dense_gflop_per_step": round(fl / 1e9, 1),
                            "achieved_TFs": round(fl / sec / 1e12, 1), "peak_TFs": 157.3,
