@@ -352,6 +352,17 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "unique_rows_per_step": U, "note": "path bytes / whole step time"}
+    if args.model == "deepfm":
+        # cfg1's bytes per step: Keras Adam's dense sweep of the 1M x 16 table (table, m, v read
+        # and written: 24·V·D B — the reference's update touches every row every step) plus the
+        # lookup and its gradient rows (B·26·(8 B id + 4D read + 4D gradient)), over the whole
+        # replayed step (MLPs and glue included in the time)
+        V_, D_ = 1_000_000, 16
+        by = 24 * V_ * D_ + B * 26 * (8 + 8 * D_)
+        gbs = by / sec / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                           "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
+                           "note": "dense Keras Adam sweep + lookup/gradient bytes / whole step time"}
     if args.model in ("esmm", "mmoe"):
         # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950)
         # — the floor the library fp32 GEMMs set for the step

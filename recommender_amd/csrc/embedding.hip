@@ -648,9 +648,20 @@ __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __res
   constexpr int G = 32, D = 128, T = 32;
   __shared__ __attribute__((aligned(16))) float ps[G][2][D];
   __shared__ uint32_t fkey[G];
+  __shared__ int skip;
   const int gi = threadIdx.x >> 5, gl = threadIdx.x & 31;
   const int64_t t = (int64_t)blockIdx.x * G + gi;
   const bool live = t < n_tiles;
+  if (threadIdx.x == 0) {  // no key of the group in [key_lo, n_rows): nothing to sum or write
+    const int64_t f = (int64_t)blockIdx.x * G * T;
+    const int64_t l = (f + (int64_t)G * T < n ? f + (int64_t)G * T : n) - 1;
+    skip = f < n && (keys[l] < a.key_lo || keys[f] >= n_rows);
+  }
+  __syncthreads();
+  if (skip) {  // the walk would find no run in range: the same (empty) tile flags
+    if (gl == 0 && live) a.tile_flags[t] = 0;
+    return;
+  }
   Tile32Edges e{};
   if (live) e = tile32_walk<OPT, Q, P>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
   if (gl == 0) fkey[gi] = live ? e.first_key : 0xFFFFFFFFu;

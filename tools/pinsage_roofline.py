@@ -1,4 +1,4 @@
-"""Join tools/r04_pinsage_prof.sh's kernel stats and PMC passes: per PinSage kernel, the average
+"""Join tools/pinsage_prof.sh's kernel stats and PMC passes: per PinSage kernel, the average
 duration in the graph step, the HBM bytes per launch from FETCH_SIZE (x2, the gfx950 16-B read
 correction) + WRITE_SIZE, and the achieved GB/s against the 8 TB/s peak."""
 import csv
@@ -7,7 +7,9 @@ import re
 from collections import defaultdict
 
 KERNELS = ["neighbors_kernel", "agg_fwd_kernel", "agg_bwd_kernel", "block_emit_kernel",
-           "first_mark_kernel", "first_emit_kernel", "walk_kernel", "pairs_gen_kernel"]
+           "first_mark_kernel", "first_emit_kernel", "walk_kernel", "pairs_gen_kernel",
+           "pair_margin_fwd_kernel", "pair_margin_terms_kernel", "multihot_mean_fwd",
+           "multihot_mean_bwd"]
 
 
 def short(name):
