@@ -363,6 +363,17 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "note": "dense Keras Adam sweep + lookup/gradient bytes / whole step time"}
+    if args.model == "eges":
+        # every table densified and updated by Keras Adam each step (GraphKerasAdam: parameter,
+        # m, v read and written = 24 B per element, the densified gradient written and read =
+        # 8 B): 32 B per parameter element, over the whole replayed step
+        n_el = sum(p.numel() for p in m.parameters())
+        by = 32 * n_el
+        gbs = by / sec / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                           "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
+                           "parameters": int(n_el),
+                           "note": "dense Keras Adam over every table / whole step time"}
     if args.model in ("esmm", "mmoe"):
         # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950)
         # — the floor the library fp32 GEMMs set for the step
