@@ -1155,6 +1155,156 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Small sorts in one workgroup (round 5): a one-slot id sort of n <= 16 384 ids over fewer than
+// 2^18 - 2 rows (the PinSage pair-term fold, small densifies) as one launch. Entry = key << 14 |
+// position in a uint32 (key: the row, or the sentinel n_rows for an excluded / OOB id; entries
+// past n: all ones). Wave w owns positions [1024 w, 1024 w + 1024), lane-strided, so (wave,
+// round, lane) order is position order. Per 8-bit digit pass, between two 64 KB LDS buffers:
+// counts per (wave, digit) from a wave match, per-wave digit offsets, then the same matches again
+// place every entry (digit base + wave offset + rank in the wave). Output identical to the
+// multi-launch forms (stable by position, sentinels after every row).
+// ---------------------------------------------------------------------------------------
+constexpr int kSmallThreads = 1024, kSmallWaves = kSmallThreads / 64;
+constexpr int kSmallMax = 16384, kSmallKPT = kSmallMax / kSmallThreads;  // 16 entries per lane
+constexpr int kSmallPosBits = 14;
+constexpr int64_t kSmallMaxRows = (int64_t(1) << (32 - kSmallPosBits)) - 2;
+
+__global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
+    const void* __restrict__ ids, int32_t dtype, int64_t n, const uint8_t* __restrict__ valid,
+    const int64_t* __restrict__ slot_offsets, int64_t n_rows, int key_bits,
+    uint32_t* __restrict__ rows_out, int32_t* __restrict__ pos_out, int32_t* __restrict__ n_unique,
+    int32_t* __restrict__ err_flag) {
+  __shared__ uint32_t bufs[2][kSmallMax];
+  __shared__ uint16_t wcnt[kSmallWaves][256];
+  __shared__ int32_t dbase[256];
+  __shared__ int32_t heads[kSmallWaves];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt64();
+  const int64_t lo = slot_offsets ? slot_offsets[0] : 0;
+  const int64_t span = slot_offsets ? slot_offsets[1] - lo : n_rows;
+  const int own = wave * (kSmallKPT * 64) + lane;  // this lane's first entry; then + 64 per round
+  bool oob = false;
+#pragma unroll 4
+  for (int r = 0; r < kSmallKPT; ++r) {
+    const int i = own + r * 64;
+    uint32_t e = 0xFFFFFFFFu;
+    if (i < n) {
+      uint32_t key = (uint32_t)n_rows;  // sentinel
+      if (!valid || valid[i]) {
+        const int64_t id = load_id(ids, dtype, i);
+        if (id >= 0 && id < span) key = (uint32_t)(lo + id);
+        else oob = true;
+      }
+      e = key << kSmallPosBits | (uint32_t)i;
+    }
+    bufs[0][i] = e;
+  }
+  if (__any(oob) && lane == 0) flag_oob(err_flag);
+  int cur = 0;
+  for (int shift = kSmallPosBits; shift < kSmallPosBits + key_bits; shift += 8) {
+    const uint32_t* src = bufs[cur];
+    uint32_t* dst = bufs[cur ^ 1];
+    for (int e = threadIdx.x; e < kSmallWaves * 256; e += kSmallThreads) (&wcnt[0][0])[e] = 0;
+    __syncthreads();
+    // counts per (wave, digit): each match group's last lane adds the group's size
+#pragma unroll 2
+    for (int r = 0; r < kSmallKPT; ++r) {
+      const uint32_t d = (src[own + r * 64] >> shift) & 0xFFu;
+      const uint64_t m = match_digit<8>(d, true);
+      const int32_t prev = wcnt[wave][d];
+      __builtin_amdgcn_wave_barrier();
+      if ((m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) {  // per digit: the waves' counts -> wave offsets, the digit total
+      const int d = threadIdx.x;
+      int32_t run = 0;
+#pragma unroll
+      for (int w = 0; w < kSmallWaves; ++w) {
+        const int32_t c = wcnt[w][d];
+        wcnt[w][d] = (uint16_t)run;
+        run += c;
+      }
+      dbase[d] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the 256 digit totals, 4 per lane
+      int32_t t[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        t[q] = dbase[4 * lane + q];
+        sum += t[q];
+      }
+      int32_t x = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+      }
+      int32_t run = x - sum;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dbase[4 * lane + q] = run;
+        run += t[q];
+      }
+    }
+    __syncthreads();
+    // the same groups again, now placed: digit base + this wave's offset + the rank in the wave
+#pragma unroll 2
+    for (int r = 0; r < kSmallKPT; ++r) {
+      const uint32_t e = src[own + r * 64];
+      const uint32_t d = (e >> shift) & 0xFFu;
+      const uint64_t m = match_digit<8>(d, true);
+      const int32_t prev = wcnt[wave][d];
+      dst[dbase[d] + prev + __popcll(m & lt)] = e;
+      __builtin_amdgcn_wave_barrier();
+      if ((m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // sorted entries out; the heads of distinct rows counted
+  const uint32_t* out = bufs[cur];
+  int32_t h = 0;
+  for (int i = threadIdx.x; i < n; i += kSmallThreads) {
+    const uint32_t e = out[i];
+    const uint32_t key = e >> kSmallPosBits;
+    rows_out[i] = key;
+    pos_out[i] = (int32_t)(e & ((1u << kSmallPosBits) - 1u));
+    if (key < (uint32_t)n_rows && (i == 0 || (out[i - 1] >> kSmallPosBits) != key)) ++h;
+  }
+  if (n_unique) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
+    if (lane == 0) heads[wave] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int32_t t = 0;
+      for (int w = 0; w < kSmallWaves; ++w) t += heads[w];
+      *n_unique = t;
+    }
+  }
+}
+
+static bool small_eligible(int64_t n_ids, int n_slots, int world, int64_t n_rows) {
+  return world == 1 && n_slots == 1 && n_ids >= 1 && n_ids <= kSmallMax && n_rows <= kSmallMaxRows;
+}
+
+static int32_t small_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const uint8_t* valid,
+                          const int64_t* slot_offsets, int64_t n_rows, uint32_t* sorted_rows,
+                          int32_t* sorted_pos, int32_t* n_unique, int32_t* err_flag, hipStream_t st) {
+  int key_bits = 1;
+  while (key_bits < 32 - kSmallPosBits && (int64_t(1) << key_bits) <= n_rows) ++key_bits;  // keys <= n_rows
+  small_sort_kernel<<<1, kSmallThreads, 0, st>>>(ids, id_dtype, n_ids, valid, slot_offsets, n_rows,
+                                                 key_bits, sorted_rows, sorted_pos, n_unique,
+                                                 err_flag);
+  RS_CHECK_LAUNCH();
+  return RS_OK;
+}
+
 static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArgs* a) {
   const size_t nt = (size_t)n_slots * tiles;
   uint32_t* k0 = c.take<uint32_t>(nt * kSegTile);
@@ -1387,6 +1537,10 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
   RS_CHECK_ARG(key_space < (int64_t(1) << 31) - 1, "key space out of range");
   if (n_unique) RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, sizeof(int32_t), st));
   if (n_ids == 0) return RS_OK;
+  if (small_eligible(n_ids, n_slots, world, n_rows) && !sort_lsd_forced())
+    // one workgroup, one launch (RS_SORT_LSD=1: the LSD sort, A/B)
+    return small_sort(ids, id_dtype, n_ids, valid, slot_offsets, n_rows, sorted_rows, sorted_pos,
+                      n_unique, err_flag, st);
   if ((slot_offsets || n_slots == 1) && seg_eligible(n_ids, n_slots, world, max_slot_rows) &&
       !sort_lsd_forced()) {
     // the slot-segmented sort: same output, four launches (RS_SORT_LSD=1: the LSD sort, A/B)

@@ -135,6 +135,66 @@ def test_sort_ids(n, V, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("n", [2, 16383, 16384])
+@pytest.mark.parametrize("V", [1, 3000, 65535, 262141])
+@pytest.mark.parametrize("masked", [False, True])
+def test_sort_ids_small_one_workgroup(n, V, masked, rng):
+    """A one-slot sort of at most 16 384 ids over fewer than 2^18 - 2 rows runs as one workgroup
+    (small_sort_kernel: 8-bit digit passes between two LDS buffers): bit-exact against the
+    oracle's stable sort — the 16 384 limit, one-row and 18-bit key spaces, OOB ids, masked
+    positions, a one-slot slab's offsets, the unique count."""
+    ids = zipf_ids(rng, n, V).astype(np.int64)
+    ids[1::7] = rng.integers(0, V, ids[1::7].shape)
+    ids[::97] = V + 3  # OOB
+    ids[5::101] = -1
+    so = np.array([0, V], np.int64) if masked else None  # a one-slot slab on one side
+    dev_so = None if so is None else torch.from_numpy(so).to(DEV)
+    if masked:
+        keep = rng.random(n) < 0.6
+        s = SortedIds(torch.from_numpy(ids.astype(np.int32)).to(DEV), V, dev_so,
+                      valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV))
+        rows_ref, pos_ref, nu_ref = O.sort_ids(np.where(keep, ids, -1), V, so)
+    else:
+        s = SortedIds(torch.from_numpy(ids).to(DEV), V, dev_so)
+        rows_ref, pos_ref, nu_ref = O.sort_ids(ids, V, so)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
+@pytest.mark.parametrize("n", [16384, 40_000])
+def test_index_add_rows_fixed_order(n, rng):
+    """rs_index_add_rows (PinSage's deterministic scatter-add: sort + tiled segmented sum) through
+    the C-ABI: out[r] = Σ rows[i] over ids[i] = r within fp32 summation error of the float64 sum,
+    run-to-run identical, masked positions left out, an out-of-range id skipped and flagged —
+    at the one-workgroup sort's limit and past it."""
+    V, D = 5000, 24
+    ids = zipf_ids(rng, n, V).astype(np.int32)
+    ids[7] = V + 1  # OOB
+    keep = rng.random(n) < 0.9
+    rows = rng.standard_normal((n, D)).astype(np.float32)
+    ok = keep & (ids >= 0) & (ids < V)
+    ref = np.zeros((V, D))
+    np.add.at(ref, ids[ok].astype(np.int64), rows[ok].astype(np.float64))
+    gi = torch.from_numpy(ids).to(DEV)
+    gv = torch.from_numpy(keep.astype(np.uint8)).to(DEV)
+    gr = torch.from_numpy(rows).to(DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(L.lib().rs_index_add_rows_workspace_size(n, D), dtype=torch.uint8, device=DEV)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(V, D, device=DEV)
+        L.call("rs_index_add_rows", L.ptr(gi), L.id_dtype_code(gi), n, L.ptr(gv), L.ptr(gr), D, V,
+               L.ptr(out), L.ptr(err), L.ptr(ws), ws.numel(), L.stream_ptr(DEV))
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    got = outs[0].cpu().numpy()
+    cnt = np.maximum(np.bincount(ids[ok].astype(np.int64), minlength=V), 1)[:, None]
+    assert (np.abs(got - ref) <= 1e-5 * (np.abs(ref) + np.sqrt(cnt) * 4.0)).all()
+    if keep[7]:  # a masked-out position is not an error
+        assert int(err.item()) != 0
+
+
 @pytest.mark.parametrize("n", [(1 << 17) - 1, 1 << 17, (1 << 20) - 1, 1 << 20])
 @pytest.mark.parametrize("masked", [False, True])
 def test_sort_ids_tile_size_switch_points(n, masked, rng):
