@@ -15,7 +15,7 @@ import torch
 
 from ..functional import binary_crossentropy
 from ..metrics import AUC
-from ..optim import KerasAdam, SparseAdam, SparseSGD
+from ..optim import FusedKerasAdam, KerasAdam, SparseAdam, SparseSGD
 from ..synthetic import aliccp_batch, scaled_vocab
 from . import ESMM, FEAT_VOCAB, MMOE, BaseModel
 
@@ -58,15 +58,23 @@ class MultiTaskStep:
             if slab is not table:
                 raise ValueError("keras_adam_deferred: one GPU (the row-sharded slab applies "
                                  "inside its exchange)")
-            self.opt_dense = KerasAdam(dense, lr=lr)
+            self.opt_dense = self._dense_adam(dense, lr)
             self.opt_sparse = SparseAdam([table], lr=lr, mode="keras", fused=True,
                                          defer_join=True, defer_decay=True)
         else:
-            self.opt_dense = KerasAdam(dense, lr=lr)
+            self.opt_dense = self._dense_adam(dense, lr)
             self.opt_sparse = SparseAdam([table], lr=lr, mode="keras" if optimizer == "keras_adam" else "lazy")
         self.sharded = slab is not table
         if self.sharded:
             slab.set_optimizer(self.opt_sparse)
+
+    @staticmethod
+    def _dense_adam(dense, lr):
+        """Keras Adam of the dense parameters: the flat-buffer form on the GPU (one fused update
+        launch, same roundings), the foreach form elsewhere."""
+        if dense and all(p.is_cuda for p in dense):
+            return FusedKerasAdam(dense, lr=lr)
+        return KerasAdam(dense, lr=lr)
 
     def __call__(self, feats, label):
         self.opt_dense.zero_grad(set_to_none=True)
