@@ -367,7 +367,7 @@ def main():
         # every table densified and updated by Keras Adam each step (GraphKerasAdam: parameter,
         # m, v read and written = 24 B per element, the densified gradient written and read =
         # 8 B): 32 B per parameter element, over the whole replayed step
-        n_el = sum(p.numel() for p in m.parameters())
+        n_el = sum(t.weight.numel() for t in m.tables())  # the tables are the variables
         by = 32 * n_el
         gbs = by / sec / 1e9
         out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
