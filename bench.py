@@ -64,8 +64,8 @@ PMC_SYMBOLS = [
     ("rs_dlrm_interaction_bwd_rank1", r"dlrm_bwd_pipe", "dlrm_bwd_pipe"),
     # the slot-segmented sort's pass-0 histogram runs once per sort (the LSD form's pass-0
     # histogram, keys built from the ids, when a slab takes that form)
-    ("rs_sort_ids_slots", r"slot_sort_|radix_|scan_|count_unique",
-     r"slot_sort_hist0_kernel|radix_hist_kernel<\d+, true"),
+    ("rs_sort_ids_slots", r"slot_sort_|small_sort|radix_|scan_|count_unique",
+     r"slot_sort_hist0_kernel|small_sort_kernel|radix_hist_kernel<\d+, true"),
     ("rs_embedding_apply", r"seg_tile|seg_group|seg_chunk|seg_fixup", "seg_tile|seg_group"),
 ]
 
@@ -131,8 +131,8 @@ def parse():
     return ap.parse_args()
 
 
-PMC_KERNEL_REGEX = ("dlrm_train_chunk|inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|radix_|scan_|"
-                    "count_unique|seg_tile|seg_group|seg_chunk|seg_fixup")
+PMC_KERNEL_REGEX = ("dlrm_train_chunk|inter_fwd_mfma|dlrm_fwd_dx_pipe|dlrm_bwd_pipe|slot_sort_|"
+                    "small_sort|radix_|scan_|count_unique|seg_tile|seg_group|seg_chunk|seg_fixup")
 FETCH_CORRECTION = 2.0  # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reports 1/2 of 16 B/lane reads
 
 

@@ -116,3 +116,17 @@ def test_graph_keras_adam_flat_layout_cpu():
         assert torch.all(opt.grad_flat[o:o + n] == float(i + 1))
         pad_mask[o:o + n] = False
     assert torch.all(opt.grad_flat[pad_mask] == 0)
+
+
+def test_bench_pmc_filter_keeps_every_family_main_kernel():
+    """bench.py's PMC passes filter kernels by PMC_KERNEL_REGEX and count each family's calls by
+    its main kernel: a main kernel the filter drops leaves the family at 0 calls and the line's
+    traffic null (a round-5 regression: the slot-segmented sort's kernels were filtered out)."""
+    import re
+
+    import bench
+
+    for entry, _, main in bench.PMC_SYMBOLS:
+        for alt in main.split("|"):
+            name = "void rs::" + re.sub(r"\\d\+", "9", alt).replace("\\", "") + "(...)"
+            assert re.search(bench.PMC_KERNEL_REGEX, name), (entry, alt)
