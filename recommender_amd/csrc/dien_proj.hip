@@ -130,17 +130,44 @@ __global__ __launch_bounds__(256) void masked_proj_kernel(const float* __restric
   }
 }
 
-// dx[r, k] = Σ_n d[r, n]·W[k, n] for the listed rows, 0 for the rows whose mask is 0; K <= 64,
-// N <= NM. Wave gw zeroes the masked rows among rows [16 gw, 16 gw + 16) and computes listed
-// rows [16 gw, 16 gw + 16) of the list: the d rows' loads issued together and staged in the
-// wave's LDS (read back as broadcasts), W's row k in lane k's VGPRs (staged once per block
-// through LDS, and only by blocks that have listed rows).
+// The masked rows' dx: 0, or the addend (its loads issued together). Wave gw takes rows
+// [16 gw, 16 gw + 16). No LDS: full occupancy for what is a copy / fill of most of the B·L rows
+// (it shared the listed-row kernel's 57 KB of LDS per block before, at 2 blocks per CU).
+__global__ __launch_bounds__(256) void masked_fill_kernel(const uint8_t* __restrict__ mask,
+                                                          int64_t R, int K,
+                                                          float* __restrict__ dx, int64_t lddx,
+                                                          const float* __restrict__ add,
+                                                          int64_t ldadd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = gw * 16;
+  const int64_t rl = r0 + (lane & 15);
+  const uint64_t zm = __ballot(lane < 16 && rl < R && mask[rl] == 0);
+  if (!zm) return;
+  float v[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int e = lane + 64 * it;
+    const int i = e / K, k = e - i * K;
+    v[it] = (add && e < 16 * K && ((zm >> i) & 1ull)) ? add[(r0 + i) * ldadd + k] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int e = lane + 64 * it;
+    const int i = e / K, k = e - i * K;
+    if (e < 16 * K && ((zm >> i) & 1ull)) dx[(r0 + i) * lddx + k] = v[it];
+  }
+}
+
+// dx[r, k] = Σ_n d[r, n]·W[k, n] (+ add[r, k]) for the listed rows; K <= 64, N <= NM (the masked
+// rows are masked_fill_kernel's). Wave gw computes listed rows [16 gw, 16 gw + 16): the d rows'
+// loads issued together and staged in the wave's LDS (read back as broadcasts), W's row k in lane
+// k's VGPRs (staged once per block through LDS, and only by blocks that have listed rows).
 template <int NM>
 __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict__ d, int64_t ldd,
                                                         const float* __restrict__ W,
-                                                        const uint8_t* __restrict__ mask,
                                                         const int32_t* __restrict__ idx,
-                                                        const int32_t* __restrict__ count, int64_t R,
+                                                        const int32_t* __restrict__ count,
                                                         int K, int N, float* __restrict__ dx,
                                                         int64_t lddx, const float* __restrict__ add,
                                                         int64_t ldadd) {
@@ -149,27 +176,6 @@ __global__ __launch_bounds__(256) void masked_dx_kernel(const float* __restrict_
   __shared__ float wsh[64 * NM];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
-  // (A) the masked rows of this wave's 16 rows: 0, or the addend (its loads issued together)
-  {
-    const int64_t r0 = gw * 16;
-    const int64_t rl = r0 + (lane & 15);
-    const uint64_t zm = __ballot(lane < 16 && rl < R && mask[rl] == 0);
-    if (zm) {
-      float v[16];
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int e = lane + 64 * it;
-        const int i = e / K, k = e - i * K;
-        v[it] = (add && e < 16 * K && ((zm >> i) & 1ull)) ? add[(r0 + i) * ldadd + k] : 0.f;
-      }
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int e = lane + 64 * it;
-        const int i = e / K, k = e - i * K;
-        if (e < 16 * K && ((zm >> i) & 1ull)) dx[(r0 + i) * lddx + k] = v[it];
-      }
-    }
-  }
   const int64_t cnt = *count;
   if ((int64_t)blockIdx.x * 64 >= cnt) return;  // block-uniform: no listed rows here
   for (int e = threadIdx.x; e < K * N; e += 256) wsh[e] = W[e];
@@ -396,7 +402,9 @@ extern "C" int32_t rs_masked_dx_acc(const float* d, int64_t ldd, const float* W,
   RS_CHECK_ARG(d && W && mask && idx && count && dx, "null pointer");
   hipStream_t st = as_stream(stream);
   const int grid = (int)ceil_div(R, 64);  // one wave per 16 rows (and per 16 listed rows)
-#define RS_DX(NM) masked_dx_kernel<NM><<<grid, 256, 0, st>>>(d, ldd, W, mask, idx, count, R, K, N, dx, lddx, add, ldadd)
+  masked_fill_kernel<<<grid, 256, 0, st>>>(mask, R, K, dx, lddx, add, ldadd);
+  RS_CHECK_LAUNCH();
+#define RS_DX(NM) masked_dx_kernel<NM><<<grid, 256, 0, st>>>(d, ldd, W, idx, count, K, N, dx, lddx, add, ldadd)
   if (N <= 64) RS_DX(64);
   else if (N <= 112) RS_DX(112);
   else if (N <= 128) RS_DX(128);
