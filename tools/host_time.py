@@ -1,6 +1,9 @@
 """Host issue cost of the north-star DLRM step (run under gpurun): the time the host needs to
 queue N steps while the GPU is held busy by a long sleep kernel queued first (so no launch ever
-waits for the device), against the GPU-bound step time. python tools/host_time.py [--prefetch 1]"""
+waits for the device), against the GPU-bound step time. python tools/host_time.py [--prefetch 1]
+[--sharded 1 --batch 8192]: the row-sharded slab's fused step at world 1 (its exchange kernels,
+its collectives as copies) — the host cost a strong-scaling rank would pay, minus the
+collectives and the world > 1 extras (rows ahead, owner halves)"""
 import argparse
 import os
 import sys
@@ -18,16 +21,28 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--prefetch", type=int, default=0)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--profile", type=int, default=0)
+ap.add_argument("--sharded", type=int, default=0)
+ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
 L.load()
 dev = torch.device("cuda", 0)
-S, D, V, B = 26, 128, 40_000_000, 65536
+S, D, V, B = 26, 128, 40_000_000, a.batch
 cards = criteo_cardinalities(V, S)
 g = torch.Generator(device=dev)
 g.manual_seed(4)
-m = build_model("DLRM", D, V, S, 13, dev, slot_cardinalities=cards, bottom=[512, 256, D],
-                top=[512, 256, 1], generator=g)
-st = TrainStep(m, "sgd", lr=0.01, fused=True, defer_sparse_join=True)
+if a.sharded:
+    from recommender_amd.ctr.model import DLRM
+    from recommender_amd.sharded import Comm, ShardedSlabEmbedding
+
+    comm = Comm()
+    emb = ShardedSlabEmbedding(cards, D, comm, device=dev, generator=g)
+    m = DLRM([512, 256, D], [512, 256, 1], D, V, S, 13, device=dev, generator=g,
+             embedding_layer=emb)
+    st = TrainStep(m, "sgd", lr=0.01, fused=True, comm=comm, defer_sparse_join=True)
+else:
+    m = build_model("DLRM", D, V, S, 13, dev, slot_cardinalities=cards, bottom=[512, 256, D],
+                    top=[512, 256, 1], generator=g)
+    st = TrainStep(m, "sgd", lr=0.01, fused=True, defer_sparse_join=True)
 rng = np.random.default_rng(4)
 pool = [tuple(torch.from_numpy(x).to(dev) for x in criteo_batch(rng, B, cards)) for _ in range(4)]
 P = len(pool)
@@ -63,6 +78,7 @@ host = (time.perf_counter() - t0) / a.steps
 if a.profile:
     pr.disable()
 torch.cuda.synchronize()
-print(f"prefetch {a.prefetch}: step {gpu * 1e3:.3f} ms, host issue {host * 1e3:.3f} ms/step")
+print(f"sharded {a.sharded} batch {B} prefetch {a.prefetch}: step {gpu * 1e3:.3f} ms, "
+      f"host issue {host * 1e3:.3f} ms/step")
 if a.profile:
     pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
