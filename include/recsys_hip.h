@@ -114,6 +114,14 @@ int32_t rs_sort_ids_masked(const void* ids, int32_t id_dtype, int64_t n_ids, con
                            uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* n_unique,
                            int32_t* err_flag, void* workspace, size_t ws_bytes, void* stream);
 
+/* The stable (row, position) sort of n_runs equal runs of n_ids / n_runs int32 rows, each
+ * ascending with its padding (ids < 0) at the end — the row-sharded slab's owner side, one run
+ * per source rank: a merge by binary searches, one launch; the output equals rs_sort_ids_masked's
+ * with the padding masked (entries past a run's valid prefix take the sentinel n_rows, in
+ * position order; rows >= n_rows among them set RS_ERRBIT_OOB). */
+int32_t rs_sort_ids_runs(const int32_t* ids, int64_t n_ids, int32_t n_runs, int64_t n_rows,
+                         uint32_t* sorted_rows, int32_t* sorted_pos, int32_t* err_flag,
+                         void* stream);
 /* rs_sort_ids_masked (valid may be NULL) with the largest slot's row count given: when the ids
  * are [B, n_slots] (B <= 131072, n_slots <= 64), one GPU, and every slot has < 2^24 rows, the
  * sort runs slot by slot (the slot of position p is p % n_slots: the order over slots is free) in

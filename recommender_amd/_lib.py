@@ -60,6 +60,7 @@ _SIGS = {
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
     "rs_sort_ids": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
     "rs_sort_ids_masked": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_sort_ids_runs": (_i32, [_p, _i64, _i32, _i64, _p, _p, _p, _p]),
     "rs_sort_ids_slots": (_i32, [_p, _i32, _i64, _p, _p, _i32, _i64, _i64, _p, _p, _p, _p, _p, _sz,
                                  _p]),
     "rs_sort_ids_sharded": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _sz,

@@ -1289,6 +1289,86 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Sorted runs merged (round 5): the row-sharded slab's owner receives n_runs blocks of run_len
+// owner-local rows, each ascending (its source's unique rows in key order) with its padding
+// (ids < 0) at the end; the stable sort of all of them by (row, position) is a merge. Element j
+// of run s lands at j + Σ_{s' < s} #{run s' rows <= its row} + Σ_{s' > s} #{run s' rows < its
+// row} (binary searches of the other runs' valid prefixes); entries past a run's valid prefix
+// (padding, rows >= n_rows: flagged) take the sentinel n_rows after every valid row, in position
+// order — the masked radix sort's output, in one launch instead of nine.
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxRuns = 1024;
+
+__global__ __launch_bounds__(256) void runs_merge_kernel(const int32_t* __restrict__ ids, int64_t n,
+                                                         int n_runs, int64_t run_len,
+                                                         int64_t n_rows, uint32_t* __restrict__ rows_out,
+                                                         int32_t* __restrict__ pos_out,
+                                                         int32_t* __restrict__ err_flag) {
+  __shared__ int64_t vl[kMaxRuns];    // valid prefix length of each run
+  __shared__ int64_t padb[kMaxRuns];  // entries past the valid prefixes of the runs before
+  __shared__ int64_t nvalid;
+  for (int r = threadIdx.x; r < n_runs; r += blockDim.x) {
+    const int32_t* run = ids + (int64_t)r * run_len;
+    int64_t lo = 0, hi = run_len;  // first index whose id is not a row (monotone predicate)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      const int32_t v = run[mid];
+      if (v >= 0 && v < n_rows) lo = mid + 1;
+      else hi = mid;
+    }
+    vl[r] = lo;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t acc = 0, pad = 0;
+    for (int r = 0; r < n_runs; ++r) {
+      padb[r] = pad;
+      acc += vl[r];
+      pad += run_len - vl[r];
+    }
+    nvalid = acc;
+  }
+  __syncthreads();
+  bool oob = false;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(e / run_len);
+    const int64_t j = e - (int64_t)s * run_len;
+    const int32_t key = ids[e];
+    int64_t out;
+    uint32_t kout;
+    if (j < vl[s]) {
+      out = j;
+      for (int r = 0; r < n_runs; ++r) {
+        if (r == s) continue;
+        const int32_t* run = ids + (int64_t)r * run_len;
+        int64_t lo = 0, hi = vl[r];
+        if (r < s) {  // upper bound: equal rows of earlier runs come first
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (run[mid] <= key) lo = mid + 1; else hi = mid;
+          }
+        } else {      // lower bound
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (run[mid] < key) lo = mid + 1; else hi = mid;
+          }
+        }
+        out += lo;
+      }
+      kout = (uint32_t)key;
+    } else {
+      out = nvalid + padb[s] + (j - vl[s]);
+      kout = (uint32_t)n_rows;
+      if (key >= n_rows) oob = true;
+    }
+    rows_out[out] = kout;
+    pos_out[out] = (int32_t)e;
+  }
+  if (__any(oob) && (threadIdx.x & 63) == 0) flag_oob(err_flag);
+}
+
 static bool small_eligible(int64_t n_ids, int n_slots, int world, int64_t n_rows) {
   return world == 1 && n_slots == 1 && n_ids >= 1 && n_ids <= kSmallMax && n_rows <= kSmallMaxRows;
 }
@@ -1576,5 +1656,20 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
     count_unique_kernel<<<cblocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)key_space, n_unique);
     RS_CHECK_LAUNCH();
   }
+  return RS_OK;
+}
+
+extern "C" int32_t rs_sort_ids_runs(const int32_t* ids, int64_t n_ids, int32_t n_runs,
+                                    int64_t n_rows, uint32_t* sorted_rows, int32_t* sorted_pos,
+                                    int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(n_ids >= 0 && n_ids < (int64_t(1) << 31), "n_ids out of range");
+  RS_CHECK_ARG(n_runs >= 1 && n_runs <= kMaxRuns && n_ids % n_runs == 0, "n_runs must divide n_ids");
+  RS_CHECK_ARG(n_rows > 0 && n_rows < (int64_t(1) << 31) - 1, "n_rows out of range");
+  if (n_ids == 0) return RS_OK;
+  RS_CHECK_ARG(ids && sorted_rows && sorted_pos, "null pointer");
+  const int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
+  runs_merge_kernel<<<blocks, 256, 0, as_stream(stream)>>>(ids, n_ids, n_runs, n_ids / n_runs,
+                                                           n_rows, sorted_rows, sorted_pos, err_flag);
+  RS_CHECK_LAUNCH();
   return RS_OK;
 }

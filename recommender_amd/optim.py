@@ -85,6 +85,26 @@ class SortedIds:
                    L.ptr(self.n_unique), L.ptr(err_flag), L.ptr(w), w.numel(), L.stream_ptr(dev))
 
     @classmethod
+    def from_runs(cls, ids: torch.Tensor, n_runs: int, n_rows: int,
+                  err_flag: torch.Tensor | None = None) -> "SortedIds":
+        """The sort of n_runs equal runs of int32 rows, each ascending with its padding (< 0) at
+        the end (a row-sharded owner's received slots, one run per source rank), as the masked
+        sort would give it: a merge (rs_sort_ids_runs), one launch."""
+        ids = ids.contiguous()
+        L.require_device(ids, "ids")
+        if ids.dtype != torch.int32:
+            raise ValueError("from_runs: int32 rows")
+        self = cls.__new__(cls)
+        n = ids.numel()
+        self.n = n
+        self.rows = torch.empty(n, dtype=torch.int32, device=ids.device)
+        self.pos = torch.empty(n, dtype=torch.int32, device=ids.device)
+        self.n_unique = None
+        L.call("rs_sort_ids_runs", L.ptr(ids), n, int(n_runs), int(n_rows), L.ptr(self.rows),
+               L.ptr(self.pos), L.ptr(err_flag), L.stream_ptr(ids.device))
+        return self
+
+    @classmethod
     def for_table(cls, table: Embedding, ids: torch.Tensor, ws: _Workspace | None = None,
                   count_unique: bool = True, valid: torch.Tensor | None = None):
         return cls(ids, table.input_dim, table.slot_offsets, table.err_flag, ws, count_unique,

@@ -483,14 +483,17 @@ class ShardedSlabEmbedding(nn.Module):
                 raise RuntimeError("ShardedSlabEmbedding has no optimizer (set_optimizer)")
             opt = self.optimizer
             params = opt._params()
-            valid = (recv_ids >= 0).to(torch.uint8)
             if self.world > 1 and not global_grads:
                 if opt.kind == L.RS_OPT_SGD:
                     params.lr = params.lr / self.world  # same as scaling the gradient
                 else:
                     recv_grad.mul_(1.0 / self.world)
+            # the received slots are W runs (one per source rank), each its source's rows in
+            # key order with the padding at the end: merged, not radix-sorted (same order as the
+            # masked sort: source-rank-major among equal rows, padding left out)
+            sorted_ids = SortedIds.from_runs(recv_ids, W, self.shard.input_dim, self.err_flag)
             # every owner applies (an owner no rank sent a row to still runs Keras' dense decay)
-            opt.apply(self.shard, recv_ids, recv_grad, params, valid=valid)
+            opt.apply(self.shard, recv_ids, recv_grad, params, sorted_ids=sorted_ids)
         self._apply_count += 1
         self._last_applied = st["seq"]
         g.record_stream(self.side)

@@ -162,6 +162,30 @@ def test_sort_ids_small_one_workgroup(n, V, masked, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("runs,run_len,V", [(1, 1000, 500), (2, 4096, 30_000), (3, 777, 50),
+                                             (8, 35_000, 5_000_000)])
+def test_sort_ids_runs_merge_equals_masked_sort(runs, run_len, V, rng):
+    """rs_sort_ids_runs (the row-sharded owner's merge of its W received blocks): each run
+    ascending unique rows then -1 padding, rows shared between runs, an all-padding run and an
+    out-of-range row at a run's end — bit-exact against the oracle's stable sort with the padding
+    masked, and the OOB row flagged."""
+    ids = np.full((runs, run_len), -1, np.int64)
+    for r in range(runs):
+        k = 0 if (runs > 2 and r == 1) else int(rng.integers(run_len // 3, run_len + 1))
+        ids[r, :k] = np.sort(rng.choice(V, size=min(k, V), replace=False))[:k]
+    if runs > 1 and (ids[0] >= 0).sum() < run_len:
+        k0 = int((ids[0] >= 0).sum())
+        ids[0, k0] = V + 2  # a row past the table: a sentinel, flagged
+    flat = ids.reshape(-1).astype(np.int32)
+    keep = (flat >= 0) & (flat < V)
+    rows_ref, pos_ref, _ = O.sort_ids(np.where(keep, flat, -1).astype(np.int64), V)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = SortedIds.from_runs(torch.from_numpy(flat).to(DEV), runs, V, err)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert (int(err.item()) != 0) == bool((flat >= V).any())
+
+
 @pytest.mark.parametrize("n", [16384, 40_000])
 def test_index_add_rows_fixed_order(n, rng):
     """rs_index_add_rows (PinSage's deterministic scatter-add: sort + tiled segmented sum) through
