@@ -171,8 +171,8 @@ def test_sort_ids_runs_merge_equals_masked_sort(runs, run_len, V, rng):
     masked, and the OOB row flagged."""
     ids = np.full((runs, run_len), -1, np.int64)
     for r in range(runs):
-        k = 0 if (runs > 2 and r == 1) else int(rng.integers(run_len // 3, run_len + 1))
-        ids[r, :k] = np.sort(rng.choice(V, size=min(k, V), replace=False))[:k]
+        k = 0 if (runs > 2 and r == 1) else min(int(rng.integers(run_len // 3, run_len + 1)), V)
+        ids[r, :k] = np.sort(rng.choice(V, size=k, replace=False))
     if runs > 1 and (ids[0] >= 0).sum() < run_len:
         k0 = int((ids[0] >= 0).sum())
         ids[0, k0] = V + 2  # a row past the table: a sentinel, flagged
