@@ -147,7 +147,10 @@ int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_t n_ids,
                             void* stream);
 /* From sorted keys: uniq_keys[u] (ascending), inverse[p] = u of position p (-1 for an OOB id),
  * n_unique[1], and owner_counts[world] (unique keys per owner rank; may be NULL).
- * Workspace: rs_sort_ids_workspace_size(n_ids) suffices. */
+ * Workspace: rs_unique_inverse_workspace_size(n_ids) bytes; it begins with int32 [n_ids], the
+ * exclusive scan of the head flags — each sorted key's segment (unique) index — which
+ * rs_embedding_dedup_grad_mapped_range takes as seg_excl for the same sorted keys. */
+size_t rs_unique_inverse_workspace_size(int64_t n_ids);
 int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos, int64_t n_ids,
                           int64_t n_rows, int32_t world, uint32_t* uniq_keys, int32_t* inverse,
                           int32_t* n_unique, int32_t* owner_counts, void* workspace,
@@ -235,7 +238,9 @@ int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows, const int32_
 /* rs_embedding_dedup_grad_mapped over the keys in [key_lo, key_hi) only (segments numbered over
  * the whole key space n_rows, so two calls over adjoining ranges emit exactly the segments one
  * call does, with the same sums); seg_ready 1: the workspace already holds the segment ids of a
- * previous call on the same sorted keys. D = 128 with 16-byte aligned rows (the group walk).
+ * previous call on the same sorted keys; seg_excl (may be NULL): those segment ids given (the
+ * head of rs_unique_inverse's workspace over the same keys), seg_ready then ignored. D = 128
+ * with 16-byte aligned rows (the group walk).
  * The row-sharded step deduplicates its two owner halves apart, so the first half's gradient
  * all-to-all runs while the second half is summed. */
 int32_t rs_embedding_dedup_grad_mapped_range(const uint32_t* sorted_rows, const int32_t* sorted_pos,
@@ -243,6 +248,7 @@ int32_t rs_embedding_dedup_grad_mapped_range(const uint32_t* sorted_rows, const 
                                              const float* row_scale, int32_t scale_group,
                                              int32_t dim, int64_t n_rows, uint32_t key_lo,
                                              uint32_t key_hi, int32_t seg_ready,
+                                             const int32_t* seg_excl,
                                              const int32_t* seg_map, uint32_t* uniq_rows,
                                              float* uniq_grad, void* workspace, size_t ws_bytes,
                                              void* stream);

@@ -76,7 +76,8 @@ _SIGS = {
     "rs_embedding_dedup_grad_mapped": (_i32, [_p, _p, _i64, _p, _p, _i32, _i32, _i64, _p, _p,
                                               _p, _p, _sz, _p]),
     "rs_embedding_dedup_grad_mapped_range": (_i32, [_p, _p, _i64, _p, _p, _i32, _i32, _i64, _u32,
-                                                    _u32, _i32, _p, _p, _p, _p, _sz, _p]),
+                                                    _u32, _i32, _p, _p, _p, _p, _p, _sz, _p]),
+    "rs_unique_inverse_workspace_size": (_sz, [_i64]),
     "rs_exchange_pack": (_i32, [_p, _p, _p, _i32, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p]),
     "rs_exchange_excess": (_i32, [_p, _i32, _i64, _p, _p]),
     "rs_exchange_pack_spill": (_i32, [_p, _p, _p, _i32, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p,

@@ -1344,7 +1344,8 @@ extern "C" int32_t rs_embedding_dedup_grad_scaled(const uint32_t* sorted_rows,
 extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
     const uint32_t* sorted_rows, const int32_t* sorted_pos, int64_t n_ids, const float* grad_out,
     const float* row_scale, int32_t scale_group, int32_t dim, int64_t n_rows, uint32_t key_lo,
-    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_map, uint32_t* uniq_rows,
+    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_excl, const int32_t* seg_map,
+    uint32_t* uniq_rows,
     float* uniq_grad, void* workspace, size_t ws_bytes, void* stream);
 
 extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
@@ -1356,14 +1357,15 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped(const uint32_t* sorted_rows,
                                                   size_t ws_bytes, void* stream) {
   return rs_embedding_dedup_grad_mapped_range(sorted_rows, sorted_pos, n_ids, grad_out, row_scale,
                                               scale_group, dim, n_rows, 0u, (uint32_t)n_rows, 0,
-                                              seg_map, uniq_rows, uniq_grad, workspace, ws_bytes,
-                                              stream);
+                                              nullptr, seg_map, uniq_rows, uniq_grad, workspace,
+                                              ws_bytes, stream);
 }
 
 extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
     const uint32_t* sorted_rows, const int32_t* sorted_pos, int64_t n_ids, const float* grad_out,
     const float* row_scale, int32_t scale_group, int32_t dim, int64_t n_rows, uint32_t key_lo,
-    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_map, uint32_t* uniq_rows,
+    uint32_t key_hi, int32_t seg_ready, const int32_t* seg_excl, const int32_t* seg_map,
+    uint32_t* uniq_rows,
     float* uniq_grad, void* workspace, size_t ws_bytes, void* stream) {
   RS_CHECK_ARG(dim > 0 && n_ids >= 0 && n_rows > 0, "bad sizes");
   RS_CHECK_ARG(key_lo < key_hi && (int64_t)key_hi <= n_rows, "key range outside [0, n_rows)");
@@ -1380,7 +1382,9 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
   int32_t* seg = c.take<int32_t>(n_ids);
   void* scan_ws = c.take<char>(exclusive_scan_ws_size(n_ids));
   int blocks = (int)std::min<int64_t>(ceil_div(n_ids, 256), 4096);
-  if (!seg_ready) {  // segment ids over the whole key space (a second range call reuses them)
+  if (seg_excl) {
+    seg = const_cast<int32_t*>(seg_excl);  // given (rs_unique_inverse's, same sorted keys)
+  } else if (!seg_ready) {  // segment ids over the whole key space (a second range call reuses them)
     head_flags_kernel<<<blocks, 256, 0, st>>>(sorted_rows, n_ids, (uint32_t)n_rows, seg);
     RS_CHECK_LAUNCH();
     int32_t s = exclusive_scan_i32(seg, seg, n_ids, nullptr, scan_ws, exclusive_scan_ws_size(n_ids), st);

@@ -1562,6 +1562,13 @@ extern "C" int32_t rs_sort_ids_sharded(const void* ids, int32_t id_dtype, int64_
                        n_rows);
 }
 
+extern "C" size_t rs_unique_inverse_workspace_size(int64_t n_ids) {
+  Carver c(nullptr, 0);
+  c.take<int32_t>(n_ids > 0 ? n_ids : 1);
+  c.take<char>(exclusive_scan_ws_size(n_ids > 0 ? n_ids : 1));
+  return c.off + 256;
+}
+
 extern "C" int32_t rs_unique_inverse(const uint32_t* sorted_keys, const int32_t* sorted_pos,
                                      int64_t n_ids, int64_t n_rows, int32_t world,
                                      uint32_t* uniq_keys, int32_t* inverse, int32_t* n_unique,

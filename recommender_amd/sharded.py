@@ -198,7 +198,10 @@ class ShardedSlabEmbedding(nn.Module):
             inverse = torch.empty(n, dtype=torch.int32, device=dev)
             n_unique = torch.zeros(1, dtype=torch.int32, device=dev)
             counts = torch.zeros(W, dtype=torch.int32, device=dev)
-            w = self.ws.get("uniq", L.lib().rs_sort_ids_workspace_size(n), dev)
+            # this step's own workspace: its head is the segment index of every sorted key,
+            # which the backward's dedup reuses (no second head-flag scan)
+            w = torch.empty(L.lib().rs_unique_inverse_workspace_size(n), dtype=torch.uint8,
+                            device=dev)
             L.call("rs_unique_inverse", L.ptr(s.rows), L.ptr(s.pos), n, self.input_dim, W,
                    L.ptr(uniq), L.ptr(inverse), L.ptr(n_unique), L.ptr(counts), L.ptr(w),
                    w.numel(), L.stream_ptr(dev))
@@ -226,7 +229,7 @@ class ShardedSlabEmbedding(nn.Module):
         return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, recv_ids=recv_ids,
                     capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
                     inverse=inverse, excess=(excess_ready, host), seq=self._seq, early=None,
-                    late=None)
+                    late=None, seg_excl=w)
 
     def _rows_ahead_ok(self) -> bool:
         """Rows a step ahead need an update that changes only the rows it receives (SGD, lazy
@@ -391,7 +394,8 @@ class ShardedSlabEmbedding(nn.Module):
         self.view.weight = rows
         self.view.input_dim = W * (C + C2)
         self._st = dict(sorted=st["s"], slot_of=st["slot_of"], recv_ids=st["recv_ids"],
-                        recv_spill=recv_spill, capacity=C, spill=C2, seq=st["seq"])
+                        recv_spill=recv_spill, capacity=C, spill=C2, seq=st["seq"],
+                        seg_excl=st["seg_excl"])
         return self.view, inverse.view(st["ids"].shape)
 
     def exchange(self, ids: torch.Tensor):
@@ -438,12 +442,14 @@ class ShardedSlabEmbedding(nn.Module):
             w = self.ws.get("dedup", L.lib().rs_dedup_workspace_size(max(s.n, 1), D), dev)
 
             def dedup(lo, hi, seg_ready):
+                # the segment ids come from exchange_begin's unique pass over the same keys
                 if s.n:
                     L.call("rs_embedding_dedup_grad_mapped_range", L.ptr(s.rows), L.ptr(s.pos),
                            s.n, L.ptr(g), L.ptr(row_scale),
                            self.n_slots if row_scale is not None else 1, D, self.key_space, lo,
-                           hi, seg_ready, L.ptr(st["slot_of"]), L.ptr(uniq_rows),
-                           L.ptr(send_grad), L.ptr(w), w.numel(), L.stream_ptr(dev))
+                           hi, seg_ready, L.ptr(st["seg_excl"]), L.ptr(st["slot_of"]),
+                           L.ptr(uniq_rows), L.ptr(send_grad), L.ptr(w), w.numel(),
+                           L.stream_ptr(dev))
 
             if W >= 2 and D == 128 and self.split_halves:
                 # owner halves [0, W/2) and [W/2, W): keys are owner-major, so half A's rows are

@@ -29,7 +29,7 @@ out1 = torch.zeros(U + 1, D, device=dev); out2 = torch.zeros(U + 1, D, device=de
 dws = torch.empty(L.lib().rs_dedup_workspace_size(n, D), dtype=torch.uint8, device=dev)
 K = V // 2
 def call(out, lo, hi, ready):
-    L.call("rs_embedding_dedup_grad_mapped_range", L.ptr(rows), L.ptr(pos), n, L.ptr(grad), L.ptr(scale), S, D, V, lo, hi, ready, L.ptr(seg_map), L.ptr(uniq_rows), L.ptr(out), L.ptr(dws), dws.numel(), st)
+    L.call("rs_embedding_dedup_grad_mapped_range", L.ptr(rows), L.ptr(pos), n, L.ptr(grad), L.ptr(scale), S, D, V, lo, hi, ready, None, L.ptr(seg_map), L.ptr(uniq_rows), L.ptr(out), L.ptr(dws), dws.numel(), st)
 def one():
     call(out1, 0, V, 0)
 def two():
