@@ -145,6 +145,7 @@ class ShardedSlabEmbedding(nn.Module):
         self.rows_ahead = True
         self.rows_ahead_modes = {"fresh": 0, "late": 0, "full": 0}
         self.late_slots = [0, 0]  # late steps: (slots re-sent W·C_late, capacity slots W·C)
+        self._overflow = None
         self._stamp = None  # int32 per local row: the last finished step (seq) that requested it
         self._seq = 0  # exchange_begin count (each step's seq)
         self._apply_count = 0
@@ -196,8 +197,9 @@ class ShardedSlabEmbedding(nn.Module):
             n = ids.numel()
             uniq = torch.empty(n, dtype=torch.int32, device=dev)
             inverse = torch.empty(n, dtype=torch.int32, device=dev)
-            n_unique = torch.zeros(1, dtype=torch.int32, device=dev)
-            counts = torch.zeros(W, dtype=torch.int32, device=dev)
+            # rs_unique_inverse zeroes the count and writes every owner's count: no fills here
+            n_unique = torch.empty(1, dtype=torch.int32, device=dev)
+            counts = torch.empty(W, dtype=torch.int32, device=dev)
             # this step's own workspace: its head is the segment index of every sorted key,
             # which the backward's dedup reuses (no second head-flag scan)
             w = torch.empty(L.lib().rs_unique_inverse_workspace_size(n), dtype=torch.uint8,
@@ -211,10 +213,13 @@ class ShardedSlabEmbedding(nn.Module):
             send_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
             slot_of = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
             inv_slot = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            # the packing's past-capacity flag is not read (the spill round sends those rows):
+            # one persistent word, not a fill per step
+            if self._overflow is None:
+                self._overflow = torch.zeros(1, dtype=torch.int32, device=dev)
             L.call("rs_exchange_pack", L.ptr(uniq), L.ptr(n_unique), L.ptr(counts), W,
                    self.stride, C, L.ptr(inverse), n, L.ptr(send_ids), L.ptr(slot_of),
-                   L.ptr(inv_slot), L.ptr(overflow), L.stream_ptr(dev))
+                   L.ptr(inv_slot), L.ptr(self._overflow), L.stream_ptr(dev))
             # the spill round's size: every rank's largest excess over C, all-reduced (MAX)
             excess = torch.empty(1, dtype=torch.int64, device=dev)
             L.call("rs_exchange_excess", L.ptr(counts), W, C, L.ptr(excess), L.stream_ptr(dev))
