@@ -128,6 +128,10 @@ class ShardedSlabEmbedding(nn.Module):
         self.view = _UniqueRows(self)
         self.ws = _Workspace()
         self.side = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+        # exchange_begin's own stream: a later step's sort / unique / packing / row-id all-to-all
+        # read no table state, so they run beside this step's exchange and apply instead of
+        # queueing in front of them on the side stream
+        self.pre = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.optimizer: SparseOptimizer | None = None
         self._st = None  # per-step exchange state
         self._prefetched: list = []  # exchange_begin states queued ahead, FIFO (prefetch)
@@ -178,20 +182,23 @@ class ShardedSlabEmbedding(nn.Module):
         self.capacity = -(-(int(need * self.capacity_factor) + 256) // 256) * 256
 
     def exchange_begin(self, ids: torch.Tensor):
-        """Queue the first half of a step's exchange on the side stream: owner-major sort, unique
+        """Queue the first half of a step's exchange on its own stream: owner-major sort, unique
         / inverse + per-owner counts, the capacity-bounded packing (rs_exchange_pack: every
         unique row within the capacity gets a fixed slot in a [world, capacity] send block, each
-        position the slot of its row), the all-reduced largest excess over the capacity (the
-        spill round's size, rs_exchange_excess) and the all-to-all of the row ids. Nothing here
-        reads the table, so it may run a step ahead (prefetch); no host sync once the capacity
-        is known."""
+        position the slot of its row) and each rank's largest excess over the capacity (the
+        spill round's size, rs_exchange_excess). Nothing here reads the table, so it may run a
+        step ahead (prefetch); no host sync once the capacity is known. Its collectives (the
+        excess all-reduce, the row-id all-to-all: _begin_comm) are issued later — by the step
+        before's exchange_finish once that step's own rows are on their way, or by this step's —
+        so that RCCL, which runs collectives in issue order, never queues the current step's
+        row transfer behind a later step's sort."""
         L.require_device(ids, "ids")
         dev = ids.device
         ids = ids.contiguous()
         main = torch.cuda.current_stream(dev)
-        self.side.wait_stream(main)
+        self.pre.wait_stream(main)
         W = self.world
-        with torch.cuda.stream(self.side):
+        with torch.cuda.stream(self.pre):
             s = SortedIds(ids, self.input_dim, self.slot_offsets, self.err_flag, self.ws,
                           count_unique=False, world=W)
             n = ids.numel()
@@ -223,18 +230,42 @@ class ShardedSlabEmbedding(nn.Module):
             # the spill round's size: every rank's largest excess over C, all-reduced (MAX)
             excess = torch.empty(1, dtype=torch.int64, device=dev)
             L.call("rs_exchange_excess", L.ptr(counts), W, C, L.ptr(excess), L.stream_ptr(dev))
+        self._seq += 1
+        return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, send_ids=send_ids,
+                    capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
+                    inverse=inverse, excess_dev=excess, seq=self._seq, early=None, late=None,
+                    seg_excl=w, comm=False)
+
+    def _begin_comm(self, st):
+        """exchange_begin's collectives, on its stream: the spill round's size all-reduced (MAX)
+        and copied to the host (read by the step's exchange_finish), the row-id all-to-all."""
+        if st["comm"]:
+            return
+        dev, W, C = st["dev"], self.world, st["capacity"]
+        with torch.cuda.stream(self.pre):
+            excess = st["excess_dev"]
             self.comm.all_reduce_(excess, dist.ReduceOp.MAX)
             host = torch.empty(1, dtype=torch.int64, pin_memory=True)
             host.copy_(excess, non_blocking=True)
             excess_ready = torch.cuda.Event()
-            excess_ready.record(self.side)
+            excess_ready.record(self.pre)
             recv_ids = torch.empty(W * C, dtype=torch.int32, device=dev)
-            self.comm.all_to_all(recv_ids, send_ids)
-        self._seq += 1
-        return dict(ids=ids, s=s, slot_of=slot_of, inv_slot=inv_slot, recv_ids=recv_ids,
-                    capacity=C, dev=dev, uniq=uniq, n_unique=n_unique, counts=counts,
-                    inverse=inverse, excess=(excess_ready, host), seq=self._seq, early=None,
-                    late=None, seg_excl=w)
+            self.comm.all_to_all(recv_ids, st["send_ids"])
+            begun = torch.cuda.Event()
+            begun.record(self.pre)
+        st.update(excess=(excess_ready, host), recv_ids=recv_ids, begun=begun, comm=True)
+
+    def _on_side(self, st):
+        """Order the side stream after st's exchange_begin (its own stream) and mark st's device
+        tensors as used there (their memory is not reused before the side stream's work on them
+        has run)."""
+        if st.get("on_side"):
+            return
+        self.side.wait_event(st["begun"])
+        for v in list(st.values()) + [st["s"].rows, st["s"].pos]:
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(self.side)
+        st["on_side"] = True
 
     def _rows_ahead_ok(self) -> bool:
         """Rows a step ahead need an update that changes only the rows it receives (SGD, lazy
@@ -338,12 +369,14 @@ class ShardedSlabEmbedding(nn.Module):
         dev, W, C = st["dev"], self.world, st["capacity"]
         main = torch.cuda.current_stream(dev)
         D = self.output_dim
+        self._begin_comm(st)  # issued here when no step before did (no prefetch)
         ev, host = st["excess"]
         ev.synchronize()  # prefetched a step ahead: long done
         C2 = int(host.item())
         n = st["ids"].numel()
         recv_spill = None
         with torch.cuda.stream(self.side):
+            self._on_side(st)
             if st["early"] is None:  # not issued ahead: gathered now, after every queued apply
                 self._issue_early(st)
             rows_c, count0 = st["early"]
@@ -386,11 +419,14 @@ class ShardedSlabEmbedding(nn.Module):
                 rows = rows_c
             ready = torch.cuda.Event()
             ready.record(self.side)
-            # the next prefetched step's rows, gathered and sent beside this step's train kernel
+            # the next prefetched step: its collectives now, behind this step's row transfers;
+            # its rows (rows ahead) gathered and sent beside this step's train kernel
             st["recv_spill"] = recv_spill
-            if self._prefetched and self._rows_ahead_ok():
+            if self._prefetched:
                 nxt = self._prefetched[0][2]
-                if nxt["early"] is None:
+                self._begin_comm(nxt)
+                if nxt["early"] is None and self._rows_ahead_ok():
+                    self._on_side(nxt)
                     self._ahead(st, nxt)
         main.wait_event(ready)
         inverse = st["inv_slot"][:n]
