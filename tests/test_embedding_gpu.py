@@ -303,6 +303,42 @@ def test_sort_ids_slot_segmented(B, layout, masked, rng):
     assert int(s.n_unique.item()) == nu_ref
 
 
+@pytest.mark.parametrize("B", [2049, 6000, 65536, 131072])
+@pytest.mark.parametrize("pattern", ["one_id", "two_buckets", "sparse_buckets", "window_edges"])
+def test_sort_ids_slot_segmented_clustered_ids(B, pattern, rng):
+    """The slot-segmented sort on clustered wide-slot ids: one id for the whole slot, two hot
+    12-bit high-digit buckets, a few occupied buckets among 4096, and runs of 1500-2600 keys per
+    bucket — bit-exact vs the oracle's stable sort, with OOB ids and masked positions mixed in."""
+    cards = [1 << 24, 5000, 9_000_001, 4097]
+    S = len(cards)
+    so = np.concatenate([[0], np.cumsum(cards)]).astype(np.int64)
+    V = int(so[-1])
+    ids = np.empty((B, S), np.int64)
+    for j, c in enumerate(cards):
+        sh = max(int(c - 1).bit_length() - 12, 0)  # low bits below the bucket digit
+        if pattern == "one_id":
+            ids[:, j] = c // 3
+        elif pattern == "two_buckets":
+            ids[:, j] = np.where(rng.random(B) < 0.5, 7, (c - 1) >> sh << sh)
+            ids[::5, j] = rng.integers(0, c, ids[::5, j].shape)
+        elif pattern == "sparse_buckets":
+            buckets = rng.choice((c - 1 >> sh) + 1, 5, replace=False)
+            ids[:, j] = (rng.choice(buckets, B) << sh) + rng.integers(0, 1 << sh, B)
+            ids[:, j] = np.minimum(ids[:, j], c - 1)
+        else:  # runs of 1500..2600 keys per bucket over consecutive buckets
+            sizes = rng.integers(1500, 2600, B // 1500 + 2)
+            bucket = np.repeat(np.arange(sizes.size), sizes)[:B] % ((c - 1 >> sh) + 1)
+            ids[:, j] = np.minimum((bucket << sh) + rng.integers(0, 1 << sh, B), c - 1)
+    ids[::97, 2] = cards[2] + 3  # OOB
+    keep = rng.random(ids.size) < 0.9
+    s = SortedIds(torch.from_numpy(ids).to(DEV), V, torch.from_numpy(so).to(DEV),
+                  valid=torch.from_numpy(keep.astype(np.uint8)).to(DEV), max_slot_rows=max(cards))
+    rows_ref, pos_ref, nu_ref = O.sort_ids(np.where(keep, ids.reshape(-1), -1).reshape(ids.shape), V, so)
+    np.testing.assert_array_equal(s.rows.cpu().numpy().view(np.uint32), rows_ref)
+    np.testing.assert_array_equal(s.pos.cpu().numpy(), pos_ref)
+    assert int(s.n_unique.item()) == nu_ref
+
+
 def test_sort_ids_lsd_slot_sentinels(rng):
     """A slab with a slot past 2^24 rows takes the LSD sort: its sentinels (OOB ids in several
     slots, masked positions) come out grouped by slot like the slot-segmented sort's."""
