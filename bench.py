@@ -722,7 +722,15 @@ def main():
                                 "ms_per_step": round(tk / args.steps * 1e3, 3),
                                 "note": "excludes the deferred decay materialize() pays"},
                  "fused_step": bool(kstep.fused_step_ready(pool[0]))}
-        del kstep
+        # materialize replays only the (m, v) chunks that are not zero (a zero state decays to
+        # itself, exactly): its cost grows with the rows the run has touched
+        mt, vt, _ = kstep.opt_sparse._slots(model.embedding_layer)
+        keras["rows_with_state"] = int(((mt.abs().amax(dim=1) + vt.abs().amax(dim=1)) != 0).sum())
+        keras["rows"] = int(mt.shape[0])
+        keras["materialize_note"] = ("the replay skips zero (m, v) state (the identity for any "
+                                     "number of steps) without reading its weights; its cost "
+                                     "grows with rows_with_state as a run touches more rows")
+        del kstep, mt, vt
         torch.cuda.empty_cache()
 
     # N > 1 under strong scaling: the same step at --batch per GPU (weak scaling), for the record

@@ -990,6 +990,20 @@ __device__ __forceinline__ void keras_decay(float& w, float& m, float& v, float 
   w = w - upd;
 }
 
+// A (m, v) chunk whose m is +0 and v is ±0 in every element decays to itself and moves no
+// weight: m·β1 = +0, v·β2 = ±0, lr·(+0) / (√v + ε) = +0 and w − (+0) = w for every w (−0
+// included). Any number of such steps is the identity, so the sweep and the replay skip the
+// chunk — bit for bit the same state — without loading its weights or storing anything (the
+// rows Keras' dense decay walks but that no gradient has reached yet). A −0 in m is not skipped
+// (w = −0 would become +0).
+template <int VEC>
+__device__ __forceinline__ bool keras_state_zero(const float (&mm)[VEC], const float (&vv)[VEC]) {
+  bool z = true;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) z &= (__float_as_uint(mm[e]) == 0u) & (vv[e] == 0.0f);
+  return z;
+}
+
 // Keras dense sweep over untouched rows (touched rows were fully updated by the sparse pass)
 template <int VEC>
 __global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restrict__ w,
@@ -1006,9 +1020,10 @@ __global__ __launch_bounds__(256) void keras_dense_sweep_kernel(float* __restric
     if ((bitmap[row >> 5] >> (row & 31)) & 1u) continue;
     int64_t off = i * VEC;
     float ww[VEC], mm[VEC], vv[VEC];
-    RowIO<VEC>::load(w + off, ww);
     RowIO<VEC>::load(m + off, mm);
     RowIO<VEC>::load(v + off, vv);
+    if (keras_state_zero<VEC>(mm, vv)) continue;
+    RowIO<VEC>::load(w + off, ww);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) keras_decay(ww[e], mm[e], vv[e], p.lr, p.beta1, p.beta2, p.epsilon);
     RowIO<VEC>::store(w + off, ww);
@@ -1031,9 +1046,10 @@ __device__ __forceinline__ void keras_replay_row(float* w, float* m, float* v, i
   for (int col = gl * VEC; col < dim; col += lpr * VEC) {
     const int64_t off = r * dim + col;
     float ww[VEC], mm[VEC], vv[VEC];
-    RowIO<VEC>::load(w + off, ww);
     RowIO<VEC>::load(m + off, mm);
     RowIO<VEC>::load(v + off, vv);
+    if (keras_state_zero<VEC>(mm, vv)) continue;  // every replayed step is the identity
+    RowIO<VEC>::load(w + off, ww);
     for (int32_t st = from; st <= to; ++st) {
       const float lr = lr_hist[st];
 #pragma unroll

@@ -578,6 +578,54 @@ def test_one_call_sparse_entry_points_match_two_call(kind, rng):
         assert torch.equal(ms[0], ms[1]) and torch.equal(vs[0], vs[1])
 
 
+@pytest.mark.parametrize("dim", [128, 18, 7])
+def test_keras_decay_zero_state_skip_bit_exact(dim, rng):
+    """The Keras dense decay of rows without a gradient skips (m, v) chunks that are +0 / ±0 —
+    the identity for any number of steps — without touching their weights. Against the oracle's
+    Keras sparse apply with no gradient rows (oracle/embedding.py apply_keras_adam: the dense
+    decay of every row), bit for bit (signed zeros compared as bits): rows of zero state, rows
+    with m = -0 and w = -0 (not skipped: w becomes +0), m = +0 with v = -0, one nonzero element
+    in a zero row, and ordinary rows — one dense sweep, and a deferred replay of 5 steps
+    (rs_keras_adam_materialize) against 5 decays."""
+    from recommender_amd.optim import keras_adam_coefficients as kc
+
+    V = 64
+    w = rng.standard_normal((V, dim)).astype(np.float32)
+    m = (rng.standard_normal((V, dim)) * 1e-3).astype(np.float32)
+    v = (rng.random((V, dim)) * 1e-4).astype(np.float32)
+    m[:32] = 0.0
+    v[:32] = 0.0
+    m[4:8] = -0.0
+    w[4:8, ::2] = -0.0
+    w[8:12, 1::2] = -0.0  # +0 state: stays -0
+    v[12:16] = -0.0
+    m[16, dim // 2] = 1e-3  # one live element in a zero row
+    v[16, dim // 2] = 1e-6
+    bits = lambda a: a.view(np.uint32)  # noqa: E731
+    none = np.zeros(0, np.int64)
+    for steps in (1, 5):
+        tw, tm, tv = (torch.from_numpy(a.copy()).to(DEV) for a in (w, m, v))
+        ow, om, ov = w.copy(), m.copy(), v.copy()
+        lr_hist = np.zeros(steps + 1, np.float32)
+        for st in range(1, steps + 1):
+            c = O.keras_adam_coefficients(st)
+            lr_hist[st] = c["lr"]
+            ow, om, ov = O.apply_keras_adam(ow, om, ov, none, np.zeros((0, dim), np.float32), c)
+        if steps == 1:
+            bm = torch.zeros((V + 31) // 32, dtype=torch.int32, device=DEV)
+            L.call("rs_keras_adam_dense_sweep", L.ptr(tw), L.ptr(tm), L.ptr(tv), V, dim, kc(1),
+                   L.ptr(bm), L.stream_ptr(DEV))
+        else:
+            last = torch.zeros(V, dtype=torch.int32, device=DEV)
+            lr_t = torch.from_numpy(lr_hist).to(DEV)
+            L.call("rs_keras_adam_materialize", L.ptr(tw), L.ptr(tm), L.ptr(tv), L.ptr(last), V,
+                   dim, L.ptr(lr_t), steps, kc(steps), L.stream_ptr(DEV))
+        torch.cuda.synchronize()
+        for got, ref in ((tw, ow), (tm, om), (tv, ov)):
+            np.testing.assert_array_equal(bits(got.cpu().numpy()), bits(ref.astype(np.float32)))
+        assert (bits(ow[4:8, ::2]) == 0).all()  # -0 w under a -0 m: +0, as the formula gives
+
+
 @pytest.mark.parametrize("V,dim,n", [(2, 8, 540_000), (100, 8, 30_000), (2048, 8, 5000),
                                      (64, 256, 3000), (20, 16, 1), (7, 4, 0)])
 @pytest.mark.parametrize("id_dtype", [np.int32, np.int64])
