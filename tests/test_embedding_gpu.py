@@ -32,6 +32,27 @@ def test_gather_shared_table(dim, id_dtype, rng):
     assert not t.oob_detected()
 
 
+@pytest.mark.parametrize("dim,ld", [(18, 36), (18, 20), (6, 10), (18, 18), (16, 40), (7, 9)])
+def test_gather_strided_vs_oracle(dim, ld, rng):
+    """rs_embedding_fwd_strided into a column block of a wider row (out_ld > dim, the flat pair
+    form for even D that is not a multiple of 4): the block equals the oracle's lookup, OOB ids
+    read zero rows and flag, and every other column keeps its sentinel."""
+    V, n = 5000, 40_961
+    w = rng.standard_normal((V, dim)).astype(np.float32)
+    ids = rng.integers(0, V, n).astype(np.int64)
+    ids[::97] = V + 5
+    out = torch.full((n, ld), 7.0, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tw = torch.from_numpy(w).to(DEV)
+    ti = torch.from_numpy(ids).to(DEV)
+    L.call("rs_embedding_fwd_strided", L.ptr(tw), V, dim, L.ptr(ti), 1, n, None, 1, L.ptr(out),
+           ld, L.ptr(err), L.stream_ptr(DEV))
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got[:, :dim], O.embedding_lookup(w, ids, raise_oob=False))
+    assert (got[:, dim:] == 7.0).all()
+    assert int(err.item()) != 0
+
+
 @pytest.mark.parametrize("da,db", [(18, 18), (16, 7), (64, 128)])
 def test_concat_lookup_matches_cat_of_lookups(da, db, rng):
     """functional.embedding_lookup_concat (two strided gathers into one [.., da + db] output,
