@@ -1166,8 +1166,8 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
 // position in a uint32 (key: the row, or the sentinel n_rows for an excluded / OOB id; entries
 // past n: all ones). Wave w owns positions [1024 w, 1024 w + 1024), lane-strided, so (wave,
 // round, lane) order is position order. Per 8-bit digit pass, between two 64 KB LDS buffers:
-// counts per (wave, digit) from a wave match, per-wave digit offsets, then the same matches again
-// place every entry (digit base + wave offset + rank in the wave). Output identical to the
+// counts per (wave, digit) and each entry's rank in its wave from one wave match, per-wave digit
+// offsets, then every entry placed (digit base + wave offset + rank in the wave). Output identical to the
 // multi-launch forms (stable by position, sentinels after every row).
 // ---------------------------------------------------------------------------------------
 constexpr int kSmallThreads = 1024, kSmallWaves = kSmallThreads / 64;
@@ -1212,12 +1212,17 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     uint32_t* dst = bufs[cur ^ 1];
     for (int e = threadIdx.x; e < kSmallWaves * 256; e += kSmallThreads) (&wcnt[0][0])[e] = 0;
     __syncthreads();
-    // counts per (wave, digit): each match group's last lane adds the group's size
-#pragma unroll 2
+    // counts per (wave, digit): each match group's last lane adds the group's size; every
+    // entry's rank among its wave's entries of the digit before it is kept for the placing loop
+    uint32_t ent[kSmallKPT];
+    int32_t rank[kSmallKPT];
+#pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      const uint32_t d = (src[own + r * 64] >> shift) & 0xFFu;
+      ent[r] = src[own + r * 64];
+      const uint32_t d = (ent[r] >> shift) & 0xFFu;
       const uint64_t m = match_digit<8>(d, true);
       const int32_t prev = wcnt[wave][d];
+      rank[r] = prev + __popcll(m & lt);
       __builtin_amdgcn_wave_barrier();
       if ((m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
       __builtin_amdgcn_wave_barrier();
@@ -1256,17 +1261,11 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
       }
     }
     __syncthreads();
-    // the same groups again, now placed: digit base + this wave's offset + the rank in the wave
-#pragma unroll 2
+    // placed: digit base + this wave's offset + the rank in the wave (no second match)
+#pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      const uint32_t e = src[own + r * 64];
-      const uint32_t d = (e >> shift) & 0xFFu;
-      const uint64_t m = match_digit<8>(d, true);
-      const int32_t prev = wcnt[wave][d];
-      dst[dbase[d] + prev + __popcll(m & lt)] = e;
-      __builtin_amdgcn_wave_barrier();
-      if ((m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
-      __builtin_amdgcn_wave_barrier();
+      const uint32_t d = (ent[r] >> shift) & 0xFFu;
+      dst[dbase[d] + wcnt[wave][d] + rank[r]] = ent[r];
     }
     __syncthreads();
     cur ^= 1;
