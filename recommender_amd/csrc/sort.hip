@@ -44,6 +44,22 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t digit, bool valid) {
   return __ballot(valid) & ~(((uint64_t)mis_hi << 32) | mis_lo);
 }
 
+// the same over the low nb <= MAXB bits (nb wave-uniform: a skipped bit costs a scalar branch)
+template <int MAXB>
+__device__ __forceinline__ uint64_t match_digit_n(uint32_t digit, bool valid, int nb) {
+  uint32_t mis_lo = 0u, mis_hi = 0u;
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    if (b < nb) {
+      const uint32_t sgn = (uint32_t)(-(int32_t)((digit >> b) & 1u));
+      const uint64_t bb = __ballot(sgn != 0u);
+      mis_lo |= (uint32_t)bb ^ sgn;
+      mis_hi |= (uint32_t)(bb >> 32) ^ sgn;
+    }
+  }
+  return __ballot(valid) & ~(((uint64_t)mis_hi << 32) | mis_lo);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt64() {
   int lane = threadIdx.x & 63;
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -1165,7 +1181,8 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
 // 2^18 - 2 rows (the PinSage pair-term fold, small densifies) as one launch. Entry = key << 14 |
 // position in a uint32 (key: the row, or the sentinel n_rows for an excluded / OOB id; entries
 // past n: all ones). Wave w owns positions [1024 w, 1024 w + 1024), lane-strided, so (wave,
-// round, lane) order is position order. Per 8-bit digit pass, between two 64 KB LDS buffers:
+// round, lane) order is position order. Per digit pass (the key bits in the fewest passes of
+// <= 9 bits, split evenly), between two 64 KB LDS buffers:
 // counts per (wave, digit) and each entry's rank in its wave from one wave match, per-wave digit
 // offsets, then every entry placed (digit base + wave offset + rank in the wave). Output identical to the
 // multi-launch forms (stable by position, sentinels after every row).
@@ -1174,6 +1191,7 @@ constexpr int kSmallThreads = 1024, kSmallWaves = kSmallThreads / 64;
 constexpr int kSmallMax = 16384, kSmallKPT = kSmallMax / kSmallThreads;  // 16 entries per lane
 constexpr int kSmallPosBits = 14;
 constexpr int64_t kSmallMaxRows = (int64_t(1) << (32 - kSmallPosBits)) - 2;
+constexpr int kSmallDigitMax = 9, kSmallBins = 1 << kSmallDigitMax;  // digits of <= 9 bits
 
 __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     const void* __restrict__ ids, int32_t dtype, int64_t n, const uint8_t* __restrict__ valid,
@@ -1181,8 +1199,8 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     uint32_t* __restrict__ rows_out, int32_t* __restrict__ pos_out, int32_t* __restrict__ n_unique,
     int32_t* __restrict__ err_flag) {
   __shared__ uint32_t bufs[2][kSmallMax];
-  __shared__ uint16_t wcnt[kSmallWaves][256];
-  __shared__ int32_t dbase[256];
+  __shared__ uint16_t wcnt[kSmallWaves][kSmallBins];
+  __shared__ int32_t dbase[kSmallBins];
   __shared__ int32_t heads[kSmallWaves];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt64();
@@ -1206,11 +1224,17 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     bufs[0][i] = e;
   }
   if (__any(oob) && lane == 0) flag_oob(err_flag);
+  // the key bits in as few passes of <= 9 bits as possible, split evenly (18 bits: 9 + 9)
+  const int passes = (key_bits + kSmallDigitMax - 1) / kSmallDigitMax;
+  const int per = (key_bits + passes - 1) / passes;
   int cur = 0;
-  for (int shift = kSmallPosBits; shift < kSmallPosBits + key_bits; shift += 8) {
+  for (int shift = kSmallPosBits; shift < kSmallPosBits + key_bits; shift += per) {
+    const int nb = kSmallPosBits + key_bits - shift < per ? kSmallPosBits + key_bits - shift : per;
+    const int bins = 1 << nb;
+    const uint32_t dmask = (uint32_t)bins - 1u;
     const uint32_t* src = bufs[cur];
     uint32_t* dst = bufs[cur ^ 1];
-    for (int e = threadIdx.x; e < kSmallWaves * 256; e += kSmallThreads) (&wcnt[0][0])[e] = 0;
+    for (int e = threadIdx.x; e < kSmallWaves * kSmallBins; e += kSmallThreads) (&wcnt[0][0])[e] = 0;
     __syncthreads();
     // counts per (wave, digit): each match group's last lane adds the group's size; every
     // entry's rank among its wave's entries of the digit before it is kept for the placing loop
@@ -1219,8 +1243,8 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
 #pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
       ent[r] = src[own + r * 64];
-      const uint32_t d = (ent[r] >> shift) & 0xFFu;
-      const uint64_t m = match_digit<8>(d, true);
+      const uint32_t d = (ent[r] >> shift) & dmask;
+      const uint64_t m = match_digit_n<kSmallDigitMax>(d, true, nb);
       const int32_t prev = wcnt[wave][d];
       rank[r] = prev + __popcll(m & lt);
       __builtin_amdgcn_wave_barrier();
@@ -1228,7 +1252,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    if (threadIdx.x < 256) {  // per digit: the waves' counts -> wave offsets, the digit total
+    if (threadIdx.x < bins) {  // per digit: the waves' counts -> wave offsets, the digit total
       const int d = threadIdx.x;
       int32_t run = 0;
 #pragma unroll
@@ -1240,11 +1264,12 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
       dbase[d] = run;
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 256 digit totals, 4 per lane
-      int32_t t[4], sum = 0;
+    if (threadIdx.x < 64) {  // exclusive scan of the digit totals, bins / 64 per lane
+      constexpr int Q = kSmallBins / 64;
+      int32_t t[Q], sum = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        t[q] = dbase[4 * lane + q];
+      for (int q = 0; q < Q; ++q) {
+        t[q] = Q * lane + q < bins ? dbase[Q * lane + q] : 0;
         sum += t[q];
       }
       int32_t x = sum;
@@ -1255,8 +1280,8 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
       }
       int32_t run = x - sum;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        dbase[4 * lane + q] = run;
+      for (int q = 0; q < Q; ++q) {
+        if (Q * lane + q < bins) dbase[Q * lane + q] = run;
         run += t[q];
       }
     }
@@ -1264,7 +1289,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     // placed: digit base + this wave's offset + the rank in the wave (no second match)
 #pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      const uint32_t d = (ent[r] >> shift) & 0xFFu;
+      const uint32_t d = (ent[r] >> shift) & dmask;
       dst[dbase[d] + wcnt[wave][d] + rank[r]] = ent[r];
     }
     __syncthreads();
