@@ -1240,16 +1240,23 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     // entry's rank among its wave's entries of the digit before it is kept for the placing loop
     uint32_t ent[kSmallKPT];
     int32_t rank[kSmallKPT];
+    // only positions < n take part (rounds wholly past n are skipped, wave-uniformly): the
+    // work scales with n, not with the 16 384-entry capacity
 #pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      ent[r] = src[own + r * 64];
-      const uint32_t d = (ent[r] >> shift) & dmask;
-      const uint64_t m = match_digit_n<kSmallDigitMax>(d, true, nb);
-      const int32_t prev = wcnt[wave][d];
-      rank[r] = prev + __popcll(m & lt);
-      __builtin_amdgcn_wave_barrier();
-      if ((m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
-      __builtin_amdgcn_wave_barrier();
+      ent[r] = 0u;
+      rank[r] = 0;
+      if (wave * (kSmallKPT * 64) + r * 64 < n) {
+        const bool in = own + r * 64 < n;
+        ent[r] = src[own + r * 64];
+        const uint32_t d = (ent[r] >> shift) & dmask;
+        const uint64_t m = match_digit_n<kSmallDigitMax>(d, in, nb);
+        const int32_t prev = in ? wcnt[wave][d] : 0;
+        rank[r] = prev + __popcll(m & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (in && (m >> lane) == 1ull) wcnt[wave][d] = (uint16_t)(prev + __popcll(m));
+        __builtin_amdgcn_wave_barrier();
+      }
     }
     __syncthreads();
     if (threadIdx.x < bins) {  // per digit: the waves' counts -> wave offsets, the digit total
@@ -1289,8 +1296,10 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     // placed: digit base + this wave's offset + the rank in the wave (no second match)
 #pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      const uint32_t d = (ent[r] >> shift) & dmask;
-      dst[dbase[d] + wcnt[wave][d] + rank[r]] = ent[r];
+      if (own + r * 64 < n) {
+        const uint32_t d = (ent[r] >> shift) & dmask;
+        dst[dbase[d] + wcnt[wave][d] + rank[r]] = ent[r];
+      }
     }
     __syncthreads();
     cur ^= 1;
