@@ -1193,6 +1193,9 @@ constexpr int kSmallPosBits = 14;
 constexpr int64_t kSmallMaxRows = (int64_t(1) << (32 - kSmallPosBits)) - 2;
 constexpr int kSmallDigitMax = 9, kSmallBins = 1 << kSmallDigitMax;  // digits of <= 9 bits
 
+// BOUNDED: only the positions below n take part (sorts well under the capacity); otherwise every
+// position does (near the capacity the bounds tests cost more than the few padding entries)
+template <bool BOUNDED>
 __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     const void* __restrict__ ids, int32_t dtype, int64_t n, const uint8_t* __restrict__ valid,
     const int64_t* __restrict__ slot_offsets, int64_t n_rows, int key_bits,
@@ -1246,8 +1249,8 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     for (int r = 0; r < kSmallKPT; ++r) {
       ent[r] = 0u;
       rank[r] = 0;
-      if (wave * (kSmallKPT * 64) + r * 64 < n) {
-        const bool in = own + r * 64 < n;
+      if (!BOUNDED || wave * (kSmallKPT * 64) + r * 64 < n) {
+        const bool in = !BOUNDED || own + r * 64 < n;
         ent[r] = src[own + r * 64];
         const uint32_t d = (ent[r] >> shift) & dmask;
         const uint64_t m = match_digit_n<kSmallDigitMax>(d, in, nb);
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_sort_kernel(
     // placed: digit base + this wave's offset + the rank in the wave (no second match)
 #pragma unroll
     for (int r = 0; r < kSmallKPT; ++r) {
-      if (own + r * 64 < n) {
+      if (!BOUNDED || own + r * 64 < n) {
         const uint32_t d = (ent[r] >> shift) & dmask;
         dst[dbase[d] + wcnt[wave][d] + rank[r]] = ent[r];
       }
@@ -1416,7 +1419,12 @@ static int32_t small_sort(const void* ids, int32_t id_dtype, int64_t n_ids, cons
                           int32_t* sorted_pos, int32_t* n_unique, int32_t* err_flag, hipStream_t st) {
   int key_bits = 1;
   while (key_bits < 32 - kSmallPosBits && (int64_t(1) << key_bits) <= n_rows) ++key_bits;  // keys <= n_rows
-  small_sort_kernel<<<1, kSmallThreads, 0, st>>>(ids, id_dtype, n_ids, valid, slot_offsets, n_rows,
+  if (n_ids <= kSmallMax * 3 / 4)
+    small_sort_kernel<true><<<1, kSmallThreads, 0, st>>>(ids, id_dtype, n_ids, valid, slot_offsets,
+                                                          n_rows, key_bits, sorted_rows, sorted_pos,
+                                                          n_unique, err_flag);
+  else
+    small_sort_kernel<false><<<1, kSmallThreads, 0, st>>>(ids, id_dtype, n_ids, valid, slot_offsets, n_rows,
                                                  key_bits, sorted_rows, sorted_pos, n_unique,
                                                  err_flag);
   RS_CHECK_LAUNCH();
