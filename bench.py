@@ -19,6 +19,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 
 import numpy as np
 import torch
@@ -217,10 +218,13 @@ def init_dist(args):
         torch.cuda.set_device(local % max(ndev, 1))
         # RS_DIST_BACKEND=gloo: rehearse several ranks on one GPU (exchange staged through host)
         backend = os.environ.get("RS_DIST_BACKEND", "nccl")
+        # a stuck collective ends the run with an error well inside the driver's limit (the
+        # NCCL watchdog aborts the rank) instead of hanging for the 10-minute default
+        to = timedelta(seconds=int(os.environ.get("RS_DIST_TIMEOUT_S", "180")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=to)
     return world, rank, local
 
 

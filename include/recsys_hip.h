@@ -42,6 +42,8 @@ extern "C" {
 
 #define RS_ERRBIT_OOB 1
 #define RS_ERRBIT_FORMAT 2  /* a malformed input record (rs_tfrecord_parse_criteo) */
+#define RS_ERRBIT_RANGE 4   /* a size past what the caller declared (rs_sort_ids_slots: a slot
+                               with more rows than max_slot_rows allows; the output is not sorted) */
 
 /* optimizer kinds for rs_embedding_apply */
 #define RS_OPT_SGD 0        /* var[u] -= lr * g_u                         (ctr/train.py:77-79) */

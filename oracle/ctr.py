@@ -168,7 +168,16 @@ def dlrm_sgd_step(st: DLRMState, cat, dense_in, y, lr, detail=None):
         dz_b = (g_abs[:, None] * q[None, : F * F, 0]).reshape(B, F, F)
         dz_b = dz_b * np.triu(np.ones((F, F)), 1)[None]
         dx_b = np.matmul(dz_b + dz_b.transpose(0, 2, 1), np.abs(c["x"]).astype(np.float64))
-        detail.update(p=p, logit=c["logit"], logit_bound=mag_logit,
+        # the top input's own float64 magnitude bound: the bottom output's |x|·|K1|·|K2|·|K3| +
+        # |biases| chain, the pair values' Cauchy–Schwarz |x_i|·|x_j| (with that bottom bound in
+        # the bottom row). Any fp32 evaluation of an input rounds relative to this, not to its value.
+        bot_bound = magnitude_chain(np.abs(dense_in), bottom_old)
+        xb = np.abs(c["x"]).astype(np.float64)
+        xb[:, S, :] = bot_bound
+        zb = np.matmul(xb, xb.transpose(0, 2, 1)) * np.triu(np.ones((F, F)), 1)[None]
+        top_in_bound = np.concatenate([zb.reshape(B, F * F), bot_bound], axis=1)
+        del xb, zb
+        detail.update(p=p, logit=c["logit"], logit_bound=mag_logit, top_in_bound=top_in_bound,
                       dx=dx[:, :S, :].reshape(B * S, D), dx_bound=dx_b[:, :S, :].reshape(B * S, D),
                       uniq_rows=u, uniq_grad=ug, top_grads=tgrads, bottom_grads=bgrads,
                       sorted_rows=sr, sorted_pos=sp,

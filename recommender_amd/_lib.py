@@ -24,6 +24,7 @@ RS_OPT_KERAS_ADAM = 2
 RS_DEDUP_TILE = 32
 RS_ERRBIT_OOB = 1
 RS_ERRBIT_FORMAT = 2
+RS_ERRBIT_RANGE = 4
 RS_DIEN_SKIP_MASKED_ROWS = 1
 
 
@@ -328,6 +329,7 @@ class KernelTimer:
         self.enabled = False
 
     def totals_ms(self):
+        """{name: (total ms, launches)} over the recorded (eagerly launched) calls."""
         torch.cuda.synchronize()
         return {n: (sum(s.elapsed_time(e) for s, e in ev), len(ev)) for n, ev in self.events.items()}
 
@@ -344,7 +346,10 @@ def call(fn: str, *args):
     """Invoke a kernel entry point; raises on a non-zero status."""
     f = getattr(lib(), fn)
     t = _timer
-    if t is not None and t.enabled and fn in t.names:
+    # no events while a stream is being captured: a graph replay does not re-record them, so
+    # their elapsed_time would be read off events that never completed (hipErrorInvalidHandle)
+    if (t is not None and t.enabled and fn in t.names
+            and not torch.cuda.is_current_stream_capturing()):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         st = f(*args)

@@ -428,11 +428,9 @@ struct Tile32Edges {
 // instead of one per run: a table load waits for every load issued before it (vmcnt counts in
 // order), so an inline update drains the in-flight gradient rows at each run end. Same
 // arithmetic, each row written once: bit-identical.
-// P > 0 (SGD only, round 5): the table rows of the tile's first P complete runs (runs that start
-// and end inside the tile: the ones updated on the spot) are loaded at the tile's start, from the
-// lane-parallel keys, ahead of every gradient-row load — so those updates wait for nothing; runs
-// past the P-th take the queue (Q) as before. Same arithmetic, each row written once.
-template <int OPT, int Q = 0, int P = 0>
+// (Round 5 also built row preloads at the tile start, RS_APPLY_PRE: measured 249-261 us against
+// 232-238 and removed in round 6.)
+template <int OPT, int Q = 0>
 __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ keys,
                                                    const int32_t* __restrict__ pos, int64_t n,
                                                    uint32_t n_rows, const float* __restrict__ grad,
@@ -440,8 +438,6 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   constexpr int T = 32, VEC = 4, CPL = 1, U = 8;
   constexpr bool kQueue = Q > 0 && OPT == OPT_SGD;
   constexpr int QN = Q > 0 ? Q : 1;
-  constexpr bool kPre = P > 0 && OPT == OPT_SGD;
-  constexpr int PN = P > 0 ? P : 1;
   const int gl = threadIdx.x & 31;
   const int64_t k0 = t * T;
   const int64_t k1 = k0 + T < n ? k0 + T : n;
@@ -460,26 +456,6 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   const uint32_t key_before = k0 > 0 ? keys[k0 - 1] : 0xFFFFFFFFu;
   const uint32_t key_after = k1 < n ? keys[k1] : 0xFFFFFFFEu;
   auto key_of = [&](int u) { return (uint32_t)__shfl((int)kv, u, 32); };
-  // the first P complete runs' table rows, loaded before any gradient row
-  float pre[PN][VEC];
-  int n_pre = 0, ci = 0;  // preloaded rows, complete runs emitted so far
-  if constexpr (kPre) {
-    const uint32_t knext = gl + 1 < ne ? key_of(gl + 1) : key_after;
-    (void)key_of(gl);  // keep the shuffles of both calls in the same (uniform) control flow
-    const bool cend = lv && knext != kv && kv != key_before;  // a complete run's last entry
-    const uint64_t bm = __ballot(cend) >> (threadIdx.x & 32);
-    uint32_t m = (uint32_t)bm;
-#pragma unroll
-    for (int i = 0; i < PN; ++i) {
-      const int e = m ? __builtin_ctz(m) : 0;
-      const uint32_t row = key_of(e);
-      if (m) {
-        RowIO<VEC>::load(a.table + (int64_t)row * dim + col, pre[i]);
-        ++n_pre;
-        m &= m - 1;
-      }
-    }
-  }
   // the row scale multiplies at the sum (consume), not here: a multiply right behind each load
   // would wait for it and serialise the batch's loads (measured: apply 215 -> 272 us alone)
   auto load_batch = [&](int b0, float (&r)[U][VEC]) {
@@ -525,21 +501,6 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   auto emit = [&](uint32_t row, bool starts, bool ends, int head_e) {
     if (!key_ok(row)) return;  // OOB sentinel (or out-of-range) run: gradient dropped
     if (starts && ends) {
-      if constexpr (kPre) {
-        bool done = false;
-#pragma unroll
-        for (int i = 0; i < PN; ++i) {
-          if (i == ci && i < n_pre) {
-            float tr[VEC];
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) tr[c] = pre[i][c] - a.p.lr * acc[0][c];
-            RowIO<VEC>::store(a.table + (int64_t)row * dim + col, tr);
-            done = true;
-          }
-        }
-        ++ci;
-        if (done) return;
-      }
       if constexpr (kQueue) {
         if (qn == QN) flush();
 #pragma unroll
@@ -639,7 +600,7 @@ __global__ __launch_bounds__(256) void seg_tile32_kernel(const uint32_t* __restr
 // (chunk[t][1], tile flag bit 0) and, at a group's first tile, the continuation's group sum
 // (chunk[t][0]); seg_fixup_kernel folds those (level 2). Bit-identical to seg_tile32 + seg_chunk
 // + seg_fixup, one launch fewer and no global partials.
-template <int OPT, int Q = 0, int P = 0>
+template <int OPT, int Q = 0>
 __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __restrict__ keys,
                                                            const int32_t* __restrict__ pos,
                                                            int64_t n, uint32_t n_rows,
@@ -663,7 +624,7 @@ __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __res
     return;
   }
   Tile32Edges e{};
-  if (live) e = tile32_walk<OPT, Q, P>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
+  if (live) e = tile32_walk<OPT, Q>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
   if (gl == 0) fkey[gi] = live ? e.first_key : 0xFFFFFFFFu;
   __syncthreads();
   if (!live) return;
@@ -1109,16 +1070,6 @@ __global__ __launch_bounds__(256) void keras_materialize_kernel(
 }
 
 // ---- host launchers -------------------------------------------------------------------
-// Opt-in occupancy cap for the D = 128 walk (A/B): unused dynamic LDS per block, so fewer walk
-// blocks fit on a CU and the co-running weight-sized kernels find free wave slots.
-static size_t apply_lds_throttle() {
-  static const size_t v = [] {
-    const char* e = getenv("RS_APPLY_LDS");
-    return e ? (size_t)atol(e) : (size_t)0;
-  }();
-  return v;
-}
-
 template <template <int, int> class K>
 struct Noop {};
 
@@ -1152,26 +1103,9 @@ __global__ __launch_bounds__(256) void keras_bitmap_mark_kernel(const uint32_t* 
   }
 }
 
-// The D = 128 SGD walk with its table updates queued 2 runs at a time (tile32_walk<OPT_SGD, 2>;
-// Q = 3 and 4 spill at 128 VGPRs): default; RS_APPLY_QUEUE=0 selects the one-run-at-a-time walk
-// (A/B, 200 steps each, interleaved: step 0.685-0.688 -> 0.671-0.674 ms, apply alone 238 -> 230
-// us, bit-identical). Read once per process.
-static bool apply_queue() {
-  static const int v = [] {
-    const char* e = getenv("RS_APPLY_QUEUE");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return v != 0;
-}
-// RS_APPLY_PRE=2 / 4: the walk loads the first 2 / 4 complete runs' table rows at each tile's
-// start instead of queueing the updates (A/B; 0 = off)
-static int apply_pre() {
-  static const int v = [] {
-    const char* e = getenv("RS_APPLY_PRE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// The D = 128 SGD walk queues its table updates 2 runs at a time (tile32_walk<OPT_SGD, 2>; Q = 3
+// and 4 spill at 128 VGPRs): round 4's A/B against the one-run-at-a-time walk, 200 steps each,
+// interleaved: step 0.685-0.688 -> 0.671-0.674 ms, apply alone 238 -> 230 us, bit-identical.
 
 static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos, int64_t n,
                                int64_t n_rows, const float* grad, const ApplyArgs& a,
@@ -1205,13 +1139,7 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
 #define RS_SEG_LAUNCH(OPTV)                                                                     \
   RS_DISPATCH_VEC_CPL(geom, ({                                                                  \
     if (g32) {                                                                                  \
-      if (OPTV == OPT_SGD && apply_pre() == 2)                                                  \
-        seg_group32_kernel<OPTV, 0, 2><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                 \
-            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
-      else if (OPTV == OPT_SGD && apply_pre() == 4)                                             \
-        seg_group32_kernel<OPTV, 0, 4><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                 \
-            keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
-      else if (OPTV == OPT_SGD && apply_queue())                                                \
+      if (OPTV == OPT_SGD)                                                                      \
         seg_group32_kernel<OPTV, 2><<<ceil_div(n_tiles, 32), 1024, 0, st>>>(                    \
             keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
       else                                                                                      \
@@ -1220,7 +1148,7 @@ static int32_t launch_segments(int opt, const uint32_t* keys, const int32_t* pos
                                                                      n_tiles);                  \
     } else {                                                                                    \
       if (t32)                                                                                  \
-        seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, apply_lds_throttle(), st>>>(       \
+        seg_tile32_kernel<OPTV><<<ceil_div(n_tiles, 8), 256, 0, st>>>(       \
             keys, pos, n, (uint32_t)n_rows, grad, a, n_tiles);                                  \
       else                                                                                      \
         seg_tile_kernel<OPTV, VEC, CPL><<<walk_blocks, 256, 0, st>>>(                           \

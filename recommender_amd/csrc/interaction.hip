@@ -1275,372 +1275,8 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
   if (__any(oob) && lane == 0) flag_oob(src.err_flag);
 }
 
-// ---------------------------------------------------------------------------------------
-// The train kernel at three waves per SIMD (round 5; RS_TRAIN3=1 selects it, D = 128): the
-// same arithmetic per example as dlrm_train_chunk, re-laid for 168 VGPRs and <= 53 KB of LDS
-// per 4-wave block (three blocks per CU):
-//   ring    X(b+1) is prefetched two chunks ahead through a two-chunk register ring (chunk s's
-//           registers take chunk s + 2 of the same example, or chunk s - 2 of the next one),
-//           not a whole example ahead: 32 VGPRs instead of 64, the third wave per SIMD covering
-//           the shorter distance;
-//   staging the U staging tile is aliased onto the chunk image (both transposed operands of a
-//           chunk are read before its staging writes; one wave's LDS operations run in issue
-//           order): 6.6 KB of LDS per wave instead of 11 KB;
-//   bottom  the bottom-MLP row's gradient G_bot,b (relu-masked) is written as a row [B, 128]
-//           instead of accumulating A_bot = Σ x_bᵀ·G_bot,b and Σ G_bot,b in 28 registers per lane;
-//           train_gbot_reduce_kernel forms both per train block (examples in order) into the
-//           block's partial row before the fold.
-// ---------------------------------------------------------------------------------------
-template <bool ID64>
-__global__ __launch_bounds__(256, 3) void dlrm_train_chunk3(GatherSrc src, int64_t batch, int F,
-                                                            TrainArgs ta, float* g_rows, int epw,
-                                                            float* __restrict__ gbot) {
-  constexpr int D = 128;
-  constexpr int NC = D / 32, DL = D / 4, RPI = 64 / DL, DPL = D / 64;
-  constexpr int TM = train_m<D>();
-  constexpr int RW = kChImage / 4 + D;  // the chunk image (staging aliased on it) + U's row S
-  __shared__ __attribute__((aligned(16))) float lds[4][RW];
-  __shared__ __attribute__((aligned(16))) float qlane[64][12];
-  __shared__ __attribute__((aligned(16))) float qsh[kTrainAtop];
-  __shared__ __attribute__((aligned(16))) bf16x8 sash[2][3][64];
-  // the A_top accumulators (12 z products + 4 dense products per lane) in lane-private LDS slots:
-  // the same sequential sums, 16 VGPRs fewer across the chunk loop
-  __shared__ __attribute__((aligned(16))) floatx4 atop[4][4][64];
-  static_assert(4 * RW >= TM, "the block's partial row fits the wave regions");
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t first = ((int64_t)blockIdx.x * 4 + wave) * epw;
-  const int64_t last = first + epw < batch ? first + epw : batch;
-  const bool active = first < batch;
-  const int r = lane & 15, g = lane >> 4;
-  const int S = src.n_slots;
-  const int nzc = F * (F - 1) / 2;
-  char* img = reinterpret_cast<char*>(lds[wave]);
-  float* stg = lds[wave];  // aliased on the image
-  float* ubot = lds[wave] + kChImage / 4;
-  for (int e = threadIdx.x; e < kTrainAtop; e += 256) qsh[e] = e < nzc + D ? ta.q[e] : 0.f;
-  if (wave == 0) {
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int i0 = 4 * g + reg, j0 = r;
-      const int i1 = 4 * g + reg, j1 = 16 + r;
-      const int i2 = 16 + 4 * g + reg, j2 = 16 + r;
-      qlane[lane][reg] = (i0 < j0 && j0 < F) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
-      qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
-      qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
-    }
-  }
-  if (wave == 1) {
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      floatx4 v[2];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = 16 * ib + r, kk = 8 * g + j;
-        const bool in = m < F && kk < F && m != kk;
-        const float q = ta.q[in ? compact_index(m < kk ? m : kk, m < kk ? kk : m, F, 0) : 0];
-        v[j >> 2][j & 3] = in ? q : 0.f;
-      }
-      split3(v[0], v[1], sash[ib][0][lane], sash[ib][1][lane], sash[ib][2][lane]);
-    }
-  }
-  __syncthreads();
-  const float cc = ta.c[0];
-  float s_top = 0.f, loss = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) atop[wave][k][lane] = floatx4{0.f, 0.f, 0.f, 0.f};
-  int64_t lo = 0, n_ok = src.n_rows;
-  if (lane < S && src.slot_offsets) {
-    lo = src.slot_offsets[lane];
-    n_ok = src.slot_offsets[lane + 1] - lo;
-  }
-  bool oob = false;
-  auto raw_id = [&](int64_t b) -> int64_t {
-    const int64_t bb = b < last ? b : first;
-    const int ln = lane < S ? lane : S - 1;
-    const int64_t v = ID64 ? static_cast<const int64_t*>(src.ids)[bb * S + ln]
-                           : static_cast<int64_t>(static_cast<const int32_t*>(src.ids)[bb * S + ln]);
-    return lane < S ? v : 0;
-  };
-  auto row_of = [&](int64_t b, int64_t id) -> const float* {
-    const bool live = b < last;
-    const bool id_ok = id >= 0 && id < n_ok;
-    if (lane < S && !id_ok && live) oob = true;
-    if (lane < S) return id_ok ? src.table + (lo + id) * D : kZeroRow;
-    return (lane == S && live) ? src.dense + (b < last ? b : first) * D : kZeroRow;
-  };
-  // the ring: slot k holds one chunk (rows r and 16 + r: two floatx4 each)
-  floatx4 a0[2][2], a1[2][2];
-  floatx4 dn4;
-  const float* p0 = nullptr;  // X(b) rows of this lane's pair
-  const float* p1 = nullptr;
-  const float* n0 = nullptr;  // X(b+1)
-  const float* n1 = nullptr;
-  auto load_into = [&](int k, const float* q0, const float* q1, int s) {
-    a0[k][0] = *(gfloatx4*)(q0 + 32 * s + 8 * g);
-    a0[k][1] = *(gfloatx4*)(q0 + 32 * s + 8 * g + 4);
-    a1[k][0] = *(gfloatx4*)(q1 + 32 * s + 8 * g);
-    a1[k][1] = *(gfloatx4*)(q1 + 32 * s + 8 * g + 4);
-  };
-  auto load_side = [&](int64_t b) {
-    const int cl = lane & (DL - 1);
-    const int64_t bb = b < last ? b : first;
-    dn4 = *(gfloatx4*)(src.dense + bb * D + 4 * cl);
-  };
-  if (active) {
-    {
-      const float* mine = row_of(first, raw_id(first));
-      p0 = shfl_ptr(mine, r);
-      p1 = shfl_ptr(mine, 16 + r);
-      load_side(first);
-      load_into(0, p0, p1, 0);
-      load_into(1, p0, p1, 1);
-    }
-    int64_t id_next = raw_id(first + 1);
-    for (int64_t b = first; b < last; ++b) {
-      int lanev;
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lanev));
-      const int r = lanev & 15, g = (lanev >> 4) & 3;
-      {
-        const float* nxt = row_of(b + 1, id_next);
-        n0 = shfl_ptr(nxt, r);
-        n1 = shfl_ptr(nxt, 16 + r);
-      }
-      id_next = raw_id(b + 2);
-      const floatx4 dn = dn4;
-      typedef __attribute__((address_space(4))) const float cfloat;
-      const int bq = __builtin_amdgcn_readfirstlane((int)b);
-      const float lb = ((const cfloat*)ta.label)[bq];
-      load_side(b + 1);
-      float* de = ta.grad_emb + b * S * (int64_t)D;
-      floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-      const int q = (lanev >> 2) & 3, p4 = lanev & 3;
-      // the chunk loop is not unrolled (the per-chunk addresses are recomputed rather than
-      // held for all four chunks): the current chunk is always ring slot 0, and after its
-      // split the slot takes the chunk two ahead and the slots swap
-#pragma unroll 1
-      for (int s = 0; s < NC; ++s) {
-        bf16x8 h0, m0, l0, h1, m1, l1;
-        split3(a0[0][0], a0[0][1], h0, m0, l0);
-        split3(a1[0][0], a1[0][1], h1, m1, l1);
-        __builtin_amdgcn_sched_barrier(0);
-        // the freed slot takes the chunk two ahead: s + 2 of X(b), or s - 2 of X(b+1)
-        {
-          const bool cur = s < 2;
-          load_into(0, cur ? p0 : n0, cur ? p1 : n1, cur ? s + 2 : s - 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const floatx4 t0 = a0[0][h], t1 = a1[0][h];
-          a0[0][h] = a0[1][h];
-          a1[0][h] = a1[1][h];
-          a0[1][h] = t0;
-          a1[1][h] = t1;
-        }
-        c00 = mfma6(h0, m0, l0, h0, m0, l0, c00);
-        c01 = mfma6(h0, m0, l0, h1, m1, l1, c01);
-        c11 = mfma6(h1, m1, l1, h1, m1, l1, c11);
-        *reinterpret_cast<bf16x8*>(img + 0 * kChPlane + ch_off(r, 8 * g)) = h0;
-        *reinterpret_cast<bf16x8*>(img + 1 * kChPlane + ch_off(r, 8 * g)) = m0;
-        *reinterpret_cast<bf16x8*>(img + 2 * kChPlane + ch_off(r, 8 * g)) = l0;
-        *reinterpret_cast<bf16x8*>(img + 0 * kChPlane + ch_off(16 + r, 8 * g)) = h1;
-        *reinterpret_cast<bf16x8*>(img + 1 * kChPlane + ch_off(16 + r, 8 * g)) = m1;
-        *reinterpret_cast<bf16x8*>(img + 2 * kChPlane + ch_off(16 + r, 8 * g)) = l1;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_sched_barrier(0);  // the split parts die here, before the U operands
-        // both 16-column tiles' products before the staging writes (aliased on the image): the
-        // tiles' results stay in registers (16), each tile's transposed operand is read in turn
-        floatx4 dd[2][2];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          bf16x8 xp[3];
-#pragma unroll
-          for (int pt = 0; pt < 3; ++pt) {
-            const int o0 = pt * kChPlane + ch_off(8 * g + q, 16 * tt + 4 * p4);
-            const int o1 = pt * kChPlane + ch_off(8 * g + 4 + q, 16 * tt + 4 * p4);
-            const shortx4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o0));
-            const shortx4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(img + o1));
-            const shortx8 v8 = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
-            xp[pt] = __builtin_bit_cast(bf16x8, v8);
-          }
-#pragma unroll
-          for (int ib = 0; ib < 2; ++ib) {
-            const bf16x8 s0 = sash[ib][0][lanev & 63], s1 = sash[ib][1][lanev & 63],
-                         s2 = sash[ib][2][lanev & 63];
-            dd[tt][ib] = mfma6_xs(xp[0], xp[1], xp[2], s0, s1, s2, floatx4{0.f, 0.f, 0.f, 0.f});
-          }
-          __builtin_amdgcn_sched_barrier(0);  // one tile's operands live at a time
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const int col = 16 * tt + 4 * g;
-          *reinterpret_cast<floatx4*>(stg + r * kChStageLd + col) = dd[tt][0];
-          *reinterpret_cast<floatx4*>(stg + (16 + r) * kChStageLd + col) = dd[tt][1];
-          if (r == S) *reinterpret_cast<floatx4*>(ubot + 32 * s + col) = dd[tt][0];
-          if (16 + r == S) *reinterpret_cast<floatx4*>(ubot + 32 * s + col) = dd[tt][1];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-          const int i = 8 * pp + (lanev >> 3), c8 = lanev & 7;
-          const floatx4 v = *reinterpret_cast<const floatx4*>(stg + i * kChStageLd + 4 * c8);
-          if (i < S)
-            __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(de + i * D + 32 * s + 4 * c8));
-        }
-        __builtin_amdgcn_wave_barrier();  // the next chunk's image writes follow these reads
-      }
-      p0 = n0;
-      p1 = n1;
-      // head, loss, G
-      const int cl = lanev & (DL - 1), rg = (lanev / DL) & (RPI - 1);
-      float zr[12];
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        zr[reg] = c00[reg];
-        zr[4 + reg] = c01[reg];
-        zr[8 + reg] = c11[reg];
-      }
-      float hacc = 0.f;
-      {
-        const floatx4* ql = reinterpret_cast<const floatx4*>(&qlane[lanev & 63][0]);
-#pragma unroll
-        for (int q4 = 0; q4 < 3; ++q4) {
-          const floatx4 qv = ql[q4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) hacc += zr[4 * q4 + k] * qv[k];
-        }
-        const floatx4 qd = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
-        if (rg == 0) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) hacc += dn[k] * qd[k];
-        }
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) hacc += __shfl_xor(hacc, off);
-      const float p = 1.f / (1.f + expf(-(hacc + cc)));
-      {
-        const float pc = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
-        loss += -(lb * logf(pc + ta.eps) + (1.f - lb) * logf((1.f - pc) + ta.eps));
-      }
-      const bool inside = p >= ta.eps && p <= 1.f - ta.eps;
-      const float pcg = fminf(fmaxf(p, ta.eps), 1.f - ta.eps);
-      const float dbce = -(lb / (pcg + ta.eps)) + (1.f - lb) / ((1.f - pcg) + ta.eps);
-      const float dp = inside ? ta.gscale * dbce : 0.f;
-      const float G = dp * (p * (1.f - p));
-      if (lanev == 0) {
-        ta.y[b] = p;
-        g_rows[b] = G;
-      }
-      s_top += G;
-#pragma unroll
-      for (int k4 = 0; k4 < 3; ++k4) {
-        floatx4 v = atop[wave][k4][lanev & 63];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] += zr[4 * k4 + k] * G;
-        atop[wave][k4][lanev & 63] = v;
-      }
-      {
-        floatx4 v = atop[wave][3][lanev & 63];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] += dn[k] * G;
-        atop[wave][3][lanev & 63] = v;
-      }
-      {  // the bottom-MLP row's gradient G·(U_S + q_d) through the relu, as a row
-        const floatx4 v = *reinterpret_cast<const floatx4*>(ubot + 4 * cl);
-        const floatx4 qdn = *reinterpret_cast<const floatx4*>(&qsh[nzc + 4 * cl]);
-        float gb2[DPL];
-#pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-          const int c = DPL * rg + k;
-          const float gd = __fmul_rn(G, v[c] + qdn[c]);
-          gb2[k] = dn[c] > 0.f ? gd : 0.f;
-        }
-        *reinterpret_cast<float2*>(gbot + b * D + 4 * cl + DPL * rg) = make_float2(gb2[0], gb2[1]);
-      }
-      __builtin_amdgcn_wave_barrier();  // the next example's ubot writes follow these reads
-    }
-  }
-  // the block's partial row, waves folded in order (0, then + 1, + 2, + 3) through one shared
-  // row; A_bot / s_bot are left 0 here (train_gbot_reduce_kernel writes them)
-  __syncthreads();
-  float* X = &lds[0][0];
-  for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
-      if (w == 0)
-        for (int e = lane; e < TM; e += 64) X[e] = 0.f;
-      __builtin_amdgcn_wave_barrier();
-      if (active) {
-        const floatx4 z0 = atop[wave][0][lane], z1 = atop[wave][1][lane], z2 = atop[wave][2][lane];
-        const floatx4 dv = atop[wave][3][lane];
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int i0 = 4 * g + reg, j0 = r, i1 = 4 * g + reg, j1 = 16 + r, i2 = 16 + 4 * g + reg,
-                    j2 = 16 + r;
-          if (i0 < j0 && j0 < F) X[compact_index(i0, j0, F, 0)] += z0[reg];
-          if (j1 < F) X[compact_index(i1, j1, F, 0)] += z1[reg];
-          if (i2 < j2 && j2 < F) X[compact_index(i2, j2, F, 0)] += z2[reg];
-        }
-        const int cl = lane & (DL - 1), rg = lane / DL;
-        if (rg == 0) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) X[nzc + 4 * cl + k] += dv[k];
-        }
-        if (lane == 0) {
-          X[kTrainAtop] += s_top;
-          X[kTrainAtop + 1] += loss;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  for (int e = threadIdx.x; e < TM; e += 256) ta.part[(int64_t)blockIdx.x * TM + e] = X[e];
-  if (__any(oob) && lane == 0) flag_oob(src.err_flag);
-}
-
-// A_bot [13][128] = Σ_b x_bᵀ·G_bot,b and s_bot [128] = Σ_b G_bot,b over train block i's examples
-// [4·epw·i, 4·epw·(i+1)) in example order, into that block's partial row. The rows are staged
-// 32 examples at a time in LDS (one round trip per 32); thread (column c, half h) sums inputs
-// 7h .. 7h + 6 of its column, input 13 being the ones column (s_bot).
-constexpr int kGbotChunk = 32;
-__global__ __launch_bounds__(256) void train_gbot_reduce_kernel(const float* __restrict__ gbot,
-                                                                const float* __restrict__ xin,
-                                                                int64_t batch, int epw,
-                                                                float* __restrict__ part) {
-  constexpr int D = 128, TM = train_m<128>();
-  __shared__ __attribute__((aligned(16))) float gs[kGbotChunk][D];
-  __shared__ float xs[kGbotChunk][kTrainNI + 1];
-  const int c = threadIdx.x & (D - 1), h = threadIdx.x >> 7;
-  const int64_t b0 = (int64_t)blockIdx.x * 4 * epw;
-  const int64_t b1 = b0 + 4 * (int64_t)epw < batch ? b0 + 4 * (int64_t)epw : batch;
-  float acc[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) acc[i] = 0.f;
-  for (int64_t cb = b0; cb < b1; cb += kGbotChunk) {
-    const int n = (int)(b1 - cb < kGbotChunk ? b1 - cb : kGbotChunk);
-    for (int e = threadIdx.x; e < n * D / 4; e += 256)
-      reinterpret_cast<floatx4*>(&gs[0][0])[e] = reinterpret_cast<const floatx4*>(gbot + cb * D)[e];
-    for (int e = threadIdx.x; e < n * kTrainNI; e += 256) {
-      const int bb = e / kTrainNI, ii = e - bb * kTrainNI;
-      xs[bb][ii] = xin[(cb + bb) * kTrainNI + ii];
-    }
-    if (threadIdx.x < kGbotChunk) xs[threadIdx.x][kTrainNI] = 1.f;
-    __syncthreads();
-    for (int bb = 0; bb < n; ++bb) {
-      const float gv = gs[bb][c];
-#pragma unroll
-      for (int i = 0; i < 7; ++i) acc[i] += xs[bb][7 * h + i] * gv;
-    }
-    __syncthreads();
-  }
-  float* row = part + (int64_t)blockIdx.x * TM + kTrainAtop + 2;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int ii = 7 * h + i;
-    if (ii < kTrainNI) row[ii * D + c] = acc[i];
-    else row[kTrainNI * D + c] = acc[i];
-  }
-}
+// (Round 5 built a three-waves-per-SIMD form of this kernel, RS_TRAIN3: 433-450 us against
+// 318-334, profiles/r05_train_kernel_pmc_2wave_vs_3wave.txt; removed in round 6.)
 
 template <int GREG, int KS, bool ID64>
 static void launch_pipe_t(const GatherSrc& src, int64_t batch, int F, InterMode md,
@@ -2053,20 +1689,8 @@ extern "C" int32_t rs_dlrm_interaction_fwd_head_dx(const float* table, int64_t n
 }
 
 extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
-  // one partial row per block (at most ceil(batch / 4) blocks) + the fold's 32 segment rows,
-  // then the 3-wave kernel's G_bot rows [batch, 128]
-  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) +
-         (size_t)batch * 128 * sizeof(float) + 256;
-}
-
-// RS_TRAIN3=1: the D = 128 train step takes dlrm_train_chunk3 (three waves per SIMD) + the
-// G_bot reduction; read once per process
-static bool train3_enabled() {
-  static const int v = [] {
-    const char* e = getenv("RS_TRAIN3");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v != 0;
+  // one partial row per block (at most ceil(batch / 4) blocks) + the fold's 32 segment rows
+  return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
 }
 
 static int32_t train_step_launch(
@@ -2099,19 +1723,7 @@ static int32_t train_step_launch(
     blocks = ceil_div(batch, 4 * (int64_t)epw);
     kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw);
   };
-  if (D == 128 && train3_enabled()) {
-    float* gbot = reinterpret_cast<float*>(
-        static_cast<char*>(workspace) +
-        align_up((size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float), 256));
-    auto go3 = [&](auto kern) {
-      const int epw = pipe_epw(reinterpret_cast<const void*>(kern), batch, 1);
-      blocks = ceil_div(batch, 4 * (int64_t)epw);
-      kern<<<blocks, 256, 0, st>>>(src, batch, F, ta, g_rows, epw, gbot);
-      train_gbot_reduce_kernel<<<blocks, 256, 0, st>>>(gbot, xin, batch, epw, part);
-    };
-    if (id_dtype == RS_ID_I64) go3(dlrm_train_chunk3<true>);
-    else go3(dlrm_train_chunk3<false>);
-  } else if (D == 128) {
+  if (D == 128) {
     if (id_dtype == RS_ID_I64) go(dlrm_train_chunk<128, true>);
     else go(dlrm_train_chunk<128, false>);
   } else {

@@ -752,6 +752,10 @@ struct SegSlot {
   int w0, w1;
 };
 
+// The host picks this form from max_slot_rows (<= 2^24); the widths come from the device
+// offsets. A slot wider than 2^24 rows (offsets that disagree with the host's bound) would need
+// w1 > 12 and overrun the 4096-bin LDS arrays: the widths are clamped to 12 (no overrun), the
+// output is not sorted, and RS_ERRBIT_RANGE is raised instead.
 __device__ __forceinline__ SegSlot seg_slot(const SegArgs& a, int s) {
   SegSlot r;
   r.lo = a.slot_offsets ? a.slot_offsets[s] : 0;
@@ -759,6 +763,10 @@ __device__ __forceinline__ SegSlot seg_slot(const SegArgs& a, int s) {
   const int bits = seg_bits(r.rows);
   r.w0 = bits < kSegBits ? bits : kSegBits;
   r.w1 = bits - r.w0;
+  if (r.w1 > kSegBits) {
+    r.w1 = kSegBits;
+    if (threadIdx.x == 0 && a.err_flag) atomicOr(a.err_flag, RS_ERRBIT_RANGE);
+  }
   return r;
 }
 
@@ -1547,16 +1555,6 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
                              int32_t* n_unique, int32_t* err_flag, void* workspace, size_t ws_bytes,
                              hipStream_t st, const uint8_t* valid, int64_t max_slot_rows);
 
-// RS_SORT_LSD=1: every id sort takes the three-pass LSD form (A/B against the slot-segmented
-// sort; the two give the same output). Read once per process.
-static bool sort_lsd_forced() {
-  static const int v = [] {
-    const char* e = getenv("RS_SORT_LSD");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 extern "C" size_t rs_sort_ids_workspace_size(int64_t n_ids) {
   Carver c(nullptr, 0);
   c.take<uint32_t>(n_ids);
@@ -1670,13 +1668,12 @@ static int32_t sort_ids_impl(const void* ids, int32_t id_dtype, int64_t n_ids,
   RS_CHECK_ARG(key_space < (int64_t(1) << 31) - 1, "key space out of range");
   if (n_unique) RS_CHECK_HIP(hipMemsetAsync(n_unique, 0, sizeof(int32_t), st));
   if (n_ids == 0) return RS_OK;
-  if (small_eligible(n_ids, n_slots, world, n_rows) && !sort_lsd_forced())
-    // one workgroup, one launch (RS_SORT_LSD=1: the LSD sort, A/B)
+  if (small_eligible(n_ids, n_slots, world, n_rows))
+    // one workgroup, one launch
     return small_sort(ids, id_dtype, n_ids, valid, slot_offsets, n_rows, sorted_rows, sorted_pos,
                       n_unique, err_flag, st);
-  if ((slot_offsets || n_slots == 1) && seg_eligible(n_ids, n_slots, world, max_slot_rows) &&
-      !sort_lsd_forced()) {
-    // the slot-segmented sort: same output, four launches (RS_SORT_LSD=1: the LSD sort, A/B)
+  if ((slot_offsets || n_slots == 1) && seg_eligible(n_ids, n_slots, world, max_slot_rows)) {
+    // the slot-segmented sort: same output as the LSD form below, six launches
     int32_t s = seg_sort(ids, id_dtype, n_ids, valid, slot_offsets, n_slots, n_rows, sorted_rows,
                          sorted_pos, err_flag, workspace, ws_bytes, st);
     if (s) return s;

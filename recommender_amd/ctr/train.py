@@ -94,6 +94,9 @@ class TrainStep:
         frozen into the graph, so capture only with constant-lr SGD."""
         if self._sched is not None or not isinstance(self.opt_sparse, SparseSGD):
             raise RuntimeError("graph capture needs constant-lr SGD (scalars are frozen)")
+        if self.sharded:
+            raise RuntimeError("a row-sharded slab's step reads its spill / late-round sizes on "
+                               "the host each step and cannot be captured")
         # the graph must join every stream it forks: the sparse update joins inside the step
         # (a replay is ordered after the previous one as a whole)
         defer = self.opt_sparse.defer_join
@@ -132,6 +135,9 @@ class TrainStep:
         runs all the steps and returns the last loss."""
         if self._sched is not None or not isinstance(self.opt_sparse, SparseSGD):
             raise RuntimeError("graph capture needs constant-lr SGD (scalars are frozen)")
+        if self.sharded:
+            raise RuntimeError("a row-sharded slab's step reads its spill / late-round sizes on "
+                               "the host each step and cannot be captured")
         defer = self.opt_sparse.defer_join
         self.opt_sparse.defer_join = self.opt_sparse.fused
         torch.cuda.synchronize()

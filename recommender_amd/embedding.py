@@ -39,12 +39,9 @@ class Embedding(nn.Module):
         self.register_buffer("weight", w)
         self.register_buffer("slot_offsets",
                              None if slot_offsets is None else slot_offsets.to(device, torch.int64))
-        # the largest slot's row count, host-side (the sort picks its form from it)
-        if slot_offsets is None:
-            self.max_slot_rows = self.input_dim
-        else:
-            so = torch.as_tensor(slot_offsets).to("cpu", torch.int64)
-            self.max_slot_rows = max(1, int((so[1:] - so[:-1]).max())) if so.numel() > 1 else 1
+        # the largest slot's row count, host-side (the sort picks its form from it); derived
+        # again whenever the slot_offsets buffer is reloaded (_load_from_state_dict)
+        self._set_max_slot_rows(slot_offsets)
         self.register_buffer("err_flag", torch.zeros(1, dtype=torch.int32, device=device))
         # zero-size leaf that keeps the lookup inside the autograd graph
         self.grad_handle = nn.Parameter(torch.zeros(0, device=device), requires_grad=True)
@@ -201,6 +198,19 @@ class Embedding(nn.Module):
                                                                    device=i.device)
                                for i, _, x in p])
         return (ids, g, v) if with_valid else (ids, g)
+
+    def _set_max_slot_rows(self, slot_offsets):
+        if slot_offsets is None:
+            self.max_slot_rows = self.input_dim
+        else:
+            so = torch.as_tensor(slot_offsets).to("cpu", torch.int64)
+            self.max_slot_rows = max(1, int((so[1:] - so[:-1]).max())) if so.numel() > 1 else 1
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kw):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kw)
+        # the slot-segmented sort trusts max_slot_rows to bound every slot: keep it the
+        # loaded offsets' own (a kernel-side guard flags RS_ERRBIT_RANGE if it ever is not)
+        self._set_max_slot_rows(self.slot_offsets)
 
     def zero_grad_pending(self):
         self._pending = []

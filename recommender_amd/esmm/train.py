@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import argparse
 import time
+from datetime import timedelta
 
 import numpy as np
 import torch
@@ -136,7 +137,8 @@ def train(argv=None):
         if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=timedelta(seconds=180))
         comm = Comm()
     from ..gemm_tuning import use_tuned_gemms
 

@@ -471,7 +471,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
            L.ptr(sums), L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
     if not sharded and emb._prefetch_queue:
         emb.flush_prefetch()  # a later batch's sort, beside this step's update and dense tail
-    if world > 1:
+    if sharded and comm is not None and comm.collective:
         # the dense half of the global step: every MLP gradient is a linear function of these
         # batch sums, so one all-reduce of ≈9 KB replaces the all-reduce of ≈3 MB of gradients
         comm.all_reduce_(sums)

@@ -112,7 +112,7 @@ class PinSageStep:
             grads.append(densify_grad(t, got[0], got[1], self._ws,
                                       out=self.opt_graph.grad_view(nd + i)) if got is not None
                          else None)
-        if self.world > 1:
+        if self.comm is not None and self.comm.collective:
             if any(g is None for g in grads):
                 raise ValueError("sharded static_step: a parameter has no gradient on this rank; "
                                  "the all-reduce needs the same flat layout on every rank")

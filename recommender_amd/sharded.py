@@ -46,18 +46,29 @@ class Comm:
     """All-to-all / all-reduce transport. gloo groups are staged through host memory (CPU tests
     and one-GPU multi-process tests); nccl (= RCCL on ROCm) runs device to device."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_collectives: bool = False):
+        """force_collectives: run the collectives through the process group even at world 1
+        (where they are copies): the RCCL path can then be exercised on a one-GPU box
+        (tests/test_rccl_gpu.py). Off, world 1 short-circuits to device copies."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
+        if force_collectives and not dist.is_initialized():
+            raise RuntimeError("Comm(force_collectives=True) needs an initialised process group")
+        self.force = bool(force_collectives)
+
+    @property
+    def collective(self) -> bool:
+        """True when the collectives go through the process group (world > 1, or forced)."""
+        return self.world > 1 or self.force
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None,
                    async_op: bool = False):
         """Splits None: equal blocks (the sharded slab's capacity-bounded exchange). async_op
         (RCCL): returns the work handle instead of ordering the current stream after it (gloo
         rehearsals stage through the host and return None)."""
-        if self.world == 1:
+        if not self.collective:
             out.copy_(inp)
             return None
         osp = None if out_splits is None else list(out_splits)
@@ -70,7 +81,7 @@ class Comm:
         return dist.all_to_all_single(out, inp, osp, isp, group=self.group, async_op=async_op)
 
     def all_reduce_(self, t: torch.Tensor, op=None):
-        if self.world == 1:
+        if not self.collective:
             return
         op = dist.ReduceOp.SUM if op is None else op
         if self.staged:
@@ -171,7 +182,7 @@ class ShardedSlabEmbedding(nn.Module):
         capacity_factor, + 256, rounded up to 256. The only host sync of the exchange; every
         later step moves fixed [world, capacity] blocks."""
         mx = counts.max().to(torch.int64).reshape(1)
-        if self.world > 1:
+        if self.comm.collective:
             if self.comm.staged:
                 c = mx.cpu()
                 dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.comm.group)
@@ -271,7 +282,7 @@ class ShardedSlabEmbedding(nn.Module):
         """Rows a step ahead need an update that changes only the rows it receives (SGD, lazy
         Adam; Keras Adam's dense decay moves every row) and rows of a multiple-of-4 width."""
         opt = self.optimizer
-        return (self.rows_ahead and self.world > 1 and self.output_dim % 4 == 0
+        return (self.rows_ahead and self.comm.collective and self.output_dim % 4 == 0
                 and opt is not None and opt.kind in (L.RS_OPT_SGD, L.RS_OPT_LAZY_ADAM))
 
     def _gather_send(self, ids: torch.Tensor, out: torch.Tensor):

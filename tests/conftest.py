@@ -79,3 +79,44 @@ def assert_close_f64(got, ref64, ref32, msg="", rtol=1e-5, noise=4.0, floor=1e-7
         raise AssertionError(f"{msg}: {int(bad.sum())} / {bad.size} elements off; first at {i}: "
                              f"got {g.reshape(-1)[i]!r} ref {r.reshape(-1)[i]!r} "
                              f"(max err/tol {float((err / np.maximum(tol, 1e-300)).max()):.3g})")
+
+
+def run_ranks(target, world, args=(), timeout=300):
+    """Spawn `world` processes target(rank, world, *args, q) and collect one (rank, status) each
+    from the queue; fails as soon as a rank dies without reporting (no silent wait for the
+    whole timeout) and prints a heartbeat while waiting. Returns {rank: status}."""
+    import queue as _queue
+    import time as _time
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world, *args, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res, t0, beat = {}, _time.time(), _time.time()
+    try:
+        while len(res) < world:
+            try:
+                r, v = q.get(timeout=5)
+                res[r] = v
+                continue
+            except _queue.Empty:
+                pass
+            dead = [i for i, p in enumerate(ps) if p.exitcode not in (None, 0) and i not in res]
+            if dead:
+                raise AssertionError(f"rank(s) {dead} died (exit {[ps[i].exitcode for i in dead]}) "
+                                     f"before reporting; got {res}")
+            if _time.time() - t0 > timeout:
+                raise AssertionError(f"ranks did not report within {timeout} s; got {res}")
+            if _time.time() - beat > 30:
+                print(f"[run_ranks] waiting: {len(res)}/{world} reported after "
+                      f"{_time.time() - t0:.0f} s", flush=True)
+                beat = _time.time()
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    return res
