@@ -3,7 +3,10 @@
 //
 // Every rank sends every owner a fixed `capacity` C of row slots per step, so both all-to-alls
 // of a step (row ids out, rows back; gradient rows out) move [world, C] blocks with EQUAL split
-// sizes: no host sync on the counts, and the whole step can be stream-ordered and graph-captured.
+// sizes: no host sync on the counts. Two per-step sizes remain host-read — the spill round's C2
+// and the rows-ahead late round's C_late, each read a step after it is known (no stall), but a
+// captured graph would freeze them, so the sharded step is NOT capturable (TrainStep.capture
+// raises for it).
 // A rank's unique rows (owner-major sorted keys, rs_unique_inverse) are dealt to the slots in
 // key order: unique u of owner o goes to slot o·C + (u − first unique of o). Slots left over are
 // padding (id −1: the owner gathers a zero row and its apply leaves the slot out). Rows past C

@@ -711,8 +711,6 @@ constexpr int kSegBins = 1 << kSegBits;
 constexpr int kSegMaxTiles = 32 * 16 / kSegKPL;  // tiles per slot: B <= 131 072
 constexpr int kSegMaxSlots = 64;
 constexpr int kSegMaxBits = 2 * kSegBits;  // slot ids < 2^24
-constexpr int kSegChunk = 256;                 // digits per scan block
-constexpr int kSegChunks = kSegBins / kSegChunk;
 constexpr int kNumXcd = 8;
 
 struct SegArgs {
@@ -730,12 +728,7 @@ struct SegArgs {
   int32_t* scnt;                // [n_slots][tiles] sentinels per tile
   uint2* tmp;                   // [n] (id, position) after pass 0 of a two-pass slot
   uint32_t* keys0;              // [n_slots][tiles][4096] pass-0 keys in tile order (bit 31: sentinel)
-  int32_t* offs0;               // [n_slots][tiles][4096] output index of a tile's first key per digit
-  int32_t* offs1;
   int32_t* starts;              // [2][kSegMaxSlots + 1] valid / sentinel starts per slot (+ totals)
-  int32_t* spre;                // [n_slots][tiles] sentinels of the slot's earlier tiles
-  int32_t* csum0;               // [n_slots][tiles][kSegChunks] keys per 256-digit chunk of a tile
-  int32_t* csum1;
   uint32_t* rows_out;
   int32_t* pos_out;
   int32_t* err_flag;
@@ -814,19 +807,9 @@ __device__ __forceinline__ void seg_load0(const SegArgs& a, const SegSlot& sl, i
   }
 }
 
-// the tile's counts as uint16, and its keys per 256-digit chunk (csum[q], q < kSegChunks): thread
-// j sums digits [16 j, 16 j + 16), 16 threads a chunk
-__device__ __forceinline__ void seg_store_hist(uint16_t* __restrict__ h, int32_t* __restrict__ csum,
-                                               const int32_t* cnt, int bins) {
+// the tile's counts as uint16
+__device__ __forceinline__ void seg_store_hist(uint16_t* __restrict__ h, const int32_t* cnt, int bins) {
   for (int d = threadIdx.x; d < bins; d += blockDim.x) h[d] = static_cast<uint16_t>(cnt[d]);
-  constexpr int PER = kSegBins / kSegThreads;  // 16
-  const int d0 = threadIdx.x * PER;
-  int32_t v = 0;
-#pragma unroll
-  for (int c = 0; c < PER; ++c) v += d0 + c < bins ? cnt[d0 + c] : 0;
-#pragma unroll
-  for (int off = 8; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  if ((threadIdx.x & 15) == 0) csum[threadIdx.x >> 4] = v;
 }
 
 template <bool ID64>
@@ -864,7 +847,7 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
     for (int k = 0; k < kSegKPL; ++k) kt[k * 64] = ((sent >> k) & 1u) ? 0x80000000u : id[k];
   }
   __syncthreads();
-  seg_store_hist(a.hist0 + tile * kSegBins, a.csum0 + tile * kSegChunks, cnt, bins);
+  seg_store_hist(a.hist0 + tile * kSegBins, cnt, bins);
   if (threadIdx.x == 0) {
     const int64_t b0 = (int64_t)t * kSegTile;
     const int64_t tn = a.B - b0 < kSegTile ? a.B - b0 : kSegTile;
@@ -914,83 +897,6 @@ __device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstar
   __syncthreads();
 }
 
-// One block per (slot, 256-digit chunk), after a pass's histograms: offs[t][d] = base + (keys
-// of digits < d in the slot) + (keys of digit d in the slot's tiles < t) for every tile t — the
-// column scan the scatter blocks then read as one 16 KB row each. The keys of the slot's lower
-// chunks come from the tiles' chunk sums (csum); thread j owns digit 256 c + j and loads its
-// column of counts once (every tile's row of the chunk is one coalesced 512 B load). Pass 0 also
-// writes the slot starts and each tile's sentinel prefix.
-template <int PASS>
-__global__ __launch_bounds__(kSegThreads) void slot_sort_scan_kernel(SegArgs a) {
-  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1];
-  __shared__ int32_t wsum[4], wlow[4];
-  const int s = blockIdx.x / kSegChunks, c = blockIdx.x % kSegChunks;
-  if (s >= a.n_slots) return;
-  const SegSlot sl = seg_slot(a, s);
-  if (PASS == 1 && sl.w1 == 0) return;
-  const int bins = 1 << (PASS == 0 ? sl.w0 : sl.w1);
-  if (c * kSegChunk >= bins) return;  // block-uniform
-  if (PASS == 0) {
-    seg_slot_starts(a, vstart, sstart);
-    if (s == 0 && c == 0)
-      for (int q = threadIdx.x; q <= a.n_slots; q += blockDim.x) {
-        a.starts[q] = vstart[q];
-        a.starts[kSegMaxSlots + 1 + q] = sstart[q];
-      }
-    if (c == 0 && threadIdx.x < 64) {  // the sentinel prefix over the slot's tiles (<= 64)
-      const int lane = threadIdx.x;
-      const int32_t z = lane < a.tiles ? a.scnt[s * a.tiles + lane] : 0;
-      int32_t x = z;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-      }
-      if (lane < a.tiles) a.spre[s * a.tiles + lane] = x - z;
-    }
-  } else {
-    if (threadIdx.x <= 1) vstart[s + threadIdx.x] = a.starts[s + threadIdx.x];
-    __syncthreads();
-  }
-  const int32_t base = vstart[s];
-  const int n_tiles = PASS == 0 ? a.tiles : (vstart[s + 1] - base + kSegTile - 1) / kSegTile;
-  const uint16_t* hist = (PASS == 0 ? a.hist0 : a.hist1) + (int64_t)s * a.tiles * kSegBins;
-  const int32_t* cs = (PASS == 0 ? a.csum0 : a.csum1) + (int64_t)s * a.tiles * kSegChunks;
-  int32_t* offs = (PASS == 0 ? a.offs0 : a.offs1) + (int64_t)s * a.tiles * kSegBins;
-  const int d = c * kSegChunk + threadIdx.x;
-  const bool in = d < bins;
-  int32_t h[kSegMaxTiles];
-  int32_t tot = 0;
-#pragma unroll
-  for (int t = 0; t < kSegMaxTiles; ++t) {
-    h[t] = (in && t < n_tiles) ? (int32_t)hist[(int64_t)t * kSegBins + d] : 0;
-    tot += h[t];
-  }
-  int32_t low = 0;  // keys of the slot's digits below this chunk
-  for (int e = threadIdx.x; e < n_tiles * c; e += blockDim.x) low += cs[(e / c) * kSegChunks + e % c];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t x = tot;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int32_t y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-    low += __shfl_xor(low, off);
-  }
-  if (lane == 63) wsum[wave] = x;
-  if (lane == 0) wlow[wave] = low;
-  __syncthreads();
-  int32_t run = base + x - tot + wlow[0] + wlow[1] + wlow[2] + wlow[3];
-  for (int w = 0; w < wave; ++w) run += wsum[w];
-  if (!in) return;
-#pragma unroll
-  for (int t = 0; t < kSegMaxTiles; ++t) {
-    if (t < n_tiles) {
-      offs[(int64_t)t * kSegBins + d] = run;
-      run += h[t];
-    }
-  }
-}
-
 // stable in-tile ranks: rank[k] = position of key k among the tile's keys of its digit that
 // precede it (waves own consecutive stretches; per-wave running counts, then each digit's
 // counts turned into wave offsets). wcnt: [4][kSegBins] uint16 in LDS.
@@ -1026,17 +932,56 @@ __device__ __forceinline__ void seg_rank(const uint32_t (&dig)[kSegKPL], uint32_
   __syncthreads();
 }
 
-// the tile's row of digit offsets into LDS (16 KB, one round trip)
-__device__ __forceinline__ void seg_stage_offs(const int32_t* __restrict__ offs, int bins,
-                                               int32_t* __restrict__ doff) {
-  const int d0 = threadIdx.x * 16;
-  if (d0 + 16 <= bins) {
+// Round 6: the column scan done inside the scatter block (no scan launch, no offs round trip):
+// doff[d] = base + (keys of the slot's digits < d) + (keys of digit d in the slot's tiles < t).
+// Thread j owns digits [16 j, 16 j + 16): it reads its 32-byte slice of every tile's histogram
+// row (the slot's n_tiles rows, L2 / MALL resident: hist0 / hist1 are a few MB), sums them for
+// the digit totals and the tiles before t for the column prefix; one block scan of the 256
+// thread totals orders the digits. The same sums round 5's separate scan launch formed, so the
+// same offsets. wsum: 4 ints of LDS. Ends with a block barrier (doff published).
+__device__ __forceinline__ void seg_offsets_inblock(const uint16_t* __restrict__ hist, int n_tiles,
+                                                    int t, int bins, int32_t base,
+                                                    int32_t* __restrict__ doff, int32_t* wsum) {
+  constexpr int PER = kSegBins / kSegThreads;  // 16
+  const int d0 = threadIdx.x * PER;
+  int32_t tot[PER], pre[PER];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      reinterpret_cast<int4*>(doff + d0)[q] = reinterpret_cast<const int4*>(offs + d0)[q];
-  } else {
-    for (int d = d0; d < bins && d < d0 + 16; ++d) doff[d] = offs[d];
+  for (int i = 0; i < PER; ++i) tot[i] = pre[i] = 0;
+  if (d0 < bins) {  // bins >= 16 or a single thread (bins < 16: the first thread alone)
+    for (int u = 0; u < n_tiles; ++u) {
+      const uint4* row = reinterpret_cast<const uint4*>(hist + (int64_t)u * kSegBins + d0);
+      const uint4 q0 = row[0], q1 = row[1];
+      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int32_t c = d0 + i < bins ? (int32_t)((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) : 0;
+        tot[i] += c;
+        if (u < t) pre[i] += c;
+      }
+    }
   }
+  int32_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) mine += tot[i];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t x = mine;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int32_t run = base + x - mine;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+  if (d0 < bins) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (d0 + i < bins) doff[d0 + i] = run + pre[i];
+      run += tot[i];
+    }
+  }
+  __syncthreads();
 }
 
 template <bool ID64>
@@ -1064,9 +1009,21 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
       else if (in) live |= 1u << k;
     }
   }
-  seg_stage_offs(a.offs0 + ((int64_t)s * a.tiles + t) * kSegBins, bins, doff);
-  const int32_t n_valid = a.starts[a.n_slots];
-  const int32_t sent_base = n_valid + a.starts[kSegMaxSlots + 1 + s] + a.spre[s * a.tiles + t];
+  // slot starts (valid / sentinel ids of the slots before s) from the pass-0 tile counts, this
+  // slot's sentinels in tiles before t, then the digit offsets — all in the block (round 6)
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1], wsc[4];
+  seg_slot_starts(a, vstart, sstart);
+  if (s == 0 && t == 0)  // for pass 1 (later launches)
+    for (int q = threadIdx.x; q <= a.n_slots; q += blockDim.x) {
+      a.starts[q] = vstart[q];
+      a.starts[kSegMaxSlots + 1 + q] = sstart[q];
+    }
+  int32_t spre = 0;
+  for (int u = 0; u < t; ++u) spre += a.scnt[s * a.tiles + u];
+  seg_offsets_inblock(a.hist0 + (int64_t)s * a.tiles * kSegBins, a.tiles, t, bins, vstart[s], doff,
+                      wsc);
+  const int32_t n_valid = vstart[a.n_slots];
+  const int32_t sent_base = n_valid + sstart[s] + spre;
   uint32_t dig[kSegKPL];
   const uint32_t mask = (uint32_t)bins - 1u;
 #pragma unroll
@@ -1149,8 +1106,7 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist1_kernel(SegArgs a)
   for (int k = 0; k < kSegKPL; ++k)
     if ((live >> k) & 1u) atomicAdd(&cnt[id[k] >> sl.w0], 1);
   __syncthreads();
-  seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins,
-                 a.csum1 + ((int64_t)s * a.tiles + t) * kSegChunks, cnt, bins);
+  seg_store_hist(a.hist1 + ((int64_t)s * a.tiles + t) * kSegBins, cnt, bins);
 }
 
 __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs a) {
@@ -1167,7 +1123,9 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter1_kernel(SegArgs
   uint32_t id[kSegKPL], live;
   int32_t pos[kSegKPL];
   seg_load1(a, start, n_s, t, id, pos, live);
-  seg_stage_offs(a.offs1 + ((int64_t)s * a.tiles + t) * kSegBins, bins, doff);
+  __shared__ int32_t wsc[4];
+  seg_offsets_inblock(a.hist1 + (int64_t)s * a.tiles * kSegBins, (n_s + kSegTile - 1) / kSegTile,
+                      t, bins, start, doff, wsc);
   uint32_t dig[kSegKPL];
 #pragma unroll
   for (int k = 0; k < kSegKPL; ++k) dig[k] = id[k] >> sl.w0;
@@ -1444,26 +1402,16 @@ static size_t seg_ws_layout(int64_t n, int n_slots, int tiles, Carver& c, SegArg
   uint32_t* k0 = c.take<uint32_t>(nt * kSegTile);
   uint16_t* h0 = c.take<uint16_t>(nt * kSegBins);
   uint16_t* h1 = c.take<uint16_t>(nt * kSegBins);
-  int32_t* o0 = c.take<int32_t>(nt * kSegBins);
-  int32_t* o1 = c.take<int32_t>(nt * kSegBins);
   int32_t* v = c.take<int32_t>(nt);
   int32_t* z = c.take<int32_t>(nt);
-  int32_t* sp = c.take<int32_t>(nt);
-  int32_t* cs0 = c.take<int32_t>(nt * kSegChunks);
-  int32_t* cs1 = c.take<int32_t>(nt * kSegChunks);
   int32_t* st = c.take<int32_t>(2 * (kSegMaxSlots + 1));
   uint2* tmp = c.take<uint2>(n);
   if (a) {
     a->keys0 = k0;
     a->hist0 = h0;
     a->hist1 = h1;
-    a->offs0 = o0;
-    a->offs1 = o1;
     a->vcnt = v;
     a->scnt = z;
-    a->spre = sp;
-    a->csum0 = cs0;
-    a->csum1 = cs1;
     a->starts = st;
     a->tmp = tmp;
   }
@@ -1482,23 +1430,8 @@ static bool seg_eligible(int64_t n_ids, int n_slots, int world, int64_t max_slot
 size_t seg_ws_size(int64_t n_ids) {
   // tiles over all slots <= n/4096 + n_slots (each slot rounds up once)
   const int64_t tiles_total = n_ids / kSegTile + kSegMaxSlots;
-  SegArgs a{};
   Carver c(nullptr, 0);
-  (void)a;
-  const size_t nt = (size_t)tiles_total;
-  c.take<uint32_t>(nt * kSegTile);
-  c.take<uint16_t>(nt * kSegBins);
-  c.take<uint16_t>(nt * kSegBins);
-  c.take<int32_t>(nt * kSegBins);
-  c.take<int32_t>(nt * kSegBins);
-  c.take<int32_t>(nt);
-  c.take<int32_t>(nt);
-  c.take<int32_t>(nt);
-  c.take<int32_t>(nt * kSegChunks);
-  c.take<int32_t>(nt * kSegChunks);
-  c.take<int32_t>(2 * (kSegMaxSlots + 1));
-  c.take<uint2>(n_ids);
-  return c.off + 1024;
+  return seg_ws_layout(n_ids, 1, (int)tiles_total, c, nullptr) + 1024;
 }
 
 static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const uint8_t* valid,
@@ -1530,15 +1463,11 @@ static int32_t seg_sort(const void* ids, int32_t id_dtype, int64_t n_ids, const 
   if (id_dtype == RS_ID_I64) slot_sort_hist0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_hist0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
-  slot_sort_scan_kernel<0><<<n_slots * kSegChunks, kSegThreads, 0, st>>>(a);
-  RS_CHECK_LAUNCH();
   if (id_dtype == RS_ID_I64) slot_sort_scatter0_kernel<true><<<grid0, kSegThreads, 0, st>>>(a);
   else slot_sort_scatter0_kernel<false><<<grid0, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   // pass 1 only matters for slots wider than 12 bits; its blocks of narrower slots exit at once
   slot_sort_hist1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
-  RS_CHECK_LAUNCH();
-  slot_sort_scan_kernel<1><<<n_slots * kSegChunks, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();
   slot_sort_scatter1_kernel<<<grid1, kSegThreads, 0, st>>>(a);
   RS_CHECK_LAUNCH();

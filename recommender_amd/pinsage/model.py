@@ -23,6 +23,17 @@ def oob_flag(dev) -> torch.Tensor:
     return f
 
 
+def check_oob(dev) -> None:
+    """Raise RecsysError (and clear the flag) if a fused pair kernel saw a node id past h's
+    rows since the last check: the index_select they replace raised on one. Synchronises; called
+    at the train loop's sync points (PinSageStep.__call__, the logging steps of main())."""
+    f = _err_flags.get(dev)
+    if f is not None and int(f.item()):
+        f.zero_()
+        raise L.RecsysError("PinSage: a node id outside the representation rows (the pair "
+                            "kernels read a zero row and dropped its gradient)")
+
+
 _ws_bufs: dict = {}
 
 

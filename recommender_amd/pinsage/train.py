@@ -26,7 +26,7 @@ from ..synthetic import ML20M, movielens_graph
 from .evaluation import (build_val_test_matrix, get_item_reprs, hit_rate_eval, recommend,
                          train_test_split_by_time)
 from .graph import HeteroGraph
-from .model import PinSageModel
+from .model import PinSageModel, check_oob
 from .sampler import PinSageSampler, item_pairs
 
 ML1M = dict(n_users=6_040, n_items=3_706, n_edges=1_000_209)
@@ -72,6 +72,7 @@ class PinSageStep:
         else:
             self.opt_dense.step()
             self.opt_sparse.step()
+        check_oob(loss.device)  # the dynamic step syncs on its shapes anyway
         return loss.detach()
 
     # -- sync-free step on capacity-shaped batches (PinSageSampler.sample_static) ------------
@@ -254,6 +255,7 @@ def main(argv=None):
             loss = step_fn(*batch)
         if step % 50 == 0:
             print(f"step {step} step_loss {float(loss):.4f}")
+            check_oob(loss.device)  # the graph steps' out-of-range node ids, checked here
         if args.eval_every and step % args.eval_every == 0:
             reprs = get_item_reprs(model, sampler, g, g.itype, 32)
             recs = recommend(g, args.top_k, reprs, None, g.utype, "timestamp", 32)

@@ -334,10 +334,16 @@ class ShardedSlabEmbedding(nn.Module):
         nxt["late"] = dict(rows=late_rows, recv_slot=recv_slot, count=(ev, host), pred=seq)
         self._issue_early(nxt)
 
-    def check_overflow(self, block: bool = True):
-        """Kept for callers of the round-4 API: a batch past the capacity now takes a spill
-        round (exchange_finish) instead of raising, so there is nothing to check."""
-        return None
+    def invalidate_rows_ahead(self):
+        """The shard's rows were written by something other than the owner apply (a
+        load_state_dict, a re-init, a manual edit): every queued step's early rows are stale, so
+        each re-sends its whole block after the applies before it ('full' mode). The mode is
+        decided from _apply_count alone, the same on every rank — call this on every rank."""
+        self._apply_count += 2
+
+    def _load_from_state_dict(self, *args, **kw):
+        super()._load_from_state_dict(*args, **kw)
+        self.invalidate_rows_ahead()
 
     @staticmethod
     def _ids_key(ids):

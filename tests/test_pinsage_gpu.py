@@ -888,7 +888,13 @@ def test_pair_margin_out_of_range_node_flags_and_reads_zero():
     ref = torch.clamp(neg + 1.0 - pos, min=0).mean()
     assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref))
     assert torch.isfinite(h1.grad).all()
-    flag.zero_()
+    # the train loop's sync points turn the flag into an error (and clear it)
+    from recommender_amd.pinsage.model import check_oob
+
+    with pytest.raises(L.RecsysError, match="outside the representation rows"):
+        check_oob(h.device)
+    assert int(flag) == 0
+    check_oob(h.device)  # clear: no error
 
 
 def test_multihot_mean_lookup_matches_gather_mean():

@@ -6,7 +6,8 @@ handles and the cross-stream order of the exchange run as they will at world 8.
 (a) The production fused DLRM step on a ShardedSlabEmbedding (reference ctr/train.py:71-97,
     ctr/model.py:45-57) over RCCL, with the exchange prefetched a step ahead (rows ahead + the
     late round run at world 1 when collectives are forced), equals the one-GPU step bit for bit:
-    loss, slab and every MLP parameter, four steps.
+    loss, slab and every MLP parameter, six steps — the fifth after a load_state_dict between its
+    prefetch and its exchange (rows ahead invalidated: it re-sends its whole block).
 (b) PinSage's sync-free step (pinsage/train/train.py:40-48) with its flat-gradient all-reduce
     captured into a HIP graph under RCCL and replayed equals the same graph without the
     collective, bit for bit."""
@@ -46,16 +47,26 @@ def _dlrm_part():
         s2.capture_sequence([])
     r = np.random.default_rng(0)
     batches = [tuple(torch.from_numpy(x).to(DEV) for x in criteo_batch(r, B, cards))
-               for _ in range(4)]
+               for _ in range(6)]
     for k, b in enumerate(batches):
         assert s2.fused_step_ready(b)
+        if k == 4:
+            # a write to the shard after this step's early rows were gathered (during step 3)
+            # and before its exchange: they are stale, so it re-sends its whole block ('full')
+            emb.join()
+            torch.cuda.synchronize()
+            new_w = m1.embedding_layer.weight * 0.5 + 0.01
+            m1.embedding_layer.weight.copy_(new_w)
+            sd2 = emb.state_dict()
+            sd2["shard.weight"] = new_w.clone()
+            emb.load_state_dict(sd2)
         if k + 1 < len(batches):
             s2.prefetch(batches[k + 1])
         l1, l2 = float(s1(b)), float(s2(b))
         assert l1 == l2, (k, l1, l2)
     emb.join()
     torch.cuda.synchronize()
-    assert emb.rows_ahead_modes == {"fresh": 1, "late": 3, "full": 0}, emb.rows_ahead_modes
+    assert emb.rows_ahead_modes == {"fresh": 1, "late": 4, "full": 1}, emb.rows_ahead_modes
     assert torch.equal(emb.full_weight(), m1.embedding_layer.weight), "slab"
     for a, b_ in zip(list(m1.bottom_mlp.parameters()) + list(m1.top_mlp.parameters()),
                      list(m2.bottom_mlp.parameters()) + list(m2.top_mlp.parameters())):

@@ -68,6 +68,10 @@ def main():
 
     dst = torch.empty_like(dxu)
     res = {}
+    sort = lambda: L.call("rs_sort_ids_slots", L.ptr(ids), L.id_dtype_code(ids), n, None,  # noqa: E731
+                          L.ptr(so), S, V, emb.max_slot_rows, L.ptr(rows), L.ptr(pos), None,
+                          L.ptr(err), L.ptr(sws), sws.numel(), st)
+    res["sort"] = [round(timed(sort), 1), round(timed(sort), 1)]
     for rep in range(2):
         for name, fn in (("apply_real", apply(pos)), ("apply_contig", apply(ar)),
                          ("apply_contig_noscale", apply(ar, False)),
