@@ -374,6 +374,11 @@ def main():
                            "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_step": int(by),
                            "parameters": int(n_el),
                            "note": "dense Keras Adam over every table / whole step time"}
+    if args.model == "dien":
+        out["roofline"] = dien_roofline(args, train_d if args.dien_mode == "graph" else step,
+                                        batches, B, sec)
+    if args.model == "pinsage":
+        out["roofline"] = pinsage_roofline(train, smp, B, sec)
     if args.model in ("esmm", "mmoe"):
         # the dense layers' GEMM work against the fp32 MFMA peak (157.3 TF/s: no xf32 on gfx950)
         # — the floor the library fp32 GEMMs set for the step
@@ -386,6 +391,73 @@ def main():
                            "note": "the whole step's time over its dense GEMM FLOPs (embedding, "
                                    "apply and elementwise work included in the time)"}
     print(json.dumps(out))
+
+
+def dien_roofline(args, ds, batches, B, sec):
+    """cfg3's step against what bounds it. The four recurrences (GRU / AUGRU, forward and
+    backward) walk L = 100 dependent steps each, so their figure is µs per dependent step
+    (timed on two eager static_steps after the run: graph replays record no kernel events);
+    the step's GEMM-shaped arithmetic (recurrences' input and recurrent products, the aux net on
+    its live rows, the head MLP: forward + both backward products, 6·in·out FLOP per row) is
+    set against the fp32 MFMA peak (157.3 TF/s, no xf32 on gfx950) over the whole step."""
+    names = ["rs_gru_fwd", "rs_gru_bwd", "rs_augru_fwd", "rs_augru_bwd", "rs_dien_aux_fwd",
+             "rs_dien_aux_bwd_acc", "rs_dien_attention_fwd", "rs_dien_attention_bwd"]
+    timer = L.KernelTimer(names)
+    L.set_timer(timer)
+    timer.enabled = True
+    for f, lab in batches[:2]:
+        ds.static_step(f, lab)
+    torch.cuda.synchronize()
+    timer.enabled = False
+    L.set_timer(None)
+    kt = {n: round(ms / c * 1e3, 1) for n, (ms, c) in timer.totals_ms().items() if c}
+    L_, H, E = 100, 36, 36
+    rec_us = sum(kt.get(n, 0.0) for n in names[:4])
+    # the aux net's live rows: history steps t whose next step t + 1 is not padding (mask_zero)
+    live = float((batches[0][0]["pos_his_item"][:, 1:] != 0).sum())
+    rows = B * L_  # the recurrences as Keras runs them: every step of every history, masked
+    fl = 6.0 * rows * (E * 3 * H + H * 3 * H) * 2          # GRU + AUGRU: x·W and h·U
+    fl += 6.0 * 2 * live * ((H + E) * 80 + 80 * 40 + 40)   # aux net, pos + neg, live rows
+    head_in = 2 * E + 2 * H + E + 18                        # the head's concat width (approx.)
+    fl += 6.0 * B * (head_in * 200 + 200 * 80 + 80)
+    return {"bound": "latency (4 recurrences x L = 100 dependent steps)",
+            "recurrences_us": round(rec_us, 1),
+            "us_per_dependent_step": round(rec_us / (4 * L_), 3),
+            "kernels_us_eager": kt,
+            "gemm_gflop_per_step": round(fl / 1e9, 2), "achieved_TFs": round(fl / sec / 1e12, 2),
+            "peak_TFs": 157.3, "frac": round(fl / sec / 157.3e12, 4),
+            "note": "frac = GEMM-shaped FLOPs / whole step time vs the fp32 MFMA peak; the step "
+                    "is bound by the recurrences' dependent chains, not by FLOPs or bytes"}
+
+
+def pinsage_roofline(train, smp, B, sec):
+    """cfg5's step in HBM bytes (algorithmic, the live sizes of one sampled batch): the metapath
+    walks (per seed 4 walks x 2 item-user-item steps, each hop an indptr pair + a neighbour:
+    20 B), the two SAGE layers' weighted mean aggregation forward and backward (per live edge a
+    source row read, 4·H B, each way; per destination its row written / read), the item
+    features (id / year lookups + genre multi-hot mean) of every source node forward and
+    backward, and Keras Adam over every variable (GraphKerasAdam: 32 B per element). Over the
+    whole replayed step; the step is bound by dependent random loads (the walks) and launches."""
+    batch = smp.sample_static(*smp.sample_pairs_static(B, 4, 10_000))
+    _, _, blocks = batch
+    torch.cuda.synchronize()
+    H = 32
+    by = 0
+    for blk in blocks:
+        n_dst = int(blk.n_dst_live.item()) if blk.n_dst_live is not None else blk.n_dst
+        n_src = int(blk.n_src_live.item()) if blk.n_src_live is not None else blk.n_src
+        n_e = int(blk.n_edges.item())
+        by += n_dst * 4 * 2 * 20                    # the walks that sampled this block's sources
+        by += 2 * (n_e * (4 * H + 12) + n_dst * 4 * H)  # aggregation forward + backward
+        by += 2 * n_src * (8 + 4 * 16)              # item features of the sources, fwd + bwd
+    n_el = sum(p.numel() for p in train.opt_graph.params) if getattr(train, "opt_graph", None) \
+        else sum(p.numel() for p in train.dense)
+    by += 32 * n_el
+    gbs = by / sec / 1e9
+    return {"bound": "hbm (latency: dependent walk loads)", "achieved": round(gbs, 1),
+            "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4),
+            "algorithmic_bytes_per_step": int(by), "adam_elements": int(n_el),
+            "note": "live-size algorithmic bytes of one sampled batch / whole replayed step"}
 
 
 def deepfm_from_file(args):

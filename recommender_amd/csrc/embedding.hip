@@ -195,6 +195,9 @@ struct ApplyArgs {
   // treated as the OOB sentinel (dropped). 0 = every key below n_rows (the row-sharded exchange
   // deduplicates its two owner halves in two launches, rs_embedding_dedup_grad_mapped_range)
   uint32_t key_lo;
+  // a key-range walk over part of the key space (the owner halves): groups with no key in range
+  // exit before walking (seg_group32_kernel); 0 for full-range walks
+  int ranged;
   // OPT_DENSE: the gradient rows in up to 4 segments — position p in [gstart[i], gstart[i+1])
   // reads gseg[i] + (p - gstart[i]) * gld[i] (a table looked up several times hands each
   // lookup's upstream rows, strided column blocks included, without concatenating them);
@@ -613,15 +616,21 @@ __global__ __launch_bounds__(1024) void seg_group32_kernel(const uint32_t* __res
   const int gi = threadIdx.x >> 5, gl = threadIdx.x & 31;
   const int64_t t = (int64_t)blockIdx.x * G + gi;
   const bool live = t < n_tiles;
-  if (threadIdx.x == 0) {  // no key of the group in [key_lo, n_rows): nothing to sum or write
-    const int64_t f = (int64_t)blockIdx.x * G * T;
-    const int64_t l = (f + (int64_t)G * T < n ? f + (int64_t)G * T : n) - 1;
-    skip = f < n && (keys[l] < a.key_lo || keys[f] >= n_rows);
-  }
-  __syncthreads();
-  if (skip) {  // the walk would find no run in range: the same (empty) tile flags
-    if (gl == 0 && live) a.tile_flags[t] = 0;
-    return;
+  // Key-range walks only (the row-sharded dedup's owner halves: a.ranged, a kernel argument,
+  // so the branch is uniform): a group with no key in [key_lo, n_rows) has nothing to sum or
+  // write. The full-range walk (the production apply) skips the check (two dependent key loads
+  // and a block barrier per group; interleaved A/B, round 6: no measurable cost either way).
+  if (a.ranged) {
+    if (threadIdx.x == 0) {
+      const int64_t f = (int64_t)blockIdx.x * G * T;
+      const int64_t l = (f + (int64_t)G * T < n ? f + (int64_t)G * T : n) - 1;
+      skip = f < n && (keys[l] < a.key_lo || keys[f] >= n_rows);
+    }
+    __syncthreads();
+    if (skip) {  // the walk would find no run in range: the same (empty) tile flags
+      if (gl == 0 && live) a.tile_flags[t] = 0;
+      return;
+    }
   }
   Tile32Edges e{};
   if (live) e = tile32_walk<OPT, Q>(keys, pos, n, n_rows, grad, a, t, &ps[gi][0][0]);
@@ -1346,6 +1355,7 @@ extern "C" int32_t rs_embedding_dedup_grad_mapped_range(
   a.scale_group = scale_group;
   a.seg_map = seg_map;
   a.key_lo = key_lo;
+  a.ranged = key_lo != 0 || (int64_t)key_hi < n_rows;
   const void* ptrs[2] = {grad_out, uniq_grad};
   RowGeom geom = row_geom(dim, ptrs, 2);
   return launch_segments(OPT_EMIT, sorted_rows, sorted_pos, n_ids, key_hi, grad_out, a, geom, st);

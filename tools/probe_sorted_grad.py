@@ -5,7 +5,8 @@ Runs rs_embedding_apply_scaled (SGD, lr 0: same bytes) on the bench's slab, ids 
   contig    positions = 0..n-1 (each tile's 32 rows read contiguously; row_scale index wrong,
             timing only)
 and the train kernel with its rows written in position order, plus a plain HBM copy of the same
-bytes for reference. HIP events over 20 launches each, interleaved twice.
+bytes for reference. HIP events over 20 launches each, interleaved three times.
+PROBE_VARIANT=<path to an A/B build's .so>: the production apply against that build's, interleaved.
     python tools/probe_sorted_grad.py
 """
 from __future__ import annotations
@@ -72,10 +73,26 @@ def main():
                           L.ptr(so), S, V, emb.max_slot_rows, L.ptr(rows), L.ptr(pos), None,
                           L.ptr(err), L.ptr(sws), sws.numel(), st)
     res["sort"] = [round(timed(sort), 1), round(timed(sort), 1)]
-    for rep in range(2):
-        for name, fn in (("apply_real", apply(pos)), ("apply_contig", apply(ar)),
-                         ("apply_contig_noscale", apply(ar, False)),
-                         ("copy_grad_bytes", lambda: dst.copy_(dxu))):
+    variant = os.environ.get("PROBE_VARIANT")  # an A/B build of the library (same C-ABI)
+    vapply = None
+    if variant:
+        import ctypes as C
+        vl = C.CDLL(variant)
+        f = vl.rs_embedding_apply_scaled
+        f.restype, f.argtypes = L.lib().rs_embedding_apply_scaled.restype, L.lib().rs_embedding_apply_scaled.argtypes
+
+        def vapply():
+            rc = f(L.RS_OPT_SGD, L.ptr(w), None, None, V, D, L.ptr(rows), L.ptr(pos), n, L.ptr(dxu),
+                   L.ptr(gb), S, prm, None, L.ptr(aws), aws.numel(), st)
+            assert rc == 0
+    for rep in range(3):
+        cases = [("apply_real", apply(pos))]
+        if vapply is not None:
+            cases.append(("apply_variant", vapply))
+        if not variant:
+            cases += [("apply_contig", apply(ar)), ("apply_contig_noscale", apply(ar, False)),
+                      ("copy_grad_bytes", lambda: dst.copy_(dxu))]
+        for name, fn in cases:
             res.setdefault(name, []).append(round(timed(fn), 1))
     uniq = int(torch.unique(rows).numel())
     print(json.dumps({"probe": "sorted_grad", "unique_rows": uniq, "us": res}), flush=True)
