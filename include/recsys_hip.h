@@ -1126,6 +1126,20 @@ int32_t rs_dlrm_train_step_fwd_unit(const float* table, int64_t n_rows, int32_t 
                                     float loss_scale, float* y, float* unit_rows, float* g_rows,
                                     float* sums, void* workspace, size_t ws_bytes,
                                     int32_t* err_flag, void* stream);
+/* The same step in two calls (round 6): _nofold runs the kernel only (y, unit_rows and g_rows are
+ * final after it; the per-block partial sums stay in the workspace), rs_dlrm_train_fold folds them
+ * into sums — bit-identical to the one-call form. The production step orders its sparse update
+ * after the kernel alone and folds on its own stream meanwhile. */
+int32_t rs_dlrm_train_step_fwd_unit_nofold(const float* table, int64_t n_rows, int32_t D,
+                                           const void* ids, int32_t id_dtype, int32_t n_slots,
+                                           const int64_t* slot_offsets, const float* dense,
+                                           const float* xin, int32_t n_in, const float* label,
+                                           int64_t batch, const float* q, const float* c,
+                                           float eps, float loss_scale, float* y,
+                                           float* unit_rows, float* g_rows, void* workspace,
+                                           size_t ws_bytes, int32_t* err_flag, void* stream);
+int32_t rs_dlrm_train_fold(const void* workspace, size_t ws_bytes, int64_t batch, int32_t D,
+                           int32_t id_dtype, float* sums, void* stream);
 
 /* ---- the production DLRM step's dense tail (ctr/train.py:77-79 SGD of every MLP parameter;
  * ctr/layers.py:5-14 linear hidden layers) ------------------------------------------------

@@ -203,6 +203,10 @@ _SIGS = {
     "rs_dlrm_train_step_fwd_unit": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32, _p,
                                            _i64, _p, _p, C.c_float, C.c_float, _p, _p, _p, _p, _p,
                                            _sz, _p, _p]),
+    "rs_dlrm_train_step_fwd_unit_nofold": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _i32,
+                                                  _p, _i64, _p, _p, C.c_float, C.c_float, _p, _p,
+                                                  _p, _p, _sz, _p, _p]),
+    "rs_dlrm_train_fold": (_i32, [_p, _sz, _i64, _i32, _i32, _p, _p]),
     "rs_tfrecord_index": (_i32, [_p, _i64, _i32, _p, _p, _i64, _p]),
     "rs_tfrecord_parse_criteo": (_i32, [_p, _p, _p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "rs_vocab_count": (_i32, [_p, _i64, _i64, _p, _p, _p, _i64, _p, _p]),

@@ -1693,12 +1693,21 @@ extern "C" size_t rs_dlrm_train_workspace_size(int64_t batch) {
   return (size_t)(ceil_div(batch, 4) + 32) * kTrainM * sizeof(float) + 256;
 }
 
+// the train kernel's grid for (batch, D): one round of resident blocks (the fold needs it too)
+static int64_t train_blocks(int64_t batch, int32_t D, int id_dtype) {
+  const void* k = D == 128 ? (id_dtype == RS_ID_I64 ? reinterpret_cast<const void*>(dlrm_train_chunk<128, true>)
+                                                    : reinterpret_cast<const void*>(dlrm_train_chunk<128, false>))
+                           : (id_dtype == RS_ID_I64 ? reinterpret_cast<const void*>(dlrm_train_chunk<64, true>)
+                                                    : reinterpret_cast<const void*>(dlrm_train_chunk<64, false>));
+  return ceil_div(batch, 4 * (int64_t)pipe_epw(k, batch, 1));
+}
+
 static int32_t train_step_launch(
     const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
     int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
     int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
     float loss_scale, float* y, float* grad_emb, float* sums, void* workspace, size_t ws_bytes,
-    int32_t* err_flag, void* stream, float* g_rows) {
+    int32_t* err_flag, void* stream, float* g_rows, bool fold = true) {
   const int F = n_slots + 1;
   RS_CHECK_ARG((D == 128 || D == 64) && n_slots >= 1 && F <= kDxRows && n_in == kTrainNI &&
                    batch >= 1,
@@ -1731,6 +1740,7 @@ static int32_t train_step_launch(
     else go(dlrm_train_chunk<64, false>);
   }
   RS_CHECK_LAUNCH();
+  if (!fold) return RS_OK;
   const int tm = D == 128 ? train_m<128>() : train_m<64>();
   return fold_two_level(part, (int)blocks, tm, part + (size_t)blocks * tm, sums, st);
 }
@@ -1745,4 +1755,32 @@ extern "C" int32_t rs_dlrm_train_step_fwd_unit(
   return train_step_launch(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets, dense, xin,
                            n_in, label, batch, q, c, eps, loss_scale, y, unit_rows, sums,
                            workspace, ws_bytes, err_flag, stream, g_rows);
+}
+
+// The same step as two calls: the kernel alone (its per-block partial rows left in the workspace),
+// then rs_dlrm_train_fold for the batch sums. The gradient rows, G and y are final after the
+// first call, so the sparse update can be ordered after the kernel alone (not after the fold too).
+extern "C" int32_t rs_dlrm_train_step_fwd_unit_nofold(
+    const float* table, int64_t n_rows, int32_t D, const void* ids, int32_t id_dtype,
+    int32_t n_slots, const int64_t* slot_offsets, const float* dense, const float* xin,
+    int32_t n_in, const float* label, int64_t batch, const float* q, const float* c, float eps,
+    float loss_scale, float* y, float* unit_rows, float* g_rows, void* workspace,
+    size_t ws_bytes, int32_t* err_flag, void* stream) {
+  RS_CHECK_ARG(g_rows, "null pointer");
+  float dummy_sums[1];
+  return train_step_launch(table, n_rows, D, ids, id_dtype, n_slots, slot_offsets, dense, xin,
+                           n_in, label, batch, q, c, eps, loss_scale, y, unit_rows, dummy_sums,
+                           workspace, ws_bytes, err_flag, stream, g_rows, false);
+}
+
+extern "C" int32_t rs_dlrm_train_fold(const void* workspace, size_t ws_bytes, int64_t batch,
+                                      int32_t D, int32_t id_dtype, float* sums, void* stream) {
+  RS_CHECK_ARG((D == 128 || D == 64) && batch >= 1, "rs_dlrm_train_fold: D = 128 or 64, batch >= 1");
+  RS_CHECK_ARG(id_dtype == RS_ID_I32 || id_dtype == RS_ID_I64, "bad id dtype");
+  RS_CHECK_ARG(workspace && sums, "null pointer");
+  RS_CHECK_ARG(ws_bytes >= rs_dlrm_train_workspace_size(batch), "workspace too small");
+  const int64_t blocks = train_blocks(batch, D, id_dtype);
+  const int tm = D == 128 ? train_m<128>() : train_m<64>();
+  float* part = static_cast<float*>(const_cast<void*>(workspace));
+  return fold_two_level(part, (int)blocks, tm, part + (size_t)blocks * tm, sums, as_stream(stream));
 }
