@@ -34,7 +34,7 @@ from recommender_amd.ctr.train import TrainStep, build_model  # noqa: E402
 from recommender_amd.synthetic import criteo_batch, criteo_cardinalities  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-WATCH = ["rs_dlrm_train_step_fwd_unit",
+WATCH = ["rs_dlrm_train_step_fwd_unit", "rs_dlrm_train_step_fwd_unit_nofold",
          "rs_dlrm_interaction_fwd", "rs_dlrm_interaction_fwd_head",
          "rs_dlrm_interaction_fwd_head_dx",
          "rs_dlrm_interaction_bwd", "rs_dlrm_interaction_bwd_rank1", "rs_sort_ids_slots",
@@ -299,7 +299,8 @@ def kernel_bytes(name, B, S, D, id_bytes, U, world=1, cap=0):
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 * Z + S * 4 * D + 4 * D)
     if name == "rs_dlrm_interaction_bwd_rank1":  # grad row = G[b] * p: 4 B per example, not 4Z
         return B * (S * id_bytes + S * 4 * D + 4 * D + 4 + S * 4 * D + 4 * D)
-    if name == "rs_dlrm_train_step_fwd_unit":  # ids, rows, bottom row, 13 inputs + label in;
+    if name in ("rs_dlrm_train_step_fwd_unit", "rs_dlrm_train_step_fwd_unit_nofold"):
+        # ids, rows, bottom row, 13 inputs + label in;
         # y, G[b] and the S unit gradient rows out (the batch sums are weight-sized)
         return B * (S * id_bytes + S * 4 * D + 4 * D + 13 * 4 + 4 + 4 + 4 + S * 4 * D)
     if name == "rs_dlrm_interaction_fwd_head_dx":  # + the unit gradient rows (S + 1 per example)
@@ -658,7 +659,8 @@ def main():
                               "achieved_GBs": round(by / (us * 1e-6) / 1e9, 1),
                               "frac": round(by / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                               "traffic": round(t) if t is not None else None,
-                              "in_step_span_us": kern.get(n_, kern.get(n_ + "_scaled", {})).get("avg_us")}
+                              "in_step_span_us": kern.get(n_, kern.get(n_ + "_scaled", kern.get(
+                                  n_ + "_nofold", {}))).get("avg_us")}
         tsum = sum(v["traffic"] for v in per_kernel.values()) if traffic and all(
             v["traffic"] is not None for v in per_kernel.values()) else None
         dom = max(iso, key=iso.get)

@@ -447,8 +447,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         w = emb.weight
         D = w.shape[1]
         dev = w.device
-        if not _train_on_side(emb):  # on the update's stream the kernel is ordered after it
-            _wait_update(emb)
+        _wait_update(emb)
         # the fused kernel is one round of resident blocks: launched while the sort stream's last
         # scatter still holds CU slots, some of dlrm_train_pipe's blocks were placed a round late
         # (measured: 0.42 -> 0.62 ms whenever the two overlapped), so that kernel waits for the
@@ -467,28 +466,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
     scale = 1.0 / n_global if reduction == "mean" else 1.0
     g_rows = torch.empty(B, device=dev, dtype=torch.float32)
     early = _APPLY_EARLY and not sharded
-    if early and _train_on_side(emb):
-        # the kernel, the fold and the update on the update's own stream: the table's chain
-        # (update k -> kernel k+1 -> update k+1) has no cross-stream hop; this stream (the bottom
-        # MLP, the dense tail) joins it only for the fold's sums
-        side = emb.fused_optimizer.side
-        main = torch.cuda.current_stream(dev)
-        side.wait_stream(main)
-        for t in (y, grad, g_rows, sums, h, x, lab, kid):
-            t.record_stream(side)
-        with torch.cuda.stream(side):
-            L.call("rs_dlrm_train_step_fwd_unit_nofold", L.ptr(w), n_rows, D, L.ptr(kid),
-                   L.id_dtype_code(kid), S, L.ptr(offs), L.ptr(h), L.ptr(x), n_in, L.ptr(lab), B,
-                   L.ptr(q), L.ptr(c), float(epsilon), scale, L.ptr(y), L.ptr(grad),
-                   L.ptr(g_rows), L.ptr(ws), ws.numel(), L.ptr(emb.err_flag), L.stream_ptr(dev))
-            L.call("rs_dlrm_train_fold", L.ptr(ws), ws.numel(), B, D, L.id_dtype_code(kid),
-                   L.ptr(sums), L.stream_ptr(dev))
-            folded = torch.cuda.Event()
-            folded.record(side)
-            emb.fused_optimizer.apply_async(emb, ids, grad, emb.take_presorted(ids),
-                                            row_scale=g_rows)
-        main.wait_event(folded)
-    elif early:
+    if early:
         # the kernel alone, then the sparse update ordered after it (the rows, G and y are final
         # there), then the batch-sum fold on this stream beside the update: the update no longer
         # waits for the fold's two launches (round 6; bit-identical to the one-call form)
@@ -630,12 +608,7 @@ def _tail_ws(n0, n1, n2, dev):
 
 _train_ws_cache: dict = {}
 _APPLY_EARLY = os.environ.get("RS_APPLY_EARLY", "1") == "1"
-_TRAIN_ON_SIDE = os.environ.get("RS_TRAIN_ON_SIDE", "0") == "1"
 
-
-def _train_on_side(emb) -> bool:
-    """The fused step launches its train kernel on the fused optimizer's update stream."""
-    return _TRAIN_ON_SIDE and getattr(emb, "fused_optimizer", None) is not None
 
 
 def _train_ws(B, dev):

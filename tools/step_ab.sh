@@ -25,7 +25,6 @@ for rep in ${REPS:-1 2}; do
       prefetch) run prefetch X=1 -- --prefetch 1 || exit 1 ;;
       waitsort) run waitsort RS_TRAIN_WAITS_SORT=1 -- || exit 1 ;;
       mainprio) run mainprio X=1 -- --prio 1 || exit 1 ;;
-      trainside) run trainside RS_TRAIN_ON_SIDE=1 -- || exit 1 ;;
     esac
   done
 done
