@@ -302,23 +302,63 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
 
   const int64_t n_live = *g.n_items;
   const int64_t n_pairs_live = (n_live + 1) / 2;
+  const float* e = set == 0 ? a.pos : a.neg;
+  float* de = set == 0 ? g.dpos : g.dneg;
+  // Round 6: a round's global inputs are loaded one round ahead (at one wave per SIMD nothing
+  // else hides their latency): the item of the round after next (stage A), and for the next
+  // round its example's count, mask bit, upstream daux, the 16 rows' x = [h, e] and — for the
+  // pos waves — the dL/dh rows the h part is added to (stage B). Same values, same arithmetic.
+  struct RoundIn {
+    int64_t b;
+    int t;
+    bool live, m;
+    float sb;
+    float xv[In / 4];
+    f4 dh[kT1];
+  };
+  auto item_of = [&](int64_t p, bool& lv) -> int64_t {
+    const int64_t li = 2 * p + io;
+    lv = p < n_pairs_live && li < n_live;
+    return lv ? g.items[li] : 0;
+  };
+  auto fetch = [&](int64_t it, bool lv, RoundIn& r) {
+    r.live = lv;
+    r.b = it % a.B;
+    r.t = 16 * (int)(it / a.B) + j;
+    const int cnt = g.cnt[r.b];
+    r.m = lv && r.t <= L - 2 && a.mask[r.b * L + r.t + 1] != 0;
+    // dL/d(loss sum of b) = daux_b / (2·cnt)  (0 rows → inf·0 = NaN, as the reference)
+    r.sb = g.daux[r.b] / ((float)cnt * 2.f);
+    if (lv) load_x<H, E>(a, e, r.b, r.t, kq, r.xv);
+#pragma unroll
+    for (int x = 0; x < kT1; ++x) {
+      r.dh[x] = f4{0.f, 0.f, 0.f, 0.f};
+      const int f0 = 16 * x + 4 * kq;
+      if (set == 0 && g.acc_hidden && lv && r.t < L && f0 < H)
+        r.dh[x] = *reinterpret_cast<const f4*>(g.dhidden + (r.b * L + r.t) * (int64_t)H + f0);
+    }
+  };
+  RoundIn cur;
+  {
+    bool lv0;
+    const int64_t it0 = item_of(blockIdx.x, lv0);
+    fetch(it0, lv0, cur);
+  }
+  bool lv1;
+  int64_t it1 = item_of((int64_t)blockIdx.x + gridDim.x, lv1);
   for (int64_t pr = blockIdx.x; pr < n_pairs_live; pr += gridDim.x) {
-    const int64_t li = 2 * pr + io;
-    const bool live = li < n_live;
-    const int64_t it = live ? g.items[li] : 0;
-    const int tile = (int)(it / a.B);
-    const int64_t b = it % a.B;
-    const int t = 16 * tile + j;
-    const int cnt = g.cnt[b];
-    const bool m = live && t <= L - 2 && a.mask[b * L + t + 1] != 0;
-    const float* e = set == 0 ? a.pos : a.neg;
-    float* de = set == 0 ? g.dpos : g.dneg;
+    RoundIn nxt;
+    fetch(it1, lv1, nxt);  // stage B of the next round
+    bool lv2;
+    const int64_t it2 = item_of(pr + 2 * (int64_t)gridDim.x, lv2);  // stage A of the one after
+    const bool live = cur.live;
+    const int64_t b = cur.b;
+    const int t = cur.t;
+    const bool m = cur.m;
     f4 dxh[kT1];
     if (live) {
-      // dL/d(loss sum of b) = daux_b / (2·cnt)  (0 rows → inf·0 = NaN, as the reference)
-      const float sb = g.daux[b] / ((float)cnt * 2.f);
-      float xv[In / 4];
-      load_x<H, E>(a, e, b, t, kq, xv);
+      const float sb = cur.sb;
+      const float (&xv)[In / 4] = cur.xv;
 #pragma unroll
       for (int k = 0; k < In / 4; ++k) T.x[j * kS1 + 4 * k + kq] = xv[k];
       for (int f = In + kq; f < kMaxIn; f += 4) T.x[j * kS1 + f] = f == In ? 1.f : 0.f;
@@ -384,7 +424,7 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
           const float* o = S.dxh[io] + j * kMaxH + f0;
           float* dst = g.dhidden + (b * L + t) * (int64_t)H + f0;
           const f4 v = dxh[x] + f4{o[0], o[1], o[2], o[3]};
-          store4(dst, g.acc_hidden ? *reinterpret_cast<const f4*>(dst) + v : v);
+          store4(dst, g.acc_hidden ? cur.dh[x] + v : v);  // dh: the upstream rows, prefetched
         }
       }
     }
@@ -432,6 +472,9 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
       }
     }
     __syncthreads();  // the set tiles are rewritten next round
+    cur = nxt;
+    it1 = it2;
+    lv1 = lv2;
   }
 
   // this block's partial gradients: [dW1 In×80 | db1 80 | dW2 80×40 | db2 40 | dW3 40 | db3 1]
