@@ -9,8 +9,10 @@ handles and the cross-stream order of the exchange run as they will at world 8.
     loss, slab and every MLP parameter, six steps — the fifth after a load_state_dict between its
     prefetch and its exchange (rows ahead invalidated: it re-sends its whole block).
 (b) PinSage's sync-free step (pinsage/train/train.py:40-48) with its flat-gradient all-reduce
-    captured into a HIP graph under RCCL and replayed equals the same graph without the
-    collective, bit for bit."""
+    captured into a HIP graph on the RCCL group and replayed equals the same graph without the
+    collective, bit for bit. At world 1 RCCL records no node for the all-reduce
+    (tools/probe_rccl_capture.py): this checks the capture path around it, not a captured
+    reduction."""
 import os
 
 import numpy as np
