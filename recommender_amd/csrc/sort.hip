@@ -784,23 +784,42 @@ __device__ __forceinline__ void seg_load0(const SegArgs& a, const SegSlot& sl, i
                                           uint32_t (&id)[kSegKPL], uint32_t& live,
                                           uint32_t& sent, bool& oob) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // Every load of the tile is issued before any is used: a load guarded per element (b < B,
+  // then the valid flag) made the compiler wait for each one in turn (round 6, gfx950 ISA: 16
+  // dependent round trips per thread). Positions past B read position 0 and are dropped below.
+  int64_t v[kSegKPL];
+  int64_t pp[kSegKPL];
+  uint32_t inb = 0u;
+#pragma unroll
+  for (int k = 0; k < kSegKPL; ++k) {
+    const int64_t b = (int64_t)t * kSegTile + wave * 64 * kSegKPL + k * 64 + lane;
+    const bool in = b < a.B;
+    inb |= (uint32_t)in << k;
+    pp[k] = in ? b * a.n_slots + s : 0;
+    v[k] = ID64 ? static_cast<const int64_t*>(a.ids)[pp[k]]
+                : static_cast<int64_t>(static_cast<const int32_t*>(a.ids)[pp[k]]);
+  }
+  uint32_t excl = 0u;
+  if (a.valid) {  // uniform: the flags' loads issued together too
+    uint8_t f[kSegKPL];
+#pragma unroll
+    for (int k = 0; k < kSegKPL; ++k) f[k] = a.valid[pp[k]];
+#pragma unroll
+    for (int k = 0; k < kSegKPL; ++k) excl |= (uint32_t)(f[k] == 0) << k;
+  }
   live = 0u;
   sent = 0u;
 #pragma unroll
   for (int k = 0; k < kSegKPL; ++k) {
-    const int64_t b = (int64_t)t * kSegTile + wave * 64 * kSegKPL + k * 64 + lane;
     id[k] = 0u;
-    if (b < a.B) {
-      const int64_t p = b * a.n_slots + s;
-      const int64_t v = ID64 ? static_cast<const int64_t*>(a.ids)[p]
-                             : static_cast<int64_t>(static_cast<const int32_t*>(a.ids)[p]);
-      if (a.valid && !a.valid[p]) {
+    if ((inb >> k) & 1u) {
+      if ((excl >> k) & 1u) {
         sent |= 1u << k;
-      } else if (v < 0 || v >= sl.rows) {
+      } else if (v[k] < 0 || v[k] >= sl.rows) {
         sent |= 1u << k;
         oob = true;
       } else {
-        id[k] = static_cast<uint32_t>(v);
+        id[k] = static_cast<uint32_t>(v[k]);
         live |= 1u << k;
       }
     }
@@ -859,19 +878,39 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_hist0_kernel(SegArgs a)
 // slot starts: vstart[s] = valid ids of slots < s, sstart[s] = sentinels of slots < s (index
 // n_slots: the totals), from the pass-0 tile counts (n_slots x tiles ints, L2 / MALL): every count
 // loaded by its own lane in one round trip, summed per slot in LDS, the slot prefix by one wave
-__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstart, int32_t* sstart) {
+__device__ __forceinline__ void seg_slot_starts(const SegArgs& a, int32_t* vstart, int32_t* sstart,
+                                                int s, int t, int32_t* spre) {
   if (threadIdx.x <= a.n_slots) {
     vstart[threadIdx.x] = 0;
     sstart[threadIdx.x] = 0;
   }
+  if (threadIdx.x == 0) *spre = 0;
   __syncthreads();
+  // every count's load issued before any is summed (at most kSegMaxSlots x kSegMaxTiles counts:
+  // 8 per thread); the sentinels of slot s in tiles before t (this block's sentinel base) summed
+  // on the way, instead of a serial loop of dependent loads
+  constexpr int kPer = kSegMaxSlots * kSegMaxTiles / kSegThreads;
   const int total = a.n_slots * a.tiles;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int sl = e / a.tiles;
-    const int32_t v = a.vcnt[e], z = a.scnt[e];
-    if (v) atomicAdd(&vstart[sl], v);
-    if (z) atomicAdd(&sstart[sl], z);
+  int32_t cv[kPer], cz[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = threadIdx.x + i * kSegThreads;
+    const int ec = e < total ? e : 0;
+    cv[i] = a.vcnt[ec];
+    cz[i] = a.scnt[ec];
   }
+  int32_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = threadIdx.x + i * kSegThreads;
+    if (e < total) {
+      const int sl = e / a.tiles;
+      if (cv[i]) atomicAdd(&vstart[sl], cv[i]);
+      if (cz[i]) atomicAdd(&sstart[sl], cz[i]);
+      if (sl == s && e - sl * a.tiles < t) mine += cz[i];
+    }
+  }
+  if (mine) atomicAdd(spre, mine);
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over the slots (n_slots <= 64), totals at n_slots
     const int lane = threadIdx.x;
@@ -948,15 +987,31 @@ __device__ __forceinline__ void seg_offsets_inblock(const uint16_t* __restrict__
 #pragma unroll
   for (int i = 0; i < PER; ++i) tot[i] = pre[i] = 0;
   if (d0 < bins) {  // bins >= 16 or a single thread (bins < 16: the first thread alone)
-    for (int u = 0; u < n_tiles; ++u) {
-      const uint4* row = reinterpret_cast<const uint4*>(hist + (int64_t)u * kSegBins + d0);
-      const uint4 q0 = row[0], q1 = row[1];
-      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    // eight tiles' rows in flight at a time (one row per loop trip waited for each load in turn:
+    // 16 dependent L2 round trips at the north star's 16 tiles per slot)
+    constexpr int kBatch = 8;
+    for (int u0 = 0; u0 < n_tiles; u0 += kBatch) {
+      uint4 q[kBatch][2];
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int32_t c = d0 + i < bins ? (int32_t)((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) : 0;
-        tot[i] += c;
-        if (u < t) pre[i] += c;
+      for (int j = 0; j < kBatch; ++j) {
+        const int u = u0 + j < n_tiles ? u0 + j : 0;
+        const uint4* row = reinterpret_cast<const uint4*>(hist + (int64_t)u * kSegBins + d0);
+        q[j][0] = row[0];
+        q[j][1] = row[1];
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int u = u0 + j;
+        if (u < n_tiles) {
+          const uint32_t w[8] = {q[j][0].x, q[j][0].y, q[j][0].z, q[j][0].w,
+                                 q[j][1].x, q[j][1].y, q[j][1].z, q[j][1].w};
+#pragma unroll
+          for (int i = 0; i < PER; ++i) {
+            const int32_t c = d0 + i < bins ? (int32_t)((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) : 0;
+            tot[i] += c;
+            if (u < t) pre[i] += c;
+          }
+        }
       }
     }
   }
@@ -1000,10 +1055,13 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
     const int tn = (int)(a.B - b0 < kSegTile ? a.B - b0 : kSegTile);
     const int w0 = (threadIdx.x >> 6) * 64 * kSegKPL + (threadIdx.x & 63);
     const uint32_t* kt = a.keys0 + ((int64_t)s * a.tiles + t) * kSegTile + w0;
+    uint32_t raw[kSegKPL];  // the whole tile is allocated (and written by hist0): load it all first
+#pragma unroll
+    for (int k = 0; k < kSegKPL; ++k) raw[k] = kt[k * 64];
 #pragma unroll
     for (int k = 0; k < kSegKPL; ++k) {
       const bool in = w0 + k * 64 < tn;
-      const uint32_t v = in ? kt[k * 64] : 0u;
+      const uint32_t v = in ? raw[k] : 0u;
       id[k] = v & 0x7FFFFFFFu;
       if (in && (v >> 31)) sent |= 1u << k;
       else if (in) live |= 1u << k;
@@ -1011,15 +1069,14 @@ __global__ __launch_bounds__(kSegThreads) void slot_sort_scatter0_kernel(SegArgs
   }
   // slot starts (valid / sentinel ids of the slots before s) from the pass-0 tile counts, this
   // slot's sentinels in tiles before t, then the digit offsets — all in the block (round 6)
-  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1], wsc[4];
-  seg_slot_starts(a, vstart, sstart);
+  __shared__ int32_t vstart[kSegMaxSlots + 1], sstart[kSegMaxSlots + 1], wsc[4], spre_sh;
+  seg_slot_starts(a, vstart, sstart, s, t, &spre_sh);
   if (s == 0 && t == 0)  // for pass 1 (later launches)
     for (int q = threadIdx.x; q <= a.n_slots; q += blockDim.x) {
       a.starts[q] = vstart[q];
       a.starts[kSegMaxSlots + 1 + q] = sstart[q];
     }
-  int32_t spre = 0;
-  for (int u = 0; u < t; ++u) spre += a.scnt[s * a.tiles + u];
+  const int32_t spre = spre_sh;
   seg_offsets_inblock(a.hist0 + (int64_t)s * a.tiles * kSegBins, a.tiles, t, bins, vstart[s], doff,
                       wsc);
   const int32_t n_valid = vstart[a.n_slots];
