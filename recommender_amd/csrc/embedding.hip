@@ -452,27 +452,35 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
   // a row of this walk: below n_rows and at or past a.key_lo (one unsigned compare)
   const uint32_t klo = a.key_lo, kspan = n_rows - a.key_lo;
   auto key_ok = [&](uint32_t k) { return k - klo < kspan; };
-  const uint32_t kv = mine ? keys[k0 + gl] : 0xFFFFFFFFu;
-  const int32_t pv = mine ? pos[k0 + gl] : 0;
+  // Round 6: every load below is issued unguarded from an address that is always valid (the
+  // guarded forms made the compiler branch around each load and wait for all of them at every
+  // join — gfx950 ISA: the two gradient batches and the queued table rows were each drained
+  // with vmcnt(0), so the next batch never flew under the current one). The tile's keys and
+  // positions and its two neighbour keys go out in one round trip.
+  const int64_t ki = k0 + (mine ? gl : 0);
+  const uint32_t kraw = keys[ki];
+  const int32_t praw = pos[ki];
+  const uint32_t kbraw = keys[k0 > 0 ? k0 - 1 : 0];
+  const uint32_t karaw = keys[k1 < n ? k1 : n - 1];
+  const uint32_t kv = mine ? kraw : 0xFFFFFFFFu;
+  const int32_t pv = mine ? praw : 0;
   const bool lv = mine && key_ok(kv);
-  const float sv = (a.row_scale && lv) ? a.row_scale[pv / a.scale_group] : 1.f;
-  const uint32_t key_before = k0 > 0 ? keys[k0 - 1] : 0xFFFFFFFFu;
-  const uint32_t key_after = k1 < n ? keys[k1] : 0xFFFFFFFEu;
+  const uint32_t key_before = k0 > 0 ? kbraw : 0xFFFFFFFFu;
+  const uint32_t key_after = k1 < n ? karaw : 0xFFFFFFFEu;
+  float sv = 1.f;
+  if (a.row_scale) sv = a.row_scale[(lv ? pv : 0) / a.scale_group];  // used at lv lanes only
   auto key_of = [&](int u) { return (uint32_t)__shfl((int)kv, u, 32); };
   // the row scale multiplies at the sum (consume), not here: a multiply right behind each load
-  // would wait for it and serialise the batch's loads (measured: apply 215 -> 272 us alone)
+  // would wait for it and serialise the batch's loads (measured: apply 215 -> 272 us alone).
+  // An entry that is not a row of this walk (past the tile, out of range) reads gradient row 0
+  // instead: its run is never emitted (emit drops rows that fail key_ok; consume stops at ne).
   auto load_batch = [&](int b0, float (&r)[U][VEC]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = b0 + u;
       const int32_t p = __shfl(pv, e, 32);
       const bool live = e < ne && key_ok(key_of(e));
-      if (live) {
-        load_stream<VEC>(grad + (int64_t)p * dim + col, r[u]);
-      } else {
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) r[u][c] = 0.f;
-      }
+      load_stream<VEC>(grad + (live ? (int64_t)p * dim : 0) + col, r[u]);
     }
   };
   uint32_t run_row = key_of(0);
@@ -488,8 +496,10 @@ __device__ __forceinline__ Tile32Edges tile32_walk(const uint32_t* __restrict__ 
     if constexpr (kQueue) {
       float tr[QN][VEC];
 #pragma unroll
-      for (int i = 0; i < QN; ++i)
-        if (i < qn) RowIO<VEC>::load(a.table + (int64_t)qrow[i] * dim + col, tr[i]);
+      for (int i = 0; i < QN; ++i) {  // unguarded (a free slot re-reads row qrow[0] or row 0)
+        const uint32_t rr = i < qn ? qrow[i] : (qn > 0 ? qrow[0] : 0u);
+        RowIO<VEC>::load(a.table + (int64_t)rr * dim + col, tr[i]);
+      }
 #pragma unroll
       for (int i = 0; i < QN; ++i) {
         if (i < qn) {
