@@ -326,6 +326,8 @@ __device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
   uint32_t run_row = keys[k0];
   int64_t run_start = k0;
   bool run_starts = (k0 == 0) || keys[k0 - 1] != run_row;
+  // an always-valid gradient address for entries that carry no gradient (loaded, never used)
+  const float* grad0 = (OPT == OPT_DENSE && a.n_gseg > 0) ? a.gseg[0] : grad;
   float acc[CPL][VEC];
 #pragma unroll
   for (int c = 0; c < CPL; ++c)
@@ -350,28 +352,39 @@ __device__ __forceinline__ void seg_tile_one(const uint32_t* __restrict__ keys,
     float r[U][CPL][VEC];
     float sc[U];  // applied at the sum: a multiply right behind each load would serialise them
     uint32_t kk[U];
+    // Round 6: unguarded loads from always-valid addresses (guarded, the compiler waited for
+    // each batch entry's loads in turn). An entry past the tile reads entry k0 (never consumed);
+    // an OOB key's rows are read from row 0 (its run is never emitted); lanes past dim read
+    // column 0 (never stored).
+    uint32_t kr[U];
+    int32_t pr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      int64_t k = kb + u;
-      bool valid = k < k1;
-      kk[u] = valid ? keys[k] : 0xFFFFFFFFu;
-      int64_t p = valid ? pos[k] : 0;
-      bool live = valid && kk[u] < n_rows;
-      sc[u] = (a.row_scale && live) ? a.row_scale[p / a.scale_group] : 1.f;
+      const int64_t k = kb + u < k1 ? kb + u : k0;
+      kr[u] = keys[k];
+      pr[u] = pos[k];
+    }
+    const float* rsp = a.row_scale ? a.row_scale : grad0;
+    float sr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool valid = kb + u < k1;
+      kk[u] = valid ? kr[u] : 0xFFFFFFFFu;
+      const int64_t p = valid ? pr[u] : 0;
+      const bool live = valid && kk[u] < n_rows;
+      sr[u] = rsp[a.row_scale && live ? p / a.scale_group : 0];
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         int col = (gl + c * lpr) * VEC;
-        if (live && col < dim) {
-          if constexpr (OPT == OPT_DENSE)
-            load_stream<VEC>(dense_grad_row(a, grad, p, dim) + col, r[u][c]);
-          else
-            load_stream<VEC>(grad + p * dim + col, r[u][c]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) r[u][c][e] = 0.f;
-        }
+        const bool ok = live && col < dim;
+        if constexpr (OPT == OPT_DENSE)
+          load_stream<VEC>(ok ? dense_grad_row(a, grad, p, dim) + col : grad0, r[u][c]);
+        else
+          load_stream<VEC>(ok ? grad + p * dim + col : grad0, r[u][c]);
       }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) sc[u] = a.row_scale ? sr[u] : 1.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       int64_t k = kb + u;

@@ -997,17 +997,30 @@ __global__ __launch_bounds__(256, 2) void dlrm_train_chunk(GatherSrc src, int64_
   char* img = reinterpret_cast<char*>(lds[wave]);
   float* stg = lds[wave] + kChImage / 4;          // the chunk's U columns, row-major
   float* ubot = stg + 32 * kChStageLd;
-  for (int e = threadIdx.x; e < kTrainAtop; e += 256) qsh[e] = e < nzc + D ? ta.q[e] : 0.f;
+  // The prologue's loads are unguarded (index 0 where a weight does not exist, zeroed after):
+  // guarded, the compiler waited for each of wave 0's twelve q loads in turn before the block
+  // barrier every wave waits at (round 6, gfx950 ISA)
+  for (int e = threadIdx.x; e < kTrainAtop; e += 256) {
+    const float v = ta.q[e < nzc + D ? e : 0];
+    qsh[e] = e < nzc + D ? v : 0.f;
+  }
   if (wave == 0) {
+    float qv[12];
+    bool qk[12];
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int i0 = 4 * g + reg, j0 = r;
       const int i1 = 4 * g + reg, j1 = 16 + r;
       const int i2 = 16 + 4 * g + reg, j2 = 16 + r;
-      qlane[lane][reg] = (i0 < j0 && j0 < F) ? ta.q[compact_index(i0, j0, F, 0)] : 0.f;
-      qlane[lane][4 + reg] = (j1 < F) ? ta.q[compact_index(i1, j1, F, 0)] : 0.f;
-      qlane[lane][8 + reg] = (i2 < j2 && j2 < F) ? ta.q[compact_index(i2, j2, F, 0)] : 0.f;
+      qk[reg] = i0 < j0 && j0 < F;
+      qk[4 + reg] = j1 < F;
+      qk[8 + reg] = i2 < j2 && j2 < F;
+      qv[reg] = ta.q[qk[reg] ? compact_index(i0, j0, F, 0) : 0];
+      qv[4 + reg] = ta.q[qk[4 + reg] ? compact_index(i1, j1, F, 0) : 0];
+      qv[8 + reg] = ta.q[qk[8 + reg] ? compact_index(i2, j2, F, 0) : 0];
     }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) qlane[lane][k] = qk[k] ? qv[k] : 0.f;
   }
   // S = M + Mᵀ as the B operand of Uᵀ = Xᵀ·S: lane (r, g) holds S[8g + j][16 ib + r], which by
   // symmetry is S[16 ib + r][8g + j]
