@@ -686,24 +686,45 @@ __global__ __launch_bounds__(256) void affine_narrow_fwd_kernel(
   const int nq = n >> 2;  // float4 columns (<= 64)
   const int rpb = 256 / nq;  // rows in flight per pass
   const int t = threadIdx.x % nq, rl = threadIdx.x / nq;
-  // this lane's column of Q̃ = [Q; c] in registers (the loop below is unrolled over N0MAX)
+  // this lane's column of Q̃ = [Q; c] in registers (the loop below is unrolled over N0MAX).
+  // Round 6: the first tile's x rows, then Q̃'s column, are loaded unguarded and together, so a
+  // block waits one round trip for both (guarded per element, the staging loop waited for each
+  // of its passes and for the column before it); the next tile's rows are loaded while this one
+  // is computed
+  constexpr int kPer = kNarrowRows * N0MAX / 256;
+  const int64_t stride = (int64_t)gridDim.x * kNarrowRows;
+  int64_t r0 = (int64_t)blockIdx.x * kNarrowRows;
+  float xv[kPer];
+  auto load_x = [&](int64_t rb) {
+    const int nrb = B - rb < kNarrowRows ? (int)(B - rb) : kNarrowRows;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = threadIdx.x + i * 256;
+      const int rr = e / n0, k = e - rr * n0;
+      xv[i] = x[e < nrb * n0 ? (rb + rr) * ldx + k : rb * ldx];
+    }
+  };
+  if (r0 < B) load_x(r0);
   float4 qr[N0MAX + 1];
 #pragma unroll
   for (int k = 0; k <= N0MAX; ++k)
-    qr[k] = k <= n0 ? reinterpret_cast<const float4*>(Qa)[k * nq + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    qr[k] = reinterpret_cast<const float4*>(Qa)[(k <= n0 ? k : 0) * nq + t];
   float4 cc = qr[0];
 #pragma unroll
-  for (int k = 1; k <= N0MAX; ++k)
+  for (int k = 0; k <= N0MAX; ++k) {
     if (k == n0) cc = qr[k];
-  for (int64_t r0 = (int64_t)blockIdx.x * kNarrowRows; r0 < B;
-       r0 += (int64_t)gridDim.x * kNarrowRows) {
+    if (k >= n0) qr[k] = make_float4(0.f, 0.f, 0.f, 0.f);  // (the rows loop stops at n0 anyway)
+  }
+  for (; r0 < B; r0 += stride) {
     const int nr = B - r0 < kNarrowRows ? (int)(B - r0) : kNarrowRows;
     __syncthreads();  // previous tile consumed
-    for (int e = threadIdx.x; e < nr * n0; e += 256) {
-      const int rr = e / n0, k = e - rr * n0;
-      xs[rr * n0 + k] = x[(r0 + rr) * ldx + k];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < nr * n0) xs[e] = xv[i];
     }
     __syncthreads();
+    if (r0 + stride < B) load_x(r0 + stride);
     if (rl >= rpb) continue;
     for (int rr = rl; rr < nr; rr += rpb) {
       const float* xr = xs + rr * n0;
@@ -711,11 +732,11 @@ __global__ __launch_bounds__(256) void affine_narrow_fwd_kernel(
 #pragma unroll
       for (int k = 0; k < N0MAX; ++k) {
         if (k < n0) {
-          const float xv = xr[k];
-          acc.x += xv * qr[k].x;
-          acc.y += xv * qr[k].y;
-          acc.z += xv * qr[k].z;
-          acc.w += xv * qr[k].w;
+          const float xk = xr[k];
+          acc.x += xk * qr[k].x;
+          acc.y += xk * qr[k].y;
+          acc.z += xk * qr[k].z;
+          acc.w += xk * qr[k].w;
         }
       }
       float4 o;
@@ -780,22 +801,33 @@ __device__ __forceinline__ void outer_sum_body(const float* __restrict__ R, int 
   if (e >= (int64_t)na * nbq) return;
   const int a = (int)(e / nbq), bq = (int)(e - (int64_t)a * nbq);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int r = 0; r <= m; ++r) {
-    float rv;
-    if (r < m) rv = R[(int64_t)r * ldr + a];
-    else if (rlast) rv = rlast[a];
-    else break;
-    float4 pv;
-    if constexpr (P4) {
-      pv = reinterpret_cast<const float4*>(P)[(int64_t)r * nbq + bq];
-    } else {
-      const float* pp = P + ((int64_t)r * nbq + bq) * 4;
-      pv = make_float4(pp[0], pp[1], pp[2], pp[3]);
+  // rows loaded 8 at a time, unguarded (a row past the last reads row 0 and is not added):
+  // one row per trip with the rlast / break branches waited for each load in turn (round 6)
+  const int rows = rlast ? m + 1 : m;
+  constexpr int kB = 8;
+  for (int r0 = 0; r0 < rows; r0 += kB) {
+    float rv[kB];
+    float4 pv[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int r = r0 + j < rows ? r0 + j : 0;
+      rv[j] = (r < m || !rlast) ? R[(int64_t)r * ldr + a] : rlast[a];
+      if constexpr (P4) {
+        pv[j] = reinterpret_cast<const float4*>(P)[(int64_t)r * nbq + bq];
+      } else {
+        const float* pp = P + ((int64_t)r * nbq + bq) * 4;
+        pv[j] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+      }
     }
-    acc.x += rv * pv.x;
-    acc.y += rv * pv.y;
-    acc.z += rv * pv.z;
-    acc.w += rv * pv.w;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (r0 + j < rows) {
+        acc.x += rv[j] * pv[j].x;
+        acc.y += rv[j] * pv[j].y;
+        acc.z += rv[j] * pv[j].z;
+        acc.w += rv[j] * pv[j].w;
+      }
+    }
   }
   reinterpret_cast<float4*>(out)[e] = acc;
 }
