@@ -381,6 +381,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 __device__ __forceinline__ void rowdot_wave(const float* M, int ld, int i_row, int n,
                                             const float* v, float* out_i, int lane) {
   float acc = 0.f;
+#pragma unroll 4  // (four trips' loads in flight: one trip waited for its loads before the next)
   for (int k = lane; k < n; k += 64) acc += M[(int64_t)i_row * ld + k] * v[k];
   acc = wave_sum(acc);
   if (lane == 0) *out_i = acc;
@@ -597,9 +598,23 @@ __device__ __forceinline__ void aug_product_body(
     float* __restrict__ out, int bx) {
   extern __shared__ float ms[];  // max((m + 1)·k, 8·MR·64) floats (aug_lds_bytes)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) {
-    const int i = e / k, kk = e - i * k;
-    ms[e] = i < m ? M[(int64_t)i * ldm + kk] : (cin ? cin[kk] : 0.f);
+  {  // staged 8 passes' loads at a time, unguarded (guarded, each pass waited for its load)
+    constexpr int kSB = 8, kT = kC3Waves * 64;
+    const int tot = (m + 1) * k;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += kSB * kT) {
+      float v[kSB];
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) {
+        const int e = e0 + j * kT < tot ? e0 + j * kT : e0;
+        const int i = e / k, kk = e - i * k;
+        v[j] = *(i < m ? M + (int64_t)i * ldm + kk : (cin ? cin + kk : M));
+      }
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) {
+        const int e = e0 + j * kT;
+        if (e < tot) ms[e] = (e / k < m || cin) ? v[j] : 0.f;
+      }
+    }
   }
   __syncthreads();
   const int c = bx * 64 + lane;
@@ -760,7 +775,18 @@ __device__ __forceinline__ void rt_product_body(const float* __restrict__ P, int
                                                 float* __restrict__ out, int bx) {
   extern __shared__ float ps[];  // (m + 1)·k floats
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int e = threadIdx.x; e < (m + 1) * k; e += kC3Waves * 64) ps[e] = P[e];
+  {  // staged 8 passes' loads at a time (one pass per trip waited for its load)
+    constexpr int kSB = 8, kT = kC3Waves * 64;
+    const int tot = (m + 1) * k;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += kSB * kT) {
+      float v[kSB];
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) v[j] = P[e0 + j * kT < tot ? e0 + j * kT : e0];
+#pragma unroll
+      for (int j = 0; j < kSB; ++j)
+        if (e0 + j * kT < tot) ps[e0 + j * kT] = v[j];
+    }
+  }
   __syncthreads();
   const int c = bx * kC3Waves + w;
   if (c >= n) return;
