@@ -70,6 +70,15 @@ int32_t rs_device_count(void);
 /* STREAM-style device copy (16-byte accesses): the measured HBM-bandwidth reference of the
  * bench's roofline; bytes a multiple of 16, both buffers 16-byte aligned. */
 int32_t rs_stream_copy(const void* src, void* dst, size_t bytes, void* stream);
+/* Device-scope stream ordering (no reference counterpart: engine plumbing between its own
+ * streams). An event created with hipEventDisableSystemFence: its record is a device-scope
+ * release, so one stream can wait for another without the system-scope cache write-back a
+ * default event's record performs. Same-device ordering only. rs_event_create returns NULL on
+ * failure (rs_last_error says why). */
+void* rs_event_create(void);
+int32_t rs_event_destroy(void* ev);
+int32_t rs_event_record(void* ev, void* stream);
+int32_t rs_stream_wait_event(void* stream, void* ev);
 
 /* ------------------------------------------------------------------------------------
  * a-1  Embedding forward (multi-slot gather).

@@ -56,6 +56,10 @@ _SIGS = {
     "rs_version": (_i32, []),
     "rs_device_count": (_i32, []),
     "rs_stream_copy": (_i32, [_p, _p, _sz, _p]),
+    "rs_event_create": (_p, []),
+    "rs_event_destroy": (_i32, [_p]),
+    "rs_event_record": (_i32, [_p, _p]),
+    "rs_stream_wait_event": (_i32, [_p, _p]),
     "rs_embedding_fwd": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p, _p]),
     "rs_embedding_fwd_strided": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _i64, _p, _p]),
     "rs_sort_ids_workspace_size": (_sz, [_i64]),
@@ -375,6 +379,71 @@ def ptr(t: torch.Tensor | None):
 
 def stream_ptr(device=None):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+# Stream ordering with device-scope events (rs_event_*): on by default, RS_DEVICE_EVENTS=0 uses
+# torch's default events (a system-scope release at every record) everywhere.
+DEVICE_EVENTS = os.environ.get("RS_DEVICE_EVENTS", "1") == "1"
+
+
+class DeviceEvent:
+    """A HIP event whose record is a device-scope release (rs_event_create): it orders the
+    engine's own streams of one device without the system-scope cache write-back of a default
+    event. Never used for host synchronisation, other devices or other processes. Re-recording
+    is allowed once the waits on the previous record are enqueued (a wait binds the record that
+    precedes it; on an in-order stream a later record only orders more work)."""
+    __slots__ = ("h",)
+
+    def __init__(self):
+        h = lib().rs_event_create()
+        if not h:
+            raise RecsysError(f"rs_event_create: {lib().rs_last_error().decode()}")
+        self.h = h
+
+    def record(self, stream):
+        call("rs_event_record", C.c_void_p(self.h), C.c_void_p(stream.cuda_stream))
+
+    def wait_by(self, stream):
+        call("rs_stream_wait_event", C.c_void_p(stream.cuda_stream), C.c_void_p(self.h))
+
+    def __del__(self):
+        try:
+            lib().rs_event_destroy(C.c_void_p(self.h))
+        except Exception:  # interpreter teardown
+            pass
+
+
+def stream_wait_event(stream, ev):
+    """`stream` waits for the record of `ev` (a DeviceEvent or a torch.cuda.Event)."""
+    if isinstance(ev, DeviceEvent):
+        ev.wait_by(stream)
+    else:
+        stream.wait_event(ev)
+
+
+def record_event(stream, ev=None):
+    """An event recorded on `stream` now: a DeviceEvent (reused when given) unless device events
+    are off or a graph is being captured, else a torch event."""
+    if not DEVICE_EVENTS or torch.cuda.is_current_stream_capturing():
+        e = torch.cuda.Event()
+        e.record(stream)
+        return e
+    e = ev if isinstance(ev, DeviceEvent) else DeviceEvent()
+    e.record(stream)
+    return e
+
+
+def stream_wait_stream(waiter, src, ev=None):
+    """`waiter` waits for everything queued on `src` so far (torch's wait_stream, device-scope
+    unless device events are off or a graph is being captured); ev: a DeviceEvent to reuse."""
+    if waiter == src:
+        return
+    if not DEVICE_EVENTS or torch.cuda.is_current_stream_capturing():
+        waiter.wait_stream(src)
+        return
+    e = ev if ev is not None else DeviceEvent()
+    e.record(src)
+    e.wait_by(waiter)
 
 
 def id_dtype_code(t: torch.Tensor) -> int:

@@ -52,3 +52,43 @@ extern "C" int32_t rs_stream_copy(const void* src, void* dst, size_t bytes, void
   RS_CHECK_LAUNCH();
   return RS_OK;
 }
+
+// Device-scope stream ordering (round 6). A default HIP event's record performs a system-scope
+// release (cache write-back / invalidate for host visibility); ordering two streams of ONE device
+// needs only a device-scope one. These events are created with hipEventDisableSystemFence and are
+// used only to order the engine's own streams (never for host synchronisation or across devices
+// or processes).
+extern "C" void* rs_event_create(void) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+    rs::set_error("hipEventCreateWithFlags failed");
+    return nullptr;
+  }
+  return e;
+}
+
+extern "C" int32_t rs_event_destroy(void* ev) {
+  if (ev && hipEventDestroy(static_cast<hipEvent_t>(ev)) != hipSuccess) {
+    rs::set_error("hipEventDestroy failed");
+    return RS_E_HIP;
+  }
+  return RS_OK;
+}
+
+extern "C" int32_t rs_event_record(void* ev, void* stream) {
+  RS_CHECK_ARG(ev, "null event");
+  if (hipEventRecord(static_cast<hipEvent_t>(ev), rs::as_stream(stream)) != hipSuccess) {
+    rs::set_error("hipEventRecord failed");
+    return RS_E_HIP;
+  }
+  return RS_OK;
+}
+
+extern "C" int32_t rs_stream_wait_event(void* stream, void* ev) {
+  RS_CHECK_ARG(ev, "null event");
+  if (hipStreamWaitEvent(rs::as_stream(stream), static_cast<hipEvent_t>(ev), 0) != hipSuccess) {
+    rs::set_error("hipStreamWaitEvent failed");
+    return RS_E_HIP;
+  }
+  return RS_OK;
+}

@@ -75,7 +75,7 @@ class Embedding(nn.Module):
     def wait_update_raw(self):
         ev, self._pending_update = self._pending_update, None
         if ev is not None:
-            torch.cuda.current_stream(self.weight.device).wait_event(ev)
+            L.stream_wait_event(torch.cuda.current_stream(self.weight.device), ev)
 
     @property
     def n_slots(self) -> int:
@@ -154,7 +154,7 @@ class Embedding(nn.Module):
                 # replay the step's rows' skipped decay on the stream the sort ran on
                 on_sort = getattr(ahead, "ready", None) is not None
                 if on_sort:
-                    opt.sort_stream.wait_event(ahead.ready)
+                    L.stream_wait_event(opt.sort_stream, ahead.ready)
                 opt.catch_up(self, ahead, opt.sort_stream if on_sort else opt.side)
 
     def take_presorted(self, ids: torch.Tensor):

@@ -455,7 +455,7 @@ def dlrm_fused_train_forward(model, cat_features, int_features, label, reduction
         ahead = emb._presorted[1] if getattr(emb, "_presorted", None) else None
         ready = getattr(ahead, "ready", None)
         if ready is not None and _TRAIN_WAITS_SORT:
-            torch.cuda.current_stream(dev).wait_event(ready)
+            L.stream_wait_event(torch.cuda.current_stream(dev), ready)
         kid, offs, n_rows = ids, emb.slot_offsets, w.shape[0]
     y = torch.empty(B, device=dev, dtype=torch.float32)
     grad = torch.empty(B * S, D, device=dev, dtype=torch.float32)

@@ -157,6 +157,7 @@ class SparseOptimizer:
         self.side = None
         self._applied = set()
         self.sort_stream, self.sort_ws = None, None
+        self._dev_events, self._ready_i = {}, 0
         # the step's presort runs on the sort stream (ordered after the current stream only), so
         # it overlaps the previous step's update instead of queueing behind it on the side
         # stream (north star with the early apply: 0.862 -> 0.841 ms/step; RS_PRESORT_STREAM=0
@@ -172,6 +173,16 @@ class SparseOptimizer:
                 t.fused_optimizer = self
                 # sorts another optimizer prefetched belong to its streams and scratch
                 t._prefetched, t._prefetch_queue, t._presorted = {}, [], None
+
+    def _dev_event(self, name):
+        """A persistent device-scope event of this optimizer's stream plumbing (None when device
+        events are off: the callers then use torch events)."""
+        if not L.DEVICE_EVENTS:
+            return None
+        e = self._dev_events.get(name)
+        if e is None:
+            e = self._dev_events[name] = L.DeviceEvent()
+        return e
 
     # ---- fused path ----
     def sort_async(self, table: Embedding, ids: torch.Tensor) -> SortedIds:
@@ -190,11 +201,13 @@ class SparseOptimizer:
             self.sort_stream = torch.cuda.Stream(device=dev)
             self.sort_ws = _Workspace()
         ss = self.sort_stream
-        ss.wait_stream(torch.cuda.current_stream(dev))
+        L.stream_wait_stream(ss, torch.cuda.current_stream(dev), self._dev_event("sort_in"))
         with torch.cuda.stream(ss):
             s = SortedIds.for_table(table, ids, self.sort_ws, count_unique=False)
-            s.ready = torch.cuda.Event()
-            s.ready.record(ss)
+            # a ring of device events: a sort's ready event is waited for within a few steps,
+            # and waiting on a later record of this in-order stream only orders more work
+            self._ready_i = (self._ready_i + 1) % 4
+            s.ready = L.record_event(ss, self._dev_event(f"ready{self._ready_i}"))
         ids.record_stream(ss)
         return s
 
@@ -208,10 +221,10 @@ class SparseOptimizer:
 
     def _launch_apply(self, table, ids, grad_rows, sorted_ids, row_scale=None):
         main = torch.cuda.current_stream(grad_rows.device)
-        self.side.wait_stream(main)
+        L.stream_wait_stream(self.side, main, self._dev_event("apply_in"))
         ready = getattr(sorted_ids, "ready", None)
         if ready is not None:  # sorted ahead on the sort stream (Embedding.prefetch)
-            self.side.wait_event(ready)
+            L.stream_wait_event(self.side, ready)
             sorted_ids.rows.record_stream(self.side)
             sorted_ids.pos.record_stream(self.side)
         with torch.cuda.stream(self.side):
@@ -261,8 +274,7 @@ class SparseOptimizer:
         applied = set()
         if self.fused:
             if self.defer_join:
-                ev = torch.cuda.Event()
-                ev.record(self.side)
+                ev = L.record_event(self.side, self._dev_event("join"))
                 for t in self.tables:
                     t._pending_update = ev
             else:

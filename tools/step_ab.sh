@@ -25,6 +25,7 @@ for rep in ${REPS:-1 2}; do
       prefetch) run prefetch X=1 -- --prefetch 1 || exit 1 ;;
       waitsort) run waitsort RS_TRAIN_WAITS_SORT=1 -- || exit 1 ;;
       mainprio) run mainprio X=1 -- --prio 1 || exit 1 ;;
+      sysev) run sysev RS_DEVICE_EVENTS=0 -- || exit 1 ;;
     esac
   done
 done
