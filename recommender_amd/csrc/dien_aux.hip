@@ -98,17 +98,32 @@ __device__ __forceinline__ int aux_count(const AuxArgs& a, int64_t b, int lane) 
 }
 
 // B operands of layer 1 for the tile's row j = lane & 15 (history step t): feature 4s + kq of
-// x = [h_t, e_{t+1}]; zero for rows past L-2 and for padding features.
+// x = [h_t, e_{t+1}]; zero for rows past L-2 and for padding features. load_x_raw issues the
+// loads unguarded (a row past L-2 reads step 0's, always in bounds) and zero_x applies the row
+// mask where the values are used: guarded per element, the compiler waited for each load in turn
+// (round 6, gfx950 ISA), and the backward's one-round-ahead fetch was drained at once.
 template <int H, int E>
-__device__ __forceinline__ void load_x(const AuxArgs& a, const float* e, int64_t b, int t,
-                                       int kq, float (&xv)[(H + E) / 4]) {
+__device__ __forceinline__ void load_x_raw(const AuxArgs& a, const float* e, int64_t b, int t,
+                                           int kq, float (&xv)[(H + E) / 4]) {
   const bool ok = t <= a.L - 2;
   const float* hr = a.hidden + (b * a.L + (ok ? t : 0)) * (int64_t)H + kq;
   const float* er = e + (b * a.L + (ok ? t + 1 : 0)) * (int64_t)E + kq;
 #pragma unroll
-  for (int s = 0; s < H / 4; ++s) xv[s] = ok ? hr[4 * s] : 0.f;
+  for (int s = 0; s < H / 4; ++s) xv[s] = hr[4 * s];
 #pragma unroll
-  for (int s = 0; s < E / 4; ++s) xv[H / 4 + s] = ok ? er[4 * s] : 0.f;
+  for (int s = 0; s < E / 4; ++s) xv[H / 4 + s] = er[4 * s];
+}
+template <int H, int E>
+__device__ __forceinline__ void zero_x(const AuxArgs& a, int t, float (&xv)[(H + E) / 4]) {
+  const bool ok = t <= a.L - 2;
+#pragma unroll
+  for (int s = 0; s < (H + E) / 4; ++s) xv[s] = ok ? xv[s] : 0.f;
+}
+template <int H, int E>
+__device__ __forceinline__ void load_x(const AuxArgs& a, const float* e, int64_t b, int t,
+                                       int kq, float (&xv)[(H + E) / 4]) {
+  load_x_raw<H, E>(a, e, b, t, kq, xv);
+  zero_x<H, E>(a, t, xv);
 }
 
 // Forward of one 16-row set: h1 (C layout, 5 tiles), h2 (3 tiles) and the logit of row j
@@ -313,30 +328,47 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
     int t;
     bool live, m;
     float sb;
+    int cnt;
+    uint8_t mraw;
+    float daux;
     float xv[In / 4];
     f4 dh[kT1];
   };
   auto item_of = [&](int64_t p, bool& lv) -> int64_t {
     const int64_t li = 2 * p + io;
     lv = p < n_pairs_live && li < n_live;
-    return lv ? g.items[li] : 0;
+    const int32_t v = g.items[lv ? li : 0];  // unguarded (items holds >= 1 entry)
+    return lv ? v : 0;
   };
+  // fetch issues every load unguarded from an in-bounds address (an item that is not live reads
+  // item 0's); finish applies the masks and the arithmetic when the round starts, so the loads
+  // stay in flight under the current round
   auto fetch = [&](int64_t it, bool lv, RoundIn& r) {
     r.live = lv;
     r.b = it % a.B;
     r.t = 16 * (int)(it / a.B) + j;
-    const int cnt = g.cnt[r.b];
-    r.m = lv && r.t <= L - 2 && a.mask[r.b * L + r.t + 1] != 0;
-    // dL/d(loss sum of b) = daux_b / (2·cnt)  (0 rows → inf·0 = NaN, as the reference)
-    r.sb = g.daux[r.b] / ((float)cnt * 2.f);
-    if (lv) load_x<H, E>(a, e, r.b, r.t, kq, r.xv);
+    const int tc = r.t <= L - 2 ? r.t : 0;
+    r.cnt = g.cnt[r.b];
+    r.mraw = a.mask[r.b * L + tc + 1];
+    r.daux = g.daux[r.b];
+    load_x_raw<H, E>(a, e, r.b, r.t, kq, r.xv);
+    const int tt = r.t < L ? r.t : 0;
 #pragma unroll
     for (int x = 0; x < kT1; ++x) {
-      r.dh[x] = f4{0.f, 0.f, 0.f, 0.f};
       const int f0 = 16 * x + 4 * kq;
-      if (set == 0 && g.acc_hidden && lv && r.t < L && f0 < H)
-        r.dh[x] = *reinterpret_cast<const f4*>(g.dhidden + (r.b * L + r.t) * (int64_t)H + f0);
+      r.dh[x] = *reinterpret_cast<const f4*>(g.dhidden + (r.b * L + tt) * (int64_t)H +
+                                             (f0 < H ? f0 : 0));
     }
+  };
+  auto finish = [&](RoundIn& r) {
+    r.m = r.live && r.t <= L - 2 && r.mraw != 0;
+    // dL/d(loss sum of b) = daux_b / (2·cnt)  (0 rows → inf·0 = NaN, as the reference)
+    r.sb = r.daux / ((float)r.cnt * 2.f);
+    zero_x<H, E>(a, r.t, r.xv);
+    const bool dh_ok = set == 0 && g.acc_hidden && r.live && r.t < L;
+#pragma unroll
+    for (int x = 0; x < kT1; ++x)
+      if (!(dh_ok && 16 * x + 4 * kq < H)) r.dh[x] = f4{0.f, 0.f, 0.f, 0.f};
   };
   RoundIn cur;
   {
@@ -351,6 +383,7 @@ __global__ __launch_bounds__(256) void aux_bwd_kernel(AuxArgs a, AuxGrad g) {
     fetch(it1, lv1, nxt);  // stage B of the next round
     bool lv2;
     const int64_t it2 = item_of(pr + 2 * (int64_t)gridDim.x, lv2);  // stage A of the one after
+    finish(cur);
     const bool live = cur.live;
     const int64_t b = cur.b;
     const int t = cur.t;
