@@ -121,19 +121,57 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
   const int64_t base = (int64_t)blockIdx.x * (kSortThreads * KPL);
   uint32_t kv[KPL];
   bool oob = false;
+  // Round 6: the tile's ids (and valid flags) are loaded unguarded, all before any is used (a
+  // position past n reads position 0 and is dropped); per element, the compiler waited for each
+  // guarded load in turn (tools/isa_wait_audit.py)
+  int64_t idv[KPL];
+  uint32_t excl = 0u;
+  // the batched path: slot offsets in LDS, or no slots at all (one range [0, n_rows))
+  const bool batched = FROM_IDS && (lds_slots || !kg.slot_offsets);
+  if (batched) {
+    if (kg.dtype == RS_ID_I64) {
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+        idv[k] = static_cast<const int64_t*>(kg.ids)[i < n ? i : 0];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+        idv[k] = static_cast<const int32_t*>(kg.ids)[i < n ? i : 0];
+      }
+    }
+    if (kg.valid) {
+      uint8_t f[KPL];
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+        f[k] = kg.valid[i < n ? i : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) excl |= (uint32_t)(f[k] == 0) << k;
+    }
+  } else if (!FROM_IDS) {
+#pragma unroll
+    for (int k = 0; k < KPL; ++k) {
+      const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
+      kv[k] = keys[i < n ? i : 0];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < KPL; ++k) {
     const int64_t i = base + (int64_t)k * kSortThreads + threadIdx.x;
     if (FROM_IDS) {
-      if (lds_slots) {
+      if (batched) {
         uint32_t key = 0u;
-        const int sl = (int)((uint32_t)i % (uint32_t)kg.n_slots);
-        if (i < n && kg.valid && !kg.valid[i]) {
+        const int sl = lds_slots ? (int)((uint32_t)i % (uint32_t)kg.n_slots) : 0;
+        if (i < n && ((excl >> k) & 1u)) {
           key = static_cast<uint32_t>(kg.key_space + sl);  // excluded position: sentinel, unflagged
           keys[i] = key;
         } else if (i < n) {
-          const int64_t id = load_id(kg.ids, kg.dtype, i);
-          const int64_t lo = offs[sl], hi = offs[sl + 1];
+          const int64_t id = idv[k];
+          const int64_t lo = lds_slots ? offs[sl] : 0, hi = lds_slots ? offs[sl + 1] : kg.n_rows;
           if (id < 0 || id >= hi - lo) {
             oob = true;
             key = static_cast<uint32_t>(kg.key_space + sl);  // sentinel: sorts after every valid row
@@ -150,7 +188,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
         if (i < n) keys[i] = kv[k];
       }
     } else {
-      kv[k] = i < n ? keys[i] : 0u;
+      kv[k] = i < n ? kv[k] : 0u;
     }
   }
 #pragma unroll
@@ -613,10 +651,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_sums_kernel(const int3
   __shared__ int32_t red[kScanThreads / 64];
   int64_t base = (int64_t)blockIdx.x * kScanTile;
   int32_t s = 0;
+  int32_t v[kScanPerThread];  // every load issued first (guarded, each was waited for in turn)
+#pragma unroll
   for (int k = 0; k < kScanPerThread; ++k) {
-    int64_t i = base + (int64_t)k * kScanThreads + threadIdx.x;
-    if (i < n) s += in[i];
+    const int64_t i = base + (int64_t)k * kScanThreads + threadIdx.x;
+    v[k] = in[i < n ? i : 0];
   }
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; ++k)
+    if (base + (int64_t)k * kScanThreads + threadIdx.x < n) s += v[k];
   for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
