@@ -257,17 +257,27 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_multi_kernel(
   const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if (b >= B) return;
   const bool on = 4 * c < D;
-  pf4 v[kMaxSide];
+  // Round 6: every load unguarded from an in-bounds address (side s < S, column 4c < D, else
+  // side 0 / column 0) and masked where used; guarded per element, the compiler waited for each
+  // (tools/isa_wait_audit.py)
+  const int cc = on ? 4 * c : 0;
+  pf4 v[kMaxSide], bb[kMaxSide];
 #pragma unroll
   for (int s = 0; s < kMaxSide; ++s)
-    if (s < S) v[s] = on ? *reinterpret_cast<const pf4*>(side + b * sb + s * ss + 4 * c)
-                         : pf4{0.f, 0.f, 0.f, 0.f};
+    v[s] = *reinterpret_cast<const pf4*>(side + b * sb + (s < S ? s : 0) * ss + cc);
+  if (sbias) {
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s)
+      bb[s] = *reinterpret_cast<const pf4*>(sbias + (s < S ? s : 0) * D + cc);
+  }
+#pragma unroll
+  for (int s = 0; s < kMaxSide; ++s)
+    if (!(s < S && on)) v[s] = pf4{0.f, 0.f, 0.f, 0.f};
   if (sbias && on) {
 #pragma unroll
     for (int s = 0; s < kMaxSide; ++s) {
       if (s < S) {
-        const pf4 bb = *reinterpret_cast<const pf4*>(sbias + s * D + 4 * c);
-        const pf4 z = v[s] + bb;
+        const pf4 z = v[s] + bb[s];
         v[s] = pf4{fmaxf(z[0], 0.f), fmaxf(z[1], 0.f), fmaxf(z[2], 0.f), fmaxf(z[3], 0.f)};
         *reinterpret_cast<pf4*>(side + b * sb + s * ss + 4 * c) = v[s];
       }
@@ -275,12 +285,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void pool_fwd_multi_kernel(
   }
   for (int t = 0; t < pt.T; ++t) {
     const float* wl = pt.wl[t] + b * pt.wl_ld;
-    float a[kMaxSide];
+    float a[kMaxSide], wv[kMaxSide];
+#pragma unroll
+    for (int s = 0; s < kMaxSide; ++s) wv[s] = wl[s < S ? s : 0];
     float mx = -INFINITY;
-    for (int s = 0; s < S; ++s) mx = fmaxf(mx, wl[s]);
+    for (int s = 0; s < S; ++s) mx = fmaxf(mx, wv[s]);
     float sum = 0.f;
     for (int s = 0; s < S; ++s) {
-      a[s] = expf(wl[s] - mx);
+      a[s] = expf(wv[s] - mx);
       sum += a[s];
     }
     for (int s = 0; s < S; ++s) a[s] = a[s] / sum;
